@@ -1,0 +1,401 @@
+/* oracle.c — CPU ORACLE for the tiresias hot path (TEST INFRASTRUCTURE ONLY).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this (as
+ * oracle/build/liboracle.so). It is the checker, never the product: the engine in
+ * asterisk-tiresias_amd/ has its own, independently written implementation.
+ *
+ * Restated behaviour (reference = /root/reference, libaubio 0.4.5 un-vendored):
+ *   frame loop ........ src/fp_handler.c:604-661 (hop 256, buffer 512, native rate,
+ *                       40 filters, 2 coefs: src/fp_handler.c:33-39)
+ *   aubio_source_do ... int16 / 32768, last hop zero-padded, loop ends when 0 samples read
+ *   aubio_pvoc_do ..... slide [old256 | new256], *= hanningz window, fvec_shift, |FFT|
+ *   aubio_mfcc_do ..... fmat_vecmul(filterbank, norm) ; fvec_log10 (MAX(2e-42, x)) ;
+ *                       fmat_vecmul(dct, log)   (aubio 0.4.5 mfcc.c / filterbank_mel.c)
+ *   dB ................ 10*log10(fabs(c)) in double, src/fp_handler.c:651
+ *   storage ........... "%f" (src/db_ctx_handler.c:479-481); +-inf -> absent key -> NULL
+ *   search ............ src/fp_handler.c:247-374 restated from its SQL (see tfo_search)
+ *
+ * Parity: search semantics pinned by tests/golden (reference SQL run through SQLite).
+ * DSP: log10f/log10/%f are glibc's own functions here; the FFT is the project's canonical
+ * 16x16 restatement because the reference's FFT backend (fftw3f) is unpinned -> DSP parity
+ * to a real libaubio build is UNPINNED.
+ *
+ * Build flags (oracle/Makefile): -O2 -ffp-contract=off -fno-builtin (runtime glibc cosf/powf,
+ * as aubio calls them; no compile-time MPFR folding).
+ */
+#include "tfp_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define AUBIO_PI (3.14159265358979323846)
+#define AUBIO_TWO_PI (AUBIO_PI * 2.)
+
+typedef struct { float re, im; } cpx;
+
+size_t tfo_frame_count(size_t n) { return (n + TFO_HOP - 1) / TFO_HOP; }
+
+/* ---------------------------------------------------------------- tables ---------- */
+
+/* aubio fvec_set_window "hanningz": w[i] = 0.5 * (1.0 - COS(TWO_PI*i/size)), COS = cosf */
+static void build_window(float* w) {
+  unsigned int i, size = TFO_WIN;
+  for (i = 0; i < size; i++) w[i] = 0.5 * (1.0 - cosf(AUBIO_TWO_PI * i / (size)));
+}
+
+/* Canonical FFT twiddles (project spec, not aubio): (cos t, -sin t), t = 2*pi*j/N in double,
+ * rounded to float; exact at multiples of N/4. */
+static void build_twiddles(int N, int count, float* re, float* im) {
+  int j;
+  for (j = 0; j < count; j++) {
+    if (j % (N / 4) == 0) {
+      static const float c4[4] = {1.f, 0.f, -1.f, 0.f}, s4[4] = {0.f, -1.f, 0.f, 1.f};
+      re[j] = c4[(j / (N / 4)) & 3];
+      im[j] = s4[(j / (N / 4)) & 3];
+    } else {
+      double t = (2.0 * AUBIO_PI * (double)j) / (double)N;
+      re[j] = (float)cos(t);
+      im[j] = (float)(-sin(t));
+    }
+  }
+}
+
+/* aubio 0.4.5 filterbank_mel.c: aubio_filterbank_set_mel_coeffs_slaney +
+ * aubio_filterbank_set_triangle_bands, float (smpl_t) arithmetic as written there. */
+static void build_mel(float sr_param, float mel[TFO_FILTERS][TFO_BINS]) {
+  float lowestFrequency = 133.3333;
+  float linearSpacing = 66.66666666;
+  float logSpacing = 1.0711703;
+  unsigned int linearFilters = 13, logFilters = 27, n_filters = 40, win_s = TFO_BINS;
+  unsigned int fn, bin;
+  float freqs[42], lastlinearCF;
+  float lower[40], center[40], upper[40], heights[40], fft_freqs[TFO_BINS];
+  float riseInc, downInc, samplerate = sr_param;
+
+  for (fn = 0; fn < linearFilters; fn++) freqs[fn] = lowestFrequency + fn * linearSpacing;
+  lastlinearCF = freqs[linearFilters - 1];
+  for (fn = 0; fn < logFilters + 2; fn++)
+    freqs[fn + linearFilters] = lastlinearCF * (powf(logSpacing, fn + 1));
+
+  for (fn = 0; fn < n_filters; fn++) {
+    lower[fn] = freqs[fn];
+    center[fn] = freqs[fn + 1];
+    upper[fn] = freqs[fn + 2];
+  }
+  for (fn = 0; fn < n_filters; fn++) heights[fn] = 2. / (upper[fn] - lower[fn]);
+  for (bin = 0; bin < win_s; bin++) {
+    /* aubio_bintofreq(bin, samplerate, (win_s - 1) * 2): freq = sr / fftsize; freq * bin */
+    float fftsize = (float)((win_s - 1) * 2);
+    float f = samplerate / fftsize;
+    fft_freqs[bin] = f * (float)bin;
+  }
+  memset(mel, 0, sizeof(float) * TFO_FILTERS * TFO_BINS);
+  for (fn = 0; fn < n_filters; fn++) {
+    for (bin = 0; bin < win_s - 1; bin++) {
+      if (fft_freqs[bin] <= lower[fn] && fft_freqs[bin + 1] > lower[fn]) {
+        bin++;
+        break;
+      }
+    }
+    riseInc = heights[fn] / (center[fn] - lower[fn]);
+    for (; bin < win_s - 1; bin++) {
+      mel[fn][bin] = (fft_freqs[bin] - lower[fn]) * riseInc;
+      if (fft_freqs[bin + 1] >= center[fn]) {
+        bin++;
+        break;
+      }
+    }
+    downInc = heights[fn] / (upper[fn] - center[fn]);
+    for (; bin < win_s - 1; bin++) {
+      mel[fn][bin] += (upper[fn] - fft_freqs[bin]) * downInc;
+      if (mel[fn][bin] < 0.) mel[fn][bin] = 0.;
+      if (fft_freqs[bin + 1] >= upper[fn]) break;
+    }
+  }
+}
+
+/* aubio 0.4.5 mfcc.c new_aubio_mfcc DCT rows (only n_coefs = 2 rows exist). */
+static void build_dct(float dct[TFO_COEFS][TFO_FILTERS]) {
+  unsigned int n_filters = TFO_FILTERS, n_coefs = TFO_COEFS, i, j;
+  float scaling = 1. / sqrtf(n_filters / 2.);
+  for (i = 0; i < n_filters; i++) {
+    for (j = 0; j < n_coefs; j++)
+      dct[j][i] = scaling * cosf(j * (i + 0.5) * AUBIO_PI / n_filters);
+    dct[0][i] *= sqrtf(2.) / 2.;
+  }
+}
+
+int tfo_build_tables(int sample_rate, tfo_tables* t) {
+  if (sample_rate <= 0 || !t) return -1;
+  memset(t, 0, sizeof *t);
+  t->sample_rate = sample_rate;
+  build_window(t->window);
+  build_twiddles(256, 256, t->tw256_re, t->tw256_im);
+  build_twiddles(512, 257, t->tw512_re, t->tw512_im);
+  build_mel((float)sample_rate, t->mel);
+  build_dct(t->dct);
+  return 0;
+}
+
+/* ---------------------------------------------------------------- canonical FFT ----- */
+
+static cpx cmul(cpx a, float wr, float wi) {
+  cpx r;
+  r.re = a.re * wr - a.im * wi;
+  r.im = a.re * wi + a.im * wr;
+  return r;
+}
+
+static void dft4(cpx a0, cpx a1, cpx a2, cpx a3, cpx* X0, cpx* X1, cpx* X2, cpx* X3) {
+  cpx t0, t1, t2, t3;
+  t0.re = a0.re + a2.re; t0.im = a0.im + a2.im;
+  t1.re = a0.re - a2.re; t1.im = a0.im - a2.im;
+  t2.re = a1.re + a3.re; t2.im = a1.im + a3.im;
+  t3.re = a1.re - a3.re; t3.im = a1.im - a3.im;
+  X0->re = t0.re + t2.re; X0->im = t0.im + t2.im;
+  X2->re = t0.re - t2.re; X2->im = t0.im - t2.im;
+  X1->re = t1.re + t3.im; X1->im = t1.im - t3.re;
+  X3->re = t1.re - t3.im; X3->im = t1.im + t3.re;
+}
+
+/* 16-point DFT, n = 4*n1 + n2, k = k1 + 4*k2; twiddle W16^e = tw256[16e]. in/out strided. */
+static void dft16(const tfo_tables* t, const cpx* in, int is, cpx* out, int os) {
+  cpx A[4][4];
+  int n2, k1;
+  for (n2 = 0; n2 < 4; n2++)
+    dft4(in[(0 + n2) * is], in[(4 + n2) * is], in[(8 + n2) * is], in[(12 + n2) * is],
+         &A[n2][0], &A[n2][1], &A[n2][2], &A[n2][3]);
+  for (n2 = 1; n2 < 4; n2++)
+    for (k1 = 1; k1 < 4; k1++) {
+      int e = 16 * n2 * k1;
+      A[n2][k1] = cmul(A[n2][k1], t->tw256_re[e], t->tw256_im[e]);
+    }
+  for (k1 = 0; k1 < 4; k1++)
+    dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], &out[(k1 + 0) * os], &out[(k1 + 4) * os],
+         &out[(k1 + 8) * os], &out[(k1 + 12) * os]);
+}
+
+/* 256-point DFT, n = 16*n1 + n2, k = k1 + 16*k2, twiddle tw256[n2*k1]. */
+static void fft256(const tfo_tables* t, const cpx* z, cpx* Z) {
+  cpx Y[16][16];
+  int n2, k1;
+  for (n2 = 0; n2 < 16; n2++) {
+    dft16(t, z + n2, 16, Y[n2], 1);
+    for (k1 = 1; k1 < 16; k1++)
+      if (n2 != 0) Y[n2][k1] = cmul(Y[n2][k1], t->tw256_re[n2 * k1], t->tw256_im[n2 * k1]);
+  }
+  for (k1 = 0; k1 < 16; k1++) {
+    cpx col[16];
+    for (n2 = 0; n2 < 16; n2++) col[n2] = Y[n2][k1];
+    dft16(t, col, 1, Z + k1, 16);
+  }
+}
+
+/* |rfft_512(x)|[0..256] via the 256-point complex FFT of z[m] = x[2m] + i x[2m+1]. */
+static void rfft512_norm(const tfo_tables* t, const float* x, float* norm) {
+  cpx z[256], Z[256];
+  int m, k;
+  for (m = 0; m < 256; m++) { z[m].re = x[2 * m]; z[m].im = x[2 * m + 1]; }
+  fft256(t, z, Z);
+  norm[0] = fabsf(Z[0].re + Z[0].im);
+  norm[256] = fabsf(Z[0].re - Z[0].im);
+  for (k = 1; k < 256; k++) {
+    float a = Z[k].re, b = Z[k].im, c = Z[256 - k].re, d = Z[256 - k].im;
+    float Er = a + c, Ei = b - d, Or = a - c, Oi = b + d;
+    float wr = t->tw512_re[k], wi = t->tw512_im[k];
+    float tr = wr * Oi + wi * Or;
+    float ti = wr * Or - wi * Oi;
+    float Xr = 0.5f * (Er + tr);
+    float Xi = 0.5f * (Ei - ti);
+    norm[k] = sqrtf(Xr * Xr + Xi * Xi);
+  }
+}
+
+/* ---------------------------------------------------------------- %f ---------------- */
+
+int64_t tfo_fmt6(double x) {
+  char buf[400];
+  const char* s = buf;
+  int neg = 0, digits = 0, i;
+  int64_t v = 0;
+  snprintf(buf, sizeof buf, "%f", x);
+  if (*s == '-') { neg = 1; s++; }
+  for (; *s >= '0' && *s <= '9'; s++) {
+    if (++digits > 12) return neg ? -((int64_t)1 << 60) : ((int64_t)1 << 60); /* saturate */
+    v = v * 10 + (*s - '0');
+  }
+  if (*s == '.') s++;
+  for (i = 0; i < 6; i++) v = v * 10 + (s[i] - '0');
+  return neg ? -v : v;
+}
+
+/* ---------------------------------------------------------------- per-clip DSP ------ */
+
+size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float* coef, double* db,
+                       int32_t* micro) {
+  float data[TFO_WIN], dataold[TFO_WIN - TFO_HOP], x[TFO_WIN], norm[TFO_BINS];
+  float band[TFO_FILTERS], out[TFO_COEFS];
+  size_t nf = tfo_frame_count(n), f;
+  int i, j;
+  memset(dataold, 0, sizeof dataold);
+  for (f = 0; f < nf; f++) {
+    /* aubio_source_do: hop of 256 samples, zero-padded past the end */
+    float hop[TFO_HOP];
+    for (i = 0; i < TFO_HOP; i++) {
+      size_t s = f * TFO_HOP + (size_t)i;
+      hop[i] = s < n ? (float)pcm[s] * (1.0f / 32768.0f) : 0.0f;
+    }
+    /* aubio_pvoc_do: swapbuffers, fvec_weight, fvec_shift, fft, norm */
+    for (i = 0; i < TFO_WIN - TFO_HOP; i++) data[i] = dataold[i];
+    for (i = 0; i < TFO_HOP; i++) data[TFO_WIN - TFO_HOP + i] = hop[i];
+    for (i = 0; i < TFO_WIN - TFO_HOP; i++) dataold[i] = data[i + TFO_HOP];
+    for (i = 0; i < TFO_WIN; i++) data[i] *= t->window[i];
+    for (i = 0; i < TFO_WIN / 2; i++) { x[i] = data[i + TFO_WIN / 2]; x[i + TFO_WIN / 2] = data[i]; }
+    rfft512_norm(t, x, norm);
+    /* aubio_mfcc_do: filterbank (fmat_vecmul), fvec_log10, DCT (fmat_vecmul) */
+    for (j = 0; j < TFO_FILTERS; j++) band[j] = 0.f;
+    for (i = 0; i < TFO_BINS; i++)
+      for (j = 0; j < TFO_FILTERS; j++) band[j] += norm[i] * t->mel[j][i];
+    for (j = 0; j < TFO_FILTERS; j++) {
+      double v = 2.e-42, b = band[j];
+      band[j] = log10f((float)(v > b ? v : b));
+    }
+    for (j = 0; j < TFO_COEFS; j++) out[j] = 0.f;
+    for (i = 0; i < TFO_FILTERS; i++)
+      for (j = 0; j < TFO_COEFS; j++) out[j] += band[i] * t->dct[j][i];
+    /* fp_handler.c:649-652 */
+    for (j = 0; j < TFO_COEFS; j++) {
+      double q = 10 * log10(fabs(out[j]));
+      if (coef) coef[2 * f + j] = out[j];
+      if (db) db[2 * f + j] = q;
+      if (micro) micro[2 * f + j] = isfinite(q) ? (int32_t)tfo_fmt6(q) : TFO_NULL;
+    }
+  }
+  return nf;
+}
+
+typedef struct {
+  const tfo_tables* t;
+  const int16_t* pcm;
+  const int64_t* off;
+  const int64_t* foff;
+  int nclips, tid, nthreads;
+  int32_t* micro;
+  double* db;
+} batch_arg;
+
+static void* batch_worker(void* p) {
+  batch_arg* a = (batch_arg*)p;
+  int c;
+  for (c = a->tid; c < a->nclips; c += a->nthreads) {
+    size_t n = (size_t)(a->off[c + 1] - a->off[c]);
+    tfo_fingerprint(a->t, a->pcm + a->off[c], n, NULL, a->db ? a->db + 2 * a->foff[c] : NULL,
+                    a->micro ? a->micro + 2 * a->foff[c] : NULL);
+  }
+  return NULL;
+}
+
+size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
+                             int nclips, int32_t* micro, double* db, int nthreads) {
+  int64_t* foff = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nclips + 1));
+  pthread_t* th;
+  batch_arg* args;
+  int c, i;
+  size_t total;
+  if (nthreads < 1) nthreads = 1;
+  foff[0] = 0;
+  for (c = 0; c < nclips; c++)
+    foff[c + 1] = foff[c] + (int64_t)tfo_frame_count((size_t)(offsets[c + 1] - offsets[c]));
+  th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  args = (batch_arg*)malloc(sizeof(batch_arg) * (size_t)nthreads);
+  for (i = 0; i < nthreads; i++) {
+    batch_arg a = {t, pcm, offsets, foff, nclips, i, nthreads, micro, db};
+    args[i] = a;
+    pthread_create(&th[i], NULL, batch_worker, &args[i]);
+  }
+  for (i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+  total = (size_t)foff[nclips];
+  free(th);
+  free(args);
+  free(foff);
+  return total;
+}
+
+/* ---------------------------------------------------------------- search ------------ */
+
+/* ast_json_real_get(ast_json_object_get(j, "maxN")): absent key (json_real(+-inf/NaN) ->
+ * NULL) reads back as 0.0. */
+static double json_real_get(double v) { return isfinite(v) ? v : 0.0; }
+
+int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, int64_t nrows,
+               const char* const* uuids, int32_t nclips, const double* q1, const double* q2,
+               int32_t nq, int coefs, double tolerance, int low, int high, int32_t* winner,
+               int32_t* match_count, int32_t* frame_count) {
+  double tole;
+  int32_t* score;
+  int32_t* stamp;
+  int32_t i, c, best = -1;
+  int64_t r;
+  *frame_count = nq; /* ast_json_array_size(j_fprints), fp_handler.c:286 */
+  *winner = -1;
+  *match_count = 0;
+  if (coefs < 1 || coefs > TFO_COEFS) return 0; /* fp_handler.c:247-250 */
+  tole = tolerance;
+  if (tole < 0) tole = 0.001; /* fp_handler.c:252-256 */
+  score = (int32_t*)calloc((size_t)(nclips > 0 ? nclips : 1), sizeof(int32_t));
+  stamp = (int32_t*)calloc((size_t)(nclips > 0 ? nclips : 1), sizeof(int32_t));
+  for (i = 0; i < nq; i++) {
+    double freq = (int)json_real_get(q1[i]); /* fp_handler.c:290 */
+    double lo1, hi1, lo2 = 0, hi2 = 0;
+    int64_t L1, U1, L2 = 0, U2 = 0;
+    int has2 = 0;
+    if (low > 0 && freq < 10 * log10(low)) continue;   /* :293-299 */
+    if (high > 0 && freq > 10 * log10(high)) continue; /* :300-306 */
+    lo1 = freq - tole;
+    hi1 = freq + tole;
+    /* "%f" of nan/inf is not a SQL literal: the statement fails, nothing is inserted */
+    if (!isfinite(lo1) || !isfinite(hi1)) continue;
+    L1 = tfo_fmt6(lo1);
+    U1 = tfo_fmt6(hi1);
+    if (coefs == 2) { /* :318-351, j = 1 */
+      double f2 = json_real_get(q2[i]);
+      int skip = 0;
+      if (low > 0 && f2 < 10 * log10(low)) skip = 1;
+      else if (high > 0 && f2 > 10 * log10(high)) skip = 1;
+      if (!skip) {
+        lo2 = f2 - tole;
+        hi2 = f2 + tole;
+        if (!isfinite(lo2) || !isfinite(hi2)) continue;
+        L2 = tfo_fmt6(lo2);
+        U2 = tfo_fmt6(hi2);
+        has2 = 1;
+      }
+    }
+    /* insert into temp select * from audio_fingerprint where ... group by audio_uuid */
+    for (r = 0; r < nrows; r++) {
+      if (m1[r] == TFO_NULL) continue; /* NULL compares false */
+      if (!(m1[r] >= L1 && m1[r] <= U1)) continue;
+      if (has2) {
+        if (m2[r] == TFO_NULL) continue;
+        if (!(m2[r] >= L2 && m2[r] <= U2)) continue;
+      }
+      c = row_clip[r];
+      if (stamp[c] != i + 1) { stamp[c] = i + 1; score[c]++; }
+    }
+  }
+  /* select *, count(*) from temp group by audio_uuid order by count(*) DESC  -> first row;
+   * ties resolve to the greatest audio_uuid (SQLite behaviour, pinned by tests/golden). */
+  for (c = 0; c < nclips; c++) {
+    if (score[c] == 0) continue;
+    if (best < 0 || score[c] > score[best] ||
+        (score[c] == score[best] && strcmp(uuids[c], uuids[best]) > 0))
+      best = c;
+  }
+  if (best >= 0) { *winner = best; *match_count = score[best]; }
+  free(score);
+  free(stamp);
+  return best >= 0;
+}

@@ -1,0 +1,129 @@
+"""ctypes front-end of the CPU ORACLE (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module.
+It loads oracle/build/liboracle.so (built by oracle/Makefile) — the plain-C restatement of
+/root/reference/src/fp_handler.c:577-671 (fingerprint) and :247-374 (search).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+NULL_MICRO = -(2**31)
+
+
+class Tables(C.Structure):
+    _fields_ = [
+        ("sample_rate", C.c_int),
+        ("window", C.c_float * 512),
+        ("tw256_re", C.c_float * 256),
+        ("tw256_im", C.c_float * 256),
+        ("tw512_re", C.c_float * 257),
+        ("tw512_im", C.c_float * 257),
+        ("mel", (C.c_float * 257) * 40),
+        ("dct", (C.c_float * 40) * 2),
+    ]
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+_lib = None
+_tables: dict[int, Tables] = {}
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        L.tfo_build_tables.argtypes = [C.c_int, C.POINTER(Tables)]
+        L.tfo_frame_count.argtypes = [C.c_size_t]
+        L.tfo_frame_count.restype = C.c_size_t
+        L.tfo_fingerprint.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tfo_fingerprint.restype = C.c_size_t
+        L.tfo_fingerprint_batch.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
+        L.tfo_fingerprint_batch.restype = C.c_size_t
+        L.tfo_search.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_char_p), C.c_int32,
+                                 C.c_void_p, C.c_void_p, C.c_int32, C.c_int, C.c_double, C.c_int, C.c_int,
+                                 C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+        L.tfo_search.restype = C.c_int
+        L.tfo_fmt6.argtypes = [C.c_double]
+        L.tfo_fmt6.restype = C.c_int64
+        _lib = L
+    return _lib
+
+
+def tables(sample_rate: int = 8000) -> Tables:
+    if sample_rate not in _tables:
+        t = Tables()
+        if lib().tfo_build_tables(sample_rate, C.byref(t)) != 0:
+            raise ValueError("bad sample rate")
+        _tables[sample_rate] = t
+    return _tables[sample_rate]
+
+
+def table_arrays(sample_rate: int = 8000) -> dict[str, np.ndarray]:
+    t = tables(sample_rate)
+    return {
+        "window": np.ctypeslib.as_array(t.window).copy(),
+        "tw256": np.ctypeslib.as_array(t.tw256_re) + 1j * np.ctypeslib.as_array(t.tw256_im).astype(np.float64),
+        "mel": np.ctypeslib.as_array(t.mel).reshape(40, 257).copy(),
+        "dct": np.ctypeslib.as_array(t.dct).reshape(2, 40).copy(),
+    }
+
+
+def frame_count(n: int) -> int:
+    return (n + 255) // 256
+
+
+def fingerprint(pcm: np.ndarray, sample_rate: int = 8000):
+    """-> (coef float32[F,2], db float64[F,2], micro int32[F,2]) for one clip."""
+    pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+    nf = frame_count(len(pcm))
+    coef = np.zeros((nf, 2), np.float32)
+    db = np.zeros((nf, 2), np.float64)
+    micro = np.zeros((nf, 2), np.int32)
+    lib().tfo_fingerprint(C.byref(tables(sample_rate)), pcm.ctypes.data, len(pcm), coef.ctypes.data,
+                          db.ctypes.data, micro.ctypes.data)
+    return coef, db, micro
+
+
+def fingerprint_batch(pcm: np.ndarray, offsets: np.ndarray, sample_rate: int = 8000, nthreads: int = 1,
+                      want_db: bool = True):
+    pcm = np.ascontiguousarray(pcm, dtype=np.int16)
+    offsets = np.ascontiguousarray(offsets, dtype=np.int64)
+    nclips = len(offsets) - 1
+    total = int(sum(frame_count(int(offsets[i + 1] - offsets[i])) for i in range(nclips)))
+    micro = np.zeros((total, 2), np.int32)
+    db = np.zeros((total, 2), np.float64) if want_db else None
+    lib().tfo_fingerprint_batch(C.byref(tables(sample_rate)), pcm.ctypes.data, offsets.ctypes.data, nclips,
+                                micro.ctypes.data, db.ctypes.data if db is not None else None, nthreads)
+    return micro, db
+
+
+def search(m1, m2, row_clip, uuids, q1, q2, coefs=1, tolerance=0.001, low=-1, high=-1):
+    """fp_search_fingerprint_info semantics -> (found, winner_index, match_count, frame_count)."""
+    m1 = np.ascontiguousarray(m1, np.int32)
+    m2 = np.ascontiguousarray(m2, np.int32)
+    row_clip = np.ascontiguousarray(row_clip, np.int32)
+    q1 = np.ascontiguousarray(q1, np.float64)
+    q2 = np.ascontiguousarray(q2, np.float64)
+    arr = (C.c_char_p * max(1, len(uuids)))(*[u.encode() for u in uuids])
+    w, mc, fc = C.c_int32(), C.c_int32(), C.c_int32()
+    found = lib().tfo_search(m1.ctypes.data, m2.ctypes.data, row_clip.ctypes.data, len(m1), arr, len(uuids),
+                             q1.ctypes.data, q2.ctypes.data, len(q1), coefs, float(tolerance), int(low), int(high),
+                             C.byref(w), C.byref(mc), C.byref(fc))
+    return bool(found), w.value, mc.value, fc.value
+
+
+def fmt6(x: float) -> int:
+    return int(lib().tfo_fmt6(float(x)))
