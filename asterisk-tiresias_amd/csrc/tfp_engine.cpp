@@ -1,0 +1,755 @@
+// tfp_engine.cpp — C-ABI implementation (include/tiresias_fp.h) on top of the gfx950 kernels.
+//
+// Owns one HIP device + stream per engine, the per-sample-rate DSP tables, the enrolled
+// index (staging rows + the m1-sorted device index rebuilt lazily after changes) and the
+// search scratch. Every entry point takes the engine mutex, so concurrent channel threads
+// (the reference runs one tiresias_exec per channel, application_handler.c:66) are safe.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tiresias_fp.h"
+#include "tfp_kernels.hpp"
+#include "tfp_math.hpp"
+#include "tfp_synth.hpp"
+#include "tfp_tables.hpp"
+
+using namespace tfp;
+
+namespace {
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  hipError_t reserve(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) { (void)hipFree(p); p = nullptr; bytes = 0; }
+    size_t want = n < 256 ? 256 : n;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct Clip {
+  std::string uuid;
+  bool alive = true;
+  int64_t nrows = 0;
+};
+
+}  // namespace
+
+struct tfp_plan {
+  int32_t nclips = 0, ntiles = 0, sample_rate = 0;
+  int64_t nsamples = 0, nframes = 0;
+  std::vector<int64_t> soff, foff;
+  std::vector<int32_t> toff;
+  DevBuf d_soff, d_foff, d_toff;
+  std::vector<int64_t> qoff;  // == foff (frames per clip as queries)
+  DevBuf d_qoff;
+  tfp_engine* eng = nullptr;
+};
+
+struct tfp_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::recursive_mutex mu;
+  std::string err;
+  std::map<int, DevBuf> tables;  // sample rate -> device DspTables
+
+  // staging (append-only) rows of every clip ever added
+  std::vector<Clip> clips;
+  std::unordered_map<std::string, int32_t> by_uuid;
+  DevBuf st_m1, st_m2, st_clip;
+  int64_t n_staged = 0, cap_staged = 0;
+  bool dirty = true;
+
+  // sorted index
+  DevBuf m1s, m2s, cols, rank_of_clip, tiekey;
+  int64_t nrows = 0;       // rows that can match (live clip, non-NULL max1)
+  int32_t ncols = 0;       // live clips
+  std::vector<int32_t> col_clip;                 // column (uuid rank) -> clip id
+  std::vector<int32_t> tiekey_host;              // column -> tie-break key
+  std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> column
+  std::vector<int32_t> tiebreak_override;        // clip id -> key (empty = uuid rank)
+
+  // scratch
+  DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
+  DevBuf pcm, q, qoff, boxes, counts, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
+  DevBuf soff, foff, toff, specs;
+};
+
+namespace {
+
+int fail(tfp_engine* e, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int fail(tfp_engine* e, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (e) e->err = buf;
+  return code;
+}
+
+#define HIPCHK(e, expr)                                                                          \
+  do {                                                                                           \
+    hipError_t _st = (expr);                                                                     \
+    if (_st != hipSuccess) return fail((e), TFP_E_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
+  } while (0)
+
+int ensure_tables(tfp_engine* e, int sr, const DspTables** out) {
+  auto it = e->tables.find(sr);
+  if (it == e->tables.end()) {
+    DspTables host;
+    if (!build_tables(sr, &host)) return fail(e, TFP_E_ARG, "bad sample rate %d", sr);
+    DevBuf& d = e->tables[sr];
+    HIPCHK(e, d.reserve(sizeof(DspTables)));
+    HIPCHK(e, hipMemcpyAsync(d.p, &host, sizeof host, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    it = e->tables.find(sr);
+  }
+  *out = it->second.as<DspTables>();
+  return TFP_OK;
+}
+
+// Clip layout: sample, frame and 16-frame-tile offsets.
+void layout(const int64_t* offsets, int32_t nclips, std::vector<int64_t>& soff, std::vector<int64_t>& foff,
+            std::vector<int32_t>& toff) {
+  soff.assign(offsets, offsets + nclips + 1);
+  const int64_t base = soff[0];
+  for (auto& v : soff) v -= base;
+  foff.assign(nclips + 1, 0);
+  toff.assign(nclips + 1, 0);
+  for (int32_t c = 0; c < nclips; c++) {
+    const int64_t nf = tfp_frame_count(soff[c + 1] - soff[c]);
+    foff[c + 1] = foff[c] + nf;
+    toff[c + 1] = toff[c] + (int32_t)((nf + kFramesPerBlock - 1) / kFramesPerBlock);
+  }
+}
+
+int upload(tfp_engine* e, DevBuf& d, const void* h, size_t bytes, hipStream_t s = nullptr) {
+  HIPCHK(e, d.reserve(bytes));
+  if (bytes) HIPCHK(e, hipMemcpyAsync(d.p, h, bytes, hipMemcpyHostToDevice, s ? s : e->stream));
+  return TFP_OK;
+}
+
+// Fingerprint host PCM; leaves micro/db on the device in e->micro / e->db.
+int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
+                     int64_t* nframes_out, std::vector<int64_t>* foff_out) {
+  const DspTables* T;
+  int rc = ensure_tables(e, sr, &T);
+  if (rc) return rc;
+  std::vector<int64_t> soff, foff;
+  std::vector<int32_t> toff;
+  layout(offsets, nclips, soff, foff, toff);
+  const int64_t ns = soff[nclips], nf = foff[nclips];
+  if ((rc = upload(e, e->pcm, pcm + offsets[0], sizeof(int16_t) * ns))) return rc;
+  if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
+  if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
+  if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
+  HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
+  HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
+  HIPCHK(e, launch_fingerprint(T, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->foff.as<int64_t>(),
+                               e->toff.as<int32_t>(), nclips, toff[nclips], e->micro.as<int32_t>(),
+                               e->db.as<double>(), e->stream));
+  *nframes_out = nf;
+  if (foff_out) *foff_out = foff;
+  return TFP_OK;
+}
+
+int copy_frames_out(tfp_engine* e, int64_t nf, const std::vector<int64_t>& foff, tfp_frame* out) {
+  std::vector<int32_t> m(2 * nf);
+  std::vector<double> d(2 * nf);
+  if (nf) {
+    HIPCHK(e, hipMemcpyAsync(m.data(), e->micro.p, sizeof(int32_t) * 2 * nf, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(d.data(), e->db.p, sizeof(double) * 2 * nf, hipMemcpyDeviceToHost, e->stream));
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  size_t c = 0;
+  for (int64_t g = 0; g < nf; g++) {
+    while (c + 1 < foff.size() && foff[c + 1] <= g) c++;
+    out[g].frame_idx = (int32_t)(g - foff[c]);
+    out[g].m1 = m[2 * g];
+    out[g].m2 = m[2 * g + 1];
+    out[g].reserved = 0;
+    out[g].q1 = d[2 * g];
+    out[g].q2 = d[2 * g + 1];
+  }
+  return TFP_OK;
+}
+
+// ---- index -------------------------------------------------------------------------------
+
+int stage_reserve(tfp_engine* e, int64_t extra) {
+  const int64_t need = e->n_staged + extra;
+  if (need <= e->cap_staged) return TFP_OK;
+  int64_t cap = std::max<int64_t>(need, std::max<int64_t>(1 << 16, e->cap_staged * 2));
+  DevBuf n1, n2, nc;
+  HIPCHK(e, n1.reserve(sizeof(int32_t) * cap));
+  HIPCHK(e, n2.reserve(sizeof(int32_t) * cap));
+  HIPCHK(e, nc.reserve(sizeof(int32_t) * cap));
+  if (e->n_staged) {
+    HIPCHK(e, hipMemcpyAsync(n1.p, e->st_m1.p, sizeof(int32_t) * e->n_staged, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(n2.p, e->st_m2.p, sizeof(int32_t) * e->n_staged, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(nc.p, e->st_clip.p, sizeof(int32_t) * e->n_staged, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+  }
+  std::swap(e->st_m1.p, n1.p); std::swap(e->st_m1.bytes, n1.bytes);
+  std::swap(e->st_m2.p, n2.p); std::swap(e->st_m2.bytes, n2.bytes);
+  std::swap(e->st_clip.p, nc.p); std::swap(e->st_clip.bytes, nc.bytes);
+  e->cap_staged = cap;
+  return TFP_OK;
+}
+
+int new_clip(tfp_engine* e, const char* uuid, int64_t nrows, int32_t* id) {
+  if (!uuid || !*uuid || strlen(uuid) >= 64) return fail(e, TFP_E_ARG, "bad uuid");
+  if (e->by_uuid.count(uuid)) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuid);
+  Clip c;
+  c.uuid = uuid;
+  c.nrows = nrows;
+  *id = (int32_t)e->clips.size();
+  e->clips.push_back(c);
+  e->by_uuid[uuid] = *id;
+  e->dirty = true;
+  return TFP_OK;
+}
+
+int rebuild(tfp_engine* e) {
+  if (!e->dirty) return TFP_OK;
+  // uuid order of live clips = columns (the tie-break order of SQLite's result sort)
+  std::vector<int32_t> live;
+  for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
+    if (e->clips[i].alive) live.push_back(i);
+  std::sort(live.begin(), live.end(), [&](int32_t a, int32_t b) { return e->clips[a].uuid < e->clips[b].uuid; });
+  std::vector<int32_t> rank(std::max<size_t>(e->clips.size(), 1), -1);
+  for (size_t r = 0; r < live.size(); r++) rank[live[r]] = (int32_t)r;
+  e->ncols = (int32_t)live.size();
+  e->col_clip = live;
+  e->tiekey_host.assign(std::max<size_t>(live.size(), 1), 0);
+  e->key_col.clear();
+  for (size_t r = 0; r < live.size(); r++) {
+    const int32_t clip = live[r];
+    const int32_t k = e->tiebreak_override.size() > (size_t)clip ? e->tiebreak_override[clip] : (int32_t)r;
+    e->tiekey_host[r] = k;
+    e->key_col[k] = (int32_t)r;
+  }
+  int rc;
+  if ((rc = upload(e, e->rank_of_clip, rank.data(), sizeof(int32_t) * rank.size()))) return rc;
+  if ((rc = upload(e, e->tiekey, e->tiekey_host.data(), sizeof(int32_t) * e->tiekey_host.size()))) return rc;
+  const int64_t n = e->n_staged;
+  e->nrows = 0;
+  if (n > 0) {
+    HIPCHK(e, e->keys_a.reserve(sizeof(int32_t) * n));
+    HIPCHK(e, e->keys_b.reserve(sizeof(int32_t) * n));
+    HIPCHK(e, e->vals_a.reserve(sizeof(int32_t) * n));
+    HIPCHK(e, e->vals_b.reserve(sizeof(int32_t) * n));
+    HIPCHK(e, launch_index_keys(e->st_m1.as<int32_t>(), e->st_clip.as<int32_t>(), e->rank_of_clip.as<int32_t>(), n,
+                                e->keys_a.as<int32_t>(), e->vals_a.as<int32_t>(), e->stream));
+    size_t tb = 0;
+    HIPCHK(e, radix_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, e->stream));
+    HIPCHK(e, e->sort_tmp.reserve(tb));
+    HIPCHK(e, radix_sort_pairs(e->sort_tmp.p, &tb, e->keys_a.as<int32_t>(), e->keys_b.as<int32_t>(),
+                               e->vals_a.as<int32_t>(), e->vals_b.as<int32_t>(), n, e->stream));
+    HIPCHK(e, e->cnt.reserve(sizeof(int64_t)));
+    HIPCHK(e, launch_count_below(e->keys_b.as<int32_t>(), n, INT32_MAX, e->cnt.as<int64_t>(), e->stream));
+    int64_t valid = 0;
+    HIPCHK(e, hipMemcpyAsync(&valid, e->cnt.p, sizeof valid, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, e->m1s.reserve(sizeof(int32_t) * (valid + 1)));
+    HIPCHK(e, e->m2s.reserve(sizeof(int32_t) * (valid + 1)));
+    HIPCHK(e, e->cols.reserve(sizeof(int32_t) * (valid + 1)));
+    if (valid) {
+      HIPCHK(e, hipMemcpyAsync(e->m1s.p, e->keys_b.p, sizeof(int32_t) * valid, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(e, launch_index_gather(e->vals_b.as<int32_t>(), e->st_m2.as<int32_t>(), e->st_clip.as<int32_t>(),
+                                    e->rank_of_clip.as<int32_t>(), valid, e->m2s.as<int32_t>(), e->cols.as<int32_t>(),
+                                    e->stream));
+    }
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->nrows = valid;
+  } else {
+    HIPCHK(e, e->m1s.reserve(4));
+    HIPCHK(e, e->m2s.reserve(4));
+    HIPCHK(e, e->cols.reserve(4));
+  }
+  e->dirty = false;
+  return TFP_OK;
+}
+
+// ---- search core: frames' q values already on device (e->q, 2 doubles per frame) -----------
+
+int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* d_q, const tfp_search_params* P,
+                std::vector<unsigned long long>& keys, unsigned long long* d_keys_out, hipStream_t s) {
+  int rc = rebuild(e);  // synchronous on e->stream
+  if (rc) return rc;
+  keys.assign(nq, 0ull);
+  const int64_t nf = h_qoff[nq] - h_qoff[0];
+  SearchConsts sc;
+  memset(&sc, 0, sizeof sc);
+  sc.coefs = P->coefs;
+  sc.tole = P->tolerance < 0 ? TFP_DEFAULT_TOLERANCE : P->tolerance;  // fp_handler.c:252-256
+  sc.has_low = P->freq_ignore_low > 0;
+  sc.has_high = P->freq_ignore_high > 0;
+  if (sc.has_low) sc.thr_low = 10 * log10((double)P->freq_ignore_low);
+  if (sc.has_high) sc.thr_high = 10 * log10((double)P->freq_ignore_high);
+
+  std::vector<int64_t> qo(h_qoff, h_qoff + nq + 1);
+  for (auto& v : qo) v -= h_qoff[0];
+  if ((rc = upload(e, e->qoff, qo.data(), sizeof(int64_t) * qo.size(), s))) return rc;
+  HIPCHK(e, e->boxes.reserve(sizeof(FrameBox) * (nf + 1)));
+  HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), s));
+  const int32_t Qp = ((nq + 127) / 128) * 128;
+  HIPCHK(e, e->best.reserve(sizeof(unsigned long long) * Qp));
+  HIPCHK(e, hipMemsetAsync(e->best.p, 0, sizeof(unsigned long long) * Qp, s));
+  const int32_t C = e->ncols;
+  const int64_t R = e->nrows;
+
+  bool done = false;
+  if (sc.coefs == 1 && C > 0 && R > 0) {
+    // vote-matrix path
+    HIPCHK(e, e->counts.reserve(sizeof(int32_t) * (size_t)nq * kKeyRange));
+    HIPCHK(e, e->mask.reserve(sizeof(uint32_t) * (kKeyRange / 32) + sizeof(int32_t)));
+    HIPCHK(e, hipMemsetAsync(e->counts.p, 0, sizeof(int32_t) * (size_t)nq * kKeyRange, s));
+    HIPCHK(e, hipMemsetAsync(e->mask.p, 0, sizeof(uint32_t) * (kKeyRange / 32) + sizeof(int32_t), s));
+    uint32_t* d_mask = e->mask.as<uint32_t>();
+    int32_t* d_max = reinterpret_cast<int32_t*>(d_mask + kKeyRange / 32);
+    HIPCHK(e, launch_key_hist(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, e->counts.as<int32_t>(), d_mask, d_max, s));
+    uint32_t hmask[kKeyRange / 32 + 1];
+    HIPCHK(e, hipMemcpyAsync(hmask, d_mask, sizeof hmask, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    const int32_t maxcount = (int32_t)hmask[kKeyRange / 32];
+    if (maxcount <= 2048) {  // counts exact in fp16
+      std::vector<int32_t> keycols;
+      std::vector<int64_t> kb;
+      for (int idx = 0; idx < kKeyRange; idx++)
+        if (hmask[idx >> 5] >> (idx & 31) & 1u) {
+          keycols.push_back(idx);
+          const double freq = (double)(idx - kKeyOffset);
+          kb.push_back(fmt6_bound(freq - sc.tole));
+          kb.push_back(fmt6_bound(freq + sc.tole));
+        }
+      const int32_t Ku = (int32_t)keycols.size();
+      if (Ku == 0) {
+        done = true;  // every frame ignored: no rows inserted -> NOTFOUND
+      } else {
+        const int32_t Kp = ((Ku + 15) / 16) * 16;
+        const int32_t Cp = ((C + 31) / 32) * 32;
+        if ((rc = upload(e, e->keycols, keycols.data(), sizeof(int32_t) * Ku, s))) return rc;
+        if ((rc = upload(e, e->kbounds, kb.data(), sizeof(int64_t) * kb.size(), s))) return rc;
+        HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * Kp));
+        HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * Kp));
+        HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), Ku, Kp, e->A.as<_Float16>(), s));
+        HIPCHK(e, hipMemsetAsync(e->Bt.p, 0, sizeof(_Float16) * (size_t)Cp * Kp, s));
+        HIPCHK(e, launch_build_B(e->m1s.as<int32_t>(), R, e->cols.as<int32_t>(), e->kbounds.as<int64_t>(), Ku, Kp,
+                                 e->Bt.as<_Float16>(), s));
+        HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, Kp, e->tiekey.as<int32_t>(),
+                                   e->best.as<unsigned long long>(), s));
+        done = true;
+      }
+    }
+  }
+  if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
+    // general path, query chunks bounded to ~512 MB of stamp+score scratch
+    const int32_t Cp = C;
+    int64_t chunk = (int64_t)(512ll << 20) / (8ll * Cp);
+    chunk = std::max<int64_t>(4, std::min<int64_t>(chunk, nq));
+    HIPCHK(e, e->stamp.reserve(sizeof(int32_t) * chunk * Cp));
+    HIPCHK(e, e->score.reserve(sizeof(int32_t) * chunk * Cp));
+    for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
+      const int32_t n = (int32_t)std::min<int64_t>(chunk, nq - q0);
+      HIPCHK(e, hipMemsetAsync(e->stamp.p, 0, sizeof(int32_t) * n * Cp, s));
+      HIPCHK(e, hipMemsetAsync(e->score.p, 0, sizeof(int32_t) * n * Cp, s));
+      HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), (int32_t)q0, n, e->m1s.as<int32_t>(),
+                            e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->tiekey.as<int32_t>(), Cp,
+                            e->stamp.as<int32_t>(), e->score.as<int32_t>(), e->best.as<unsigned long long>(), s));
+    }
+  }
+  if (d_keys_out) {
+    HIPCHK(e, hipMemcpyAsync(d_keys_out, e->best.p, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+    return TFP_OK;
+  }
+  if (nq) HIPCHK(e, hipMemcpyAsync(keys.data(), e->best.p, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
+  HIPCHK(e, hipStreamSynchronize(s));
+  return TFP_OK;
+}
+
+void fill_results(tfp_engine* e, const std::vector<unsigned long long>& keys, const int64_t* qoff, int32_t nq,
+                  tfp_result* out) {
+  for (int32_t i = 0; i < nq; i++) {
+    tfp_result& r = out[i];
+    memset(&r, 0, sizeof r);
+    r.frame_count = (int32_t)(qoff[i + 1] - qoff[i]);
+    r.clip_id = -1;
+    const unsigned long long k = keys[i];
+    if (!k) continue;
+    auto it = e->key_col.find((int32_t)(uint32_t)(k & 0xffffffffu));
+    if (it == e->key_col.end()) continue;
+    const int32_t clip = e->col_clip[it->second];
+    r.found = 1;
+    r.match_count = (int32_t)(k >> 32);
+    r.clip_id = clip;
+    snprintf(r.uuid, sizeof r.uuid, "%s", e->clips[clip].uuid.c_str());
+  }
+}
+
+bool valid_params(const tfp_search_params* P) { return P && P->coefs >= 1 && P->coefs <= 2; }
+
+}  // namespace
+
+// =========================================================================================
+extern "C" {
+
+int tfp_abi_version(void) { return TFP_ABI_VERSION; }
+
+int tfp_device_count(int32_t* count) {
+  int n = 0;
+  if (!count) return TFP_E_ARG;
+  *count = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return TFP_E_NODEV;
+  *count = n;
+  return TFP_OK;
+}
+
+int64_t tfp_frame_count(int64_t n) { return n <= 0 ? 0 : (n + TFP_HOP - 1) / TFP_HOP; }
+
+int tfp_engine_create(int32_t device, tfp_engine** out) {
+  if (!out) return TFP_E_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || device < 0 || device >= n) return TFP_E_NODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TFP_E_NODEV;
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TFP_E_NODEV;  // code objects are gfx950-only
+  if (hipSetDevice(device) != hipSuccess) return TFP_E_HIP;
+  tfp_engine* e = new tfp_engine();
+  e->device = device;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return TFP_E_HIP;
+  }
+  *out = e;
+  return TFP_OK;
+}
+
+void tfp_engine_destroy(tfp_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipStreamSynchronize(e->stream);
+  hipStream_t s = e->stream;
+  delete e;
+  (void)hipStreamDestroy(s);
+}
+
+const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+int tfp_fingerprint_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
+                          tfp_frame* out, int64_t cap, int64_t* nframes) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (!offsets || nclips < 0 || !nframes || (!pcm && nclips && offsets[nclips] > offsets[0]))
+    return fail(e, TFP_E_ARG, "bad arguments");
+  for (int32_t c = 0; c < nclips; c++)
+    if (offsets[c + 1] < offsets[c]) return fail(e, TFP_E_ARG, "offsets not monotone");
+  int64_t need = 0;
+  for (int32_t c = 0; c < nclips; c++) need += tfp_frame_count(offsets[c + 1] - offsets[c]);
+  *nframes = need;
+  if (need > 0 && (!out || cap < need)) return fail(e, TFP_E_CAPACITY, "need %lld frames", (long long)need);
+  if (need == 0) return TFP_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  int64_t nf;
+  std::vector<int64_t> foff;
+  int rc = fingerprint_host(e, pcm, offsets, nclips, sr, &nf, &foff);
+  if (rc) return rc;
+  return copy_frames_out(e, nf, foff, out);
+}
+
+int tfp_fingerprint_pcm(tfp_engine* e, const int16_t* pcm, int64_t n, int32_t sr, tfp_frame* out, int64_t cap,
+                        int64_t* nframes) {
+  if (n < 0) return TFP_E_ARG;
+  int64_t off[2] = {0, n};
+  return tfp_fingerprint_batch(e, pcm, off, 1, sr, out, cap, nframes);
+}
+
+int tfp_plan_create(tfp_engine* e, const int64_t* offsets, int32_t nclips, int32_t sr, tfp_plan** out) {
+  if (!e || !offsets || nclips < 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  const DspTables* T;
+  int rc = ensure_tables(e, sr, &T);
+  if (rc) return rc;
+  tfp_plan* p = new tfp_plan();
+  p->eng = e;
+  p->nclips = nclips;
+  p->sample_rate = sr;
+  layout(offsets, nclips, p->soff, p->foff, p->toff);
+  p->nsamples = p->soff[nclips];
+  p->nframes = p->foff[nclips];
+  p->ntiles = p->toff[nclips];
+  if ((rc = upload(e, p->d_soff, p->soff.data(), sizeof(int64_t) * p->soff.size())) ||
+      (rc = upload(e, p->d_foff, p->foff.data(), sizeof(int64_t) * p->foff.size())) ||
+      (rc = upload(e, p->d_toff, p->toff.data(), sizeof(int32_t) * p->toff.size())) ||
+      (rc = upload(e, p->d_qoff, p->foff.data(), sizeof(int64_t) * p->foff.size()))) {
+    delete p;
+    return rc;
+  }
+  if (hipStreamSynchronize(e->stream) != hipSuccess) { delete p; return fail(e, TFP_E_HIP, "sync"); }
+  *out = p;
+  return TFP_OK;
+}
+
+void tfp_plan_destroy(tfp_plan* p) { delete p; }
+int64_t tfp_plan_frames(const tfp_plan* p) { return p ? p->nframes : -1; }
+
+int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, int32_t* d_micro, double* d_db,
+                           void* stream) {
+  if (!e || !p || !d_micro || (!d_pcm && p->nsamples)) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  const DspTables* T;
+  int rc = ensure_tables(e, p->sample_rate, &T);
+  if (rc) return rc;
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
+                               p->nclips, p->ntiles, d_micro, d_db, s));
+  return TFP_OK;
+}
+
+int tfp_index_add(tfp_engine* e, const char* uuid, const int32_t* m1, const int32_t* m2, int32_t nframes,
+                  int32_t* clip_id) {
+  if (!e || nframes < 0 || (nframes && (!m1 || !m2))) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  int32_t id;
+  int rc = new_clip(e, uuid, nframes, &id);
+  if (rc) return rc;
+  if ((rc = stage_reserve(e, nframes))) return rc;
+  if (nframes) {
+    std::vector<int32_t> cl(nframes, id);
+    const int64_t o = e->n_staged;
+    HIPCHK(e, hipMemcpyAsync(e->st_m1.as<int32_t>() + o, m1, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_m2.as<int32_t>() + o, m2, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_clip.as<int32_t>() + o, cl.data(), sizeof(int32_t) * nframes, hipMemcpyHostToDevice,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->n_staged += nframes;
+  }
+  if (clip_id) *clip_id = id;
+  return TFP_OK;
+}
+
+// de-interleave (m1, m2) pairs + clip ids into staging
+__global__ void stage_from_micro_kernel(const int32_t* micro, int64_t nf, const int64_t* foff, int32_t nclips,
+                                        int32_t clip0, int32_t* m1, int32_t* m2, int32_t* clip) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < nf; g += (int64_t)gridDim.x * blockDim.x) {
+    int lo = 0, hi = nclips;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (foff[mid] <= g) lo = mid; else hi = mid;
+    }
+    m1[g] = micro[2 * g];
+    m2[g] = micro[2 * g + 1];
+    clip[g] = clip0 + lo;
+  }
+}
+
+int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
+                         const int32_t* d_micro, void* stream) {
+  if (!e || nclips < 0 || !uuids || !frame_offsets || (!d_micro && frame_offsets[nclips] > frame_offsets[0]))
+    return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  for (int32_t c = 0; c < nclips; c++) {
+    if (!uuids[c] || !*uuids[c] || strlen(uuids[c]) >= 64) return fail(e, TFP_E_ARG, "bad uuid %d", c);
+    if (e->by_uuid.count(uuids[c])) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
+  }
+  const int64_t nf = frame_offsets[nclips] - frame_offsets[0];
+  int rc = stage_reserve(e, nf);
+  if (rc) return rc;
+  const int32_t clip0 = (int32_t)e->clips.size();
+  for (int32_t c = 0; c < nclips; c++) {
+    int32_t id;
+    if ((rc = new_clip(e, uuids[c], frame_offsets[c + 1] - frame_offsets[c], &id))) return rc;
+  }
+  if (nf) {
+    std::vector<int64_t> fo(frame_offsets, frame_offsets + nclips + 1);
+    for (auto& v : fo) v -= frame_offsets[0];
+    if ((rc = upload(e, e->foff, fo.data(), sizeof(int64_t) * fo.size()))) return rc;
+    hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+    if (s != e->stream) HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t o = e->n_staged;
+    hipLaunchKernelGGL(stage_from_micro_kernel, dim3(2048), dim3(256), 0, s, d_micro + 2 * frame_offsets[0], nf,
+                       e->foff.as<int64_t>(), nclips, clip0, e->st_m1.as<int32_t>() + o, e->st_m2.as<int32_t>() + o,
+                       e->st_clip.as<int32_t>() + o);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipStreamSynchronize(s));
+    e->n_staged += nf;
+  }
+  return TFP_OK;
+}
+
+int tfp_index_remove(tfp_engine* e, const char* uuid) {
+  if (!e || !uuid) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  auto it = e->by_uuid.find(uuid);
+  if (it == e->by_uuid.end()) return fail(e, TFP_E_NOENT, "uuid %s not indexed", uuid);
+  e->clips[it->second].alive = false;
+  e->by_uuid.erase(it);
+  e->dirty = true;
+  return TFP_OK;
+}
+
+int tfp_index_clear(tfp_engine* e) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  e->clips.clear();
+  e->by_uuid.clear();
+  e->tiebreak_override.clear();
+  e->n_staged = 0;
+  e->dirty = true;
+  return TFP_OK;
+}
+
+int tfp_index_stats(tfp_engine* e, int64_t* nrows, int32_t* nclips) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  int64_t r = 0;
+  int32_t c = 0;
+  for (const auto& cl : e->clips)
+    if (cl.alive) { r += cl.nrows; c++; }
+  if (nrows) *nrows = r;
+  if (nclips) *nclips = c;
+  return TFP_OK;
+}
+
+int tfp_index_commit(tfp_engine* e) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  return rebuild(e);
+}
+
+int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {
+  if (!e || n < 0 || (n && !keys)) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  e->tiebreak_override.assign(keys, keys + n);
+  e->dirty = true;
+  return TFP_OK;
+}
+
+int tfp_index_uuid_of_key(tfp_engine* e, int32_t key, char* uuid, int32_t len) {
+  if (!e || !uuid || len <= 0) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  auto it = e->key_col.find(key);
+  if (it == e->key_col.end()) return fail(e, TFP_E_NOENT, "no clip with key %d", key);
+  snprintf(uuid, len, "%s", e->clips[e->col_clip[it->second]].uuid.c_str());
+  return TFP_OK;
+}
+
+int tfp_search_batch(tfp_engine* e, const tfp_frame* frames, const int64_t* qoff, int32_t nq,
+                     const tfp_search_params* P, tfp_result* out) {
+  if (!e || !qoff || nq < 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  const int64_t nf = nq ? qoff[nq] - qoff[0] : 0;
+  if (nf && !frames) return fail(e, TFP_E_ARG, "frames is NULL");
+  std::vector<unsigned long long> keys(nq, 0ull);
+  if (valid_params(P) && nq) {  // coefs out of range: NULL for every query (fp_handler.c:247-250)
+    HIPCHK(e, hipSetDevice(e->device));
+    std::vector<double> q(2 * (nf + 1));
+    for (int64_t i = 0; i < nf; i++) {
+      q[2 * i] = frames[qoff[0] + i].q1;
+      q[2 * i + 1] = frames[qoff[0] + i].q2;
+    }
+    int rc = upload(e, e->q, q.data(), sizeof(double) * q.size());
+    if (rc) return rc;
+    if ((rc = search_core(e, qoff, nq, e->q.as<double>(), P, keys, nullptr, e->stream))) return rc;
+  }
+  fill_results(e, keys, qoff, nq, out);
+  return TFP_OK;
+}
+
+int tfp_search(tfp_engine* e, const tfp_frame* frames, int32_t nframes, const tfp_search_params* P, tfp_result* out) {
+  if (nframes < 0) return TFP_E_ARG;
+  int64_t qoff[2] = {0, nframes};
+  return tfp_search_batch(e, frames, qoff, 1, P, out);
+}
+
+int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nq, int32_t sr,
+                         const tfp_search_params* P, tfp_result* out) {
+  if (!e || !offsets || nq < 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  std::vector<int64_t> soff, foff;
+  std::vector<int32_t> toff;
+  layout(offsets, nq, soff, foff, toff);
+  std::vector<unsigned long long> keys(nq, 0ull);
+  if (valid_params(P) && nq && foff[nq] > 0) {
+    int64_t nf;
+    int rc = fingerprint_host(e, pcm, offsets, nq, sr, &nf, nullptr);
+    if (rc) return rc;
+    if ((rc = search_core(e, foff.data(), nq, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
+  }
+  fill_results(e, keys, foff.data(), nq, out);
+  return TFP_OK;
+}
+
+int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, const tfp_search_params* P,
+                      uint64_t* d_keys, void* stream) {
+  if (!e || !p || !d_keys || !valid_params(P)) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  const DspTables* T;
+  int rc = ensure_tables(e, p->sample_rate, &T);
+  if (rc) return rc;
+  HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
+  HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
+  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
+                               p->nclips, p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
+  std::vector<unsigned long long> keys;
+  return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
+                     reinterpret_cast<unsigned long long*>(d_keys), s);
+}
+
+int tfp_synth_pcm(const tfp_synth_spec* specs, int32_t nclips, int64_t spc, int16_t* out) {
+  if (nclips < 0 || spc < 0 || (nclips && (!specs || !out))) return TFP_E_ARG;
+  for (int32_t c = 0; c < nclips; c++) {
+    const SynthClip p = synth_clip(specs[c].seed, specs[c].clip);
+    for (int64_t s = 0; s < spc; s++) out[(int64_t)c * spc + s] = synth_sample(p, specs[c].offset + s);
+  }
+  return TFP_OK;
+}
+
+int tfp_synth_pcm_device(tfp_engine* e, const tfp_synth_spec* specs, int32_t nclips, int64_t spc, int16_t* d_out,
+                         void* stream) {
+  if (!e || nclips < 0 || spc < 0 || (nclips && (!specs || !d_out))) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  static_assert(sizeof(tfp_synth_spec) == sizeof(SynthSpecDev), "spec layout");
+  int rc = upload(e, e->specs, specs, sizeof(tfp_synth_spec) * nclips);
+  if (rc) return rc;
+  if (s != e->stream) HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, launch_synth(e->specs.as<SynthSpecDev>(), nclips, spc, d_out, s));
+  HIPCHK(e, hipStreamSynchronize(s));  // specs buffer is reused by the next call
+  return TFP_OK;
+}
+
+int tfp_synchronize(tfp_engine* e, void* stream) {
+  if (!e) return TFP_E_ARG;
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipStreamSynchronize(stream ? (hipStream_t)stream : e->stream));
+  return TFP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,66 @@
+// tfp_kernels.hpp — host-callable launchers for the gfx950 kernels (internal interface).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tfp_tables.hpp"
+
+namespace tfp {
+
+constexpr int kFramesPerBlock = 16;   // 16 lanes per frame x 16 frames = 256 threads
+constexpr int32_t kKeyOffset = 512;   // trunc(dB) key k stored at k + 512 (|k| <= 459)
+constexpr int32_t kKeyRange = 1024;
+
+// One query frame's search box (fp_handler.c:287-351 restated). flags: 1 = the frame runs
+// its SQL (not ignored, bounds printable), 2 = the max2 condition is present.
+struct FrameBox {
+  int64_t L1, U1, L2, U2;
+  int32_t k;
+  int32_t flags;
+};
+
+struct SearchConsts {
+  int32_t coefs;
+  int32_t has_low, has_high;
+  int32_t pad;
+  double tole, thr_low, thr_high;
+};
+
+struct SynthSpecDev {
+  uint64_t seed;
+  int64_t clip;
+  int64_t offset;
+};
+
+// Fingerprint clips described by sample offsets soff[nclips+1], frame offsets foff[nclips+1]
+// and 16-frame tile offsets toff[nclips+1]; ntiles = toff[nclips].
+hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_soff,
+                              const int64_t* d_foff, const int32_t* d_toff, int32_t nclips, int32_t ntiles,
+                              int32_t* d_micro, double* d_db, hipStream_t s);
+
+hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
+
+// Index build: key = m1 (or INT32_MAX for rows that never match), value = staging index.
+hipError_t launch_index_keys(const int32_t* st_m1, const int32_t* st_clip, const int32_t* rank_of_clip,
+                             int64_t n, int32_t* keys, int32_t* vals, hipStream_t s);
+hipError_t launch_index_gather(const int32_t* sorted_vals, const int32_t* st_m2, const int32_t* st_clip,
+                               const int32_t* rank_of_clip, int64_t n, int32_t* m2s, int32_t* cols, hipStream_t s);
+hipError_t launch_count_below(const int32_t* sorted_keys, int64_t n, int32_t bound, int64_t* out, hipStream_t s);
+hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, int32_t* kout, const int32_t* vin,
+                            int32_t* vout, int64_t n, hipStream_t s);
+
+// Search.
+hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, hipStream_t s);
+hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts /*[nq][kKeyRange]*/,
+                           uint32_t* d_mask /*[kKeyRange/32]*/, int32_t* d_maxcount, hipStream_t s);
+hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, int32_t Ku, int32_t Kp,
+                          _Float16* d_A, hipStream_t s);
+hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds /*[Ku][2]*/,
+                          int32_t Ku, int32_t Kp, _Float16* d_Bt, hipStream_t s);
+hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
+                            const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
+hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
+                       const int32_t* m2s, const int32_t* cols, int64_t R, const int32_t* d_tiekey, int32_t Cp,
+                       int32_t* d_stamp, int32_t* d_score, unsigned long long* d_best, hipStream_t s);
+
+}  // namespace tfp

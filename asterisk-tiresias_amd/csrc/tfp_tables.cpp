@@ -1,0 +1,120 @@
+// tfp_tables.cpp — host construction of DspTables (see tfp_tables.hpp for provenance).
+// Compiled with -ffp-contract=off -fno-builtin so every float expression rounds where the
+// C source of libaubio rounds and cosf/powf are glibc's run-time functions.
+#include "tfp_tables.hpp"
+
+#include <math.h>
+#include <string.h>
+
+namespace tfp {
+
+namespace {
+const double kPi = 3.14159265358979323846;  // aubio_priv.h PI
+const double kTwoPi = kPi * 2.;             // aubio_priv.h TWO_PI
+
+void hanningz(float* w, unsigned size) {
+  for (unsigned i = 0; i < size; i++) {
+    const float c = cosf((float)(kTwoPi * i / size));
+    w[i] = (float)(0.5 * (1.0 - (double)c));
+  }
+}
+
+// (cos t, -sin t), t = 2 pi j / N; exact at quarter turns.
+void twiddles(int N, int count, float* re, float* im) {
+  for (int j = 0; j < count; j++) {
+    const int q = N / 4;
+    if (j % q == 0) {
+      switch ((j / q) & 3) {
+        case 0: re[j] = 1.f; im[j] = 0.f; break;
+        case 1: re[j] = 0.f; im[j] = -1.f; break;
+        case 2: re[j] = -1.f; im[j] = 0.f; break;
+        default: re[j] = 0.f; im[j] = 1.f; break;
+      }
+      continue;
+    }
+    const double t = (2.0 * kPi * (double)j) / (double)N;
+    re[j] = (float)cos(t);
+    im[j] = (float)(-sin(t));
+  }
+}
+}  // namespace
+
+void build_mel_dense(int sample_rate, float (*mel)[kBins]) {
+  // aubio_filterbank_set_mel_coeffs_slaney: Malcolm Slaney's auditory-toolbox constants.
+  const float lowest = 133.3333f;
+  const float lin_spacing = 66.66666666f;
+  const float log_spacing = 1.0711703f;
+  const unsigned n_lin = 13, n_log = 27, n_filters = kFilters;
+  float freqs[n_lin + n_log + 2];
+  for (unsigned fn = 0; fn < n_lin; fn++) {
+    const float step = (float)fn * lin_spacing;
+    freqs[fn] = lowest + step;
+  }
+  const float last_lin = freqs[n_lin - 1];
+  for (unsigned fn = 0; fn < n_log + 2; fn++)
+    freqs[n_lin + fn] = last_lin * powf(log_spacing, (float)(fn + 1));
+
+  // aubio_filterbank_set_triangle_bands
+  const float sr = (float)sample_rate;
+  const unsigned nb = kBins;
+  float fft_freqs[kBins];
+  const float bin_hz = sr / (float)((nb - 1) * 2);  // aubio_bintofreq
+  for (unsigned b = 0; b < nb; b++) fft_freqs[b] = bin_hz * (float)b;
+  memset(mel, 0, sizeof(float) * kFilters * kBins);
+  for (unsigned fn = 0; fn < n_filters; fn++) {
+    const float lo = freqs[fn], ce = freqs[fn + 1], up = freqs[fn + 2];
+    const float height = (float)(2. / (double)(up - lo));  // unit-area triangles
+    unsigned b = 0;
+    for (; b < nb - 1; b++) {                                // skip first elements
+      if (fft_freqs[b] <= lo && fft_freqs[b + 1] > lo) { b++; break; }
+    }
+    const float rise = height / (ce - lo);
+    for (; b < nb - 1; b++) {
+      mel[fn][b] = (fft_freqs[b] - lo) * rise;
+      if (fft_freqs[b + 1] >= ce) { b++; break; }
+    }
+    const float down = height / (up - ce);
+    for (; b < nb - 1; b++) {
+      mel[fn][b] += (up - fft_freqs[b]) * down;
+      if (mel[fn][b] < 0.f) mel[fn][b] = 0.f;
+      if (fft_freqs[b + 1] >= up) break;
+    }
+  }
+}
+
+bool build_tables(int sample_rate, DspTables* t) {
+  if (sample_rate <= 0 || !t) return false;
+  memset(t, 0, sizeof *t);
+  t->sample_rate = sample_rate;
+  hanningz(t->window, kWin);
+  twiddles(256, 256, t->tw256_re, t->tw256_im);
+  twiddles(512, kBins, t->tw512_re, t->tw512_im);
+
+  // new_aubio_mfcc (0.4.5): scaling = 1/SQRT(n/2); row j: scaling*COS(j(i+.5)PI/n); row 0 *= SQRT(2)/2
+  const unsigned n = kFilters;
+  const float scaling = (float)(1. / (double)sqrtf((float)(n / 2.)));
+  const double row0 = (double)sqrtf(2.f) / 2.;
+  for (unsigned i = 0; i < n; i++) {
+    for (unsigned j = 0; j < (unsigned)kCoefs; j++)
+      t->dct[j][i] = scaling * cosf((float)(j * (i + 0.5) * kPi / n));
+    t->dct[0][i] = (float)((double)t->dct[0][i] * row0);
+  }
+
+  static float mel[kFilters][kBins];
+  build_mel_dense(sample_rate, mel);
+  int off = 0;
+  for (int j = 0; j < kFilters; j++) {
+    int first = -1, last = -1;
+    for (int b = 0; b < kBins; b++)
+      if (mel[j][b] != 0.f) { if (first < 0) first = b; last = b; }
+    t->mel_off[j] = off;
+    if (first < 0) { t->mel_start[j] = 0; t->mel_len[j] = 0; continue; }
+    t->mel_start[j] = first;
+    t->mel_len[j] = last - first + 1;
+    for (int b = first; b <= last; b++) t->mel_w[off++] = mel[j][b];
+  }
+  t->mel_total = off;
+  return true;
+}
+
+}  // namespace tfp

@@ -1,0 +1,205 @@
+"""Pythonic wrapper of the C-ABI engine (numpy in/out)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from ._lib import Frame, Result, SearchParams, SynthSpec, TfpError, check, lib
+
+FRAME_DTYPE = np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                        ("q1", "<f8"), ("q2", "<f8")])
+assert FRAME_DTYPE.itemsize == C.sizeof(Frame) == 32
+
+
+def device_count() -> int:
+    n = C.c_int32()
+    rc = lib().tfp_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def frame_count(nsamples: int) -> int:
+    return int(lib().tfp_frame_count(int(nsamples)))
+
+
+def params(coefs=1, tolerance=-1.0, freq_ignore_low=-1, freq_ignore_high=-1) -> SearchParams:
+    return SearchParams(int(coefs), int(freq_ignore_low), int(freq_ignore_high), 0, float(tolerance))
+
+
+def synth_specs(seed: int, clips, offsets=None):
+    clips = list(clips)
+    offsets = [0] * len(clips) if offsets is None else list(offsets)
+    arr = (SynthSpec * max(1, len(clips)))()
+    for i, (c, o) in enumerate(zip(clips, offsets)):
+        arr[i] = SynthSpec(seed & (2**64 - 1), int(c), int(o))
+    return arr
+
+
+def synth_pcm(seed: int, clips, samples_per_clip: int, offsets=None) -> np.ndarray:
+    """Deterministic synthetic PCM (host side of tfp_synth_pcm) -> int16[nclips, samples]."""
+    clips = list(clips)
+    out = np.zeros((len(clips), samples_per_clip), np.int16)
+    specs = synth_specs(seed, clips, offsets)
+    check(lib().tfp_synth_pcm(specs, len(clips), samples_per_clip, out.ctypes.data))
+    return out
+
+
+class Engine:
+    """One engine per GPU (tfp_engine)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        rc = lib().tfp_engine_create(int(device), C.byref(self._h))
+        if rc != 0:
+            raise TfpError(rc, f"cannot create engine on device {device}")
+        self.device = device
+
+    def close(self):
+        if self._h:
+            lib().tfp_engine_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _chk(self, rc):
+        return check(rc, self._h)
+
+    # ---- fingerprinting -----------------------------------------------------------
+    def fingerprint(self, pcm: np.ndarray, sample_rate: int = 8000) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        n = frame_count(len(pcm))
+        out = np.zeros(n, FRAME_DTYPE)
+        got = C.c_int64()
+        self._chk(lib().tfp_fingerprint_pcm(self._h, pcm.ctypes.data, len(pcm), sample_rate, out.ctypes.data, n,
+                                            C.byref(got)))
+        return out
+
+    def fingerprint_batch(self, pcm: np.ndarray, offsets, sample_rate: int = 8000) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nclips = len(offsets) - 1
+        n = sum(frame_count(int(offsets[i + 1] - offsets[i])) for i in range(nclips))
+        out = np.zeros(max(n, 1), FRAME_DTYPE)
+        got = C.c_int64()
+        self._chk(lib().tfp_fingerprint_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nclips, sample_rate,
+                                              out.ctypes.data, n, C.byref(got)))
+        return out[:n]
+
+    # ---- index ----------------------------------------------------------------------
+    def index_add(self, uuid: str, m1, m2) -> int:
+        m1 = np.ascontiguousarray(m1, np.int32)
+        m2 = np.ascontiguousarray(m2, np.int32)
+        cid = C.c_int32()
+        self._chk(lib().tfp_index_add(self._h, uuid.encode(), m1.ctypes.data, m2.ctypes.data, len(m1), C.byref(cid)))
+        return cid.value
+
+    def index_remove(self, uuid: str):
+        self._chk(lib().tfp_index_remove(self._h, uuid.encode()))
+
+    def index_clear(self):
+        self._chk(lib().tfp_index_clear(self._h))
+
+    def index_stats(self):
+        r, c = C.c_int64(), C.c_int32()
+        self._chk(lib().tfp_index_stats(self._h, C.byref(r), C.byref(c)))
+        return r.value, c.value
+
+    def index_commit(self):
+        self._chk(lib().tfp_index_commit(self._h))
+
+    def set_tiebreak(self, keys):
+        keys = np.ascontiguousarray(keys, np.int32)
+        self._chk(lib().tfp_index_set_tiebreak(self._h, keys.ctypes.data, len(keys)))
+
+    def uuid_of_key(self, key: int) -> str:
+        buf = C.create_string_buffer(64)
+        self._chk(lib().tfp_index_uuid_of_key(self._h, int(key), buf, 64))
+        return buf.value.decode()
+
+    # ---- search ---------------------------------------------------------------------
+    @staticmethod
+    def _results(res, n):
+        return [None if not r.found else {"audio_uuid": r.uuid.decode(), "match_count": r.match_count,
+                                          "frame_count": r.frame_count, "clip_id": r.clip_id}
+                for r in res[:n]], [r.frame_count for r in res[:n]]
+
+    def search_batch(self, frames: np.ndarray, qoffsets, p: SearchParams):
+        frames = np.ascontiguousarray(frames, FRAME_DTYPE)
+        qoffsets = np.ascontiguousarray(qoffsets, np.int64)
+        nq = len(qoffsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_search_batch(self._h, frames.ctypes.data, qoffsets.ctypes.data, nq, C.byref(p), res))
+        return self._results(res, nq)
+
+    def search(self, frames: np.ndarray, p: SearchParams):
+        r, fc = self.search_batch(frames, [0, len(frames)], p)
+        return r[0], fc[0]
+
+    def search_pcm_batch(self, pcm: np.ndarray, offsets, p: SearchParams, sample_rate: int = 8000):
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nq = len(offsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_search_pcm_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nq, sample_rate,
+                                             C.byref(p), res))
+        return self._results(res, nq)
+
+    # ---- device-resident paths (pointers are raw device addresses, e.g. tensor.data_ptr())
+    def plan(self, offsets, sample_rate: int = 8000) -> "Plan":
+        return Plan(self, offsets, sample_rate)
+
+    def fingerprint_device(self, plan: "Plan", d_pcm: int, d_micro: int, d_db: int = 0, stream: int = 0):
+        self._chk(lib().tfp_fingerprint_device(self._h, plan.handle, C.c_void_p(d_pcm), C.c_void_p(d_micro),
+                                               C.c_void_p(d_db or None), C.c_void_p(stream or None)))
+
+    def index_add_device(self, uuids, frame_offsets, d_micro: int, stream: int = 0):
+        frame_offsets = np.ascontiguousarray(frame_offsets, np.int64)
+        arr = (C.c_char_p * max(1, len(uuids)))(*[u.encode() for u in uuids])
+        self._chk(lib().tfp_index_add_device(self._h, len(uuids), arr, frame_offsets.ctypes.data,
+                                             C.c_void_p(d_micro), C.c_void_p(stream or None)))
+
+    def search_device(self, plan: "Plan", d_pcm: int, p: SearchParams, d_keys: int, stream: int = 0):
+        self._chk(lib().tfp_search_device(self._h, plan.handle, C.c_void_p(d_pcm), C.byref(p), C.c_void_p(d_keys),
+                                          C.c_void_p(stream or None)))
+
+    def synth_device(self, seed: int, clips, samples_per_clip: int, d_out: int, offsets=None, stream: int = 0):
+        clips = list(clips)
+        specs = synth_specs(seed, clips, offsets)
+        self._chk(lib().tfp_synth_pcm_device(self._h, specs, len(clips), samples_per_clip, C.c_void_p(d_out),
+                                             C.c_void_p(stream or None)))
+
+    def synchronize(self, stream: int = 0):
+        self._chk(lib().tfp_synchronize(self._h, C.c_void_p(stream or None)))
+
+
+class Plan:
+    def __init__(self, eng: Engine, offsets, sample_rate: int = 8000):
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        self._h = C.c_void_p()
+        eng._chk(lib().tfp_plan_create(eng.handle, offsets.ctypes.data, len(offsets) - 1, sample_rate,
+                                       C.byref(self._h)))
+        self.nframes = int(lib().tfp_plan_frames(self._h))
+        self.offsets = offsets
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if self._h:
+            lib().tfp_plan_destroy(self._h)
+            self._h = C.c_void_p()

@@ -1,0 +1,188 @@
+"""Host-side mirror of the reference engine facade (/root/reference/src/fp_handler.h:13-38).
+
+Same names, argument meaning and error behaviour as fp_handler.c, so tests read like the
+reference's callers (application_handler.c, cli_handler.c, app_tiresias.c):
+  * functions return True/False, a dict (the ast_json object) or None (NULL);
+  * fp_search_fingerprint_info returns None for both "no match" and "error"
+    (fp_handler.c:247-250, :386-390) and otherwise {uuid, name, context, hash,
+    frame_count, match_count} (fp_handler.c:394-404);
+  * fp_craete_audio_list_info (sic) returns True when the file is already enrolled
+    (fp_handler.c:181-185).
+
+The control plane (context_list / audio_list catalog, MD5 dedup, uuid v4) stays on SQLite,
+as the reference keeps it; the hot path — fingerprinting and matching — runs on the GPU via
+the C-ABI engine. The DB snapshot load/backup of fp_init/fp_term (fp_handler.c:68-108) is
+not part of the hot path and is not mirrored here.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import sqlite3
+import uuid as uuidlib
+import wave
+
+import numpy as np
+
+from .engine import Engine, params
+
+DEF_SEARCH_TOLERANCE = 0.001  # fp_handler.c:41
+DEF_AUBIO_COEFS = 2           # fp_handler.c:39
+
+
+def read_wav_mono16(filename: str):
+    """aubio_source at the file's native rate (DEF_AUBIO_SAMPLERATE 0): int16 PCM + rate."""
+    with wave.open(filename, "rb") as w:
+        if w.getsampwidth() != 2:
+            raise ValueError("only 16-bit PCM WAV is supported")
+        if w.getnchannels() != 1:
+            raise ValueError("only mono WAV is supported (multichannel downmix is out of scope)")
+        sr = w.getframerate()
+        data = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2").astype(np.int16)
+    return data, sr
+
+
+def write_wav_mono16(filename: str, pcm: np.ndarray, sample_rate: int = 8000):
+    with wave.open(filename, "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(sample_rate)
+        w.writeframes(np.ascontiguousarray(pcm, "<i2").tobytes())
+
+
+class FpHandler:
+    """One loaded module instance (g_db_ctx + the GPU engine)."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        self.db = None
+        self.engine = None
+
+    # fp_handler.c:68 — init_database (the catalog tables) + engine
+    def fp_init(self) -> bool:
+        self.db = sqlite3.connect(":memory:", check_same_thread=False)
+        c = self.db.cursor()
+        c.execute("create table context_list(   name        varchar(255),   directory   varchar(1023),"
+                  "   primary key(name));")
+        c.execute("create table audio_list(   uuid           varchar(255),   name           varchar(255),"
+                  "   context        varchar(255),\thash           varchar(1023));")
+        self.engine = Engine(self.device)
+        return True
+
+    def fp_term(self) -> bool:
+        if self.engine:
+            self.engine.close()
+        self.engine = None
+        if self.db:
+            self.db.close()
+        self.db = None
+        return True
+
+    # ---- contexts (fp_handler.c:912-1095) ----------------------------------------------
+    def fp_create_context_list_info(self, name: str, directory: str, replace: bool) -> bool:
+        if name is None or directory is None:
+            return False
+        verb = "insert or replace" if replace else "insert"
+        try:
+            self.db.execute("%s into context_list(name, directory) values (?, ?);" % verb, (name, directory))
+        except sqlite3.Error:
+            return False
+        return True
+
+    def fp_delete_context_list_info(self, name: str) -> bool:
+        if name is None:
+            return False
+        self.db.execute("delete from context_list where name = ?;", (name,))
+        return True
+
+    def fp_get_context_lists_all(self):
+        return [dict(zip(("name", "directory"), r)) for r in self.db.execute("select * from context_list;")]
+
+    def fp_get_context_list_info(self, name: str):
+        r = self.db.execute("select * from context_list where name = ?;", (name,)).fetchone()
+        return dict(zip(("name", "directory"), r)) if r else None
+
+    # ---- audio list ---------------------------------------------------------------------
+    def fp_get_audio_lists_all(self):
+        return [self._audio_row(r) for r in self.db.execute("select * from audio_list;")]
+
+    def fp_get_audio_lists_by_contextname(self, name: str):
+        if name is None:
+            return None
+        return [self._audio_row(r) for r in self.db.execute("select * from audio_list where context = ?;", (name,))]
+
+    @staticmethod
+    def _audio_row(r):
+        return dict(zip(("uuid", "name", "context", "hash"), r))
+
+    def _audio_list_info(self, uuid: str):
+        r = self.db.execute("select * from audio_list where uuid = ?;", (uuid,)).fetchone()
+        return self._audio_row(r) if r else None
+
+    @staticmethod
+    def fp_generate_uuid() -> str:
+        return str(uuidlib.uuid4())
+
+    @staticmethod
+    def fp_create_hash(filename: str):
+        try:
+            with open(filename, "rb") as f:
+                return hashlib.md5(f.read()).hexdigest()
+        except OSError:
+            return None
+
+    def fp_craete_audio_list_info(self, context: str, filename: str) -> bool:
+        """fp_handler.c:161-197: catalog row (MD5 dedup per context) + fingerprint rows."""
+        if context is None or filename is None:
+            return False
+        uuid = self.fp_generate_uuid()
+        h = self.fp_create_hash(filename)
+        if h is None:
+            return False
+        if self.db.execute("select * from audio_list where context = ? and hash = ?;", (context, h)).fetchone():
+            return True  # already enrolled
+        self.db.execute("insert into audio_list(uuid, name, context, hash) values (?, ?, ?, ?);",
+                        (uuid, os.path.basename(filename), context, h))
+        try:
+            pcm, sr = read_wav_mono16(filename)
+            fr = self.engine.fingerprint(pcm, sr)
+            self.engine.index_add(uuid, fr["m1"], fr["m2"])
+        except Exception:
+            self.fp_delete_audio_list_info(uuid)
+            return False
+        return True
+
+    def fp_delete_audio_list_info(self, uuid: str) -> bool:
+        """fp_handler.c:115-159: audio_list row + its fingerprint rows."""
+        if uuid is None:
+            return False
+        if self._audio_list_info(uuid) is None:
+            return False
+        self.db.execute("delete from audio_list where uuid = ?;", (uuid,))
+        try:
+            self.engine.index_remove(uuid)
+        except Exception:
+            pass  # no fingerprint rows (e.g. the fingerprint step failed)
+        return True
+
+    # ---- search (fp_handler.c:207-408) ------------------------------------------------
+    def fp_search_fingerprint_info(self, context, filename, coefs, tolerance, freq_ignore_low, freq_ignore_high):
+        if context is None or filename is None:
+            return None
+        if coefs < 1 or coefs > DEF_AUBIO_COEFS:
+            return None
+        try:
+            pcm, sr = read_wav_mono16(filename)
+        except (OSError, ValueError, EOFError, wave.Error):
+            return None
+        res, _ = self.engine.search_pcm_batch(pcm, [0, len(pcm)],
+                                              params(coefs, tolerance, freq_ignore_low, freq_ignore_high), sr)
+        hit = res[0]
+        if hit is None:
+            return None
+        info = self._audio_list_info(hit["audio_uuid"])
+        if info is None:
+            return None
+        info["frame_count"] = hit["frame_count"]
+        info["match_count"] = hit["match_count"]
+        return info

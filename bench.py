@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""Benchmark: fingerprints/sec + match latency p50, 8 kHz mono (BASELINE.json:metric).
+
+Step = one pass of the fingerprint hot path (create_audio_fingerprints, fp_handler.c:577-671)
+over one batch of synthetic PCM already resident in HBM: configs[1] = 1,024 clips x 30 s at
+8 kHz per GPU (960,512 fingerprints). Multi-GPU: one process per GPU (torchrun), each rank
+fingerprints its own 1,024 clips (clip-sharded, no collective on the data path): weak scaling.
+
+Also reported (same JSON line):
+  roofline      the fingerprint kernel: algorithmic 520 B/fingerprint (512 B PCM in + 8 B out,
+                SURVEY §8d) / average launch time measured with HIP events on the launch stream,
+                against 8 TB/s HBM; traffic = PMC-measured HBM bytes per launch if a profile exists.
+  cpu_baseline  the C oracle (oracle/, the reference path restated; `port`) on a bounded sample of
+                the same workload, all threads of this host.
+  match         configs[2]: 4,096 x 5 s queries vs a 100k-clip DB (93.8 M rows), coefs=1,
+                tolerance 0.001; batch-4096 time and batch-1 latency p50/p99 (host PCM in ->
+                result out); with N GPUs the DB is clip-sharded and the per-query keys are
+                combined by one RCCL all_reduce(MAX) (configs[3]).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "asterisk-tiresias_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+HOP = 256
+BYTES_PER_FP = 512 + 8
+HBM_PEAK_GBS = 8000.0
+SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def uuid_of(global_clip: int) -> str:
+    """Deterministic v4-shaped uuid per global clip id (same on every rank)."""
+    h = np.uint64(global_clip) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(0x7153A1)
+    a = int(h) & (2**64 - 1)
+    b = (a * 0xBF58476D1CE4E5B9 + global_clip) & (2**64 - 1)
+    x = (a << 64) | b
+    s = "%032x" % x
+    s = s[:12] + "4" + s[13:16] + "89ab"[int(s[16], 16) & 3] + s[17:]
+    return "%s-%s-%s-%s-%s" % (s[:8], s[8:12], s[12:16], s[16:20], s[20:32])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=1024)
+    ap.add_argument("--seconds", type=int, default=30)
+    ap.add_argument("--db-clips", type=int, default=100_000)
+    ap.add_argument("--queries", type=int, default=4096)
+    ap.add_argument("--latency-queries", type=int, default=40)
+    ap.add_argument("--no-match", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import tiresias_amd as T
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    eng = T.Engine(local)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    def max_over_ranks(x: float) -> float:
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    # ---------------------------------------------------------------- fingerprint (C2)
+    n = 8000 * args.seconds
+    nclips = args.clips
+    pcm = torch.empty((nclips, n), dtype=torch.int16, device=dev)
+    eng.synth_device(SEED_DB, range(rank * nclips, (rank + 1) * nclips), n, pcm.data_ptr(), stream=sh)
+    offsets = np.arange(nclips + 1, dtype=np.int64) * n
+    plan = eng.plan(offsets)
+    F = plan.nframes
+    micro = torch.empty((F, 2), dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    for _ in range(args.warmup):
+        eng.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, sh)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for i in range(args.steps):
+        eng.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, sh)
+        evs[i + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    launch_ms = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+    wall = max_over_ranks(wall)
+    ms_step = wall * 1e3 / args.steps
+    total_fp = F * world * args.steps
+    value = total_fp / wall
+    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    achieved = BYTES_PER_FP * F / avg_launch_s / 1e9
+    traffic = None
+    tpath = os.path.join(REPO, "profiles", "traffic_fingerprint.json")
+    if os.path.exists(tpath):
+        with open(tpath) as f:
+            tj = json.load(f)
+        if tj.get("frames_per_launch") == F:
+            traffic = tj.get("hbm_bytes_per_launch")
+    log(f"[rank {rank}] fingerprint: {F} fp/launch, avg launch {avg_launch_s*1e3:.3f} ms, {F/avg_launch_s/1e9:.3f} Gfp/s")
+
+    out = {
+        "metric": "fingerprints/sec + match latency p50, 8 kHz mono, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "fingerprints/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (deterministic counter-based 8 kHz PCM, tfp_synth)",
+        "config": {"workload": f"configs[1]: {nclips} x {args.seconds} s 8 kHz mono clips per GPU, fingerprint-only",
+                   "clips_per_gpu": nclips, "samples_per_clip": n, "frames_per_step_per_gpu": F,
+                   "parallelism": f"clip-sharded x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "fingerprint_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "bytes_per_unit": BYTES_PER_FP, "units_per_launch": F, "avg_launch_ms": avg_launch_s * 1e3},
+    }
+    del micro
+
+    # ---------------------------------------------------------------- CPU baseline (oracle)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import oracle_py
+        threads = min(os.cpu_count() or 1, 16)
+        host = pcm[: min(nclips, 256)].cpu().numpy()
+        probe = 2
+        t1 = time.perf_counter()
+        oracle_py.fingerprint_batch(host[:probe].reshape(-1), np.arange(probe + 1) * n, nthreads=1, want_db=False)
+        per_clip = (time.perf_counter() - t1) / probe
+        k = int(max(threads, min(len(host), args.cpu_seconds * threads / max(per_clip, 1e-6))))
+        k = min(k, len(host))
+        t1 = time.perf_counter()
+        oracle_py.fingerprint_batch(host[:k].reshape(-1), np.arange(k + 1) * n, nthreads=threads, want_db=False)
+        dt = time.perf_counter() - t1
+        fps = k * F / nclips / dt
+        out["cpu_baseline"] = {"value": fps, "unit": "fingerprints/s", "cores": threads, "kind": "port",
+                               "sample": f"{k} of the {nclips} x {args.seconds} s clips ({k * F // nclips} frames), "
+                                         f"oracle/oracle.c, {threads} threads, {dt:.1f} s"}
+        log(f"cpu baseline {fps:.0f} fp/s on {threads} threads ({dt:.1f} s)")
+    del pcm
+    torch.cuda.empty_cache()
+
+    # ---------------------------------------------------------------- match (C3 / C4)
+    if not args.no_match and args.db_clips > 0:
+        out["match"] = run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T):
+    n_db = 8000 * 30
+    nf_db = (n_db + HOP - 1) // HOP
+    mine = list(range(rank, args.db_clips, world))  # clip-sharded round robin
+    chunk = 2048
+    buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
+    micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
+    plan = eng.plan(np.arange(chunk + 1, dtype=np.int64) * n_db)
+    eng.index_clear()
+    t_build = time.perf_counter()
+    for s in range(0, len(mine), chunk):
+        ids = mine[s:s + chunk]
+        k = len(ids)
+        if k < chunk:
+            plan = eng.plan(np.arange(k + 1, dtype=np.int64) * n_db)
+        eng.synth_device(SEED_DB, ids, n_db, buf.data_ptr(), stream=sh)
+        eng.fingerprint_device(plan, buf.data_ptr(), micro.data_ptr(), 0, sh)
+        eng.index_add_device([uuid_of(g) for g in ids], np.arange(k + 1, dtype=np.int64) * nf_db, micro.data_ptr(), sh)
+    # global tie-break: rank of each uuid among all clips (every rank derives it, no exchange)
+    if world > 1:
+        all_u = [uuid_of(g) for g in range(args.db_clips)]
+        order = np.argsort(np.array(all_u))
+        grank = np.empty(args.db_clips, np.int32)
+        grank[order] = np.arange(args.db_clips, dtype=np.int32)
+        eng.set_tiebreak(grank[mine])
+    eng.index_commit()
+    torch.cuda.synchronize(dev)
+    t_build = time.perf_counter() - t_build
+    rows, nclips_local = eng.index_stats()
+    del buf, micro
+    torch.cuda.empty_cache()
+
+    # queries: 75 % excerpts of DB clips at 256-aligned offsets, 25 % unrelated
+    rng = np.random.default_rng(SEED_Q)
+    nq, qn = args.queries, 8000 * 5
+    seeds, clips, offs = [], [], []
+    for i in range(nq):
+        if i % 4 != 3:
+            clips.append(int(rng.integers(args.db_clips)))
+            offs.append(256 * int(rng.integers(0, (n_db - qn) // HOP)))
+            seeds.append(SEED_DB)
+        else:
+            clips.append(i)
+            offs.append(0)
+            seeds.append(SEED_Q)
+    qpcm = torch.empty((nq, qn), dtype=torch.int16, device=dev)
+    for sd in (SEED_DB, SEED_Q):
+        idx = [i for i in range(nq) if seeds[i] == sd]
+        tmp = torch.empty((len(idx), qn), dtype=torch.int16, device=dev)
+        eng.synth_device(sd, [clips[i] for i in idx], qn, tmp.data_ptr(), offsets=[offs[i] for i in idx], stream=sh)
+        qpcm[torch.tensor(idx, device=dev)] = tmp
+    qplan = eng.plan(np.arange(nq + 1, dtype=np.int64) * qn)
+    keys = torch.zeros(nq, dtype=torch.int64, device=dev)
+    p = T.params(1, 0.001)
+    torch.cuda.synchronize(dev)
+    for _ in range(2):
+        eng.search_device(qplan, qpcm.data_ptr(), p, keys.data_ptr(), sh)
+    torch.cuda.synchronize(dev)
+    reps = 5
+    times = []
+    for _ in range(reps):
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        eng.search_device(qplan, qpcm.data_ptr(), p, keys.data_ptr(), sh)
+        if dist:
+            dist.all_reduce(keys, op=dist.ReduceOp.MAX)
+        torch.cuda.synchronize(dev)
+        times.append(max_over_ranks(time.perf_counter() - t0))
+    batch_ms = float(np.median(times)) * 1e3
+    k = keys.cpu().numpy().view(np.uint64)
+    found = int((k != 0).sum())
+
+    # batch-1 latency: host PCM in -> (uuid, match_count, frame_count) out
+    host_q = qpcm[: args.latency_queries].cpu().numpy()
+    lat = []
+    for i in range(len(host_q)):
+        barrier()
+        t0 = time.perf_counter()
+        if dist:
+            dq = torch.from_numpy(host_q[i:i + 1]).to(dev)
+            kk = torch.zeros(1, dtype=torch.int64, device=dev)
+            eng.search_device(eng.plan(np.array([0, qn], np.int64)), dq.data_ptr(), p, kk.data_ptr(), sh)
+            dist.all_reduce(kk, op=dist.ReduceOp.MAX)
+            torch.cuda.synchronize(dev)
+            kk.item()
+        else:
+            eng.search_pcm_batch(host_q[i], [0, qn], p)
+        lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
+    return {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
+                        f" ({'sharded x%d, RCCL all_reduce MAX' % world if world > 1 else '1 GPU'})",
+            "coefs": 1, "tolerance": 0.001, "db_rows_local": rows, "db_clips_local": nclips_local,
+            "db_build_s": t_build, "batch_queries": nq, "batch_ms": batch_ms,
+            "queries_per_s": nq / (batch_ms / 1e3), "found": found,
+            "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
+            "latency_samples": len(lat)}
+
+
+if __name__ == "__main__":
+    main()

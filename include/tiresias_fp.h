@@ -1,0 +1,163 @@
+/* tiresias_fp.h — C-ABI of the MI355X-native tiresias fingerprint engine.
+ *
+ * Drop-in boundary for the hot path of pchero/asterisk-tiresias (/root/reference):
+ * the Asterisk-side C (application_handler.c, cli_handler.c, app_tiresias.c and the SQLite
+ * catalog in db_ctx_handler.c) keeps working and calls these entry points from a thin
+ * fp_handler.c shim. Plain C types only; memory is caller-allocated unless
+ * stated; every int return is TFP_OK (0) or a negative TFP_E_* code, with the message in
+ * tfp_engine_last_error(). All engine calls are thread-safe (serialised per engine).
+ *
+ * Reference interfaces replaced (file:line in /root/reference/src):
+ *   tfp_fingerprint_pcm / _batch      create_audio_fingerprints      fp_handler.c:577-671
+ *   tfp_index_add                     create_audio_fingerprint_info  fp_handler.c:538-575
+ *                                     (+ the INSERT it issues        db_ctx_handler.c:413-556)
+ *   tfp_index_remove                  fp_delete_audio_list_info's    fp_handler.c:146-157
+ *                                     "delete from audio_fingerprint where audio_uuid=..."
+ *   tfp_search / _batch / _pcm_batch  fp_search_fingerprint_info     fp_handler.c:207-408
+ *                                     (declared in fp_handler.h:28-35)
+ */
+#ifndef TIRESIAS_FP_H
+#define TIRESIAS_FP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFP_ABI_VERSION 1
+#define TFP_HOP 256              /* DEF_AUBIO_HOPSIZE, fp_handler.c:33 */
+#define TFP_WIN 512              /* DEF_AUBIO_BUFSIZE, fp_handler.c:34 */
+#define TFP_DEFAULT_TOLERANCE 0.001 /* DEF_SEARCH_TOLERANCE, fp_handler.c:41 */
+#define TFP_NULL_MICRO INT32_MIN /* a max1/max2 value the reference stores as SQL NULL */
+
+enum {
+  TFP_OK = 0,
+  TFP_E_ARG = -1,       /* bad argument (NULL pointer, bad size, coefs out of range ...) */
+  TFP_E_HIP = -2,       /* HIP runtime / kernel launch failure */
+  TFP_E_NOMEM = -3,     /* device or host allocation failed */
+  TFP_E_NOENT = -4,     /* uuid not in the index */
+  TFP_E_CAPACITY = -5,  /* caller buffer too small (needed size returned through out param) */
+  TFP_E_EXISTS = -6,    /* uuid already indexed */
+  TFP_E_NODEV = -7      /* no usable gfx950 device */
+};
+
+typedef struct tfp_engine tfp_engine;
+typedef struct tfp_plan tfp_plan;
+
+/* One fingerprint row = one 256-sample hop (reference JSON row {frame_idx, audio_uuid,
+ * max1, max2}, fp_handler.c:645-652). m1/m2 are the values as STORED: printf("%f") of
+ * 10*log10|c| in integer micro-units (db_ctx_handler.c:479-481); TFP_NULL_MICRO where the
+ * reference stores NULL. q1/q2 are the unrounded doubles the search loop reads back
+ * (fp_handler.c:290,321); -inf where the key is absent. */
+typedef struct tfp_frame {
+  int32_t frame_idx;
+  int32_t m1;
+  int32_t m2;
+  int32_t reserved;
+  double q1;
+  double q2;
+} tfp_frame;
+
+/* fp_search_fingerprint_info arguments (fp_handler.h:28-35). coefs in [1,2]; tolerance < 0
+ * selects TFP_DEFAULT_TOLERANCE; freq_ignore_* <= 0 disables the filter. */
+typedef struct tfp_search_params {
+  int32_t coefs;
+  int32_t freq_ignore_low;
+  int32_t freq_ignore_high;
+  int32_t reserved;
+  double tolerance;
+} tfp_search_params;
+
+/* Result of one search: the reference returns NULL (found = 0) or
+ * {uuid,...,frame_count,match_count} (fp_handler.c:394-404). */
+typedef struct tfp_result {
+  int32_t found;
+  int32_t match_count;   /* count(*) of the winning audio_uuid */
+  int32_t frame_count;   /* all query frames, ignored ones included */
+  int32_t clip_id;       /* engine clip id of the winner, -1 if none */
+  char uuid[64];         /* winning audio_uuid, NUL-terminated ("" if none) */
+} tfp_result;
+
+/* ---- engine ------------------------------------------------------------------------ */
+int tfp_abi_version(void);
+int tfp_device_count(int32_t* count);
+int tfp_engine_create(int32_t device, tfp_engine** out);
+void tfp_engine_destroy(tfp_engine* eng);
+const char* tfp_engine_last_error(const tfp_engine* eng);
+int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
+
+/* ---- fingerprinting: create_audio_fingerprints (fp_handler.c:577-671) -------------- */
+/* One clip of mono int16 PCM at its native rate (DEF_AUBIO_SAMPLERATE 0, :37). */
+int tfp_fingerprint_pcm(tfp_engine* eng, const int16_t* pcm, int64_t nsamples, int32_t sample_rate,
+                        tfp_frame* out, int64_t cap, int64_t* nframes);
+/* Many clips: offsets[nclips+1] are sample offsets into pcm; frames are concatenated in
+ * clip order (clip c starts at sum of tfp_frame_count of clips < c). */
+int tfp_fingerprint_batch(tfp_engine* eng, const int16_t* pcm, const int64_t* offsets, int32_t nclips,
+                          int32_t sample_rate, tfp_frame* out, int64_t cap, int64_t* nframes);
+
+/* Device-resident batches (inputs already in HBM; used by the benchmark and by callers that
+ * keep PCM on the GPU). A plan uploads the clip layout once. d_micro receives 2 int32 per
+ * frame (m1, m2), d_db 2 doubles per frame (q1, q2) or may be NULL. stream: hipStream_t or
+ * NULL for the engine's stream. Asynchronous: returns after the launch. */
+int tfp_plan_create(tfp_engine* eng, const int64_t* offsets, int32_t nclips, int32_t sample_rate,
+                    tfp_plan** out);
+void tfp_plan_destroy(tfp_plan* plan);
+int64_t tfp_plan_frames(const tfp_plan* plan);
+int tfp_fingerprint_device(tfp_engine* eng, const tfp_plan* plan, const int16_t* d_pcm, int32_t* d_micro,
+                           double* d_db, void* stream);
+
+/* ---- enrolled index: the audio_fingerprint table (fp_handler.c:713-753) ------------- */
+/* Append one clip's rows (create_audio_fingerprint_info). m1/m2 in micro-units. */
+int tfp_index_add(tfp_engine* eng, const char* uuid, const int32_t* m1, const int32_t* m2, int32_t nframes,
+                  int32_t* clip_id);
+/* Append nclips clips whose rows are already on the device: d_micro holds 2 int32 per frame
+ * in the layout tfp_fingerprint_device writes, frame_offsets[nclips+1] on the host. */
+int tfp_index_add_device(tfp_engine* eng, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
+                         const int32_t* d_micro, void* stream);
+int tfp_index_remove(tfp_engine* eng, const char* uuid);
+int tfp_index_clear(tfp_engine* eng);
+int tfp_index_stats(tfp_engine* eng, int64_t* nrows, int32_t* nclips);
+/* Rebuild the sorted device index now (otherwise done lazily by the next search). */
+int tfp_index_commit(tfp_engine* eng);
+/* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
+ * this engine's uuids). keys[clip_id] must order like the uuids across all shards. */
+int tfp_index_set_tiebreak(tfp_engine* eng, const int32_t* keys, int32_t nclip_ids);
+
+/* ---- search: fp_search_fingerprint_info (fp_handler.c:207-408) ---------------------- */
+int tfp_search(tfp_engine* eng, const tfp_frame* frames, int32_t nframes, const tfp_search_params* params,
+               tfp_result* out);
+/* qoffsets[nqueries+1] index into frames. */
+int tfp_search_batch(tfp_engine* eng, const tfp_frame* frames, const int64_t* qoffsets, int32_t nqueries,
+                     const tfp_search_params* params, tfp_result* out);
+/* PCM in, results out: fingerprints the queries on the GPU and searches without a host
+ * round trip of the frames (fp_handler.c:275 + :287-374). */
+int tfp_search_pcm_batch(tfp_engine* eng, const int16_t* pcm, const int64_t* offsets, int32_t nqueries,
+                         int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+/* Device form for benchmarks / sharded search: per query a 64-bit key
+ * (match_count << 32 | tiebreak key), 0 = NOTFOUND, written to d_keys[nqueries] (device).
+ * The maximum key over shards is the global winner (RCCL allreduce MAX). */
+int tfp_search_device(tfp_engine* eng, const tfp_plan* plan, const int16_t* d_pcm,
+                      const tfp_search_params* params, uint64_t* d_keys, void* stream);
+/* Map a tie-break key from tfp_search_device back to the uuid (this engine's clips only). */
+int tfp_index_uuid_of_key(tfp_engine* eng, int32_t key, char* uuid, int32_t len);
+
+/* ---- deterministic synthetic PCM (benchmark / test data; identical host and device) -- */
+/* One spec per clip: samples s of clip = synth(seed, clip, offset + s). */
+typedef struct tfp_synth_spec {
+  uint64_t seed;
+  int64_t clip;
+  int64_t offset;
+} tfp_synth_spec;
+int tfp_synth_pcm(const tfp_synth_spec* specs, int32_t nclips, int64_t samples_per_clip, int16_t* out);
+int tfp_synth_pcm_device(tfp_engine* eng, const tfp_synth_spec* specs, int32_t nclips, int64_t samples_per_clip,
+                         int16_t* d_out, void* stream);
+
+/* ---- misc --------------------------------------------------------------------------- */
+int tfp_synchronize(tfp_engine* eng, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,45 @@
+"""Shared test setup: paths, builds, the `gpu` marker."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "asterisk-tiresias_amd")
+for p in (PKG, os.path.join(REPO, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) — run with -m gpu")
+    config.addinivalue_line("markers", "slow: long-running check")
+
+
+def _make(path):
+    subprocess.run(["make", "-s", "-C", path], check=True)
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    _make(os.path.join(REPO, "oracle"))
+    import oracle_py
+    return oracle_py
+
+
+@pytest.fixture(scope="session")
+def tfp_lib():
+    if not os.path.exists(os.path.join(PKG, "lib", "libtiresias_fp.so")):
+        _make(PKG)
+    import tiresias_amd
+    return tiresias_amd
+
+
+@pytest.fixture(scope="session")
+def engine(tfp_lib):
+    if tfp_lib.device_count() < 1:
+        pytest.skip("no GPU visible")
+    e = tfp_lib.Engine(0)
+    yield e
+    e.close()

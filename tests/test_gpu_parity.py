@@ -1,0 +1,252 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle and the SQL goldens.
+
+Bar: bit-exact micro-units (the stored max1/max2 "hash set") and identical search results
+(uuid, match_count, frame_count) — integer work, no tolerance.
+"""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
+
+
+def _pcm_cases():
+    rng = np.random.default_rng(11)
+    cases = {
+        "empty": np.zeros(0, np.int16),
+        "one": np.array([1234], np.int16),
+        "hop-1": rng.integers(-30000, 30000, 255).astype(np.int16),
+        "hop": rng.integers(-30000, 30000, 256).astype(np.int16),
+        "hop+1": rng.integers(-30000, 30000, 257).astype(np.int16),
+        "silence": np.zeros(3000, np.int16),
+        "fullscale": np.where(np.arange(5000) % 2 == 0, 32767, -32768).astype(np.int16),
+        "dc": np.full(4097, -32768, np.int16),
+        "noise": rng.integers(-32768, 32767, 20000).astype(np.int16),
+        "tiny": rng.integers(-2, 3, 9000).astype(np.int16),
+    }
+    return cases
+
+
+def _assert_frames_equal(fr, micro, db):
+    assert len(fr) == len(micro)
+    assert np.array_equal(fr["m1"], micro[:, 0]), np.nonzero(fr["m1"] != micro[:, 0])
+    assert np.array_equal(fr["m2"], micro[:, 1]), np.nonzero(fr["m2"] != micro[:, 1])
+    # q: same float c in, glibc log10 (oracle) vs own log10 (GPU): equal or 1 ulp apart
+    for k, col in (("q1", 0), ("q2", 1)):
+        a, b = fr[k], db[:, col]
+        same = (a == b) | (np.isinf(a) & np.isinf(b))
+        near = np.abs(a - b) <= np.abs(np.spacing(b))
+        assert np.all(same | near)
+
+
+@pytest.mark.parametrize("name", list(_pcm_cases().keys()))
+def test_fingerprint_edge_cases_bit_exact(engine, oracle, name):
+    pcm = _pcm_cases()[name]
+    fr = engine.fingerprint(pcm)
+    _, db, micro = oracle.fingerprint(pcm)
+    _assert_frames_equal(fr, micro, db)
+    assert np.array_equal(fr["frame_idx"], np.arange(len(fr)))
+
+
+def test_fingerprint_synthetic_clips_bit_exact(engine, oracle, tfp_lib):
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(24), 80000)  # C1 shape: 10 s at 8 kHz
+    flat = pcm.reshape(-1)
+    off = np.arange(25) * 80000
+    fr = engine.fingerprint_batch(flat, off)
+    micro, db = oracle.fingerprint_batch(flat, off, nthreads=8)
+    _assert_frames_equal(fr, micro, db)
+    assert len(fr) == 24 * 313
+
+
+def test_fingerprint_ragged_batch_equals_single(engine, tfp_lib):
+    rng = np.random.default_rng(2)
+    lens = [0, 17, 256, 511, 4096, 4097, 12345, 0, 80000]
+    clips = [tfp_lib.synth_pcm(SEED_Q, [i], n)[0] if n else np.zeros(0, np.int16) for i, n in enumerate(lens)]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    batch = engine.fingerprint_batch(np.concatenate(clips), off)
+    single = np.concatenate([engine.fingerprint(c) for c in clips])
+    assert np.array_equal(batch, single)
+    rng.shuffle(clips)
+
+
+def test_fingerprint_other_sample_rates(engine, oracle, tfp_lib):
+    pcm = tfp_lib.synth_pcm(5, [0], 30000)[0]
+    for sr in (16000, 44100):
+        fr = engine.fingerprint(pcm, sr)
+        _, db, micro = oracle.fingerprint(pcm, sr)
+        _assert_frames_equal(fr, micro, db)
+
+
+# ---------------------------------------------------------------------------------- search
+
+def _load_golden():
+    with open(os.path.join(REPO, "tests", "golden", "match_cases.json")) as f:
+        return json.load(f)
+
+
+def _frames_from_q(q1, q2):
+    fr = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                     ("q1", "<f8"), ("q2", "<f8")]))
+    fr["q1"] = [-math.inf if v is None else v for v in q1]
+    fr["q2"] = [-math.inf if v is None else v for v in q2]
+    return fr
+
+
+def test_search_golden_sqlite(engine, tfp_lib):
+    """Every SQLite-produced golden case, through tfp_index_add + tfp_search."""
+    g = _load_golden()
+    n = 0
+    for s in g["scenarios"]:
+        engine.index_clear()
+        clip = np.asarray(s["clip"], np.int64)
+        m1 = np.asarray(s["m1"], np.int64)
+        m2 = np.asarray(s["m2"], np.int64)
+        for c, u in enumerate(s["uuids"]):
+            sel = clip == c
+            engine.index_add(u, m1[sel].astype(np.int32), m2[sel].astype(np.int32))
+        for q in s["queries"]:
+            p = tfp_lib.params(q["coefs"], q["tol"], q["low"], q["high"])
+            r, fc = engine.search(_frames_from_q(q["q1"], q["q2"]), p)
+            got = None if r is None else {"audio_uuid": r["audio_uuid"], "match_count": r["match_count"],
+                                          "frame_count": r["frame_count"]}
+            assert got == q["expect"], (s["name"], q["coefs"], q["tol"], q["low"], q["high"])
+            assert fc == q["frame_count"]
+            n += 1
+    engine.index_clear()
+    assert n > 900
+
+
+def _build_db(engine, oracle, tfp_lib, nclips, seconds, seed=SEED_DB):
+    n = 8000 * seconds
+    pcm = tfp_lib.synth_pcm(seed, range(nclips), n)
+    off = np.arange(nclips + 1) * n
+    micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), off, nthreads=8, want_db=False)
+    nf = (n + 255) // 256
+    rng = np.random.default_rng(seed)
+    uuids = [str(__import__("uuid").UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
+    engine.index_clear()
+    for c in range(nclips):
+        engine.index_add(uuids[c], micro[c * nf:(c + 1) * nf, 0], micro[c * nf:(c + 1) * nf, 1])
+    clip = np.repeat(np.arange(nclips), nf)
+    return uuids, micro, clip
+
+
+def _queries(tfp_lib, nq, db_clips, seconds_db, seconds_q, seed=SEED_Q):
+    rng = np.random.default_rng(seed)
+    specs_seed, clips, offs = [], [], []
+    n = 8000 * seconds_q
+    out = np.zeros((nq, n), np.int16)
+    for i in range(nq):
+        if i % 4 != 3:
+            c = int(rng.integers(db_clips))
+            o = 256 * int(rng.integers(0, (8000 * seconds_db - n) // 256))
+            out[i] = tfp_lib.synth_pcm(SEED_DB, [c], n, offsets=[o])[0]
+        else:
+            out[i] = tfp_lib.synth_pcm(seed, [i], n)[0]
+    return out
+
+
+@pytest.mark.parametrize("coefs,tol,low,high", [
+    (1, 0.001, -1, -1), (1, -1.0, -1, -1), (1, 0.01, -1, -1), (1, 0.1, 100, 3400), (1, 0.45, -1, -1),
+    (2, 0.001, -1, -1), (2, 0.1, -1, -1), (2, 0.45, 100, 3400), (2, 1.0, -1, -1),
+])
+def test_search_pcm_vs_oracle(engine, oracle, tfp_lib, coefs, tol, low, high):
+    uuids, micro, clip = _build_db(engine, oracle, tfp_lib, 120, 12)
+    qpcm = _queries(tfp_lib, 24, 120, 12, 5)
+    off = np.arange(25) * qpcm.shape[1]
+    res, fcs = engine.search_pcm_batch(qpcm.reshape(-1), off, tfp_lib.params(coefs, tol, low, high))
+    for i in range(24):
+        _, qdb, _ = oracle.fingerprint(qpcm[i])
+        found, w, mc, fc = oracle.search(micro[:, 0], micro[:, 1], clip, uuids, qdb[:, 0], qdb[:, 1],
+                                         coefs, tol, low, high)
+        exp = {"audio_uuid": uuids[w], "match_count": mc} if found else None
+        got = None if res[i] is None else {"audio_uuid": res[i]["audio_uuid"], "match_count": res[i]["match_count"]}
+        assert got == exp, (i, coefs, tol)
+        assert fcs[i] == fc == 157
+
+
+def test_search_scan_fallback_many_frames_one_key(engine, oracle, tfp_lib):
+    """> 2048 frames with the same key exceed fp16-exact counts: the scan path must take over."""
+    uuids, micro, clip = _build_db(engine, oracle, tfp_lib, 40, 6)
+    q = np.zeros(2100 * 256, np.int16)  # silence: every frame has the same trunc key
+    res, fcs = engine.search_pcm_batch(q, [0, len(q)], tfp_lib.params(1, 0.45))
+    _, qdb, _ = oracle.fingerprint(q)
+    found, w, mc, fc = oracle.search(micro[:, 0], micro[:, 1], clip, uuids, qdb[:, 0], qdb[:, 1], 1, 0.45, -1, -1)
+    got = None if res[0] is None else (res[0]["audio_uuid"], res[0]["match_count"])
+    assert got == ((uuids[w], mc) if found else None)
+    assert fcs[0] == 2100
+
+
+def test_index_remove_and_readd(engine, oracle, tfp_lib):
+    uuids, micro, clip = _build_db(engine, oracle, tfp_lib, 30, 6)
+    qpcm = _queries(tfp_lib, 8, 30, 6, 3)
+    off = np.arange(9) * qpcm.shape[1]
+    p = tfp_lib.params(1, 0.1)
+    res, _ = engine.search_pcm_batch(qpcm.reshape(-1), off, p)
+    winners = {r["audio_uuid"] for r in res if r}
+    assert winners
+    for u in winners:
+        engine.index_remove(u)
+    keep = np.array([u not in winners for u in uuids])
+    res2, _ = engine.search_pcm_batch(qpcm.reshape(-1), off, p)
+    sel = keep[clip]
+    for i in range(8):
+        _, qdb, _ = oracle.fingerprint(qpcm[i])
+        found, w, mc, _ = oracle.search(micro[sel, 0], micro[sel, 1], clip[sel],
+                                        uuids, qdb[:, 0], qdb[:, 1], 1, 0.1, -1, -1)
+        got = None if res2[i] is None else (res2[i]["audio_uuid"], res2[i]["match_count"])
+        assert got == ((uuids[w], mc) if found else None)
+    with pytest.raises(tfp_lib.TfpError):
+        engine.index_remove(next(iter(winners)))
+    with pytest.raises(tfp_lib.TfpError):
+        engine.index_add(uuids[0] if uuids[0] not in winners else uuids[1], [1], [1])
+
+
+def test_search_bad_coefs_is_notfound(engine, tfp_lib):
+    fr = _frames_from_q([24.3], [1.0])
+    for c in (0, 3, -1):
+        r, fc = engine.search(fr, tfp_lib.params(c, 0.001))
+        assert r is None and fc == 1
+
+
+def test_fp_handler_mirror_end_to_end(tmp_path, oracle, tfp_lib):
+    """The reference's create/search flow (app_tiresias enrolment + dialplan search)."""
+    from tiresias_amd.fp_handler import FpHandler, write_wav_mono16
+    fp = FpHandler(0)
+    assert fp.fp_init()
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(12), 8000 * 8)
+    files = []
+    for i in range(12):
+        f = str(tmp_path / f"clip{i}.wav")
+        write_wav_mono16(f, pcm[i])
+        files.append(f)
+        assert fp.fp_craete_audio_list_info("ctx%d" % (i % 2), f)
+    assert fp.fp_craete_audio_list_info("ctx0", files[0])  # already enrolled -> true
+    assert len(fp.fp_get_audio_lists_all()) == 12
+    q = str(tmp_path / "q.wav")
+    write_wav_mono16(q, pcm[5][256 * 40: 256 * 40 + 24000])
+    res = fp.fp_search_fingerprint_info("ctx1", q, 1, 0.45, -1, -1)
+    # expected through the oracle chain
+    rows = [oracle.fingerprint(pcm[i])[2] for i in range(12)]
+    uu = {r["name"]: r["uuid"] for r in fp.fp_get_audio_lists_all()}
+    uuids = [uu["clip%d.wav" % i] for i in range(12)]
+    micro = np.concatenate(rows)
+    clip = np.repeat(np.arange(12), len(rows[0]))
+    _, qdb, _ = oracle.fingerprint(pcm[5][256 * 40: 256 * 40 + 24000])
+    found, w, mc, fc = oracle.search(micro[:, 0], micro[:, 1], clip, uuids, qdb[:, 0], qdb[:, 1], 1, 0.45, -1, -1)
+    if found:
+        assert res["uuid"] == uuids[w] and res["match_count"] == mc and res["frame_count"] == fc == 94
+        assert res["name"] == "clip%d.wav" % w and res["context"] == "ctx%d" % (w % 2)
+        assert fp.fp_delete_audio_list_info(res["uuid"])
+    else:
+        assert res is None
+    assert fp.fp_search_fingerprint_info("ctx1", q, 3, 0.45, -1, -1) is None
+    assert fp.fp_search_fingerprint_info("ctx1", str(tmp_path / "missing.wav"), 1, 0.45, -1, -1) is None
+    assert fp.fp_term()
