@@ -135,7 +135,11 @@ __global__ __launch_bounds__(256) void fingerprint_kernel(const DspTables* __res
       const float ti = wr * Or - wi * Oi;
       const float Xr = 0.5f * (Er + tr);
       const float Xi = 0.5f * (Ei - ti);
-      nrm[k2] = __fsqrt_rn(Xr * Xr + Xi * Xi);
+      // sqrtf, correctly rounded as SSE sqrtss is: v_sqrt_f32 is not, but the double root of
+      // a float rounds to the correctly rounded float root (no float input has its root within
+      // 2^-50 of a float midpoint, and the f64 sqrt sequence is accurate to < 1 ulp).
+      const float s2 = Xr * Xr + Xi * Xi;
+      nrm[k2] = (float)__builtin_sqrt((double)s2);
     }
   }
   __syncthreads();

@@ -36,6 +36,12 @@ def _pcm_cases():
 
 def _assert_frames_equal(fr, micro, db):
     assert len(fr) == len(micro)
+    bad = (fr["m1"] != micro[:, 0]) | (fr["m2"] != micro[:, 1])
+    if bad.any():
+        i = np.nonzero(bad)[0]
+        print("mismatching frames:", len(i), "of", len(fr), "first:", i[:10])
+        print("gpu q1,q2:", fr["q1"][i[:5]], fr["q2"][i[:5]])
+        print("cpu q1,q2:", db[i[:5], 0], db[i[:5], 1])
     assert np.array_equal(fr["m1"], micro[:, 0]), np.nonzero(fr["m1"] != micro[:, 0])
     assert np.array_equal(fr["m2"], micro[:, 1]), np.nonzero(fr["m2"] != micro[:, 1])
     # q: same float c in, glibc log10 (oracle) vs own log10 (GPU): equal or 1 ulp apart
