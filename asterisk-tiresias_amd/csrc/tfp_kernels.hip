@@ -56,118 +56,304 @@ __device__ __forceinline__ void dft16(const DspTables* __restrict__ T, const flo
 }
 
 // ------------------------------------------------------------------------------------
-// Fingerprint kernel. Block = 16 frames of one clip; lane group (16 lanes) = one frame.
-//   LDS: PCM tile of 17 hops (frame t's window = hops t, t+1) + one 16x17 complex scratch per frame.
-constexpr int kTileSamples = (kFramesPerBlock + 1) * kHop;
-constexpr int kScratch = 16 * 17;  // float2 per frame
+// Fingerprint kernel (persistent, wave-independent).
+//   * A workgroup stages the DSP tables in LDS once; afterwards its 4 waves never wait on each
+//     other: each wave walks 16-frame tiles on its own (tile = 16 consecutive frames of a clip).
+//   * FFT stage: 16 lanes per frame, 4 frames per pass, 4 passes per tile. The 256-point complex
+//     FFT is 16x16 Cooley-Tukey with the transpose through an XOR-swizzled LDS square; the real
+//     split, |X|, the filterbank and the log10 stay on the frame's 16 lanes. Each frame leaves its
+//     40 band logs in the wave's log buffer.
+//   * Tail: once per tile, 32 lanes (frame, coef) run the DCT row, 10*log10|c| and "%f" rounding.
+//   * PCM is read straight from HBM into registers (each hop is read by two frames; the second
+//     read hits L2).
+#ifndef TFP_FP_WAVES
+#define TFP_FP_WAVES 3  // waves per SIMD the register budget is cut for (A/B: scripts/ab_waves.sh)
+#endif
+constexpr int kWaveFrames = 16;     // frames per wave tile (== kFramesPerBlock: tile offsets)
+constexpr int kFrameStride = 258;   // float2 per frame scratch: 16x16 square + 16 B bank shift
+constexpr int kLogStride = 41;      // floats per frame row in the log buffer (bank-conflict free)
+constexpr int kMelLds = 512;        // packed filterbank weights kept in LDS (8 kHz: 490)
 
-__global__ __launch_bounds__(256) void fingerprint_kernel(const DspTables* __restrict__ T, const int16_t* __restrict__ pcm,
-                                                          const int64_t* __restrict__ soff, const int64_t* __restrict__ foff,
-                                                          const int32_t* __restrict__ toff, int32_t nclips,
-                                                          int32_t* __restrict__ micro, double* __restrict__ db) {
-  __shared__ int16_t tile[kTileSamples];
-  __shared__ float2 work[kFramesPerBlock][kScratch];
+struct LdsTables {
+  float window[kWin];
+  float tw256_re[256], tw256_im[256];
+  float tw512_re[kBins], tw512_im[kBins];
+  float dct[kCoefs][kFilters];
+  int32_t mel_start[kFilters], mel_len[kFilters], mel_off[kFilters];
+  float mel_w[kMelLds];
+};
 
-  const int b = blockIdx.x;
-  int lo = 0, hi = nclips;  // clip c with toff[c] <= b < toff[c+1]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (toff[mid] <= b) lo = mid; else hi = mid;
+constexpr int kPassSamples = 5 * kHop;           // one pass = 4 frames = hops f-1 .. f+3
+constexpr int kPassChunks = kPassSamples / 8;     // 16-byte chunks per pass (160)
+constexpr int kChunkRounds = (kPassChunks + 63) / 64;
+
+// The pass's staged PCM aliases the FFT scratch: it is read into registers (z) before the first
+// write of the transpose square, and restaged only after the filterbank has read |X|.
+struct WaveLds {
+  union {
+    float2 scratch[4][kFrameStride];
+    alignas(16) int16_t pcm[kPassSamples];
+  };
+  float logs[kWaveFrames * kLogStride];
+};
+static_assert(sizeof(int16_t) * kPassSamples <= sizeof(float2) * 4 * kFrameStride, "pcm alias fits");
+
+// Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
+struct PassSrc {
+  const int16_t* clip;
+  int64_t ns;
+  int64_t sbase;
+  bool aligned;  // clip + sbase is 16-byte aligned
+};
+
+// Slow path of one 16-byte chunk: clip edges (zeros outside [0, ns): aubio_source pads the last
+// hop, the phase vocoder's first history hop is zeros) and unaligned clips.
+__device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns, int64_t s) {
+  uint32_t w[4];
+  for (int e = 0; e < 4; e++) {
+    const int64_t a = s + 2 * e;
+    const uint32_t lo = (a >= 0 && a < ns) ? (uint16_t)clip[a] : 0u;
+    const uint32_t hi = (a + 1 >= 0 && a + 1 < ns) ? (uint16_t)clip[a + 1] : 0u;
+    w[e] = lo | (hi << 16);
   }
-  const int c = lo;
-  const int64_t s0 = soff[c], ns = soff[c + 1] - s0;
-  const int64_t nf = (ns + kHop - 1) / kHop;
-  const int64_t f0 = (int64_t)(b - toff[c]) * kFramesPerBlock;
+  return make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+}
+
+// 16-byte chunks of a pass into registers, issued one pass ahead of use.
+__device__ __forceinline__ void fetch_pass(const PassSrc& p, bool valid, int lane, int4 (&pf)[kChunkRounds]) {
+#pragma unroll
+  for (int r = 0; r < kChunkRounds; r++) {
+    const int chunk = lane + 64 * r;
+    int4 v = make_int4(0, 0, 0, 0);
+    if (valid && chunk < kPassChunks) {
+      const int64_t s = p.sbase + 8 * chunk;
+      if (p.aligned && s >= 0 && s + 8 <= p.ns) v = *reinterpret_cast<const int4*>(p.clip + s);
+      else v = fetch_chunk_checked(p.clip, p.ns, s);
+    }
+    pf[r] = v;
+  }
+}
+
+// All LDS exchanges below stay inside one wave: a wave-level fence + barrier orders them.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float pcm_f(int16_t v) { return (float)v * (1.0f / 32768.0f); }
+
+// Correctly rounded sqrtf (= SSE sqrtss, what glibc's sqrtf is). For inputs in [2^-100, 2^100)
+// the raw v_sqrt_f32 (<= 1 ulp) is corrected with two exact fma residuals — the sequence LLVM
+// emits for IEEE sqrt minus its denormal scaling and special-value handling, which are only
+// needed outside that range; there the full builtin runs.
+__device__ __forceinline__ float cr_sqrtf(float x) {
+  if (x >= 0x1p-100f && x < 0x1p100f) {
+    float y = __builtin_amdgcn_sqrtf(x);
+    const float ym = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) - 1u);
+    const float yp = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) + 1u);
+    const float rm = __builtin_fmaf(-ym, y, x);
+    const float rp = __builtin_fmaf(-yp, y, x);
+    y = rm <= 0.f ? ym : y;
+    y = rp > 0.f ? yp : y;
+    return y;
+  }
+  return __builtin_sqrtf(x);
+}
+
+__global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const DspTables* __restrict__ T, const int16_t* __restrict__ pcm,
+                                                             const int64_t* __restrict__ soff, const int64_t* __restrict__ foff,
+                                                             const int32_t* __restrict__ toff, int32_t nclips, int32_t ntiles,
+                                                             int32_t* __restrict__ micro, double* __restrict__ db,
+                                                             int32_t ablate) {
+  __shared__ LdsTables S;
+  __shared__ __attribute__((aligned(16))) WaveLds WL[4];
   const int tid = threadIdx.x;
-
-  // Stage hops f0-1 .. f0+15 (zeros before the clip and past its end: aubio_source_do pads).
-  const int64_t base = (f0 - 1) * kHop;
-  for (int i = tid; i < kTileSamples; i += 256) {
-    const int64_t s = base + i;
-    tile[i] = (s >= 0 && s < ns) ? pcm[s0 + s] : (int16_t)0;
-  }
-  __syncthreads();
-
-  const int t = tid >> 4, L = tid & 15;
-  const int16_t* win = tile + t * kHop;
-  float2* W = work[t];
-
-  // z[m] = x[2m] + i x[2m+1], x = fftshift(window * [old | new]); lane L holds m = 16 n1 + L.
-  float2 z[16], Y[16];
-#pragma unroll
-  for (int n1 = 0; n1 < 16; n1++) {
-    const int j = (32 * n1 + 2 * L + 256) & 511;
-    const float a = (float)win[j] * (1.0f / 32768.0f);
-    const float bb = (float)win[j + 1] * (1.0f / 32768.0f);
-    z[n1].x = a * T->window[j];
-    z[n1].y = bb * T->window[j + 1];
-  }
-  dft16(T, z, Y);
-#pragma unroll
-  for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], T->tw256_re[L * k1], T->tw256_im[L * k1]);
-#pragma unroll
-  for (int k1 = 0; k1 < 16; k1++) W[L * 17 + k1] = Y[k1];
-  __syncthreads();
-#pragma unroll
-  for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * 17 + L];
-  dft16(T, z, Y);  // Y[k2] = Z[L + 16 k2]
-  __syncthreads();
-#pragma unroll
-  for (int k2 = 0; k2 < 16; k2++) W[L + 16 * k2] = Y[k2];
-  __syncthreads();
-  float2 P[16];
-#pragma unroll
-  for (int k2 = 0; k2 < 16; k2++) P[k2] = W[(256 - (L + 16 * k2)) & 255];
-  // |X[k]| of the 512-point real FFT, k = L + 16 k2 (k = 0 and 256 from Z[0]).
-  float nrm[16];
-  float nrm256 = 0.f;
-#pragma unroll
-  for (int k2 = 0; k2 < 16; k2++) {
-    const int k = L + 16 * k2;
-    const float a = Y[k2].x, bq = Y[k2].y, cc = P[k2].x, d = P[k2].y;
-    if (k == 0) {
-      nrm[k2] = fabsf(a + bq);
-      nrm256 = fabsf(a - bq);
-    } else {
-      const float Er = a + cc, Ei = bq - d, Or = a - cc, Oi = bq + d;
-      const float wr = T->tw512_re[k], wi = T->tw512_im[k];
-      const float tr = wr * Oi + wi * Or;
-      const float ti = wr * Or - wi * Oi;
-      const float Xr = 0.5f * (Er + tr);
-      const float Xi = 0.5f * (Ei - ti);
-      // sqrtf, correctly rounded as SSE sqrtss is: v_sqrt_f32 is not, but the double root of
-      // a float rounds to the correctly rounded float root (no float input has its root within
-      // 2^-50 of a float midpoint, and the f64 sqrt sequence is accurate to < 1 ulp).
-      const float s2 = Xr * Xr + Xi * Xi;
-      nrm[k2] = (float)__builtin_sqrt((double)s2);
+  {
+    const float* src = T->window;  // window .. tw512_im are contiguous in both structs
+    float* dst = S.window;
+    for (int i = tid; i < kWin + 512 + 2 * kBins; i += 256) dst[i] = src[i];
+    for (int i = tid; i < kCoefs * kFilters; i += 256) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
+    for (int i = tid; i < kFilters; i += 256) {
+      S.mel_start[i] = T->mel_start[i];
+      S.mel_len[i] = T->mel_len[i];
+      S.mel_off[i] = T->mel_off[i];
     }
+    const int mt = T->mel_total < kMelLds ? T->mel_total : kMelLds;
+    for (int i = tid; i < mt; i += 256) S.mel_w[i] = T->mel_w[i];
   }
+  const bool mel_in_lds = T->mel_total <= kMelLds;
+  const float* __restrict__ melw = mel_in_lds ? S.mel_w : T->mel_w;
   __syncthreads();
-  float* N = reinterpret_cast<float*>(W);  // norms at [0, 257), band logs at [260, 300)
-#pragma unroll
-  for (int k2 = 0; k2 < 16; k2++) N[L + 16 * k2] = nrm[k2];
-  if (L == 0) N[256] = nrm256;
-  __syncthreads();
-  // Filterbank (sequential ascending-bin sums, as fmat_vecmul) + fvec_log10.
-#pragma unroll
-  for (int r = 0; r < 3; r++) {
-    const int jf = L + 16 * r;
-    if (jf < kFilters) {
-      const int st = T->mel_start[jf], len = T->mel_len[jf], off = T->mel_off[jf];
-      float acc = 0.f;
-      for (int q = 0; q < len; q++) acc = acc + N[st + q] * T->mel_w[off + q];
-      N[260 + jf] = aubio_log10_clamped(acc);
+
+  const int wave = tid >> 6, lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  WaveLds& M = WL[wave];
+  float2* W = M.scratch[grp];
+  float* N = reinterpret_cast<float*>(W);  // |X| at [0, 257) after the FFT
+  const int nwaves = gridDim.x * 4;
+
+  // tile b -> (clip, first frame); PassSrc of pass `sub` of tile b
+  auto tile_clip = [&](int b, int& c, int64_t& f0) {
+    int lo = 0, hi = nclips;  // clip c with toff[c] <= b < toff[c+1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (toff[mid] <= b) lo = mid; else hi = mid;
     }
-  }
-  __syncthreads();
-  const int64_t f = f0 + t;
-  if (L < kCoefs && f < nf) {
-    float acc = 0.f;
-    for (int i = 0; i < kFilters; i++) acc = acc + N[260 + i] * T->dct[L][i];
-    const double q = db_of_coef(acc);
-    const int64_t g = foff[c] + f;
-    micro[2 * g + L] = micro_of_db(q);
-    if (db) db[2 * g + L] = q;
+    c = lo;
+    f0 = (int64_t)(b - toff[c]) * kWaveFrames;
+  };
+  auto pass_src = [&](int c, int64_t f0, int sub) {
+    PassSrc p;
+    const int64_t s0 = soff[c];
+    p.clip = pcm + s0;
+    p.ns = soff[c + 1] - s0;
+    p.sbase = (f0 + 4 * sub - 1) * kHop;
+    p.aligned = ((reinterpret_cast<uintptr_t>(p.clip) & 15) == 0);
+    return p;
+  };
+
+  int4 pf[kChunkRounds];
+  int b = blockIdx.x * 4 + wave;
+  int c = 0;
+  int64_t f0 = 0;
+  if (b < ntiles) tile_clip(b, c, f0);
+  fetch_pass(pass_src(c, f0, 0), b < ntiles, lane, pf);
+  for (; b < ntiles; b += nwaves) {
+    const int64_t s0 = soff[c], ns = soff[c + 1] - s0;
+    const int64_t nf = (ns + kHop - 1) / kHop;
+    const int cur_c = c;
+    const int64_t cur_f0 = f0;
+    const int bn = b + nwaves;
+    int cn = c;
+    int64_t fn0 = f0;
+    if (bn < ntiles) tile_clip(bn, cn, fn0);
+
+    for (int sub = 0; sub < 4; sub++) {
+      const int row = sub * 4 + grp;
+      const int64_t f = cur_f0 + row;
+      // stage this pass's PCM (prefetched) and prefetch the next pass
+      wave_sync();  // the previous pass's readers of M.pcm are done
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        if (chunk < kPassChunks) reinterpret_cast<int4*>(M.pcm)[chunk] = pf[r];
+      }
+      {
+        const bool same = sub < 3;
+        fetch_pass(pass_src(same ? cur_c : cn, same ? cur_f0 : fn0, same ? sub + 1 : 0), same || bn < ntiles, lane, pf);
+      }
+      wave_sync();
+      // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
+      // m = 16 n1 + L. Frame grp's window starts at hop grp of the staged pass.
+      const int32_t* __restrict__ w32 = reinterpret_cast<const int32_t*>(M.pcm + grp * kHop);
+      // Opaque zero: keeps the per-lane table reads (window, twiddles) in LDS instead of letting
+      // the compiler hoist ~90 of them into registers for the whole kernel (occupancy).
+      int oz = 0;
+      asm volatile("" : "+v"(oz));
+      const float* __restrict__ win = S.window + oz;
+      const float* __restrict__ t256r = S.tw256_re + oz;
+      const float* __restrict__ t256i = S.tw256_im + oz;
+      const float* __restrict__ t512r = S.tw512_re + oz;
+      const float* __restrict__ t512i = S.tw512_im + oz;
+      float2 z[16], Y[16];
+      if (ablate & 1) {
+#pragma unroll
+        for (int n1 = 0; n1 < 16; n1++) { z[n1].x = S.window[n1 + L]; z[n1].y = (float)f; }
+      } else {
+#pragma unroll
+        for (int n1 = 0; n1 < 16; n1++) {
+          const int j = (32 * n1 + 2 * L + 256) & 511;
+          const int32_t v = w32[j >> 1];
+          z[n1].x = pcm_f((int16_t)(v & 0xffff)) * win[j];
+          z[n1].y = pcm_f((int16_t)(v >> 16)) * win[j + 1];
+        }
+      }
+      if (ablate & 2) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) Y[k] = z[k];
+      } else {
+      dft16(T, z, Y);
+#pragma unroll
+      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], t256r[L * k1], t256i[L * k1]);
+      wave_sync();  // the previous pass's readers of W are done
+#pragma unroll
+      for (int k1 = 0; k1 < 16; k1++) W[L * 16 + (k1 ^ L)] = Y[k1];
+      wave_sync();
+#pragma unroll
+      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * 16 + (L ^ n2)];
+      dft16(T, z, Y);  // Y[k2] = Z[L + 16 k2]
+      }
+      wave_sync();       // every lane has read its column of the square: W is free for |X|
+      // |X[k]| of the 512-point real FFT, k = L + 16 k2, needs Z[256 - k]: for L >= 1 that is
+      // Y[15 - k2] of lane 16 - L, for L = 0 it is this lane's own Y[16 - k2] (Z[256] = Z[0]).
+      if (ablate & 4) {
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) N[L + 16 * k2] = Y[k2].x + Y[k2].y;
+        if (L == 0) N[256] = Y[0].x;
+      } else
+#pragma unroll
+      for (int k2 = 0; k2 < 16; k2++) {
+        const int k = L + 16 * k2;
+        float2 P;
+        P.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
+        P.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
+        if (L == 0) P = Y[(16 - k2) & 15];
+        const float a = Y[k2].x, bq = Y[k2].y, cc = P.x, d = P.y;
+        if (k == 0) {
+          N[0] = fabsf(a + bq);
+          N[256] = fabsf(a - bq);
+        } else {
+          const float Er = a + cc, Ei = bq - d, Or = a - cc, Oi = bq + d;
+          const float wr = t512r[k], wi = t512i[k];
+          const float tr = wr * Oi + wi * Or;
+          const float ti = wr * Or - wi * Oi;
+          const float Xr = 0.5f * (Er + tr);
+          const float Xi = 0.5f * (Ei - ti);
+          N[k] = cr_sqrtf(Xr * Xr + Xi * Xi);
+        }
+      }
+      wave_sync();
+      // Filterbank (sequential ascending-bin sums, as fmat_vecmul) + fvec_log10.
+      float* lrow = M.logs + row * kLogStride;
+      if (ablate & 8) {
+        for (int r = 0; r < 3; r++) if (L + 16 * r < kFilters) lrow[L + 16 * r] = N[L + 16 * r];
+      } else
+#pragma unroll
+      for (int r = 0; r < 3; r++) {
+        const int jf = L + 16 * r;
+        if (jf < kFilters) {
+          const int st = S.mel_start[jf], len = S.mel_len[jf], off = S.mel_off[jf];
+          float acc = 0.f;
+#pragma unroll 4
+          for (int q = 0; q < len; q++) acc = acc + N[st + q] * melw[off + q];
+          lrow[jf] = aubio_log10_clamped(acc);
+        }
+      }
+    }
+    wave_sync();
+    // Tail: lane = (frame row, coef) for the tile's 16 frames: DCT row (fmat_vecmul order),
+    // 10*log10|c| (fp_handler.c:651), "%f" micro-units / NULL (db_ctx_handler.c:479-481).
+    if ((ablate & 16) && lane < 2 * kWaveFrames) {
+      const int row = lane >> 1, cf = lane & 1;
+      const int64_t f = f0 + row;
+      if (f < nf) micro[2 * (foff[cur_c] + f) + cf] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cf]);
+    } else if (lane < 2 * kWaveFrames) {
+      const int row = lane >> 1, cf = lane & 1;
+      const int64_t f = f0 + row;
+      if (f < nf) {
+        const float* lrow = M.logs + row * kLogStride;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cf][i];
+        const double q = db_of_coef(acc);
+        const int64_t g = foff[cur_c] + f;
+        micro[2 * g + cf] = micro_of_db(q);
+        if (db) db[2 * g + cf] = q;
+      }
+    }
+    wave_sync();  // the log buffer is rewritten by the next tile
+    c = cn;
+    f0 = fn0;
   }
 }
 
@@ -175,8 +361,23 @@ hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, c
                               const int64_t* d_foff, const int32_t* d_toff, int32_t nclips, int32_t ntiles,
                               int32_t* d_micro, double* d_db, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(fingerprint_kernel, dim3(ntiles), dim3(256), 0, s, d_tables, d_pcm, d_soff, d_foff, d_toff,
-                     nclips, d_micro, d_db);
+  static int grid_cap = 0;
+  if (!grid_cap) {
+    int dev = 0, cus = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, 256, 0);
+    grid_cap = cus * (per > 0 ? per : 1);
+  }
+  const int want = (ntiles + 3) / 4;  // 4 waves per workgroup, one tile per wave per step
+  const int grid = want < grid_cap ? want : grid_cap;
+  static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production
+  if (ablate < 0) {
+    const char* a = getenv("TFP_ABLATE");
+    ablate = a ? atoi(a) : 0;
+  }
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(256), 0, s, d_tables, d_pcm, d_soff, d_foff, d_toff,
+                     nclips, ntiles, d_micro, d_db, ablate);
   return hipGetLastError();
 }
 
@@ -317,29 +518,39 @@ hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc
 // [fmt6(k - tol), fmt6(k + tol)] — exactly the per-frame "group by audio_uuid" hit count.
 __global__ void key_hist_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
                                 int32_t* __restrict__ counts, uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= nq) return;
-  int32_t local_max = 0;
-  for (int64_t i = qoff[q]; i < qoff[q + 1]; i++) {
+  __shared__ uint32_t smask[kKeyRange / 32];
+  __shared__ int32_t smax;
+  for (int i = threadIdx.x; i < kKeyRange / 32; i += blockDim.x) smask[i] = 0;
+  if (threadIdx.x == 0) smax = 0;
+  __syncthreads();
+  const int64_t nf = qoff[nq];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
     const FrameBox bx = boxes[i];
     if (!(bx.flags & 1)) continue;
     const int64_t idx = (int64_t)bx.k + kKeyOffset;
     if (idx < 0 || idx >= kKeyRange) {  // not a fingerprint-range key: send the batch to the scan path
-      local_max = INT32_MAX;
+      atomicMax(&smax, INT32_MAX);
       continue;
     }
-    const int32_t v = ++counts[(int64_t)q * kKeyRange + idx];
-    local_max = v > local_max ? v : local_max;
-    atomicOr(&mask[idx >> 5], 1u << (idx & 31));
+    int lo = 0, hi = nq;  // query of frame i
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (qoff[mid] <= i) lo = mid; else hi = mid;
+    }
+    const int32_t v = atomicAdd(&counts[(int64_t)lo * kKeyRange + idx], 1) + 1;
+    if (v > 1024) atomicMax(&smax, v);  // only large counts matter (fp16 exactness limit 2048)
+    atomicOr(&smask[idx >> 5], 1u << (idx & 31));
   }
-  if (local_max) atomicMax(maxc, local_max);
+  __syncthreads();
+  for (int i = threadIdx.x; i < kKeyRange / 32; i += blockDim.x)
+    if (smask[i]) atomicOr(&mask[i], smask[i]);
+  if (threadIdx.x == 0 && smax) atomicMax(maxc, smax);
 }
 
 hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts, uint32_t* d_mask,
                            int32_t* d_maxcount, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_hist_kernel, dim3((nq + 255) / 256), dim3(256), 0, s, boxes, d_qoff, nq, d_counts, d_mask,
-                     d_maxcount);
+  hipLaunchKernelGGL(key_hist_kernel, dim3(1024), dim3(256), 0, s, boxes, d_qoff, nq, d_counts, d_mask, d_maxcount);
   return hipGetLastError();
 }
 

@@ -64,6 +64,7 @@ def main():
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only to rehearse N ranks on one GPU")
     args = ap.parse_args()
 
     import torch
@@ -73,14 +74,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    ndev = torch.cuda.device_count()
+    gpu = local if args.dist_backend == "nccl" else local % max(ndev, 1)
+    torch.cuda.set_device(gpu)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    eng = T.Engine(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.dist_backend)
+    dev = torch.device("cuda", gpu)
+    eng = T.Engine(gpu)
     # a real (non-null) stream: every launch and every event goes on it
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
@@ -196,9 +200,11 @@ def main():
 
 
 def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T):
+    from tiresias_amd import sharding
     n_db = 8000 * 30
     nf_db = (n_db + HOP - 1) // HOP
-    mine = list(range(rank, args.db_clips, world))  # clip-sharded round robin
+    from tiresias_amd import sharding
+    mine = sharding.shard_clips(args.db_clips, world, rank).tolist()  # clip-sharded round robin
     chunk = 2048
     buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
     micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
@@ -215,10 +221,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         eng.index_add_device([uuid_of(g) for g in ids], np.arange(k + 1, dtype=np.int64) * nf_db, micro.data_ptr(), sh)
     # global tie-break: rank of each uuid among all clips (every rank derives it, no exchange)
     if world > 1:
-        all_u = [uuid_of(g) for g in range(args.db_clips)]
-        order = np.argsort(np.array(all_u))
-        grank = np.empty(args.db_clips, np.int32)
-        grank[order] = np.arange(args.db_clips, dtype=np.int32)
+        grank = sharding.global_tiebreak([uuid_of(g) for g in range(args.db_clips)])
         eng.set_tiebreak(grank[mine])
     eng.index_commit()
     torch.cuda.synchronize(dev)
@@ -260,8 +263,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         eng.search_device(qplan, qpcm.data_ptr(), p, keys.data_ptr(), sh)
-        if dist:
-            dist.all_reduce(keys, op=dist.ReduceOp.MAX)
+        sharding.combine(keys, dist)
         torch.cuda.synchronize(dev)
         times.append(max_over_ranks(time.perf_counter() - t0))
     batch_ms = float(np.median(times)) * 1e3
@@ -278,7 +280,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             dq = torch.from_numpy(host_q[i:i + 1]).to(dev)
             kk = torch.zeros(1, dtype=torch.int64, device=dev)
             eng.search_device(eng.plan(np.array([0, qn], np.int64)), dq.data_ptr(), p, kk.data_ptr(), sh)
-            dist.all_reduce(kk, op=dist.ReduceOp.MAX)
+            sharding.combine(kk, dist)
             torch.cuda.synchronize(dev)
             kk.item()
         else:
@@ -286,6 +288,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
     return {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, RCCL all_reduce MAX' % world if world > 1 else '1 GPU'})",
+            "collective": "all_reduce(MAX) of one int64 key per query" if world > 1 else None,
             "coefs": 1, "tolerance": 0.001, "db_rows_local": rows, "db_clips_local": nclips_local,
             "db_build_s": t_build, "batch_queries": nq, "batch_ms": batch_ms,
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,

@@ -5,6 +5,11 @@ import sys
 
 import pytest
 
+try:  # torch first: it and libtiresias_fp.so must share one HIP runtime (same SONAME)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is plumbing for the device-path tests only
+    torch = None
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "asterisk-tiresias_amd")
 for p in (PKG, os.path.join(REPO, "oracle")):
