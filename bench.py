@@ -287,7 +287,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             eng.search_pcm_batch(host_q[i], [0, qn], p)
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
     return {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
-                        f" ({'sharded x%d, RCCL all_reduce MAX' % world if world > 1 else '1 GPU'})",
+                        f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": "all_reduce(MAX) of one int64 key per query" if world > 1 else None,
             "coefs": 1, "tolerance": 0.001, "db_rows_local": rows, "db_clips_local": nclips_local,
             "db_build_s": t_build, "batch_queries": nq, "batch_ms": batch_ms,
