@@ -55,8 +55,8 @@ struct tfp_plan {
   int32_t nclips = 0, ntiles = 0, sample_rate = 0;
   int64_t nsamples = 0, nframes = 0;
   std::vector<int64_t> soff, foff;
-  std::vector<int32_t> toff;
-  DevBuf d_soff, d_foff, d_toff;
+  std::vector<int32_t> toff, tclip;
+  DevBuf d_soff, d_foff, d_toff, d_tclip;
   std::vector<int64_t> qoff;  // == foff (frames per clip as queries)
   DevBuf d_qoff;
   tfp_engine* eng = nullptr;
@@ -88,7 +88,7 @@ struct tfp_engine {
   // scratch
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
   DevBuf pcm, q, qoff, boxes, counts, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
-  DevBuf soff, foff, toff, specs;
+  DevBuf soff, foff, toff, tclip, specs;
 };
 
 namespace {
@@ -127,7 +127,7 @@ int ensure_tables(tfp_engine* e, int sr, const DspTables** out) {
 
 // Clip layout: sample, frame and 16-frame-tile offsets.
 void layout(const int64_t* offsets, int32_t nclips, std::vector<int64_t>& soff, std::vector<int64_t>& foff,
-            std::vector<int32_t>& toff) {
+            std::vector<int32_t>& toff, std::vector<int32_t>* tclip = nullptr) {
   soff.assign(offsets, offsets + nclips + 1);
   const int64_t base = soff[0];
   for (auto& v : soff) v -= base;
@@ -137,6 +137,11 @@ void layout(const int64_t* offsets, int32_t nclips, std::vector<int64_t>& soff, 
     const int64_t nf = tfp_frame_count(soff[c + 1] - soff[c]);
     foff[c + 1] = foff[c] + nf;
     toff[c + 1] = toff[c] + (int32_t)((nf + kFramesPerBlock - 1) / kFramesPerBlock);
+  }
+  if (tclip) {
+    tclip->assign(std::max<int32_t>(toff[nclips], 1), 0);
+    for (int32_t c = 0; c < nclips; c++)
+      for (int32_t t = toff[c]; t < toff[c + 1]; t++) (*tclip)[t] = c;
   }
 }
 
@@ -153,17 +158,18 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   int rc = ensure_tables(e, sr, &T);
   if (rc) return rc;
   std::vector<int64_t> soff, foff;
-  std::vector<int32_t> toff;
-  layout(offsets, nclips, soff, foff, toff);
+  std::vector<int32_t> toff, tclip;
+  layout(offsets, nclips, soff, foff, toff, &tclip);
   const int64_t ns = soff[nclips], nf = foff[nclips];
   if ((rc = upload(e, e->pcm, pcm + offsets[0], sizeof(int16_t) * ns))) return rc;
   if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
   if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
   if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
+  if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
   HIPCHK(e, launch_fingerprint(T, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->foff.as<int64_t>(),
-                               e->toff.as<int32_t>(), nclips, toff[nclips], e->micro.as<int32_t>(),
+                               e->toff.as<int32_t>(), e->tclip.as<int32_t>(), toff[nclips], e->micro.as<int32_t>(),
                                e->db.as<double>(), e->stream));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
@@ -493,13 +499,14 @@ int tfp_plan_create(tfp_engine* e, const int64_t* offsets, int32_t nclips, int32
   p->eng = e;
   p->nclips = nclips;
   p->sample_rate = sr;
-  layout(offsets, nclips, p->soff, p->foff, p->toff);
+  layout(offsets, nclips, p->soff, p->foff, p->toff, &p->tclip);
   p->nsamples = p->soff[nclips];
   p->nframes = p->foff[nclips];
   p->ntiles = p->toff[nclips];
   if ((rc = upload(e, p->d_soff, p->soff.data(), sizeof(int64_t) * p->soff.size())) ||
       (rc = upload(e, p->d_foff, p->foff.data(), sizeof(int64_t) * p->foff.size())) ||
       (rc = upload(e, p->d_toff, p->toff.data(), sizeof(int32_t) * p->toff.size())) ||
+      (rc = upload(e, p->d_tclip, p->tclip.data(), sizeof(int32_t) * p->tclip.size())) ||
       (rc = upload(e, p->d_qoff, p->foff.data(), sizeof(int64_t) * p->foff.size()))) {
     delete p;
     return rc;
@@ -521,7 +528,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
-                               p->nclips, p->ntiles, d_micro, d_db, s));
+                               p->d_tclip.as<int32_t>(), p->ntiles, d_micro, d_db, s));
   return TFP_OK;
 }
 
@@ -715,7 +722,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
   HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
-                               p->nclips, p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
+                               p->d_tclip.as<int32_t>(), p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
   std::vector<unsigned long long> keys;
   return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
                      reinterpret_cast<unsigned long long*>(d_keys), s);

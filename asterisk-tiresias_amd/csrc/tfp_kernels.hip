@@ -40,7 +40,7 @@ __device__ __forceinline__ void dft4(float2 a0, float2 a1, float2 a2, float2 a3,
 }
 
 // 16-point DFT in registers: n = 4 n1 + n2, k = k1 + 4 k2, W16^e = tw256[16 e].
-__device__ __forceinline__ void dft16(const DspTables* __restrict__ T, const float2 (&in)[16], float2 (&out)[16]) {
+__device__ __forceinline__ void dft16(const float2* __restrict__ w16, const float2 (&in)[16], float2 (&out)[16]) {
   float2 A[4][4];
 #pragma unroll
   for (int n2 = 0; n2 < 4; n2++) dft4(in[n2], in[4 + n2], in[8 + n2], in[12 + n2], A[n2][0], A[n2][1], A[n2][2], A[n2][3]);
@@ -49,7 +49,8 @@ __device__ __forceinline__ void dft16(const DspTables* __restrict__ T, const flo
 #pragma unroll
     for (int k1 = 1; k1 < 4; k1++) {
       const int e = 16 * n2 * k1;
-      A[n2][k1] = cmul(A[n2][k1], T->tw256_re[e], T->tw256_im[e]);
+      const float2 w = w16[e >> 4];
+      A[n2][k1] = cmul(A[n2][k1], w.x, w.y);
     }
 #pragma unroll
   for (int k1 = 0; k1 < 4; k1++) dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
@@ -64,39 +65,45 @@ __device__ __forceinline__ void dft16(const DspTables* __restrict__ T, const flo
 //     split, |X|, the filterbank and the log10 stay on the frame's 16 lanes. Each frame leaves its
 //     40 band logs in the wave's log buffer.
 //   * Tail: once per tile, 32 lanes (frame, coef) run the DCT row, 10*log10|c| and "%f" rounding.
-//   * PCM is read straight from HBM into registers (each hop is read by two frames; the second
-//     read hits L2).
+//   * PCM: each pass's 5 hops are fetched with coalesced 16-byte loads one pass ahead (registers),
+//     then staged in the wave's LDS scratch.
+//   * Filterbank: a lane's 3 filters (slot schedule, see DspTables) are summed interleaved.
 #ifndef TFP_FP_WAVES
-#define TFP_FP_WAVES 3  // waves per SIMD the register budget is cut for (A/B: scripts/ab_waves.sh)
+#define TFP_FP_WAVES 2  // waves per SIMD the register budget is cut for (A/B: scripts/ab_waves.sh)
 #endif
 constexpr int kWaveFrames = 16;     // frames per wave tile (== kFramesPerBlock: tile offsets)
-constexpr int kFrameStride = 258;   // float2 per frame scratch: 16x16 square + 16 B bank shift
+constexpr int kFrameStride = 258;   // float2 per frame scratch: 16x16 XOR-swizzled square + pad
 constexpr int kLogStride = 41;      // floats per frame row in the log buffer (bank-conflict free)
-constexpr int kMelLds = 512;        // packed filterbank weights kept in LDS (8 kHz: 490)
+constexpr int kMsLds = 864;         // filterbank slot-schedule weights kept in LDS (8 kHz: 848)
 
 struct LdsTables {
   float window[kWin];
-  float tw256_re[256], tw256_im[256];
-  float tw512_re[kBins], tw512_im[kBins];
+  float2 lane_tw[15][16];          // lane_tw[k1-1][L] = w256^(L*k1), k1 = 1..15
+  float2 w16[10];                  // W16^e = tw256[16 e] (dft16's internal twiddles)
+  float2 tw512[kBins];             // w512^k for the real split
   float dct[kCoefs][kFilters];
-  int32_t mel_start[kFilters], mel_len[kFilters], mel_off[kFilters];
-  float mel_w[kMelLds];
+  int32_t ms_len[3], ms_woff[3];
+  int32_t ms_filter[3][16], ms_start[3][16];
+  LogfEntry logf[16];
+  float ms_w[kMsLds];
 };
 
 constexpr int kPassSamples = 5 * kHop;           // one pass = 4 frames = hops f-1 .. f+3
 constexpr int kPassChunks = kPassSamples / 8;     // 16-byte chunks per pass (160)
 constexpr int kChunkRounds = (kPassChunks + 63) / 64;
+constexpr int kHopStride = kHop + 32;  // staged hop stride in samples: frames 0/1 (and 2/3) of a
+                                       // 32-lane half read disjoint LDS bank halves
 
 // The pass's staged PCM aliases the FFT scratch: it is read into registers (z) before the first
 // write of the transpose square, and restaged only after the filterbank has read |X|.
 struct WaveLds {
   union {
     float2 scratch[4][kFrameStride];
-    alignas(16) int16_t pcm[kPassSamples];
+    alignas(16) int16_t pcm[5 * kHopStride];
   };
   float logs[kWaveFrames * kLogStride];
 };
-static_assert(sizeof(int16_t) * kPassSamples <= sizeof(float2) * 4 * kFrameStride, "pcm alias fits");
+static_assert(sizeof(int16_t) * 5 * kHopStride <= sizeof(float2) * 4 * kFrameStride, "pcm alias fits");
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
 struct PassSrc {
@@ -161,29 +168,52 @@ __device__ __forceinline__ float cr_sqrtf(float x) {
   return __builtin_sqrtf(x);
 }
 
-__global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const DspTables* __restrict__ T, const int16_t* __restrict__ pcm,
-                                                             const int64_t* __restrict__ soff, const int64_t* __restrict__ foff,
-                                                             const int32_t* __restrict__ toff, int32_t nclips, int32_t ntiles,
-                                                             int32_t* __restrict__ micro, double* __restrict__ db,
-                                                             int32_t ablate) {
+// One lane's 3 filterbank sums (slots A/B/C, lenA >= lenB >= lenC), interleaved in three
+// branch-free phases. Each sum runs over its bins in ascending order from 0 (fmat_vecmul); the
+// zero-padded tail of a short filter adds exact +0 (N beyond bin 256 is zero-filled).
+// W is instantiated per address space (LDS or global) so every load is a ds_read/global_load.
+template <class WPtr>
+__device__ __forceinline__ void mel3(const float* __restrict__ N, WPtr wA, WPtr wB, WPtr wC, int stA, int stB,
+                                     int stC, int lenA, int lenB, int lenC, float& aA, float& aB, float& aC) {
+  int q = 0;
+#pragma unroll 4
+  for (; q < lenC; q++) {
+    aA = aA + N[stA + q] * wA[16 * q];
+    aB = aB + N[stB + q] * wB[16 * q];
+    aC = aC + N[stC + q] * wC[16 * q];
+  }
+#pragma unroll 4
+  for (; q < lenB; q++) {
+    aA = aA + N[stA + q] * wA[16 * q];
+    aB = aB + N[stB + q] * wB[16 * q];
+  }
+#pragma unroll 4
+  for (; q < lenA; q++) aA = aA + N[stA + q] * wA[16 * q];
+}
+
+__global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
+    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ soff,
+    const int64_t* __restrict__ foff, const int32_t* __restrict__ toff, const int32_t* __restrict__ tclip,
+    int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
   __shared__ LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[4];
   const int tid = threadIdx.x;
-  {
-    const float* src = T->window;  // window .. tw512_im are contiguous in both structs
-    float* dst = S.window;
-    for (int i = tid; i < kWin + 512 + 2 * kBins; i += 256) dst[i] = src[i];
-    for (int i = tid; i < kCoefs * kFilters; i += 256) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
-    for (int i = tid; i < kFilters; i += 256) {
-      S.mel_start[i] = T->mel_start[i];
-      S.mel_len[i] = T->mel_len[i];
-      S.mel_off[i] = T->mel_off[i];
-    }
-    const int mt = T->mel_total < kMelLds ? T->mel_total : kMelLds;
-    for (int i = tid; i < mt; i += 256) S.mel_w[i] = T->mel_w[i];
+  for (int i = tid; i < kWin; i += 256) S.window[i] = T->window[i];
+  for (int i = tid; i < 15 * 16; i += 256) {
+    const int k1 = 1 + i / 16, L = i % 16;
+    S.lane_tw[k1 - 1][L] = make_float2(T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]);
   }
-  const bool mel_in_lds = T->mel_total <= kMelLds;
-  const float* __restrict__ melw = mel_in_lds ? S.mel_w : T->mel_w;
+  for (int i = tid; i < 10; i += 256) S.w16[i] = make_float2(T->tw256_re[16 * i], T->tw256_im[16 * i]);
+  for (int i = tid; i < kBins; i += 256) S.tw512[i] = make_float2(T->tw512_re[i], T->tw512_im[i]);
+  for (int i = tid; i < kCoefs * kFilters; i += 256) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
+  for (int i = tid; i < 48; i += 256) {
+    (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
+    (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
+  }
+  if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
+  if (tid < 16) S.logf[tid] = logf_table()[tid];
+  const bool ms_in_lds = T->ms_total <= kMsLds;
+  for (int i = tid; i < (ms_in_lds ? T->ms_total : 0); i += 256) S.ms_w[i] = T->ms_w[i];
   __syncthreads();
 
   const int wave = tid >> 6, lane = tid & 63, grp = lane >> 4, L = lane & 15;
@@ -191,17 +221,10 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
   float2* W = M.scratch[grp];
   float* N = reinterpret_cast<float*>(W);  // |X| at [0, 257) after the FFT
   const int nwaves = gridDim.x * 4;
+  const int lenA = S.ms_len[0], lenB = S.ms_len[1], lenC = S.ms_len[2];
+  const int maxbin = T->ms_maxbin;
+  const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
 
-  // tile b -> (clip, first frame); PassSrc of pass `sub` of tile b
-  auto tile_clip = [&](int b, int& c, int64_t& f0) {
-    int lo = 0, hi = nclips;  // clip c with toff[c] <= b < toff[c+1]
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (toff[mid] <= b) lo = mid; else hi = mid;
-    }
-    c = lo;
-    f0 = (int64_t)(b - toff[c]) * kWaveFrames;
-  };
   auto pass_src = [&](int c, int64_t f0, int sub) {
     PassSrc p;
     const int64_t s0 = soff[c];
@@ -214,29 +237,27 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
 
   int4 pf[kChunkRounds];
   int b = blockIdx.x * 4 + wave;
-  int c = 0;
-  int64_t f0 = 0;
-  if (b < ntiles) tile_clip(b, c, f0);
+  int c = b < ntiles ? tclip[b] : 0;
+  int64_t f0 = b < ntiles ? (int64_t)(b - toff[c]) * kWaveFrames : 0;
   fetch_pass(pass_src(c, f0, 0), b < ntiles, lane, pf);
   for (; b < ntiles; b += nwaves) {
-    const int64_t s0 = soff[c], ns = soff[c + 1] - s0;
-    const int64_t nf = (ns + kHop - 1) / kHop;
+    const int64_t nf = (soff[c + 1] - soff[c] + kHop - 1) / kHop;
     const int cur_c = c;
     const int64_t cur_f0 = f0;
     const int bn = b + nwaves;
-    int cn = c;
-    int64_t fn0 = f0;
-    if (bn < ntiles) tile_clip(bn, cn, fn0);
+    const int cn = bn < ntiles ? tclip[bn] : c;
+    const int64_t fn0 = bn < ntiles ? (int64_t)(bn - toff[cn]) * kWaveFrames : f0;
 
     for (int sub = 0; sub < 4; sub++) {
       const int row = sub * 4 + grp;
       const int64_t f = cur_f0 + row;
-      // stage this pass's PCM (prefetched) and prefetch the next pass
-      wave_sync();  // the previous pass's readers of M.pcm are done
+      // stage this pass's PCM (prefetched; hop h at h * kHopStride) and prefetch the next pass
+      wave_sync();  // the previous pass's readers of the scratch are done
 #pragma unroll
       for (int r = 0; r < kChunkRounds; r++) {
         const int chunk = lane + 64 * r;
-        if (chunk < kPassChunks) reinterpret_cast<int4*>(M.pcm)[chunk] = pf[r];
+        if (chunk < kPassChunks)
+          *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
       }
       {
         const bool same = sub < 3;
@@ -244,26 +265,24 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
       }
       wave_sync();
       // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
-      // m = 16 n1 + L. Frame grp's window starts at hop grp of the staged pass.
-      const int32_t* __restrict__ w32 = reinterpret_cast<const int32_t*>(M.pcm + grp * kHop);
-      // Opaque zero: keeps the per-lane table reads (window, twiddles) in LDS instead of letting
-      // the compiler hoist ~90 of them into registers for the whole kernel (occupancy).
+      // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
+      // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
+      const int16_t* hop0 = M.pcm + grp * kHopStride;
+      // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
+      // ~90 of them into registers for the whole kernel (occupancy).
       int oz = 0;
       asm volatile("" : "+v"(oz));
       const float* __restrict__ win = S.window + oz;
-      const float* __restrict__ t256r = S.tw256_re + oz;
-      const float* __restrict__ t256i = S.tw256_im + oz;
-      const float* __restrict__ t512r = S.tw512_re + oz;
-      const float* __restrict__ t512i = S.tw512_im + oz;
       float2 z[16], Y[16];
       if (ablate & 1) {
 #pragma unroll
-        for (int n1 = 0; n1 < 16; n1++) { z[n1].x = S.window[n1 + L]; z[n1].y = (float)f; }
+        for (int n1 = 0; n1 < 16; n1++) { z[n1].x = win[n1 + L]; z[n1].y = (float)f; }
       } else {
 #pragma unroll
         for (int n1 = 0; n1 < 16; n1++) {
           const int j = (32 * n1 + 2 * L + 256) & 511;
-          const int32_t v = w32[j >> 1];
+          const int hsel = n1 < 8 ? 1 : 0;
+          const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
           z[n1].x = pcm_f((int16_t)(v & 0xffff)) * win[j];
           z[n1].y = pcm_f((int16_t)(v >> 16)) * win[j + 1];
         }
@@ -272,62 +291,71 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
 #pragma unroll
         for (int k = 0; k < 16; k++) Y[k] = z[k];
       } else {
-      dft16(T, z, Y);
+        dft16(S.w16, z, Y);
 #pragma unroll
-      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], t256r[L * k1], t256i[L * k1]);
-      wave_sync();  // the previous pass's readers of W are done
+        for (int k1 = 1; k1 < 16; k1++) {
+          const float2 w = S.lane_tw[k1 - 1][L + oz];
+          Y[k1] = cmul(Y[k1], w.x, w.y);
+        }
+        wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
-      for (int k1 = 0; k1 < 16; k1++) W[L * 16 + (k1 ^ L)] = Y[k1];
-      wave_sync();
+        for (int k1 = 0; k1 < 16; k1++) W[L * 16 + (k1 ^ L)] = Y[k1];
+        wave_sync();
 #pragma unroll
-      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * 16 + (L ^ n2)];
-      dft16(T, z, Y);  // Y[k2] = Z[L + 16 k2]
+        for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * 16 + (L ^ n2)];
+        dft16(S.w16, z, Y);  // Y[k2] = Z[L + 16 k2]
       }
-      wave_sync();       // every lane has read its column of the square: W is free for |X|
+      wave_sync();  // every lane has read its column of the square: W is free for |X|
       // |X[k]| of the 512-point real FFT, k = L + 16 k2, needs Z[256 - k]: for L >= 1 that is
       // Y[15 - k2] of lane 16 - L, for L = 0 it is this lane's own Y[16 - k2] (Z[256] = Z[0]).
       if (ablate & 4) {
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) N[L + 16 * k2] = Y[k2].x + Y[k2].y;
         if (L == 0) N[256] = Y[0].x;
-      } else
+      } else {
 #pragma unroll
-      for (int k2 = 0; k2 < 16; k2++) {
-        const int k = L + 16 * k2;
-        float2 P;
-        P.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
-        P.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
-        if (L == 0) P = Y[(16 - k2) & 15];
-        const float a = Y[k2].x, bq = Y[k2].y, cc = P.x, d = P.y;
-        if (k == 0) {
-          N[0] = fabsf(a + bq);
-          N[256] = fabsf(a - bq);
-        } else {
-          const float Er = a + cc, Ei = bq - d, Or = a - cc, Oi = bq + d;
-          const float wr = t512r[k], wi = t512i[k];
-          const float tr = wr * Oi + wi * Or;
-          const float ti = wr * Or - wi * Oi;
-          const float Xr = 0.5f * (Er + tr);
-          const float Xi = 0.5f * (Ei - ti);
-          N[k] = cr_sqrtf(Xr * Xr + Xi * Xi);
+        for (int k2 = 0; k2 < 16; k2++) {
+          const int k = L + 16 * k2;
+          float2 P;
+          P.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
+          P.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
+          if (L == 0) P = Y[(16 - k2) & 15];
+          const float a = Y[k2].x, bq = Y[k2].y, cc = P.x, d = P.y;
+          if (k == 0) {
+            N[0] = fabsf(a + bq);
+            N[256] = fabsf(a - bq);
+          } else {
+            const float Er = a + cc, Ei = bq - d, Or = a - cc, Oi = bq + d;
+            const float2 w = S.tw512[k + oz];
+            const float tr = w.x * Oi + w.y * Or;
+            const float ti = w.x * Or - w.y * Oi;
+            const float Xr = 0.5f * (Er + tr);
+            const float Xi = 0.5f * (Ei - ti);
+            N[k] = cr_sqrtf(Xr * Xr + Xi * Xi);
+          }
         }
       }
+      for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;  // bins past 256 read by padded filters
       wave_sync();
-      // Filterbank (sequential ascending-bin sums, as fmat_vecmul) + fvec_log10.
+      // Filterbank: this lane's 3 filters (slots A, B, C) summed interleaved, each in ascending
+      // bin order from 0 (fmat_vecmul); then fvec_log10 of each.
       float* lrow = M.logs + row * kLogStride;
       if (ablate & 8) {
-        for (int r = 0; r < 3; r++) if (L + 16 * r < kFilters) lrow[L + 16 * r] = N[L + 16 * r];
-      } else
-#pragma unroll
-      for (int r = 0; r < 3; r++) {
-        const int jf = L + 16 * r;
-        if (jf < kFilters) {
-          const int st = S.mel_start[jf], len = S.mel_len[jf], off = S.mel_off[jf];
-          float acc = 0.f;
-#pragma unroll 4
-          for (int q = 0; q < len; q++) acc = acc + N[st + q] * melw[off + q];
-          lrow[jf] = aubio_log10_clamped(acc);
-        }
+        lrow[fA] = N[L];
+        if (fB >= 0) lrow[fB] = N[L + 16];
+        if (fC >= 0) lrow[fC] = N[L + 32];
+      } else {
+        const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+        float aA = 0.f, aB = 0.f, aC = 0.f;
+        if (ms_in_lds)
+          mel3(N, S.ms_w + S.ms_woff[0] + L, S.ms_w + S.ms_woff[1] + L, S.ms_w + S.ms_woff[2] + L, stA, stB, stC,
+               lenA, lenB, lenC, aA, aB, aC);
+        else
+          mel3(N, T->ms_w + S.ms_woff[0] + L, T->ms_w + S.ms_woff[1] + L, T->ms_w + S.ms_woff[2] + L, stA, stB,
+               stC, lenA, lenB, lenC, aA, aB, aC);
+        if (fA >= 0) lrow[fA] = aubio_log10_clamped(aA, S.logf);
+        if (fB >= 0) lrow[fB] = aubio_log10_clamped(aB, S.logf);
+        if (fC >= 0) lrow[fC] = aubio_log10_clamped(aC, S.logf);
       }
     }
     wave_sync();
@@ -335,11 +363,11 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
     // 10*log10|c| (fp_handler.c:651), "%f" micro-units / NULL (db_ctx_handler.c:479-481).
     if ((ablate & 16) && lane < 2 * kWaveFrames) {
       const int row = lane >> 1, cf = lane & 1;
-      const int64_t f = f0 + row;
+      const int64_t f = cur_f0 + row;
       if (f < nf) micro[2 * (foff[cur_c] + f) + cf] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cf]);
     } else if (lane < 2 * kWaveFrames) {
       const int row = lane >> 1, cf = lane & 1;
-      const int64_t f = f0 + row;
+      const int64_t f = cur_f0 + row;
       if (f < nf) {
         const float* lrow = M.logs + row * kLogStride;
         float acc = 0.f;
@@ -358,7 +386,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(const Ds
 }
 
 hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_soff,
-                              const int64_t* d_foff, const int32_t* d_toff, int32_t nclips, int32_t ntiles,
+                              const int64_t* d_foff, const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles,
                               int32_t* d_micro, double* d_db, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
   static int grid_cap = 0;
@@ -377,7 +405,7 @@ hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, c
     ablate = a ? atoi(a) : 0;
   }
   hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(256), 0, s, d_tables, d_pcm, d_soff, d_foff, d_toff,
-                     nclips, ntiles, d_micro, d_db, ablate);
+                     d_tclip, ntiles, d_micro, d_db, ablate);
   return hipGetLastError();
 }
 

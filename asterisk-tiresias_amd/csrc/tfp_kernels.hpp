@@ -34,8 +34,9 @@ struct SynthSpecDev {
 
 // Fingerprint clips described by sample offsets soff[nclips+1], frame offsets foff[nclips+1]
 // and 16-frame tile offsets toff[nclips+1]; ntiles = toff[nclips].
+// tclip[tile] = clip of each 16-frame tile.
 hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_soff,
-                              const int64_t* d_foff, const int32_t* d_toff, int32_t nclips, int32_t ntiles,
+                              const int64_t* d_foff, const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles,
                               int32_t* d_micro, double* d_db, hipStream_t s);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);

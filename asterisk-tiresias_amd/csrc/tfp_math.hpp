@@ -64,8 +64,9 @@ inline const LogfEntry* logf_table() {
   return T;
 }
 
-// Valid for positive normal finite x (tfp_log10f only passes [0.5, 2)).
-TFP_HD float logf_glibc(float x) {
+// Valid for positive normal finite x (tfp_log10f only passes [0.5, 2)). T: the 16-entry table
+// (device code passes a copy staged in LDS).
+TFP_HD float logf_glibc(float x, const LogfEntry* T = logf_table()) {
   const double Ln2 = 0x1.62e42fefa39efp-1;
   const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
   const uint32_t ix = f2u(x);
@@ -73,7 +74,7 @@ TFP_HD float logf_glibc(float x) {
   const int i = (int)((tmp >> 19) & 15u);
   const int k = (int32_t)tmp >> 23;
   const uint32_t iz = ix - (tmp & 0xff800000u);
-  const LogfEntry e = logf_table()[i];
+  const LogfEntry e = T[i];
   const double z = (double)u2f(iz);
   const double r = z * e.invc - 1.0;
   const double y0 = e.logc + (double)k * Ln2;
@@ -85,7 +86,7 @@ TFP_HD float logf_glibc(float x) {
 }
 
 // glibc 2.35 log10f = fdlibm e_log10f.c float wrapper (all float arithmetic).
-TFP_HD float log10f_glibc(float x) {
+TFP_HD float log10f_glibc(float x, const LogfEntry* T = logf_table()) {
   const float two25 = 3.3554432000e+07f, ivln10 = 4.3429449201e-01f;
   const float log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
   int32_t hx = (int32_t)f2u(x);
@@ -103,17 +104,17 @@ TFP_HD float log10f_glibc(float x) {
   hx = (hx & 0x007fffff) | ((0x7f - i) << 23);
   const float y = (float)(k + i);
   x = u2f((uint32_t)hx);
-  const float z = y * log10_2lo + ivln10 * logf_glibc(x);
+  const float z = y * log10_2lo + ivln10 * logf_glibc(x, T);
   return z + y * log10_2hi;
 }
 
 // aubio fvec_log10: LOG10(MAX(VERY_SMALL_NUMBER, x)), VERY_SMALL_NUMBER = 2.e-42 (a double
 // literal, so the comparison is done in double and the clamp value is (float)2e-42).
-TFP_HD float aubio_log10_clamped(float x) {
+TFP_HD float aubio_log10_clamped(float x, const LogfEntry* T = logf_table()) {
   const double v = 2.e-42;
   const double xd = (double)x;
   const float a = (float)((v > xd) ? v : xd);
-  return log10f_glibc(a);
+  return log10f_glibc(a, T);
 }
 
 // ---------------------------------------------------------------------------------------

@@ -114,6 +114,43 @@ bool build_tables(int sample_rate, DspTables* t) {
     for (int b = first; b <= last; b++) t->mel_w[off++] = mel[j][b];
   }
   t->mel_total = off;
+
+  // filterbank slot schedule
+  int order[kFilters];
+  for (int j = 0; j < kFilters; j++) order[j] = j;
+  for (int a = 0; a < kFilters; a++)  // stable selection sort by length, longest first
+    for (int b = a + 1; b < kFilters; b++)
+      if (t->mel_len[order[b]] > t->mel_len[order[a]]) { const int x = order[a]; order[a] = order[b]; order[b] = x; }
+  int woff = 0;
+  for (int sl = 0; sl < 3; sl++) {
+    int len = 0;
+    for (int L = 0; L < 16; L++) {
+      const int idx = sl * 16 + L;
+      const int j = idx < kFilters ? order[idx] : -1;
+      t->ms_filter[sl][L] = j;
+      t->ms_start[sl][L] = j >= 0 ? t->mel_start[j] : 0;
+      if (j >= 0 && t->mel_len[j] > len) len = t->mel_len[j];
+    }
+    t->ms_len[sl] = len;
+    t->ms_woff[sl] = woff;
+    for (int q = 0; q < len; q++)
+      for (int L = 0; L < 16; L++) {
+        const int j = t->ms_filter[sl][L];
+        t->ms_w[woff + q * 16 + L] = (j >= 0 && q < t->mel_len[j]) ? t->mel_w[t->mel_off[j] + q] : 0.f;
+      }
+    woff += len * 16;
+  }
+  t->ms_total = woff;
+  t->ms_maxbin = kBins;
+  for (int sl = 0; sl < 3; sl++)
+    for (int L = 0; L < 16; L++)
+      if (t->ms_start[sl][L] + t->ms_len[sl] > t->ms_maxbin) t->ms_maxbin = t->ms_start[sl][L] + t->ms_len[sl];
+  if (t->ms_maxbin > 500) return false;  // the kernel's per-frame |X| row holds 516 floats
+  for (int k1 = 0; k1 < 16; k1++)
+    for (int L = 0; L < 16; L++) {
+      t->lane_tw_re[k1][L] = t->tw256_re[(L * k1) & 255];
+      t->lane_tw_im[k1][L] = t->tw256_im[(L * k1) & 255];
+    }
   return true;
 }
 
