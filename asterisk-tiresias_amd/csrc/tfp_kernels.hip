@@ -74,10 +74,10 @@ __device__ __forceinline__ void dft16(const float2* __restrict__ w16, const floa
 constexpr int kWaveFrames = 16;     // frames per wave tile (== kFramesPerBlock: tile offsets)
 constexpr int kFrameStride = 258;   // float2 per frame scratch: 16x16 XOR-swizzled square + pad
 constexpr int kLogStride = 41;      // floats per frame row in the log buffer (bank-conflict free)
-constexpr int kMsLds = 864;         // filterbank slot-schedule weights kept in LDS (8 kHz: 848)
+constexpr int kMsLds = 896;         // filterbank slot-schedule weights kept in LDS (8 kHz: 16 x 56)
 
 struct LdsTables {
-  float window[kWin];
+  float window[kWin];              // hanningz * 2^-15 (window_s)
   float2 lane_tw[15][16];          // lane_tw[k1-1][L] = w256^(L*k1), k1 = 1..15
   float2 w16[10];                  // W16^e = tw256[16 e] (dft16's internal twiddles)
   float2 tw512[kBins];             // w512^k for the real split
@@ -85,7 +85,7 @@ struct LdsTables {
   int32_t ms_len[3], ms_woff[3];
   int32_t ms_filter[3][16], ms_start[3][16];
   LogfEntry logf[16];
-  float ms_w[kMsLds];
+  alignas(16) float ms_w[kMsLds];
 };
 
 constexpr int kPassSamples = 5 * kHop;           // one pass = 4 frames = hops f-1 .. f+3
@@ -175,30 +175,55 @@ __device__ __forceinline__ float cr_sqrtf(float x) {
 template <class WPtr>
 __device__ __forceinline__ void mel3(const float* __restrict__ N, WPtr wA, WPtr wB, WPtr wC, int stA, int stB,
                                      int stC, int lenA, int lenB, int lenC, float& aA, float& aB, float& aC) {
+  // lengths are multiples of 4; weights of a lane are contiguous: one 16-byte read per 4 bins
   int q = 0;
-#pragma unroll 4
-  for (; q < lenC; q++) {
-    aA = aA + N[stA + q] * wA[16 * q];
-    aB = aB + N[stB + q] * wB[16 * q];
-    aC = aC + N[stC + q] * wC[16 * q];
+  for (; q < lenC; q += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(wA + q);
+    const float4 b = *reinterpret_cast<const float4*>(wB + q);
+    const float4 c = *reinterpret_cast<const float4*>(wC + q);
+    aA = aA + N[stA + q] * a.x; aB = aB + N[stB + q] * b.x; aC = aC + N[stC + q] * c.x;
+    aA = aA + N[stA + q + 1] * a.y; aB = aB + N[stB + q + 1] * b.y; aC = aC + N[stC + q + 1] * c.y;
+    aA = aA + N[stA + q + 2] * a.z; aB = aB + N[stB + q + 2] * b.z; aC = aC + N[stC + q + 2] * c.z;
+    aA = aA + N[stA + q + 3] * a.w; aB = aB + N[stB + q + 3] * b.w; aC = aC + N[stC + q + 3] * c.w;
   }
-#pragma unroll 4
-  for (; q < lenB; q++) {
-    aA = aA + N[stA + q] * wA[16 * q];
-    aB = aB + N[stB + q] * wB[16 * q];
+  for (; q < lenB; q += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(wA + q);
+    const float4 b = *reinterpret_cast<const float4*>(wB + q);
+    aA = aA + N[stA + q] * a.x; aB = aB + N[stB + q] * b.x;
+    aA = aA + N[stA + q + 1] * a.y; aB = aB + N[stB + q + 1] * b.y;
+    aA = aA + N[stA + q + 2] * a.z; aB = aB + N[stB + q + 2] * b.z;
+    aA = aA + N[stA + q + 3] * a.w; aB = aB + N[stB + q + 3] * b.w;
   }
-#pragma unroll 4
-  for (; q < lenA; q++) aA = aA + N[stA + q] * wA[16 * q];
+  for (; q < lenA; q += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(wA + q);
+    aA = aA + N[stA + q] * a.x;
+    aA = aA + N[stA + q + 1] * a.y;
+    aA = aA + N[stA + q + 2] * a.z;
+    aA = aA + N[stA + q + 3] * a.w;
+  }
+}
+
+// v_sqrt_f32 (<= 1 ulp) + exact fma-residual correction: the correctly rounded sqrtf for
+// x in [2^-100, 2^100) (cr_sqrtf without the range test).
+__device__ __forceinline__ float sqrtf_fast_cr(float x) {
+  float y = __builtin_amdgcn_sqrtf(x);
+  const float ym = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) - 1u);
+  const float yp = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, y) + 1u);
+  const float rm = __builtin_fmaf(-ym, y, x);
+  const float rp = __builtin_fmaf(-yp, y, x);
+  y = rm <= 0.f ? ym : y;
+  y = rp > 0.f ? yp : y;
+  return y;
 }
 
 __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ soff,
     const int64_t* __restrict__ foff, const int32_t* __restrict__ toff, const int32_t* __restrict__ tclip,
     int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
-  __shared__ LdsTables S;
+  __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[4];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += 256) S.window[i] = T->window[i];
+  for (int i = tid; i < kWin; i += 256) S.window[i] = T->window_s[i];
   for (int i = tid; i < 15 * 16; i += 256) {
     const int k1 = 1 + i / 16, L = i % 16;
     S.lane_tw[k1 - 1][L] = make_float2(T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]);
@@ -272,7 +297,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
       // ~90 of them into registers for the whole kernel (occupancy).
       int oz = 0;
       asm volatile("" : "+v"(oz));
-      const float* __restrict__ win = S.window + oz;
+      const float* __restrict__ win = S.window;  // may live in registers (32 per lane)
       float2 z[16], Y[16];
       if (ablate & 1) {
 #pragma unroll
@@ -283,8 +308,8 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
           const int j = (32 * n1 + 2 * L + 256) & 511;
           const int hsel = n1 < 8 ? 1 : 0;
           const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
-          z[n1].x = pcm_f((int16_t)(v & 0xffff)) * win[j];
-          z[n1].y = pcm_f((int16_t)(v >> 16)) * win[j + 1];
+          z[n1].x = (float)(int16_t)(v & 0xffff) * win[j];  // == (s / 32768) * hanningz[j], exactly
+          z[n1].y = (float)(int16_t)(v >> 16) * win[j + 1];
         }
       }
       if (ablate & 2) {
@@ -313,26 +338,51 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
         for (int k2 = 0; k2 < 16; k2++) N[L + 16 * k2] = Y[k2].x + Y[k2].y;
         if (L == 0) N[256] = Y[0].x;
       } else {
+        // branch-free: generic split + corrected v_sqrt for every k; lanes whose |X|^2 falls
+        // outside [2^-100, 2^100) redo that bin with the full IEEE sqrt below (wave-uniform
+        // test, practically never taken); lane 0 then writes the two real bins 0 and 256.
+        bool rare = false;
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) {
           const int k = L + 16 * k2;
           float2 P;
           P.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
           P.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
-          if (L == 0) P = Y[(16 - k2) & 15];
-          const float a = Y[k2].x, bq = Y[k2].y, cc = P.x, d = P.y;
-          if (k == 0) {
-            N[0] = fabsf(a + bq);
-            N[256] = fabsf(a - bq);
-          } else {
-            const float Er = a + cc, Ei = bq - d, Or = a - cc, Oi = bq + d;
-            const float2 w = S.tw512[k + oz];
+          const float2 own = Y[(16 - k2) & 15];
+          P.x = L == 0 ? own.x : P.x;
+          P.y = L == 0 ? own.y : P.y;
+          const float a = Y[k2].x, bq = Y[k2].y;
+          const float Er = a + P.x, Ei = bq - P.y, Or = a - P.x, Oi = bq + P.y;
+          const float2 w = S.tw512[k + oz];
+          const float tr = w.x * Oi + w.y * Or;
+          const float ti = w.x * Or - w.y * Oi;
+          const float Xr = 0.5f * (Er + tr);
+          const float Xi = 0.5f * (Ei - ti);
+          const float x = Xr * Xr + Xi * Xi;
+          rare |= !(x >= 0x1p-100f && x < 0x1p100f);
+          N[k] = sqrtf_fast_cr(x);
+        }
+        if (__builtin_expect(__any(rare), 0)) {
+          for (int k2 = 0; k2 < 16; k2++) {
+            const int k = L + 16 * k2;
+            float2 Q;
+            Q.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
+            Q.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
+            if (L == 0) Q = Y[(16 - k2) & 15];
+            const float a = Y[k2].x, bq = Y[k2].y;
+            const float Er = a + Q.x, Ei = bq - Q.y, Or = a - Q.x, Oi = bq + Q.y;
+            const float2 w = S.tw512[k];
             const float tr = w.x * Oi + w.y * Or;
             const float ti = w.x * Or - w.y * Oi;
             const float Xr = 0.5f * (Er + tr);
             const float Xi = 0.5f * (Ei - ti);
-            N[k] = cr_sqrtf(Xr * Xr + Xi * Xi);
+            const float x = Xr * Xr + Xi * Xi;
+            if (!(x >= 0x1p-100f && x < 0x1p100f)) N[k] = __builtin_sqrtf(x);
           }
+        }
+        if (L == 0) {
+          N[0] = fabsf(Y[0].x + Y[0].y);
+          N[256] = fabsf(Y[0].x - Y[0].y);
         }
       }
       for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;  // bins past 256 read by padded filters
@@ -347,15 +397,18 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
       } else {
         const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
         float aA = 0.f, aB = 0.f, aC = 0.f;
+        const int oA = S.ms_woff[0] + L * lenA, oB = S.ms_woff[1] + L * lenB, oC = S.ms_woff[2] + L * lenC;
         if (ms_in_lds)
-          mel3(N, S.ms_w + S.ms_woff[0] + L, S.ms_w + S.ms_woff[1] + L, S.ms_w + S.ms_woff[2] + L, stA, stB, stC,
-               lenA, lenB, lenC, aA, aB, aC);
+          mel3(N, S.ms_w + oA, S.ms_w + oB, S.ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);
         else
-          mel3(N, T->ms_w + S.ms_woff[0] + L, T->ms_w + S.ms_woff[1] + L, T->ms_w + S.ms_woff[2] + L, stA, stB,
-               stC, lenA, lenB, lenC, aA, aB, aC);
-        if (fA >= 0) lrow[fA] = aubio_log10_clamped(aA, S.logf);
-        if (fB >= 0) lrow[fB] = aubio_log10_clamped(aB, S.logf);
-        if (fC >= 0) lrow[fC] = aubio_log10_clamped(aC, S.logf);
+          mel3(N, T->ms_w + oA, T->ms_w + oB, T->ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);
+        // three independent log chains, computed unconditionally so they interleave (ILP 3)
+        const float lA = aubio_log10_clamped(aA, S.logf);
+        const float lB = aubio_log10_clamped(aB, S.logf);
+        const float lC = aubio_log10_clamped(aC, S.logf);
+        if (fA >= 0) lrow[fA] = lA;
+        if (fB >= 0) lrow[fB] = lB;
+        if (fC >= 0) lrow[fC] = lC;
       }
     }
     wave_sync();

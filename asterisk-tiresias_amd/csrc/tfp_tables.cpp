@@ -131,12 +131,13 @@ bool build_tables(int sample_rate, DspTables* t) {
       t->ms_start[sl][L] = j >= 0 ? t->mel_start[j] : 0;
       if (j >= 0 && t->mel_len[j] > len) len = t->mel_len[j];
     }
+    len = (len + 3) & ~3;
     t->ms_len[sl] = len;
     t->ms_woff[sl] = woff;
-    for (int q = 0; q < len; q++)
-      for (int L = 0; L < 16; L++) {
+    for (int L = 0; L < 16; L++)
+      for (int q = 0; q < len; q++) {
         const int j = t->ms_filter[sl][L];
-        t->ms_w[woff + q * 16 + L] = (j >= 0 && q < t->mel_len[j]) ? t->mel_w[t->mel_off[j] + q] : 0.f;
+        t->ms_w[woff + L * len + q] = (j >= 0 && q < t->mel_len[j]) ? t->mel_w[t->mel_off[j] + q] : 0.f;
       }
     woff += len * 16;
   }
@@ -146,6 +147,7 @@ bool build_tables(int sample_rate, DspTables* t) {
     for (int L = 0; L < 16; L++)
       if (t->ms_start[sl][L] + t->ms_len[sl] > t->ms_maxbin) t->ms_maxbin = t->ms_start[sl][L] + t->ms_len[sl];
   if (t->ms_maxbin > 500) return false;  // the kernel's per-frame |X| row holds 516 floats
+  for (int i = 0; i < kWin; i++) t->window_s[i] = t->window[i] * 0x1p-15f;
   for (int k1 = 0; k1 < 16; k1++)
     for (int L = 0; L < 16; L++) {
       t->lane_tw_re[k1][L] = t->tw256_re[(L * k1) & 255];

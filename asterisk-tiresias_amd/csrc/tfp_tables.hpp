@@ -29,15 +29,19 @@ struct DspTables {
   float mel_w[kFilters * kBins];
   // Kernel schedule of the filterbank: filters sorted by length are dealt to 3 slots x 16
   // lanes (slot 0 = the 16 longest); a lane runs its 3 filters' sums interleaved. Weights are
-  // laid out [slot][q][lane], zero-padded to the slot's longest filter (padding adds exact +0
-  // after a filter's last bin, so every sum is still aubio's sequential ascending-bin sum).
-  int32_t ms_len[3];
+  // laid out [slot][lane][q] (q contiguous, read 4 at a time), zero-padded to the slot's longest
+  // filter rounded up to 4 (padding adds exact +0 after a filter's last bin, so every sum is
+  // still aubio's sequential ascending-bin sum).
+  int32_t ms_len[3];         // padded slot length (multiple of 4)
   int32_t ms_filter[3][16];  // filter id or -1
   int32_t ms_start[3][16];   // first bin
   int32_t ms_woff[3];        // offset of slot s in ms_w
   int32_t ms_total;          // floats used in ms_w
   int32_t ms_maxbin;         // 1 + the highest bin a padded slot reads (bins > 256 read zeros)
-  float ms_w[3 * kBins * 16];
+  alignas(16) float ms_w[3 * kBins * 16];
+  // hanningz window pre-scaled by 2^-15 (exact): x = (float)sample * window_s[j] equals aubio's
+  // ((float)sample / 32768) * window[j] bit for bit.
+  float window_s[kWin];
   // Inter-stage FFT twiddles per lane: lane_tw[k1][L] = w256^(L*k1) (re, im), conflict-free reads.
   float lane_tw_re[16][16], lane_tw_im[16][16];
 };
