@@ -47,6 +47,7 @@ struct Clip {
   std::string uuid;
   bool alive = true;
   int64_t nrows = 0;
+  int64_t off = 0;  // first staging row (a clip's rows are contiguous, in frame order)
 };
 
 }  // namespace
@@ -168,7 +169,8 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
-  HIPCHK(e, launch_fingerprint(T, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->foff.as<int64_t>(),
+  HIPCHK(e, launch_fingerprint(T, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->soff.as<int64_t>() + 1,
+                               e->foff.as<int64_t>(),
                                e->toff.as<int32_t>(), e->tclip.as<int32_t>(), toff[nclips], e->micro.as<int32_t>(),
                                e->db.as<double>(), e->stream));
   *nframes_out = nf;
@@ -220,12 +222,13 @@ int stage_reserve(tfp_engine* e, int64_t extra) {
   return TFP_OK;
 }
 
-int new_clip(tfp_engine* e, const char* uuid, int64_t nrows, int32_t* id) {
+int new_clip(tfp_engine* e, const char* uuid, int64_t nrows, int64_t off, int32_t* id) {
   if (!uuid || !*uuid || strlen(uuid) >= 64) return fail(e, TFP_E_ARG, "bad uuid");
   if (e->by_uuid.count(uuid)) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuid);
   Clip c;
   c.uuid = uuid;
   c.nrows = nrows;
+  c.off = off;
   *id = (int32_t)e->clips.size();
   e->clips.push_back(c);
   e->by_uuid[uuid] = *id;
@@ -527,7 +530,8 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   int rc = ensure_tables(e, p->sample_rate, &T);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
+  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+                               p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, d_micro, d_db, s));
   return TFP_OK;
 }
@@ -538,9 +542,11 @@ int tfp_index_add(tfp_engine* e, const char* uuid, const int32_t* m1, const int3
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
   int32_t id;
-  int rc = new_clip(e, uuid, nframes, &id);
+  if (!uuid || !*uuid || strlen(uuid) >= 64) return fail(e, TFP_E_ARG, "bad uuid");
+  if (e->by_uuid.count(uuid)) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuid);
+  int rc = stage_reserve(e, nframes);
   if (rc) return rc;
-  if ((rc = stage_reserve(e, nframes))) return rc;
+  if ((rc = new_clip(e, uuid, nframes, e->n_staged, &id))) return rc;
   if (nframes) {
     std::vector<int32_t> cl(nframes, id);
     const int64_t o = e->n_staged;
@@ -586,7 +592,9 @@ int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids
   const int32_t clip0 = (int32_t)e->clips.size();
   for (int32_t c = 0; c < nclips; c++) {
     int32_t id;
-    if ((rc = new_clip(e, uuids[c], frame_offsets[c + 1] - frame_offsets[c], &id))) return rc;
+    if ((rc = new_clip(e, uuids[c], frame_offsets[c + 1] - frame_offsets[c],
+                       e->n_staged + frame_offsets[c] - frame_offsets[0], &id)))
+      return rc;
   }
   if (nf) {
     std::vector<int64_t> fo(frame_offsets, frame_offsets + nclips + 1);
@@ -601,6 +609,63 @@ int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(s));
     e->n_staged += nf;
+  }
+  return TFP_OK;
+}
+
+int tfp_index_add_batch(tfp_engine* e, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
+                        const int32_t* m1, const int32_t* m2) {
+  if (!e || nclips < 0 || !uuids || !frame_offsets) return TFP_E_ARG;
+  const int64_t nf = frame_offsets[nclips] - frame_offsets[0];
+  if (nf < 0 || (nf && (!m1 || !m2))) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  std::unordered_map<std::string, int> seen;
+  for (int32_t c = 0; c < nclips; c++) {
+    if (!uuids[c] || !*uuids[c] || strlen(uuids[c]) >= 64) return fail(e, TFP_E_ARG, "bad uuid %d", c);
+    if (frame_offsets[c + 1] < frame_offsets[c]) return fail(e, TFP_E_ARG, "frame_offsets not monotone at %d", c);
+    if (e->by_uuid.count(uuids[c]) || !seen.emplace(uuids[c], c).second)
+      return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
+  }
+  int rc = stage_reserve(e, nf);
+  if (rc) return rc;
+  std::vector<int32_t> cl(nf);
+  const int32_t clip0 = (int32_t)e->clips.size();
+  for (int32_t c = 0; c < nclips; c++) {
+    int32_t id;
+    const int64_t b = frame_offsets[c] - frame_offsets[0], n = frame_offsets[c + 1] - frame_offsets[c];
+    if ((rc = new_clip(e, uuids[c], n, e->n_staged + b, &id))) return rc;
+    std::fill(cl.begin() + b, cl.begin() + b + n, clip0 + c);
+  }
+  if (nf) {
+    const int64_t o = e->n_staged;
+    const int32_t* s1 = m1 + frame_offsets[0];
+    const int32_t* s2 = m2 + frame_offsets[0];
+    HIPCHK(e, hipMemcpyAsync(e->st_m1.as<int32_t>() + o, s1, sizeof(int32_t) * nf, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_m2.as<int32_t>() + o, s2, sizeof(int32_t) * nf, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->st_clip.as<int32_t>() + o, cl.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->n_staged += nf;
+  }
+  return TFP_OK;
+}
+
+int tfp_index_rows(tfp_engine* e, const char* uuid, int32_t* m1, int32_t* m2, int64_t cap, int64_t* nframes) {
+  if (!e || !uuid || cap < 0 || (cap && (!m1 || !m2))) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  auto it = e->by_uuid.find(uuid);
+  if (it == e->by_uuid.end()) return fail(e, TFP_E_NOENT, "uuid %s not indexed", uuid);
+  const Clip& c = e->clips[it->second];
+  if (nframes) *nframes = c.nrows;
+  if (cap < c.nrows) return fail(e, TFP_E_CAPACITY, "need %lld rows", (long long)c.nrows);
+  if (c.nrows) {
+    HIPCHK(e, hipSetDevice(e->device));
+    HIPCHK(e, hipMemcpyAsync(m1, e->st_m1.as<int32_t>() + c.off, sizeof(int32_t) * c.nrows, hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipMemcpyAsync(m2, e->st_m2.as<int32_t>() + c.off, sizeof(int32_t) * c.nrows, hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
   }
   return TFP_OK;
 }
@@ -721,11 +786,127 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
+  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+                               p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
   std::vector<unsigned long long> keys;
   return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
                      reinterpret_cast<unsigned long long*>(d_keys), s);
+}
+
+// ---- streams ------------------------------------------------------------------------------
+
+struct tfp_stream {
+  tfp_engine* eng = nullptr;
+  int32_t nch = 0, sr = 0;
+  int64_t W = 0;                 // window samples
+  int64_t wpos = 0;              // ring position of the oldest sample of every window
+  std::vector<int64_t> filled;   // samples of history per channel (saturates at W)
+  DevBuf ring, tick, sbeg, send, foff, toff, tclip;
+};
+
+// ring[c][2W]: every sample is written at p and p + W, so the last W samples of a channel are
+// always the contiguous run ring[c][wpos .. wpos + W).
+__global__ void stream_scatter_kernel(const int16_t* __restrict__ tick, int32_t T, int64_t W, int64_t wpos,
+                                      int32_t nch, int16_t* __restrict__ ring) {
+  const int64_t n = (int64_t)nch * T;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t c = i / T, t = i % T;
+    int64_t p = wpos + t;
+    if (p >= W) p -= W;
+    const int16_t v = tick[i];
+    ring[c * 2 * W + p] = v;
+    ring[c * 2 * W + p + W] = v;
+  }
+}
+
+int tfp_stream_create(tfp_engine* e, int32_t nch, int32_t sr, int64_t W, tfp_stream** out) {
+  if (!e || nch <= 0 || W <= 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  const DspTables* T;
+  int rc = ensure_tables(e, sr, &T);
+  if (rc) return rc;
+  tfp_stream* st = new tfp_stream();
+  st->eng = e;
+  st->nch = nch;
+  st->sr = sr;
+  st->W = W;
+  st->filled.assign(nch, 0);
+  if (st->ring.reserve(sizeof(int16_t) * 2 * W * nch) != hipSuccess) {
+    delete st;
+    return fail(e, TFP_E_NOMEM, "stream ring of %lld bytes", (long long)(4 * W * nch));
+  }
+  (void)hipMemsetAsync(st->ring.p, 0, sizeof(int16_t) * 2 * W * nch, e->stream);
+  *out = st;
+  return TFP_OK;
+}
+
+void tfp_stream_destroy(tfp_stream* st) { delete st; }
+
+int tfp_stream_reset(tfp_stream* st, int32_t ch) {
+  if (!st || ch >= st->nch) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(st->eng->mu);
+  if (ch < 0) std::fill(st->filled.begin(), st->filled.end(), 0);
+  else st->filled[ch] = 0;
+  return TFP_OK;
+}
+
+int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, tfp_result* out) {
+  if (!st || !pcm || T <= 0 || T > st->W || (P && !out)) return TFP_E_ARG;
+  tfp_engine* e = st->eng;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  int rc = upload(e, st->tick, pcm, sizeof(int16_t) * (size_t)st->nch * T);
+  if (rc) return rc;
+  hipLaunchKernelGGL(stream_scatter_kernel, dim3(1024), dim3(256), 0, e->stream, st->tick.as<int16_t>(), T, st->W,
+                     st->wpos, st->nch, st->ring.as<int16_t>());
+  HIPCHK(e, hipGetLastError());
+  st->wpos = (st->wpos + T) % st->W;
+  for (auto& f : st->filled) f = std::min<int64_t>(st->W, f + T);
+  if (!P) return TFP_OK;
+  for (int32_t c = 0; c < st->nch; c++) {
+    memset(&out[c], 0, sizeof out[c]);
+    out[c].clip_id = -1;
+  }
+  if (!valid_params(P)) return TFP_OK;  // fp_handler.c:247-250: NULL
+  // full windows only
+  std::vector<int32_t> act;
+  for (int32_t c = 0; c < st->nch; c++)
+    if (st->filled[c] >= st->W) act.push_back(c);
+  const int32_t na = (int32_t)act.size();
+  if (!na) return TFP_OK;
+  const DspTables* Tb;
+  if ((rc = ensure_tables(e, st->sr, &Tb))) return rc;
+  const int64_t F = tfp_frame_count(st->W);
+  const int32_t tiles = (int32_t)((F + kFramesPerBlock - 1) / kFramesPerBlock);
+  std::vector<int64_t> sb(na), se(na), fo(na + 1);
+  std::vector<int32_t> to(na + 1), tc((size_t)na * tiles);
+  for (int32_t i = 0; i < na; i++) {
+    sb[i] = (int64_t)act[i] * 2 * st->W + st->wpos;
+    se[i] = sb[i] + st->W;
+    fo[i] = (int64_t)i * F;
+    to[i] = i * tiles;
+    for (int32_t t = 0; t < tiles; t++) tc[(size_t)i * tiles + t] = i;
+  }
+  fo[na] = (int64_t)na * F;
+  to[na] = na * tiles;
+  if ((rc = upload(e, st->sbeg, sb.data(), sizeof(int64_t) * na)) || (rc = upload(e, st->send, se.data(), sizeof(int64_t) * na)) ||
+      (rc = upload(e, st->foff, fo.data(), sizeof(int64_t) * (na + 1))) ||
+      (rc = upload(e, st->toff, to.data(), sizeof(int32_t) * (na + 1))) ||
+      (rc = upload(e, st->tclip, tc.data(), sizeof(int32_t) * tc.size())))
+    return rc;
+  HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
+  HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
+  HIPCHK(e, launch_fingerprint(Tb, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
+                               st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na],
+                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+  std::vector<unsigned long long> keys;
+  if ((rc = search_core(e, fo.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
+  std::vector<tfp_result> res(na);
+  fill_results(e, keys, fo.data(), na, res.data());
+  for (int32_t i = 0; i < na; i++) out[act[i]] = res[i];
+  return TFP_OK;
 }
 
 int tfp_synth_pcm(const tfp_synth_spec* specs, int32_t nclips, int64_t spc, int16_t* out) {

@@ -217,8 +217,9 @@ __device__ __forceinline__ float sqrtf_fast_cr(float x) {
 }
 
 __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
-    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ soff,
-    const int64_t* __restrict__ foff, const int32_t* __restrict__ toff, const int32_t* __restrict__ tclip,
+    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
+    const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
+    const int32_t* __restrict__ tclip,
     int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[4];
@@ -252,9 +253,9 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
 
   auto pass_src = [&](int c, int64_t f0, int sub) {
     PassSrc p;
-    const int64_t s0 = soff[c];
+    const int64_t s0 = sbeg[c];
     p.clip = pcm + s0;
-    p.ns = soff[c + 1] - s0;
+    p.ns = send[c] - s0;
     p.sbase = (f0 + 4 * sub - 1) * kHop;
     p.aligned = ((reinterpret_cast<uintptr_t>(p.clip) & 15) == 0);
     return p;
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
   int64_t f0 = b < ntiles ? (int64_t)(b - toff[c]) * kWaveFrames : 0;
   fetch_pass(pass_src(c, f0, 0), b < ntiles, lane, pf);
   for (; b < ntiles; b += nwaves) {
-    const int64_t nf = (soff[c + 1] - soff[c] + kHop - 1) / kHop;
+    const int64_t nf = (send[c] - sbeg[c] + kHop - 1) / kHop;
     const int cur_c = c;
     const int64_t cur_f0 = f0;
     const int bn = b + nwaves;
@@ -438,9 +439,9 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
   }
 }
 
-hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_soff,
-                              const int64_t* d_foff, const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles,
-                              int32_t* d_micro, double* d_db, hipStream_t s) {
+hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_sbeg,
+                              const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
+                              const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
   static int grid_cap = 0;
   if (!grid_cap) {
@@ -457,8 +458,8 @@ hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, c
     const char* a = getenv("TFP_ABLATE");
     ablate = a ? atoi(a) : 0;
   }
-  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(256), 0, s, d_tables, d_pcm, d_soff, d_foff, d_toff,
-                     d_tclip, ntiles, d_micro, d_db, ablate);
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(256), 0, s, d_tables, d_pcm, d_sbeg, d_send, d_foff,
+                     d_toff, d_tclip, ntiles, d_micro, d_db, ablate);
   return hipGetLastError();
 }
 

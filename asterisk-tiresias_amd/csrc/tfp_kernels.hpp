@@ -32,12 +32,12 @@ struct SynthSpecDev {
   int64_t offset;
 };
 
-// Fingerprint clips described by sample offsets soff[nclips+1], frame offsets foff[nclips+1]
-// and 16-frame tile offsets toff[nclips+1]; ntiles = toff[nclips].
-// tclip[tile] = clip of each 16-frame tile.
-hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_soff,
-                              const int64_t* d_foff, const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles,
-                              int32_t* d_micro, double* d_db, hipStream_t s);
+// Fingerprint clips: clip c = samples [sbeg[c], send[c]) of d_pcm (for concatenated clips pass
+// send = soff + 1); frames of clip c are written from foff[c]; toff[nclips+1] are 16-frame tile
+// offsets (ntiles = toff[nclips]) and tclip[tile] the clip of each tile.
+hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_sbeg,
+                              const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
+                              const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
 

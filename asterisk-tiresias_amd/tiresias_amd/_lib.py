@@ -60,6 +60,8 @@ _SIGS = {
     "tfp_fingerprint_device": (C.c_int, [P, P, P, P, P, P]),
     "tfp_index_add": (C.c_int, [P, C.c_char_p, P, P, C.c_int32, C.POINTER(C.c_int32)]),
     "tfp_index_add_device": (C.c_int, [P, C.c_int32, C.POINTER(C.c_char_p), P, P, P]),
+    "tfp_index_add_batch": (C.c_int, [P, C.c_int32, C.POINTER(C.c_char_p), P, P, P]),
+    "tfp_index_rows": (C.c_int, [P, C.c_char_p, P, P, C.c_int64, C.POINTER(C.c_int64)]),
     "tfp_index_remove": (C.c_int, [P, C.c_char_p]),
     "tfp_index_clear": (C.c_int, [P]),
     "tfp_index_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
@@ -70,6 +72,10 @@ _SIGS = {
     "tfp_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_device": (C.c_int, [P, P, P, C.POINTER(SearchParams), P, P]),
     "tfp_index_uuid_of_key": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int32]),
+    "tfp_stream_create": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]),
+    "tfp_stream_destroy": (None, [P]),
+    "tfp_stream_reset": (C.c_int, [P, C.c_int32]),
+    "tfp_stream_push": (C.c_int, [P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_synth_pcm": (C.c_int, [P, C.c_int32, C.c_int64, P]),
     "tfp_synth_pcm_device": (C.c_int, [P, P, C.c_int32, C.c_int64, P, P]),
     "tfp_synchronize": (C.c_int, [P, P]),

@@ -107,6 +107,25 @@ class Engine:
         self._chk(lib().tfp_index_add(self._h, uuid.encode(), m1.ctypes.data, m2.ctypes.data, len(m1), C.byref(cid)))
         return cid.value
 
+    def index_add_batch(self, uuids, frame_offsets, m1, m2):
+        frame_offsets = np.ascontiguousarray(frame_offsets, np.int64)
+        m1 = np.ascontiguousarray(m1, np.int32)
+        m2 = np.ascontiguousarray(m2, np.int32)
+        arr = (C.c_char_p * max(1, len(uuids)))(*[u.encode() for u in uuids])
+        self._chk(lib().tfp_index_add_batch(self._h, len(uuids), arr, frame_offsets.ctypes.data, m1.ctypes.data,
+                                            m2.ctypes.data))
+
+    def index_rows(self, uuid: str):
+        """Stored (m1, m2) micro-unit rows of one clip, frame order."""
+        n = C.c_int64()
+        rc = lib().tfp_index_rows(self._h, uuid.encode(), None, None, 0, C.byref(n))
+        if rc not in (0, -5):
+            self._chk(rc)
+        m1 = np.zeros(max(n.value, 1), np.int32)
+        m2 = np.zeros(max(n.value, 1), np.int32)
+        self._chk(lib().tfp_index_rows(self._h, uuid.encode(), m1.ctypes.data, m2.ctypes.data, n.value, C.byref(n)))
+        return m1[:n.value], m2[:n.value]
+
     def index_remove(self, uuid: str):
         self._chk(lib().tfp_index_remove(self._h, uuid.encode()))
 
@@ -184,6 +203,37 @@ class Engine:
 
     def synchronize(self, stream: int = 0):
         self._chk(lib().tfp_synchronize(self._h, C.c_void_p(stream or None)))
+
+
+class Stream:
+    """Live channels (tfp_stream): rolling window fingerprint + match per tick."""
+
+    def __init__(self, eng: Engine, nchannels: int, window_samples: int, sample_rate: int = 8000):
+        self._eng = eng
+        self._h = C.c_void_p()
+        eng._chk(lib().tfp_stream_create(eng.handle, int(nchannels), int(sample_rate), int(window_samples),
+                                         C.byref(self._h)))
+        self.nchannels = nchannels
+        self._res = (Result * nchannels)()
+
+    def reset(self, channel: int = -1):
+        self._eng._chk(lib().tfp_stream_reset(self._h, int(channel)))
+
+    def push(self, pcm: np.ndarray, p: SearchParams = None):
+        """pcm int16[nchannels, tick] -> list of per-channel results (None = NOTFOUND / not full)."""
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        assert pcm.shape[0] == self.nchannels
+        self._eng._chk(lib().tfp_stream_push(self._h, pcm.ctypes.data, pcm.shape[1],
+                                             C.byref(p) if p is not None else None, self._res if p is not None else None))
+        if p is None:
+            return None
+        return [None if not r.found else {"audio_uuid": r.uuid.decode(), "match_count": r.match_count,
+                                          "frame_count": r.frame_count} for r in self._res]
+
+    def __del__(self):
+        if self._h:
+            lib().tfp_stream_destroy(self._h)
+            self._h = C.c_void_p()
 
 
 class Plan:

@@ -11,8 +11,9 @@ reference's callers (application_handler.c, cli_handler.c, app_tiresias.c):
 
 The control plane (context_list / audio_list catalog, MD5 dedup, uuid v4) stays on SQLite,
 as the reference keeps it; the hot path — fingerprinting and matching — runs on the GPU via
-the C-ABI engine. The DB snapshot load/backup of fp_init/fp_term (fp_handler.c:68-108) is
-not part of the hot path and is not mirrored here.
+the C-ABI engine. fp_init/fp_term load and write the audio_recongition.db snapshot
+(fp_handler.c:68-108) when a backup path is given — catalog tables to SQLite, fingerprint
+rows straight into / out of the device index (dbio.py).
 """
 from __future__ import annotations
 
@@ -24,6 +25,7 @@ import wave
 
 import numpy as np
 
+from . import dbio
 from .engine import Engine, params
 
 DEF_SEARCH_TOLERANCE = 0.001  # fp_handler.c:41
@@ -53,30 +55,41 @@ def write_wav_mono16(filename: str, pcm: np.ndarray, sample_rate: int = 8000):
 class FpHandler:
     """One loaded module instance (g_db_ctx + the GPU engine)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, backup_path: str | None = None):
+        """backup_path: the snapshot file (the reference hard-codes dbio.DEF_BACKUP_DATABASE);
+        None keeps the state in memory only."""
         self.device = device
+        self.backup_path = backup_path
         self.db = None
         self.engine = None
 
-    # fp_handler.c:68 — init_database (the catalog tables) + engine
+    # fp_handler.c:68-90 — init_database (the catalog tables) + engine, then the snapshot
     def fp_init(self) -> bool:
         self.db = sqlite3.connect(":memory:", check_same_thread=False)
-        c = self.db.cursor()
-        c.execute("create table context_list(   name        varchar(255),   directory   varchar(1023),"
-                  "   primary key(name));")
-        c.execute("create table audio_list(   uuid           varchar(255),   name           varchar(255),"
-                  "   context        varchar(255),\thash           varchar(1023));")
+        dbio.create_catalog(self.db)
         self.engine = Engine(self.device)
+        if self.backup_path:
+            try:
+                dbio.load_backup(self.db, self.engine, self.backup_path)
+            except Exception:
+                return False  # "Could not load the database data."
         return True
 
+    # fp_handler.c:92-108 — backup, then tear down
     def fp_term(self) -> bool:
+        ok = True
+        if self.backup_path and self.db and self.engine:
+            try:
+                dbio.write_backup(self.db, self.engine, self.backup_path)
+            except Exception:
+                ok = False  # "Could not write database."
         if self.engine:
             self.engine.close()
         self.engine = None
         if self.db:
             self.db.close()
         self.db = None
-        return True
+        return ok
 
     # ---- contexts (fp_handler.c:912-1095) ----------------------------------------------
     def fp_create_context_list_info(self, name: str, directory: str, replace: bool) -> bool:

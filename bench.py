@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stream-channels", type=int, default=512)
+    ap.add_argument("--stream-ticks", type=int, default=200)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only to rehearse N ranks on one GPU")
     args = ap.parse_args()
 
@@ -192,6 +194,8 @@ def main():
     # ---------------------------------------------------------------- match (C3 / C4)
     if not args.no_match and args.db_clips > 0:
         out["match"] = run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T)
+        if world == 1 and args.stream_channels > 0:
+            out["stream"] = run_stream(args, eng, T)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -294,6 +298,41 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat)}
+
+
+def run_stream(args, eng, T):
+    """configs[4] (C5): live channels, 160-sample SLIN ticks, 3000 ms window (24000 samples =
+    94 frames), rolling fingerprint + match against the DB run_match enrolled. Latency = host
+    tick in -> every channel's result on the host (tfp_stream_push, application_handler.c:152-185)."""
+    from tiresias_amd import Stream
+    nch, W, tick, nt = args.stream_channels, 24000, 160, args.stream_ticks
+    n_db = 8000 * 30
+    rng = np.random.default_rng(SEED_Q + 1)
+    span = W + nt * tick
+    clips = [int(rng.integers(args.db_clips)) for _ in range(nch)]
+    offs = [256 * int(rng.integers(0, (n_db - span) // HOP)) for _ in range(nch)]
+    pcm = T.synth_pcm(SEED_DB, clips, span, offsets=offs)
+    pcm[3::4] = T.synth_pcm(SEED_Q + 7, range(len(pcm[3::4])), span)  # every 4th channel: unrelated audio
+    st = Stream(eng, nch, W)
+    p = T.params(1, 0.001)
+    for t in range(W // tick):  # fill the windows (ingest only)
+        st.push(pcm[:, t * tick:(t + 1) * tick])
+    lat, found = [], 0
+    base = W // tick
+    for t in range(nt):
+        s0 = (base + t) * tick
+        blk = np.ascontiguousarray(pcm[:, s0:s0 + tick])
+        t0 = time.perf_counter()
+        res = st.push(blk, p)
+        lat.append((time.perf_counter() - t0) * 1e3)
+        found = sum(r is not None for r in res)
+    lat = np.array(lat)
+    log(f"stream: {nch} ch, p50 {np.percentile(lat, 50):.2f} ms p99 {np.percentile(lat, 99):.2f} ms per tick")
+    return {"workload": f"configs[4]: {nch} live channels, {tick}-sample ticks, {W}-sample window ({W // HOP + (W % HOP > 0)} frames), "
+                        f"match vs {args.db_clips} clips every tick, 1 GPU",
+            "ticks_timed": len(lat), "tick_latency_p50_ms": float(np.percentile(lat, 50)),
+            "tick_latency_p99_ms": float(np.percentile(lat, 99)), "tick_budget_ms": 1e3 * tick / 8000,
+            "fingerprints_per_tick": nch * ((W + HOP - 1) // HOP), "channels_found_last_tick": found}
 
 
 if __name__ == "__main__":

@@ -116,6 +116,16 @@ int tfp_index_add(tfp_engine* eng, const char* uuid, const int32_t* m1, const in
  * in the layout tfp_fingerprint_device writes, frame_offsets[nclips+1] on the host. */
 int tfp_index_add_device(tfp_engine* eng, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
                          const int32_t* d_micro, void* stream);
+/* Append nclips clips from host rows (m1/m2 indexed by frame_offsets[0..nclips]); the bulk
+ * form of tfp_index_add used to load an audio_recongition.db snapshot (fp_init ->
+ * db_ctx_load_db_data, fp_handler.c:68-90, db_ctx_handler.c:750-772). All-or-nothing on
+ * argument errors (bad/duplicate uuid). */
+int tfp_index_add_batch(tfp_engine* eng, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
+                        const int32_t* m1, const int32_t* m2);
+/* Read back one clip's stored rows in frame order (for the fp_term backup,
+ * db_ctx_backup db_ctx_handler.c:673-717). *nframes always receives the row count;
+ * TFP_E_CAPACITY if cap is smaller. */
+int tfp_index_rows(tfp_engine* eng, const char* uuid, int32_t* m1, int32_t* m2, int64_t cap, int64_t* nframes);
 int tfp_index_remove(tfp_engine* eng, const char* uuid);
 int tfp_index_clear(tfp_engine* eng);
 int tfp_index_stats(tfp_engine* eng, int64_t* nrows, int32_t* nclips);
@@ -142,6 +152,24 @@ int tfp_search_device(tfp_engine* eng, const tfp_plan* plan, const int16_t* d_pc
                       const tfp_search_params* params, uint64_t* d_keys, void* stream);
 /* Map a tie-break key from tfp_search_device back to the uuid (this engine's clips only). */
 int tfp_index_uuid_of_key(tfp_engine* eng, int32_t key, char* uuid, int32_t len);
+
+/* ---- live channels: rolling fingerprint + match (configs[4]) --------------------------
+ * The dialplan app records `duration` ms of a channel to a WAV and searches it
+ * (application_handler.c:152-185, record_voice :248-312). A stream keeps the most recent
+ * window_samples of every channel on the GPU; after each tick (every channel's next
+ * tick_samples, SLIN 20 ms = 160 samples at 8 kHz) the result of a channel whose history
+ * holds a full window equals fp_search_fingerprint_info on a recording of exactly those
+ * samples. Channels with less history report found = 0, frame_count = 0. */
+typedef struct tfp_stream tfp_stream;
+int tfp_stream_create(tfp_engine* eng, int32_t nchannels, int32_t sample_rate, int64_t window_samples,
+                      tfp_stream** out);
+void tfp_stream_destroy(tfp_stream* st);
+/* A new call on `channel` (< 0: every channel): its history restarts empty. */
+int tfp_stream_reset(tfp_stream* st, int32_t channel);
+/* pcm[nchannels][tick_samples] (host); tick_samples <= window_samples. params NULL: only
+ * ingest. out[nchannels] receives each channel's result when params != NULL. */
+int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t tick_samples, const tfp_search_params* params,
+                    tfp_result* out);
 
 /* ---- deterministic synthetic PCM (benchmark / test data; identical host and device) -- */
 /* One spec per clip: samples s of clip = synth(seed, clip, offset + s). */
