@@ -20,38 +20,38 @@ namespace tfp {
 // ------------------------------------------------------------------------------------
 // Canonical FFT building blocks (spec: DESIGN.md §FFT; oracle: dft4/dft16/fft256).
 
-__device__ __forceinline__ float2 cmul(float2 a, float wr, float wi) {
-  float2 r;
-  r.x = a.x * wr - a.y * wi;
-  r.y = a.x * wi + a.y * wr;
-  return r;
+// Complex values as (re, im) register pairs: every operation below is a v_pk_*_f32 whose lanes
+// perform exactly the scalar IEEE operations of the canonical spec (x + (-y) == x - y, products
+// and sums commute), with swaps and negations folded into op_sel / neg modifiers.
+typedef float cf __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ cf swapneg_lo(cf a) { return cf{-a.y, a.x}; }  // (-im, re) = i a
+__device__ __forceinline__ cf swapneg_hi(cf a) { return cf{a.y, -a.x}; }  // (im, -re) = -i a
+
+// a * w: (a.x wr - a.y wi, a.x wi + a.y wr)
+__device__ __forceinline__ cf cmul(cf a, cf w) {
+  const cf p = a * cf{w.x, w.x};
+  const cf q = cf{a.y, a.x} * cf{-w.y, w.y};
+  return p + q;
 }
 
-__device__ __forceinline__ void dft4(float2 a0, float2 a1, float2 a2, float2 a3, float2& X0, float2& X1,
-                                     float2& X2, float2& X3) {
-  const float t0r = a0.x + a2.x, t0i = a0.y + a2.y;
-  const float t1r = a0.x - a2.x, t1i = a0.y - a2.y;
-  const float t2r = a1.x + a3.x, t2i = a1.y + a3.y;
-  const float t3r = a1.x - a3.x, t3i = a1.y - a3.y;
-  X0.x = t0r + t2r; X0.y = t0i + t2i;
-  X2.x = t0r - t2r; X2.y = t0i - t2i;
-  X1.x = t1r + t3i; X1.y = t1i - t3r;
-  X3.x = t1r - t3i; X3.y = t1i + t3r;
+__device__ __forceinline__ void dft4(cf a0, cf a1, cf a2, cf a3, cf& X0, cf& X1, cf& X2, cf& X3) {
+  const cf t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
+  X0 = t0 + t2;
+  X2 = t0 - t2;
+  X1 = t1 + swapneg_hi(t3);  // (t1r + t3i, t1i - t3r)
+  X3 = t1 + swapneg_lo(t3);  // (t1r - t3i, t1i + t3r)
 }
 
 // 16-point DFT in registers: n = 4 n1 + n2, k = k1 + 4 k2, W16^e = tw256[16 e].
-__device__ __forceinline__ void dft16(const float2* __restrict__ w16, const float2 (&in)[16], float2 (&out)[16]) {
-  float2 A[4][4];
+__device__ __forceinline__ void dft16(const cf* __restrict__ w16, const cf (&in)[16], cf (&out)[16]) {
+  cf A[4][4];
 #pragma unroll
   for (int n2 = 0; n2 < 4; n2++) dft4(in[n2], in[4 + n2], in[8 + n2], in[12 + n2], A[n2][0], A[n2][1], A[n2][2], A[n2][3]);
 #pragma unroll
   for (int n2 = 1; n2 < 4; n2++)
 #pragma unroll
-    for (int k1 = 1; k1 < 4; k1++) {
-      const int e = 16 * n2 * k1;
-      const float2 w = w16[e >> 4];
-      A[n2][k1] = cmul(A[n2][k1], w.x, w.y);
-    }
+    for (int k1 = 1; k1 < 4; k1++) A[n2][k1] = cmul(A[n2][k1], w16[n2 * k1]);
 #pragma unroll
   for (int k1 = 0; k1 < 4; k1++) dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
 }
@@ -72,15 +72,15 @@ __device__ __forceinline__ void dft16(const float2* __restrict__ w16, const floa
 #define TFP_FP_WAVES 2  // waves per SIMD the register budget is cut for (A/B: scripts/ab_waves.sh)
 #endif
 constexpr int kWaveFrames = 16;     // frames per wave tile (== kFramesPerBlock: tile offsets)
-constexpr int kFrameStride = 258;   // float2 per frame scratch: 16x16 XOR-swizzled square + pad
+constexpr int kFrameStride = 258;   // complex per frame scratch: 16x16 XOR-swizzled square + pad
 constexpr int kLogStride = 41;      // floats per frame row in the log buffer (bank-conflict free)
-constexpr int kMsLds = 896;         // filterbank slot-schedule weights kept in LDS (8 kHz: 16 x 56)
+constexpr int kMsLds = 960;         // filterbank slot-schedule weights kept in LDS (8 kHz: 16 x 60)
 
 struct LdsTables {
   float window[kWin];              // hanningz * 2^-15 (window_s)
-  float2 lane_tw[15][16];          // lane_tw[k1-1][L] = w256^(L*k1), k1 = 1..15
-  float2 w16[10];                  // W16^e = tw256[16 e] (dft16's internal twiddles)
-  float2 tw512[kBins];             // w512^k for the real split
+  cf lane_tw[15][16];              // lane_tw[k1-1][L] = w256^(L*k1), k1 = 1..15
+  cf w16[10];                      // W16^e = tw256[16 e] (dft16's internal twiddles)
+  cf tw512[kBins];                 // w512^k for the real split
   float dct[kCoefs][kFilters];
   int32_t ms_len[3], ms_woff[3];
   int32_t ms_filter[3][16], ms_start[3][16];
@@ -98,12 +98,12 @@ constexpr int kHopStride = kHop + 32;  // staged hop stride in samples: frames 0
 // write of the transpose square, and restaged only after the filterbank has read |X|.
 struct WaveLds {
   union {
-    float2 scratch[4][kFrameStride];
+    cf scratch[4][kFrameStride];
     alignas(16) int16_t pcm[5 * kHopStride];
   };
   float logs[kWaveFrames * kLogStride];
 };
-static_assert(sizeof(int16_t) * 5 * kHopStride <= sizeof(float2) * 4 * kFrameStride, "pcm alias fits");
+static_assert(sizeof(int16_t) * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride, "pcm alias fits");
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
 struct PassSrc {
@@ -175,32 +175,104 @@ __device__ __forceinline__ float cr_sqrtf(float x) {
 template <class WPtr>
 __device__ __forceinline__ void mel3(const float* __restrict__ N, WPtr wA, WPtr wB, WPtr wC, int stA, int stB,
                                      int stC, int lenA, int lenB, int lenC, float& aA, float& aB, float& aC) {
-  // lengths are multiples of 4; weights of a lane are contiguous: one 16-byte read per 4 bins
+  // lengths and starts are multiples of 4; per 4 bins one 16-byte weight read (the lane's
+  // 16-B slot of the 64-float row of bins q..q+3: w + 16 q) and one aligned 16-byte |X| read per slot
+#define TFP_MAC4(ACC, NV, WV) \
+  ACC = ACC + NV.x * WV.x; ACC = ACC + NV.y * WV.y; ACC = ACC + NV.z * WV.z; ACC = ACC + NV.w * WV.w
   int q = 0;
   for (; q < lenC; q += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(wA + q);
-    const float4 b = *reinterpret_cast<const float4*>(wB + q);
-    const float4 c = *reinterpret_cast<const float4*>(wC + q);
-    aA = aA + N[stA + q] * a.x; aB = aB + N[stB + q] * b.x; aC = aC + N[stC + q] * c.x;
-    aA = aA + N[stA + q + 1] * a.y; aB = aB + N[stB + q + 1] * b.y; aC = aC + N[stC + q + 1] * c.y;
-    aA = aA + N[stA + q + 2] * a.z; aB = aB + N[stB + q + 2] * b.z; aC = aC + N[stC + q + 2] * c.z;
-    aA = aA + N[stA + q + 3] * a.w; aB = aB + N[stB + q + 3] * b.w; aC = aC + N[stC + q + 3] * c.w;
+    const float4 a = *reinterpret_cast<const float4*>(wA + 16 * q);
+    const float4 b = *reinterpret_cast<const float4*>(wB + 16 * q);
+    const float4 c = *reinterpret_cast<const float4*>(wC + 16 * q);
+    const float4 na = *reinterpret_cast<const float4*>(N + stA + q);
+    const float4 nb = *reinterpret_cast<const float4*>(N + stB + q);
+    const float4 nc = *reinterpret_cast<const float4*>(N + stC + q);
+    aA = aA + na.x * a.x; aB = aB + nb.x * b.x; aC = aC + nc.x * c.x;
+    aA = aA + na.y * a.y; aB = aB + nb.y * b.y; aC = aC + nc.y * c.y;
+    aA = aA + na.z * a.z; aB = aB + nb.z * b.z; aC = aC + nc.z * c.z;
+    aA = aA + na.w * a.w; aB = aB + nb.w * b.w; aC = aC + nc.w * c.w;
   }
   for (; q < lenB; q += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(wA + q);
-    const float4 b = *reinterpret_cast<const float4*>(wB + q);
-    aA = aA + N[stA + q] * a.x; aB = aB + N[stB + q] * b.x;
-    aA = aA + N[stA + q + 1] * a.y; aB = aB + N[stB + q + 1] * b.y;
-    aA = aA + N[stA + q + 2] * a.z; aB = aB + N[stB + q + 2] * b.z;
-    aA = aA + N[stA + q + 3] * a.w; aB = aB + N[stB + q + 3] * b.w;
+    const float4 a = *reinterpret_cast<const float4*>(wA + 16 * q);
+    const float4 b = *reinterpret_cast<const float4*>(wB + 16 * q);
+    const float4 na = *reinterpret_cast<const float4*>(N + stA + q);
+    const float4 nb = *reinterpret_cast<const float4*>(N + stB + q);
+    aA = aA + na.x * a.x; aB = aB + nb.x * b.x;
+    aA = aA + na.y * a.y; aB = aB + nb.y * b.y;
+    aA = aA + na.z * a.z; aB = aB + nb.z * b.z;
+    aA = aA + na.w * a.w; aB = aB + nb.w * b.w;
   }
   for (; q < lenA; q += 4) {
-    const float4 a = *reinterpret_cast<const float4*>(wA + q);
-    aA = aA + N[stA + q] * a.x;
-    aA = aA + N[stA + q + 1] * a.y;
-    aA = aA + N[stA + q + 2] * a.z;
-    aA = aA + N[stA + q + 3] * a.w;
+    const float4 a = *reinterpret_cast<const float4*>(wA + 16 * q);
+    const float4 na = *reinterpret_cast<const float4*>(N + stA + q);
+    TFP_MAC4(aA, na, a);
   }
+#undef TFP_MAC4
+}
+
+// mel3 for a compile-time slot schedule (8 kHz: 36/16/8): fully unrolled, so every weight and
+// |X| read of the three slots is issued before the first sum needs it (the runtime-length loop
+// waits out one LDS round trip per 4 bins). One dependent chain per slot, each in ascending bin
+// order; the products of 4 bins pair into v_pk_mul_f32 without register moves.
+template <int LA, int LB, int LC, class WPtr>
+__device__ __forceinline__ void mel3_fixed(const float* __restrict__ N, WPtr wA, WPtr wB, WPtr wC, int stA, int stB,
+                                           int stC, float& aA, float& aB, float& aC) {
+  float4 wa[LA / 4], na[LA / 4], wb[LB / 4], nb[LB / 4], wc[LC / 4], nc[LC / 4];
+#pragma unroll
+  for (int i = 0; i < LC / 4; i++) {
+    wc[i] = *reinterpret_cast<const float4*>(wC + 64 * i);
+    nc[i] = *reinterpret_cast<const float4*>(N + stC + 4 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < LB / 4; i++) {
+    wb[i] = *reinterpret_cast<const float4*>(wB + 64 * i);
+    nb[i] = *reinterpret_cast<const float4*>(N + stB + 4 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < LA / 4; i++) {
+    wa[i] = *reinterpret_cast<const float4*>(wA + 64 * i);
+    na[i] = *reinterpret_cast<const float4*>(N + stA + 4 * i);
+  }
+#pragma unroll
+  for (int i = 0; i < LC / 4; i++) {
+    aC = aC + nc[i].x * wc[i].x; aC = aC + nc[i].y * wc[i].y; aC = aC + nc[i].z * wc[i].z; aC = aC + nc[i].w * wc[i].w;
+  }
+#pragma unroll
+  for (int i = 0; i < LB / 4; i++) {
+    aB = aB + nb[i].x * wb[i].x; aB = aB + nb[i].y * wb[i].y; aB = aB + nb[i].z * wb[i].z; aB = aB + nb[i].w * wb[i].w;
+  }
+#pragma unroll
+  for (int i = 0; i < LA / 4; i++) {
+    aA = aA + na[i].x * wa[i].x; aA = aA + na[i].y * wa[i].y; aA = aA + na[i].z * wa[i].z; aA = aA + na[i].w * wa[i].w;
+  }
+}
+
+// |X[k]|^2 of the 512-point real FFT from Z[k] = y and Z[256 - k] = P with w = w512^k:
+// E = (a + Px, b - Py), O = (a - Px, b + Py), tr = wx Oi + wy Or, ti = wx Or - wy Oi,
+// X = (0.5 (Er + tr), 0.5 (Ei - ti)), |X|^2 = Xr Xr + Xi Xi — each lane of each packed op is
+// that scalar operation (-(a - b) and (-a) + b round alike; only a zero's sign may differ in
+// Xi, which Xi * Xi erases).
+#ifndef TFP_SPLIT_VARIANT
+#define TFP_SPLIT_VARIANT 1
+#endif
+__device__ __forceinline__ float split_power(cf y, cf P, cf w) {
+#if TFP_SPLIT_VARIANT == 1
+  const cf Pc = cf{P.x, -P.y};
+  const cf E = y + Pc;
+  const cf O = y - Pc;
+  const cf u = cf{O.y, O.x} * cf{w.x, w.x};  // (wx Oi, wx Or)
+  const cf v = O * cf{w.y, w.y};             // (wy Or, wy Oi)
+  const cf T = cf{u.x, -u.y} + v;            // (tr, -ti)
+#else
+  const cf E = cf{y.x + P.x, y.y - P.y};
+  const cf O = cf{y.x - P.x, y.y + P.y};
+  const cf u = cf{O.y, O.x} * cf{w.x, -w.x};  // (wx Oi, -(wx Or))
+  const cf v = O * cf{w.y, w.y};              // (wy Or, wy Oi)
+  const cf T = u + v;                         // (tr, -ti)
+#endif
+  const cf X = cf{0.5f, 0.5f} * (E + T);
+  const cf X2 = X * X;
+  return X2.x + X2.y;
 }
 
 // v_sqrt_f32 (<= 1 ulp) + exact fma-residual correction: the correctly rounded sqrtf for
@@ -216,6 +288,11 @@ __device__ __forceinline__ float sqrtf_fast_cr(float x) {
   return y;
 }
 
+// Value of lane (16 - L) & 15 of this lane's 16-lane row (L = lane & 15). ds_bpermute: measured
+// faster than the two-DPP-mov form (row_mirror + row_ror:1, 0.937 vs 0.911 ms per C2 launch),
+// whose chained DPP reads cost wait states.
+__device__ __forceinline__ float partner16(float v) { return __shfl(v, (16 - (int)(threadIdx.x & 15)) & 15, 16); }
+
 __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
@@ -227,10 +304,10 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
   for (int i = tid; i < kWin; i += 256) S.window[i] = T->window_s[i];
   for (int i = tid; i < 15 * 16; i += 256) {
     const int k1 = 1 + i / 16, L = i % 16;
-    S.lane_tw[k1 - 1][L] = make_float2(T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]);
+    S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
   }
-  for (int i = tid; i < 10; i += 256) S.w16[i] = make_float2(T->tw256_re[16 * i], T->tw256_im[16 * i]);
-  for (int i = tid; i < kBins; i += 256) S.tw512[i] = make_float2(T->tw512_re[i], T->tw512_im[i]);
+  for (int i = tid; i < 10; i += 256) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
+  for (int i = tid; i < kBins; i += 256) S.tw512[i] = cf{T->tw512_re[i], T->tw512_im[i]};
   for (int i = tid; i < kCoefs * kFilters; i += 256) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
   for (int i = tid; i < 48; i += 256) {
     (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
@@ -244,7 +321,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
 
   const int wave = tid >> 6, lane = tid & 63, grp = lane >> 4, L = lane & 15;
   WaveLds& M = WL[wave];
-  float2* W = M.scratch[grp];
+  cf* W = M.scratch[grp];
   float* N = reinterpret_cast<float*>(W);  // |X| at [0, 257) after the FFT
   const int nwaves = gridDim.x * 4;
   const int lenA = S.ms_len[0], lenB = S.ms_len[1], lenC = S.ms_len[2];
@@ -298,8 +375,8 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
       // ~90 of them into registers for the whole kernel (occupancy).
       int oz = 0;
       asm volatile("" : "+v"(oz));
-      const float* __restrict__ win = S.window;  // may live in registers (32 per lane)
-      float2 z[16], Y[16];
+      const float* __restrict__ win = S.window + oz;  // read per pass (registers: occupancy)
+      cf z[16], Y[16];
       if (ablate & 1) {
 #pragma unroll
         for (int n1 = 0; n1 < 16; n1++) { z[n1].x = win[n1 + L]; z[n1].y = (float)f; }
@@ -309,8 +386,8 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
           const int j = (32 * n1 + 2 * L + 256) & 511;
           const int hsel = n1 < 8 ? 1 : 0;
           const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
-          z[n1].x = (float)(int16_t)(v & 0xffff) * win[j];  // == (s / 32768) * hanningz[j], exactly
-          z[n1].y = (float)(int16_t)(v >> 16) * win[j + 1];
+          const cf wj = *reinterpret_cast<const cf*>(win + j);  // j even
+          z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wj;  // (s / 32768) * hanningz[j]
         }
       }
       if (ablate & 2) {
@@ -319,10 +396,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
       } else {
         dft16(S.w16, z, Y);
 #pragma unroll
-        for (int k1 = 1; k1 < 16; k1++) {
-          const float2 w = S.lane_tw[k1 - 1][L + oz];
-          Y[k1] = cmul(Y[k1], w.x, w.y);
-        }
+        for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
         wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
         for (int k1 = 0; k1 < 16; k1++) W[L * 16 + (k1 ^ L)] = Y[k1];
@@ -343,41 +417,32 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
         // outside [2^-100, 2^100) redo that bin with the full IEEE sqrt below (wave-uniform
         // test, practically never taken); lane 0 then writes the two real bins 0 and 256.
         bool rare = false;
+#ifndef TFP_SPLIT_PERBIN
+        cf P[16];  // every partner fetched before the first use: the 32 bpermutes overlap
+                   // (0.854 vs 0.865 ms per C2 launch fetched per bin)
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) P[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+#endif
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) {
           const int k = L + 16 * k2;
-          float2 P;
-          P.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
-          P.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
-          const float2 own = Y[(16 - k2) & 15];
-          P.x = L == 0 ? own.x : P.x;
-          P.y = L == 0 ? own.y : P.y;
-          const float a = Y[k2].x, bq = Y[k2].y;
-          const float Er = a + P.x, Ei = bq - P.y, Or = a - P.x, Oi = bq + P.y;
-          const float2 w = S.tw512[k + oz];
-          const float tr = w.x * Oi + w.y * Or;
-          const float ti = w.x * Or - w.y * Oi;
-          const float Xr = 0.5f * (Er + tr);
-          const float Xi = 0.5f * (Ei - ti);
-          const float x = Xr * Xr + Xi * Xi;
+          const cf own = Y[(16 - k2) & 15];
+#ifndef TFP_SPLIT_PERBIN
+          const cf Pk = cf{L == 0 ? own.x : P[k2].x, L == 0 ? own.y : P[k2].y};
+#else
+          const cf Pg = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+          const cf Pk = cf{L == 0 ? own.x : Pg.x, L == 0 ? own.y : Pg.y};
+#endif
+          const float x = split_power(Y[k2], Pk, S.tw512[k + oz]);
           rare |= !(x >= 0x1p-100f && x < 0x1p100f);
           N[k] = sqrtf_fast_cr(x);
         }
         if (__builtin_expect(__any(rare), 0)) {
           for (int k2 = 0; k2 < 16; k2++) {
             const int k = L + 16 * k2;
-            float2 Q;
-            Q.x = __shfl(Y[15 - k2].x, (16 - L) & 15, 16);
-            Q.y = __shfl(Y[15 - k2].y, (16 - L) & 15, 16);
+            cf Q = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
             if (L == 0) Q = Y[(16 - k2) & 15];
-            const float a = Y[k2].x, bq = Y[k2].y;
-            const float Er = a + Q.x, Ei = bq - Q.y, Or = a - Q.x, Oi = bq + Q.y;
-            const float2 w = S.tw512[k];
-            const float tr = w.x * Oi + w.y * Or;
-            const float ti = w.x * Or - w.y * Oi;
-            const float Xr = 0.5f * (Er + tr);
-            const float Xi = 0.5f * (Ei - ti);
-            const float x = Xr * Xr + Xi * Xi;
+            const float x = split_power(Y[k2], Q, S.tw512[k]);
             if (!(x >= 0x1p-100f && x < 0x1p100f)) N[k] = __builtin_sqrtf(x);
           }
         }
@@ -398,8 +463,14 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
       } else {
         const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
         float aA = 0.f, aB = 0.f, aC = 0.f;
-        const int oA = S.ms_woff[0] + L * lenA, oB = S.ms_woff[1] + L * lenB, oC = S.ms_woff[2] + L * lenC;
-        if (ms_in_lds)
+        const int oA = S.ms_woff[0] + 4 * L, oB = S.ms_woff[1] + 4 * L, oC = S.ms_woff[2] + 4 * L;
+#ifndef TFP_MEL_GENERIC
+        if (ms_in_lds && lenA == 36 && lenB == 16 && lenC == 8)  // the 8 kHz schedule
+#else
+        if (false)
+#endif
+          mel3_fixed<36, 16, 8>(N, S.ms_w + oA, S.ms_w + oB, S.ms_w + oC, stA, stB, stC, aA, aB, aC);
+        else if (ms_in_lds)
           mel3(N, S.ms_w + oA, S.ms_w + oB, S.ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);
         else
           mel3(N, T->ms_w + oA, T->ms_w + oB, T->ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);

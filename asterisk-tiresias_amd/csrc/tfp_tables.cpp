@@ -115,12 +115,16 @@ bool build_tables(int sample_rate, DspTables* t) {
   }
   t->mel_total = off;
 
-  // filterbank slot schedule
-  int order[kFilters];
+  // filterbank slot schedule: each filter's bins are read from its start rounded down to a
+  // multiple of 4, so the kernel reads |X| with aligned 16-byte loads; the lead-in weights are
+  // zero and add exact +0 to the +0 sum (fmat_vecmul sums every bin from 0 anyway)
+  int order[kFilters], lead[kFilters];
+  for (int j = 0; j < kFilters; j++) lead[j] = t->mel_len[j] ? (t->mel_start[j] & 3) : 0;
   for (int j = 0; j < kFilters; j++) order[j] = j;
-  for (int a = 0; a < kFilters; a++)  // stable selection sort by length, longest first
+  auto span = [&](int j) { return t->mel_len[j] ? lead[j] + t->mel_len[j] : 0; };
+  for (int a = 0; a < kFilters; a++)  // stable selection sort by span read, longest first
     for (int b = a + 1; b < kFilters; b++)
-      if (t->mel_len[order[b]] > t->mel_len[order[a]]) { const int x = order[a]; order[a] = order[b]; order[b] = x; }
+      if (span(order[b]) > span(order[a])) { const int x = order[a]; order[a] = order[b]; order[b] = x; }
   int woff = 0;
   for (int sl = 0; sl < 3; sl++) {
     int len = 0;
@@ -128,8 +132,8 @@ bool build_tables(int sample_rate, DspTables* t) {
       const int idx = sl * 16 + L;
       const int j = idx < kFilters ? order[idx] : -1;
       t->ms_filter[sl][L] = j;
-      t->ms_start[sl][L] = j >= 0 ? t->mel_start[j] : 0;
-      if (j >= 0 && t->mel_len[j] > len) len = t->mel_len[j];
+      t->ms_start[sl][L] = j >= 0 ? t->mel_start[j] - lead[j] : 0;
+      if (j >= 0 && t->mel_len[j] && lead[j] + t->mel_len[j] > len) len = lead[j] + t->mel_len[j];
     }
     len = (len + 3) & ~3;
     t->ms_len[sl] = len;
@@ -137,7 +141,10 @@ bool build_tables(int sample_rate, DspTables* t) {
     for (int L = 0; L < 16; L++)
       for (int q = 0; q < len; q++) {
         const int j = t->ms_filter[sl][L];
-        t->ms_w[woff + L * len + q] = (j >= 0 && q < t->mel_len[j]) ? t->mel_w[t->mel_off[j] + q] : 0.f;
+        const int r = j >= 0 ? q - lead[j] : -1;
+        // [slot][q / 4][lane][q % 4]: a 16-lane ds_read_b128 group reads 16 consecutive 16-B slots
+        t->ms_w[woff + (q >> 2) * 64 + L * 4 + (q & 3)] =
+            (j >= 0 && r >= 0 && r < t->mel_len[j]) ? t->mel_w[t->mel_off[j] + r] : 0.f;
       }
     woff += len * 16;
   }

@@ -34,11 +34,11 @@ struct DspTables {
   // still aubio's sequential ascending-bin sum).
   int32_t ms_len[3];         // padded slot length (multiple of 4)
   int32_t ms_filter[3][16];  // filter id or -1
-  int32_t ms_start[3][16];   // first bin
+  int32_t ms_start[3][16];   // first bin read, a multiple of 4 (leading weights are zero)
   int32_t ms_woff[3];        // offset of slot s in ms_w
   int32_t ms_total;          // floats used in ms_w
   int32_t ms_maxbin;         // 1 + the highest bin a padded slot reads (bins > 256 read zeros)
-  alignas(16) float ms_w[3 * kBins * 16];
+  alignas(16) float ms_w[3 * (kBins + 8) * 16];  // [slot][q / 4][lane][q % 4], slot at ms_woff
   // hanningz window pre-scaled by 2^-15 (exact): x = (float)sample * window_s[j] equals aubio's
   // ((float)sample / 32768) * window[j] bit for bit.
   float window_s[kWin];
