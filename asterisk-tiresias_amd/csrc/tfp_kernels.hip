@@ -61,7 +61,7 @@ __device__ __forceinline__ void dft16(const cf* __restrict__ w16, const cf (&in)
 //   * A workgroup stages the DSP tables in LDS once; afterwards its 4 waves never wait on each
 //     other: each wave walks 16-frame tiles on its own (tile = 16 consecutive frames of a clip).
 //   * FFT stage: 16 lanes per frame, 4 frames per pass, 4 passes per tile. The 256-point complex
-//     FFT is 16x16 Cooley-Tukey with the transpose through an XOR-swizzled LDS square; the real
+//     FFT is 16x16 Cooley-Tukey with the transpose through a padded (16x17) LDS square; the real
 //     split, |X|, the filterbank and the log10 stay on the frame's 16 lanes. Each frame leaves its
 //     40 band logs in the wave's log buffer.
 //   * Tail: once per tile, 32 lanes (frame, coef) run the DCT row, 10*log10|c| and "%f" rounding.
@@ -71,8 +71,15 @@ __device__ __forceinline__ void dft16(const cf* __restrict__ w16, const cf (&in)
 #ifndef TFP_FP_WAVES
 #define TFP_FP_WAVES 2  // waves per SIMD the register budget is cut for (A/B: scripts/ab_waves.sh)
 #endif
+#ifndef TFP_FP_BLOCK_WAVES
+#define TFP_FP_BLOCK_WAVES 4  // waves per workgroup (LDS: tables once per block + per-wave scratch)
+#endif
+constexpr int kBlockWaves = TFP_FP_BLOCK_WAVES;
+constexpr int kBlockThreads = 64 * kBlockWaves;
 constexpr int kWaveFrames = 16;     // frames per wave tile (== kFramesPerBlock: tile offsets)
-constexpr int kFrameStride = 258;   // complex per frame scratch: 16x16 XOR-swizzled square + pad
+constexpr int kFrameStride = 272;   // complex per frame scratch: 16x17 padded square (2 x 272 floats
+                                    // = 32 mod 64 banks: frames g, g+1 of a b64 read take opposite halves)
+constexpr int kSq = 17;             // padded row of the transpose square (affine addresses, no conflicts)
 constexpr int kLogStride = 41;      // floats per frame row in the log buffer (bank-conflict free)
 constexpr int kMsLds = 960;         // filterbank slot-schedule weights kept in LDS (8 kHz: 16 x 60)
 
@@ -104,6 +111,7 @@ struct WaveLds {
   float logs[kWaveFrames * kLogStride];
 };
 static_assert(sizeof(int16_t) * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride, "pcm alias fits");
+static_assert(16 * kSq <= kFrameStride && 16 + 500 <= 2 * kFrameStride, "square and |X| rows (ms_maxbin <= 500) fit");
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
 struct PassSrc {
@@ -293,37 +301,39 @@ __device__ __forceinline__ float sqrtf_fast_cr(float x) {
 // whose chained DPP reads cost wait states.
 __device__ __forceinline__ float partner16(float v) { return __shfl(v, (16 - (int)(threadIdx.x & 15)) & 15, 16); }
 
-__global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
+__global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip,
     int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
   __shared__ __attribute__((aligned(16))) LdsTables S;
-  __shared__ __attribute__((aligned(16))) WaveLds WL[4];
+  __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += 256) S.window[i] = T->window_s[i];
-  for (int i = tid; i < 15 * 16; i += 256) {
+  for (int i = tid; i < kWin; i += kBlockThreads) S.window[i] = T->window_s[i];
+  for (int i = tid; i < 15 * 16; i += kBlockThreads) {
     const int k1 = 1 + i / 16, L = i % 16;
     S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
   }
-  for (int i = tid; i < 10; i += 256) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
-  for (int i = tid; i < kBins; i += 256) S.tw512[i] = cf{T->tw512_re[i], T->tw512_im[i]};
-  for (int i = tid; i < kCoefs * kFilters; i += 256) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
-  for (int i = tid; i < 48; i += 256) {
+  for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
+  for (int i = tid; i < kBins; i += kBlockThreads) S.tw512[i] = cf{T->tw512_re[i], T->tw512_im[i]};
+  for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
+  for (int i = tid; i < 48; i += kBlockThreads) {
     (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
     (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
   }
   if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
   if (tid < 16) S.logf[tid] = logf_table()[tid];
   const bool ms_in_lds = T->ms_total <= kMsLds;
-  for (int i = tid; i < (ms_in_lds ? T->ms_total : 0); i += 256) S.ms_w[i] = T->ms_w[i];
+  for (int i = tid; i < (ms_in_lds ? T->ms_total : 0); i += kBlockThreads) S.ms_w[i] = T->ms_w[i];
   __syncthreads();
 
   const int wave = tid >> 6, lane = tid & 63, grp = lane >> 4, L = lane & 15;
   WaveLds& M = WL[wave];
   cf* W = M.scratch[grp];
-  float* N = reinterpret_cast<float*>(W);  // |X| at [0, 257) after the FFT
-  const int nwaves = gridDim.x * 4;
+  // |X| at [0, 257) after the FFT; odd frames' rows are shifted by 16 floats so that the |X|
+  // stores of frames g and g+1 (one ds_write_b32 lane half) take opposite bank halves
+  float* N = reinterpret_cast<float*>(W) + 16 * (grp & 1);
+  const int nwaves = gridDim.x * kBlockWaves;
   const int lenA = S.ms_len[0], lenB = S.ms_len[1], lenC = S.ms_len[2];
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
@@ -339,7 +349,7 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
   };
 
   int4 pf[kChunkRounds];
-  int b = blockIdx.x * 4 + wave;
+  int b = blockIdx.x * kBlockWaves + wave;
   int c = b < ntiles ? tclip[b] : 0;
   int64_t f0 = b < ntiles ? (int64_t)(b - toff[c]) * kWaveFrames : 0;
   fetch_pass(pass_src(c, f0, 0), b < ntiles, lane, pf);
@@ -399,10 +409,10 @@ __global__ __launch_bounds__(256, TFP_FP_WAVES) void fingerprint_kernel(
         for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
         wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
-        for (int k1 = 0; k1 < 16; k1++) W[L * 16 + (k1 ^ L)] = Y[k1];
+        for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
         wave_sync();
 #pragma unroll
-        for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * 16 + (L ^ n2)];
+        for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
         dft16(S.w16, z, Y);  // Y[k2] = Z[L + 16 k2]
       }
       wave_sync();  // every lane has read its column of the square: W is free for |X|
@@ -519,17 +529,17 @@ hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, c
     int dev = 0, cus = 256, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, 256, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, kBlockThreads, 0);
     grid_cap = cus * (per > 0 ? per : 1);
   }
-  const int want = (ntiles + 3) / 4;  // 4 waves per workgroup, one tile per wave per step
+  const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
   const int grid = want < grid_cap ? want : grid_cap;
   static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production
   if (ablate < 0) {
     const char* a = getenv("TFP_ABLATE");
     ablate = a ? atoi(a) : 0;
   }
-  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(256), 0, s, d_tables, d_pcm, d_sbeg, d_send, d_foff,
+  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send, d_foff,
                      d_toff, d_tclip, ntiles, d_micro, d_db, ablate);
   return hipGetLastError();
 }

@@ -153,7 +153,7 @@ bool build_tables(int sample_rate, DspTables* t) {
   for (int sl = 0; sl < 3; sl++)
     for (int L = 0; L < 16; L++)
       if (t->ms_start[sl][L] + t->ms_len[sl] > t->ms_maxbin) t->ms_maxbin = t->ms_start[sl][L] + t->ms_len[sl];
-  if (t->ms_maxbin > 500) return false;  // the kernel's per-frame |X| row holds 516 floats
+  if (t->ms_maxbin > 500) return false;  // the kernel's per-frame |X| row holds 528 floats
   for (int i = 0; i < kWin; i++) t->window_s[i] = t->window[i] * 0x1p-15f;
   for (int k1 = 0; k1 < 16; k1++)
     for (int L = 0; L < 16; L++) {

@@ -8,6 +8,8 @@ import sys
 sys.path.insert(0, ".")
 FS = int(sys.argv[1]) if len(sys.argv) > 1 else 258
 HS = int(sys.argv[2]) if len(sys.argv) > 2 else 288
+PAD = len(sys.argv) > 3 and sys.argv[3] == "pad17"  # padded square W[L*17 + k] instead of XOR swizzle
+NOFF = 16 if PAD else 0                                 # |X| row of odd frames shifted by 16 floats
 
 G_B32 = [list(range(0, 32)), list(range(32, 64))]
 G_B128 = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)],
@@ -59,14 +61,14 @@ def main():
     pcm_base = 0
     # transpose write b64 / read b64
     for k1 in range(16):
-        ad = [(g * FS + L * 16 + (k1 ^ L)) * 8 for g, L in lanes()]
+        ad = [(g * FS + (L * 17 + k1 if PAD else L * 16 + (k1 ^ L))) * 8 for g, L in lanes()]
         tot["transpose w64"] = tot.get("transpose w64", 0) + extra("ds_write_b64", ad)
     for n2 in range(16):
-        ad = [(g * FS + n2 * 16 + (L ^ n2)) * 8 for g, L in lanes()]
+        ad = [(g * FS + (n2 * 17 + L if PAD else n2 * 16 + (L ^ n2))) * 8 for g, L in lanes()]
         tot["transpose r64"] = tot.get("transpose r64", 0) + extra("ds_read_b64", ad)
     # |X| writes b32
     for k2 in range(16):
-        ad = [(g * FS * 2 + L + 16 * k2) * 4 for g, L in lanes()]
+        ad = [(g * FS * 2 + NOFF * (g & 1) + L + 16 * k2) * 4 for g, L in lanes()]
         tot["N write b32"] = tot.get("N write b32", 0) + extra("ds_write_b32", ad)
     # filterbank: |X| b128 reads + weight b128 reads (8 kHz slot schedule from the host tables)
     try:
@@ -79,13 +81,14 @@ def main():
         lens, starts = sched
         for sl in range(3):
             for q in range(0, lens[sl], 4):
-                ad = [(g * FS * 2 + starts[sl][L] + q) * 4 for g, L in lanes()]
+                ad = [(g * FS * 2 + NOFF * (g & 1) + starts[sl][L] + q) * 4 for g, L in lanes()]
                 tot["mel N r128"] = tot.get("mel N r128", 0) + extra("ds_read_b128", ad)
                 ad = [(16 * q + 4 * L) * 4 for g, L in lanes()]
                 tot["mel w r128 (interleaved)"] = tot.get("mel w r128 (interleaved)", 0) + extra("ds_read_b128", ad)
                 ad = [(L * lens[sl] + q) * 4 for g, L in lanes()]
                 tot["mel w r128 (per-lane rows)"] = tot.get("mel w r128 (per-lane rows)", 0) + extra("ds_read_b128", ad)
-    print(f"frame stride {FS} float2, hop stride {HS} samples: extra LDS cycles per pass")
+    print(f"frame stride {FS} float2, hop stride {HS} samples, {'padded' if PAD else 'xor'} square:"
+          " extra LDS cycles per pass")
     for k, v in tot.items():
         print(f"  {k:28s} {v}")
 
