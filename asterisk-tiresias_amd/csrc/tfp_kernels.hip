@@ -92,6 +92,7 @@ struct LdsTables {
   int32_t ms_len[3], ms_woff[3];
   int32_t ms_filter[3][16], ms_start[3][16];
   LogfEntry logf[16];
+  int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
   alignas(16) float ms_w[kMsLds];
 };
 
@@ -323,6 +324,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   }
   if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
   if (tid < 16) S.logf[tid] = logf_table()[tid];
+  if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
   const bool ms_in_lds = T->ms_total <= kMsLds;
   for (int i = tid; i < (ms_in_lds ? T->ms_total : 0); i += kBlockThreads) S.ms_w[i] = T->ms_w[i];
   __syncthreads();
@@ -337,6 +339,16 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   const int lenA = S.ms_len[0], lenB = S.ms_len[1], lenC = S.ms_len[2];
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
+  const bool c_defer = S.c_defer != 0;
+  const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
+  {
+    // log rows of empty filters (zero sum) never change: the constant log of the clamped 0
+    const float lempty = aubio_log10_fast(0.f, S.logf);
+    for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
+      const int j = i % kFilters;
+      if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
+    }
+  }
 
   auto pass_src = [&](int c, int64_t f0, int sub) {
     PassSrc p;
@@ -485,15 +497,29 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
         else
           mel3(N, T->ms_w + oA, T->ms_w + oB, T->ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);
         // three independent log chains, computed unconditionally so they interleave (ILP 3)
-        const float lA = aubio_log10_clamped(aA, S.logf);
-        const float lB = aubio_log10_clamped(aB, S.logf);
-        const float lC = aubio_log10_clamped(aC, S.logf);
+        const float lA = aubio_log10_fast(aA, S.logf);  // branch-free: the chains interleave
+        const float lB = aubio_log10_fast(aB, S.logf);
         if (fA >= 0) lrow[fA] = lA;
         if (fB >= 0) lrow[fB] = lB;
-        if (fC >= 0) lrow[fC] = lC;
+        if (c_defer) {
+          if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+        } else {
+          const float lC = aubio_log10_fast(aC, S.logf);
+          if (fC >= 0) lrow[fC] = lC;
+        }
       }
     }
     wave_sync();
+    if (c_defer) {  // the deferred slot-2 logs: lane = (frame row, filter)
+      if (lane < 2 * kWaveFrames) {
+        const int f = S.c_real[lane & 1];
+        if (f >= 0) {
+          float* p = M.logs + (lane >> 1) * kLogStride + f;
+          *p = aubio_log10_fast(*p, S.logf);
+        }
+      }
+      wave_sync();
+    }
     // Tail: lane = (frame row, coef) for the tile's 16 frames: DCT row (fmat_vecmul order),
     // 10*log10|c| (fp_handler.c:651), "%f" micro-units / NULL (db_ctx_handler.c:479-481).
     if ((ablate & 16) && lane < 2 * kWaveFrames) {

@@ -117,6 +117,27 @@ TFP_HD float aubio_log10_clamped(float x, const LogfEntry* T = logf_table()) {
   return log10f_glibc(a, T);
 }
 
+// aubio_log10_clamped for the filterbank sums (finite, >= -0), branch-free. For any non-NaN
+// float x the double-precision clamp (2e-42 > (double)x ? (float)2e-42 : x) equals
+// max(x, (float)2e-42), after which the only special case of log10f left is a subnormal
+// argument (rescaled by 2^25 under a select). Bit-identical to aubio_log10_clamped on every
+// non-negative float (tests/native/check_math.cpp #5, exhaustive log committed).
+TFP_HD float aubio_log10_fast(float x, const LogfEntry* T = logf_table()) {
+  const float two25 = 3.3554432000e+07f, ivln10 = 4.3429449201e-01f;
+  const float log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+  const float c = (float)2.e-42;
+  float a = x > c ? x : c;
+  const bool den = f2u(a) < 0x00800000u;
+  a = den ? a * two25 : a;
+  int32_t hx = (int32_t)f2u(a);
+  const int32_t k = (den ? -25 : 0) + (hx >> 23) - 127;
+  const int32_t i = (int32_t)(((uint32_t)k & 0x80000000u) >> 31);
+  hx = (hx & 0x007fffff) | ((0x7f - i) << 23);
+  const float y = (float)(k + i);
+  const float z = y * log10_2lo + ivln10 * logf_glibc(u2f((uint32_t)hx), T);
+  return z + y * log10_2hi;
+}
+
 // ---------------------------------------------------------------------------------------
 // Near-correctly-rounded natural log for x in [0.5, 2): reduce to [sqrt(1/2), sqrt(2)),
 // log(m) = 2 atanh(s), s = (m-1)/(m+1) kept as a double-double, series tail in double.

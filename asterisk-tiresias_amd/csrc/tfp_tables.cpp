@@ -149,6 +149,16 @@ bool build_tables(int sample_rate, DspTables* t) {
     woff += len * 16;
   }
   t->ms_total = woff;
+  t->ms_c_real[0] = t->ms_c_real[1] = -1;
+  int nreal = 0;
+  for (int L = 0; L < 16; L++) {
+    const int j = t->ms_filter[2][L];
+    if (j >= 0 && t->mel_len[j] > 0) {
+      if (nreal < 2) t->ms_c_real[nreal] = j;
+      nreal++;
+    }
+  }
+  t->ms_c_defer = nreal <= 2 ? 1 : 0;
   t->ms_maxbin = kBins;
   for (int sl = 0; sl < 3; sl++)
     for (int L = 0; L < 16; L++)

@@ -27,11 +27,11 @@ struct DspTables {
   int32_t mel_total;
   int32_t sample_rate;
   float mel_w[kFilters * kBins];
-  // Kernel schedule of the filterbank: filters sorted by length are dealt to 3 slots x 16
-  // lanes (slot 0 = the 16 longest); a lane runs its 3 filters' sums interleaved. Weights are
-  // laid out [slot][lane][q] (q contiguous, read 4 at a time), zero-padded to the slot's longest
-  // filter rounded up to 4 (padding adds exact +0 after a filter's last bin, so every sum is
-  // still aubio's sequential ascending-bin sum).
+  // Kernel schedule of the filterbank: filters sorted by the span they read are dealt to 3
+  // slots x 16 lanes (slot 0 = the 16 longest); a lane computes one sum per slot. Each span
+  // starts at the filter's first bin rounded down to a multiple of 4 and is zero-padded to the
+  // slot's longest span rounded up to 4 (zero weights add exact +0 before the first and after
+  // the last bin, so every sum is still aubio's sequential ascending-bin sum).
   int32_t ms_len[3];         // padded slot length (multiple of 4)
   int32_t ms_filter[3][16];  // filter id or -1
   int32_t ms_start[3][16];   // first bin read, a multiple of 4 (leading weights are zero)
@@ -44,6 +44,11 @@ struct DspTables {
   float window_s[kWin];
   // Inter-stage FFT twiddles per lane: lane_tw[k1][L] = w256^(L*k1) (re, im), conflict-free reads.
   float lane_tw_re[16][16], lane_tw_im[16][16];
+  // Slot 2 with at most 2 non-empty filters (8 kHz: 2 real + 6 empty): the kernel writes those
+  // 2 raw sums and takes their logs once per 16-frame tile on 32 lanes, instead of a third
+  // log per lane per pass; empty filters' log rows hold the constant log of the clamped 0.
+  int32_t ms_c_defer;       // 1 when slot 2 qualifies
+  int32_t ms_c_real[2];     // its non-empty filter ids (-1: none)
 };
 
 // Dense filterbank as aubio lays it out (40 x 257), for tests.

@@ -86,6 +86,20 @@ int main(int argc, char** argv) {
     printf("fmt6 vs printf(\"%%f\") : %lu / %lu mismatches\n", bad, tot);
     rc |= bad != 0;
   }
+  // 5. aubio_log10_fast (branch-free, kernel) == aubio_log10_clamped on every non-negative float
+  {
+    uint64_t tot = 0, bad = 0;
+#pragma omp parallel for reduction(+ : tot, bad) schedule(static)
+    for (int64_t u = 0; u <= 0x7f7fffffLL; u += (int64_t)stride) {
+      const float x = u2f((uint32_t)u);
+      tot++;
+      if (f2u(aubio_log10_fast(x)) != f2u(aubio_log10_clamped(x))) bad++;
+    }
+    tot++;
+    if (f2u(aubio_log10_fast(-0.0f)) != f2u(aubio_log10_clamped(-0.0f))) bad++;
+    printf("aubio_log10_fast vs aubio_log10_clamped : %lu / %lu mismatches\n", bad, tot);
+    rc |= bad != 0;
+  }
   printf(rc ? "FAIL\n" : "OK\n");
   return rc;
 }
