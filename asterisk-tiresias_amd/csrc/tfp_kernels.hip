@@ -22,25 +22,27 @@ namespace tfp {
 
 // Complex values as (re, im) register pairs: every operation below is a v_pk_*_f32 whose lanes
 // perform exactly the scalar IEEE operations of the canonical spec (x + (-y) == x - y, products
-// and sums commute), with swaps and negations folded into op_sel / neg modifiers.
+// and sums commute). Per-lane signs ride on an exact fma: fma(p, (1, -1), c) rounds c + p.x and
+// c - p.y once each — the plain add and subtract — so (re, im) sign patterns cost no moves.
 typedef float cf __attribute__((ext_vector_type(2)));
 
-__device__ __forceinline__ cf swapneg_lo(cf a) { return cf{-a.y, a.x}; }  // (-im, re) = i a
-__device__ __forceinline__ cf swapneg_hi(cf a) { return cf{a.y, -a.x}; }  // (im, -re) = -i a
+__device__ __forceinline__ cf swap(cf a) { return __builtin_shufflevector(a, a, 1, 0); }
+__device__ __forceinline__ cf addsub(cf c, cf p) { return __builtin_elementwise_fma(p, cf{1.f, -1.f}, c); }  // (c.x + p.x, c.y - p.y)
+__device__ __forceinline__ cf subadd(cf c, cf p) { return __builtin_elementwise_fma(p, cf{-1.f, 1.f}, c); }  // (c.x - p.x, c.y + p.y)
 
 // a * w: (a.x wr - a.y wi, a.x wi + a.y wr)
 __device__ __forceinline__ cf cmul(cf a, cf w) {
-  const cf p = a * cf{w.x, w.x};
-  const cf q = cf{a.y, a.x} * cf{-w.y, w.y};
-  return p + q;
+  const cf p = a * cf{w.x, w.x};        // (a.x wr, a.y wr)
+  const cf q = swap(a) * cf{w.y, w.y};  // (a.y wi, a.x wi)
+  return subadd(p, q);
 }
 
 __device__ __forceinline__ void dft4(cf a0, cf a1, cf a2, cf a3, cf& X0, cf& X1, cf& X2, cf& X3) {
   const cf t0 = a0 + a2, t1 = a0 - a2, t2 = a1 + a3, t3 = a1 - a3;
   X0 = t0 + t2;
   X2 = t0 - t2;
-  X1 = t1 + swapneg_hi(t3);  // (t1r + t3i, t1i - t3r)
-  X3 = t1 + swapneg_lo(t3);  // (t1r - t3i, t1i + t3r)
+  X1 = addsub(t1, swap(t3));  // (t1r + t3i, t1i - t3r)
+  X3 = subadd(t1, swap(t3));  // (t1r - t3i, t1i + t3r)
 }
 
 // 16-point DFT in registers: n = 4 n1 + n2, k = k1 + 4 k2, W16^e = tw256[16 e].
@@ -261,24 +263,10 @@ __device__ __forceinline__ void mel3_fixed(const float* __restrict__ N, WPtr wA,
 // X = (0.5 (Er + tr), 0.5 (Ei - ti)), |X|^2 = Xr Xr + Xi Xi — each lane of each packed op is
 // that scalar operation (-(a - b) and (-a) + b round alike; only a zero's sign may differ in
 // Xi, which Xi * Xi erases).
-#ifndef TFP_SPLIT_VARIANT
-#define TFP_SPLIT_VARIANT 1
-#endif
 __device__ __forceinline__ float split_power(cf y, cf P, cf w) {
-#if TFP_SPLIT_VARIANT == 1
-  const cf Pc = cf{P.x, -P.y};
-  const cf E = y + Pc;
-  const cf O = y - Pc;
-  const cf u = cf{O.y, O.x} * cf{w.x, w.x};  // (wx Oi, wx Or)
-  const cf v = O * cf{w.y, w.y};             // (wy Or, wy Oi)
-  const cf T = cf{u.x, -u.y} + v;            // (tr, -ti)
-#else
-  const cf E = cf{y.x + P.x, y.y - P.y};
-  const cf O = cf{y.x - P.x, y.y + P.y};
-  const cf u = cf{O.y, O.x} * cf{w.x, -w.x};  // (wx Oi, -(wx Or))
-  const cf v = O * cf{w.y, w.y};              // (wy Or, wy Oi)
-  const cf T = u + v;                         // (tr, -ti)
-#endif
+  const cf E = addsub(y, P);                           // (a + Px, b - Py)
+  const cf O = subadd(y, P);                           // (a - Px, b + Py)
+  const cf T = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});  // (wy Or + wx Oi, wy Oi - wx Or) = (tr, -ti)
   const cf X = cf{0.5f, 0.5f} * (E + T);
   const cf X2 = X * X;
   return X2.x + X2.y;
