@@ -290,7 +290,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         else:
             eng.search_pcm_batch(host_q[i], [0, qn], p)
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
-    return {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
+    res = {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": "all_reduce(MAX) of one int64 key per query" if world > 1 else None,
             "coefs": 1, "tolerance": 0.001, "db_rows_local": rows, "db_clips_local": nclips_local,
@@ -298,6 +298,49 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat)}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        res["cpu_baseline"] = match_cpu_baseline(args, T)
+    return res
+
+
+def match_cpu_baseline(args, T, db_clips=200):
+    """The reference's own search path on the CPU: its SQL (oracle/sql_oracle.py restates
+    fp_handler.c:287-374 string for string) through SQLite 3.37, on a reduced DB — 200 of the
+    30 s clips inserted as db_ctx_insert does — with queries fingerprinted by the C oracle.
+    A smaller DB makes each range query cheaper, so this over-states the CPU's rate at C3."""
+    import oracle_py
+    from sql_oracle import SqlFingerprintDB
+    n_db, qn = 8000 * 30, 8000 * 5
+    nf_db = (n_db + HOP - 1) // HOP
+    ids = list(range(db_clips))
+    pcm = T.synth_pcm(SEED_DB, ids, n_db)
+    micro, _ = oracle_py.fingerprint_batch(pcm.reshape(-1), np.arange(db_clips + 1) * n_db, nthreads=16, want_db=False)
+    db = SqlFingerprintDB()
+    for i, g in enumerate(ids):
+        db.insert_rows("bench", uuid_of(g), micro[i * nf_db:(i + 1) * nf_db, 0], micro[i * nf_db:(i + 1) * nf_db, 1])
+    rng = np.random.default_rng(SEED_Q + 2)
+    queries = []
+    for i in range(64):
+        if i % 4 != 3:
+            q = T.synth_pcm(SEED_DB, [int(rng.integers(db_clips))], qn, offsets=[256 * int(rng.integers(0, (n_db - qn) // HOP))])[0]
+        else:
+            q = T.synth_pcm(SEED_Q, [100000 + i], qn)[0]
+        _, qdb, _ = oracle_py.fingerprint(q)
+        queries.append(([None if not np.isfinite(v) else float(v) for v in qdb[:, 0]],
+                        [None if not np.isfinite(v) else float(v) for v in qdb[:, 1]]))
+    done, found, t0 = 0, 0, time.perf_counter()
+    while True:
+        q1, q2 = queries[done % len(queries)]
+        found += db.search(q1, q2, 1, 0.001, -1, -1) is not None
+        done += 1
+        dt = time.perf_counter() - t0
+        if dt >= args.cpu_seconds and done >= len(queries):
+            break
+    log(f"match cpu baseline {done / dt:.1f} queries/s ({done} queries, {dt:.1f} s)")
+    return {"value": done / dt, "unit": "queries/s", "cores": 1, "kind": "port",
+            "sample": f"{done} x 5 s queries (75 % excerpts) vs {db_clips} x 30 s clips "
+                      f"({db_clips * nf_db} rows) through the reference SQL in SQLite {__import__('sqlite3').sqlite_version}, "
+                      f"1 thread, {dt:.1f} s; the GPU figure is against {args.db_clips} clips"}
 
 
 def run_stream(args, eng, T):
