@@ -46,7 +46,7 @@ __device__ __forceinline__ void dft4(cf a0, cf a1, cf a2, cf a3, cf& X0, cf& X1,
 }
 
 // 16-point DFT in registers: n = 4 n1 + n2, k = k1 + 4 k2, W16^e = tw256[16 e].
-__device__ __forceinline__ void dft16(const cf* __restrict__ w16, const cf (&in)[16], cf (&out)[16]) {
+__device__ __forceinline__ void dft16(const cf (&w16)[10], const cf (&in)[16], cf (&out)[16]) {
   cf A[4][4];
 #pragma unroll
   for (int n2 = 0; n2 < 4; n2++) dft4(in[n2], in[4 + n2], in[8 + n2], in[12 + n2], A[n2][0], A[n2][1], A[n2][2], A[n2][3]);
@@ -327,6 +327,21 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   const int lenA = S.ms_len[0], lenB = S.ms_len[1], lenC = S.ms_len[2];
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
+  // Loop-invariant twiddles in registers (2 waves/SIMD leave VGPR room): dft16's W16^e and this
+  // lane's inter-stage w256^(L k1), read from LDS once instead of every pass.
+#ifndef TFP_HOIST
+#define TFP_HOIST 3  // bit 0: dft16 twiddles, bit 1: inter-stage lane twiddles; 3 = 0.740 ms vs 0.772 (1), 0.757 (2), 0.771 (0)
+#endif
+#if TFP_HOIST & 1
+  cf w16r[10];
+#pragma unroll
+  for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
+#endif
+#if TFP_HOIST & 2
+  cf ltw[15];
+#pragma unroll
+  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+#endif
   const bool c_defer = S.c_defer != 0;
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
   {
@@ -387,6 +402,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       asm volatile("" : "+v"(oz));
       const float* __restrict__ win = S.window + oz;  // read per pass (registers: occupancy)
       cf z[16], Y[16];
+#if !(TFP_HOIST & 1)
+      cf w16r[10];
+#pragma unroll
+      for (int e = 0; e < 10; e++) w16r[e] = S.w16[e + oz];
+#endif
       if (ablate & 1) {
 #pragma unroll
         for (int n1 = 0; n1 < 16; n1++) { z[n1].x = win[n1 + L]; z[n1].y = (float)f; }
@@ -404,16 +424,20 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
 #pragma unroll
         for (int k = 0; k < 16; k++) Y[k] = z[k];
       } else {
-        dft16(S.w16, z, Y);
+        dft16(w16r, z, Y);
 #pragma unroll
+#if TFP_HOIST & 2
+        for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+#else
         for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
+#endif
         wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
         for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
         wave_sync();
 #pragma unroll
         for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
-        dft16(S.w16, z, Y);  // Y[k2] = Z[L + 16 k2]
+        dft16(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       }
       wave_sync();  // every lane has read its column of the square: W is free for |X|
       // |X[k]| of the 512-point real FFT, k = L + 16 k2, needs Z[256 - k]: for L >= 1 that is
