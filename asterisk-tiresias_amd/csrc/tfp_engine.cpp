@@ -69,6 +69,7 @@ struct tfp_engine {
   std::recursive_mutex mu;
   std::string err;
   std::map<int, DevBuf> tables;  // sample rate -> device DspTables
+  std::map<int, bool> tables_fixed8k;  // sample rate -> DspTables_fixed8k (kernel variant)
 
   // staging (append-only) rows of every clip ever added
   std::vector<Clip> clips;
@@ -111,11 +112,12 @@ int fail(tfp_engine* e, int code, const char* fmt, ...) {
     if (_st != hipSuccess) return fail((e), TFP_E_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
   } while (0)
 
-int ensure_tables(tfp_engine* e, int sr, const DspTables** out) {
+int ensure_tables(tfp_engine* e, int sr, const DspTables** out, bool* fixed8k = nullptr) {
   auto it = e->tables.find(sr);
   if (it == e->tables.end()) {
     DspTables host;
     if (!build_tables(sr, &host)) return fail(e, TFP_E_ARG, "bad sample rate %d", sr);
+    e->tables_fixed8k[sr] = DspTables_fixed8k(host);
     DevBuf& d = e->tables[sr];
     HIPCHK(e, d.reserve(sizeof(DspTables)));
     HIPCHK(e, hipMemcpyAsync(d.p, &host, sizeof host, hipMemcpyHostToDevice, e->stream));
@@ -123,6 +125,7 @@ int ensure_tables(tfp_engine* e, int sr, const DspTables** out) {
     it = e->tables.find(sr);
   }
   *out = it->second.as<DspTables>();
+  if (fixed8k) *fixed8k = e->tables_fixed8k[sr];
   return TFP_OK;
 }
 
@@ -156,7 +159,8 @@ int upload(tfp_engine* e, DevBuf& d, const void* h, size_t bytes, hipStream_t s 
 int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
                      int64_t* nframes_out, std::vector<int64_t>* foff_out) {
   const DspTables* T;
-  int rc = ensure_tables(e, sr, &T);
+  bool fx = false;
+  int rc = ensure_tables(e, sr, &T, &fx);
   if (rc) return rc;
   std::vector<int64_t> soff, foff;
   std::vector<int32_t> toff, tclip;
@@ -169,7 +173,7 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
-  HIPCHK(e, launch_fingerprint(T, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(T, fx, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->soff.as<int64_t>() + 1,
                                e->foff.as<int64_t>(),
                                e->toff.as<int32_t>(), e->tclip.as<int32_t>(), toff[nclips], e->micro.as<int32_t>(),
                                e->db.as<double>(), e->stream));
@@ -527,10 +531,11 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   if (!e || !p || !d_micro || (!d_pcm && p->nsamples)) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   const DspTables* T;
-  int rc = ensure_tables(e, p->sample_rate, &T);
+  bool fx = false;
+  int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, d_micro, d_db, s));
   return TFP_OK;
@@ -782,11 +787,12 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   HIPCHK(e, hipSetDevice(e->device));
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   const DspTables* T;
-  int rc = ensure_tables(e, p->sample_rate, &T);
+  bool fx = false;
+  int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(T, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
   std::vector<unsigned long long> keys;
@@ -877,7 +883,8 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   const int32_t na = (int32_t)act.size();
   if (!na) return TFP_OK;
   const DspTables* Tb;
-  if ((rc = ensure_tables(e, st->sr, &Tb))) return rc;
+  bool fx = false;
+  if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
   const int64_t F = tfp_frame_count(st->W);
   const int32_t tiles = (int32_t)((F + kFramesPerBlock - 1) / kFramesPerBlock);
   std::vector<int64_t> sb(na), se(na), fo(na + 1);
@@ -898,7 +905,7 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
     return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
-  HIPCHK(e, launch_fingerprint(Tb, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
+  HIPCHK(e, launch_fingerprint(Tb, fx, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
                                st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na],
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   std::vector<unsigned long long> keys;

@@ -558,20 +558,307 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   }
 }
 
-hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_sbeg,
+// ------------------------------------------------------------------------------------
+// 8 kHz specialization of fingerprint_kernel (the configs' rate; DspTables::fixed8k()):
+// the same arithmetic, with the filterbank slot schedule (36/16/8 bins, slot 2 = 2 real
+// filters, deferred logs) fixed at compile time, so the pass has no schedule branches, and:
+//   * tile and pass addressing in scalar registers (clip, tile and bounds are wave-uniform):
+//     interior passes issue their 16-byte PCM loads unconditionally from an SGPR base;
+//   * dft16's multiply by W16^4 = (0, -1) done as a swap (exact up to the sign of a zero,
+//     which no magnitude sees);
+//   * the real split's 0.5 folded into the filterbank: S = E + T = 2X exactly, the kernel
+//     stores N' = sqrt(|S|^2) = 2|X| and sums with half weights w/2, so every product
+//     (w/2)(2|X|) and every partial sum equals aubio's w|X| bit for bit (exact power-of-2
+//     scalings; proof in DESIGN.md §4); bins with 0 < |S|^2 < 2^-98 (where the scaling or the
+//     fast sqrt could round differently) take the spec sequence in a wave-uniform slow path;
+//   * filterbank products formed in pairs (v_pk_mul_f32 on the b128 halves), sums sequential.
+__device__ __forceinline__ float hadd(cf v) {  // v.x + v.y as one v_add_f32 (no pair repacking)
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(v.x), "v"(v.y));
+  return r;
+}
+
+// dft16 with the W16^4 = (0, -1) multiply as (y, -x).
+__device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], cf (&out)[16]) {
+  cf A[4][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 4; n2++) dft4(in[n2], in[4 + n2], in[8 + n2], in[12 + n2], A[n2][0], A[n2][1], A[n2][2], A[n2][3]);
+#pragma unroll
+  for (int n2 = 1; n2 < 4; n2++)
+#pragma unroll
+    for (int k1 = 1; k1 < 4; k1++) {
+      if (n2 * k1 == 4) A[n2][k1] = cf{A[n2][k1].y, -A[n2][k1].x};
+      else A[n2][k1] = cmul(A[n2][k1], w16[n2 * k1]);
+    }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; k1++) dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
+}
+
+// Filterbank sum over LEN bins (multiple of 4) with pair products: acc = ((acc + n0 w0) + n1 w1) ...
+template <int LEN>
+__device__ __forceinline__ float mel_sum(const float* __restrict__ N, const float* __restrict__ w, int st) {
+  float4 wv[LEN / 4], nv[LEN / 4];
+#pragma unroll
+  for (int i = 0; i < LEN / 4; i++) {
+    wv[i] = *reinterpret_cast<const float4*>(w + 64 * i);
+    nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * i);
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < LEN / 4; i++) {
+    const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
+    const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
+    acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_kernel(
+    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
+    const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
+    const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
+    float rare_thr) {
+  constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
+  const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
+  __shared__ __attribute__((aligned(16))) LdsTables S;
+  __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kWin; i += kBlockThreads) S.window[i] = T->window_s[i];
+  for (int i = tid; i < 15 * 16; i += kBlockThreads) {
+    const int k1 = 1 + i / 16, L = i % 16;
+    S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
+  }
+  for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
+  for (int i = tid; i < kBins; i += kBlockThreads) S.tw512[i] = cf{T->tw512_re[i], T->tw512_im[i]};
+  for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
+  for (int i = tid; i < 48; i += kBlockThreads) {
+    (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
+    (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
+  }
+  if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
+  if (tid < 16) S.logf[tid] = logf_table()[tid];
+  if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
+  for (int i = tid; i < T->ms_total; i += kBlockThreads) S.ms_w[i] = 0.5f * T->ms_w[i];  // exact: w/2
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  WaveLds& M = WL[wave];
+  cf* W = M.scratch[grp];
+  float* N = reinterpret_cast<float*>(W) + 16 * (grp & 1);  // |X| row (see fingerprint_kernel)
+  const int nwaves = gridDim.x * kBlockWaves;
+  const int maxbin = T->ms_maxbin;
+  const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
+  const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
+  cf w16r[10];
+#pragma unroll
+  for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
+  cf ltw[15];
+#pragma unroll
+  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+  {
+    const float lempty = aubio_log10_fast(0.f, S.logf);
+    for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
+      const int j = i % kFilters;
+      if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
+    }
+  }
+
+  // Wave-uniform tile state (scalar registers): clip, first frame, clip sample range.
+  struct Tile {
+    int c;
+    int64_t f0, s0, ns;
+  };
+  auto tile_of = [&](int b) {
+    Tile t;
+    t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
+    t.f0 = (int64_t)(b - toff[t.c]) * kWaveFrames;
+    t.s0 = sbeg[t.c];
+    t.ns = send[t.c] - t.s0;
+    return t;
+  };
+  // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
+  auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
+    const int16_t* clip = pcm + t.s0;
+    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
+    const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
+    if (interior) {
+      const int4* src = reinterpret_cast<const int4*>(clip + sb);
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (valid && chunk < kPassChunks) ? fetch_chunk_checked(clip, t.ns, sb + 8 * chunk) : make_int4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  int4 pf[kChunkRounds];
+  int b = blockIdx.x * kBlockWaves + wave;
+  Tile cur = tile_of(b < ntiles ? b : 0);
+  fetch(cur, 0, b < ntiles, pf);
+  for (; b < ntiles; b += nwaves) {
+    const int64_t nf = (cur.ns + kHop - 1) / kHop;
+    const int bn = b + nwaves;
+    const Tile nxt = bn < ntiles ? tile_of(bn) : cur;
+
+    for (int sub = 0; sub < 4; sub++) {
+      const int row = sub * 4 + grp;
+      wave_sync();  // the previous pass's readers of the scratch are done
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        if (chunk < kPassChunks)
+          *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+      }
+      if (sub < 3) fetch(cur, sub + 1, true, pf);
+      else fetch(nxt, 0, bn < ntiles, pf);
+      wave_sync();
+      const int16_t* hop0 = M.pcm + grp * kHopStride;
+      int oz = 0;
+      asm volatile("" : "+v"(oz));
+      const float* __restrict__ win = S.window + oz;
+      cf z[16], Y[16];
+#pragma unroll
+      for (int n1 = 0; n1 < 16; n1++) {
+        const int j = (32 * n1 + 2 * L + 256) & 511;
+        const int hsel = n1 < 8 ? 1 : 0;
+        const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
+        const cf wj = *reinterpret_cast<const cf*>(win + j);
+        z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wj;
+      }
+      dft16q(w16r, z, Y);
+#pragma unroll
+      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+      wave_sync();
+#pragma unroll
+      for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
+      wave_sync();
+#pragma unroll
+      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
+      dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
+      wave_sync();
+      {
+        cf P[16];
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) P[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+        uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) {
+          const int k = L + 16 * k2;
+          const cf own = Y[(16 - k2) & 15];
+          const cf Pk = cf{L == 0 ? own.x : P[k2].x, L == 0 ? own.y : P[k2].y};
+          const cf w = S.tw512[k + oz];
+          const cf E = addsub(Y[k2], Pk);
+          const cf O = subadd(Y[k2], Pk);
+          const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+          const cf Sv = E + Tt;  // = 2X exactly
+          const float x = hadd(Sv * Sv);
+          umin = min(umin, __builtin_bit_cast(uint32_t, x) - 1u);
+          N[k] = sqrtf_fast_cr(x);  // 2|X| for x = 0 and x >= 2^-98
+        }
+        if (__builtin_expect(__any(umin < rare_m1), 0)) {  // some 0 < |S|^2 < rare_thr
+          for (int k2 = 0; k2 < 16; k2++) {
+            const int k = L + 16 * k2;
+            cf Q = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+            if (L == 0) Q = Y[(16 - k2) & 15];
+            const cf w = S.tw512[k];
+            const cf E = addsub(Y[k2], Q);
+            const cf O = subadd(Y[k2], Q);
+            const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+            const cf Sv = E + Tt;
+            const float xs = Sv.x * Sv.x + Sv.y * Sv.y;
+            if (xs > 0.f && xs < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(Y[k2], Q, w));
+          }
+        }
+        if (L == 0) {
+          N[0] = 2.f * fabsf(Y[0].x + Y[0].y);
+          N[256] = 2.f * fabsf(Y[0].x - Y[0].y);
+        }
+      }
+      for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
+      wave_sync();
+      float* lrow = M.logs + row * kLogStride;
+      {
+        const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+        const float* wbase = S.ms_w + 4 * L + oz;
+        const float aC = mel_sum<LC>(N, wbase + S.ms_woff[2], stC);
+        const float aB = mel_sum<LB>(N, wbase + S.ms_woff[1], stB);
+        const float aA = mel_sum<LA>(N, wbase + S.ms_woff[0], stA);
+        const float lA = aubio_log10_fast(aA, S.logf);
+        const float lB = aubio_log10_fast(aB, S.logf);
+        lrow[fA] = lA;
+        lrow[fB] = lB;
+        if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+      }
+    }
+    wave_sync();
+    if (lane < 2 * kWaveFrames) {  // the deferred slot-2 logs: lane = (frame row, filter)
+      const int f = S.c_real[lane & 1];
+      if (f >= 0) {
+        float* p = M.logs + (lane >> 1) * kLogStride + f;
+        *p = aubio_log10_fast(*p, S.logf);
+      }
+    }
+    wave_sync();
+    if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
+      const int row = lane >> 1, cfi = lane & 1;
+      const int64_t f = cur.f0 + row;
+      if (f < nf) {
+        const float* lrow = M.logs + row * kLogStride;
+        float acc = 0.f;
+#pragma unroll 8
+        for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+        const double q = db_of_coef(acc);
+        const int64_t g = foff[cur.c] + f;
+        micro[2 * g + cfi] = micro_of_db(q);
+        if (db) db[2 * g + cfi] = q;
+      }
+    }
+    wave_sync();
+    cur = nxt;
+  }
+}
+
+bool DspTables_fixed8k(const DspTables& t) {
+  return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
+         t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
+}
+
+hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
                               const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
-  static int grid_cap = 0;
-  if (!grid_cap) {
+  static int grid_cap[2] = {0, 0};
+  // Test/A-B knobs, read per launch: TFP_GENERIC=1 runs the generic kernel at 8 kHz too;
+  // TFP_RARE_THR_LOG2=n (n >= -98) sends every bin with 0 < |S|^2 < 2^n through the spec-order
+  // slow path of the real split (any such threshold gives the same, exact, result).
+  const char* g = getenv("TFP_GENERIC");
+  const int v = (fixed8k && !(g && atoi(g))) ? 1 : 0;
+  const char* rt = getenv("TFP_RARE_THR_LOG2");
+  int rl = rt ? atoi(rt) : -98;
+  rl = rl < -98 ? -98 : (rl > 100 ? 100 : rl);
+  const float rare_thr = ldexpf(1.f, rl);
+  if (!grid_cap[v]) {
     int dev = 0, cus = 256, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, kBlockThreads, 0);
-    grid_cap = cus * (per > 0 ? per : 1);
+    if (v) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint8k_kernel, kBlockThreads, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, kBlockThreads, 0);
+    grid_cap[v] = cus * (per > 0 ? per : 1);
   }
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
-  const int grid = want < grid_cap ? want : grid_cap;
+  const int grid = want < grid_cap[v] ? want : grid_cap[v];
+  if (v) {
+    hipLaunchKernelGGL(fingerprint8k_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                       d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+    return hipGetLastError();
+  }
   static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production
   if (ablate < 0) {
     const char* a = getenv("TFP_ABLATE");

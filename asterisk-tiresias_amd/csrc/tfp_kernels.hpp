@@ -35,7 +35,10 @@ struct SynthSpecDev {
 // Fingerprint clips: clip c = samples [sbeg[c], send[c]) of d_pcm (for concatenated clips pass
 // send = soff + 1); frames of clip c are written from foff[c]; toff[nclips+1] are 16-frame tile
 // offsets (ntiles = toff[nclips]) and tclip[tile] the clip of each tile.
-hipError_t launch_fingerprint(const DspTables* d_tables, const int16_t* d_pcm, const int64_t* d_sbeg,
+// fixed8k: the tables' filterbank schedule is the 8 kHz one (DspTables_fixed8k), so the
+// specialized fingerprint8k_kernel runs; otherwise the generic fingerprint_kernel.
+bool DspTables_fixed8k(const DspTables& t);
+hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
                               const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s);
 

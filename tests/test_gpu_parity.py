@@ -256,3 +256,21 @@ def test_fp_handler_mirror_end_to_end(tmp_path, oracle, tfp_lib):
     assert fp.fp_search_fingerprint_info("ctx1", q, 3, 0.45, -1, -1) is None
     assert fp.fp_search_fingerprint_info("ctx1", str(tmp_path / "missing.wav"), 1, 0.45, -1, -1) is None
     assert fp.fp_term()
+
+
+@pytest.mark.parametrize("knob", [("TFP_GENERIC", "1"), ("TFP_RARE_THR_LOG2", "100")])
+def test_fingerprint_kernel_variants_bit_exact(engine, oracle, tfp_lib, knob):
+    """The 8 kHz kernel's other paths against the oracle: the generic kernel (TFP_GENERIC=1), and
+    the real split's spec-order slow path taken by every non-zero bin (TFP_RARE_THR_LOG2=100;
+    in production only bins with 0 < |S|^2 < 2^-98 take it)."""
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(6), 80000)
+    flat = np.concatenate([pcm.reshape(-1)] + list(_pcm_cases().values()))
+    lens = [80000] * 6 + [len(v) for v in _pcm_cases().values()]
+    off = np.concatenate([[0], np.cumsum(lens)])
+    micro, db = oracle.fingerprint_batch(flat, off, nthreads=8)
+    os.environ[knob[0]] = knob[1]
+    try:
+        fr = engine.fingerprint_batch(flat, off)
+    finally:
+        del os.environ[knob[0]]
+    _assert_frames_equal(fr, micro, db)
