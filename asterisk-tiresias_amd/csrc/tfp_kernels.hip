@@ -595,20 +595,31 @@ __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], 
 }
 
 // Filterbank sum over LEN bins (multiple of 4) with pair products: acc = ((acc + n0 w0) + n1 w1) ...
+#ifndef TFP8_MEL_BATCH
+#define TFP8_MEL_BATCH 9  // 4-bin groups whose loads are issued together (register pressure vs latency)
+#endif
 template <int LEN>
 __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const float* __restrict__ w, int st) {
-  float4 wv[LEN / 4], nv[LEN / 4];
-#pragma unroll
-  for (int i = 0; i < LEN / 4; i++) {
-    wv[i] = *reinterpret_cast<const float4*>(w + 64 * i);
-    nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * i);
-  }
+  constexpr int G = LEN / 4, B = TFP8_MEL_BATCH < G ? TFP8_MEL_BATCH : G;
   float acc = 0.f;
 #pragma unroll
-  for (int i = 0; i < LEN / 4; i++) {
-    const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
-    const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
-    acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+  for (int i0 = 0; i0 < G; i0 += B) {
+    float4 wv[B], nv[B];
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      if (i0 + i < G) {
+        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
+        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B; i++) {
+      if (i0 + i < G) {
+        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
+        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
+        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+      }
+    }
   }
   return acc;
 }
@@ -623,13 +634,22 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += kBlockThreads) S.window[i] = T->window_s[i];
+  // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
+  // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
+  cf* winr = reinterpret_cast<cf*>(S.window);
+  cf* twr = S.tw512;
+  for (int i = tid; i < 256; i += kBlockThreads) {
+    const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
+    const int j = (32 * n1 + 2 * L + 256) & 511;
+    winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
+    const int k = L + 16 * n1;
+    twr[i] = cf{T->tw512_re[k], T->tw512_im[k]};
+  }
   for (int i = tid; i < 15 * 16; i += kBlockThreads) {
     const int k1 = 1 + i / 16, L = i % 16;
     S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
   }
   for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
-  for (int i = tid; i < kBins; i += kBlockThreads) S.tw512[i] = cf{T->tw512_re[i], T->tw512_im[i]};
   for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
   for (int i = tid; i < 48; i += kBlockThreads) {
     (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
@@ -650,12 +670,30 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
+#ifndef TFP8_W16_REGS
+#define TFP8_W16_REGS 1  // dft16 twiddles held in registers (20 VGPRs) vs read per pass
+#endif
+#if TFP8_W16_REGS
   cf w16r[10];
 #pragma unroll
   for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
+#endif
+#ifndef TFP8_LTW_REGS
+#define TFP8_LTW_REGS 1  // inter-stage lane twiddles held in registers (30 VGPRs) vs read per pass
+#endif
+#if TFP8_LTW_REGS
   cf ltw[15];
 #pragma unroll
   for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+#endif
+#ifndef TFP8_WIN_REGS
+#define TFP8_WIN_REGS 0  // this lane's 16 window pairs held in registers (32 VGPRs) vs read per pass
+#endif
+#if TFP8_WIN_REGS
+  cf wreg[16];
+#pragma unroll
+  for (int n1 = 0; n1 < 16; n1++) wreg[n1] = winr[((n1 >> 1) * 16 + L) * 2 + (n1 & 1)];
+#endif
   {
     const float lempty = aubio_log10_fast(0.f, S.logf);
     for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
@@ -722,19 +760,35 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       const int16_t* hop0 = M.pcm + grp * kHopStride;
       int oz = 0;
       asm volatile("" : "+v"(oz));
-      const float* __restrict__ win = S.window + oz;
+#if !TFP8_WIN_REGS
+      cf wreg[16];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const float4 w4 = *reinterpret_cast<const float4*>(winr + (i * 16 + L) * 2 + oz);
+        wreg[2 * i] = cf{w4.x, w4.y};
+        wreg[2 * i + 1] = cf{w4.z, w4.w};
+      }
+#endif
+#if !TFP8_W16_REGS
+      cf w16r[10];
+#pragma unroll
+      for (int e = 0; e < 10; e++) w16r[e] = S.w16[e + oz];
+#endif
       cf z[16], Y[16];
 #pragma unroll
       for (int n1 = 0; n1 < 16; n1++) {
         const int j = (32 * n1 + 2 * L + 256) & 511;
         const int hsel = n1 < 8 ? 1 : 0;
         const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
-        const cf wj = *reinterpret_cast<const cf*>(win + j);
-        z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wj;
+        z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
       }
       dft16q(w16r, z, Y);
 #pragma unroll
+#if TFP8_LTW_REGS
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+#else
+      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
+#endif
       wave_sync();
 #pragma unroll
       for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
@@ -744,16 +798,22 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       wave_sync();
       {
-        cf P[16];
+        cf P[16], tw[16];
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) P[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+          const float4 t4 = *reinterpret_cast<const float4*>(twr + (i * 16 + L) * 2 + oz);
+          tw[2 * i] = cf{t4.x, t4.y};
+          tw[2 * i + 1] = cf{t4.z, t4.w};
+        }
         uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) {
           const int k = L + 16 * k2;
           const cf own = Y[(16 - k2) & 15];
           const cf Pk = cf{L == 0 ? own.x : P[k2].x, L == 0 ? own.y : P[k2].y};
-          const cf w = S.tw512[k + oz];
+          const cf w = tw[k2];
           const cf E = addsub(Y[k2], Pk);
           const cf O = subadd(Y[k2], Pk);
           const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
@@ -767,7 +827,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
             const int k = L + 16 * k2;
             cf Q = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
             if (L == 0) Q = Y[(16 - k2) & 15];
-            const cf w = S.tw512[k];
+            const cf w = twr[((k2 >> 1) * 16 + L) * 2 + (k2 & 1)];
             const cf E = addsub(Y[k2], Q);
             const cf O = subadd(Y[k2], Q);
             const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});

@@ -12,7 +12,7 @@ for fl in "$@"; do
   g=0
   for grp in "$G1" "$G2" "$G3"; do
     g=$((g+1))
-    timeout -k 10 240 rocprofv3 --pmc $grp --kernel-include-regex fingerprint_kernel --output-format csv -d gpurun_out/pmcc/v${v}g$g -o run -- python3 bench.py --no-match --no-cpu --steps 3 --warmup 1 > gpurun_out/pmcc/v${v}g$g.log 2>&1; rc=$?
+    timeout -k 10 240 rocprofv3 --pmc $grp --kernel-include-regex "fingerprint(8k)?_kernel" --output-format csv -d gpurun_out/pmcc/v${v}g$g -o run -- python3 bench.py --no-match --no-cpu --steps 3 --warmup 1 > gpurun_out/pmcc/v${v}g$g.log 2>&1; rc=$?
     echo "[$fl] group $g rc=$rc"; case $rc in 0) ;; *) exit $rc;; esac
   done
 done

@@ -4,10 +4,11 @@ The bench's first fingerprint_kernel dispatches are the configs[1] batch: `warmu
 `steps` timed launches, all with the C2 grid (later dispatches are DB-build / query batches).
 Usage: python scripts/tools/c2_dispatches.py TRACE.csv WARMUP STEPS OUT.csv"""
 import csv
+import re
 import sys
 
 trace, warm, steps, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
-rows = [r for r in csv.DictReader(open(trace)) if "fingerprint_kernel" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(trace)) if re.search(r"fingerprint(8k)?_kernel", r["Kernel_Name"])]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 rows = rows[: warm + steps]
 with open(out, "w") as f:

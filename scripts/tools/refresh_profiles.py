@@ -7,6 +7,7 @@ Usage: python scripts/tools/refresh_profiles.py R WARMUP STEPS KERNEL_BUILD_NOTE
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB), per MI355X_MICROARCH.md's gfx950
 correction for 16-B/lane streaming reads; averaged over the C2-sized dispatches."""
 import csv
+import re
 import json
 import os
 import shutil
@@ -30,7 +31,7 @@ subprocess.run([sys.executable, os.path.join(REPO, "scripts", "tools", "c2_dispa
 def pmc(counter):
     path = os.path.join(src, "%s_pmc_%s" % (R, counter), "run_counter_collection.csv")
     shutil.copy(path, os.path.join(dst, "pmc_%s.csv" % counter))
-    rows = [r for r in csv.DictReader(open(path)) if "fingerprint_kernel" in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(path)) if re.search(r"fingerprint(8k)?_kernel", r["Kernel_Name"])]
     grid = max(int(r["Grid_Size"]) for r in rows)
     vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == grid]
     return sum(vals) / len(vals)
@@ -40,7 +41,7 @@ fetch_kb, write_kb = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
 hbm = (2 * fetch_kb + write_kb) * 1024.0
 alg = 520 * C2_FRAMES
 out = {
-    "kernel": "fingerprint_kernel",
+    "kernel": "fingerprint8k_kernel",
     "frames_per_launch": C2_FRAMES,
     "hbm_bytes_per_launch": hbm,
     "fetch_size_kb_raw": fetch_kb,
