@@ -598,6 +598,27 @@ __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], 
 #ifndef TFP8_MEL_BATCH
 #define TFP8_MEL_BATCH 9  // 4-bin groups whose loads are issued together (register pressure vs latency)
 #endif
+// ... with the weights already in registers (loaded a phase early, TFP8_HOIST_W)
+template <int LEN>
+__device__ __forceinline__ float mel_sum_w(const float* __restrict__ N, const float4 (&wv)[LEN / 4], int st) {
+  float4 nv[LEN / 4];
+#pragma unroll
+  for (int i = 0; i < LEN / 4; i++) nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * i);
+  float acc = 0.f;
+#pragma unroll
+  for (int i = 0; i < LEN / 4; i++) {
+    const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
+    const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
+    acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+  }
+  return acc;
+}
+template <int LEN>
+__device__ __forceinline__ void load_w(const float* __restrict__ w, float4 (&wv)[LEN / 4]) {
+#pragma unroll
+  for (int i = 0; i < LEN / 4; i++) wv[i] = *reinterpret_cast<const float4*>(w + 64 * i);
+}
+
 template <int LEN>
 __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const float* __restrict__ w, int st) {
   constexpr int G = LEN / 4, B = TFP8_MEL_BATCH < G ? TFP8_MEL_BATCH : G;
@@ -624,6 +645,33 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
   return acc;
 }
 
+#ifndef TFP8_ABL
+#define TFP8_ABL 0  // timing-only phase ablation (wrong results): 1 FFT, 2 split, 4 mel, 8 logs, 16 tail
+#endif
+#ifndef TFP8_HOIST_TW
+#define TFP8_HOIST_TW 0  // 1: split twiddles read before the second-stage DFT16 (measured 0.604 vs 0.583 ms)
+#endif
+#ifndef TFP8_HOIST_W
+#define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
+#endif
+#ifndef TFP8_DPP
+#define TFP8_DPP 0  // split partners by DPP row_mirror (VALU) instead of ds_bpermute (LDS)
+#endif
+// Second-stage column of lane L. With TFP8_DPP the columns are numbered so that the partner
+// column 16 - k1 of every k1 other than 0 and 8 sits on the mirror lane 15 - L (row_mirror):
+// sigma = 0..7 on lanes 0..7, 9..15 on lanes 8..14, 8 on lane 15.
+__device__ __forceinline__ int col_of_lane(int L) {
+#if TFP8_DPP
+  return L < 8 ? L : (L == 15 ? 8 : L + 1);
+#else
+  return L;
+#endif
+}
+
+__device__ __forceinline__ float mirror16(float v) {  // lane 15 - L of the 16-lane row
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xf, 0xf, false));
+}
+
 __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
@@ -642,7 +690,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
     const int j = (32 * n1 + 2 * L + 256) & 511;
     winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
-    const int k = L + 16 * n1;
+    const int k = col_of_lane(L) + 16 * n1;
     twr[i] = cf{T->tw512_re[k], T->tw512_im[k]};
   }
   for (int i = tid; i < 15 * 16; i += kBlockThreads) {
@@ -663,6 +711,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  const int sg = col_of_lane(L);  // second-stage FFT column (= bins sg + 16 k2) of this lane
+#if TFP8_DPP
+  const bool selfpair = L == 0 || L == 15;
+  const int plane = selfpair ? L : 15 - L;  // partner lane in the 16-lane row
+#else
+  const int plane = (16 - L) & 15;
+#endif
   WaveLds& M = WL[wave];
   cf* W = M.scratch[grp];
   float* N = reinterpret_cast<float*>(W) + 16 * (grp & 1);  // |X| row (see fingerprint_kernel)
@@ -782,6 +837,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
         z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
       }
+      if constexpr (TFP8_ABL & 1) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) Y[k] = z[k];
+      } else {
       dft16q(w16r, z, Y);
 #pragma unroll
 #if TFP8_LTW_REGS
@@ -789,30 +848,71 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #else
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
 #endif
+      }
       wave_sync();
 #pragma unroll
       for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
       wave_sync();
 #pragma unroll
-      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
-      dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
-      wave_sync();
-      {
-        cf P[16], tw[16];
+      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + sg];
+      cf tw[16];
+#if TFP8_HOIST_TW
 #pragma unroll
-        for (int k2 = 0; k2 < 16; k2++) P[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+      for (int i = 0; i < 8; i++) {
+        const float4 t4 = *reinterpret_cast<const float4*>(twr + (i * 16 + L) * 2 + oz);
+        tw[2 * i] = cf{t4.x, t4.y};
+        tw[2 * i + 1] = cf{t4.z, t4.w};
+      }
+#endif
+      if constexpr (TFP8_ABL & 1) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) Y[k] = z[k];
+      } else {
+        dft16q(w16r, z, Y);  // Y[k2] = Z[sg + 16 k2]
+      }
+      wave_sync();
+      const float* wbase = S.ms_w + 4 * L + oz;
+      float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
+      if (TFP8_HOIST_W & 1) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
+      if (TFP8_HOIST_W & 2) load_w<LA>(wbase + S.ms_woff[0], wA);
+      if constexpr (TFP8_ABL & 2) {
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) N[sg + 16 * k2] = Y[k2].x + Y[k2].y;
+      } else {
+        // P[k2] = Z[256 - k]: Y[15 - k2] of the partner lane; column 0 (lane 0) pairs with its
+        // own Y[16 - k2] (Z[256] = Z[0]), column 8 (lane 15 under TFP8_DPP) with its own Y[15 - k2]
+#if TFP8_DPP
+        // (formed per bin inside the split loop: VALU, no latency to cover)
+#else
+        cf P[16];
+#pragma unroll
+        for (int k2 = 0; k2 < 16; k2++) {
+          const cf own = Y[(16 - k2) & 15];
+          P[k2] = cf{L == 0 ? own.x : partner16(Y[15 - k2].x), L == 0 ? own.y : partner16(Y[15 - k2].y)};
+        }
+#endif
+#if !TFP8_HOIST_TW
 #pragma unroll
         for (int i = 0; i < 8; i++) {
           const float4 t4 = *reinterpret_cast<const float4*>(twr + (i * 16 + L) * 2 + oz);
           tw[2 * i] = cf{t4.x, t4.y};
           tw[2 * i + 1] = cf{t4.z, t4.w};
         }
+#endif
         uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) {
-          const int k = L + 16 * k2;
-          const cf own = Y[(16 - k2) & 15];
-          const cf Pk = cf{L == 0 ? own.x : P[k2].x, L == 0 ? own.y : P[k2].y};
+          const int k = sg + 16 * k2;
+#if TFP8_DPP
+          cf y0 = Y[(16 - k2) & 15];
+          asm("" : "+v"(y0.x), "+v"(y0.y));  // a value, so the select below stays a v_cndmask
+          const cf own = L == 0 ? y0 : Y[15 - k2];
+          cf mir = cf{mirror16(Y[15 - k2].x), mirror16(Y[15 - k2].y)};
+          asm volatile("" : "+v"(mir.x), "+v"(mir.y));  // computed on every lane, then selected
+          const cf Pk = cf{selfpair ? own.x : mir.x, selfpair ? own.y : mir.y};
+#else
+          const cf Pk = P[k2];
+#endif
           const cf w = tw[k2];
           const cf E = addsub(Y[k2], Pk);
           const cf O = subadd(Y[k2], Pk);
@@ -823,9 +923,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           N[k] = sqrtf_fast_cr(x);  // 2|X| for x = 0 and x >= 2^-98
         }
         if (__builtin_expect(__any(umin < rare_m1), 0)) {  // some 0 < |S|^2 < rare_thr
+#if TFP8_DPP
+#pragma unroll  // (rolled, Y[] would be indexed dynamically)
+#endif
           for (int k2 = 0; k2 < 16; k2++) {
-            const int k = L + 16 * k2;
-            cf Q = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+            const int k = sg + 16 * k2;
+            cf Q = cf{__shfl(Y[15 - k2].x, plane, 16), __shfl(Y[15 - k2].y, plane, 16)};
             if (L == 0) Q = Y[(16 - k2) & 15];
             const cf w = twr[((k2 >> 1) * 16 + L) * 2 + (k2 & 1)];
             const cf E = addsub(Y[k2], Q);
@@ -844,14 +947,19 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
       wave_sync();
       float* lrow = M.logs + row * kLogStride;
-      {
+      if constexpr (TFP8_ABL & 4) {
+        lrow[fA] = N[L];
+        lrow[fB] = N[L + 16];
+        if (c_real) lrow[fC] = N[L + 32];
+      } else {
         const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
-        const float* wbase = S.ms_w + 4 * L + oz;
-        const float aC = mel_sum<LC>(N, wbase + S.ms_woff[2], stC);
-        const float aB = mel_sum<LB>(N, wbase + S.ms_woff[1], stB);
-        const float aA = mel_sum<LA>(N, wbase + S.ms_woff[0], stA);
-        const float lA = aubio_log10_fast(aA, S.logf);
-        const float lB = aubio_log10_fast(aB, S.logf);
+        if (!(TFP8_HOIST_W & 1)) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
+        if (!(TFP8_HOIST_W & 2)) load_w<LA>(wbase + S.ms_woff[0], wA);
+        const float aC = mel_sum_w<LC>(N, wC, stC);
+        const float aB = mel_sum_w<LB>(N, wB, stB);
+        const float aA = mel_sum_w<LA>(N, wA, stA);
+        const float lA = (TFP8_ABL & 8) ? aA : aubio_log10_fast(aA, S.logf);
+        const float lB = (TFP8_ABL & 8) ? aB : aubio_log10_fast(aB, S.logf);
         lrow[fA] = lA;
         lrow[fB] = lB;
         if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
@@ -866,7 +974,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
-    if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
+    if ((TFP8_ABL & 16) && lane < 2 * kWaveFrames) {
+      const int row = lane >> 1, cfi = lane & 1;
+      const int64_t f = cur.f0 + row;
+      if (f < nf) micro[2 * (foff[cur.c] + f) + cfi] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cfi]);
+    } else if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
       const int row = lane >> 1, cfi = lane & 1;
       const int64_t f = cur.f0 + row;
       if (f < nf) {
