@@ -654,6 +654,9 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
 #ifndef TFP8_HOIST_W
 #define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
 #endif
+#ifndef TFP8_PAIRSPLIT
+#define TFP8_PAIRSPLIT 1  // real split per conjugate pair (k, 256 - k) on one lane (see the split)
+#endif
 #ifndef TFP8_DPP
 #define TFP8_DPP 0  // split partners by DPP row_mirror (VALU) instead of ds_bpermute (LDS)
 #endif
@@ -690,8 +693,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
     const int j = (32 * n1 + 2 * L + 256) & 511;
     winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
+#if TFP8_PAIRSPLIT
+    // [k2][L] = (w512^k, w512^(256 - k)), k = L + 16 k2 (k2 < 8; lane 0 at k2 = 0: k = 128)
+    const int k2 = i >> 5, kk = (L == 0 && k2 == 0) ? 128 : L + 16 * k2, kp = 256 - kk;
+    twr[i] = (i & 1) ? cf{T->tw512_re[kp], T->tw512_im[kp]} : cf{T->tw512_re[kk], T->tw512_im[kk]};
+#else
     const int k = col_of_lane(L) + 16 * n1;
     twr[i] = cf{T->tw512_re[k], T->tw512_im[k]};
+#endif
   }
   for (int i = tid; i < 15 * 16; i += kBlockThreads) {
     const int k1 = 1 + i / 16, L = i % 16;
@@ -878,6 +887,51 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       if constexpr (TFP8_ABL & 2) {
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) N[sg + 16 * k2] = Y[k2].x + Y[k2].y;
+      } else if constexpr (TFP8_PAIRSPLIT) {
+        // Conjugate pairs on one lane: lane L (k2 < 8) owns bins k = L + 16 k2 and 256 - k, whose
+        // Z values are its Y[k2] and Y[15 - k2] of lane 16 - L (8 ds_bpermute pairs instead of 16).
+        // Column 0 pairs inside lane 0: (16 k2, 256 - 16 k2) for k2 = 1..7 and (128, 128) at k2 = 0;
+        // bins 0 and 256 come from Z[0] below. The spec's partner-side operands are exact sign
+        // flips of this side's: E' = (E.re, -E.im), O' = (-O.re, O.im) (a - b = -(b - a),
+        // a + b = b + a in IEEE), so E and O are formed once per pair; each bin then takes its
+        // own table twiddle (w512^k, w512^(256-k)) through the spec's T and S = E + T = 2X.
+        cf Pq[8];
+#pragma unroll
+        for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+        // bins 0 and 256 (lane 0) from Z[0], taken now so Y[0] is not kept alive
+        const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
+#pragma unroll
+        for (int k2 = 0; k2 < 8; k2++) {
+          cf own = Y[k2 == 0 ? 8 : 16 - k2];
+          asm("" : "+v"(own.x), "+v"(own.y));  // a value: the selects stay v_cndmask
+          cf y = Y[k2];
+          if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
+          const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
+          const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
+          const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
+          const cf E = addsub(y, p);
+          const cf O = subadd(y, p);
+          const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+          const cf Sv = E + Tt;
+          const cf O2 = cf{-O.x, O.y};
+          const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
+          const cf S2 = cf{E.x, -E.y} + T2;
+          const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
+          const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
+          float nk = sqrtf_fast_cr(x), nk2 = sqrtf_fast_cr(x2);
+          // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order instead
+          const uint32_t m = min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u);
+          if (__builtin_expect(__any(m < rare_m1), 0)) {
+            if (x > 0.f && x < rare_thr) nk = 2.f * __builtin_sqrtf(split_power(y, p, w));
+            if (x2 > 0.f && x2 < rare_thr) nk2 = 2.f * __builtin_sqrtf(split_power(p, y, w2));
+          }
+          N[k] = nk;
+          N[256 - k] = nk2;
+        }
+        if (L == 0) {
+          N[0] = n0;
+          N[256] = n256;
+        }
       } else {
         // P[k2] = Z[256 - k]: Y[15 - k2] of the partner lane; column 0 (lane 0) pairs with its
         // own Y[16 - k2] (Z[256] = Z[0]), column 8 (lane 15 under TFP8_DPP) with its own Y[15 - k2]
