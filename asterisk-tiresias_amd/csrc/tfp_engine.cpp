@@ -43,6 +43,22 @@ struct DevBuf {
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// Pinned host staging (one H2D copy per small call instead of one per array).
+struct HostBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~HostBuf() { if (p) (void)hipHostFree(p); }
+  hipError_t reserve(size_t n) {
+    if (n <= bytes) return hipSuccess;
+    if (p) { (void)hipHostFree(p); p = nullptr; bytes = 0; }
+    size_t want = n < 65536 ? 65536 : n;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) bytes = want;
+    return e;
+  }
+  template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
 struct Clip {
   std::string uuid;
   bool alive = true;
@@ -91,6 +107,13 @@ struct tfp_engine {
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
   DevBuf pcm, q, qoff, boxes, counts, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
   DevBuf soff, foff, toff, tclip, specs;
+  // small host calls: packed upload + the small-batch search workspace
+  HostBuf hstage;
+  DevBuf dstage;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_pending = false;
+  DevBuf small_work, small_bk;
+  ~tfp_engine() { if (stage_ev) (void)hipEventDestroy(stage_ev); }
 };
 
 namespace {
@@ -166,17 +189,51 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   std::vector<int32_t> toff, tclip;
   layout(offsets, nclips, soff, foff, toff, &tclip);
   const int64_t ns = soff[nclips], nf = foff[nclips];
-  if ((rc = upload(e, e->pcm, pcm + offsets[0], sizeof(int16_t) * ns))) return rc;
-  if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
-  if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
-  if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
-  if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
-  HIPCHK(e, launch_fingerprint(T, fx, e->pcm.as<int16_t>(), e->soff.as<int64_t>(), e->soff.as<int64_t>() + 1,
-                               e->foff.as<int64_t>(),
-                               e->toff.as<int32_t>(), e->tclip.as<int32_t>(), toff[nclips], e->micro.as<int32_t>(),
-                               e->db.as<double>(), e->stream));
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_pcm = al(sizeof(int16_t) * ns), b_so = al(sizeof(int64_t) * soff.size()),
+               b_fo = al(sizeof(int64_t) * foff.size()), b_to = al(sizeof(int32_t) * toff.size()),
+               b_tc = al(sizeof(int32_t) * tclip.size());
+  const size_t total = b_pcm + b_so + b_fo + b_to + b_tc;
+  const int16_t* d_pcm;
+  const int64_t *d_soff, *d_foff;
+  const int32_t *d_toff, *d_tclip;
+  if (total <= ((size_t)8 << 20)) {
+    // small call: pack every array into pinned staging, one H2D copy (batch-1 latency)
+    if (e->stage_pending) HIPCHK(e, hipEventSynchronize(e->stage_ev));  // previous copy done reading
+    HIPCHK(e, e->hstage.reserve(total));
+    HIPCHK(e, e->dstage.reserve(total));
+    char* h = e->hstage.as<char>();
+    if (ns) memcpy(h, pcm + offsets[0], sizeof(int16_t) * ns);
+    memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
+    memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
+    memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
+    memcpy(h + b_pcm + b_so + b_fo + b_to, tclip.data(), sizeof(int32_t) * tclip.size());
+    HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
+    if (!e->stage_ev) HIPCHK(e, hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
+    HIPCHK(e, hipEventRecord(e->stage_ev, e->stream));
+    e->stage_pending = true;
+    char* d = e->dstage.as<char>();
+    d_pcm = reinterpret_cast<const int16_t*>(d);
+    d_soff = reinterpret_cast<const int64_t*>(d + b_pcm);
+    d_foff = reinterpret_cast<const int64_t*>(d + b_pcm + b_so);
+    d_toff = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo);
+    d_tclip = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo + b_to);
+  } else {
+    if ((rc = upload(e, e->pcm, pcm + offsets[0], sizeof(int16_t) * ns))) return rc;
+    if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
+    if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
+    if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
+    if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
+    d_pcm = e->pcm.as<int16_t>();
+    d_soff = e->soff.as<int64_t>();
+    d_foff = e->foff.as<int64_t>();
+    d_toff = e->toff.as<int32_t>();
+    d_tclip = e->tclip.as<int32_t>();
+  }
+  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips],
+                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
   return TFP_OK;
@@ -320,6 +377,32 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
 
   std::vector<int64_t> qo(h_qoff, h_qoff + nq + 1);
   for (auto& v : qo) v -= h_qoff[0];
+  if (!d_keys_out && sc.coefs == 1 && nq >= 1 && nq <= kSmallQ && e->ncols > 0 && e->nrows > 0) {
+    // small batch (batch-1 latency): three kernels, one copy back, no host round trip between them
+    bool fits = true;
+    for (int32_t i = 0; i < nq; i++) fits &= qo[i + 1] - qo[i] <= 2048;  // counts bounded like the fp16 path
+    if (fits) {
+      SmallQueries sq;
+      memset(&sq, 0, sizeof sq);
+      sq.nq = nq;
+      for (int32_t i = 0; i <= nq; i++) sq.qoff[i] = qo[i];
+      const int32_t C = e->ncols, Cp4 = ((C + 3) / 4) * 4;
+      HIPCHK(e, e->small_work.reserve(sizeof(SmallWork)));
+      HIPCHK(e, e->small_bk.reserve((size_t)kKeyRange * Cp4));
+      SmallWork* w = e->small_work.as<SmallWork>();
+      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, e->m1s.as<int32_t>(), e->nrows,
+                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
+      struct { int32_t ku, bad; unsigned long long best[kSmallQ]; } h;
+      static_assert(offsetof(SmallWork, best) == offsetof(SmallWork, ku) + 8, "ku, bad, best contiguous");
+      HIPCHK(e, hipMemcpyAsync(&h, &w->ku, 8 + sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
+      HIPCHK(e, hipStreamSynchronize(s));
+      if (!h.bad) {
+        for (int32_t i = 0; i < nq; i++) keys[i] = h.best[i];
+        return TFP_OK;
+      }
+      // a key outside the vote range: redo the batch on the general path below
+    }
+  }
   if ((rc = upload(e, e->qoff, qo.data(), sizeof(int64_t) * qo.size(), s))) return rc;
   HIPCHK(e, e->boxes.reserve(sizeof(FrameBox) * (nf + 1)));
   HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), s));

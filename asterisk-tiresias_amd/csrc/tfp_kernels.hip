@@ -1363,6 +1363,117 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
   return hipGetLastError();
 }
 
+// ---- small-batch path (see tfp_kernels.hpp). Same sets and counts as key_hist + build_A/B +
+// vote_gemm: a query frame with trunc key k votes once for every clip with a row in k's box.
+__global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restrict__ q, SmallQueries sq,
+                                                          SearchConsts sc, SmallWork* __restrict__ w) {
+  __shared__ int32_t hist[kSmallQ][kKeyRange];
+  __shared__ int32_t scan[kKeyRange];
+  __shared__ int32_t bad;
+  const int t = threadIdx.x;
+  for (int i = t; i < kSmallQ * kKeyRange; i += blockDim.x) (&hist[0][0])[i] = 0;
+  if (t == 0) bad = 0;
+  if (t <= kSmallQ) w->best[t] = 0ull;
+  __syncthreads();
+  const int64_t nf = sq.qoff[sq.nq];
+  for (int64_t i = t; i < nf; i += blockDim.x) {
+    const double q1 = q[2 * i];
+    const double v1 = __builtin_isfinite(q1) ? q1 : 0.0;  // ast_json_real_get(NULL) = 0.0
+    const int32_t ki = (v1 > -2147483649.0 && v1 < 2147483648.0) ? (int32_t)v1 : INT32_MIN;  // :290
+    const double freq = (double)ki;
+    if (sc.has_low && freq < sc.thr_low) continue;   // :293-306
+    if (sc.has_high && freq > sc.thr_high) continue;
+    if (!__builtin_isfinite(freq - sc.tole) || !__builtin_isfinite(freq + sc.tole)) continue;
+    const int64_t idx = (int64_t)ki + kKeyOffset;
+    if (idx < 0 || idx >= kKeyRange) { bad = 1; continue; }
+    int qi = 0;
+    while (qi + 1 < sq.nq && sq.qoff[qi + 1] <= i) qi++;
+    atomicAdd(&hist[qi][idx], 1);
+  }
+  __syncthreads();
+  // compaction of the used keys (ascending key order) by a block-wide inclusive scan
+  int used = 0;
+  for (int qi = 0; qi < sq.nq; qi++) used |= hist[qi][t] != 0;
+  scan[t] = used;
+  __syncthreads();
+  for (int off = 1; off < kKeyRange; off <<= 1) {
+    const int v = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  if (used) {
+    const int kc = scan[t] - 1;
+    const double freq = (double)(t - kKeyOffset);
+    w->kb[kc][0] = fmt6_bound(freq - sc.tole);
+    w->kb[kc][1] = fmt6_bound(freq + sc.tole);
+    for (int qi = 0; qi < sq.nq; qi++) w->A[qi][kc] = hist[qi][t];
+  }
+  if (t == kKeyRange - 1) {
+    w->ku = scan[t];
+    w->bad = bad;
+  }
+}
+
+// One block per used key: clear the key's byte row, then mark the clips with a row in its box.
+__global__ __launch_bounds__(256) void small_mark_kernel(const SmallWork* __restrict__ w, uint8_t* __restrict__ bk,
+                                                         int32_t Cp, const int32_t* __restrict__ m1s, int64_t R,
+                                                         const int32_t* __restrict__ cols) {
+  const int kc = blockIdx.x;
+  if (kc >= w->ku || w->bad) return;
+  uint8_t* row = bk + (int64_t)kc * Cp;
+  for (int c = 4 * threadIdx.x; c < Cp; c += 4 * blockDim.x) *reinterpret_cast<uint32_t*>(row + c) = 0u;
+  __shared__ int64_t lohi[2];
+  if (threadIdx.x < 2) lohi[threadIdx.x] = threadIdx.x == 0 ? lower_bound_i32(m1s, R, w->kb[kc][0])
+                                                              : upper_bound_i32(m1s, R, w->kb[kc][1]);
+  __syncthreads();
+  for (int64_t r = lohi[0] + threadIdx.x; r < lohi[1]; r += blockDim.x) row[cols[r]] = 1;
+}
+
+// Clip-parallel scores of every query; the per-query max of score << 32 | tie key (a later uuid
+// wins a tie, as SQLite's ORDER BY count(*) DESC returns it).
+__global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__ w, const uint8_t* __restrict__ bk,
+                                                         int32_t Cp, int32_t C, int32_t nq,
+                                                         const int32_t* __restrict__ tiekey) {
+  __shared__ int32_t A[kSmallQ][kKeyRange];
+  const int ku = w->ku;
+  if (w->bad || ku == 0) return;  // no used key: every frame ignored -> NOTFOUND (best stays 0)
+  for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = w->A[i / ku][i % ku];
+  __syncthreads();
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  int32_t sc[kSmallQ];
+#pragma unroll
+  for (int qi = 0; qi < kSmallQ; qi++) sc[qi] = 0;
+  if (c < C) {
+    for (int kc = 0; kc < ku; kc++) {
+      if (bk[(int64_t)kc * Cp + c]) {
+#pragma unroll
+        for (int qi = 0; qi < kSmallQ; qi++) sc[qi] += qi < nq ? A[qi][kc] : 0;
+      }
+    }
+  }
+  const unsigned tk = c < C ? (unsigned)tiekey[c] : 0u;
+  for (int qi = 0; qi < nq; qi++) {
+    unsigned long long key = sc[qi] > 0 ? (((unsigned long long)(unsigned)sc[qi] << 32) | tk) : 0ull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const unsigned long long o = __shfl_xor(key, off, 64);
+      key = o > key ? o : key;
+    }
+    if ((threadIdx.x & 63) == 0 && key) atomicMax(&w->best[qi], key);
+  }
+}
+
+hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
+                               uint8_t* d_bk, int32_t Cp, const int32_t* m1s, int64_t R, const int32_t* cols,
+                               int32_t C, const int32_t* d_tiekey, hipStream_t s) {
+  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || (Cp & 3)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, d_work);
+  hipLaunchKernelGGL(small_mark_kernel, dim3(kKeyRange), dim3(256), 0, s, d_work, d_bk, Cp, m1s, R, cols);
+  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey);
+  return hipGetLastError();
+}
+
 // ---- general path (any coefs / tolerance): one wave per query, frames in order; per frame the
 // rows with max1 in [L1, U1] (binary search on the sorted index) filtered by the max2 box; each
 // clip counts once per frame (stamp), i.e. the per-frame GROUP BY audio_uuid of :353.

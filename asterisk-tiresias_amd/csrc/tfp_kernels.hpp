@@ -63,6 +63,27 @@ hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, co
                           int32_t Ku, int32_t Kp, _Float16* d_Bt, hipStream_t s);
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
+// ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
+// no host round trip between the stages. One block builds every query's per-key frame counts,
+// compacts the used keys and their "%f" boxes; one block per used key marks the clips with a row
+// in its box (a byte per clip, key-major); a clip-parallel pass scores and arg-maxes.
+constexpr int kSmallQ = 8;
+struct SmallQueries {
+  int32_t nq;
+  int32_t pad;
+  int64_t qoff[kSmallQ + 1];  // frame offsets of the queries in d_q (relative)
+};
+struct SmallWork {              // device workspace of the small path
+  int32_t A[kSmallQ][kKeyRange];  // A[q][kc]: query q's frames whose key is the kc-th used key
+  int64_t kb[kKeyRange][2];       // "%f" box [lo, hi] (micro-units) of the kc-th used key
+  int32_t ku;                     // used keys
+  int32_t bad;                    // a key outside [-512, 511]: the caller redoes the batch generally
+  unsigned long long best[kSmallQ + 1];  // per query score << 32 | tie key; best[kSmallQ] unused
+};
+hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
+                               uint8_t* d_bk /*[kKeyRange][Cp] bytes*/, int32_t Cp, const int32_t* m1s, int64_t R,
+                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s);
+
 hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
                        const int32_t* m2s, const int32_t* cols, int64_t R, const int32_t* d_tiekey, int32_t Cp,
                        int32_t* d_stamp, int32_t* d_score, unsigned long long* d_best, hipStream_t s);

@@ -274,3 +274,36 @@ def test_fingerprint_kernel_variants_bit_exact(engine, oracle, tfp_lib, knob):
     finally:
         del os.environ[knob[0]]
     _assert_frames_equal(fr, micro, db)
+
+
+@pytest.mark.parametrize("tol,low,high", [(0.001, -1, -1), (0.1, 100, 3400), (0.45, -1, -1), (-1.0, 300, -1)])
+def test_search_small_batches_equal_general(engine, oracle, tfp_lib, tol, low, high):
+    """Batches of <= 8 queries take the small-batch kernels (tfp_kernels.hpp, kSmallQ); a batch of
+    24 takes the vote GEMM. Both must give the same (uuid, match_count, frame_count)."""
+    _build_db(engine, oracle, tfp_lib, 120, 12)
+    qpcm = _queries(tfp_lib, 24, 120, 12, 5)
+    n = qpcm.shape[1]
+    p = tfp_lib.params(1, tol, low, high)
+    big, fb = engine.search_pcm_batch(qpcm.reshape(-1), np.arange(25) * n, p)
+    small, fs = [], []
+    for lo, hi in ((0, 1), (1, 4), (4, 12), (12, 13), (13, 21), (21, 24)):
+        r, f = engine.search_pcm_batch(qpcm[lo:hi].reshape(-1), np.arange(hi - lo + 1) * n, p)
+        small += r
+        fs += list(f)
+    key = lambda r: None if r is None else (r["audio_uuid"], r["match_count"])  # noqa: E731
+    assert [key(r) for r in small] == [key(r) for r in big]
+    assert list(fs) == list(fb)
+    if low < 0 and high < 0:
+        assert any(r is not None for r in big)
+
+
+def test_search_small_out_of_range_key_falls_back(engine, tfp_lib):
+    """A query key outside the vote range (|k| > 511, impossible for real fingerprints) sends a
+    small batch to the general scan path, as key_hist does for large batches."""
+    engine.index_clear()
+    engine.index_add("00000000-0000-4000-8000-000000000001", np.array([1000000000, 24000000], np.int32),
+                     np.array([0, 0], np.int32))
+    engine.index_add("00000000-0000-4000-8000-000000000002", np.array([24000100], np.int32), np.array([0], np.int32))
+    r, fc = engine.search(_frames_from_q([1000.0005, 24.2], [0.0, 0.0]), tfp_lib.params(1, 0.001))
+    assert r is not None and r["audio_uuid"].endswith("001") and r["match_count"] == 2 and fc == 2
+    engine.index_clear()
