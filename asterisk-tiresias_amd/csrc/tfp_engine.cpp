@@ -112,7 +112,8 @@ struct tfp_engine {
   DevBuf dstage;
   hipEvent_t stage_ev = nullptr;
   bool stage_pending = false;
-  DevBuf small_work, small_bk;
+  DevBuf small_work, small_bk, key_rng;
+  uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
   ~tfp_engine() { if (stage_ev) (void)hipEventDestroy(stage_ev); }
 };
 
@@ -388,10 +389,19 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       for (int32_t i = 0; i <= nq; i++) sq.qoff[i] = qo[i];
       const int32_t C = e->ncols, Cp4 = ((C + 3) / 4) * 4;
       HIPCHK(e, e->small_work.reserve(sizeof(SmallWork)));
-      HIPCHK(e, e->small_bk.reserve((size_t)kKeyRange * Cp4));
+      const size_t bk_bytes = (size_t)kKeyRange * Cp4;
+      if (bk_bytes > e->small_bk.bytes) {
+        HIPCHK(e, e->small_bk.reserve(bk_bytes));
+        e->small_epoch = 255;  // force a clear below
+      }
+      if (e->small_epoch == 255) {  // stamps wrap: clear once every 255 calls
+        HIPCHK(e, hipMemsetAsync(e->small_bk.p, 0, e->small_bk.bytes, s));
+        e->small_epoch = 0;
+      }
+      const uint8_t epoch = ++e->small_epoch;
       SmallWork* w = e->small_work.as<SmallWork>();
-      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, e->m1s.as<int32_t>(), e->nrows,
-                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
+      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->m1s.as<int32_t>(),
+                                    e->nrows, e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
       struct { int32_t ku, bad; unsigned long long best[kSmallQ]; } h;
       static_assert(offsetof(SmallWork, best) == offsetof(SmallWork, ku) + 8, "ku, bad, best contiguous");
       HIPCHK(e, hipMemcpyAsync(&h, &w->ku, 8 + sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
@@ -448,8 +458,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * Kp));
         HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), Ku, Kp, e->A.as<_Float16>(), s));
         HIPCHK(e, hipMemsetAsync(e->Bt.p, 0, sizeof(_Float16) * (size_t)Cp * Kp, s));
+        HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * Ku));
         HIPCHK(e, launch_build_B(e->m1s.as<int32_t>(), R, e->cols.as<int32_t>(), e->kbounds.as<int64_t>(), Ku, Kp,
-                                 e->Bt.as<_Float16>(), s));
+                                 e->key_rng.as<int64_t>(), e->Bt.as<_Float16>(), s));
         HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, Kp, e->tiekey.as<int32_t>(),
                                    e->best.as<unsigned long long>(), s));
         done = true;

@@ -1288,18 +1288,32 @@ hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const
   return hipGetLastError();
 }
 
-__global__ void build_B_kernel(const int32_t* __restrict__ m1s, int64_t R, const int32_t* __restrict__ cols,
-                               const int64_t* __restrict__ kb, int32_t Kp, _Float16* __restrict__ Bt) {
-  const int col = blockIdx.x;
-  const int64_t lo = lower_bound_i32(m1s, R, kb[2 * col]);
-  const int64_t hi = upper_bound_i32(m1s, R, kb[2 * col + 1]);
-  for (int64_t r = lo + threadIdx.x; r < hi; r += blockDim.x) Bt[(int64_t)cols[r] * Kp + col] = (_Float16)1.0f;
+// Row range [lo, hi) of each used key's box in the m1-sorted index (one thread per key).
+__global__ void key_ranges_kernel(const int32_t* __restrict__ m1s, int64_t R, const int64_t* __restrict__ kb, int32_t Ku,
+                                  int64_t* __restrict__ rng) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= Ku) return;
+  rng[2 * k] = lower_bound_i32(m1s, R, kb[2 * k]);
+  rng[2 * k + 1] = upper_bound_i32(m1s, R, kb[2 * k + 1]);
+}
+
+// Bt[clip][key] = 1 for every row in the key's box. The rows of all keys are spread over the
+// whole grid (a box can hold a large share of the index when fingerprints concentrate).
+__global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
+                                                      int32_t Ku, int32_t Kp, _Float16* __restrict__ Bt) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < Ku; k++) {
+    const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
+    for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride)
+      Bt[(int64_t)cols[r] * Kp + k] = (_Float16)1.0f;
+  }
 }
 
 hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds, int32_t Ku,
-                          int32_t Kp, _Float16* d_Bt, hipStream_t s) {
+                          int32_t Kp, int64_t* d_rng, _Float16* d_Bt, hipStream_t s) {
   if (Ku <= 0) return hipSuccess;
-  hipLaunchKernelGGL(build_B_kernel, dim3(Ku), dim3(256), 0, s, m1s, R, cols, d_kbounds, Kp, d_Bt);
+  hipLaunchKernelGGL(key_ranges_kernel, dim3((Ku + 63) / 64), dim3(64), 0, s, m1s, R, d_kbounds, Ku, d_rng);
+  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, Ku, Kp, d_Bt);
   return hipGetLastError();
 }
 
@@ -1366,7 +1380,8 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
 // ---- small-batch path (see tfp_kernels.hpp). Same sets and counts as key_hist + build_A/B +
 // vote_gemm: a query frame with trunc key k votes once for every clip with a row in k's box.
 __global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restrict__ q, SmallQueries sq,
-                                                          SearchConsts sc, SmallWork* __restrict__ w) {
+                                                          SearchConsts sc, const int32_t* __restrict__ m1s, int64_t R,
+                                                          SmallWork* __restrict__ w) {
   __shared__ int32_t hist[kSmallQ][kKeyRange];
   __shared__ int32_t scan[kKeyRange];
   __shared__ int32_t bad;
@@ -1405,8 +1420,8 @@ __global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restri
   if (used) {
     const int kc = scan[t] - 1;
     const double freq = (double)(t - kKeyOffset);
-    w->kb[kc][0] = fmt6_bound(freq - sc.tole);
-    w->kb[kc][1] = fmt6_bound(freq + sc.tole);
+    w->kb[kc][0] = lower_bound_i32(m1s, R, fmt6_bound(freq - sc.tole));  // the box's row range
+    w->kb[kc][1] = upper_bound_i32(m1s, R, fmt6_bound(freq + sc.tole));
     for (int qi = 0; qi < sq.nq; qi++) w->A[qi][kc] = hist[qi][t];
   }
   if (t == kKeyRange - 1) {
@@ -1415,26 +1430,25 @@ __global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restri
   }
 }
 
-// One block per used key: clear the key's byte row, then mark the clips with a row in its box.
+// Stamp the clips with a row in each used key's box: bk[kc][clip] = epoch (a per-call byte, so
+// rows of earlier calls never need clearing). Every key's rows are spread over the whole grid.
 __global__ __launch_bounds__(256) void small_mark_kernel(const SmallWork* __restrict__ w, uint8_t* __restrict__ bk,
-                                                         int32_t Cp, const int32_t* __restrict__ m1s, int64_t R,
-                                                         const int32_t* __restrict__ cols) {
-  const int kc = blockIdx.x;
-  if (kc >= w->ku || w->bad) return;
-  uint8_t* row = bk + (int64_t)kc * Cp;
-  for (int c = 4 * threadIdx.x; c < Cp; c += 4 * blockDim.x) *reinterpret_cast<uint32_t*>(row + c) = 0u;
-  __shared__ int64_t lohi[2];
-  if (threadIdx.x < 2) lohi[threadIdx.x] = threadIdx.x == 0 ? lower_bound_i32(m1s, R, w->kb[kc][0])
-                                                              : upper_bound_i32(m1s, R, w->kb[kc][1]);
-  __syncthreads();
-  for (int64_t r = lohi[0] + threadIdx.x; r < lohi[1]; r += blockDim.x) row[cols[r]] = 1;
+                                                         int32_t Cp, const int32_t* __restrict__ cols, uint8_t epoch) {
+  if (w->bad) return;
+  const int ku = w->ku;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int kc = 0; kc < ku; kc++) {
+    uint8_t* row = bk + (int64_t)kc * Cp;
+    const int64_t lo = w->kb[kc][0], hi = w->kb[kc][1];
+    for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride) row[cols[r]] = epoch;
+  }
 }
 
 // Clip-parallel scores of every query; the per-query max of score << 32 | tie key (a later uuid
 // wins a tie, as SQLite's ORDER BY count(*) DESC returns it).
 __global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__ w, const uint8_t* __restrict__ bk,
                                                          int32_t Cp, int32_t C, int32_t nq,
-                                                         const int32_t* __restrict__ tiekey) {
+                                                         const int32_t* __restrict__ tiekey, uint8_t epoch) {
   __shared__ int32_t A[kSmallQ][kKeyRange];
   const int ku = w->ku;
   if (w->bad || ku == 0) return;  // no used key: every frame ignored -> NOTFOUND (best stays 0)
@@ -1446,7 +1460,7 @@ __global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__
   for (int qi = 0; qi < kSmallQ; qi++) sc[qi] = 0;
   if (c < C) {
     for (int kc = 0; kc < ku; kc++) {
-      if (bk[(int64_t)kc * Cp + c]) {
+      if (bk[(int64_t)kc * Cp + c] == epoch) {
 #pragma unroll
         for (int qi = 0; qi < kSmallQ; qi++) sc[qi] += qi < nq ? A[qi][kc] : 0;
       }
@@ -1465,12 +1479,13 @@ __global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__
 }
 
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk, int32_t Cp, const int32_t* m1s, int64_t R, const int32_t* cols,
-                               int32_t C, const int32_t* d_tiekey, hipStream_t s) {
-  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || (Cp & 3)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, d_work);
-  hipLaunchKernelGGL(small_mark_kernel, dim3(kKeyRange), dim3(256), 0, s, d_work, d_bk, Cp, m1s, R, cols);
-  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey);
+                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int32_t* m1s, int64_t R,
+                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s) {
+  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, m1s, R, d_work);
+  hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_work, d_bk, Cp, cols, epoch);
+  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey,
+                     epoch);
   return hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t
 hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, int32_t Ku, int32_t Kp,
                           _Float16* d_A, hipStream_t s);
 hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds /*[Ku][2]*/,
-                          int32_t Ku, int32_t Kp, _Float16* d_Bt, hipStream_t s);
+                          int32_t Ku, int32_t Kp, int64_t* d_rng /*[Ku][2] scratch*/, _Float16* d_Bt, hipStream_t s);
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
@@ -75,13 +75,15 @@ struct SmallQueries {
 };
 struct SmallWork {              // device workspace of the small path
   int32_t A[kSmallQ][kKeyRange];  // A[q][kc]: query q's frames whose key is the kc-th used key
-  int64_t kb[kKeyRange][2];       // "%f" box [lo, hi] (micro-units) of the kc-th used key
+  int64_t kb[kKeyRange][2];       // row range [lo, hi) in the m1-sorted index of the kc-th used key's box
   int32_t ku;                     // used keys
   int32_t bad;                    // a key outside [-512, 511]: the caller redoes the batch generally
   unsigned long long best[kSmallQ + 1];  // per query score << 32 | tie key; best[kSmallQ] unused
 };
+// d_bk: [kKeyRange][Cp] bytes stamped with `epoch` (1..255, a new one per call; the caller clears
+// d_bk when the epoch wraps).
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk /*[kKeyRange][Cp] bytes*/, int32_t Cp, const int32_t* m1s, int64_t R,
+                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int32_t* m1s, int64_t R,
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s);
 
 hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
