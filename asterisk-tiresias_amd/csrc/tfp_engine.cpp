@@ -415,27 +415,30 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   }
   if ((rc = upload(e, e->qoff, qo.data(), sizeof(int64_t) * qo.size(), s))) return rc;
   HIPCHK(e, e->boxes.reserve(sizeof(FrameBox) * (nf + 1)));
-  HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), s));
   const int32_t Qp = ((nq + 127) / 128) * 128;
-  HIPCHK(e, e->best.reserve(sizeof(unsigned long long) * Qp));
-  HIPCHK(e, hipMemsetAsync(e->best.p, 0, sizeof(unsigned long long) * Qp, s));
+  // one buffer: the vote path's key mask (32 words), max count (1), pad (1), then best[Qp] (u64);
+  // zeroed by prep_boxes
+  constexpr int kMaskWords = kKeyRange / 32, kMiscWords = kMaskWords + 2;
+  const int32_t nzero = kMiscWords + 2 * Qp;
+  HIPCHK(e, e->best.reserve(sizeof(uint32_t) * nzero));
+  uint32_t* d_mask = e->best.as<uint32_t>();
+  int32_t* d_max = reinterpret_cast<int32_t*>(d_mask + kMaskWords);
+  unsigned long long* d_best = reinterpret_cast<unsigned long long*>(d_mask + kMiscWords);
+  HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   const int32_t C = e->ncols;
   const int64_t R = e->nrows;
+  int64_t max_frames = 0;
+  for (int32_t i = 0; i < nq; i++) max_frames = std::max<int64_t>(max_frames, qo[i + 1] - qo[i]);
 
   bool done = false;
-  if (sc.coefs == 1 && C > 0 && R > 0) {
+  if (sc.coefs == 1 && C > 0 && R > 0 && max_frames < 16384) {  // packed scores exact below 16384 frames
     // vote-matrix path
     HIPCHK(e, e->counts.reserve(sizeof(int32_t) * (size_t)nq * kKeyRange));
-    HIPCHK(e, e->mask.reserve(sizeof(uint32_t) * (kKeyRange / 32) + sizeof(int32_t)));
-    HIPCHK(e, hipMemsetAsync(e->counts.p, 0, sizeof(int32_t) * (size_t)nq * kKeyRange, s));
-    HIPCHK(e, hipMemsetAsync(e->mask.p, 0, sizeof(uint32_t) * (kKeyRange / 32) + sizeof(int32_t), s));
-    uint32_t* d_mask = e->mask.as<uint32_t>();
-    int32_t* d_max = reinterpret_cast<int32_t*>(d_mask + kKeyRange / 32);
     HIPCHK(e, launch_key_hist(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, e->counts.as<int32_t>(), d_mask, d_max, s));
-    uint32_t hmask[kKeyRange / 32 + 1];
+    uint32_t hmask[kMaskWords + 1];
     HIPCHK(e, hipMemcpyAsync(hmask, d_mask, sizeof hmask, hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
-    const int32_t maxcount = (int32_t)hmask[kKeyRange / 32];
+    const int32_t maxcount = (int32_t)hmask[kMaskWords];
     if (maxcount <= 2048) {  // counts exact in fp16
       std::vector<int32_t> keycols;
       std::vector<int64_t> kb;
@@ -450,7 +453,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       if (Ku == 0) {
         done = true;  // every frame ignored: no rows inserted -> NOTFOUND
       } else {
-        const int32_t Kp = ((Ku + 15) / 16) * 16;
+        const int32_t Kp = ((Ku + 1 + 15) / 16) * 16;  // + the column-index entry (packed argmax)
         const int32_t Cp = ((C + 31) / 32) * 32;
         if ((rc = upload(e, e->keycols, keycols.data(), sizeof(int32_t) * Ku, s))) return rc;
         if ((rc = upload(e, e->kbounds, kb.data(), sizeof(int64_t) * kb.size(), s))) return rc;
@@ -459,10 +462,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), Ku, Kp, e->A.as<_Float16>(), s));
         HIPCHK(e, hipMemsetAsync(e->Bt.p, 0, sizeof(_Float16) * (size_t)Cp * Kp, s));
         HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * Ku));
-        HIPCHK(e, launch_build_B(e->m1s.as<int32_t>(), R, e->cols.as<int32_t>(), e->kbounds.as<int64_t>(), Ku, Kp,
+        HIPCHK(e, launch_build_B(e->m1s.as<int32_t>(), R, e->cols.as<int32_t>(), e->kbounds.as<int64_t>(), Ku, Kp, Cp,
                                  e->key_rng.as<int64_t>(), e->Bt.as<_Float16>(), s));
-        HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, Kp, e->tiekey.as<int32_t>(),
-                                   e->best.as<unsigned long long>(), s));
+        HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, Kp, e->tiekey.as<int32_t>(), d_best, s));
         done = true;
       }
     }
@@ -480,14 +482,14 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       HIPCHK(e, hipMemsetAsync(e->score.p, 0, sizeof(int32_t) * n * Cp, s));
       HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), (int32_t)q0, n, e->m1s.as<int32_t>(),
                             e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->tiekey.as<int32_t>(), Cp,
-                            e->stamp.as<int32_t>(), e->score.as<int32_t>(), e->best.as<unsigned long long>(), s));
+                            e->stamp.as<int32_t>(), e->score.as<int32_t>(), d_best, s));
     }
   }
   if (d_keys_out) {
-    HIPCHK(e, hipMemcpyAsync(d_keys_out, e->best.p, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
     return TFP_OK;
   }
-  if (nq) HIPCHK(e, hipMemcpyAsync(keys.data(), e->best.p, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
+  if (nq) HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
   HIPCHK(e, hipStreamSynchronize(s));
   return TFP_OK;
 }

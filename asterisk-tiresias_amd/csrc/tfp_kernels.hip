@@ -1183,7 +1183,11 @@ hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, 
 
 // ------------------------------------------------------------------------------------
 // Search: per query frame box (fp_handler.c:287-351).
-__global__ void prep_boxes_kernel(const double* __restrict__ q, int64_t n, SearchConsts sc, FrameBox* __restrict__ boxes) {
+__global__ void prep_boxes_kernel(const double* __restrict__ q, int64_t n, SearchConsts sc, FrameBox* __restrict__ boxes,
+                                  uint32_t* __restrict__ zero_words, int32_t nzero) {
+  // the vote path's key mask, max count and per-query best keys start at 0 (read by later kernels)
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nzero; i += (int64_t)gridDim.x * blockDim.x)
+    zero_words[i] = 0u;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const double q1 = q[2 * i], q2 = q[2 * i + 1];
     const double v1 = __builtin_isfinite(q1) ? q1 : 0.0;  // ast_json_real_get(NULL) = 0.0
@@ -1219,52 +1223,68 @@ __global__ void prep_boxes_kernel(const double* __restrict__ q, int64_t n, Searc
   }
 }
 
-hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, hipStream_t s) {
-  if (nframes <= 0) return hipSuccess;
-  int64_t g = (nframes + 255) / 256;
+hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, uint32_t* zero_words,
+                             int32_t nzero, hipStream_t s) {
+  if (nframes <= 0 && nzero <= 0) return hipSuccess;
+  int64_t g = ((nframes > nzero ? nframes : nzero) + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(prep_boxes_kernel, dim3((unsigned)g), dim3(256), 0, s, d_q, nframes, sc, boxes);
+  hipLaunchKernelGGL(prep_boxes_kernel, dim3((unsigned)g), dim3(256), 0, s, d_q, nframes, sc, boxes, zero_words, nzero);
   return hipGetLastError();
 }
+
+constexpr int kVoteColsPerBlock = 1024;  // clips per vote_gemm block (a power of 2)
+constexpr float kVoteScale = 1024.f;      // Bt's box entries: acc = 1024 * score + column-in-chunk
 
 // ---- coefs = 1: vote matrix. score[q][clip] = sum_k N[q][k] * B[k][clip], where N counts the
 // query's non-ignored frames with trunc key k and B[k][clip] = 1 iff the clip has a row in
 // [fmt6(k - tol), fmt6(k + tol)] — exactly the per-frame "group by audio_uuid" hit count.
-__global__ void key_hist_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
-                                int32_t* __restrict__ counts, uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
-  __shared__ uint32_t smask[kKeyRange / 32];
+// One block per query (frames of a query are contiguous): the per-key frame counts in LDS, written
+// out as the query's whole row (no memset, no global atomics on counts); used keys ORed into the
+// batch mask; counts above 1024 reported through maxc (fp16 holds counts up to 2048 exactly).
+__global__ __launch_bounds__(256) void key_hist_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff,
+                                                       int32_t nq, int32_t* __restrict__ counts,
+                                                       uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
+  __shared__ int32_t hist[kKeyRange];
   __shared__ int32_t smax;
-  for (int i = threadIdx.x; i < kKeyRange / 32; i += blockDim.x) smask[i] = 0;
-  if (threadIdx.x == 0) smax = 0;
-  __syncthreads();
-  const int64_t nf = qoff[nq];
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
-    const FrameBox bx = boxes[i];
-    if (!(bx.flags & 1)) continue;
-    const int64_t idx = (int64_t)bx.k + kKeyOffset;
-    if (idx < 0 || idx >= kKeyRange) {  // not a fingerprint-range key: send the batch to the scan path
-      atomicMax(&smax, INT32_MAX);
-      continue;
+  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
+    for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) hist[i] = 0;
+    if (threadIdx.x == 0) smax = 0;
+    __syncthreads();
+    for (int64_t i = qoff[q] + threadIdx.x; i < qoff[q + 1]; i += blockDim.x) {
+      const FrameBox bx = boxes[i];
+      if (!(bx.flags & 1)) continue;
+      const int64_t idx = (int64_t)bx.k + kKeyOffset;
+      if (idx < 0 || idx >= kKeyRange) {  // not a fingerprint-range key: send the batch to the scan path
+        atomicMax(&smax, INT32_MAX);
+        continue;
+      }
+      atomicAdd(&hist[idx], 1);
     }
-    int lo = 0, hi = nq;  // query of frame i
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (qoff[mid] <= i) lo = mid; else hi = mid;
+    __syncthreads();
+    int32_t* row = counts + (int64_t)q * kKeyRange;
+    int32_t m = 0;
+    for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) {
+      const int32_t v = hist[i];
+      row[i] = v;
+      m = v > m ? v : m;
     }
-    const int32_t v = atomicAdd(&counts[(int64_t)lo * kKeyRange + idx], 1) + 1;
-    if (v > 1024) atomicMax(&smax, v);  // only large counts matter (fp16 exactness limit 2048)
-    atomicOr(&smask[idx >> 5], 1u << (idx & 31));
+    if (m > 1024) atomicMax(&smax, m);  // only large counts matter (fp16 exactness limit 2048)
+    if (threadIdx.x < kKeyRange / 32) {
+      uint32_t w = 0;
+      for (int b = 0; b < 32; b++) w |= (hist[32 * threadIdx.x + b] != 0 ? 1u : 0u) << b;
+      if (w) atomicOr(&mask[threadIdx.x], w);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0 && smax) atomicMax(maxc, smax);
+    __syncthreads();
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < kKeyRange / 32; i += blockDim.x)
-    if (smask[i]) atomicOr(&mask[i], smask[i]);
-  if (threadIdx.x == 0 && smax) atomicMax(maxc, smax);
 }
 
 hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts, uint32_t* d_mask,
                            int32_t* d_maxcount, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_hist_kernel, dim3(1024), dim3(256), 0, s, boxes, d_qoff, nq, d_counts, d_mask, d_maxcount);
+  hipLaunchKernelGGL(key_hist_kernel, dim3(nq < 8192 ? nq : 8192), dim3(256), 0, s, boxes, d_qoff, nq, d_counts, d_mask,
+                     d_maxcount);
   return hipGetLastError();
 }
 
@@ -1275,6 +1295,7 @@ __global__ void build_A_kernel(const int32_t* __restrict__ counts, int32_t nq, i
     const int q = (int)(i / Kp), col = (int)(i % Kp);
     int32_t v = 0;
     if (q < nq && col < Ku) v = counts[(int64_t)q * kKeyRange + keycols[col]];
+    if (q < nq && col == Ku) v = 1;  // picks up Bt's column-index entry (vote_gemm's packed argmax)
     A[i] = (_Float16)(float)v;  // exact: v <= 2048 (checked by the host)
   }
 }
@@ -1299,32 +1320,38 @@ __global__ void key_ranges_kernel(const int32_t* __restrict__ m1s, int64_t R, co
 
 // Bt[clip][key] = 1 for every row in the key's box. The rows of all keys are spread over the
 // whole grid (a box can hold a large share of the index when fingerprints concentrate).
+// Bt[clip][key] = kVoteScale for every row in the key's box, and Bt[clip][Ku] = clip mod 1024 (the
+// clip's position in its vote_gemm chunk). The rows of all keys are spread over the whole grid (a
+// box can hold a large share of the index when fingerprints concentrate).
 __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
-                                                      int32_t Ku, int32_t Kp, _Float16* __restrict__ Bt) {
+                                                      int32_t Ku, int32_t Kp, int32_t Cp, _Float16* __restrict__ Bt) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t c = t0; c < Cp; c += stride) Bt[c * Kp + Ku] = (_Float16)(float)(c & (kVoteColsPerBlock - 1));
   for (int k = 0; k < Ku; k++) {
     const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
-    for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride)
-      Bt[(int64_t)cols[r] * Kp + k] = (_Float16)1.0f;
+    for (int64_t r = lo + t0; r < hi; r += stride) Bt[(int64_t)cols[r] * Kp + k] = (_Float16)kVoteScale;
   }
 }
 
 hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds, int32_t Ku,
-                          int32_t Kp, int64_t* d_rng, _Float16* d_Bt, hipStream_t s) {
+                          int32_t Kp, int32_t Cp, int64_t* d_rng, _Float16* d_Bt, hipStream_t s) {
   if (Ku <= 0) return hipSuccess;
   hipLaunchKernelGGL(key_ranges_kernel, dim3((Ku + 63) / 64), dim3(64), 0, s, m1s, R, d_kbounds, Ku, d_rng);
-  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, Ku, Kp, d_Bt);
+  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, Ku, Kp, Cp, d_Bt);
   return hipGetLastError();
 }
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-constexpr int kVoteColsPerBlock = 1024;
 
 // Wave = 32 queries x (32-clip sub-tiles of the block's 1024-clip chunk); 4 waves = 128 queries
-// share each B fragment through L1. Fused argmax: per row the max (score, column); columns are
-// the clips in ascending uuid order, so a later column wins a tie (SQLite returns the greatest
-// audio_uuid). Result key = score << 32 | tiekey[column], merged with atomicMax.
+// share each B fragment through L1. Packed argmax: the K dimension carries one extra column,
+// A = 1 against Bt = the clip's position in the chunk, and the box entries are 1024, so each
+// accumulator is exactly 1024 * score + position (< 2^24 for scores < 16384 frames, exact in fp32):
+// one v_max per score keeps the best (score, latest column) — columns are the clips in ascending
+// uuid order, so a later column wins a tie, as SQLite returns the greatest audio_uuid. Result key
+// = score << 32 | tiekey[column], merged across chunks with atomicMax.
 __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
                                                         int32_t Qp, int32_t Cp, int32_t Kp,
                                                         const int32_t* __restrict__ tiekey,
@@ -1335,9 +1362,9 @@ __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restri
   if (q0 >= Qp) return;
   const int cbeg = blockIdx.x * kVoteColsPerBlock;
   const int cend = min(cbeg + kVoteColsPerBlock, Cp);
-  int bs[16], bc[16];
+  floatx16 m;
 #pragma unroll
-  for (int i = 0; i < 16; i++) { bs[i] = 0; bc[i] = 0; }
+  for (int i = 0; i < 16; i++) m[i] = 0.f;
   const _Float16* arow = A + (int64_t)(q0 + r) * Kp + 8 * h;
   for (int c0 = cbeg; c0 < cend; c0 += 32) {
     floatx16 acc;
@@ -1349,23 +1376,21 @@ __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restri
       const half8 bv = *reinterpret_cast<const half8*>(brow + kb);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bv, acc, 0, 0, 0);
     }
-    const int col = c0 + r;
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const int s = (int)acc[i];
-      if (s > 0 && s >= bs[i]) { bs[i] = s; bc[i] = col; }
-    }
+    for (int i = 0; i < 16; i++) m[i] = fmaxf(m[i], acc[i]);
   }
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    unsigned long long key = bs[i] > 0 ? (((unsigned long long)(unsigned)bs[i] << 32) | (unsigned)tiekey[bc[i]]) : 0ull;
+    float v = m[i];
 #pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) {
-      const unsigned long long o = __shfl_xor(key, off, 64);
-      key = o > key ? o : key;
-    }
+    for (int off = 16; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    const uint32_t packed = (uint32_t)v;
+    const uint32_t score = packed / (uint32_t)kVoteScale;
     const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (r == 0 && key) atomicMax(&best[q0 + row], key);
+    if (r == 0 && score > 0) {
+      const int col = cbeg + (int)(packed % (uint32_t)kVoteScale);
+      atomicMax(&best[q0 + row], ((unsigned long long)score << 32) | (unsigned)tiekey[col]);
+    }
   }
 }
 

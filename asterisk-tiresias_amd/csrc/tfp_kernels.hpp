@@ -54,13 +54,16 @@ hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, 
                             int32_t* vout, int64_t n, hipStream_t s);
 
 // Search.
-hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, hipStream_t s);
+// Also zeroes zero_words[0, nzero) (the vote path's mask, max count and best keys).
+hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, uint32_t* zero_words,
+                             int32_t nzero, hipStream_t s);
 hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts /*[nq][kKeyRange]*/,
                            uint32_t* d_mask /*[kKeyRange/32]*/, int32_t* d_maxcount, hipStream_t s);
 hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, int32_t Ku, int32_t Kp,
                           _Float16* d_A, hipStream_t s);
 hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds /*[Ku][2]*/,
-                          int32_t Ku, int32_t Kp, int64_t* d_rng /*[Ku][2] scratch*/, _Float16* d_Bt, hipStream_t s);
+                          int32_t Ku, int32_t Kp /*>= Ku + 1*/, int32_t Cp, int64_t* d_rng /*[Ku][2] scratch*/,
+                          _Float16* d_Bt, hipStream_t s);
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
