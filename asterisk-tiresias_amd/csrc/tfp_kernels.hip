@@ -1051,6 +1051,282 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Software-pipelined 8 kHz kernel: iteration g runs the FRONT of pass g (PCM, FFT, real split,
+// |X| into the wave's |X| buffer) and the BACK of pass g-1 (filterbank + logs from that buffer),
+// so the filterbank's LDS reads and the FFT's VALU work of two passes share one basic block and
+// overlap; a tile's tail (DCT, dB, "%f") runs after the back of its last pass. Arithmetic and
+// results are fingerprint8k_kernel's (same helpers, same order per value).
+#ifndef TFP8P_MEL_BATCH
+#define TFP8P_MEL_BATCH 1
+#endif
+constexpr int kNRow = 288;  // |X| row per frame: bins 0..271 read (8 kHz ms_maxbin = 272); 288 = 32 mod 64 banks
+struct WaveLds8P {
+  union {
+    cf scratch[4][kFrameStride];
+    alignas(16) int16_t pcm[5 * kHopStride];
+  };
+  alignas(16) float nbuf[4][kNRow];
+  float logs[kWaveFrames * kLogStride];
+};
+
+template <int LEN, int BATCH>
+__device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const float* __restrict__ w, int st) {
+  constexpr int G = LEN / 4, B = BATCH < G ? BATCH : G;
+  float acc = 0.f;
+#pragma unroll
+  for (int i0 = 0; i0 < G; i0 += B) {
+    float4 wv[B], nv[B];
+#pragma unroll
+    for (int i = 0; i < B; i++)
+      if (i0 + i < G) {
+        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
+        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
+      }
+#pragma unroll
+    for (int i = 0; i < B; i++)
+      if (i0 + i < G) {
+        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
+        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
+        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+      }
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_pipe_kernel(
+    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
+    const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
+    const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
+    float rare_thr) {
+  constexpr int LA = 36, LB = 16, LC = 8;  // DspTables_fixed8k()
+  const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;
+  __shared__ __attribute__((aligned(16))) LdsTables S;
+  __shared__ __attribute__((aligned(16))) WaveLds8P WL[kBlockWaves];
+  const int tid = threadIdx.x;
+  cf* winr = reinterpret_cast<cf*>(S.window);  // [n1/2][L][2] window pairs (see fingerprint8k_kernel)
+  cf* twr = S.tw512;                           // [k2][L] = (w512^k, w512^(256-k)) pair-split twiddles
+  for (int i = tid; i < 256; i += kBlockThreads) {
+    const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
+    const int j = (32 * n1 + 2 * L + 256) & 511;
+    winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
+    const int k2 = i >> 5, kk = (L == 0 && k2 == 0) ? 128 : L + 16 * k2, kp = 256 - kk;
+    twr[i] = (i & 1) ? cf{T->tw512_re[kp], T->tw512_im[kp]} : cf{T->tw512_re[kk], T->tw512_im[kk]};
+  }
+  for (int i = tid; i < 15 * 16; i += kBlockThreads) {
+    const int k1 = 1 + i / 16, L = i % 16;
+    S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
+  }
+  for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
+  for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
+  for (int i = tid; i < 48; i += kBlockThreads) {
+    (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
+    (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
+  }
+  if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
+  if (tid < 16) S.logf[tid] = logf_table()[tid];
+  if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
+  for (int i = tid; i < T->ms_total; i += kBlockThreads) S.ms_w[i] = 0.5f * T->ms_w[i];  // exact: w/2
+  __syncthreads();
+
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  WaveLds8P& M = WL[wave];
+  cf* W = M.scratch[grp];
+  float* Nf = M.nbuf[grp];
+  const int nwaves = gridDim.x * kBlockWaves;
+  const int maxbin = T->ms_maxbin;
+  const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
+  const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
+  cf w16r[10];
+#pragma unroll
+  for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
+  cf ltw[15];
+#pragma unroll
+  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+  {
+    const float lempty = aubio_log10_fast(0.f, S.logf);
+    for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
+      const int j = i % kFilters;
+      if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
+    }
+    for (int i = lane; i < 4 * kNRow; i += 64) (&M.nbuf[0][0])[i] = 0.f;  // the first (dummy) back pass
+  }
+
+  struct Tile {
+    int c;
+    int64_t f0, s0, ns;
+  };
+  auto tile_of = [&](int b) {
+    Tile t;
+    t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
+    t.f0 = (int64_t)(b - toff[t.c]) * kWaveFrames;
+    t.s0 = sbeg[t.c];
+    t.ns = send[t.c] - t.s0;
+    return t;
+  };
+  auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
+    const int16_t* clip = pcm + t.s0;
+    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
+    const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
+    if (interior) {
+      const int4* src = reinterpret_cast<const int4*>(clip + sb);
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (valid && chunk < kPassChunks) ? fetch_chunk_checked(clip, t.ns, sb + 8 * chunk) : make_int4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  const int b0 = blockIdx.x * kBlockWaves + wave;
+  const int my_tiles = b0 < ntiles ? (ntiles - 1 - b0) / nwaves + 1 : 0;
+  const int npass = 4 * my_tiles;
+  int bf = b0, subf = 0;  // front pass: tile bf, pass subf
+  Tile tf = tile_of(b0 < ntiles ? b0 : 0);
+  Tile tn = (b0 + nwaves < ntiles) ? tile_of(b0 + nwaves) : tf;
+  Tile tb = tf;           // tile of the back pass
+  int4 pf[kChunkRounds];
+  fetch(tf, 0, b0 < ntiles, pf);
+  for (int g = 0; g <= npass; g++) {
+    const bool front_valid = g < npass;
+    const int subb = (g + 3) & 3;  // pass of the back half (g - 1)
+    wave_sync();  // the previous iteration's readers of the scratch are done
+#pragma unroll
+    for (int r = 0; r < kChunkRounds; r++) {
+      const int chunk = lane + 64 * r;
+      if (chunk < kPassChunks) *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+    }
+    if (subf < 3) fetch(tf, subf + 1, front_valid, pf);
+    else fetch(tn, 0, front_valid && bf + nwaves < ntiles, pf);
+    wave_sync();
+    int oz = 0;
+    asm volatile("" : "+v"(oz));
+    // ---- FRONT (pass g): PCM -> window -> first DFT16 -> inter-stage twiddles
+    const int16_t* hop0 = M.pcm + grp * kHopStride;
+    cf wreg[16];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const float4 w4 = *reinterpret_cast<const float4*>(winr + (i * 16 + L) * 2 + oz);
+      wreg[2 * i] = cf{w4.x, w4.y};
+      wreg[2 * i + 1] = cf{w4.z, w4.w};
+    }
+    cf z[16], Y[16];
+#pragma unroll
+    for (int n1 = 0; n1 < 16; n1++) {
+      const int j = (32 * n1 + 2 * L + 256) & 511;
+      const int hsel = n1 < 8 ? 1 : 0;
+      const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
+      z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
+    }
+    dft16q(w16r, z, Y);
+#pragma unroll
+    for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+    // ---- BACK (pass g - 1): filterbank + logs from the |X| buffer (same basic block as the FFT)
+    {
+      const float* Nb = Nf;
+      float* lrow = M.logs + (subb * 4 + grp) * kLogStride;
+      const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+      const float* wbase = S.ms_w + 4 * L + oz;
+      const float aC = mel_sum_b<LC, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[2], stC);
+      const float aB = mel_sum_b<LB, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[1], stB);
+      const float aA = mel_sum_b<LA, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[0], stA);
+      const float lA = aubio_log10_fast(aA, S.logf);
+      const float lB = aubio_log10_fast(aB, S.logf);
+      lrow[fA] = lA;
+      lrow[fB] = lB;
+      if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+    }
+    wave_sync();
+    // ---- FRONT: transpose, second DFT16, real split -> |X| buffer
+#pragma unroll
+    for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
+    wave_sync();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
+    dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
+    {
+      cf Pq[8];
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+      const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) {
+        cf own = Y[k2 == 0 ? 8 : 16 - k2];
+        asm("" : "+v"(own.x), "+v"(own.y));
+        cf y = Y[k2];
+        if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
+        const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
+        const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
+        const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
+        const cf E = addsub(y, p);
+        const cf O = subadd(y, p);
+        const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+        const cf Sv = E + Tt;
+        const cf O2 = cf{-O.x, O.y};
+        const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
+        const cf S2 = cf{E.x, -E.y} + T2;
+        const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
+        const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
+        float nk = sqrtf_fast_cr(x), nk2 = sqrtf_fast_cr(x2);
+        const uint32_t m = min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u);
+        if (__builtin_expect(__any(m < rare_m1), 0)) {
+          if (x > 0.f && x < rare_thr) nk = 2.f * __builtin_sqrtf(split_power(y, p, w));
+          if (x2 > 0.f && x2 < rare_thr) nk2 = 2.f * __builtin_sqrtf(split_power(p, y, w2));
+        }
+        Nf[k] = nk;
+        Nf[256 - k] = nk2;
+      }
+      if (L == 0) {
+        Nf[0] = n0;
+        Nf[256] = n256;
+      }
+      for (int i = 257 + L; i < maxbin; i += 16) Nf[i] = 0.f;
+    }
+    // ---- tail of the back tile after the back of its last pass
+    if (g >= 1 && subb == 3) {
+      wave_sync();
+      if (lane < 2 * kWaveFrames) {  // the deferred slot-2 logs: lane = (frame row, filter)
+        const int f = S.c_real[lane & 1];
+        if (f >= 0) {
+          float* p = M.logs + (lane >> 1) * kLogStride + f;
+          *p = aubio_log10_fast(*p, S.logf);
+        }
+      }
+      wave_sync();
+      if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
+        const int row = lane >> 1, cfi = lane & 1;
+        const int64_t f = tb.f0 + row;
+        const int64_t nfb = (tb.ns + kHop - 1) / kHop;
+        if (f < nfb) {
+          const float* lrow = M.logs + row * kLogStride;
+          float acc = 0.f;
+#pragma unroll 8
+          for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+          const double q = db_of_coef(acc);
+          const int64_t gi = foff[tb.c] + f;
+          micro[2 * gi + cfi] = micro_of_db(q);
+          if (db) db[2 * gi + cfi] = q;
+        }
+      }
+    }
+    // advance: the back half of the next iteration is this iteration's front pass
+    tb = tf;
+    if (++subf == 4) {
+      subf = 0;
+      bf += nwaves;
+      tf = tn;
+      tn = (bf + nwaves < ntiles) ? tile_of(bf + nwaves) : tf;
+    }
+  }
+}
+
 bool DspTables_fixed8k(const DspTables& t) {
   return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
@@ -1081,8 +1357,13 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
   const int grid = want < grid_cap[v] ? want : grid_cap[v];
   if (v) {
-    hipLaunchKernelGGL(fingerprint8k_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                       d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+    const char* pp = getenv("TFP_PIPE");
+    if (pp && atoi(pp))
+      hipLaunchKernelGGL(fingerprint8k_pipe_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+    else
+      hipLaunchKernelGGL(fingerprint8k_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
     return hipGetLastError();
   }
   static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production
