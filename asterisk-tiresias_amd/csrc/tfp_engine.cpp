@@ -114,6 +114,9 @@ struct tfp_engine {
   bool stage_pending = false;
   DevBuf small_work, small_bk, key_rng;
   uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
+  DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
+  double rng_tol = 0.0;
+  bool rng_valid = false;
   ~tfp_engine() { if (stage_ev) (void)hipEventDestroy(stage_ev); }
 };
 
@@ -356,6 +359,17 @@ int rebuild(tfp_engine* e) {
     HIPCHK(e, e->cols.reserve(4));
   }
   e->dirty = false;
+  e->rng_valid = false;  // the key-range cache follows the index
+  return TFP_OK;
+}
+
+// Row ranges of every key's box at tolerance tole, cached per index version and tolerance.
+int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
+  if (e->rng_valid && memcmp(&e->rng_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  HIPCHK(e, e->rng_all.reserve(sizeof(int64_t) * 2 * kKeyRange));
+  HIPCHK(e, launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, tole, e->rng_all.as<int64_t>(), s));
+  e->rng_tol = tole;
+  e->rng_valid = true;
   return TFP_OK;
 }
 
@@ -400,8 +414,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       }
       const uint8_t epoch = ++e->small_epoch;
       SmallWork* w = e->small_work.as<SmallWork>();
-      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->m1s.as<int32_t>(),
-                                    e->nrows, e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
+      if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
+      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->rng_all.as<int64_t>(),
+                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
       struct { int32_t ku, bad; unsigned long long best[kSmallQ]; } h;
       static_assert(offsetof(SmallWork, best) == offsetof(SmallWork, ku) + 8, "ku, bad, best contiguous");
       HIPCHK(e, hipMemcpyAsync(&h, &w->ku, 8 + sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
@@ -424,50 +439,44 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   uint32_t* d_mask = e->best.as<uint32_t>();
   int32_t* d_max = reinterpret_cast<int32_t*>(d_mask + kMaskWords);
   unsigned long long* d_best = reinterpret_cast<unsigned long long*>(d_mask + kMiscWords);
-  HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   const int32_t C = e->ncols;
   const int64_t R = e->nrows;
   int64_t max_frames = 0;
   for (int32_t i = 0; i < nq; i++) max_frames = std::max<int64_t>(max_frames, qo[i + 1] - qo[i]);
+  const bool vote = sc.coefs == 1 && C > 0 && R > 0 && max_frames < 16384;  // packed scores exact below 16384 frames
+  // the vote path needs only the zeroing; the scan path the frames' boxes too
+  HIPCHK(e, launch_prep_boxes(d_q, vote ? 0 : nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
 
   bool done = false;
-  if (sc.coefs == 1 && C > 0 && R > 0 && max_frames < 16384) {  // packed scores exact below 16384 frames
-    // vote-matrix path
+  if (vote) {
+    // vote-matrix path, no host round trip: histogram -> used-key compaction -> A, Bt -> GEMM
+    const int32_t Cp = ((C + 31) / 32) * 32;
     HIPCHK(e, e->counts.reserve(sizeof(int32_t) * (size_t)nq * kKeyRange));
-    HIPCHK(e, launch_key_hist(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, e->counts.as<int32_t>(), d_mask, d_max, s));
-    uint32_t hmask[kMaskWords + 1];
-    HIPCHK(e, hipMemcpyAsync(hmask, d_mask, sizeof hmask, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, e->keycols.reserve(sizeof(int32_t) * kKeyRange));
+    HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * kKeyRange));
+    HIPCHK(e, e->kbounds.reserve(sizeof(VoteMeta)));
+    HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
+    HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
+    VoteMeta* d_meta = e->kbounds.as<VoteMeta>();
+    if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
+    HIPCHK(e, launch_key_hist(d_q, sc, e->qoff.as<int64_t>(), nq, e->counts.as<int32_t>(), d_mask, d_max, s));
+    HIPCHK(e, launch_vote_compact(d_mask, d_max, e->rng_all.as<int64_t>(), e->keycols.as<int32_t>(),
+                                  e->key_rng.as<int64_t>(), d_meta, s));
+    HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), d_meta, e->A.as<_Float16>(), s));
+    HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
+    HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(), d_best, s));
+    VoteMeta hm;
+    HIPCHK(e, hipMemcpyAsync(&hm, d_meta, sizeof hm, hipMemcpyDeviceToHost, s));
+    if (!d_keys_out && nq)
+      HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
-    const int32_t maxcount = (int32_t)hmask[kMaskWords];
-    if (maxcount <= 2048) {  // counts exact in fp16
-      std::vector<int32_t> keycols;
-      std::vector<int64_t> kb;
-      for (int idx = 0; idx < kKeyRange; idx++)
-        if (hmask[idx >> 5] >> (idx & 31) & 1u) {
-          keycols.push_back(idx);
-          const double freq = (double)(idx - kKeyOffset);
-          kb.push_back(fmt6_bound(freq - sc.tole));
-          kb.push_back(fmt6_bound(freq + sc.tole));
-        }
-      const int32_t Ku = (int32_t)keycols.size();
-      if (Ku == 0) {
-        done = true;  // every frame ignored: no rows inserted -> NOTFOUND
-      } else {
-        const int32_t Kp = ((Ku + 1 + 15) / 16) * 16;  // + the column-index entry (packed argmax)
-        const int32_t Cp = ((C + 31) / 32) * 32;
-        if ((rc = upload(e, e->keycols, keycols.data(), sizeof(int32_t) * Ku, s))) return rc;
-        if ((rc = upload(e, e->kbounds, kb.data(), sizeof(int64_t) * kb.size(), s))) return rc;
-        HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * Kp));
-        HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * Kp));
-        HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), Ku, Kp, e->A.as<_Float16>(), s));
-        HIPCHK(e, hipMemsetAsync(e->Bt.p, 0, sizeof(_Float16) * (size_t)Cp * Kp, s));
-        HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * Ku));
-        HIPCHK(e, launch_build_B(e->m1s.as<int32_t>(), R, e->cols.as<int32_t>(), e->kbounds.as<int64_t>(), Ku, Kp, Cp,
-                                 e->key_rng.as<int64_t>(), e->Bt.as<_Float16>(), s));
-        HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, Kp, e->tiekey.as<int32_t>(), d_best, s));
-        done = true;
-      }
+    if (hm.ok) {
+      if (d_keys_out)
+        HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+      return TFP_OK;
     }
+    // a count above fp16's exact range or a key outside the vote range: the scan path below
+    HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }
   if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
     // general path, query chunks bounded to ~512 MB of stamp+score scratch

@@ -1519,22 +1519,37 @@ constexpr float kVoteScale = 1024.f;      // Bt's box entries: acc = 1024 * scor
 // ---- coefs = 1: vote matrix. score[q][clip] = sum_k N[q][k] * B[k][clip], where N counts the
 // query's non-ignored frames with trunc key k and B[k][clip] = 1 iff the clip has a row in
 // [fmt6(k - tol), fmt6(k + tol)] — exactly the per-frame "group by audio_uuid" hit count.
+// The trunc key of a query frame and whether its SQL runs (prep_boxes' flags & 1, restated for
+// the vote path, which needs nothing else of the box).
+__device__ __forceinline__ bool frame_key(const double* __restrict__ q, int64_t i, const SearchConsts& sc, int32_t& k) {
+  const double q1 = q[2 * i];
+  const double v1 = __builtin_isfinite(q1) ? q1 : 0.0;  // ast_json_real_get(NULL) = 0.0
+  k = (v1 > -2147483649.0 && v1 < 2147483648.0) ? (int32_t)v1 : INT32_MIN;  // (int) truncation, :290
+  const double freq = (double)k;
+  if (sc.has_low && freq < sc.thr_low) return false;   // :293-306
+  if (sc.has_high && freq > sc.thr_high) return false;
+  return __builtin_isfinite(freq - sc.tole) && __builtin_isfinite(freq + sc.tole);
+}
+
 // One block per query (frames of a query are contiguous): the per-key frame counts in LDS, written
 // out as the query's whole row (no memset, no global atomics on counts); used keys ORed into the
-// batch mask; counts above 1024 reported through maxc (fp16 holds counts up to 2048 exactly).
-__global__ __launch_bounds__(256) void key_hist_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff,
-                                                       int32_t nq, int32_t* __restrict__ counts,
-                                                       uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
+// batch mask (one ballot per 64 keys); counts above 1024 reported through maxc (fp16 holds counts
+// up to 2048 exactly), a key outside the vote range as INT32_MAX.
+__global__ __launch_bounds__(256) void key_hist_kernel(const double* __restrict__ qv, SearchConsts sc,
+                                                       const int64_t* __restrict__ qoff, int32_t nq,
+                                                       int32_t* __restrict__ counts, uint32_t* __restrict__ mask,
+                                                       int32_t* __restrict__ maxc) {
   __shared__ int32_t hist[kKeyRange];
   __shared__ int32_t smax;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int q = blockIdx.x; q < nq; q += gridDim.x) {
     for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) hist[i] = 0;
     if (threadIdx.x == 0) smax = 0;
     __syncthreads();
     for (int64_t i = qoff[q] + threadIdx.x; i < qoff[q + 1]; i += blockDim.x) {
-      const FrameBox bx = boxes[i];
-      if (!(bx.flags & 1)) continue;
-      const int64_t idx = (int64_t)bx.k + kKeyOffset;
+      int32_t k;
+      if (!frame_key(qv, i, sc, k)) continue;
+      const int64_t idx = (int64_t)k + kKeyOffset;
       if (idx < 0 || idx >= kKeyRange) {  // not a fingerprint-range key: send the batch to the scan path
         atomicMax(&smax, INT32_MAX);
         continue;
@@ -1550,10 +1565,12 @@ __global__ __launch_bounds__(256) void key_hist_kernel(const FrameBox* __restric
       m = v > m ? v : m;
     }
     if (m > 1024) atomicMax(&smax, m);  // only large counts matter (fp16 exactness limit 2048)
-    if (threadIdx.x < kKeyRange / 32) {
-      uint32_t w = 0;
-      for (int b = 0; b < 32; b++) w |= (hist[32 * threadIdx.x + b] != 0 ? 1u : 0u) << b;
-      if (w) atomicOr(&mask[threadIdx.x], w);
+    for (int base = 64 * wave; base < kKeyRange; base += blockDim.x) {
+      const unsigned long long bits = __ballot(hist[base + lane] != 0);
+      if (lane == 0 && bits) {
+        if ((uint32_t)bits) atomicOr(&mask[base >> 5], (uint32_t)bits);
+        if ((uint32_t)(bits >> 32)) atomicOr(&mask[(base >> 5) + 1], (uint32_t)(bits >> 32));
+      }
     }
     __syncthreads();
     if (threadIdx.x == 0 && smax) atomicMax(maxc, smax);
@@ -1561,51 +1578,106 @@ __global__ __launch_bounds__(256) void key_hist_kernel(const FrameBox* __restric
   }
 }
 
-hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts, uint32_t* d_mask,
-                           int32_t* d_maxcount, hipStream_t s) {
+hipError_t launch_key_hist(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t* d_counts,
+                           uint32_t* d_mask, int32_t* d_maxcount, hipStream_t s) {
   if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_hist_kernel, dim3(nq < 8192 ? nq : 8192), dim3(256), 0, s, boxes, d_qoff, nq, d_counts, d_mask,
+  hipLaunchKernelGGL(key_hist_kernel, dim3(nq < 8192 ? nq : 8192), dim3(256), 0, s, d_q, sc, d_qoff, nq, d_counts, d_mask,
                      d_maxcount);
   return hipGetLastError();
 }
 
+// Row range [lo, hi) in the m1-sorted index of every key's "%f" box at tolerance tole (all 1024
+// keys: cached by the engine per index version and tolerance).
+__global__ void key_ranges_all_kernel(const int32_t* __restrict__ m1s, int64_t R, double tole, int64_t* __restrict__ rng) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= kKeyRange) return;
+  const double freq = (double)(t - kKeyOffset);
+  rng[2 * t] = lower_bound_i32(m1s, R, fmt6_bound(freq - tole));
+  rng[2 * t + 1] = upper_bound_i32(m1s, R, fmt6_bound(freq + tole));
+}
+
+hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int64_t* d_rng_all, hipStream_t s) {
+  hipLaunchKernelGGL(key_ranges_all_kernel, dim3(kKeyRange / 64), dim3(64), 0, s, m1s, R, tole, d_rng_all);
+  return hipGetLastError();
+}
+
+// Used-key compaction on the GPU (no host round trip): the batch's key mask -> keycols (ascending
+// key order, the order the host used to build them), each key's "%f" box and its row range in the
+// m1-sorted index; meta = (Ku, Kp = padded Ku + 1, ok = counts exact in fp16).
+__global__ __launch_bounds__(1024) void vote_compact_kernel(const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
+                                                            const int64_t* __restrict__ rng_all,
+                                                            int32_t* __restrict__ keycols, int64_t* __restrict__ rng,
+                                                            VoteMeta* __restrict__ meta) {
+  __shared__ int32_t scan[kKeyRange];
+  const int t = threadIdx.x;
+  const int used = (mask[t >> 5] >> (t & 31)) & 1;
+  scan[t] = used;
+  __syncthreads();
+  for (int off = 1; off < kKeyRange; off <<= 1) {
+    const int v = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  if (used) {
+    const int kc = scan[t] - 1;
+    keycols[kc] = t;
+    rng[2 * kc] = rng_all[2 * t];
+    rng[2 * kc + 1] = rng_all[2 * t + 1];
+  }
+  if (t == kKeyRange - 1) {
+    const int ku = scan[t];
+    meta->ku = ku;
+    meta->kp = ((ku + 1 + 15) / 16) * 16;
+    meta->ok = *maxc <= 2048 ? 1 : 0;  // counts exact in fp16 (and every key in range)
+  }
+}
+
+hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int32_t* d_keycols,
+                               int64_t* d_rng, VoteMeta* d_meta, hipStream_t s) {
+  hipLaunchKernelGGL(vote_compact_kernel, dim3(1), dim3(kKeyRange), 0, s, d_mask, d_maxc, d_rng_all, d_keycols, d_rng,
+                     d_meta);
+  return hipGetLastError();
+}
+
 __global__ void build_A_kernel(const int32_t* __restrict__ counts, int32_t nq, int32_t Qp, const int32_t* __restrict__ keycols,
-                               int32_t Ku, int32_t Kp, _Float16* __restrict__ A) {
+                               const VoteMeta* __restrict__ meta, _Float16* __restrict__ A) {
+  const int32_t Ku = meta->ku, Kp = meta->kp;
   const int64_t total = (int64_t)Qp * Kp;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int q = (int)(i / Kp), col = (int)(i % Kp);
     int32_t v = 0;
     if (q < nq && col < Ku) v = counts[(int64_t)q * kKeyRange + keycols[col]];
     if (q < nq && col == Ku) v = 1;  // picks up Bt's column-index entry (vote_gemm's packed argmax)
-    A[i] = (_Float16)(float)v;  // exact: v <= 2048 (checked by the host)
+    A[i] = (_Float16)(float)v;  // exact: v <= 2048 when meta->ok
   }
 }
 
-hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, int32_t Ku,
-                          int32_t Kp, _Float16* d_A, hipStream_t s) {
-  const int64_t total = (int64_t)Qp * Kp;
+hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, const VoteMeta* d_meta,
+                          _Float16* d_A, hipStream_t s) {
+  const int64_t total = (int64_t)Qp * kVoteKpMax;
   int64_t g = (total + 255) / 256;
   if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)g), dim3(256), 0, s, d_counts, nq, Qp, d_keycols, Ku, Kp, d_A);
+  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)g), dim3(256), 0, s, d_counts, nq, Qp, d_keycols, d_meta, d_A);
   return hipGetLastError();
 }
 
-// Row range [lo, hi) of each used key's box in the m1-sorted index (one thread per key).
-__global__ void key_ranges_kernel(const int32_t* __restrict__ m1s, int64_t R, const int64_t* __restrict__ kb, int32_t Ku,
-                                  int64_t* __restrict__ rng) {
-  const int k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= Ku) return;
-  rng[2 * k] = lower_bound_i32(m1s, R, kb[2 * k]);
-  rng[2 * k + 1] = upper_bound_i32(m1s, R, kb[2 * k + 1]);
+// Bt[clip][key] = kVoteScale for every row in the key's box, Bt[clip][Ku] = clip mod 1024 (the
+// clip's position in its vote_gemm chunk), 0 elsewhere: zero_bt clears the [Cp][Kp] region the
+// GEMM reads, then build_B marks.
+__global__ void zero_bt_kernel(_Float16* __restrict__ Bt, int32_t Cp, const VoteMeta* __restrict__ meta) {
+  const int64_t n16 = (int64_t)Cp * meta->kp / 8;  // 16-byte units (Kp is a multiple of 16)
+  uint4* p = reinterpret_cast<uint4*>(Bt);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// Bt[clip][key] = 1 for every row in the key's box. The rows of all keys are spread over the
-// whole grid (a box can hold a large share of the index when fingerprints concentrate).
-// Bt[clip][key] = kVoteScale for every row in the key's box, and Bt[clip][Ku] = clip mod 1024 (the
-// clip's position in its vote_gemm chunk). The rows of all keys are spread over the whole grid (a
-// box can hold a large share of the index when fingerprints concentrate).
+// The rows of all keys are spread over the whole grid (a box can hold a large share of the index
+// when fingerprints concentrate).
 __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
-                                                      int32_t Ku, int32_t Kp, int32_t Cp, _Float16* __restrict__ Bt) {
+                                                      const VoteMeta* __restrict__ meta, int32_t Cp,
+                                                      _Float16* __restrict__ Bt) {
+  const int32_t Ku = meta->ku, Kp = meta->kp;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t c = t0; c < Cp; c += stride) Bt[c * Kp + Ku] = (_Float16)(float)(c & (kVoteColsPerBlock - 1));
@@ -1615,11 +1687,10 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
   }
 }
 
-hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds, int32_t Ku,
-                          int32_t Kp, int32_t Cp, int64_t* d_rng, _Float16* d_Bt, hipStream_t s) {
-  if (Ku <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_ranges_kernel, dim3((Ku + 63) / 64), dim3(64), 0, s, m1s, R, d_kbounds, Ku, d_rng);
-  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, Ku, Kp, Cp, d_Bt);
+hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(zero_bt_kernel, dim3(2048), dim3(256), 0, s, d_Bt, Cp, d_meta);
+  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, d_meta, Cp, d_Bt);
   return hipGetLastError();
 }
 
@@ -1634,9 +1705,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // uuid order, so a later column wins a tie, as SQLite returns the greatest audio_uuid. Result key
 // = score << 32 | tiekey[column], merged across chunks with atomicMax.
 __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
-                                                        int32_t Qp, int32_t Cp, int32_t Kp,
+                                                        int32_t Qp, int32_t Cp, const VoteMeta* __restrict__ meta,
                                                         const int32_t* __restrict__ tiekey,
                                                         unsigned long long* __restrict__ best) {
+  if (!meta->ok) return;  // the host redoes the batch on the scan path
+  const int32_t Kp = meta->kp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int r = lane & 31, h = lane >> 5;
   const int q0 = (blockIdx.y * 4 + wave) * 32;
@@ -1647,18 +1720,29 @@ __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restri
 #pragma unroll
   for (int i = 0; i < 16; i++) m[i] = 0.f;
   const _Float16* arow = A + (int64_t)(q0 + r) * Kp + 8 * h;
-  for (int c0 = cbeg; c0 < cend; c0 += 32) {
-    floatx16 acc;
+  constexpr int kSub = 4;  // 32-clip sub-tiles per step: their B fragments are loaded together
+  for (int c0 = cbeg; c0 < cend; c0 += 32 * kSub) {
+    floatx16 acc[kSub];
 #pragma unroll
-    for (int i = 0; i < 16; i++) acc[i] = 0.f;
-    const _Float16* brow = Bt + (int64_t)(c0 + r) * Kp + 8 * h;
+    for (int j = 0; j < kSub; j++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[j][i] = 0.f;
     for (int kb = 0; kb < Kp; kb += 16) {
       const half8 a = *reinterpret_cast<const half8*>(arow + kb);
-      const half8 bv = *reinterpret_cast<const half8*>(brow + kb);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bv, acc, 0, 0, 0);
+      half8 bv[kSub];
+#pragma unroll
+      for (int j = 0; j < kSub; j++) {
+        const int c = min(c0 + 32 * j, cend - 32);  // (a clamped duplicate sub-tile is not used below)
+        bv[j] = *reinterpret_cast<const half8*>(Bt + (int64_t)(c + r) * Kp + 8 * h + kb);
+      }
+#pragma unroll
+      for (int j = 0; j < kSub; j++) acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a, bv[j], acc[j], 0, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 16; i++) m[i] = fmaxf(m[i], acc[i]);
+    for (int j = 0; j < kSub; j++)
+      if (c0 + 32 * j < cend)
+#pragma unroll
+        for (int i = 0; i < 16; i++) m[i] = fmaxf(m[i], acc[j][i]);
   }
 #pragma unroll
   for (int i = 0; i < 16; i++) {
@@ -1675,18 +1759,18 @@ __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restri
   }
 }
 
-hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
+hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s) {
   if (Qp <= 0 || Cp <= 0) return hipSuccess;
   dim3 grid((Cp + kVoteColsPerBlock - 1) / kVoteColsPerBlock, (Qp / 32 + 3) / 4);
-  hipLaunchKernelGGL(vote_gemm_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, Kp, d_tiekey, d_best);
+  hipLaunchKernelGGL(vote_gemm_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_best);
   return hipGetLastError();
 }
 
 // ---- small-batch path (see tfp_kernels.hpp). Same sets and counts as key_hist + build_A/B +
 // vote_gemm: a query frame with trunc key k votes once for every clip with a row in k's box.
 __global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restrict__ q, SmallQueries sq,
-                                                          SearchConsts sc, const int32_t* __restrict__ m1s, int64_t R,
+                                                          SearchConsts sc, const int64_t* __restrict__ rng_all,
                                                           SmallWork* __restrict__ w) {
   __shared__ int32_t hist[kSmallQ][kKeyRange];
   __shared__ int32_t scan[kKeyRange];
@@ -1725,9 +1809,8 @@ __global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restri
   }
   if (used) {
     const int kc = scan[t] - 1;
-    const double freq = (double)(t - kKeyOffset);
-    w->kb[kc][0] = lower_bound_i32(m1s, R, fmt6_bound(freq - sc.tole));  // the box's row range
-    w->kb[kc][1] = upper_bound_i32(m1s, R, fmt6_bound(freq + sc.tole));
+    w->kb[kc][0] = rng_all[2 * t];  // the box's row range
+    w->kb[kc][1] = rng_all[2 * t + 1];
     for (int qi = 0; qi < sq.nq; qi++) w->A[qi][kc] = hist[qi][t];
   }
   if (t == kKeyRange - 1) {
@@ -1785,10 +1868,10 @@ __global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__
 }
 
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int32_t* m1s, int64_t R,
+                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s) {
   if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, m1s, R, d_work);
+  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, d_rng_all, d_work);
   hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_work, d_bk, Cp, cols, epoch);
   hipLaunchKernelGGL(small_vote_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey,
                      epoch);

@@ -57,15 +57,30 @@ hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, 
 // Also zeroes zero_words[0, nzero) (the vote path's mask, max count and best keys).
 hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, uint32_t* zero_words,
                              int32_t nzero, hipStream_t s);
-hipError_t launch_key_hist(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int32_t* d_counts /*[nq][kKeyRange]*/,
-                           uint32_t* d_mask /*[kKeyRange/32]*/, int32_t* d_maxcount, hipStream_t s);
-hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, int32_t Ku, int32_t Kp,
-                          _Float16* d_A, hipStream_t s);
-hipError_t launch_build_B(const int32_t* m1s, int64_t R, const int32_t* cols, const int64_t* d_kbounds /*[Ku][2]*/,
-                          int32_t Ku, int32_t Kp /*>= Ku + 1*/, int32_t Cp, int64_t* d_rng /*[Ku][2] scratch*/,
-                          _Float16* d_Bt, hipStream_t s);
-hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, int32_t Kp,
+hipError_t launch_key_hist(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq,
+                           int32_t* d_counts /*[nq][kKeyRange]*/, uint32_t* d_mask /*[kKeyRange/32], zeroed*/,
+                           int32_t* d_maxcount /*zeroed*/, hipStream_t s);
+// Row ranges of all kKeyRange keys' boxes at one tolerance (the engine caches them per index version).
+hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int64_t* d_rng_all /*[kKeyRange][2]*/,
+                                 hipStream_t s);
+// Vote path bookkeeping computed on the GPU by vote_compact (read by the later kernels).
+struct VoteMeta {
+  int32_t ku;  // used keys
+  int32_t kp;  // GEMM K: Ku + 1 (the packed-argmax column) rounded up to 16
+  int32_t ok;  // counts exact in fp16 and keys in range: else the host redoes the batch on the scan path
+  int32_t pad;
+};
+constexpr int32_t kVoteKpMax = ((kKeyRange + 1 + 15) / 16) * 16;
+hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
+                               int32_t* d_keycols /*[kKeyRange]*/, int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta,
+                               hipStream_t s);
+hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, const VoteMeta* d_meta,
+                          _Float16* d_A /*[Qp][kVoteKpMax]*/, hipStream_t s);
+hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
+                          _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
+hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
+
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
 // no host round trip between the stages. One block builds every query's per-key frame counts,
 // compacts the used keys and their "%f" boxes; one block per used key marks the clips with a row
@@ -86,7 +101,7 @@ struct SmallWork {              // device workspace of the small path
 // d_bk: [kKeyRange][Cp] bytes stamped with `epoch` (1..255, a new one per call; the caller clears
 // d_bk when the epoch wraps).
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int32_t* m1s, int64_t R,
+                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s);
 
 hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
