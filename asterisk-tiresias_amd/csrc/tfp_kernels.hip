@@ -654,6 +654,9 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
 #ifndef TFP8_HOIST_W
 #define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
 #endif
+#ifndef TFP8_RARE_AFTER
+#define TFP8_RARE_AFTER 1  // one wave-uniform rare test after the pair loop (not one branch per pair)
+#endif
 #ifndef TFP8_PAIRSPLIT
 #define TFP8_PAIRSPLIT 1  // real split per conjugate pair (k, 256 - k) on one lane (see the split)
 #endif
@@ -900,6 +903,8 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
         // bins 0 and 256 (lane 0) from Z[0], taken now so Y[0] is not kept alive
         const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
+        uint32_t umin = 0xffffffffu;
+        (void)umin;
 #pragma unroll
         for (int k2 = 0; k2 < 8; k2++) {
           cf own = Y[k2 == 0 ? 8 : 16 - k2];
@@ -921,13 +926,41 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           float nk = sqrtf_fast_cr(x), nk2 = sqrtf_fast_cr(x2);
           // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order instead
           const uint32_t m = min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u);
+#if TFP8_RARE_AFTER
+          umin = min(umin, m);
+#else
           if (__builtin_expect(__any(m < rare_m1), 0)) {
             if (x > 0.f && x < rare_thr) nk = 2.f * __builtin_sqrtf(split_power(y, p, w));
             if (x2 > 0.f && x2 < rare_thr) nk2 = 2.f * __builtin_sqrtf(split_power(p, y, w2));
           }
+#endif
           N[k] = nk;
           N[256 - k] = nk2;
         }
+#if TFP8_RARE_AFTER
+        if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
+#pragma unroll
+          for (int k2 = 0; k2 < 8; k2++) {
+            const cf own = Y[k2 == 0 ? 8 : 16 - k2];
+            cf y = Y[k2];
+            if (k2 == 0 && L == 0) y = own;
+            const cf p = L == 0 ? own : Pq[k2];
+            const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2);
+            const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
+            const cf E = addsub(y, p);
+            const cf O = subadd(y, p);
+            const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+            const cf Sv = E + Tt;
+            const cf O2 = cf{-O.x, O.y};
+            const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
+            const cf S2 = cf{E.x, -E.y} + T2;
+            const float x = Sv.x * Sv.x + Sv.y * Sv.y, x2 = S2.x * S2.x + S2.y * S2.y;
+            const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
+            if (x > 0.f && x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
+            if (x2 > 0.f && x2 < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
+          }
+        }
+#endif
         if (L == 0) {
           N[0] = n0;
           N[256] = n256;
