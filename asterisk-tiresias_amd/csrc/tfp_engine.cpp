@@ -236,7 +236,7 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
     d_toff = e->toff.as<int32_t>();
     d_tclip = e->tclip.as<int32_t>();
   }
-  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips],
+  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips], nf,
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
@@ -642,7 +642,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
-                               p->d_tclip.as<int32_t>(), p->ntiles, d_micro, d_db, s));
+                               p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s));
   return TFP_OK;
 }
 
@@ -899,7 +899,8 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
   HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
-                               p->d_tclip.as<int32_t>(), p->ntiles, e->micro.as<int32_t>(), e->db.as<double>(), s));
+                               p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
+                               e->db.as<double>(), s));
   std::vector<unsigned long long> keys;
   return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
                      reinterpret_cast<unsigned long long*>(d_keys), s);
@@ -1011,7 +1012,7 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
   HIPCHK(e, launch_fingerprint(Tb, fx, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
-                               st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na],
+                               st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na], fo[na],
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   std::vector<unsigned long long> keys;
   if ((rc = search_core(e, fo.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;

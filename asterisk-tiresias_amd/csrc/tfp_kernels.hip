@@ -654,6 +654,9 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
 #ifndef TFP8_HOIST_W
 #define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
 #endif
+#ifndef TFP8_SPLIT_TAIL
+#define TFP8_SPLIT_TAIL 1  // the tile tail stores the DCT coefficient; dB and "%f" run in finish_db_kernel
+#endif
 #ifndef TFP8_RARE_AFTER
 #define TFP8_RARE_AFTER 1  // one wave-uniform rare test after the pair loop (not one branch per pair)
 #endif
@@ -1073,10 +1076,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         float acc = 0.f;
 #pragma unroll 8
         for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
-        const double q = db_of_coef(acc);
         const int64_t g = foff[cur.c] + f;
+#if TFP8_SPLIT_TAIL
+        micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
+#else
+        const double q = db_of_coef(acc);
         micro[2 * g + cfi] = micro_of_db(q);
         if (db) db[2 * g + cfi] = q;
+#endif
       }
     }
     wave_sync();
@@ -1360,6 +1367,17 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_pip
   }
 }
 
+// 10*log10|c| (fp_handler.c:651) and "%f" micro-units / NULL (db_ctx_handler.c:479-481) of every
+// coefficient fingerprint8k_kernel stored (as float bits) in micro[], in place, on full waves: the
+// kernel's tile tail would run this double-precision work on 32 of 64 lanes.
+__global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict__ db, int64_t nvals) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += (int64_t)gridDim.x * blockDim.x) {
+    const double q = db_of_coef(__builtin_bit_cast(float, micro[i]));
+    micro[i] = micro_of_db(q);
+    if (db) db[i] = q;
+  }
+}
+
 bool DspTables_fixed8k(const DspTables& t) {
   return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
@@ -1367,7 +1385,8 @@ bool DspTables_fixed8k(const DspTables& t) {
 
 hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                              const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s) {
+                              const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
+                              hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
   static int grid_cap[2] = {0, 0};
   // Test/A-B knobs, read per launch: TFP_GENERIC=1 runs the generic kernel at 8 kHz too;
@@ -1394,9 +1413,16 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int
     if (pp && atoi(pp))
       hipLaunchKernelGGL(fingerprint8k_pipe_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                          d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
-    else
+    else {
       hipLaunchKernelGGL(fingerprint8k_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                          d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+#if TFP8_SPLIT_TAIL
+      const int64_t nv = 2 * nframes;
+      int64_t g = (nv + 255) / 256;
+      if (g > 8192) g = 8192;
+      if (nv > 0) hipLaunchKernelGGL(finish_db_kernel, dim3((unsigned)g), dim3(256), 0, s, d_micro, d_db, nv);
+#endif
+    }
     return hipGetLastError();
   }
   static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production

@@ -40,7 +40,8 @@ struct SynthSpecDev {
 bool DspTables_fixed8k(const DspTables& t);
 hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                              const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s);
+                              const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
+                              hipStream_t s);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
 
