@@ -161,7 +161,7 @@ def main():
         "config": {"workload": f"configs[1]: {nclips} x {args.seconds} s 8 kHz mono clips per GPU, fingerprint-only",
                    "clips_per_gpu": nclips, "samples_per_clip": n, "frames_per_step_per_gpu": F,
                    "parallelism": f"clip-sharded x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "fingerprint8k_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
+        "roofline": {"bound": "hbm", "kernel": "fingerprint8k_kernel + finish_db_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_unit": BYTES_PER_FP, "units_per_launch": F, "avg_launch_ms": avg_launch_s * 1e3},
     }

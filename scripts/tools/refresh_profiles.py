@@ -28,20 +28,27 @@ subprocess.run([sys.executable, os.path.join(REPO, "scripts", "tools", "c2_dispa
                 os.path.join(dst, "fingerprint_c2_dispatches.csv")], check=True)
 
 
+FIN_GRID = min(8192, (2 * C2_FRAMES + 255) // 256) * 256  # finish_db_kernel's grid for a C2 step
+
+
 def pmc(counter):
+    """Mean counter value per C2 step: fingerprint kernel (largest grid) + its finish_db_kernel."""
     path = os.path.join(src, "%s_pmc_%s" % (R, counter), "run_counter_collection.csv")
     shutil.copy(path, os.path.join(dst, "pmc_%s.csv" % counter))
-    rows = [r for r in csv.DictReader(open(path)) if re.search(r"fingerprint(8k)?_kernel", r["Kernel_Name"])]
-    grid = max(int(r["Grid_Size"]) for r in rows)
-    vals = [float(r["Counter_Value"]) for r in rows if int(r["Grid_Size"]) == grid]
-    return sum(vals) / len(vals)
+    rows = list(csv.DictReader(open(path)))
+    fp = [r for r in rows if re.search(r"fingerprint(8k)?_kernel", r["Kernel_Name"])]
+    grid = max(int(r["Grid_Size"]) for r in fp)
+    vals = [float(r["Counter_Value"]) for r in fp if int(r["Grid_Size"]) == grid]
+    fin = [float(r["Counter_Value"]) for r in rows
+           if "finish_db_kernel" in r["Kernel_Name"] and int(r["Grid_Size"]) == FIN_GRID]
+    return sum(vals) / len(vals) + (sum(fin) / len(fin) if fin else 0.0)
 
 
 fetch_kb, write_kb = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
 hbm = (2 * fetch_kb + write_kb) * 1024.0
 alg = 520 * C2_FRAMES
 out = {
-    "kernel": "fingerprint8k_kernel",
+    "kernel": "fingerprint8k_kernel + finish_db_kernel (one C2 step)",
     "frames_per_launch": C2_FRAMES,
     "hbm_bytes_per_launch": hbm,
     "fetch_size_kb_raw": fetch_kb,
