@@ -23,6 +23,8 @@ C2_FRAMES = 960512
 for f in ("bench_kernel_stats.csv", "bench_kernel_trace.csv", "bench_domain_stats.csv"):
     shutil.copy(os.path.join(src, R + "_trace", f), os.path.join(dst, f))
 shutil.copy(os.path.join(src, R + "_trace.json"), os.path.join(dst, "bench_under_rocprof.json"))
+# untimed steps before the timed ones: --warmup plus bench.py's clock warm-up steps
+warm = str(int(warm) + json.load(open(os.path.join(dst, "bench_under_rocprof.json"))).get("clock_warmup_steps", 0))
 subprocess.run([sys.executable, os.path.join(REPO, "scripts", "tools", "c2_dispatches.py"),
                 os.path.join(dst, "bench_kernel_trace.csv"), warm, steps,
                 os.path.join(dst, "fingerprint_c2_dispatches.csv")], check=True)
