@@ -654,6 +654,9 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
 #ifndef TFP8_HOIST_W
 #define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
 #endif
+#ifndef TFP8_MELB
+#define TFP8_MELB 0  // > 0: filterbank loads issued in groups of this many 4-bin steps (register pressure)
+#endif
 #ifndef TFP8_SPLIT_TAIL
 #define TFP8_SPLIT_TAIL 1  // the tile tail stores the DCT coefficient; dB and "%f" run in finish_db_kernel
 #endif
@@ -679,6 +682,30 @@ __device__ __forceinline__ int col_of_lane(int L) {
 
 __device__ __forceinline__ float mirror16(float v) {  // lane 15 - L of the 16-lane row
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xf, 0xf, false));
+}
+
+template <int LEN, int BATCH>
+__device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const float* __restrict__ w, int st) {
+  constexpr int G = LEN / 4, B = BATCH < G ? BATCH : G;
+  float acc = 0.f;
+#pragma unroll
+  for (int i0 = 0; i0 < G; i0 += B) {
+    float4 wv[B], nv[B];
+#pragma unroll
+    for (int i = 0; i < B; i++)
+      if (i0 + i < G) {
+        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
+        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
+      }
+#pragma unroll
+    for (int i = 0; i < B; i++)
+      if (i0 + i < G) {
+        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
+        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
+        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+      }
+  }
+  return acc;
 }
 
 __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_kernel(
@@ -1043,11 +1070,18 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         if (c_real) lrow[fC] = N[L + 32];
       } else {
         const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+#if TFP8_MELB
+        (void)wA; (void)wB; (void)wC;
+        const float aC = mel_sum_b<LC, TFP8_MELB>(N, wbase + S.ms_woff[2], stC);
+        const float aB = mel_sum_b<LB, TFP8_MELB>(N, wbase + S.ms_woff[1], stB);
+        const float aA = mel_sum_b<LA, TFP8_MELB>(N, wbase + S.ms_woff[0], stA);
+#else
         if (!(TFP8_HOIST_W & 1)) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
         if (!(TFP8_HOIST_W & 2)) load_w<LA>(wbase + S.ms_woff[0], wA);
         const float aC = mel_sum_w<LC>(N, wC, stC);
         const float aB = mel_sum_w<LB>(N, wB, stB);
         const float aA = mel_sum_w<LA>(N, wA, stA);
+#endif
         const float lA = (TFP8_ABL & 8) ? aA : aubio_log10_fast(aA, S.logf);
         const float lB = (TFP8_ABL & 8) ? aB : aubio_log10_fast(aB, S.logf);
         lrow[fA] = lA;
@@ -1109,30 +1143,6 @@ struct WaveLds8P {
   alignas(16) float nbuf[4][kNRow];
   float logs[kWaveFrames * kLogStride];
 };
-
-template <int LEN, int BATCH>
-__device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const float* __restrict__ w, int st) {
-  constexpr int G = LEN / 4, B = BATCH < G ? BATCH : G;
-  float acc = 0.f;
-#pragma unroll
-  for (int i0 = 0; i0 < G; i0 += B) {
-    float4 wv[B], nv[B];
-#pragma unroll
-    for (int i = 0; i < B; i++)
-      if (i0 + i < G) {
-        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
-        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
-      }
-#pragma unroll
-    for (int i = 0; i < B; i++)
-      if (i0 + i < G) {
-        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
-        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
-        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
-      }
-  }
-  return acc;
-}
 
 __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_pipe_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
