@@ -158,7 +158,7 @@ int ensure_tables(tfp_engine* e, int sr, const DspTables** out, bool* fixed8k = 
 
 // Clip layout: sample, frame and 16-frame-tile offsets.
 void layout(const int64_t* offsets, int32_t nclips, std::vector<int64_t>& soff, std::vector<int64_t>& foff,
-            std::vector<int32_t>& toff, std::vector<int32_t>* tclip = nullptr) {
+            std::vector<int32_t>& toff, std::vector<int32_t>* tclip = nullptr, int tile_frames = kFramesPerBlock) {
   soff.assign(offsets, offsets + nclips + 1);
   const int64_t base = soff[0];
   for (auto& v : soff) v -= base;
@@ -167,7 +167,7 @@ void layout(const int64_t* offsets, int32_t nclips, std::vector<int64_t>& soff, 
   for (int32_t c = 0; c < nclips; c++) {
     const int64_t nf = tfp_frame_count(soff[c + 1] - soff[c]);
     foff[c + 1] = foff[c] + nf;
-    toff[c + 1] = toff[c] + (int32_t)((nf + kFramesPerBlock - 1) / kFramesPerBlock);
+    toff[c + 1] = toff[c] + (int32_t)((nf + tile_frames - 1) / tile_frames);
   }
   if (tclip) {
     tclip->assign(std::max<int32_t>(toff[nclips], 1), 0);
@@ -191,7 +191,14 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   if (rc) return rc;
   std::vector<int64_t> soff, foff;
   std::vector<int32_t> toff, tclip;
-  layout(offsets, nclips, soff, foff, toff, &tclip);
+  // small batches at 8 kHz: 4-frame wave tiles (4x the waves, a quarter of the per-wave passes)
+  int tile_frames = kFramesPerBlock;
+  if (fx) {
+    int64_t nf16 = 0;
+    for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(offsets[c + 1] - offsets[c]) + 15) / 16;
+    if (nf16 <= 256) tile_frames = 4;
+  }
+  layout(offsets, nclips, soff, foff, toff, &tclip, tile_frames);
   const int64_t ns = soff[nclips], nf = foff[nclips];
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
@@ -236,7 +243,7 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
     d_toff = e->toff.as<int32_t>();
     d_tclip = e->tclip.as<int32_t>();
   }
-  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips], nf,
+  HIPCHK(e, launch_fingerprint(T, fx, tile_frames, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips], nf,
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
@@ -640,7 +647,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s));
   return TFP_OK;
@@ -897,7 +904,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(T, fx, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
                                e->db.as<double>(), s));
@@ -1011,7 +1018,7 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
     return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
-  HIPCHK(e, launch_fingerprint(Tb, fx, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
+  HIPCHK(e, launch_fingerprint(Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
                                st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na], fo[na],
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   std::vector<unsigned long long> keys;

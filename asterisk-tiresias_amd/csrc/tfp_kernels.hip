@@ -708,6 +708,9 @@ __device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const fl
   return acc;
 }
 
+// kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
+// small batches: 4x the waves on a short query, a quarter of the per-wave latency).
+template <int kPasses>
 __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
@@ -793,7 +796,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #endif
   {
     const float lempty = aubio_log10_fast(0.f, S.logf);
-    for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
+    for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
       const int j = i % kFilters;
       if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
     }
@@ -807,7 +810,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   auto tile_of = [&](int b) {
     Tile t;
     t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
-    t.f0 = (int64_t)(b - toff[t.c]) * kWaveFrames;
+    t.f0 = (int64_t)(b - toff[t.c]) * (4 * kPasses);
     t.s0 = sbeg[t.c];
     t.ns = send[t.c] - t.s0;
     return t;
@@ -842,7 +845,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const int bn = b + nwaves;
     const Tile nxt = bn < ntiles ? tile_of(bn) : cur;
 
-    for (int sub = 0; sub < 4; sub++) {
+    for (int sub = 0; sub < kPasses; sub++) {
       const int row = sub * 4 + grp;
       wave_sync();  // the previous pass's readers of the scratch are done
 #pragma unroll
@@ -851,7 +854,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         if (chunk < kPassChunks)
           *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
       }
-      if (sub < 3) fetch(cur, sub + 1, true, pf);
+      if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
       else fetch(nxt, 0, bn < ntiles, pf);
       wave_sync();
       const int16_t* hop0 = M.pcm + grp * kHopStride;
@@ -1090,7 +1093,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
-    if (lane < 2 * kWaveFrames) {  // the deferred slot-2 logs: lane = (frame row, filter)
+    if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];
       if (f >= 0) {
         float* p = M.logs + (lane >> 1) * kLogStride + f;
@@ -1098,11 +1101,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
-    if ((TFP8_ABL & 16) && lane < 2 * kWaveFrames) {
+    if ((TFP8_ABL & 16) && lane < 2 * 4 * kPasses) {
       const int row = lane >> 1, cfi = lane & 1;
       const int64_t f = cur.f0 + row;
       if (f < nf) micro[2 * (foff[cur.c] + f) + cfi] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cfi]);
-    } else if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
+    } else if (lane < 2 * 4 * kPasses) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
       const int row = lane >> 1, cfi = lane & 1;
       const int64_t f = cur.f0 + row;
       if (f < nf) {
@@ -1393,10 +1396,11 @@ bool DspTables_fixed8k(const DspTables& t) {
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
 }
 
-hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
-                              const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
+hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t tile_frames, const int16_t* d_pcm,
+                              const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
                               const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
                               hipStream_t s) {
+  if (tile_frames != 16 && !(tile_frames == 4 && fixed8k)) return hipErrorInvalidValue;
   if (ntiles <= 0) return hipSuccess;
   static int grid_cap[2] = {0, 0};
   // Test/A-B knobs, read per launch: TFP_GENERIC=1 runs the generic kernel at 8 kHz too;
@@ -1412,7 +1416,7 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int
     int dev = 0, cus = 256, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (v) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint8k_kernel, kBlockThreads, 0);
+    if (v) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint8k_kernel<4>, kBlockThreads, 0);
     else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, kBlockThreads, 0);
     grid_cap[v] = cus * (per > 0 ? per : 1);
   }
@@ -1420,12 +1424,16 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int
   const int grid = want < grid_cap[v] ? want : grid_cap[v];
   if (v) {
     const char* pp = getenv("TFP_PIPE");
-    if (pp && atoi(pp))
+    if (pp && atoi(pp) && tile_frames == 16)
       hipLaunchKernelGGL(fingerprint8k_pipe_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                          d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
     else {
-      hipLaunchKernelGGL(fingerprint8k_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+      if (tile_frames == 4)
+        hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                           d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
+      else
+        hipLaunchKernelGGL(fingerprint8k_kernel<4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                           d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
 #if TFP8_SPLIT_TAIL
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
@@ -1902,37 +1910,73 @@ __global__ __launch_bounds__(256) void small_mark_kernel(const SmallWork* __rest
   }
 }
 
-// Clip-parallel scores of every query; the per-query max of score << 32 | tie key (a later uuid
-// wins a tie, as SQLite's ORDER BY count(*) DESC returns it).
+// Clip-parallel scores of every query (4 clips per thread: one 32-bit stamp word per key row);
+// the per-query max of score << 32 | tie key (a later uuid wins a tie, as SQLite's
+// ORDER BY count(*) DESC returns it), reduced per block before one atomicMax per block.
 __global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__ w, const uint8_t* __restrict__ bk,
                                                          int32_t Cp, int32_t C, int32_t nq,
                                                          const int32_t* __restrict__ tiekey, uint8_t epoch) {
   __shared__ int32_t A[kSmallQ][kKeyRange];
+  __shared__ unsigned long long bmax[kSmallQ][4];
   const int ku = w->ku;
   if (w->bad || ku == 0) return;  // no used key: every frame ignored -> NOTFOUND (best stays 0)
   for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = w->A[i / ku][i % ku];
   __syncthreads();
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  int32_t sc[kSmallQ];
+  const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);  // first of this thread's 4 clips
+  int32_t sc[kSmallQ][4];
 #pragma unroll
-  for (int qi = 0; qi < kSmallQ; qi++) sc[qi] = 0;
-  if (c < C) {
-    for (int kc = 0; kc < ku; kc++) {
-      if (bk[(int64_t)kc * Cp + c] == epoch) {
+  for (int qi = 0; qi < kSmallQ; qi++)
 #pragma unroll
-        for (int qi = 0; qi < kSmallQ; qi++) sc[qi] += qi < nq ? A[qi][kc] : 0;
+    for (int j = 0; j < 4; j++) sc[qi][j] = 0;
+  if (c4 < C) {
+    const uint32_t ep4 = 0x01010101u * epoch;
+    int kc = 0;
+    for (; kc + 4 <= ku; kc += 4) {  // 4 independent row loads in flight
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint32_t*>(bk + (int64_t)(kc + u) * Cp + c4);
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t x = v[u] ^ ep4;  // byte j == 0 <=> clip c4 + j stamped this call
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (((x >> (8 * j)) & 0xffu) == 0u)
+#pragma unroll
+            for (int qi = 0; qi < kSmallQ; qi++) sc[qi][j] += qi < nq ? A[qi][kc + u] : 0;
       }
     }
+    for (; kc < ku; kc++) {
+      const uint32_t x = *reinterpret_cast<const uint32_t*>(bk + (int64_t)kc * Cp + c4) ^ ep4;
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (((x >> (8 * j)) & 0xffu) == 0u)
+#pragma unroll
+          for (int qi = 0; qi < kSmallQ; qi++) sc[qi][j] += qi < nq ? A[qi][kc] : 0;
+    }
   }
-  const unsigned tk = c < C ? (unsigned)tiekey[c] : 0u;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int qi = 0; qi < nq; qi++) {
-    unsigned long long key = sc[qi] > 0 ? (((unsigned long long)(unsigned)sc[qi] << 32) | tk) : 0ull;
+    unsigned long long key = 0ull;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const int c = c4 + j;
+      if (c < C && sc[qi][j] > 0) {
+        const unsigned long long k = ((unsigned long long)(unsigned)sc[qi][j] << 32) | (unsigned)tiekey[c];
+        key = k > key ? k : key;
+      }
+    }
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) {
       const unsigned long long o = __shfl_xor(key, off, 64);
       key = o > key ? o : key;
     }
-    if ((threadIdx.x & 63) == 0 && key) atomicMax(&w->best[qi], key);
+    if (lane == 0) bmax[qi][wv] = key;
+  }
+  __syncthreads();
+  if (threadIdx.x < nq) {
+    unsigned long long key = bmax[threadIdx.x][0];
+    for (int i = 1; i < 4; i++) key = bmax[threadIdx.x][i] > key ? bmax[threadIdx.x][i] : key;
+    if (key && key > w->best[threadIdx.x]) atomicMax(&w->best[threadIdx.x], key);  // read first: few atomics
   }
 }
 
@@ -1942,7 +1986,7 @@ hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, Search
   if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, d_rng_all, d_work);
   hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_work, d_bk, Cp, cols, epoch);
-  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 255) / 256), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey,
+  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 1023) / 1024), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey,
                      epoch);
   return hipGetLastError();
 }

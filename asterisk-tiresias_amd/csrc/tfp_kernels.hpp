@@ -38,7 +38,8 @@ struct SynthSpecDev {
 // fixed8k: the tables' filterbank schedule is the 8 kHz one (DspTables_fixed8k), so the
 // specialized fingerprint8k_kernel runs; otherwise the generic fingerprint_kernel.
 bool DspTables_fixed8k(const DspTables& t);
-hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, const int16_t* d_pcm, const int64_t* d_sbeg,
+// tile_frames: frames per wave tile in toff/tclip, 16 (any rate) or 4 (8 kHz only: small batches).
+hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t tile_frames, const int16_t* d_pcm, const int64_t* d_sbeg,
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
                               const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
                               hipStream_t s);
