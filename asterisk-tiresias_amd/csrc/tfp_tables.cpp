@@ -37,6 +37,68 @@ void twiddles(int N, int count, float* re, float* im) {
     im[j] = (float)(-sin(t));
   }
 }
+// Filterbank lane order with few LDS bank conflicts. The kernels read |X| for 4 bins per lane
+// with ds_read_b128 from per-frame rows that start at 16-B slot 136 g + 4 (g & 1) (frame g of a
+// wave: fingerprint_kernel / fingerprint8k_kernel's |X| row). Such a read is served in four
+// 16-lane groups; two lanes of a group collide when they read different slots that are equal
+// mod 16. Which lane computes which filter of a slot is free (each sum goes to its filter's log
+// row), so this permutes the slot's lanes to minimise the modelled extra cycles: deterministic
+// random restarts + pairwise swaps.
+int bank_cost(const int32_t* filt, const int32_t* start, const int* perm, int len) {
+  static const int G[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                               {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                               {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                               {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+  int extra = 0;
+  for (int i = 0; i < len / 4; i++)
+    for (int g = 0; g < 4; g++) {
+      int slot_of_bank[16], cnt[16];
+      for (int b = 0; b < 16; b++) { slot_of_bank[b] = -1; cnt[b] = 0; }
+      int worst = 0;
+      for (int k = 0; k < 16; k++) {
+        const int l = G[g][k], fr = l >> 4, L = l & 15;
+        if (filt[perm[L]] < 0) continue;
+        const int sl = 136 * fr + 4 * (fr & 1) + start[perm[L]] / 4 + i;
+        const int b = sl & 15;
+        // distinct slots on one bank group cost a cycle each (same slot broadcasts); lanes of one
+        // frame never share a slot, lanes of two frames do only by coincidence: count distinct
+        if (slot_of_bank[b] != sl) { cnt[b]++; slot_of_bank[b] = sl; }
+        if (cnt[b] > worst) worst = cnt[b];
+      }
+      extra += worst > 0 ? worst - 1 : 0;
+    }
+  return extra;
+}
+
+void lane_order_for_banks(int32_t* filt, int32_t* start, int len) {
+  int best[16], perm[16];
+  for (int L = 0; L < 16; L++) best[L] = L;
+  int best_cost = bank_cost(filt, start, best, len);
+  uint32_t rng = 0x9e3779b9u;
+  for (int rs = 0; rs < 64 && best_cost > 0; rs++) {
+    for (int L = 0; L < 16; L++) perm[L] = L;
+    for (int L = 15; L > 0; L--) {  // Fisher-Yates with an LCG: deterministic
+      rng = rng * 1664525u + 1013904223u;
+      const int r = (int)((rng >> 8) % (uint32_t)(L + 1));
+      const int x = perm[L]; perm[L] = perm[r]; perm[r] = x;
+    }
+    int c = bank_cost(filt, start, perm, len);
+    for (bool improved = true; improved;) {
+      improved = false;
+      for (int a = 0; a < 16; a++)
+        for (int b = a + 1; b < 16; b++) {
+          int x = perm[a]; perm[a] = perm[b]; perm[b] = x;
+          const int c2 = bank_cost(filt, start, perm, len);
+          if (c2 < c) { c = c2; improved = true; }
+          else { x = perm[a]; perm[a] = perm[b]; perm[b] = x; }
+        }
+    }
+    if (c < best_cost) { best_cost = c; for (int L = 0; L < 16; L++) best[L] = perm[L]; }
+  }
+  int32_t f2[16], s2[16];
+  for (int L = 0; L < 16; L++) { f2[L] = filt[best[L]]; s2[L] = start[best[L]]; }
+  for (int L = 0; L < 16; L++) { filt[L] = f2[L]; start[L] = s2[L]; }
+}
 }  // namespace
 
 void build_mel_dense(int sample_rate, float (*mel)[kBins]) {
@@ -136,6 +198,7 @@ bool build_tables(int sample_rate, DspTables* t) {
       if (j >= 0 && t->mel_len[j] && lead[j] + t->mel_len[j] > len) len = lead[j] + t->mel_len[j];
     }
     len = (len + 3) & ~3;
+    lane_order_for_banks(t->ms_filter[sl], t->ms_start[sl], len);
     t->ms_len[sl] = len;
     t->ms_woff[sl] = woff;
     for (int L = 0; L < 16; L++)
