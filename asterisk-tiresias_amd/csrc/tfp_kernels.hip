@@ -654,6 +654,9 @@ __device__ __forceinline__ float mel_sum(const float* __restrict__ N, const floa
 #ifndef TFP8_HOIST_W
 #define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
 #endif
+#ifndef TFP8_GLDS
+#define TFP8_GLDS 0  // PCM staged by LDS-DMA into two per-wave buffers (vs registers + ds_write_b128)
+#endif
 #ifndef TFP8_MELB
 #define TFP8_MELB 0  // > 0: filterbank loads issued in groups of this many 4-bin steps (register pressure)
 #endif
@@ -720,6 +723,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
+#if TFP8_GLDS
+  // two PCM staging buffers per wave, filled by LDS-DMA one pass ahead (hop h at h * kHopStride)
+  __shared__ __attribute__((aligned(16))) int16_t PB[kBlockWaves][2][5 * kHopStride];
+#endif
   const int tid = threadIdx.x;
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
@@ -817,6 +824,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   };
   // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
   auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
+    (void)pf;
     const int16_t* clip = pcm + t.s0;
     const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
     const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
@@ -836,10 +844,45 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
   };
 
+#if TFP8_GLDS
+  // One pass's 5 hops into buf: interior passes by LDS-DMA (global_load_lds_dwordx4, one 32-lane
+  // instruction per hop so each lands in its padded row), edge passes by checked loads + ds_write.
+  auto issue = [&](const Tile& t, int sub, bool valid, int16_t* buf) {
+    if (!valid) return;
+    const int16_t* clip = pcm + t.s0;
+    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
+    const bool interior = ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
+    if (interior) {
+      if (lane < 32) {
+#pragma unroll
+        for (int h = 0; h < 5; h++)
+          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(clip + sb + h * kHop + 8 * lane),
+                                           (__attribute__((address_space(3))) void*)(buf + h * kHopStride), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        if (chunk < kPassChunks)
+          *reinterpret_cast<int4*>(buf + (chunk >> 5) * kHopStride + (chunk & 31) * 8) =
+              fetch_chunk_checked(clip, t.ns, sb + 8 * chunk);
+      }
+    }
+  };
+  int16_t* const pb0 = PB[wave][0];
+  int16_t* const pb1 = PB[wave][1];
+  int par = 0;
+#endif
   int4 pf[kChunkRounds];
   int b = blockIdx.x * kBlockWaves + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
+#if TFP8_GLDS
+  issue(cur, 0, b < ntiles, pb0);
+  (void)pf;
+  (void)fetch;
+#else
   fetch(cur, 0, b < ntiles, pf);
+#endif
   for (; b < ntiles; b += nwaves) {
     const int64_t nf = (cur.ns + kHop - 1) / kHop;
     const int bn = b + nwaves;
@@ -848,16 +891,31 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     for (int sub = 0; sub < kPasses; sub++) {
       const int row = sub * 4 + grp;
       wave_sync();  // the previous pass's readers of the scratch are done
+#if TFP8_GLDS
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pass's hops have landed in LDS
+      int16_t* const pcur = par ? pb1 : pb0;
+      // the other buffer was read by the previous pass: refill it for the next pass now
+      if (sub < kPasses - 1) issue(cur, sub + 1, true, par ? pb0 : pb1);
+      else issue(nxt, 0, bn < ntiles, par ? pb0 : pb1);
+      par ^= 1;
+#else
+      if constexpr (!(TFP8_ABL & 32)) {
 #pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        if (chunk < kPassChunks)
-          *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+        for (int r = 0; r < kChunkRounds; r++) {
+          const int chunk = lane + 64 * r;
+          if (chunk < kPassChunks)
+            *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+        }
+        if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
+        else fetch(nxt, 0, bn < ntiles, pf);
       }
-      if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
-      else fetch(nxt, 0, bn < ntiles, pf);
+#endif
       wave_sync();
+#if TFP8_GLDS
+      const int16_t* hop0 = pcur + grp * kHopStride;
+#else
       const int16_t* hop0 = M.pcm + grp * kHopStride;
+#endif
       int oz = 0;
       asm volatile("" : "+v"(oz));
 #if !TFP8_WIN_REGS
