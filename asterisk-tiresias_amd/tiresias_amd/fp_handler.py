@@ -165,6 +165,51 @@ class FpHandler:
             return False
         return True
 
+    def create_new_audio_info(self, context: str) -> bool:
+        """app_tiresias.c:365-424 (the module's directory enrolment) batched onto the GPU.
+
+        The reference scans the context's directory (alphasort, without "." and "..") and calls
+        fp_craete_audio_list_info per file, skipping files that fail. Here the same catalog rows
+        are written in the same order and with the same per-context MD5 dedup (also among the
+        files of this scan). The fingerprints of all new files are computed by one
+        tfp_fingerprint_batch call per sample rate and enrolled by one tfp_index_add_batch."""
+        ctx = self.fp_get_context_list_info(context) if context is not None else None
+        if ctx is None or ctx["directory"] is None:
+            return False
+        directory = ctx["directory"]
+        try:
+            names = sorted(n for n in os.listdir(directory) if n not in (".", ".."))
+        except OSError:
+            return False
+        new = []  # (uuid, path, pcm, rate)
+        seen = set()
+        for name in names:
+            path = "%s/%s" % (directory, name)
+            h = self.fp_create_hash(path)
+            if h is None:
+                continue  # "Could not create fingerprint info."
+            if h in seen or self.db.execute("select * from audio_list where context = ? and hash = ?;",
+                                            (context, h)).fetchone():
+                continue  # already enrolled
+            try:
+                pcm, sr = read_wav_mono16(path)
+            except (OSError, ValueError, EOFError, wave.Error):
+                continue
+            uuid = self.fp_generate_uuid()
+            self.db.execute("insert into audio_list(uuid, name, context, hash) values (?, ?, ?, ?);",
+                            (uuid, os.path.basename(path), context, h))
+            seen.add(h)
+            new.append((uuid, pcm, sr))
+        for sr in sorted({n[2] for n in new}):
+            group = [n for n in new if n[2] == sr]
+            lens = [len(n[1]) for n in group]
+            off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+            fr = self.engine.fingerprint_batch(np.concatenate([n[1] for n in group]) if group else np.zeros(0, np.int16),
+                                               off, sr)
+            foff = np.concatenate([[0], np.cumsum([(n + 255) // 256 for n in lens])]).astype(np.int64)
+            self.engine.index_add_batch([n[0] for n in group], foff, fr["m1"], fr["m2"])
+        return True
+
     def fp_delete_audio_list_info(self, uuid: str) -> bool:
         """fp_handler.c:115-159: audio_list row + its fingerprint rows."""
         if uuid is None:
