@@ -577,7 +577,8 @@ void tfp_engine_destroy(tfp_engine* e) {
   (void)hipStreamDestroy(s);
 }
 
-const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : "null engine"; }
+__attribute__((visibility("hidden"))) const char* tfp_ingest_last_error();  // tfp_wav.cpp: engine-less errors of this thread
+const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : tfp_ingest_last_error(); }
 
 int tfp_fingerprint_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
                           tfp_frame* out, int64_t cap, int64_t* nframes) {

@@ -15,7 +15,7 @@ HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "tiresias_fp.h")
 
 TFP_OK = 0
 ERRORS = {-1: "TFP_E_ARG", -2: "TFP_E_HIP", -3: "TFP_E_NOMEM", -4: "TFP_E_NOENT", -5: "TFP_E_CAPACITY",
-          -6: "TFP_E_EXISTS", -7: "TFP_E_NODEV"}
+          -6: "TFP_E_EXISTS", -7: "TFP_E_NODEV", -8: "TFP_E_FORMAT"}
 NULL_MICRO = -(2**31)
 
 
@@ -52,6 +52,8 @@ _SIGS = {
     "tfp_engine_destroy": (None, [P]),
     "tfp_engine_last_error": (C.c_char_p, [P]),
     "tfp_frame_count": (C.c_int64, [C.c_int64]),
+    "tfp_wav_decode": (C.c_int, [P, C.c_int64, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "tfp_wav_read": (C.c_int, [C.c_char_p, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_fingerprint_pcm": (C.c_int, [P, P, C.c_int64, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
     "tfp_fingerprint_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
     "tfp_plan_create": (C.c_int, [P, P, C.c_int32, C.c_int32, C.POINTER(P)]),
@@ -107,7 +109,7 @@ def lib() -> C.CDLL:
 
 
 def check(rc: int, eng=None):
+    """Raise TfpError for a non-OK code; eng None reads the thread's engine-less error."""
     if rc != TFP_OK:
-        msg = lib().tfp_engine_last_error(eng).decode() if eng else ""
-        raise TfpError(rc, msg)
+        raise TfpError(rc, lib().tfp_engine_last_error(eng).decode())
     return rc

@@ -26,6 +26,27 @@ def params(coefs=1, tolerance=-1.0, freq_ignore_low=-1, freq_ignore_high=-1) -> 
     return SearchParams(int(coefs), int(freq_ignore_low), int(freq_ignore_high), 0, float(tolerance))
 
 
+def _wav(call) -> tuple[np.ndarray, int]:
+    n, sr = C.c_int64(), C.c_int32()
+    check(call(None, 0, C.byref(n), C.byref(sr)))
+    pcm = np.empty(n.value, np.int16)
+    check(call(pcm.ctypes.data, n.value, C.byref(n), C.byref(sr)))
+    return pcm, sr.value
+
+
+def decode_wav(data: bytes) -> tuple[np.ndarray, int]:
+    """tfp_wav_decode: RIFF/WAVE bytes -> (mono int16 PCM, native rate), aubio_source semantics
+    (fp_handler.c:37, :604, :633). TfpError(TFP_E_FORMAT) for audio the engine cannot take exactly."""
+    buf = C.create_string_buffer(bytes(data), len(data))
+    return _wav(lambda pcm, cap, n, sr: lib().tfp_wav_decode(buf, len(data), pcm, cap, n, sr))
+
+
+def read_wav(path: str) -> tuple[np.ndarray, int]:
+    """tfp_wav_read: decode_wav of a file."""
+    p = path.encode()
+    return _wav(lambda pcm, cap, n, sr: lib().tfp_wav_read(p, pcm, cap, n, sr))
+
+
 def synth_specs(seed: int, clips, offsets=None):
     clips = list(clips)
     offsets = [0] * len(clips) if offsets is None else list(offsets)

@@ -26,22 +26,18 @@ import wave
 import numpy as np
 
 from . import dbio
-from .engine import Engine, params
+from ._lib import TfpError
+from .engine import Engine, params, read_wav
 
 DEF_SEARCH_TOLERANCE = 0.001  # fp_handler.c:41
 DEF_AUBIO_COEFS = 2           # fp_handler.c:39
 
 
 def read_wav_mono16(filename: str):
-    """aubio_source at the file's native rate (DEF_AUBIO_SAMPLERATE 0): int16 PCM + rate."""
-    with wave.open(filename, "rb") as w:
-        if w.getsampwidth() != 2:
-            raise ValueError("only 16-bit PCM WAV is supported")
-        if w.getnchannels() != 1:
-            raise ValueError("only mono WAV is supported (multichannel downmix is out of scope)")
-        sr = w.getframerate()
-        data = np.frombuffer(w.readframes(w.getnframes()), dtype="<i2").astype(np.int16)
-    return data, sr
+    """aubio_source at the file's native rate (DEF_AUBIO_SAMPLERATE 0, fp_handler.c:37, :604):
+    int16 PCM + rate, decoded by the engine library (tfp_wav_read). Raises TfpError for a
+    missing file (TFP_E_NOENT) or audio the engine cannot take exactly (TFP_E_FORMAT)."""
+    return read_wav(filename)
 
 
 def write_wav_mono16(filename: str, pcm: np.ndarray, sample_rate: int = 8000):
@@ -193,7 +189,7 @@ class FpHandler:
                 continue  # already enrolled
             try:
                 pcm, sr = read_wav_mono16(path)
-            except (OSError, ValueError, EOFError, wave.Error):
+            except TfpError:
                 continue
             uuid = self.fp_generate_uuid()
             self.db.execute("insert into audio_list(uuid, name, context, hash) values (?, ?, ?, ?);",
@@ -231,7 +227,7 @@ class FpHandler:
             return None
         try:
             pcm, sr = read_wav_mono16(filename)
-        except (OSError, ValueError, EOFError, wave.Error):
+        except TfpError:
             return None
         res, _ = self.engine.search_pcm_batch(pcm, [0, len(pcm)],
                                               params(coefs, tolerance, freq_ignore_low, freq_ignore_high), sr)

@@ -15,6 +15,8 @@
  *                                     "delete from audio_fingerprint where audio_uuid=..."
  *   tfp_search / _batch / _pcm_batch  fp_search_fingerprint_info     fp_handler.c:207-408
  *                                     (declared in fp_handler.h:28-35)
+ *   tfp_wav_decode / tfp_wav_read     new_aubio_source + aubio_source_do at the native rate
+ *                                     fp_handler.c:37, :604, :633 (libaubio source_wavread)
  */
 #ifndef TIRESIAS_FP_H
 #define TIRESIAS_FP_H
@@ -40,7 +42,8 @@ enum {
   TFP_E_NOENT = -4,     /* uuid not in the index */
   TFP_E_CAPACITY = -5,  /* caller buffer too small (needed size returned through out param) */
   TFP_E_EXISTS = -6,    /* uuid already indexed */
-  TFP_E_NODEV = -7      /* no usable gfx950 device */
+  TFP_E_NODEV = -7,     /* no usable gfx950 device */
+  TFP_E_FORMAT = -8     /* audio the engine cannot take exactly (tfp_wav_*) or a malformed file */
 };
 
 typedef struct tfp_engine tfp_engine;
@@ -85,8 +88,21 @@ int tfp_abi_version(void);
 int tfp_device_count(int32_t* count);
 int tfp_engine_create(int32_t device, tfp_engine** out);
 void tfp_engine_destroy(tfp_engine* eng);
-const char* tfp_engine_last_error(const tfp_engine* eng);
+const char* tfp_engine_last_error(const tfp_engine* eng); /* eng == NULL: this thread's last
+                                                          * engine-less error (tfp_wav_*) */
 int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
+
+/* ---- audio ingest: the aubio_source step of create_audio_fingerprints ------------------ */
+/* RIFF/WAVE -> mono int16 PCM at the file's native rate (fp_handler.c:37 DEF_AUBIO_SAMPLERATE 0,
+ * :604, :633). Accepts integer PCM (format 1, or EXTENSIBLE with the PCM subformat), mono,
+ * 16-bit (samples as stored) or 8-bit ((u - 128) << 8: aubio's (u - 128) / 128 exactly). Other
+ * audio has aubio values between int16 steps (multichannel mean, 24/32-bit, float) and returns
+ * TFP_E_FORMAT. A data size of 0 or past the end of the bytes takes the whole samples present.
+ * pcm == NULL (cap 0) only sets *nsamples / *sample_rate; cap < samples -> TFP_E_CAPACITY with
+ * *nsamples set. Host-only (no GPU); errors via tfp_engine_last_error(NULL). */
+int tfp_wav_decode(const void* bytes, int64_t nbytes, int16_t* pcm, int64_t cap, int64_t* nsamples,
+                   int32_t* sample_rate);
+int tfp_wav_read(const char* path, int16_t* pcm, int64_t cap, int64_t* nsamples, int32_t* sample_rate);
 
 /* ---- fingerprinting: create_audio_fingerprints (fp_handler.c:577-671) -------------- */
 /* One clip of mono int16 PCM at its native rate (DEF_AUBIO_SAMPLERATE 0, :37). */

@@ -37,6 +37,23 @@ static int run_host(void) {
   rc = tfp_synth_pcm(&spec, 1, 1024, pcm);
   if (rc != TFP_OK) return fail("synth", rc, NULL);
   if (tfp_synth_pcm(NULL, 1, 1024, pcm) != TFP_E_ARG) return fail("synth NULL specs", 0, NULL);
+  {
+    /* audio ingest: the 44-byte header Asterisk's format_wav writes, then 2 samples */
+    static const unsigned char wav[48] = {'R', 'I', 'F', 'F', 40, 0, 0, 0, 'W', 'A', 'V', 'E', 'f', 'm', 't', ' ',
+                                          16, 0, 0, 0, 1, 0, 1, 0, 0x40, 0x1f, 0, 0, 0x80, 0x3e, 0, 0, 2, 0, 16, 0,
+                                          'd', 'a', 't', 'a', 4, 0, 0, 0, 0x34, 0x12, 0xff, 0xff};
+    unsigned char stereo[48];
+    int16_t s[2];
+    int64_t ns = 0;
+    int32_t sr = 0;
+    rc = tfp_wav_decode(wav, sizeof wav, s, 2, &ns, &sr);
+    if (rc != TFP_OK || ns != 2 || sr != 8000 || s[0] != 0x1234 || s[1] != -1) return fail("wav_decode", rc, NULL);
+    memcpy(stereo, wav, sizeof wav);
+    stereo[22] = 2;
+    stereo[32] = 4;
+    rc = tfp_wav_decode(stereo, sizeof stereo, s, 2, &ns, &sr);
+    if (rc != TFP_E_FORMAT || !tfp_engine_last_error(NULL)[0]) return fail("wav_decode stereo", rc, NULL);
+  }
   printf("host ok: abi %d, first sample %d\n", tfp_abi_version(), (int)pcm[0]);
   free(pcm);
   return 0;
