@@ -8,6 +8,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -105,19 +106,27 @@ struct tfp_engine {
 
   // scratch
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
-  DevBuf pcm, q, qoff, boxes, counts, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
+  DevBuf pcm, q, qoff, boxes, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
   DevBuf soff, foff, toff, tclip, specs;
   // small host calls: packed upload + the small-batch search workspace
   HostBuf hstage;
   DevBuf dstage;
   hipEvent_t stage_ev = nullptr;
   bool stage_pending = false;
+  HostBuf qoff_pin;                   // pinned source of the qoff copy
+  std::vector<int64_t> qoff_host;     // what e->qoff holds (copied on stream qoff_stream)
+  hipStream_t qoff_stream = nullptr;
+  hipEvent_t qoff_ev = nullptr;
+  bool qoff_pending = false;
   DevBuf small_work, small_bk, key_rng;
   uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
-  ~tfp_engine() { if (stage_ev) (void)hipEventDestroy(stage_ev); }
+  ~tfp_engine() {
+    if (stage_ev) (void)hipEventDestroy(stage_ev);
+    if (qoff_ev) (void)hipEventDestroy(qoff_ev);
+  }
 };
 
 namespace {
@@ -382,6 +391,13 @@ int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
 
 // ---- search core: frames' q values already on device (e->q, 2 doubles per frame) -----------
 
+// Used-key count up to which the vote takes the pattern-class path (test/A-B knob read per call:
+// TFP_VOTE_CLASS_MAX, default 10, the kernels' limit; -1 always runs the Bt GEMM).
+int32_t vote_class_ku_max() {
+  const char* s = getenv("TFP_VOTE_CLASS_MAX");
+  return s ? (int32_t)atoi(s) : (int32_t)10;
+}
+
 int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* d_q, const tfp_search_params* P,
                 std::vector<unsigned long long>& keys, unsigned long long* d_keys_out, hipStream_t s) {
   int rc = rebuild(e);  // synchronous on e->stream
@@ -435,7 +451,22 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       // a key outside the vote range: redo the batch on the general path below
     }
   }
-  if ((rc = upload(e, e->qoff, qo.data(), sizeof(int64_t) * qo.size(), s))) return rc;
+  // Query offsets are the same on every call of one plan or stream: copy them only when they
+  // change, from pinned memory so the copy is asynchronous (a pageable copy would make the host
+  // wait for the queries' fingerprint kernels before it could launch the search).
+  if (qo != e->qoff_host || s != e->qoff_stream) {
+    const size_t bytes = sizeof(int64_t) * qo.size();
+    if (e->qoff_pending) HIPCHK(e, hipEventSynchronize(e->qoff_ev));  // previous copy done reading
+    HIPCHK(e, e->qoff.reserve(bytes));
+    HIPCHK(e, e->qoff_pin.reserve(bytes));
+    memcpy(e->qoff_pin.p, qo.data(), bytes);
+    HIPCHK(e, hipMemcpyAsync(e->qoff.p, e->qoff_pin.p, bytes, hipMemcpyHostToDevice, s));
+    if (!e->qoff_ev) HIPCHK(e, hipEventCreateWithFlags(&e->qoff_ev, hipEventDisableTiming));
+    HIPCHK(e, hipEventRecord(e->qoff_ev, s));
+    e->qoff_pending = true;
+    e->qoff_host = qo;
+    e->qoff_stream = s;
+  }
   HIPCHK(e, e->boxes.reserve(sizeof(FrameBox) * (nf + 1)));
   const int32_t Qp = ((nq + 127) / 128) * 128;
   // one buffer: the vote path's key mask (32 words), max count (1), pad (1), then best[Qp] (u64);
@@ -456,32 +487,33 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
 
   bool done = false;
   if (vote) {
-    // vote-matrix path, no host round trip: histogram -> used-key compaction -> A, Bt -> GEMM
+    // vote-matrix path, no host round trip: key mask -> used-key compaction -> A (per-query
+    // counts) and Bt -> GEMM
     const int32_t Cp = ((C + 31) / 32) * 32;
-    HIPCHK(e, e->counts.reserve(sizeof(int32_t) * (size_t)nq * kKeyRange));
-    HIPCHK(e, e->keycols.reserve(sizeof(int32_t) * kKeyRange));
+    HIPCHK(e, e->keycols.reserve(sizeof(int32_t) * 2 * kKeyRange));
     HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * kKeyRange));
     HIPCHK(e, e->kbounds.reserve(sizeof(VoteMeta)));
     HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
     HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
     VoteMeta* d_meta = e->kbounds.as<VoteMeta>();
     if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
-    HIPCHK(e, launch_key_hist(d_q, sc, e->qoff.as<int64_t>(), nq, e->counts.as<int32_t>(), d_mask, d_max, s));
+    HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, s));
     HIPCHK(e, launch_vote_compact(d_mask, d_max, e->rng_all.as<int64_t>(), e->keycols.as<int32_t>(),
-                                  e->key_rng.as<int64_t>(), d_meta, s));
-    HIPCHK(e, launch_build_A(e->counts.as<int32_t>(), nq, Qp, e->keycols.as<int32_t>(), d_meta, e->A.as<_Float16>(), s));
+                                  e->key_rng.as<int64_t>(), d_meta, vote_class_ku_max(), s));
+    HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, e->keycols.as<int32_t>(), d_meta, e->A.as<_Float16>(), s));
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(), d_best, s));
     VoteMeta hm;
-    HIPCHK(e, hipMemcpyAsync(&hm, d_meta, sizeof hm, hipMemcpyDeviceToHost, s));
-    if (!d_keys_out && nq)
+    // the results go out before the ok flag is known (one host wait); a redo overwrites them
+    if (d_keys_out)
+      HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+    else if (nq)
       HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(&hm, d_meta, sizeof hm, hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
-    if (hm.ok) {
-      if (d_keys_out)
-        HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
-      return TFP_OK;
-    }
+    static const bool dbg = getenv("TFP_DEBUG_VOTE") != nullptr;
+    if (dbg) fprintf(stderr, "[tfp] vote: nq %d Qp %d C %d ku %d kp %d ok %d\n", nq, Qp, C, hm.ku, hm.kp, hm.ok);
+    if (hm.ok) return TFP_OK;
     // a count above fp16's exact range or a key outside the vote range: the scan path below
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }

@@ -1649,6 +1649,7 @@ hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc
 }
 
 constexpr int kVoteColsPerBlock = 1024;  // clips per vote_gemm block (a power of 2)
+constexpr int kClassKuMax = 10;  // pattern-class vote path: at most 2^10 - 1 patterns
 constexpr float kVoteScale = 1024.f;      // Bt's box entries: acc = 1024 * score + column-in-chunk
 
 // ---- coefs = 1: vote matrix. score[q][clip] = sum_k N[q][k] * B[k][clip], where N counts the
@@ -1666,58 +1667,47 @@ __device__ __forceinline__ bool frame_key(const double* __restrict__ q, int64_t 
   return __builtin_isfinite(freq - sc.tole) && __builtin_isfinite(freq + sc.tole);
 }
 
-// One block per query (frames of a query are contiguous): the per-key frame counts in LDS, written
-// out as the query's whole row (no memset, no global atomics on counts); used keys ORed into the
-// batch mask (one ballot per 64 keys); counts above 1024 reported through maxc (fp16 holds counts
-// up to 2048 exactly), a key outside the vote range as INT32_MAX.
-__global__ __launch_bounds__(256) void key_hist_kernel(const double* __restrict__ qv, SearchConsts sc,
-                                                       const int64_t* __restrict__ qoff, int32_t nq,
-                                                       int32_t* __restrict__ counts, uint32_t* __restrict__ mask,
-                                                       int32_t* __restrict__ maxc) {
-  __shared__ int32_t hist[kKeyRange];
-  __shared__ int32_t smax;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-    for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) hist[i] = 0;
-    if (threadIdx.x == 0) smax = 0;
-    __syncthreads();
-    for (int64_t i = qoff[q] + threadIdx.x; i < qoff[q + 1]; i += blockDim.x) {
-      int32_t k;
-      if (!frame_key(qv, i, sc, k)) continue;
-      const int64_t idx = (int64_t)k + kKeyOffset;
-      if (idx < 0 || idx >= kKeyRange) {  // not a fingerprint-range key: send the batch to the scan path
-        atomicMax(&smax, INT32_MAX);
-        continue;
-      }
-      atomicAdd(&hist[idx], 1);
+// The batch's used-key mask over all frames at once (every frame's key is independent of its
+// query): bits set in a 32-word LDS mask per block, ORed into the global mask; a key outside the
+// vote range is reported through maxc as INT32_MAX (the batch then goes to the scan path).
+__global__ __launch_bounds__(256) void key_mask_kernel(const double* __restrict__ qv, SearchConsts sc, int64_t nf,
+                                                       uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
+  // one byte per key, set by plain stores (keys concentrate on a few values, so LDS atomics on a
+  // few mask words would serialise), then folded to mask words by ballots
+  __shared__ uint8_t used[kKeyRange];
+  for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) used[i] = 0;
+  __syncthreads();
+  bool out_of_range = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    int32_t k;
+    if (!frame_key(qv, i, sc, k)) continue;
+    const int64_t idx = (int64_t)k + kKeyOffset;
+    if (idx < 0 || idx >= kKeyRange) {
+      out_of_range = true;
+      continue;
     }
-    __syncthreads();
-    int32_t* row = counts + (int64_t)q * kKeyRange;
-    int32_t m = 0;
-    for (int i = threadIdx.x; i < kKeyRange; i += blockDim.x) {
-      const int32_t v = hist[i];
-      row[i] = v;
-      m = v > m ? v : m;
+    used[idx] = 1;
+  }
+  if (out_of_range) atomicMax(maxc, INT32_MAX);
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  for (int base = threadIdx.x & ~63; base < kKeyRange; base += blockDim.x) {
+    const unsigned long long bits = __ballot(used[base + lane] != 0);
+    if (lane == 0) {
+      if ((uint32_t)bits) atomicOr(&mask[base >> 5], (uint32_t)bits);
+      if ((uint32_t)(bits >> 32)) atomicOr(&mask[(base >> 5) + 1], (uint32_t)(bits >> 32));
     }
-    if (m > 1024) atomicMax(&smax, m);  // only large counts matter (fp16 exactness limit 2048)
-    for (int base = 64 * wave; base < kKeyRange; base += blockDim.x) {
-      const unsigned long long bits = __ballot(hist[base + lane] != 0);
-      if (lane == 0 && bits) {
-        if ((uint32_t)bits) atomicOr(&mask[base >> 5], (uint32_t)bits);
-        if ((uint32_t)(bits >> 32)) atomicOr(&mask[(base >> 5) + 1], (uint32_t)(bits >> 32));
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && smax) atomicMax(maxc, smax);
-    __syncthreads();
   }
 }
 
-hipError_t launch_key_hist(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t* d_counts,
-                           uint32_t* d_mask, int32_t* d_maxcount, hipStream_t s) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(key_hist_kernel, dim3(nq < 8192 ? nq : 8192), dim3(256), 0, s, d_q, sc, d_qoff, nq, d_counts, d_mask,
-                     d_maxcount);
+hipError_t launch_key_mask(const double* d_q, SearchConsts sc, int64_t nf, uint32_t* d_mask, int32_t* d_maxc,
+                           hipStream_t s) {
+  if (nf <= 0) return hipSuccess;
+  // few blocks: each ORs its words into the same few global mask words, and same-address atomics
+  // serialise in L2 (4096 blocks cost ~50 us)
+  int64_t g = (nf + 255) / 256;
+  if (g > 256) g = 256;
+  hipLaunchKernelGGL(key_mask_kernel, dim3((unsigned)g), dim3(256), 0, s, d_q, sc, nf, d_mask, d_maxc);
   return hipGetLastError();
 }
 
@@ -1742,7 +1732,7 @@ hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int
 __global__ __launch_bounds__(1024) void vote_compact_kernel(const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
                                                             const int64_t* __restrict__ rng_all,
                                                             int32_t* __restrict__ keycols, int64_t* __restrict__ rng,
-                                                            VoteMeta* __restrict__ meta) {
+                                                            VoteMeta* __restrict__ meta, int32_t class_ku_max) {
   __shared__ int32_t scan[kKeyRange];
   const int t = threadIdx.x;
   const int used = (mask[t >> 5] >> (t & 31)) & 1;
@@ -1754,6 +1744,7 @@ __global__ __launch_bounds__(1024) void vote_compact_kernel(const uint32_t* __re
     scan[t] += v;
     __syncthreads();
   }
+  keycols[kKeyRange + t] = used ? scan[t] - 1 : -1;  // key -> used-key column (build_A)
   if (used) {
     const int kc = scan[t] - 1;
     keycols[kc] = t;
@@ -1764,44 +1755,79 @@ __global__ __launch_bounds__(1024) void vote_compact_kernel(const uint32_t* __re
     const int ku = scan[t];
     meta->ku = ku;
     meta->kp = ((ku + 1 + 15) / 16) * 16;
-    meta->ok = *maxc <= 2048 ? 1 : 0;  // counts exact in fp16 (and every key in range)
+    meta->ok = *maxc <= 2048 ? 1 : 0;  // every key in range (build_A clears it for a count > 2048)
+    meta->cls = ku <= class_ku_max && ku <= kClassKuMax ? 1 : 0;
   }
 }
 
 hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int32_t* d_keycols,
-                               int64_t* d_rng, VoteMeta* d_meta, hipStream_t s) {
+                               int64_t* d_rng, VoteMeta* d_meta, int32_t class_ku_max, hipStream_t s) {
   hipLaunchKernelGGL(vote_compact_kernel, dim3(1), dim3(kKeyRange), 0, s, d_mask, d_maxc, d_rng_all, d_keycols, d_rng,
-                     d_meta);
+                     d_meta, class_ku_max);
   return hipGetLastError();
 }
 
-__global__ void build_A_kernel(const int32_t* __restrict__ counts, int32_t nq, int32_t Qp, const int32_t* __restrict__ keycols,
-                               const VoteMeta* __restrict__ meta, _Float16* __restrict__ A) {
+// One wave per query row of A: the query's frames counted per used key in LDS, then the row
+// written as fp16 (A[q][Ku] = 1 picks up Bt's column-position entry for vote_gemm's packed argmax;
+// rows q >= nq up to Qp are zero). A count above 2048 (not exact in fp16) clears meta->ok, before
+// vote_gemm reads it, and the host redoes the batch on the scan path.
+__global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__ qv, SearchConsts sc,
+                                                      const int64_t* __restrict__ qoff, int32_t nq, int32_t Qp,
+                                                      const int32_t* __restrict__ keycols, VoteMeta* __restrict__ meta,
+                                                      _Float16* __restrict__ A) {
+  __shared__ int32_t hist[4][kVoteKpMax];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + wave;
+  if (q >= Qp) return;
   const int32_t Ku = meta->ku, Kp = meta->kp;
-  const int64_t total = (int64_t)Qp * Kp;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int q = (int)(i / Kp), col = (int)(i % Kp);
-    int32_t v = 0;
-    if (q < nq && col < Ku) v = counts[(int64_t)q * kKeyRange + keycols[col]];
-    if (q < nq && col == Ku) v = 1;  // picks up Bt's column-index entry (vote_gemm's packed argmax)
-    A[i] = (_Float16)(float)v;  // exact: v <= 2048 when meta->ok
+  int32_t* h = hist[wave];
+  for (int c = lane; c < Kp; c += 64) h[c] = 0;
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  if (q < nq) {
+    const int32_t* kmap = keycols + kKeyRange;
+    for (int64_t i = qoff[q] + lane; i < qoff[q + 1]; i += 64) {
+      int32_t k;
+      if (!frame_key(qv, i, sc, k)) continue;
+      const int64_t idx = (int64_t)k + kKeyOffset;
+      if (idx < 0 || idx >= kKeyRange) continue;  // already flagged by key_mask (meta->ok = 0)
+      atomicAdd(&h[kmap[idx]], 1);
+    }
   }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  bool big = false;
+  _Float16* row = A + (int64_t)q * Kp;
+  for (int c = lane; c < Kp; c += 64) {
+    int32_t v = q < nq ? h[c] : 0;
+    if (q < nq && c == Ku) v = 1;
+    big |= v > 2048;
+    row[c] = (_Float16)(float)v;  // exact for v <= 2048
+  }
+  if (big) meta->ok = 0;
 }
 
-hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, const VoteMeta* d_meta,
-                          _Float16* d_A, hipStream_t s) {
-  const int64_t total = (int64_t)Qp * kVoteKpMax;
-  int64_t g = (total + 255) / 256;
-  if (g > 4096) g = 4096;
-  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)g), dim3(256), 0, s, d_counts, nq, Qp, d_keycols, d_meta, d_A);
+hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
+                          const int32_t* d_keycols, VoteMeta* d_meta, _Float16* d_A, hipStream_t s) {
+  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, d_q, sc, d_qoff, nq, Qp, d_keycols,
+                     d_meta, d_A);
   return hipGetLastError();
 }
 
 // Bt[clip][key] = kVoteScale for every row in the key's box, Bt[clip][Ku] = clip mod 1024 (the
 // clip's position in its vote_gemm chunk), 0 elsewhere: zero_bt clears the [Cp][Kp] region the
 // GEMM reads, then build_B marks.
+//
+// Few used keys (meta->cls: Ku <= kClassKuMax) take the pattern-class path instead, in the same
+// buffer: a clip's score for query q is the sum of q's counts over the keys whose boxes hold a row
+// of the clip, so it depends only on that key set (the clip's pattern, Ku bits). Per pattern only
+// the greatest column matters (a tie goes to the greatest uuid), so the vote is an argmax over at
+// most 2^Ku - 1 classes per query instead of over every clip. Layout: cls[2^kClassKuMax] int32
+// (greatest column + 1 per pattern, 0 = none), then flags[Cp][16] bytes (flag k: the clip has a
+// row in the k-th used key's box; plain byte stores, since a box can hold ~10^5 rows).
 __global__ void zero_bt_kernel(_Float16* __restrict__ Bt, int32_t Cp, const VoteMeta* __restrict__ meta) {
-  const int64_t n16 = (int64_t)Cp * meta->kp / 8;  // 16-byte units (Kp is a multiple of 16)
+  const int64_t n16 = meta->cls ? (1 << kClassKuMax) / 4 + (int64_t)Cp  // 16-byte units
+                                : (int64_t)Cp * meta->kp / 8;            // (Kp is a multiple of 16)
   uint4* p = reinterpret_cast<uint4*>(Bt);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -1815,6 +1841,14 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
   const int32_t Ku = meta->ku, Kp = meta->kp;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (meta->cls) {
+    uint8_t* flags = reinterpret_cast<uint8_t*>(reinterpret_cast<int32_t*>(Bt) + (1 << kClassKuMax));
+    for (int k = 0; k < Ku; k++) {
+      const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
+      for (int64_t r = lo + t0; r < hi; r += stride) flags[(int64_t)cols[r] * 16 + k] = 1;
+    }
+    return;
+  }
   for (int64_t c = t0; c < Cp; c += stride) Bt[c * Kp + Ku] = (_Float16)(float)(c & (kVoteColsPerBlock - 1));
   for (int k = 0; k < Ku; k++) {
     const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
@@ -1822,35 +1856,155 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
   }
 }
 
+// Pattern-class path: every clip's pattern from its flags, the greatest column per pattern
+// reduced in LDS per block first (many clips share a pattern; same-address global atomics
+// serialise), then merged with one global atomicMax per pattern present in the block.
+__global__ __launch_bounds__(256) void class_max_kernel(int32_t Cp, const VoteMeta* __restrict__ meta,
+                                                        _Float16* __restrict__ Bt) {
+  if (!meta->cls) return;
+  __shared__ int32_t best[1 << kClassKuMax];
+  for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x) best[i] = 0;
+  __syncthreads();
+  int32_t* cls = reinterpret_cast<int32_t*>(Bt);
+  const uint4* flags = reinterpret_cast<const uint4*>(cls + (1 << kClassKuMax));
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < Cp; c += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 f = flags[c];
+    const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+    uint32_t pat = 0;
+#pragma unroll
+    for (int k = 0; k < kClassKuMax; k++) pat |= ((w[k >> 2] >> (8 * (k & 3))) & 1u) << k;
+    if (pat) atomicMax(&best[pat], (int32_t)c + 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x)
+    if (best[i]) atomicMax(&cls[i], best[i]);
+}
+
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt,
                           hipStream_t s) {
   hipLaunchKernelGGL(zero_bt_kernel, dim3(2048), dim3(256), 0, s, d_Bt, Cp, d_meta);
   hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, d_meta, Cp, d_Bt);
+  hipLaunchKernelGGL(class_max_kernel, dim3((unsigned)std::min<int64_t>(64, (Cp + 255) / 256)), dim3(256), 0, s, Cp,
+                     d_meta, d_Bt);
   return hipGetLastError();
+}
+
+// Pattern-class path: one wave per query, lanes over the patterns present; score = the query's
+// counts (A, exact in fp16) summed over the pattern's keys; key = score << 32 | tiekey of the
+// pattern's greatest column, max over patterns with a non-zero score.
+__global__ __launch_bounds__(256) void class_vote_kernel(const _Float16* __restrict__ A, int32_t Qp,
+                                                         const VoteMeta* __restrict__ meta,
+                                                         const _Float16* __restrict__ Bt,
+                                                         const int32_t* __restrict__ tiekey,
+                                                         unsigned long long* __restrict__ best) {
+  const int32_t Ku = meta->ku, Kp = meta->kp;
+  if (!meta->ok || !meta->cls) return;
+  const int lane = threadIdx.x & 63;
+  const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (q >= Qp) return;
+  const int32_t* cls = reinterpret_cast<const int32_t*>(Bt);
+  int32_t cnt[kClassKuMax];
+#pragma unroll
+  for (int k = 0; k < kClassKuMax; k++) cnt[k] = k < Ku ? (int32_t)(float)A[(int64_t)q * Kp + k] : 0;
+  unsigned long long mine = 0;
+  for (int P = lane + 1; P < (1 << Ku); P += 64) {
+    const int32_t c1 = cls[P];
+    if (!c1) continue;
+    uint32_t score = 0;
+#pragma unroll
+    for (int k = 0; k < kClassKuMax; k++) score += (P >> k) & 1 ? (uint32_t)cnt[k] : 0u;
+    if (!score) continue;
+    const unsigned long long key = ((unsigned long long)score << 32) | (unsigned)tiekey[c1 - 1];
+    mine = key > mine ? key : mine;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    const unsigned long long o = __shfl_xor(mine, off, 64);
+    mine = o > mine ? o : mine;
+  }
+  if (lane == 0 && mine) atomicMax(&best[q], mine);
 }
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// Wave = 32 queries x (32-clip sub-tiles of the block's 1024-clip chunk); 4 waves = 128 queries
-// share each B fragment through L1. Packed argmax: the K dimension carries one extra column,
-// A = 1 against Bt = the clip's position in the chunk, and the box entries are 1024, so each
-// accumulator is exactly 1024 * score + position (< 2^24 for scores < 16384 frames, exact in fp32):
-// one v_max per score keeps the best (score, latest column) — columns are the clips in ascending
-// uuid order, so a later column wins a tie, as SQLite returns the greatest audio_uuid. Result key
-// = score << 32 | tiekey[column], merged across chunks with atomicMax.
-__global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
-                                                        int32_t Qp, int32_t Cp, const VoteMeta* __restrict__ meta,
-                                                        const int32_t* __restrict__ tiekey,
-                                                        unsigned long long* __restrict__ best) {
-  if (!meta->ok) return;  // the host redoes the batch on the scan path
-  const int32_t Kp = meta->kp;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = lane & 31, h = lane >> 5;
-  const int q0 = (blockIdx.y * 4 + wave) * 32;
-  if (q0 >= Qp) return;
-  const int cbeg = blockIdx.x * kVoteColsPerBlock;
-  const int cend = min(cbeg + kVoteColsPerBlock, Cp);
+// Packed argmax: the K dimension carries one extra column, A = 1 against Bt = the clip's position
+// in its 1024-clip chunk, and the box entries are 1024, so each accumulator is exactly
+// 1024 * score + position (< 2^24 for scores < 16384 frames, exact in fp32): one v_max per score
+// keeps the best (score, latest column) — columns are the clips in ascending uuid order, so a
+// later column wins a tie, as SQLite returns the greatest audio_uuid. Result key =
+// score << 32 | tiekey[column], merged across chunks with atomicMax.
+constexpr int kVoteChunk = 512;  // clips per block (a divisor of kVoteColsPerBlock)
+
+__device__ __forceinline__ void vote_reduce_rows(const floatx16& m, int q0, int h, int r, int base,
+                                                 const int32_t* __restrict__ tiekey,
+                                                 unsigned long long* __restrict__ best) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    float v = m[i];
+#pragma unroll
+    for (int off = 16; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    const uint32_t packed = (uint32_t)v;
+    const uint32_t score = packed / (uint32_t)kVoteScale;
+    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (r == 0 && score > 0) {
+      const int col = base + (int)(packed % (uint32_t)kVoteScale);
+      atomicMax(&best[q0 + row], ((unsigned long long)score << 32) | (unsigned)tiekey[col]);
+    }
+  }
+}
+
+// Kp = 16 * KS <= 128: the wave's two 32-query A tiles stay in registers for the whole chunk and
+// each B fragment (32 clips x 16 keys) feeds two MFMAs; the next 32 clips' fragments are loaded
+// while the current ones are multiplied.
+template <int KS>
+__device__ __forceinline__ void vote_tile_regs(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt, int q0,
+                                               int cbeg, int cend, const int32_t* __restrict__ tiekey,
+                                               unsigned long long* __restrict__ best) {
+  constexpr int Kp = 16 * KS;
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
+  half8 a0[KS], a1[KS], b[KS];
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    a0[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + r) * Kp + 16 * s + 8 * h);
+    a1[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + 32 + r) * Kp + 16 * s + 8 * h);
+    b[s] = *reinterpret_cast<const half8*>(Bt + (int64_t)(cbeg + r) * Kp + 16 * s + 8 * h);
+  }
+  floatx16 m0, m1;
+#pragma unroll
+  for (int i = 0; i < 16; i++) m0[i] = m1[i] = 0.f;
+  for (int c = cbeg; c < cend; c += 32) {
+    const int cn = c + 32 < cend ? c + 32 : c;
+    half8 bn[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) bn[s] = *reinterpret_cast<const half8*>(Bt + (int64_t)(cn + r) * Kp + 16 * s + 8 * h);
+    floatx16 acc0, acc1;
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.f;
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[s], b[s], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[s], b[s], acc1, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      m0[i] = fmaxf(m0[i], acc0[i]);
+      m1[i] = fmaxf(m1[i], acc1[i]);
+    }
+#pragma unroll
+    for (int s = 0; s < KS; s++) b[s] = bn[s];
+  }
+  const int base = cbeg & ~(kVoteColsPerBlock - 1);
+  vote_reduce_rows(m0, q0, h, r, base, tiekey, best);
+  vote_reduce_rows(m1, q0 + 32, h, r, base, tiekey, best);
+}
+
+// Any Kp (up to kVoteKpMax): A and B fragments streamed from memory per 16-key step.
+__device__ __forceinline__ void vote_tile_stream(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
+                                                 int32_t Kp, int q0, int cbeg, int cend,
+                                                 const int32_t* __restrict__ tiekey,
+                                                 unsigned long long* __restrict__ best) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
   floatx16 m;
 #pragma unroll
   for (int i = 0; i < 16; i++) m[i] = 0.f;
@@ -1879,26 +2033,44 @@ __global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restri
 #pragma unroll
         for (int i = 0; i < 16; i++) m[i] = fmaxf(m[i], acc[j][i]);
   }
-#pragma unroll
-  for (int i = 0; i < 16; i++) {
-    float v = m[i];
-#pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    const uint32_t packed = (uint32_t)v;
-    const uint32_t score = packed / (uint32_t)kVoteScale;
-    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (r == 0 && score > 0) {
-      const int col = cbeg + (int)(packed % (uint32_t)kVoteScale);
-      atomicMax(&best[q0 + row], ((unsigned long long)score << 32) | (unsigned)tiekey[col]);
-    }
+  vote_reduce_rows(m, q0, h, r, cbeg & ~(kVoteColsPerBlock - 1), tiekey, best);
+}
+
+// Block = 4 waves x 64 queries against one kVoteChunk-clip chunk (Qp is a multiple of 128, Cp of
+// 32, so every wave's 64 rows and every 32-clip step are in range).
+__global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
+                                                        int32_t Qp, int32_t Cp, const VoteMeta* __restrict__ meta,
+                                                        const int32_t* __restrict__ tiekey,
+                                                        unsigned long long* __restrict__ best) {
+  if (!meta->ok || meta->cls) return;  // scan path on the host's redo / class_vote
+  const int32_t Kp = meta->kp;
+  const int wave = threadIdx.x >> 6;
+  const int q0 = (blockIdx.y * 4 + wave) * 64;
+  if (q0 >= Qp) return;
+  const int cbeg = blockIdx.x * kVoteChunk;
+  const int cend = min(cbeg + kVoteChunk, Cp);
+  switch (Kp >> 4) {
+    case 1: vote_tile_regs<1>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 2: vote_tile_regs<2>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 3: vote_tile_regs<3>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 4: vote_tile_regs<4>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 5: vote_tile_regs<5>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 6: vote_tile_regs<6>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 7: vote_tile_regs<7>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    case 8: vote_tile_regs<8>(A, Bt, q0, cbeg, cend, tiekey, best); break;
+    default:
+      vote_tile_stream(A, Bt, Kp, q0, cbeg, cend, tiekey, best);
+      vote_tile_stream(A, Bt, Kp, q0 + 32, cbeg, cend, tiekey, best);
   }
 }
 
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s) {
   if (Qp <= 0 || Cp <= 0) return hipSuccess;
-  dim3 grid((Cp + kVoteColsPerBlock - 1) / kVoteColsPerBlock, (Qp / 32 + 3) / 4);
+  if (Qp % 128 || Cp % 32) return hipErrorInvalidValue;  // the tiles assume these paddings
+  dim3 grid((Cp + kVoteChunk - 1) / kVoteChunk, (Qp / 64 + 3) / 4);
   hipLaunchKernelGGL(vote_gemm_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_best);
+  hipLaunchKernelGGL(class_vote_kernel, dim3((unsigned)(Qp / 4)), dim3(256), 0, s, d_A, Qp, d_meta, d_Bt, d_tiekey, d_best);
   return hipGetLastError();
 }
 

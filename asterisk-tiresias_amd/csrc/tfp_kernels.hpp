@@ -59,9 +59,9 @@ hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, 
 // Also zeroes zero_words[0, nzero) (the vote path's mask, max count and best keys).
 hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, uint32_t* zero_words,
                              int32_t nzero, hipStream_t s);
-hipError_t launch_key_hist(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq,
-                           int32_t* d_counts /*[nq][kKeyRange]*/, uint32_t* d_mask /*[kKeyRange/32], zeroed*/,
-                           int32_t* d_maxcount /*zeroed*/, hipStream_t s);
+// Used-key mask of all nf frames (d_mask zeroed); a key outside the vote range sets *d_maxc = INT32_MAX.
+hipError_t launch_key_mask(const double* d_q, SearchConsts sc, int64_t nf, uint32_t* d_mask /*[kKeyRange/32]*/,
+                           int32_t* d_maxc /*zeroed*/, hipStream_t s);
 // Row ranges of all kKeyRange keys' boxes at one tolerance (the engine caches them per index version).
 hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int64_t* d_rng_all /*[kKeyRange][2]*/,
                                  hipStream_t s);
@@ -70,14 +70,16 @@ struct VoteMeta {
   int32_t ku;  // used keys
   int32_t kp;  // GEMM K: Ku + 1 (the packed-argmax column) rounded up to 16
   int32_t ok;  // counts exact in fp16 and keys in range: else the host redoes the batch on the scan path
-  int32_t pad;
+  int32_t cls; // pattern-class path (Ku <= class_ku_max) instead of the Bt GEMM
 };
 constexpr int32_t kVoteKpMax = ((kKeyRange + 1 + 15) / 16) * 16;
 hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
-                               int32_t* d_keycols /*[kKeyRange]*/, int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta,
+                               int32_t* d_keycols /*[2][kKeyRange]: used keys, key -> column*/,
+                               int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max,
                                hipStream_t s);
-hipError_t launch_build_A(const int32_t* d_counts, int32_t nq, int32_t Qp, const int32_t* d_keycols, const VoteMeta* d_meta,
-                          _Float16* d_A /*[Qp][kVoteKpMax]*/, hipStream_t s);
+hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
+                          const int32_t* d_keycols /*vote_compact's [2][kKeyRange]*/, VoteMeta* d_meta, _Float16* d_A,
+                          hipStream_t s);
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
                           _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,

@@ -282,8 +282,12 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     keys = torch.zeros(nq, dtype=torch.int64, device=dev)
     p = T.params(1, 0.001)
     torch.cuda.synchronize(dev)
-    for _ in range(2):
+    # untimed: 2 calls, then back-to-back calls for --clock-warmup-s so the batches are timed at
+    # the steady-state clock, as the fingerprint steps are
+    n_warm, t_w = 0, time.perf_counter()
+    while n_warm < 2 or time.perf_counter() - t_w < args.clock_warmup_s:
         eng.search_device(qplan, qpcm.data_ptr(), p, keys.data_ptr(), sh)
+        n_warm += 1
     torch.cuda.synchronize(dev)
     reps = 5
     times = []
@@ -319,7 +323,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": "all_reduce(MAX) of one int64 key per query" if world > 1 else None,
             "coefs": 1, "tolerance": 0.001, "db_rows_local": rows, "db_clips_local": nclips_local,
-            "db_build_s": t_build, "batch_queries": nq, "batch_ms": batch_ms,
+            "db_build_s": t_build, "batch_queries": nq, "batch_warmup_calls": n_warm, "batch_ms": batch_ms,
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat)}

@@ -307,3 +307,52 @@ def test_search_small_out_of_range_key_falls_back(engine, tfp_lib):
     r, fc = engine.search(_frames_from_q([1000.0005, 24.2], [0.0, 0.0]), tfp_lib.params(1, 0.001))
     assert r is not None and r["audio_uuid"].endswith("001") and r["match_count"] == 2 and fc == 2
     engine.index_clear()
+
+
+def _many_key_index(engine, nclips, spread, seed):
+    """Rows whose max1 sit within +-0.002 of integers in [-spread, spread] (half inside the
+    tol=0.001 boxes), so queries with keys over that range use up to 2*spread+1 vote keys."""
+    rng = np.random.default_rng(seed)
+    uuids = sorted(str(__import__("uuid").UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips))
+    rng.shuffle(uuids)
+    m1s, m2s, clip = [], [], []
+    engine.index_clear()
+    for c in range(nclips):
+        n = int(rng.integers(5, 60))
+        k = rng.integers(-spread, spread + 1, n)
+        m1 = (k * 1000000 + rng.integers(-2000, 2001, n)).astype(np.int32)
+        m2 = rng.integers(-5000000, 5000000, n).astype(np.int32)
+        engine.index_add(uuids[c], m1, m2)
+        m1s.append(m1), m2s.append(m2), clip.append(np.full(n, c, np.int32))
+    return uuids, np.concatenate(m1s), np.concatenate(m2s), np.concatenate(clip)
+
+
+@pytest.mark.parametrize("spread", [1, 4, 40, 300])
+@pytest.mark.parametrize("class_max", ["-1", "10"])
+def test_vote_paths_vs_oracle(engine, oracle, tfp_lib, spread, class_max):
+    """The coefs=1 vote: the pattern-class path (few used keys, Ku <= 10), the GEMM with A in
+    registers (Kp <= 128) and the streamed GEMM (larger Kp). TFP_VOTE_CLASS_MAX=-1 forces the
+    GEMM for every batch. Same (uuid, match_count) as the oracle's per-query search."""
+    uuids, m1, m2, clip = _many_key_index(engine, 700, spread, 17 + spread)
+    rng = np.random.default_rng(spread)
+    nq, lens = 40, rng.integers(1, 120, 40)
+    qoff = np.concatenate([[0], np.cumsum(lens)])
+    k = rng.integers(-spread, spread + 1, qoff[-1])
+    q1 = k + rng.choice([0.2, 0.7, -0.3], qoff[-1]) * np.sign(k + 0.5)  # trunc(q1) == k
+    q2 = np.zeros(qoff[-1])
+    os.environ["TFP_VOTE_CLASS_MAX"] = class_max
+    try:
+        res, fcs = engine.search_batch(_frames_from_q(q1, q2), qoff, tfp_lib.params(1, 0.001))
+    finally:
+        del os.environ["TFP_VOTE_CLASS_MAX"]
+    nfound = 0
+    for i in range(nq):
+        a, b = qoff[i], qoff[i + 1]
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[a:b], q2[a:b], 1, 0.001, -1, -1)
+        exp = (uuids[w], mc) if found else None
+        got = None if res[i] is None else (res[i]["audio_uuid"], res[i]["match_count"])
+        assert got == exp, (i, spread, class_max)
+        assert fcs[i] == fc == b - a
+        nfound += found
+    assert nfound > nq // 2
+    engine.index_clear()
