@@ -106,7 +106,7 @@ struct tfp_engine {
 
   // scratch
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
-  DevBuf pcm, q, qoff, boxes, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
+  DevBuf pcm, q, qoff, boxes, vote_part, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
   DevBuf soff, foff, toff, tclip, specs;
   // small host calls: packed upload + the small-batch search workspace
   HostBuf hstage;
@@ -502,7 +502,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
                                   e->key_rng.as<int64_t>(), d_meta, vote_class_ku_max(), s));
     HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, e->keycols.as<int32_t>(), d_meta, e->A.as<_Float16>(), s));
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
-    HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(), d_best, s));
+    HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
+    HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),
+                               e->vote_part.as<unsigned long long>(), d_best, s));
     VoteMeta hm;
     // the results go out before the ok flag is known (one host wait); a redo overwrites them
     if (d_keys_out)

@@ -1934,69 +1934,180 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 // keeps the best (score, latest column) — columns are the clips in ascending uuid order, so a
 // later column wins a tie, as SQLite returns the greatest audio_uuid. Result key =
 // score << 32 | tiekey[column], merged across chunks with atomicMax.
-constexpr int kVoteChunk = 512;  // clips per block (a divisor of kVoteColsPerBlock)
+#ifndef TFP_VOTE_CHUNK
+#define TFP_VOTE_CHUNK 1024
+#endif
+constexpr int kVoteChunk = TFP_VOTE_CHUNK;  // clips per block (a divisor of kVoteColsPerBlock)
 
-__device__ __forceinline__ void vote_reduce_rows(const floatx16& m, int q0, int h, int r, int base,
+// m holds the bit patterns of the running maxima. Every accumulator is a non-negative float
+// (non-negative operands), and non-negative floats order as their bit patterns, so the max is an
+// integer v_max_u32 (fmaxf would canonicalise both operands first: 3 VALU per element).
+typedef uint32_t uintx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ void vote_max_into(uintx16& m, const floatx16& acc) {
+#pragma unroll
+  for (int i = 0; i < 16; i++) m[i] = max(m[i], __float_as_uint(acc[i]));
+}
+
+// The wave's 32 rows of its chunk's partial results (part = this chunk's row of [nchunks][Qp]):
+// plain stores, merged by vote_final_kernel. Device-scope atomics on shared addresses go past the
+// per-XCD L2s and serialise: 400 k of them cost ~50 us.
+__device__ __forceinline__ void vote_reduce_rows(const uintx16& m, int q0, int h, int r, int base,
                                                  const int32_t* __restrict__ tiekey,
-                                                 unsigned long long* __restrict__ best) {
+                                                 unsigned long long* __restrict__ part) {
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    float v = m[i];
+    uint32_t v = m[i];
 #pragma unroll
-    for (int off = 16; off >= 1; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    const uint32_t packed = (uint32_t)v;
+    for (int off = 16; off >= 1; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    const uint32_t packed = (uint32_t)__uint_as_float(v);
     const uint32_t score = packed / (uint32_t)kVoteScale;
     const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (r == 0 && score > 0) {
+    if (r == 0) {
       const int col = base + (int)(packed % (uint32_t)kVoteScale);
-      atomicMax(&best[q0 + row], ((unsigned long long)score << 32) | (unsigned)tiekey[col]);
+      part[q0 + row] = score > 0 ? ((unsigned long long)score << 32) | (unsigned)tiekey[col] : 0ull;
     }
   }
 }
 
 // Kp = 16 * KS <= 128: the wave's two 32-query A tiles stay in registers for the whole chunk and
-// each B fragment (32 clips x 16 keys) feeds two MFMAs; the next 32 clips' fragments are loaded
-// while the current ones are multiplied.
-template <int KS>
+// each B fragment (32 clips x 16 keys) feeds two MFMAs. B is loaded G 32-clip steps at a time,
+// double-buffered: the next group's loads are in flight while the current group is multiplied
+// (with few keys a step is only a few MFMAs, so one step of prefetch cannot cover the latency).
+template <int KS, int G>
 __device__ __forceinline__ void vote_tile_regs(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt, int q0,
                                                int cbeg, int cend, const int32_t* __restrict__ tiekey,
                                                unsigned long long* __restrict__ best) {
   constexpr int Kp = 16 * KS;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  half8 a0[KS], a1[KS], b[KS];
+  const uint32_t voff = (uint32_t)((r * Kp + 8 * h) * sizeof(_Float16));  // lane's byte offset in a step
+  half8 a0[KS], a1[KS], b[G][KS];
 #pragma unroll
   for (int s = 0; s < KS; s++) {
     a0[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + r) * Kp + 16 * s + 8 * h);
     a1[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + 32 + r) * Kp + 16 * s + 8 * h);
-    b[s] = *reinterpret_cast<const half8*>(Bt + (int64_t)(cbeg + r) * Kp + 16 * s + 8 * h);
   }
-  floatx16 m0, m1;
+  auto load_group = [&](int c, half8 (&dst)[G][KS]) {
 #pragma unroll
-  for (int i = 0; i < 16; i++) m0[i] = m1[i] = 0.f;
-  for (int c = cbeg; c < cend; c += 32) {
-    const int cn = c + 32 < cend ? c + 32 : c;
-    half8 bn[KS];
+    for (int g = 0; g < G; g++) {
+      const int cc = min(c + 32 * g, cend - 32);  // past the chunk: a duplicate, not used
+      const char* sb = reinterpret_cast<const char*>(Bt + (int64_t)cc * Kp);  // wave-uniform base
 #pragma unroll
-    for (int s = 0; s < KS; s++) bn[s] = *reinterpret_cast<const half8*>(Bt + (int64_t)(cn + r) * Kp + 16 * s + 8 * h);
-    floatx16 acc0, acc1;
+      for (int s = 0; s < KS; s++) dst[g][s] = *reinterpret_cast<const half8*>(sb + voff + 32 * s);
+    }
+  };
+  load_group(cbeg, b);
+  uintx16 m0, m1;
 #pragma unroll
-    for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.f;
+  for (int i = 0; i < 16; i++) m0[i] = m1[i] = 0u;
+  for (int c = cbeg; c < cend; c += 32 * G) {
+    half8 bn[G][KS];
+    load_group(c + 32 * G < cend ? c + 32 * G : c, bn);
 #pragma unroll
-    for (int s = 0; s < KS; s++) {
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[s], b[s], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[s], b[s], acc1, 0, 0, 0);
+    for (int g = 0; g < G; g++) {
+      if (G > 1 && c + 32 * g >= cend) break;
+      floatx16 acc0, acc1;
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.f;
+#pragma unroll
+      for (int s = 0; s < KS; s++) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[s], b[g][s], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[s], b[g][s], acc1, 0, 0, 0);
+      }
+      vote_max_into(m0, acc0);
+      vote_max_into(m1, acc1);
     }
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      m0[i] = fmaxf(m0[i], acc0[i]);
-      m1[i] = fmaxf(m1[i], acc1[i]);
-    }
+    for (int g = 0; g < G; g++)
 #pragma unroll
-    for (int s = 0; s < KS; s++) b[s] = bn[s];
+      for (int s = 0; s < KS; s++) b[g][s] = bn[g][s];
   }
   const int base = cbeg & ~(kVoteColsPerBlock - 1);
   vote_reduce_rows(m0, q0, h, r, base, tiekey, best);
   vote_reduce_rows(m1, q0 + 32, h, r, base, tiekey, best);
+}
+
+// Kp = 16 * KS in (32, 128]: B shared by the block's 4 waves through LDS. Each B fragment feeds
+// two MFMAs per wave, so per-wave loads of B (6 KB per 32 clips at Kp = 96) ran the kernel at the
+// L1 bandwidth with waves parked on s_waitcnt 72 % of their cycles; staged once per block, B
+// costs a quarter of that. Groups of 4 steps (128 clips) are loaded into registers while the
+// previous group is multiplied from the other LDS buffer; rows are padded by 16 B (an odd number
+// of 16-byte units) so the 8 lanes of each ds_read_b128 phase hit distinct bank groups. All four
+// waves take part in the loads and barriers; a wave whose rows are past Qp only skips the math.
+constexpr int kVoteGroupClips = 128;
+constexpr int kVoteLdsRow = 2 * 128 + 16;  // bytes per clip row at the largest Kp of this path
+
+template <int KS>
+__device__ __forceinline__ void vote_tile_lds(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
+                                              int q0, bool rows_valid, int cbeg, int cend,
+                                              const int32_t* __restrict__ tiekey, unsigned long long* __restrict__ part,
+                                              char* __restrict__ lds /*[2][kVoteGroupClips * kVoteLdsRow]*/) {
+  constexpr int Kp = 16 * KS;
+  constexpr int kRow = 2 * Kp + 16;                      // padded LDS row (bytes)
+  constexpr int kBuf = kVoteGroupClips * kRow;
+  constexpr int kChunksPerClip = 2 * KS;                 // 16-byte units per clip row
+  constexpr int kLoads = kVoteGroupClips * kChunksPerClip / 256;  // per thread (= KS)
+  const int t = threadIdx.x, lane = t & 63, r = lane & 31, h = lane >> 5;
+  half8 a0[KS], a1[KS];
+  if (rows_valid) {
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      a0[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + r) * Kp + 16 * s + 8 * h);
+      a1[s] = *reinterpret_cast<const half8*>(A + (int64_t)(q0 + 32 + r) * Kp + 16 * s + 8 * h);
+    }
+  }
+  int4 pre[kLoads];
+  auto load_regs = [&](int g0) {
+#pragma unroll
+    for (int i = 0; i < kLoads; i++) {
+      const int id = t + 256 * i, clip = id / kChunksPerClip, j = id % kChunksPerClip;
+      pre[i] = g0 + clip < cend ? *reinterpret_cast<const int4*>(Bt + (int64_t)(g0 + clip) * Kp + 8 * j)
+                                : make_int4(0, 0, 0, 0);
+    }
+  };
+  auto store_lds = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < kLoads; i++) {
+      const int id = t + 256 * i, clip = id / kChunksPerClip, j = id % kChunksPerClip;
+      *reinterpret_cast<int4*>(lds + buf * kBuf + clip * kRow + 16 * j) = pre[i];
+    }
+  };
+  uintx16 m0, m1;
+#pragma unroll
+  for (int i = 0; i < 16; i++) m0[i] = m1[i] = 0u;
+  const int ngroups = (cend - cbeg + kVoteGroupClips - 1) / kVoteGroupClips;
+  load_regs(cbeg);
+  store_lds(0);
+  __syncthreads();
+  for (int g = 0; g < ngroups; g++) {
+    const int g0 = cbeg + g * kVoteGroupClips;
+    if (g + 1 < ngroups) load_regs(g0 + kVoteGroupClips);
+    if (rows_valid) {
+      const char* buf = lds + (g & 1) * kBuf + r * kRow + 16 * h;
+#pragma unroll
+      for (int st = 0; st < kVoteGroupClips / 32; st++) {
+        if (g0 + 32 * st >= cend) break;
+        floatx16 acc0, acc1;
+#pragma unroll
+        for (int i = 0; i < 16; i++) acc0[i] = acc1[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          const half8 b = *reinterpret_cast<const half8*>(buf + st * 32 * kRow + 32 * s);
+          acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0[s], b, acc0, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1[s], b, acc1, 0, 0, 0);
+        }
+        vote_max_into(m0, acc0);
+        vote_max_into(m1, acc1);
+      }
+    }
+    if (g + 1 < ngroups) store_lds((g + 1) & 1);
+    __syncthreads();
+  }
+  if (rows_valid) {
+    const int base = cbeg & ~(kVoteColsPerBlock - 1);
+    vote_reduce_rows(m0, q0, h, r, base, tiekey, part);
+    vote_reduce_rows(m1, q0 + 32, h, r, base, tiekey, part);
+  }
 }
 
 // Any Kp (up to kVoteKpMax): A and B fragments streamed from memory per 16-key step.
@@ -2005,9 +2116,9 @@ __device__ __forceinline__ void vote_tile_stream(const _Float16* __restrict__ A,
                                                  const int32_t* __restrict__ tiekey,
                                                  unsigned long long* __restrict__ best) {
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5;
-  floatx16 m;
+  uintx16 m;
 #pragma unroll
-  for (int i = 0; i < 16; i++) m[i] = 0.f;
+  for (int i = 0; i < 16; i++) m[i] = 0u;
   const _Float16* arow = A + (int64_t)(q0 + r) * Kp + 8 * h;
   constexpr int kSub = 4;  // 32-clip sub-tiles per step: their B fragments are loaded together
   for (int c0 = cbeg; c0 < cend; c0 += 32 * kSub) {
@@ -2029,47 +2140,98 @@ __device__ __forceinline__ void vote_tile_stream(const _Float16* __restrict__ A,
     }
 #pragma unroll
     for (int j = 0; j < kSub; j++)
-      if (c0 + 32 * j < cend)
-#pragma unroll
-        for (int i = 0; i < 16; i++) m[i] = fmaxf(m[i], acc[j][i]);
+      if (c0 + 32 * j < cend) vote_max_into(m, acc[j]);
   }
   vote_reduce_rows(m, q0, h, r, cbeg & ~(kVoteColsPerBlock - 1), tiekey, best);
 }
 
 // Block = 4 waves x 64 queries against one kVoteChunk-clip chunk (Qp is a multiple of 128, Cp of
-// 32, so every wave's 64 rows and every 32-clip step are in range).
-__global__ __launch_bounds__(256) void vote_gemm_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
-                                                        int32_t Qp, int32_t Cp, const VoteMeta* __restrict__ meta,
-                                                        const int32_t* __restrict__ tiekey,
-                                                        unsigned long long* __restrict__ best) {
-  if (!meta->ok || meta->cls) return;  // scan path on the host's redo / class_vote
+// 32, so every wave's 64 rows and every 32-clip step are in range). Two kernels, both launched,
+// each returning at once unless Kp is its own (the host does not wait for Kp): Kp <= 32 (A and B
+// in registers, more waves per SIMD) and Kp > 128 (fragments streamed) in the kernel without
+// LDS, 32 < Kp <= 128 in the LDS-staged one.
+__global__ __launch_bounds__(256) void vote_gemm_regs_kernel(const _Float16* __restrict__ A,
+                                                              const _Float16* __restrict__ Bt, int32_t Qp, int32_t Cp,
+                                                              const VoteMeta* __restrict__ meta,
+                                                              const int32_t* __restrict__ tiekey,
+                                                              unsigned long long* __restrict__ part) {
   const int32_t Kp = meta->kp;
-  const int wave = threadIdx.x >> 6;
-  const int q0 = (blockIdx.y * 4 + wave) * 64;
+  if (!meta->ok || meta->cls || (Kp > 32 && Kp <= 128)) return;
+  const int q0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * 64;
   if (q0 >= Qp) return;
+  unsigned long long* __restrict__ best = part + (int64_t)blockIdx.x * Qp;
   const int cbeg = blockIdx.x * kVoteChunk;
   const int cend = min(cbeg + kVoteChunk, Cp);
-  switch (Kp >> 4) {
-    case 1: vote_tile_regs<1>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 2: vote_tile_regs<2>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 3: vote_tile_regs<3>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 4: vote_tile_regs<4>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 5: vote_tile_regs<5>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 6: vote_tile_regs<6>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 7: vote_tile_regs<7>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    case 8: vote_tile_regs<8>(A, Bt, q0, cbeg, cend, tiekey, best); break;
-    default:
-      vote_tile_stream(A, Bt, Kp, q0, cbeg, cend, tiekey, best);
-      vote_tile_stream(A, Bt, Kp, q0 + 32, cbeg, cend, tiekey, best);
+  if (Kp == 16) {
+    vote_tile_regs<1, 4>(A, Bt, q0, cbeg, cend, tiekey, best);
+  } else if (Kp == 32) {
+    vote_tile_regs<2, 4>(A, Bt, q0, cbeg, cend, tiekey, best);
+  } else {
+    vote_tile_stream(A, Bt, Kp, q0, cbeg, cend, tiekey, best);
+    vote_tile_stream(A, Bt, Kp, q0 + 32, cbeg, cend, tiekey, best);
   }
 }
 
+__global__ __launch_bounds__(256) void vote_gemm_lds_kernel(const _Float16* __restrict__ A, const _Float16* __restrict__ Bt,
+                                                        int32_t Qp, int32_t Cp, const VoteMeta* __restrict__ meta,
+                                                        const int32_t* __restrict__ tiekey,
+                                                        unsigned long long* __restrict__ part) {
+  if (!meta->ok || meta->cls || meta->kp <= 32 || meta->kp > 128) return;  // redo / class / regs kernel
+  __shared__ __attribute__((aligned(16))) char lds[2 * kVoteGroupClips * kVoteLdsRow];
+  const int32_t Kp = meta->kp;
+  const int wave = threadIdx.x >> 6;
+  const int q0 = (blockIdx.y * 4 + wave) * 64;
+  const bool rows_valid = q0 < Qp;
+  unsigned long long* __restrict__ best = part + (int64_t)blockIdx.x * Qp;
+  const int cbeg = blockIdx.x * kVoteChunk;
+  const int cend = min(cbeg + kVoteChunk, Cp);
+  switch (Kp >> 4) {  // uniform over the block: every wave reaches the same barriers
+    case 3: vote_tile_lds<3>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+    case 4: vote_tile_lds<4>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+    case 5: vote_tile_lds<5>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+    case 6: vote_tile_lds<6>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+    case 7: vote_tile_lds<7>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+    case 8: vote_tile_lds<8>(A, Bt, q0, rows_valid, cbeg, cend, tiekey, best, lds); break;
+  }
+}
+
+// best[q] = max over the chunks' partial keys: 64 queries per block, 16 threads per query over
+// the chunks (one thread per query left the loads latency-bound: 24 us for 98 chunks).
+__global__ __launch_bounds__(1024) void vote_final_kernel(const unsigned long long* __restrict__ part, int32_t nchunks,
+                                                          int32_t Qp, const VoteMeta* __restrict__ meta,
+                                                          unsigned long long* __restrict__ best) {
+  if (!meta->ok || meta->cls) return;
+  __shared__ unsigned long long red[16][64];
+  const int ql = threadIdx.x & 63, cl = threadIdx.x >> 6;
+  const int q = blockIdx.x * 64 + ql;
+  unsigned long long b = 0;
+  if (q < Qp)
+    for (int c = cl; c < nchunks; c += 16) {
+      const unsigned long long v = part[(int64_t)c * Qp + q];
+      b = v > b ? v : b;
+    }
+  red[cl][ql] = b;
+  __syncthreads();
+  if (cl == 0 && q < Qp) {
+#pragma unroll
+    for (int i = 1; i < 16; i++) b = red[i][ql] > b ? red[i][ql] : b;
+    best[q] = b;
+  }
+}
+
+int32_t vote_chunks(int32_t Cp) { return (Cp + kVoteChunk - 1) / kVoteChunk; }
+
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
-                            const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s) {
+                            const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
+                            hipStream_t s) {
   if (Qp <= 0 || Cp <= 0) return hipSuccess;
   if (Qp % 128 || Cp % 32) return hipErrorInvalidValue;  // the tiles assume these paddings
-  dim3 grid((Cp + kVoteChunk - 1) / kVoteChunk, (Qp / 64 + 3) / 4);
-  hipLaunchKernelGGL(vote_gemm_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_best);
+  const int32_t nchunks = vote_chunks(Cp);
+  dim3 grid(nchunks, (Qp / 64 + 3) / 4);
+  hipLaunchKernelGGL(vote_gemm_regs_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
+  hipLaunchKernelGGL(vote_gemm_lds_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
+  hipLaunchKernelGGL(vote_final_kernel, dim3((unsigned)((Qp + 63) / 64)), dim3(1024), 0, s, d_part, nchunks, Qp, d_meta,
+                     d_best);
   hipLaunchKernelGGL(class_vote_kernel, dim3((unsigned)(Qp / 4)), dim3(256), 0, s, d_A, Qp, d_meta, d_Bt, d_tiekey, d_best);
   return hipGetLastError();
 }

@@ -82,8 +82,11 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
                           hipStream_t s);
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
                           _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
+// Partial results: d_part holds vote_chunks(Cp) x Qp keys.
+int32_t vote_chunks(int32_t Cp);
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
-                            const int32_t* d_tiekey, unsigned long long* d_best, hipStream_t s);
+                            const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
+                            hipStream_t s);
 
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
 // no host round trip between the stages. One block builds every query's per-key frame counts,
