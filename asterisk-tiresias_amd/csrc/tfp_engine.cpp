@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <string>
@@ -49,11 +50,11 @@ struct HostBuf {
   void* p = nullptr;
   size_t bytes = 0;
   ~HostBuf() { if (p) (void)hipHostFree(p); }
-  hipError_t reserve(size_t n) {
+  hipError_t reserve(size_t n, unsigned flags = hipHostMallocDefault) {
     if (n <= bytes) return hipSuccess;
     if (p) { (void)hipHostFree(p); p = nullptr; bytes = 0; }
     size_t want = n < 65536 ? 65536 : n;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    hipError_t e = hipHostMalloc(&p, want, flags);
     if (e == hipSuccess) bytes = want;
     return e;
   }
@@ -111,8 +112,7 @@ struct tfp_engine {
   // small host calls: packed upload + the small-batch search workspace
   HostBuf hstage;
   DevBuf dstage;
-  hipEvent_t stage_ev = nullptr;
-  bool stage_pending = false;
+  bool stage_pending = false;  // hstage may still be read by a copy on e->stream
   HostBuf qoff_pin;                   // pinned source of the qoff copy
   std::vector<int64_t> qoff_host;     // what e->qoff holds (copied on stream qoff_stream)
   hipStream_t qoff_stream = nullptr;
@@ -120,11 +120,13 @@ struct tfp_engine {
   bool qoff_pending = false;
   DevBuf small_work, small_bk, key_rng;
   uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
+  HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
+  SmallResult* small_res_dev = nullptr;
+  uint32_t small_seq = 0;
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
   ~tfp_engine() {
-    if (stage_ev) (void)hipEventDestroy(stage_ev);
     if (qoff_ev) (void)hipEventDestroy(qoff_ev);
   }
 };
@@ -221,7 +223,9 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   const int32_t *d_toff, *d_tclip;
   if (total <= ((size_t)8 << 20)) {
     // small call: pack every array into pinned staging, one H2D copy (batch-1 latency)
-    if (e->stage_pending) HIPCHK(e, hipEventSynchronize(e->stage_ev));  // previous copy done reading
+    // Every caller waits for e->stream before it returns and then clears stage_pending, so the
+    // staging buffer is free here; after an error return the stream is drained first.
+    if (e->stage_pending) HIPCHK(e, hipStreamSynchronize(e->stream));
     HIPCHK(e, e->hstage.reserve(total));
     HIPCHK(e, e->dstage.reserve(total));
     char* h = e->hstage.as<char>();
@@ -231,8 +235,6 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
     memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
     memcpy(h + b_pcm + b_so + b_fo + b_to, tclip.data(), sizeof(int32_t) * tclip.size());
     HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
-    if (!e->stage_ev) HIPCHK(e, hipEventCreateWithFlags(&e->stage_ev, hipEventDisableTiming));
-    HIPCHK(e, hipEventRecord(e->stage_ev, e->stream));
     e->stage_pending = true;
     char* d = e->dstage.as<char>();
     d_pcm = reinterpret_cast<const int16_t*>(d);
@@ -267,6 +269,7 @@ int copy_frames_out(tfp_engine* e, int64_t nf, const std::vector<int64_t>& foff,
     HIPCHK(e, hipMemcpyAsync(d.data(), e->db.p, sizeof(double) * 2 * nf, hipMemcpyDeviceToHost, e->stream));
   }
   HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->stage_pending = false;
   size_t c = 0;
   for (int64_t g = 0; g < nf; g++) {
     while (c + 1 < foff.size() && foff[c + 1] <= g) c++;
@@ -398,6 +401,13 @@ int32_t vote_class_ku_max() {
   return s ? (int32_t)atoi(s) : (int32_t)10;
 }
 
+// Batch-1 completion wait (A/B knob read per call): 1 = hipStreamSynchronize (default; measured
+// 2 us faster at p50), 0 = spin on the published result.
+bool small_sync_mode() {
+  const char* v = getenv("TFP_SMALL_SYNC");
+  return !v || atoi(v) != 0;
+}
+
 int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* d_q, const tfp_search_params* P,
                 std::vector<unsigned long long>& keys, unsigned long long* d_keys_out, hipStream_t s) {
   int rc = rebuild(e);  // synchronous on e->stream
@@ -437,15 +447,33 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       }
       const uint8_t epoch = ++e->small_epoch;
       SmallWork* w = e->small_work.as<SmallWork>();
+      if (!e->small_res_dev) {
+        HIPCHK(e, e->small_res.reserve(sizeof(SmallResult), hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&e->small_res_dev), e->small_res.p, 0));
+      }
       if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
+      const uint32_t seq = ++e->small_seq;
       HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->rng_all.as<int64_t>(),
-                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), s));
-      struct { int32_t ku, bad; unsigned long long best[kSmallQ]; } h;
-      static_assert(offsetof(SmallWork, best) == offsetof(SmallWork, ku) + 8, "ku, bad, best contiguous");
-      HIPCHK(e, hipMemcpyAsync(&h, &w->ku, 8 + sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
-      HIPCHK(e, hipStreamSynchronize(s));
-      if (!h.bad) {
-        for (int32_t i = 0; i < nq; i++) keys[i] = h.best[i];
+                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), e->small_res_dev, seq, s));
+      // Wait for the end of the stream (default), or spin on the result itself: the publishing
+      // kernel stores seq after (ku, bad, best) with system-scope release. The spin is bounded;
+      // past it the stream is synchronised and the result read after that.
+      const volatile SmallResult* h = e->small_res.as<SmallResult>();
+      bool seen = false;
+      if (!small_sync_mode()) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+          if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
+          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
+        }
+      }
+      if (!seen) HIPCHK(e, hipStreamSynchronize(s));
+      // the vote ran after the fingerprint kernel, which read the staged upload: it is free again
+      e->stage_pending = false;
+      if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq)
+        return fail(e, TFP_E_HIP, "small search: result of call %u not published", seq);
+      if (!h->bad) {
+        for (int32_t i = 0; i < nq; i++) keys[i] = h->best[i];
         return TFP_OK;
       }
       // a key outside the vote range: redo the batch on the general path below
@@ -922,6 +950,7 @@ int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offse
     int rc = fingerprint_host(e, pcm, offsets, nq, sr, &nf, nullptr);
     if (rc) return rc;
     if ((rc = search_core(e, foff.data(), nq, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
+    e->stage_pending = false;  // search_core waited for e->stream (keys on the host)
   }
   fill_results(e, keys, foff.data(), nq, out);
   return TFP_OK;

@@ -720,6 +720,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
     float rare_thr) {
   constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
+  // dB + "%f" in finish_db_kernel for throughput launches; in the tile tail for small ones (4-frame
+  // tiles, batch-1 latency), which saves a launch
+  constexpr bool kSplitTail = TFP8_SPLIT_TAIL && kPasses == 4;
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
@@ -728,6 +731,51 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   __shared__ __attribute__((aligned(16))) int16_t PB[kBlockWaves][2][5 * kHopStride];
 #endif
   const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  // Wave-uniform tile state (scalar registers): clip, first frame, clip sample range.
+  struct Tile {
+    int c;
+    int64_t f0, s0, ns;
+  };
+  auto tile_of = [&](int b) {
+    Tile t;
+    t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
+    t.f0 = (int64_t)(b - toff[t.c]) * (4 * kPasses);
+    t.s0 = sbeg[t.c];
+    t.ns = send[t.c] - t.s0;
+    return t;
+  };
+  // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
+  auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
+    (void)pf;
+    const int16_t* clip = pcm + t.s0;
+    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
+    const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
+    if (interior) {
+      const int4* src = reinterpret_cast<const int4*>(clip + sb);
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        pf[r] = (valid && chunk < kPassChunks) ? fetch_chunk_checked(clip, t.ns, sb + 8 * chunk) : make_int4(0, 0, 0, 0);
+      }
+    }
+  };
+
+  // The first tile's bounds and PCM are requested before the tables are staged, so their
+  // latency overlaps the staging (most of a small launch's time).
+  int4 pf[kChunkRounds];
+  int b = blockIdx.x * kBlockWaves + wave;
+  Tile cur = tile_of(b < ntiles ? b : 0);
+#if !TFP8_GLDS
+  fetch(cur, 0, b < ntiles, pf);
+#endif
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
   cf* winr = reinterpret_cast<cf*>(S.window);
@@ -761,8 +809,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   for (int i = tid; i < T->ms_total; i += kBlockThreads) S.ms_w[i] = 0.5f * T->ms_w[i];  // exact: w/2
   __syncthreads();
 
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
   const int sg = col_of_lane(L);  // second-stage FFT column (= bins sg + 16 k2) of this lane
 #if TFP8_DPP
   const bool selfpair = L == 0 || L == 15;
@@ -809,41 +855,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
   }
 
-  // Wave-uniform tile state (scalar registers): clip, first frame, clip sample range.
-  struct Tile {
-    int c;
-    int64_t f0, s0, ns;
-  };
-  auto tile_of = [&](int b) {
-    Tile t;
-    t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
-    t.f0 = (int64_t)(b - toff[t.c]) * (4 * kPasses);
-    t.s0 = sbeg[t.c];
-    t.ns = send[t.c] - t.s0;
-    return t;
-  };
-  // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
-  auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
-    (void)pf;
-    const int16_t* clip = pcm + t.s0;
-    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
-    const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
-    if (interior) {
-      const int4* src = reinterpret_cast<const int4*>(clip + sb);
-#pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        pf[r] = (valid && chunk < kPassChunks) ? fetch_chunk_checked(clip, t.ns, sb + 8 * chunk) : make_int4(0, 0, 0, 0);
-      }
-    }
-  };
-
 #if TFP8_GLDS
   // One pass's 5 hops into buf: interior passes by LDS-DMA (global_load_lds_dwordx4, one 32-lane
   // instruction per hop so each lands in its padded row), edge passes by checked loads + ds_write.
@@ -873,15 +884,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   int16_t* const pb1 = PB[wave][1];
   int par = 0;
 #endif
-  int4 pf[kChunkRounds];
-  int b = blockIdx.x * kBlockWaves + wave;
-  Tile cur = tile_of(b < ntiles ? b : 0);
 #if TFP8_GLDS
   issue(cur, 0, b < ntiles, pb0);
   (void)pf;
   (void)fetch;
-#else
-  fetch(cur, 0, b < ntiles, pf);
 #endif
   for (; b < ntiles; b += nwaves) {
     const int64_t nf = (cur.ns + kHop - 1) / kHop;
@@ -1172,13 +1178,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #pragma unroll 8
         for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
         const int64_t g = foff[cur.c] + f;
-#if TFP8_SPLIT_TAIL
-        micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
-#else
-        const double q = db_of_coef(acc);
-        micro[2 * g + cfi] = micro_of_db(q);
-        if (db) db[2 * g + cfi] = q;
-#endif
+        if constexpr (kSplitTail) {
+          micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
+        } else {
+          const double q = db_of_coef(acc);
+          micro[2 * g + cfi] = micro_of_db(q);
+          if (db) db[2 * g + cfi] = q;
+        }
       }
     }
     wave_sync();
@@ -1493,7 +1499,7 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t t
         hipLaunchKernelGGL(fingerprint8k_kernel<4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                            d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
 #if TFP8_SPLIT_TAIL
-      const int64_t nv = 2 * nframes;
+      const int64_t nv = tile_frames == 16 ? 2 * nframes : 0;  // fingerprint8k_kernel<1> finishes its own tail
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;
       if (nv > 0) hipLaunchKernelGGL(finish_db_kernel, dim3((unsigned)g), dim3(256), 0, s, d_micro, d_db, nv);
@@ -2238,148 +2244,242 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
 
 // ---- small-batch path (see tfp_kernels.hpp). Same sets and counts as key_hist + build_A/B +
 // vote_gemm: a query frame with trunc key k votes once for every clip with a row in k's box.
-__global__ __launch_bounds__(1024) void small_prep_kernel(const double* __restrict__ q, SmallQueries sq,
-                                                          SearchConsts sc, const int64_t* __restrict__ rng_all,
-                                                          SmallWork* __restrict__ w) {
-  __shared__ int32_t hist[kSmallQ][kKeyRange];
-  __shared__ int32_t scan[kKeyRange];
-  __shared__ int32_t bad;
+#ifndef TFP_SMALL_PUBLISH
+// 0: small_vote's last block publishes the results (a done counter + fences in every block: the
+// vote measured 11.7 us); 1: a one-wave kernel after the vote (4.6 + 4.0 us, batch-1 p50 -5 us);
+// 2: as 1 without the system-scope fence (the host then waits for the stream, not on seq)
+#define TFP_SMALL_PUBLISH 1
+#endif
+// The batch's used keys (ascending key order = column order kc), derived by each block from the
+// query frames with frame_key's filter; bad = a key outside the vote range.
+struct SmallKeySet {
+  uint8_t used[kKeyRange];
+  uint32_t mask[kKeyRange / 32];
+  int32_t pre[kKeyRange / 32];  // used keys below mask word w
+  int32_t ku, bad;
+};
+__device__ void small_keys(const double* __restrict__ q, int64_t nf, const SearchConsts& sc, SmallKeySet& K) {
   const int t = threadIdx.x;
-  for (int i = t; i < kSmallQ * kKeyRange; i += blockDim.x) (&hist[0][0])[i] = 0;
-  if (t == 0) bad = 0;
-  if (t <= kSmallQ) w->best[t] = 0ull;
+  for (int i = t; i < kKeyRange; i += blockDim.x) K.used[i] = 0;
+  if (t == 0) K.bad = 0;
   __syncthreads();
-  const int64_t nf = sq.qoff[sq.nq];
   for (int64_t i = t; i < nf; i += blockDim.x) {
-    const double q1 = q[2 * i];
-    const double v1 = __builtin_isfinite(q1) ? q1 : 0.0;  // ast_json_real_get(NULL) = 0.0
-    const int32_t ki = (v1 > -2147483649.0 && v1 < 2147483648.0) ? (int32_t)v1 : INT32_MIN;  // :290
-    const double freq = (double)ki;
-    if (sc.has_low && freq < sc.thr_low) continue;   // :293-306
-    if (sc.has_high && freq > sc.thr_high) continue;
-    if (!__builtin_isfinite(freq - sc.tole) || !__builtin_isfinite(freq + sc.tole)) continue;
-    const int64_t idx = (int64_t)ki + kKeyOffset;
-    if (idx < 0 || idx >= kKeyRange) { bad = 1; continue; }
-    int qi = 0;
-    while (qi + 1 < sq.nq && sq.qoff[qi + 1] <= i) qi++;
-    atomicAdd(&hist[qi][idx], 1);
+    int32_t k;
+    if (!frame_key(q, i, sc, k)) continue;
+    const int64_t idx = (int64_t)k + kKeyOffset;
+    if (idx < 0 || idx >= kKeyRange) K.bad = 1;
+    else K.used[idx] = 1;  // plain byte stores: keys concentrate on a few values
   }
   __syncthreads();
-  // compaction of the used keys (ascending key order) by a block-wide inclusive scan
-  int used = 0;
-  for (int qi = 0; qi < sq.nq; qi++) used |= hist[qi][t] != 0;
-  scan[t] = used;
+  const int lane = t & 63;
+  for (int base = t & ~63; base < kKeyRange; base += blockDim.x) {
+    const unsigned long long bits = __ballot(K.used[base + lane] != 0);
+    if (lane == 0) {
+      K.mask[base >> 5] = (uint32_t)bits;
+      K.mask[(base >> 5) + 1] = (uint32_t)(bits >> 32);
+    }
+  }
   __syncthreads();
-  for (int off = 1; off < kKeyRange; off <<= 1) {
-    const int v = t >= off ? scan[t - off] : 0;
-    __syncthreads();
-    scan[t] += v;
-    __syncthreads();
+  if (t < 32) {  // exclusive prefix of the words' popcounts
+    const int c = __popc(K.mask[t]);
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) {
+      const int v = __shfl_up(incl, off, 32);
+      if (t >= off) incl += v;
+    }
+    K.pre[t] = incl - c;
+    if (t == 31) K.ku = incl;
   }
-  if (used) {
-    const int kc = scan[t] - 1;
-    w->kb[kc][0] = rng_all[2 * t];  // the box's row range
-    w->kb[kc][1] = rng_all[2 * t + 1];
-    for (int qi = 0; qi < sq.nq; qi++) w->A[qi][kc] = hist[qi][t];
-  }
-  if (t == kKeyRange - 1) {
-    w->ku = scan[t];
-    w->bad = bad;
-  }
+  __syncthreads();
+}
+__device__ __forceinline__ int small_kc(const SmallKeySet& K, int key) {
+  const int w = key >> 5;
+  return K.pre[w] + __popc(K.mask[w] & ((1u << (key & 31)) - 1u));
 }
 
 // Stamp the clips with a row in each used key's box: bk[kc][clip] = epoch (a per-call byte, so
 // rows of earlier calls never need clearing). Every key's rows are spread over the whole grid.
-__global__ __launch_bounds__(256) void small_mark_kernel(const SmallWork* __restrict__ w, uint8_t* __restrict__ bk,
-                                                         int32_t Cp, const int32_t* __restrict__ cols, uint8_t epoch) {
-  if (w->bad) return;
-  const int ku = w->ku;
+// Block 0 also resets the vote's workspace (small_vote runs after this launch on the stream).
+__global__ __launch_bounds__(256) void small_mark_kernel(const double* __restrict__ q, SmallQueries sq, SearchConsts sc,
+                                                         const int64_t* __restrict__ rng_all, uint8_t* __restrict__ bk,
+                                                         int32_t Cp, const int32_t* __restrict__ cols, uint8_t epoch,
+                                                         SmallWork* __restrict__ w) {
+  const int64_t nf = sq.qoff[sq.nq];
+  __shared__ SmallKeySet K;
+  small_keys(q, nf, sc, K);
+  if (blockIdx.x == 0) {  // the vote's bookkeeping: counts per (query, used key), ku, bad
+    const int ku = K.ku;
+    if (threadIdx.x <= kSmallQ) w->best[threadIdx.x] = 0ull;
+    if (threadIdx.x == 0) {
+      w->done = 0u;
+      w->ku = ku;
+      w->bad = K.bad;
+    }
+    if (!K.bad) {
+      for (int i = threadIdx.x; i < sq.nq * ku; i += blockDim.x) w->A[i / ku][i % ku] = 0;
+      __syncthreads();
+      // per 64 frames of a wave: one ballot per distinct (query, key) among them, one add per
+      // ballot (keys concentrate on a few values, where per-frame atomics would serialise)
+      for (int64_t base = threadIdx.x & ~63; base < nf; base += blockDim.x) {
+        const int64_t i = base + (threadIdx.x & 63);
+        int32_t k = 0;
+        int slot = -1;  // qi * kKeyRange + kc of this frame, -1 if ignored
+        if (i < nf && frame_key(q, i, sc, k)) {
+          int qi = 0;
+          while (qi + 1 < sq.nq && sq.qoff[qi + 1] <= i) qi++;
+          slot = qi * kKeyRange + small_kc(K, k + kKeyOffset);
+        }
+        unsigned long long todo = __ballot(slot >= 0);
+        while (todo) {
+          const int lead = __builtin_ctzll(todo);
+          const int ls = __shfl(slot, lead, 64);
+          const unsigned long long same = __ballot(slot == ls);
+          if ((threadIdx.x & 63) == lead) atomicAdd(&w->A[0][0] + ls, (int)__popcll(same));
+          todo &= ~same;
+        }
+      }
+    }
+  }
+  if (K.bad) return;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int kc = 0; kc < ku; kc++) {
-    uint8_t* row = bk + (int64_t)kc * Cp;
-    const int64_t lo = w->kb[kc][0], hi = w->kb[kc][1];
-    for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride) row[cols[r]] = epoch;
+  int kc = 0;
+  for (int wd = 0; wd < kKeyRange / 32; wd++) {
+    for (uint32_t m = K.mask[wd]; m; m &= m - 1u, kc++) {
+      const int key = 32 * wd + __builtin_ctz(m);
+      uint8_t* row = bk + (int64_t)kc * Cp;
+      const int64_t lo = rng_all[2 * key], hi = rng_all[2 * key + 1];
+      for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride) row[cols[r]] = epoch;
+    }
   }
 }
 
 // Clip-parallel scores of every query (4 clips per thread: one 32-bit stamp word per key row);
 // the per-query max of score << 32 | tie key (a later uuid wins a tie, as SQLite's
-// ORDER BY count(*) DESC returns it), reduced per block before one atomicMax per block.
-__global__ __launch_bounds__(256) void small_vote_kernel(SmallWork* __restrict__ w, const uint8_t* __restrict__ bk,
-                                                         int32_t Cp, int32_t C, int32_t nq,
-                                                         const int32_t* __restrict__ tiekey, uint8_t epoch) {
+// ORDER BY count(*) DESC returns it), reduced per block before one atomicMax per block. The last
+// block to finish publishes (ku, bad, best[]) and the call's sequence number to host memory.
+__global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, SmallWork* __restrict__ w,
+                                                         const uint8_t* __restrict__ bk, int32_t Cp, int32_t C,
+                                                         const int32_t* __restrict__ tiekey, uint8_t epoch,
+                                                         SmallResult* __restrict__ out, uint32_t seq) {
   __shared__ int32_t A[kSmallQ][kKeyRange];
   __shared__ unsigned long long bmax[kSmallQ][4];
-  const int ku = w->ku;
-  if (w->bad || ku == 0) return;  // no used key: every frame ignored -> NOTFOUND (best stays 0)
-  for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = w->A[i / ku][i % ku];
-  __syncthreads();
-  const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);  // first of this thread's 4 clips
-  int32_t sc[kSmallQ][4];
+  __shared__ int32_t last;
+  const int nq = sq.nq;
+  const int ku = w->ku, bad = w->bad;
+  if (!bad && ku > 0) {  // else every frame was ignored (NOTFOUND: best stays 0) or the caller redoes it
+    for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = w->A[i / ku][i % ku];
+    __syncthreads();
+    const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);  // first of this thread's 4 clips
+    int32_t sc4[kSmallQ][4];
 #pragma unroll
-  for (int qi = 0; qi < kSmallQ; qi++)
+    for (int qi = 0; qi < kSmallQ; qi++)
 #pragma unroll
-    for (int j = 0; j < 4; j++) sc[qi][j] = 0;
-  if (c4 < C) {
-    const uint32_t ep4 = 0x01010101u * epoch;
-    int kc = 0;
-    for (; kc + 4 <= ku; kc += 4) {  // 4 independent row loads in flight
-      uint32_t v[4];
+      for (int j = 0; j < 4; j++) sc4[qi][j] = 0;
+    if (c4 < C) {
+      const uint32_t ep4 = 0x01010101u * epoch;
+      int kc = 0;
+      for (; kc + 4 <= ku; kc += 4) {  // 4 independent row loads in flight
+        uint32_t v[4];
 #pragma unroll
-      for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint32_t*>(bk + (int64_t)(kc + u) * Cp + c4);
+        for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint32_t*>(bk + (int64_t)(kc + u) * Cp + c4);
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t x = v[u] ^ ep4;  // byte j == 0 <=> clip c4 + j stamped this call
+        for (int u = 0; u < 4; u++) {
+          const uint32_t x = v[u] ^ ep4;  // byte j == 0 <=> clip c4 + j stamped this call
+#pragma unroll
+          for (int j = 0; j < 4; j++)
+            if (((x >> (8 * j)) & 0xffu) == 0u)
+#pragma unroll
+              for (int qi = 0; qi < kSmallQ; qi++) sc4[qi][j] += qi < nq ? A[qi][kc + u] : 0;
+        }
+      }
+      for (; kc < ku; kc++) {
+        const uint32_t x = *reinterpret_cast<const uint32_t*>(bk + (int64_t)kc * Cp + c4) ^ ep4;
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (((x >> (8 * j)) & 0xffu) == 0u)
 #pragma unroll
-            for (int qi = 0; qi < kSmallQ; qi++) sc[qi][j] += qi < nq ? A[qi][kc + u] : 0;
+            for (int qi = 0; qi < kSmallQ; qi++) sc4[qi][j] += qi < nq ? A[qi][kc] : 0;
       }
     }
-    for (; kc < ku; kc++) {
-      const uint32_t x = *reinterpret_cast<const uint32_t*>(bk + (int64_t)kc * Cp + c4) ^ ep4;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int qi = 0; qi < nq; qi++) {
+      unsigned long long key = 0ull;
 #pragma unroll
-      for (int j = 0; j < 4; j++)
-        if (((x >> (8 * j)) & 0xffu) == 0u)
-#pragma unroll
-          for (int qi = 0; qi < kSmallQ; qi++) sc[qi][j] += qi < nq ? A[qi][kc] : 0;
-    }
-  }
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int qi = 0; qi < nq; qi++) {
-    unsigned long long key = 0ull;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const int c = c4 + j;
-      if (c < C && sc[qi][j] > 0) {
-        const unsigned long long k = ((unsigned long long)(unsigned)sc[qi][j] << 32) | (unsigned)tiekey[c];
-        key = k > key ? k : key;
+      for (int j = 0; j < 4; j++) {
+        const int c = c4 + j;
+        if (c < C && sc4[qi][j] > 0) {
+          const unsigned long long k = ((unsigned long long)(unsigned)sc4[qi][j] << 32) | (unsigned)tiekey[c];
+          key = k > key ? k : key;
+        }
       }
-    }
 #pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      const unsigned long long o = __shfl_xor(key, off, 64);
-      key = o > key ? o : key;
+      for (int off = 32; off >= 1; off >>= 1) {
+        const unsigned long long o = __shfl_xor(key, off, 64);
+        key = o > key ? o : key;
+      }
+      if (lane == 0) bmax[qi][wv] = key;
     }
-    if (lane == 0) bmax[qi][wv] = key;
+    __syncthreads();
+    if (threadIdx.x < nq) {
+      unsigned long long key = bmax[threadIdx.x][0];
+      for (int i = 1; i < 4; i++) key = bmax[threadIdx.x][i] > key ? bmax[threadIdx.x][i] : key;
+      if (key) atomicMax(&w->best[threadIdx.x], key);
+    }
   }
+#if TFP_SMALL_PUBLISH == 0
+  // last block done: publish to host memory
+  __threadfence();
   __syncthreads();
-  if (threadIdx.x < nq) {
-    unsigned long long key = bmax[threadIdx.x][0];
-    for (int i = 1; i < 4; i++) key = bmax[threadIdx.x][i] > key ? bmax[threadIdx.x][i] : key;
-    if (key && key > w->best[threadIdx.x]) atomicMax(&w->best[threadIdx.x], key);  // read first: few atomics
+  if (threadIdx.x == 0) last = atomicAdd(&w->done, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (last) {
+    __threadfence();
+    if (threadIdx.x < kSmallQ)
+      out->best[threadIdx.x] = threadIdx.x < nq ? __hip_atomic_load(&w->best[threadIdx.x], __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                                : 0ull;
+    if (threadIdx.x == 0) {
+      out->ku = ku;
+      out->bad = bad;
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+#else
+  (void)out; (void)seq; (void)last;
+#endif
+}
+
+// TFP_SMALL_PUBLISH=1: the results are published by a one-wave kernel after the vote
+__global__ __launch_bounds__(64) void small_publish_kernel(const SmallWork* __restrict__ w, int32_t nq,
+                                                           SmallResult* __restrict__ out, uint32_t seq) {
+  const int t = threadIdx.x;
+  if (t < kSmallQ) out->best[t] = t < nq ? w->best[t] : 0ull;
+  if (t == 0) {
+    out->ku = w->ku;
+    out->bad = w->bad;
+  }
+#if TFP_SMALL_PUBLISH == 1
+  __threadfence_system();
+  if (t == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+  if (t == 0) out->seq = seq;
+#endif
 }
 
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
                                uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
-                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s) {
-  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_prep_kernel, dim3(1), dim3(kKeyRange), 0, s, d_q, sq, sc, d_rng_all, d_work);
-  hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_work, d_bk, Cp, cols, epoch);
-  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 1023) / 1024), dim3(256), 0, s, d_work, d_bk, Cp, C, sq.nq, d_tiekey,
-                     epoch);
+                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
+                               uint32_t seq, hipStream_t s) {
+  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0 || !h_out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_q, sq, sc, d_rng_all, d_bk, Cp, cols, epoch, d_work);
+  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 1023) / 1024), dim3(256), 0, s, sq, d_work, d_bk, Cp, C,
+                     d_tiekey, epoch, h_out, seq);
+#if TFP_SMALL_PUBLISH >= 1
+  hipLaunchKernelGGL(small_publish_kernel, dim3(1), dim3(64), 0, s, d_work, sq.nq, h_out, seq);
+#endif
   return hipGetLastError();
 }
 

@@ -89,27 +89,36 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
                             hipStream_t s);
 
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
-// no host round trip between the stages. One block builds every query's per-key frame counts,
-// compacts the used keys and their "%f" boxes; one block per used key marks the clips with a row
-// in its box (a byte per clip, key-major); a clip-parallel pass scores and arg-maxes.
+// two launches, no host round trip and no copy back. Every block of small_mark derives the
+// batch's used keys from the query frames itself (a few KB of L2-resident reads) and stamps the
+// clips with a row in each used key's box (a byte per clip, key-major); its block 0 also writes
+// the per-query key counts. small_vote scores clip-parallel, arg-maxes, and its last block writes
+// the results straight into the caller's host-mapped SmallResult.
 constexpr int kSmallQ = 8;
 struct SmallQueries {
   int32_t nq;
   int32_t pad;
   int64_t qoff[kSmallQ + 1];  // frame offsets of the queries in d_q (relative)
 };
-struct SmallWork {              // device workspace of the small path
-  int32_t A[kSmallQ][kKeyRange];  // A[q][kc]: query q's frames whose key is the kc-th used key
-  int64_t kb[kKeyRange][2];       // row range [lo, hi) in the m1-sorted index of the kc-th used key's box
-  int32_t ku;                     // used keys
-  int32_t bad;                    // a key outside [-512, 511]: the caller redoes the batch generally
+struct SmallWork {                       // device workspace of the small path (written by small_mark)
+  int32_t A[kSmallQ][kKeyRange];         // A[q][kc]: query q's frames whose key is the kc-th used key
+  int32_t ku;                            // used keys
+  int32_t bad;                           // a key outside [-512, 511]
   unsigned long long best[kSmallQ + 1];  // per query score << 32 | tie key; best[kSmallQ] unused
+  uint32_t done;                         // small_vote blocks finished (the last one publishes)
+};
+struct SmallResult {  // host-mapped (pinned) result of one small call
+  int32_t ku;         // used keys
+  int32_t bad;        // a key outside [-512, 511]: the caller redoes the batch generally
+  unsigned long long best[kSmallQ];
+  uint32_t seq;       // the call's sequence number, stored last
 };
 // d_bk: [kKeyRange][Cp] bytes stamped with `epoch` (1..255, a new one per call; the caller clears
-// d_bk when the epoch wraps).
+// d_bk when the epoch wraps). h_out: host-mapped memory the device may write.
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
                                uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
-                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, hipStream_t s);
+                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
+                               uint32_t seq, hipStream_t s);
 
 hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
                        const int32_t* m2s, const int32_t* cols, int64_t R, const int32_t* d_tiekey, int32_t Cp,

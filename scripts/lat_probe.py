@@ -41,10 +41,13 @@ qs = [T.synth_pcm(0x7153A1, [int(rng.integers(a.db_clips))], qn, offsets=[256 * 
 p = T.params(1, 0.001)
 for q in qs[:4]:
     eng.search_pcm_batch(q, [0, qn], p)
-lat = []
-for i in range(a.n):
-    q = qs[i % len(qs)]
-    t0 = time.perf_counter()
-    res, fc = eng.search_pcm_batch(q, [0, qn], p)
-    lat.append((time.perf_counter() - t0) * 1e3)
-print("batch-1 latency p50 %.3f ms p99 %.3f ms (n=%d, db %d clips)" % (np.percentile(lat, 50), np.percentile(lat, 99), a.n, a.db_clips))
+for mode in ("0", "1"):  # TFP_SMALL_SYNC: 0 = spin on the published result, 1 = stream sync
+    os.environ["TFP_SMALL_SYNC"] = mode
+    lat = []
+    for i in range(a.n):
+        q = qs[i % len(qs)]
+        t0 = time.perf_counter()
+        res, fc = eng.search_pcm_batch(q, [0, qn], p)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    print("TFP_SMALL_SYNC=%s batch-1 latency p50 %.3f ms p99 %.3f ms (n=%d, db %d clips)"
+          % (mode, np.percentile(lat, 50), np.percentile(lat, 99), a.n, a.db_clips))
