@@ -824,7 +824,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
 #ifndef TFP8_W16_REGS
-#define TFP8_W16_REGS 1  // dft16 twiddles held in registers (20 VGPRs) vs read per pass
+#define TFP8_W16_REGS 0  // 1: dft16 twiddles held in registers (20 VGPRs; 8 VGPRs spilled: 0.541 vs 0.539 ms)
 #endif
 #if TFP8_W16_REGS
   cf w16r[10];

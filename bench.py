@@ -304,20 +304,25 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     found = int((k != 0).sum())
 
     # batch-1 latency: host PCM in -> (uuid, match_count, frame_count) out
+    # On N GPUs every rank runs the same small-batch path on its shard, turns its local winner into
+    # the global key (match_count << 32 | global uuid rank) and one all_reduce(MAX) of 8 bytes
+    # picks the winner with the reference's tie-break.
     host_q = qpcm[: args.latency_queries].cpu().numpy()
+    if dist:
+        uuid_grank = {uuid_of(g): int(grank[g]) for g in range(args.db_clips)}
+        kpin = torch.zeros(1, dtype=torch.int64).pin_memory()
+        kdev = torch.zeros(1, dtype=torch.int64, device=dev)
     lat = []
     for i in range(len(host_q)):
         barrier()
         t0 = time.perf_counter()
+        res, _ = eng.search_pcm_batch(host_q[i], [0, qn], p)
         if dist:
-            dq = torch.from_numpy(host_q[i:i + 1]).to(dev)
-            kk = torch.zeros(1, dtype=torch.int64, device=dev)
-            eng.search_device(eng.plan(np.array([0, qn], np.int64)), dq.data_ptr(), p, kk.data_ptr(), sh)
-            sharding.combine(kk, dist)
-            torch.cuda.synchronize(dev)
-            kk.item()
-        else:
-            eng.search_pcm_batch(host_q[i], [0, qn], p)
+            r = res[0]
+            kpin[0] = sharding.make_key(r["match_count"], uuid_grank[r["audio_uuid"]]) if r else 0
+            kdev.copy_(kpin, non_blocking=True)
+            sharding.combine(kdev, dist)
+            kdev.item()
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
     res = {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",

@@ -1,0 +1,9 @@
+# One call for the round's evidence: GPU parity suite + smoke + default bench (gpu_check.sh), the
+# 2-rank gloo rehearsal of the sharded path on the one GPU, then the rocprofv3 trace + PMC passes
+# (profile_round.sh). Stops at the first failing step.
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+TAG=${TAG:-rX} bash scripts/gpu_check.sh || exit $?
+timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 --clips 256 --db-clips 20000 --queries 1024 --latency-queries 20 --stream-channels 64 --stream-ticks 20 --dist-backend gloo > gpurun_out/${TAG}_dist2.json 2> gpurun_out/${TAG}_dist2.err; rc=$?; echo "dist2 rc=$rc"; tail -3 gpurun_out/${TAG}_dist2.err; cat gpurun_out/${TAG}_dist2.json; [ $rc = 0 ] || exit $rc
+[ -n "$NOPROF" ] || R=${R:-r01} bash scripts/profile_round.sh
