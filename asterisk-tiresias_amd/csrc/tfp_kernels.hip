@@ -711,6 +711,21 @@ __device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const fl
   return acc;
 }
 
+#ifndef TFP8_TIMING
+#define TFP8_TIMING 0  // 1: lane 0 of each of the first 64 tiles' waves records s_memtime at 8 points
+#endif
+#if TFP8_TIMING
+__device__ unsigned long long g_tfp8_t[64][8];
+#define TFP8_TS(i)                                                                          \
+  do {                                                                                      \
+    const int tb_ = blockIdx.x * kBlockWaves + (threadIdx.x >> 6);                          \
+    if ((threadIdx.x & 63) == 0 && tb_ < 64) g_tfp8_t[tb_][i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TFP8_TS(i) \
+  do {             \
+  } while (0)
+#endif
 // kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
 // small batches: 4x the waves on a short query, a quarter of the per-wave latency).
 template <int kPasses>
@@ -733,6 +748,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
+  TFP8_TS(0);
   // Wave-uniform tile state (scalar registers): clip, first frame, clip sample range.
   struct Tile {
     int c;
@@ -775,39 +791,66 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   Tile cur = tile_of(b < ntiles ? b : 0);
 #if !TFP8_GLDS
   fetch(cur, 0, b < ntiles, pf);
+  TFP8_TS(1);
 #endif
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
   cf* winr = reinterpret_cast<cf*>(S.window);
   cf* twr = S.tw512;
-  for (int i = tid; i < 256; i += kBlockThreads) {
-    const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
-    const int j = (32 * n1 + 2 * L + 256) & 511;
-    winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
+  // Table staging: every global load below is issued before any LDS write (indices clamped,
+  // writes predicated), so a block waits for one round trip instead of one per table: a small
+  // launch is latency-bound (fp_timing.py: 4200 -> cycles to here).
+  static_assert(kBlockThreads == 256, "one entry per thread per table");
+  constexpr int kMsW = 16 * (LA + LB + LC);  // DspTables::fixed8k()'s ms_total
+  const int wL = (tid >> 1) & 15, wn1 = 2 * (tid >> 5) + (tid & 1);
+  const int wj = (32 * wn1 + 2 * wL + 256) & 511;
+  const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
 #if TFP8_PAIRSPLIT
-    // [k2][L] = (w512^k, w512^(256 - k)), k = L + 16 k2 (k2 < 8; lane 0 at k2 = 0: k = 128)
-    const int k2 = i >> 5, kk = (L == 0 && k2 == 0) ? 128 : L + 16 * k2, kp = 256 - kk;
-    twr[i] = (i & 1) ? cf{T->tw512_re[kp], T->tw512_im[kp]} : cf{T->tw512_re[kk], T->tw512_im[kk]};
+  // [k2][L] = (w512^k, w512^(256 - k)), k = L + 16 k2 (k2 < 8; lane 0 at k2 = 0: k = 128)
+  const int tk2 = tid >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
+  const int tk = (tid & 1) ? 256 - tkk : tkk;
 #else
-    const int k = col_of_lane(L) + 16 * n1;
-    twr[i] = cf{T->tw512_re[k], T->tw512_im[k]};
+  const int tk = col_of_lane(wL) + 16 * wn1;
 #endif
+  const float twre = T->tw512_re[tk], twim = T->tw512_im[tk];
+  const int li = tid < 240 ? tid : 239, lk1 = 1 + li / 16, lL = li % 16;
+  const float ltre = T->lane_tw_re[lk1][lL], ltim = T->lane_tw_im[lk1][lL];
+  const int i10 = tid < 10 ? tid : 9;
+  const float w16re = T->tw256_re[16 * i10], w16im = T->tw256_im[16 * i10];
+  const int i80 = tid < kCoefs * kFilters ? tid : kCoefs * kFilters - 1;
+  const float dctv = (&T->dct[0][0])[i80];
+  const int i48 = tid < 48 ? tid : 47;
+  const int msf = (&T->ms_filter[0][0])[i48], mss = (&T->ms_start[0][0])[i48];
+  const int i3 = tid < 3 ? tid : 2;
+  const int msl = T->ms_len[i3], mso = T->ms_woff[i3];
+  const LogfEntry lge = logf_table()[tid & 15];
+  float mw[(kMsW + kBlockThreads - 1) / kBlockThreads];
+#pragma unroll
+  for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
+    const int idx = tid + kBlockThreads * r;
+    mw[r] = T->ms_w[idx < kMsW ? idx : kMsW - 1];
   }
-  for (int i = tid; i < 15 * 16; i += kBlockThreads) {
-    const int k1 = 1 + i / 16, L = i % 16;
-    S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
+  const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
+  winr[tid] = cf{win0, win1};
+  twr[tid] = cf{twre, twim};
+  if (tid < 240) S.lane_tw[lk1 - 1][lL] = cf{ltre, ltim};
+  if (tid < 10) S.w16[tid] = cf{w16re, w16im};
+  if (tid < kCoefs * kFilters) (&S.dct[0][0])[tid] = dctv;
+  if (tid < 48) {
+    (&S.ms_filter[0][0])[tid] = msf;
+    (&S.ms_start[0][0])[tid] = mss;
   }
-  for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
-  for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
-  for (int i = tid; i < 48; i += kBlockThreads) {
-    (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
-    (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
-  }
-  if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
-  if (tid < 16) S.logf[tid] = logf_table()[tid];
+  if (tid < 3) { S.ms_len[tid] = msl; S.ms_woff[tid] = mso; }
+  if (tid < 16) S.logf[tid] = lge;
   if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
-  for (int i = tid; i < T->ms_total; i += kBlockThreads) S.ms_w[i] = 0.5f * T->ms_w[i];  // exact: w/2
+#pragma unroll
+  for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
+    const int idx = tid + kBlockThreads * r;
+    if (idx < kMsW) S.ms_w[idx] = 0.5f * mw[r];  // exact: w/2
+  }
+  const unsigned long long empty_filters = __ballot(lane < kFilters && mlen == 0);  // (log of 0 + 2e-42)
   __syncthreads();
+  TFP8_TS(2);
 
   const int sg = col_of_lane(L);  // second-stage FFT column (= bins sg + 16 k2) of this lane
 #if TFP8_DPP
@@ -851,7 +894,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const float lempty = aubio_log10_fast(0.f, S.logf);
     for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
       const int j = i % kFilters;
-      if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
+      if ((empty_filters >> j) & 1) M.logs[(i / kFilters) * kLogStride + j] = lempty;
     }
   }
 
@@ -917,6 +960,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
 #endif
       wave_sync();
+      TFP8_TS(3);
 #if TFP8_GLDS
       const int16_t* hop0 = pcur + grp * kHopStride;
 #else
@@ -980,6 +1024,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         dft16q(w16r, z, Y);  // Y[k2] = Z[sg + 16 k2]
       }
       wave_sync();
+      TFP8_TS(4);
       const float* wbase = S.ms_w + 4 * L + oz;
       float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
       if (TFP8_HOIST_W & 1) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
@@ -1130,6 +1175,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
       for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
       wave_sync();
+      TFP8_TS(5);
       float* lrow = M.logs + row * kLogStride;
       if constexpr (TFP8_ABL & 4) {
         lrow[fA] = N[L];
@@ -1157,6 +1203,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
+    TFP8_TS(6);
     if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];
       if (f >= 0) {
@@ -1188,6 +1235,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
+    TFP8_TS(7);
     cur = nxt;
   }
 }
@@ -1456,7 +1504,8 @@ __global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict
 }
 
 bool DspTables_fixed8k(const DspTables& t) {
-  return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
+  return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total == 16 * (36 + 16 + 8) &&
+         t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
 }
 
@@ -2530,3 +2579,9 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_b
 }
 
 }  // namespace tfp
+
+#if TFP8_TIMING
+extern "C" int tfp_debug_fp_timing(unsigned long long* out) {  // 64 x 8 s_memtime stamps
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tfp::g_tfp8_t), sizeof(tfp::g_tfp8_t)) == hipSuccess ? 0 : -2;
+}
+#endif

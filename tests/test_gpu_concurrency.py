@@ -1,0 +1,70 @@
+"""Concurrent callers on one engine. The reference's fp_search_fingerprint_info is called from many
+channel threads at once, plus the CLI and the load thread (SURVEY §8b threading row); the C-ABI
+serialises every call per engine, so results under concurrency must equal the serial ones.
+ctypes releases the GIL during each foreign call, so these threads really overlap in the C-ABI."""
+import threading
+
+import numpy as np
+import pytest
+
+from test_gpu_parity import _build_db, _queries
+
+pytestmark = pytest.mark.gpu
+
+
+def _key(r):
+    return None if r is None else (r["audio_uuid"], r["match_count"])
+
+
+def test_concurrent_searches_equal_serial(engine, oracle, tfp_lib):
+    _build_db(engine, oracle, tfp_lib, 120, 12)
+    qpcm = _queries(tfp_lib, 24, 120, 12, 5)
+    n = qpcm.shape[1]
+    params = [tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.1), tfp_lib.params(2, 0.5), tfp_lib.params(1, 0.001, 100, 3400)]
+    # serial answers: single queries (small path) per parameter set, and the fingerprints
+    want = {}
+    for pi, p in enumerate(params):
+        for q in range(24):
+            r, f = engine.search_pcm_batch(qpcm[q], [0, n], p)
+            want[pi, q] = (_key(r[0]), f[0])
+    fp_want = engine.fingerprint_batch(qpcm[:6].reshape(-1), np.arange(7) * n)
+
+    errors = []
+
+    def worker(t):
+        rng = np.random.default_rng(100 + t)
+        try:
+            for it in range(12):
+                pi = int(rng.integers(len(params)))
+                kind = int(rng.integers(4))
+                if kind == 0:  # one query (batch-1 path)
+                    q = int(rng.integers(24))
+                    r, f = engine.search_pcm_batch(qpcm[q], [0, n], params[pi])
+                    got = [(_key(r[0]), f[0])]
+                    exp = [want[pi, q]]
+                elif kind == 1:  # a few queries (small batch)
+                    q0 = int(rng.integers(0, 21))
+                    r, f = engine.search_pcm_batch(qpcm[q0:q0 + 3].reshape(-1), np.arange(4) * n, params[pi])
+                    got = [(_key(a), b) for a, b in zip(r, f)]
+                    exp = [want[pi, q] for q in range(q0, q0 + 3)]
+                elif kind == 2:  # the whole set (vote GEMM / class path)
+                    r, f = engine.search_pcm_batch(qpcm.reshape(-1), np.arange(25) * n, params[pi])
+                    got = [(_key(a), b) for a, b in zip(r, f)]
+                    exp = [want[pi, q] for q in range(24)]
+                else:  # fingerprints in between searches
+                    fr = engine.fingerprint_batch(qpcm[:6].reshape(-1), np.arange(7) * n)
+                    got = [bool(np.array_equal(fr["m1"], fp_want["m1"]) and np.array_equal(fr["m2"], fp_want["m2"]))]
+                    exp = [True]
+                if got != exp:
+                    errors.append((t, it, kind, pi, got[:3], exp[:3]))
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append((t, repr(ex)))
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=100)
+    assert not any(th.is_alive() for th in threads), "a caller thread did not finish"
+    assert not errors, errors[:5]
+    assert any(v[0] is not None for v in want.values())
