@@ -193,9 +193,12 @@ int upload(tfp_engine* e, DevBuf& d, const void* h, size_t bytes, hipStream_t s 
   return TFP_OK;
 }
 
-// Fingerprint host PCM; leaves micro/db on the device in e->micro / e->db.
-int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
+// Fingerprint host samples (int16 PCM, or with f32 the fp32 values aubio_source produced);
+// leaves micro/db on the device in e->micro / e->db.
+int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nclips, int32_t sr,
                      int64_t* nframes_out, std::vector<int64_t>* foff_out) {
+  const size_t ss = f32 ? sizeof(float) : sizeof(int16_t);
+  const char* src = static_cast<const char*>(pcm);
   const DspTables* T;
   bool fx = false;
   int rc = ensure_tables(e, sr, &T, &fx);
@@ -204,7 +207,7 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   std::vector<int32_t> toff, tclip;
   // small batches at 8 kHz: 4-frame wave tiles (4x the waves, a quarter of the per-wave passes)
   int tile_frames = kFramesPerBlock;
-  if (fx) {
+  if (fx && !f32) {
     int64_t nf16 = 0;
     for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(offsets[c + 1] - offsets[c]) + 15) / 16;
     if (nf16 <= 256) tile_frames = 4;
@@ -214,11 +217,11 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t b_pcm = al(sizeof(int16_t) * ns), b_so = al(sizeof(int64_t) * soff.size()),
+  const size_t b_pcm = al(ss * ns), b_so = al(sizeof(int64_t) * soff.size()),
                b_fo = al(sizeof(int64_t) * foff.size()), b_to = al(sizeof(int32_t) * toff.size()),
                b_tc = al(sizeof(int32_t) * tclip.size());
   const size_t total = b_pcm + b_so + b_fo + b_to + b_tc;
-  const int16_t* d_pcm;
+  const void* d_pcm;
   const int64_t *d_soff, *d_foff;
   const int32_t *d_toff, *d_tclip;
   if (total <= ((size_t)8 << 20)) {
@@ -229,7 +232,7 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
     HIPCHK(e, e->hstage.reserve(total));
     HIPCHK(e, e->dstage.reserve(total));
     char* h = e->hstage.as<char>();
-    if (ns) memcpy(h, pcm + offsets[0], sizeof(int16_t) * ns);
+    if (ns) memcpy(h, src + ss * offsets[0], ss * ns);
     memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
     memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
     memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
@@ -237,25 +240,30 @@ int fingerprint_host(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, 
     HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
     e->stage_pending = true;
     char* d = e->dstage.as<char>();
-    d_pcm = reinterpret_cast<const int16_t*>(d);
+    d_pcm = d;
     d_soff = reinterpret_cast<const int64_t*>(d + b_pcm);
     d_foff = reinterpret_cast<const int64_t*>(d + b_pcm + b_so);
     d_toff = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo);
     d_tclip = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo + b_to);
   } else {
-    if ((rc = upload(e, e->pcm, pcm + offsets[0], sizeof(int16_t) * ns))) return rc;
+    if ((rc = upload(e, e->pcm, src + ss * offsets[0], ss * ns))) return rc;
     if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
     if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
     if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
     if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
-    d_pcm = e->pcm.as<int16_t>();
+    d_pcm = e->pcm.p;
     d_soff = e->soff.as<int64_t>();
     d_foff = e->foff.as<int64_t>();
     d_toff = e->toff.as<int32_t>();
     d_tclip = e->tclip.as<int32_t>();
   }
-  HIPCHK(e, launch_fingerprint(T, fx, tile_frames, d_pcm, d_soff, d_soff + 1, d_foff, d_toff, d_tclip, toff[nclips], nf,
-                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+  if (f32)
+    HIPCHK(e, launch_fingerprint_f32(T, static_cast<const float*>(d_pcm), d_soff, d_soff + 1, d_foff, d_toff, d_tclip,
+                                     toff[nclips], e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+  else
+    HIPCHK(e, launch_fingerprint(T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
+                                 d_toff, d_tclip, toff[nclips], nf, e->micro.as<int32_t>(), e->db.as<double>(),
+                                 e->stream));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
   return TFP_OK;
@@ -642,8 +650,9 @@ void tfp_engine_destroy(tfp_engine* e) {
 __attribute__((visibility("hidden"))) const char* tfp_ingest_last_error();  // tfp_wav.cpp: engine-less errors of this thread
 const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : tfp_ingest_last_error(); }
 
-int tfp_fingerprint_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
-                          tfp_frame* out, int64_t cap, int64_t* nframes) {
+namespace {
+int fingerprint_batch_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nclips,
+                           int32_t sr, tfp_frame* out, int64_t cap, int64_t* nframes) {
   if (!e) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (!offsets || nclips < 0 || !nframes || (!pcm && nclips && offsets[nclips] > offsets[0]))
@@ -658,9 +667,20 @@ int tfp_fingerprint_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offs
   HIPCHK(e, hipSetDevice(e->device));
   int64_t nf;
   std::vector<int64_t> foff;
-  int rc = fingerprint_host(e, pcm, offsets, nclips, sr, &nf, &foff);
+  int rc = fingerprint_host(e, pcm, f32, offsets, nclips, sr, &nf, &foff);
   if (rc) return rc;
   return copy_frames_out(e, nf, foff, out);
+}
+}  // namespace
+
+int tfp_fingerprint_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
+                          tfp_frame* out, int64_t cap, int64_t* nframes) {
+  return fingerprint_batch_impl(e, pcm, false, offsets, nclips, sr, out, cap, nframes);
+}
+
+int tfp_fingerprint_f32_batch(tfp_engine* e, const float* x, const int64_t* offsets, int32_t nclips, int32_t sr,
+                              tfp_frame* out, int64_t cap, int64_t* nframes) {
+  return fingerprint_batch_impl(e, x, true, offsets, nclips, sr, out, cap, nframes);
 }
 
 int tfp_fingerprint_pcm(tfp_engine* e, const int16_t* pcm, int64_t n, int32_t sr, tfp_frame* out, int64_t cap,
@@ -936,8 +956,9 @@ int tfp_search(tfp_engine* e, const tfp_frame* frames, int32_t nframes, const tf
   return tfp_search_batch(e, frames, qoff, 1, P, out);
 }
 
-int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nq, int32_t sr,
-                         const tfp_search_params* P, tfp_result* out) {
+namespace {
+int search_samples_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
+                        const tfp_search_params* P, tfp_result* out) {
   if (!e || !offsets || nq < 0 || !out) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
@@ -947,13 +968,24 @@ int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offse
   std::vector<unsigned long long> keys(nq, 0ull);
   if (valid_params(P) && nq && foff[nq] > 0) {
     int64_t nf;
-    int rc = fingerprint_host(e, pcm, offsets, nq, sr, &nf, nullptr);
+    int rc = fingerprint_host(e, pcm, f32, offsets, nq, sr, &nf, nullptr);
     if (rc) return rc;
     if ((rc = search_core(e, foff.data(), nq, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
     e->stage_pending = false;  // search_core waited for e->stream (keys on the host)
   }
   fill_results(e, keys, foff.data(), nq, out);
   return TFP_OK;
+}
+}  // namespace
+
+int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offsets, int32_t nq, int32_t sr,
+                         const tfp_search_params* P, tfp_result* out) {
+  return search_samples_impl(e, pcm, false, offsets, nq, sr, P, out);
+}
+
+int tfp_search_f32_batch(tfp_engine* e, const float* x, const int64_t* offsets, int32_t nq, int32_t sr,
+                         const tfp_search_params* P, tfp_result* out) {
+  return search_samples_impl(e, x, true, offsets, nq, sr, P, out);
 }
 
 int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, const tfp_search_params* P,

@@ -110,22 +110,39 @@ struct WaveLds {
   union {
     cf scratch[4][kFrameStride];
     alignas(16) int16_t pcm[5 * kHopStride];
+    alignas(16) float pcmf[5 * kHopStride];  // fp32-sample launches of the generic kernel
   };
   float logs[kWaveFrames * kLogStride];
 };
-static_assert(sizeof(int16_t) * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride, "pcm alias fits");
+static_assert(sizeof(float) * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride, "pcm alias fits");
 static_assert(16 * kSq <= kFrameStride && 16 + 500 <= 2 * kFrameStride, "square and |X| rows (ms_maxbin <= 500) fit");
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
+template <typename Smp>
 struct PassSrc {
-  const int16_t* clip;
+  const Smp* clip;
   int64_t ns;
   int64_t sbase;
   bool aligned;  // clip + sbase is 16-byte aligned
 };
+// Sample types of the generic kernel: int16 PCM (x / 32768 folded into window_s) or the fp32
+// values aubio_source produced (multichannel mean, 24/32-bit, float WAV; tfp_wav_decode_f32).
+template <typename Smp>
+struct SmpLayout {
+  static constexpr int kPer = 16 / (int)sizeof(Smp);          // samples per 16-byte chunk
+  static constexpr int kChunks = kPassSamples / kPer;         // chunks per pass
+  static constexpr int kRounds = (kChunks + 63) / 64;         // wave-wide chunk rounds
+  static constexpr int kHopChunks = kHop / kPer;              // chunks per staged hop
+};
 
 // Slow path of one 16-byte chunk: clip edges (zeros outside [0, ns): aubio_source pads the last
 // hop, the phase vocoder's first history hop is zeros) and unaligned clips.
+__device__ __noinline__ int4 fetch_chunk_checked(const float* clip, int64_t ns, int64_t s) {
+  float v[4];
+  for (int e = 0; e < 4; e++) v[e] = (s + e >= 0 && s + e < ns) ? clip[s + e] : 0.f;
+  return make_int4(__builtin_bit_cast(int, v[0]), __builtin_bit_cast(int, v[1]), __builtin_bit_cast(int, v[2]),
+                   __builtin_bit_cast(int, v[3]));
+}
 __device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns, int64_t s) {
   uint32_t w[4];
   for (int e = 0; e < 4; e++) {
@@ -138,14 +155,17 @@ __device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns
 }
 
 // 16-byte chunks of a pass into registers, issued one pass ahead of use.
-__device__ __forceinline__ void fetch_pass(const PassSrc& p, bool valid, int lane, int4 (&pf)[kChunkRounds]) {
+template <typename Smp>
+__device__ __forceinline__ void fetch_pass(const PassSrc<Smp>& p, bool valid, int lane,
+                                           int4 (&pf)[SmpLayout<Smp>::kRounds]) {
+  using Ly = SmpLayout<Smp>;
 #pragma unroll
-  for (int r = 0; r < kChunkRounds; r++) {
+  for (int r = 0; r < Ly::kRounds; r++) {
     const int chunk = lane + 64 * r;
     int4 v = make_int4(0, 0, 0, 0);
-    if (valid && chunk < kPassChunks) {
-      const int64_t s = p.sbase + 8 * chunk;
-      if (p.aligned && s >= 0 && s + 8 <= p.ns) v = *reinterpret_cast<const int4*>(p.clip + s);
+    if (valid && chunk < Ly::kChunks) {
+      const int64_t s = p.sbase + Ly::kPer * chunk;
+      if (p.aligned && s >= 0 && s + Ly::kPer <= p.ns) v = *reinterpret_cast<const int4*>(p.clip + s);
       else v = fetch_chunk_checked(p.clip, p.ns, s);
     }
     pf[r] = v;
@@ -290,15 +310,19 @@ __device__ __forceinline__ float sqrtf_fast_cr(float x) {
 // whose chained DPP reads cost wait states.
 __device__ __forceinline__ float partner16(float v) { return __shfl(v, (16 - (int)(threadIdx.x & 15)) & 15, 16); }
 
+template <typename Smp>
 __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kernel(
-    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
+    const DspTables* __restrict__ T, const Smp* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip,
     int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
   const int tid = threadIdx.x;
-  for (int i = tid; i < kWin; i += kBlockThreads) S.window[i] = T->window_s[i];
+  using Ly = SmpLayout<Smp>;
+  constexpr bool kF32 = sizeof(Smp) == 4;
+  // int16: hanningz * 2^-15 (aubio's x / 32768 folded in, exact); fp32 samples: hanningz
+  for (int i = tid; i < kWin; i += kBlockThreads) S.window[i] = kF32 ? T->window[i] : T->window_s[i];
   for (int i = tid; i < 15 * 16; i += kBlockThreads) {
     const int k1 = 1 + i / 16, L = i % 16;
     S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
@@ -354,7 +378,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   }
 
   auto pass_src = [&](int c, int64_t f0, int sub) {
-    PassSrc p;
+    PassSrc<Smp> p;
     const int64_t s0 = sbeg[c];
     p.clip = pcm + s0;
     p.ns = send[c] - s0;
@@ -363,7 +387,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
     return p;
   };
 
-  int4 pf[kChunkRounds];
+  int4 pf[Ly::kRounds];
   int b = blockIdx.x * kBlockWaves + wave;
   int c = b < ntiles ? tclip[b] : 0;
   int64_t f0 = b < ntiles ? (int64_t)(b - toff[c]) * kWaveFrames : 0;
@@ -381,11 +405,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       const int64_t f = cur_f0 + row;
       // stage this pass's PCM (prefetched; hop h at h * kHopStride) and prefetch the next pass
       wave_sync();  // the previous pass's readers of the scratch are done
+      Smp* const stage = reinterpret_cast<Smp*>(kF32 ? (void*)M.pcmf : (void*)M.pcm);
 #pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
+      for (int r = 0; r < Ly::kRounds; r++) {
         const int chunk = lane + 64 * r;
-        if (chunk < kPassChunks)
-          *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+        if (chunk < Ly::kChunks)
+          *reinterpret_cast<int4*>(stage + (chunk / Ly::kHopChunks) * kHopStride + (chunk % Ly::kHopChunks) * Ly::kPer) =
+              pf[r];
       }
       {
         const bool same = sub < 3;
@@ -395,7 +421,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
       // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
       // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
-      const int16_t* hop0 = M.pcm + grp * kHopStride;
+      const Smp* hop0 = stage + grp * kHopStride;
       // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
       // ~90 of them into registers for the whole kernel (occupancy).
       int oz = 0;
@@ -415,9 +441,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
         for (int n1 = 0; n1 < 16; n1++) {
           const int j = (32 * n1 + 2 * L + 256) & 511;
           const int hsel = n1 < 8 ? 1 : 0;
-          const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
           const cf wj = *reinterpret_cast<const cf*>(win + j);  // j even
-          z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wj;  // (s / 32768) * hanningz[j]
+          if constexpr (kF32) {
+            z[n1] = *reinterpret_cast<const cf*>(hop0 + hsel * kHopStride + (j & 255)) * wj;  // x * hanningz[j]
+          } else {
+            const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
+            z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wj;  // (s / 32768) * hanningz[j]
+          }
         }
       }
       if (ablate & 2) {
@@ -1530,7 +1560,7 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t t
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (v) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint8k_kernel<4>, kBlockThreads, 0);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel, kBlockThreads, 0);
+    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel<int16_t>, kBlockThreads, 0);
     grid_cap[v] = cus * (per > 0 ? per : 1);
   }
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
@@ -1561,8 +1591,27 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t t
     const char* a = getenv("TFP_ABLATE");
     ablate = a ? atoi(a) : 0;
   }
-  hipLaunchKernelGGL(fingerprint_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send, d_foff,
-                     d_toff, d_tclip, ntiles, d_micro, d_db, ablate);
+  hipLaunchKernelGGL(fingerprint_kernel<int16_t>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, ablate);
+  return hipGetLastError();
+}
+
+hipError_t launch_fingerprint_f32(const DspTables* d_tables, const float* d_x, const int64_t* d_sbeg,
+                                  const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
+                                  const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s) {
+  if (ntiles <= 0) return hipSuccess;
+  static int grid_cap = 0;
+  if (!grid_cap) {
+    int dev = 0, cus = 256, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel<float>, kBlockThreads, 0);
+    grid_cap = cus * (per > 0 ? per : 1);
+  }
+  const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;
+  const int grid = want < grid_cap ? want : grid_cap;
+  hipLaunchKernelGGL(fingerprint_kernel<float>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_x, d_sbeg, d_send,
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, 0);
   return hipGetLastError();
 }
 

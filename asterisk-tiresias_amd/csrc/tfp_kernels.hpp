@@ -43,6 +43,11 @@ hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t t
                               const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
                               const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
                               hipStream_t s);
+// fp32 samples (the values aubio_source_do produces: multichannel mean, 24/32-bit or float
+// WAV, tfp_wav_decode_f32) through the generic kernel, 16-frame tiles; same outputs as above.
+hipError_t launch_fingerprint_f32(const DspTables* d_tables, const float* d_x, const int64_t* d_sbeg,
+                                  const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
+                                  const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
 

@@ -54,6 +54,10 @@ _SIGS = {
     "tfp_frame_count": (C.c_int64, [C.c_int64]),
     "tfp_wav_decode": (C.c_int, [P, C.c_int64, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_wav_read": (C.c_int, [C.c_char_p, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "tfp_wav_decode_f32": (C.c_int, [P, C.c_int64, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "tfp_wav_read_f32": (C.c_int, [C.c_char_p, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "tfp_fingerprint_f32_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
+    "tfp_search_f32_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_fingerprint_pcm": (C.c_int, [P, P, C.c_int64, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
     "tfp_fingerprint_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
     "tfp_plan_create": (C.c_int, [P, P, C.c_int32, C.c_int32, C.POINTER(P)]),

@@ -26,10 +26,10 @@ def params(coefs=1, tolerance=-1.0, freq_ignore_low=-1, freq_ignore_high=-1) -> 
     return SearchParams(int(coefs), int(freq_ignore_low), int(freq_ignore_high), 0, float(tolerance))
 
 
-def _wav(call) -> tuple[np.ndarray, int]:
+def _wav(call, dtype=np.int16) -> tuple[np.ndarray, int]:
     n, sr = C.c_int64(), C.c_int32()
     check(call(None, 0, C.byref(n), C.byref(sr)))
-    pcm = np.empty(n.value, np.int16)
+    pcm = np.empty(n.value, dtype)
     check(call(pcm.ctypes.data, n.value, C.byref(n), C.byref(sr)))
     return pcm, sr.value
 
@@ -45,6 +45,19 @@ def read_wav(path: str) -> tuple[np.ndarray, int]:
     """tfp_wav_read: decode_wav of a file."""
     p = path.encode()
     return _wav(lambda pcm, cap, n, sr: lib().tfp_wav_read(p, pcm, cap, n, sr))
+
+
+def decode_wav_f32(data: bytes) -> tuple[np.ndarray, int]:
+    """tfp_wav_decode_f32: RIFF/WAVE bytes -> (fp32 mono hop values as aubio_source computes them,
+    native rate), for every PCM width / float format and channel count."""
+    buf = C.create_string_buffer(bytes(data), len(data))
+    return _wav(lambda x, cap, n, sr: lib().tfp_wav_decode_f32(buf, len(data), x, cap, n, sr), np.float32)
+
+
+def read_wav_f32(path: str) -> tuple[np.ndarray, int]:
+    """tfp_wav_read_f32: decode_wav_f32 of a file."""
+    p = path.encode()
+    return _wav(lambda x, cap, n, sr: lib().tfp_wav_read_f32(p, x, cap, n, sr), np.float32)
 
 
 def synth_specs(seed: int, clips, offsets=None):
@@ -118,6 +131,18 @@ class Engine:
         got = C.c_int64()
         self._chk(lib().tfp_fingerprint_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nclips, sample_rate,
                                               out.ctypes.data, n, C.byref(got)))
+        return out[:n]
+
+    def fingerprint_f32_batch(self, x: np.ndarray, offsets, sample_rate: int = 8000) -> np.ndarray:
+        """tfp_fingerprint_f32_batch: fingerprint_batch over fp32 hop values (decode_wav_f32)."""
+        x = np.ascontiguousarray(x, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nclips = len(offsets) - 1
+        n = sum(frame_count(int(offsets[i + 1] - offsets[i])) for i in range(nclips))
+        out = np.zeros(max(n, 1), FRAME_DTYPE)
+        got = C.c_int64()
+        self._chk(lib().tfp_fingerprint_f32_batch(self._h, x.ctypes.data, offsets.ctypes.data, nclips, sample_rate,
+                                                  out.ctypes.data, n, C.byref(got)))
         return out[:n]
 
     # ---- index ----------------------------------------------------------------------
@@ -195,6 +220,16 @@ class Engine:
         nq = len(offsets) - 1
         res = (Result * max(1, nq))()
         self._chk(lib().tfp_search_pcm_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nq, sample_rate,
+                                             C.byref(p), res))
+        return self._results(res, nq)
+
+    def search_f32_batch(self, x: np.ndarray, offsets, p: SearchParams, sample_rate: int = 8000):
+        """tfp_search_f32_batch: search_pcm_batch over fp32 hop values."""
+        x = np.ascontiguousarray(x, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nq = len(offsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_search_f32_batch(self._h, x.ctypes.data, offsets.ctypes.data, nq, sample_rate,
                                              C.byref(p), res))
         return self._results(res, nq)
 

@@ -27,7 +27,9 @@ import numpy as np
 
 from . import dbio
 from ._lib import TfpError
-from .engine import Engine, params, read_wav
+from .engine import Engine, params, read_wav, read_wav_f32
+
+TFP_E_FORMAT = -8
 
 DEF_SEARCH_TOLERANCE = 0.001  # fp_handler.c:41
 DEF_AUBIO_COEFS = 2           # fp_handler.c:39
@@ -38,6 +40,18 @@ def read_wav_mono16(filename: str):
     int16 PCM + rate, decoded by the engine library (tfp_wav_read). Raises TfpError for a
     missing file (TFP_E_NOENT) or audio the engine cannot take exactly (TFP_E_FORMAT)."""
     return read_wav(filename)
+
+
+def read_audio(filename: str):
+    """aubio_source's mono hop values of a WAV file: int16 PCM (tfp_wav_read) when they are int16
+    steps (8/16-bit mono), else the fp32 values (tfp_wav_read_f32: multichannel mean, 24/32-bit,
+    float). Raises TfpError (TFP_E_NOENT, TFP_E_FORMAT for non-WAV / unsupported encodings)."""
+    try:
+        return read_wav(filename)
+    except TfpError as e:
+        if e.code != TFP_E_FORMAT:
+            raise
+    return read_wav_f32(filename)
 
 
 def write_wav_mono16(filename: str, pcm: np.ndarray, sample_rate: int = 8000):
@@ -153,13 +167,18 @@ class FpHandler:
         self.db.execute("insert into audio_list(uuid, name, context, hash) values (?, ?, ?, ?);",
                         (uuid, os.path.basename(filename), context, h))
         try:
-            pcm, sr = read_wav_mono16(filename)
-            fr = self.engine.fingerprint(pcm, sr)
+            pcm, sr = read_audio(filename)
+            fr = self._fingerprint(pcm, [0, len(pcm)], sr)
             self.engine.index_add(uuid, fr["m1"], fr["m2"])
         except Exception:
             self.fp_delete_audio_list_info(uuid)
             return False
         return True
+
+    def _fingerprint(self, samples: np.ndarray, offsets, sr: int):
+        if samples.dtype == np.float32:
+            return self.engine.fingerprint_f32_batch(samples, offsets, sr)
+        return self.engine.fingerprint_batch(samples, offsets, sr)
 
     def create_new_audio_info(self, context: str) -> bool:
         """app_tiresias.c:365-424 (the module's directory enrolment) batched onto the GPU.
@@ -188,7 +207,7 @@ class FpHandler:
                                             (context, h)).fetchone():
                 continue  # already enrolled
             try:
-                pcm, sr = read_wav_mono16(path)
+                pcm, sr = read_audio(path)
             except TfpError:
                 continue
             uuid = self.fp_generate_uuid()
@@ -196,12 +215,11 @@ class FpHandler:
                             (uuid, os.path.basename(path), context, h))
             seen.add(h)
             new.append((uuid, pcm, sr))
-        for sr in sorted({n[2] for n in new}):
-            group = [n for n in new if n[2] == sr]
+        for sr, dt in sorted({(n[2], n[1].dtype.str) for n in new}):
+            group = [n for n in new if n[2] == sr and n[1].dtype.str == dt]
             lens = [len(n[1]) for n in group]
             off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
-            fr = self.engine.fingerprint_batch(np.concatenate([n[1] for n in group]) if group else np.zeros(0, np.int16),
-                                               off, sr)
+            fr = self._fingerprint(np.concatenate([n[1] for n in group]), off, sr)
             foff = np.concatenate([[0], np.cumsum([(n + 255) // 256 for n in lens])]).astype(np.int64)
             self.engine.index_add_batch([n[0] for n in group], foff, fr["m1"], fr["m2"])
         return True
@@ -226,11 +244,14 @@ class FpHandler:
         if coefs < 1 or coefs > DEF_AUBIO_COEFS:
             return None
         try:
-            pcm, sr = read_wav_mono16(filename)
+            pcm, sr = read_audio(filename)
         except TfpError:
             return None
-        res, _ = self.engine.search_pcm_batch(pcm, [0, len(pcm)],
-                                              params(coefs, tolerance, freq_ignore_low, freq_ignore_high), sr)
+        p = params(coefs, tolerance, freq_ignore_low, freq_ignore_high)
+        if pcm.dtype == np.float32:
+            res, _ = self.engine.search_f32_batch(pcm, [0, len(pcm)], p, sr)
+        else:
+            res, _ = self.engine.search_pcm_batch(pcm, [0, len(pcm)], p, sr)
         hit = res[0]
         if hit is None:
             return None

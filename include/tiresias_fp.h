@@ -103,6 +103,17 @@ int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
 int tfp_wav_decode(const void* bytes, int64_t nbytes, int16_t* pcm, int64_t cap, int64_t* nsamples,
                    int32_t* sample_rate);
 int tfp_wav_read(const char* path, int16_t* pcm, int64_t cap, int64_t* nsamples, int32_t* sample_rate);
+/* RIFF/WAVE -> the fp32 mono hop values aubio_source_do produces (fp_handler.c:604, :633), for
+ * every file tfp_wav_decode refuses as well: 8/16/24/32-bit integer PCM and 32/64-bit float
+ * (format 3, or EXTENSIBLE), any channel count. Per sample: unsigned 8-bit (u - 128) / 128,
+ * signed w-bit x / 2^(w-1) (32-bit x rounded to float first, as libsndfile's normalised read),
+ * float as stored, double rounded to float; per frame the channels are summed in fp32 in channel
+ * order and divided by the channel count in fp32 (aubio 0.4.5 sndfile/wavread downmix). Feed
+ * the result to tfp_fingerprint_f32_batch / tfp_search_f32_batch. Same size-query, capacity and
+ * error conventions as tfp_wav_decode. Host-only. */
+int tfp_wav_decode_f32(const void* bytes, int64_t nbytes, float* x, int64_t cap, int64_t* nsamples,
+                       int32_t* sample_rate);
+int tfp_wav_read_f32(const char* path, float* x, int64_t cap, int64_t* nsamples, int32_t* sample_rate);
 
 /* ---- fingerprinting: create_audio_fingerprints (fp_handler.c:577-671) -------------- */
 /* One clip of mono int16 PCM at its native rate (DEF_AUBIO_SAMPLERATE 0, :37). */
@@ -112,6 +123,11 @@ int tfp_fingerprint_pcm(tfp_engine* eng, const int16_t* pcm, int64_t nsamples, i
  * clip order (clip c starts at sum of tfp_frame_count of clips < c). */
 int tfp_fingerprint_batch(tfp_engine* eng, const int16_t* pcm, const int64_t* offsets, int32_t nclips,
                           int32_t sample_rate, tfp_frame* out, int64_t cap, int64_t* nframes);
+/* The same over fp32 hop values (tfp_wav_decode_f32: multichannel, 24/32-bit or float audio):
+ * aubio's x is taken as given instead of int16 / 32768. For int16-valued input (x = s / 32768)
+ * the frames equal tfp_fingerprint_batch's on s. */
+int tfp_fingerprint_f32_batch(tfp_engine* eng, const float* x, const int64_t* offsets, int32_t nclips,
+                              int32_t sample_rate, tfp_frame* out, int64_t cap, int64_t* nframes);
 
 /* Device-resident batches (inputs already in HBM; used by the benchmark and by callers that
  * keep PCM on the GPU). A plan uploads the clip layout once. d_micro receives 2 int32 per
@@ -160,6 +176,9 @@ int tfp_search_batch(tfp_engine* eng, const tfp_frame* frames, const int64_t* qo
 /* PCM in, results out: fingerprints the queries on the GPU and searches without a host
  * round trip of the frames (fp_handler.c:275 + :287-374). */
 int tfp_search_pcm_batch(tfp_engine* eng, const int16_t* pcm, const int64_t* offsets, int32_t nqueries,
+                         int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+/* The same over fp32 hop values (tfp_wav_decode_f32). */
+int tfp_search_f32_batch(tfp_engine* eng, const float* x, const int64_t* offsets, int32_t nqueries,
                          int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
 /* Device form for benchmarks / sharded search: per query a 64-bit key
  * (match_count << 32 | tiebreak key), 0 = NOTFOUND, written to d_keys[nqueries] (device).

@@ -234,8 +234,11 @@ int64_t tfo_fmt6(double x) {
 
 /* ---------------------------------------------------------------- per-clip DSP ------ */
 
-size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float* coef, double* db,
-                       int32_t* micro) {
+/* One clip whose aubio_source_do hop values come either from int16 PCM (pcm: s / 32768.f, the
+ * 16-bit sndfile/wavread conversion) or are given as fp32 (x: multichannel mean, 24/32-bit or
+ * float data, as tfp_wav_decode_f32 restates aubio's source for them). */
+static size_t fingerprint_core(const tfo_tables* t, const int16_t* pcm, const float* xin, size_t n, float* coef,
+                               double* db, int32_t* micro) {
   float data[TFO_WIN], dataold[TFO_WIN - TFO_HOP], x[TFO_WIN], norm[TFO_BINS];
   float band[TFO_FILTERS], out[TFO_COEFS];
   size_t nf = tfo_frame_count(n), f;
@@ -246,7 +249,7 @@ size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float*
     float hop[TFO_HOP];
     for (i = 0; i < TFO_HOP; i++) {
       size_t s = f * TFO_HOP + (size_t)i;
-      hop[i] = s < n ? (float)pcm[s] * (1.0f / 32768.0f) : 0.0f;
+      hop[i] = s >= n ? 0.0f : pcm ? (float)pcm[s] * (1.0f / 32768.0f) : xin[s];
     }
     /* aubio_pvoc_do: swapbuffers, fvec_weight, fvec_shift, fft, norm */
     for (i = 0; i < TFO_WIN - TFO_HOP; i++) data[i] = dataold[i];
@@ -275,6 +278,16 @@ size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float*
     }
   }
   return nf;
+}
+
+size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float* coef, double* db,
+                       int32_t* micro) {
+  return fingerprint_core(t, pcm, NULL, n, coef, db, micro);
+}
+
+size_t tfo_fingerprint_f32(const tfo_tables* t, const float* x, size_t n, float* coef, double* db,
+                           int32_t* micro) {
+  return fingerprint_core(t, NULL, x, n, coef, db, micro);
 }
 
 typedef struct {

@@ -50,6 +50,8 @@ def lib():
         L.tfo_frame_count.restype = C.c_size_t
         L.tfo_fingerprint.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
         L.tfo_fingerprint.restype = C.c_size_t
+        L.tfo_fingerprint_f32.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.tfo_fingerprint_f32.restype = C.c_size_t
         L.tfo_fingerprint_batch.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.tfo_fingerprint_batch.restype = C.c_size_t
         L.tfo_search.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_char_p), C.c_int32,
@@ -95,6 +97,38 @@ def fingerprint(pcm: np.ndarray, sample_rate: int = 8000):
     lib().tfo_fingerprint(C.byref(tables(sample_rate)), pcm.ctypes.data, len(pcm), coef.ctypes.data,
                           db.ctypes.data, micro.ctypes.data)
     return coef, db, micro
+
+
+def fingerprint_f32(x: np.ndarray, sample_rate: int = 8000):
+    """fingerprint() from fp32 hop values (aubio's source output) instead of int16 PCM."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    nf = frame_count(len(x))
+    coef = np.zeros((nf, 2), np.float32)
+    db = np.zeros((nf, 2), np.float64)
+    micro = np.zeros((nf, 2), np.int32)
+    lib().tfo_fingerprint_f32(C.byref(tables(sample_rate)), x.ctypes.data, len(x), coef.ctypes.data,
+                              db.ctypes.data, micro.ctypes.data)
+    return coef, db, micro
+
+
+def wav_mono_f32(frames: np.ndarray, bits: int, is_float: bool = False) -> np.ndarray:
+    """aubio 0.4.5's source output for decoded WAV frames [n, channels] (restated in numpy fp32,
+    the restatement tfp_wav_decode_f32 is checked against): per sample (u - 128) / 128 for 8-bit,
+    x / 2^(bits-1) for 16/24-bit, fp32(x) * 2^-31 for 32-bit, float data as fp32; then the channels
+    summed in fp32 in channel order and divided by the channel count in fp32."""
+    f32 = np.float32
+    if is_float:
+        v = frames.astype(np.float32)
+    elif bits == 8:
+        v = (frames.astype(np.int32) - 128).astype(f32) / f32(128)
+    elif bits == 32:
+        v = frames.astype(np.int32).astype(f32) * f32(2.0 ** -31)
+    else:
+        v = frames.astype(np.int32).astype(f32) / f32(2.0 ** (bits - 1))
+    acc = np.zeros(v.shape[0], f32)
+    for c in range(v.shape[1]):
+        acc = (acc + v[:, c]).astype(f32)
+    return (acc / f32(v.shape[1])).astype(f32)
 
 
 def fingerprint_batch(pcm: np.ndarray, offsets: np.ndarray, sample_rate: int = 8000, nthreads: int = 1,

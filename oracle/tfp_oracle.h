@@ -43,6 +43,10 @@ size_t tfo_frame_count(size_t nsamples);
  * micro[2f..] = "%f" micro-units or TFO_NULL. Any output pointer may be NULL. Returns frames. */
 size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float* coef, double* db,
                        int32_t* micro);
+/* The same from fp32 hop values x (aubio's source output for multichannel / 24-32-bit / float
+ * audio) instead of int16 PCM: x[s] replaces pcm[s] / 32768.f. */
+size_t tfo_fingerprint_f32(const tfo_tables* t, const float* x, size_t n, float* coef, double* db,
+                           int32_t* micro);
 
 /* Batch of clips over `nthreads` POSIX threads (cpu_baseline). offsets has nclips+1 entries
  * (sample offsets); frame outputs are concatenated in clip order. Returns total frames. */

@@ -73,3 +73,55 @@ def test_directory_enrolment_bad_context(tfp_lib, tmp_path):
         assert not h.create_new_audio_info("c2")
     finally:
         h.fp_term()
+
+
+def test_stereo_and_24bit_enrolment_through_fp32_path(tfp_lib, oracle, tmp_path):
+    """Files the int16 ingest refuses (stereo 16-bit, 24-bit) are enrolled through
+    tfp_wav_read_f32 + tfp_fingerprint_f32_batch; stored rows equal the oracle's fingerprints of
+    aubio's fp32 source values; the mirror's search reads them the same way."""
+    import struct
+    from tiresias_amd import FpHandler
+    pcm = tfp_lib.synth_pcm(0x7153A1, [1, 2], 40000)
+
+    def riff(ch, bits, data):
+        align = ch * bits // 8
+        fmt = struct.pack("<HHIIHH", 1, ch, 8000, 8000 * align, align, bits)
+        body = b"WAVE" + b"fmt " + struct.pack("<I", 16) + fmt + b"data" + struct.pack("<I", len(data)) + data
+        return b"RIFF" + struct.pack("<I", len(body)) + body
+
+    d = tmp_path / "st"
+    d.mkdir()
+    st = np.stack([pcm[0], pcm[1]], 1)
+    (d / "a_stereo.wav").write_bytes(riff(2, 16, st.astype("<i2").tobytes()))
+    x24 = (pcm[0].astype(np.int64) << 8) + np.arange(40000) % 256
+    u = x24 & 0xFFFFFF
+    (d / "b_24bit.wav").write_bytes(riff(1, 24, np.stack([u & 255, (u >> 8) & 255, u >> 16], 1).astype(np.uint8).tobytes()))
+    want = {"a_stereo.wav": oracle.wav_mono_f32(st, 16), "b_24bit.wav": oracle.wav_mono_f32(x24[:, None], 24)}
+    h = FpHandler(0)
+    assert h.fp_init()
+    try:
+        assert h.fp_create_context_list_info("ctx", str(d), False)
+        assert h.create_new_audio_info("ctx")
+        rows = {r["name"]: r["uuid"] for r in h.fp_get_audio_lists_all()}
+        assert sorted(rows) == sorted(want)
+        for name, x in want.items():
+            m1, m2 = h.engine.index_rows(rows[name])
+            _, _, micro = oracle.fingerprint_f32(x)
+            assert np.array_equal(m1, micro[:, 0]) and np.array_equal(m2, micro[:, 1]), name
+        # the mirror's search of the stereo file = the oracle's fp_search_fingerprint_info over the
+        # enrolled rows, with the query's fp32 fingerprints
+        names = sorted(want)
+        uuids = [rows[n] for n in names]
+        mic = [oracle.fingerprint_f32(want[n])[2] for n in names]
+        m1 = np.concatenate([m[:, 0] for m in mic])
+        m2 = np.concatenate([m[:, 1] for m in mic])
+        clip = np.concatenate([np.full(len(m), i, np.int32) for i, m in enumerate(mic)])
+        _, qdb, _ = oracle.fingerprint_f32(want["a_stereo.wav"])
+        for tol in (0.45, 0.001):
+            res = h.fp_search_fingerprint_info("ctx", str(d / "a_stereo.wav"), 1, tol, -1, -1)
+            found, w, mc, fc = oracle.search(m1, m2, clip, uuids, qdb[:, 0], qdb[:, 1], 1, tol)
+            assert (res is not None) == found
+            if found:
+                assert (res["uuid"], res["match_count"], res["frame_count"]) == (uuids[w], mc, fc) == (uuids[w], mc, 157)
+    finally:
+        h.fp_term()

@@ -356,3 +356,67 @@ def test_vote_paths_vs_oracle(engine, oracle, tfp_lib, spread, class_max):
         nfound += found
     assert nfound > nq // 2
     engine.index_clear()
+
+
+# ---- fp32-sample path (tfp_fingerprint_f32_batch / tfp_search_f32_batch) ------------------
+def _f32_cases(tfp_lib):
+    """aubio hop values that are not int16 steps: stereo / 3-channel means of synthetic clips (as
+    tfp_wav_decode_f32 computes them), 24-bit-like fine values, and edge lengths."""
+    import oracle_py
+    rng = np.random.default_rng(21)
+    a = tfp_lib.synth_pcm(SEED_DB, [1, 2, 3], 30000)
+    cases = {
+        "stereo": oracle_py.wav_mono_f32(a[:2].T, 16),
+        "3ch": oracle_py.wav_mono_f32(a.T, 16),
+        "24bit": oracle_py.wav_mono_f32(rng.integers(-(1 << 23), 1 << 23, (20000, 2)), 24),
+        "float": (rng.standard_normal(7000) * 0.2).astype(np.float32),
+        "tiny": (rng.standard_normal(3000) * 1e-7).astype(np.float32),
+    }
+    for n in (0, 1, 255, 256, 257):
+        cases["len%d" % n] = (rng.standard_normal(n) * 0.5).astype(np.float32)
+    return cases
+
+
+@pytest.mark.parametrize("sr", [8000, 16000])
+def test_fingerprint_f32_bit_exact(engine, oracle, tfp_lib, sr):
+    cases = _f32_cases(tfp_lib)
+    xs = list(cases.values())
+    off = np.concatenate([[0], np.cumsum([len(x) for x in xs])]).astype(np.int64)
+    fr = engine.fingerprint_f32_batch(np.concatenate(xs), off, sr)
+    want = [oracle.fingerprint_f32(x, sr) for x in xs]
+    micro = np.concatenate([w[2] for w in want]) if len(fr) else np.zeros((0, 2), np.int32)
+    db = np.concatenate([w[1] for w in want]) if len(fr) else np.zeros((0, 2))
+    _assert_frames_equal(fr, micro, db)
+    single = engine.fingerprint_f32_batch(cases["stereo"], [0, len(cases["stereo"])], sr)
+    assert np.array_equal(single["m1"], fr["m1"][:len(single)])
+
+
+def test_f32_path_equals_int16_path(engine, tfp_lib):
+    """x = s / 32768 through the fp32 kernel gives the int16 path's frames (aubio's value is the
+    same real number; the window scaling by 2^-15 is exact)."""
+    pcm = tfp_lib.synth_pcm(SEED_Q, [4, 5], 24000).reshape(-1)
+    off = np.array([0, 24000, 48000], np.int64)
+    a = engine.fingerprint_batch(pcm, off)
+    b = engine.fingerprint_f32_batch(pcm.astype(np.float32) / np.float32(32768), off)
+    assert np.array_equal(a["m1"], b["m1"]) and np.array_equal(a["m2"], b["m2"])
+    assert np.array_equal(a["q1"], b["q1"]) and np.array_equal(a["q2"], b["q2"])
+
+
+def test_search_f32_equals_frame_search(engine, oracle, tfp_lib):
+    """search_f32_batch == tfp_search_batch on the fp32 path's own frames (whose search is the
+    SQL-golden-pinned path), for stereo-mean queries of enrolled clips."""
+    _build_db(engine, oracle, tfp_lib, 60, 12)
+    import oracle_py
+    q = tfp_lib.synth_pcm(SEED_DB, [7, 9, 11, 13], 40000, offsets=[2560, 0, 5120, 256])
+    xs = [oracle_py.wav_mono_f32(np.stack([q[i], q[(i + 1) % 4]], 1), 16) for i in range(4)]
+    xs.append(oracle_py.wav_mono_f32(np.stack([q[0], q[0]], 1), 16))  # identical channels: == int16 path
+    off = np.concatenate([[0], np.cumsum([len(x) for x in xs])]).astype(np.int64)
+    for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.45), tfp_lib.params(2, 0.5)):
+        got, fc = engine.search_f32_batch(np.concatenate(xs), off, p)
+        fr = engine.fingerprint_f32_batch(np.concatenate(xs), off)
+        qoff = np.concatenate([[0], np.cumsum([(len(x) + 255) // 256 for x in xs])]).astype(np.int64)
+        want, fw = engine.search_batch(fr, qoff, p)
+        assert got == want and list(fc) == list(fw)
+    r16, _ = engine.search_pcm_batch(q[0], [0, 40000], tfp_lib.params(1, 0.001))
+    r32, _ = engine.search_f32_batch(xs[4], [0, 40000], tfp_lib.params(1, 0.001))
+    assert r32 == r16

@@ -125,3 +125,77 @@ def test_capacity_and_missing_file(tmp_path):
     with pytest.raises(TfpError) as e:
         read_wav(str(tmp_path / "absent.wav"))
     assert e.value.code == TFP_E_NOENT
+
+
+# ---- fp32 form (tfp_wav_decode_f32): every encoding, channels averaged as aubio does ---------
+def _frames(rng, n, ch, bits, is_float=False):
+    if is_float:
+        return (rng.standard_normal((n, ch)) * 0.3).astype(np.float64 if bits == 64 else np.float32)
+    if bits == 8:
+        return rng.integers(0, 256, (n, ch)).astype(np.uint8)
+    lo, hi = -(1 << (bits - 1)), 1 << (bits - 1)
+    x = rng.integers(lo, hi, (n, ch), dtype=np.int64)
+    x[:3] = [[lo] * ch, [hi - 1] * ch, [0] * ch][:min(3, n)]  # extremes
+    return x
+
+
+def _data_bytes(fr, bits, is_float):
+    if is_float:
+        return fr.astype("<f8" if bits == 64 else "<f4").tobytes()
+    if bits == 8:
+        return fr.astype(np.uint8).tobytes()
+    if bits == 24:
+        u = fr.astype(np.int64).reshape(-1) & 0xFFFFFF
+        return np.stack([u & 0xFF, (u >> 8) & 0xFF, (u >> 16) & 0xFF], 1).astype(np.uint8).tobytes()
+    return fr.astype("<i2" if bits == 16 else "<i4").tobytes()
+
+
+@pytest.mark.parametrize("ch,bits,is_float", [(2, 16, False), (3, 16, False), (6, 16, False), (2, 8, False),
+                                              (1, 24, False), (2, 24, False), (1, 32, False), (2, 32, False),
+                                              (1, 32, True), (2, 32, True), (2, 64, True), (1, 16, False)])
+def test_f32_decode_equals_aubio_restatement(oracle, ch, bits, is_float):
+    """Parity of the fp32 ingest with oracle_py.wav_mono_f32 (the numpy restatement of aubio
+    0.4.5's sndfile/wavread conversion and channel mean), bit for bit."""
+    from tiresias_amd.engine import decode_wav_f32
+    rng = np.random.default_rng(ch * 100 + bits)
+    fr = _frames(rng, 5000, ch, bits, is_float)
+    raw = riff(fmt_pcm(ch, 16000, bits, 3 if is_float else 1), chunk(b"data", _data_bytes(fr, bits, is_float)))
+    x, sr = decode_wav_f32(raw)
+    assert sr == 16000 and x.dtype == np.float32 and len(x) == 5000
+    want = oracle.wav_mono_f32(fr, bits, is_float)
+    np.testing.assert_array_equal(x.view(np.uint32), want.view(np.uint32))
+
+
+def test_f32_decode_of_int16_mono_is_pcm_over_32768():
+    """On the int16 path's inputs the fp32 form is exactly s / 32768 (so both entry points give
+    the same fingerprints); 8-bit likewise ((u - 128) << 8) / 32768."""
+    from tiresias_amd.engine import decode_wav_f32
+    pcm = np.arange(-32768, 32768, 7, dtype=np.int16)
+    x, _ = decode_wav_f32(riff(fmt_pcm(), chunk(b"data", pcm.tobytes())))
+    np.testing.assert_array_equal(x, pcm.astype(np.float32) / np.float32(32768))
+    u = np.arange(256, dtype=np.uint8)
+    x8, _ = decode_wav_f32(riff(fmt_pcm(bits=8), chunk(b"data", u.tobytes())))
+    p8, _ = decode_wav(riff(fmt_pcm(bits=8), chunk(b"data", u.tobytes())))
+    np.testing.assert_array_equal(x8, p8.astype(np.float32) / np.float32(32768))
+
+
+def test_f32_decode_extensible_and_errors(tmp_path):
+    from tiresias_amd.engine import decode_wav_f32, read_wav_f32
+    v = np.array([0.5, -0.25, 1.0, 0.125], np.float32)
+    x, _ = decode_wav_f32(riff(fmt_extensible(3, 1, 8000, 32), chunk(b"data", v.tobytes())))
+    np.testing.assert_array_equal(x, v)
+    with pytest.raises(TfpError) as e:  # 12-bit PCM: not a supported width
+        decode_wav_f32(riff(fmt_pcm(1, 8000, 12), chunk(b"data", b"\0" * 8)))
+    assert e.value.code == TFP_E_FORMAT
+    with pytest.raises(TfpError) as e:  # A-law
+        decode_wav_f32(riff(fmt_pcm(1, 8000, 8, tag=6), chunk(b"data", b"\0" * 8)))
+    assert e.value.code == TFP_E_FORMAT
+    path = tmp_path / "st.wav"
+    st = np.array([[100, -100], [32767, 32767], [-32768, 1]], np.int16)
+    path.write_bytes(riff(fmt_pcm(2), chunk(b"data", st.tobytes())))
+    x, sr = read_wav_f32(str(path))
+    assert sr == 8000
+    np.testing.assert_array_equal(x, np.array([0.0, 32767 / 32768, -32767 / 65536], np.float32))
+    with pytest.raises(TfpError) as e:
+        read_wav_f32(str(tmp_path / "missing.wav"))
+    assert e.value.code == TFP_E_NOENT
