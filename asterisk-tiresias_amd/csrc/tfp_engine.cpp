@@ -434,7 +434,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   std::vector<int64_t> qo(h_qoff, h_qoff + nq + 1);
   for (auto& v : qo) v -= h_qoff[0];
   if (!d_keys_out && sc.coefs == 1 && nq >= 1 && nq <= kSmallQ && e->ncols > 0 && e->nrows > 0) {
-    // small batch (batch-1 latency): three kernels, one copy back, no host round trip between them
+    // small batch (batch-1 latency): mark + vote + publish kernels, results into host-mapped memory
     bool fits = true;
     for (int32_t i = 0; i < nq; i++) fits &= qo[i + 1] - qo[i] <= 2048;  // counts bounded like the fp16 path
     if (fits) {
@@ -1007,6 +1007,19 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   std::vector<unsigned long long> keys;
   return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
                      reinterpret_cast<unsigned long long*>(d_keys), s);
+}
+
+int tfp_search_q_device(tfp_engine* e, const double* d_q, const int64_t* qoff, int32_t nq, const tfp_search_params* P,
+                        uint64_t* d_keys, void* stream) {
+  if (!e || !qoff || nq < 0 || !d_keys || !valid_params(P) || (!d_q && nq && qoff[nq] > qoff[0])) return TFP_E_ARG;
+  for (int32_t i = 0; i < nq; i++)
+    if (qoff[i + 1] < qoff[i]) return fail(e, TFP_E_ARG, "query offsets not monotone");
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t s = stream ? (hipStream_t)stream : e->stream;
+  std::vector<unsigned long long> keys;
+  return search_core(e, qoff, nq, d_q ? d_q + 2 * qoff[0] : d_q, P, keys, reinterpret_cast<unsigned long long*>(d_keys),
+                     s);
 }
 
 // ---- streams ------------------------------------------------------------------------------

@@ -77,6 +77,7 @@ _SIGS = {
     "tfp_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_device": (C.c_int, [P, P, P, C.POINTER(SearchParams), P, P]),
+    "tfp_search_q_device": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P, P]),
     "tfp_index_uuid_of_key": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int32]),
     "tfp_stream_create": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]),
     "tfp_stream_destroy": (None, [P]),

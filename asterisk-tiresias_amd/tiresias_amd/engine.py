@@ -251,6 +251,12 @@ class Engine:
         self._chk(lib().tfp_search_device(self._h, plan.handle, C.c_void_p(d_pcm), C.byref(p), C.c_void_p(d_keys),
                                           C.c_void_p(stream or None)))
 
+    def search_q_device(self, d_q: int, qoffsets, p: SearchParams, d_keys: int, stream: int = 0):
+        """tfp_search_q_device: search from device-resident frame values (2 doubles per frame)."""
+        qoffsets = np.ascontiguousarray(qoffsets, np.int64)
+        self._chk(lib().tfp_search_q_device(self._h, C.c_void_p(d_q), qoffsets.ctypes.data, len(qoffsets) - 1,
+                                            C.byref(p), C.c_void_p(d_keys), C.c_void_p(stream or None)))
+
     def synth_device(self, seed: int, clips, samples_per_clip: int, d_out: int, offsets=None, stream: int = 0):
         clips = list(clips)
         specs = synth_specs(seed, clips, offsets)

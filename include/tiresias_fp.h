@@ -185,6 +185,12 @@ int tfp_search_f32_batch(tfp_engine* eng, const float* x, const int64_t* offsets
  * The maximum key over shards is the global winner (RCCL allreduce MAX). */
 int tfp_search_device(tfp_engine* eng, const tfp_plan* plan, const int16_t* d_pcm,
                       const tfp_search_params* params, uint64_t* d_keys, void* stream);
+/* The same from frame values already on the device: d_q holds 2 doubles per frame (q1, q2 as
+ * tfp_fingerprint_device writes them to d_db), queries at frame offsets qoffsets[nqueries+1]
+ * (host). Lets N ranks each fingerprint 1/N of a query batch, all-gather the frame values and
+ * search their clip shard (the reference's per-frame SQL, fp_handler.c:287-374, on q1/q2). */
+int tfp_search_q_device(tfp_engine* eng, const double* d_q, const int64_t* qoffsets, int32_t nqueries,
+                        const tfp_search_params* params, uint64_t* d_keys, void* stream);
 /* Map a tie-break key from tfp_search_device back to the uuid (this engine's clips only). */
 int tfp_index_uuid_of_key(tfp_engine* eng, int32_t key, char* uuid, int32_t len);
 
