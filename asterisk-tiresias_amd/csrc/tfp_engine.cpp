@@ -120,6 +120,7 @@ struct tfp_engine {
   bool qoff_pending = false;
   DevBuf small_work, small_bk, key_rng;
   uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
+  HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
   uint32_t small_seq = 0;
@@ -505,9 +506,10 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   }
   HIPCHK(e, e->boxes.reserve(sizeof(FrameBox) * (nf + 1)));
   const int32_t Qp = ((nq + 127) / 128) * 128;
-  // one buffer: the vote path's key mask (32 words), max count (1), pad (1), then best[Qp] (u64);
-  // zeroed by prep_boxes
-  constexpr int kMaskWords = kKeyRange / 32, kMiscWords = kMaskWords + 2;
+  // one buffer: the vote path's key mask (32 words), max count (1), pad (1), VoteMeta (4), then
+  // best[Qp] (u64); zeroed by prep_boxes. VoteMeta directly before best[]: one copy brings both back.
+  constexpr int kMaskWords = kKeyRange / 32, kMetaWord = kMaskWords + 2, kMiscWords = kMetaWord + 4;
+  static_assert(sizeof(VoteMeta) == 16 && kMiscWords % 2 == 0, "meta + 8-byte aligned best[]");
   const int32_t nzero = kMiscWords + 2 * Qp;
   HIPCHK(e, e->best.reserve(sizeof(uint32_t) * nzero));
   uint32_t* d_mask = e->best.as<uint32_t>();
@@ -528,10 +530,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     const int32_t Cp = ((C + 31) / 32) * 32;
     HIPCHK(e, e->keycols.reserve(sizeof(int32_t) * 2 * kKeyRange));
     HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * kKeyRange));
-    HIPCHK(e, e->kbounds.reserve(sizeof(VoteMeta)));
     HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
     HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
-    VoteMeta* d_meta = e->kbounds.as<VoteMeta>();
+    VoteMeta* d_meta = reinterpret_cast<VoteMeta*>(d_mask + kMetaWord);
     if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
     HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, s));
     HIPCHK(e, launch_vote_compact(d_mask, d_max, e->rng_all.as<int64_t>(), e->keycols.as<int32_t>(),
@@ -541,14 +542,18 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),
                                e->vote_part.as<unsigned long long>(), d_best, s));
-    VoteMeta hm;
-    // the results go out before the ok flag is known (one host wait); a redo overwrites them
+    // the results go out before the ok flag is known (one host wait); a redo overwrites them.
+    // Host results: (VoteMeta, best[nq]) in one copy into pinned memory.
+    const size_t back = sizeof(VoteMeta) + (d_keys_out ? 0 : sizeof(unsigned long long) * nq);
+    HIPCHK(e, e->vres_pin.reserve(back));
     if (d_keys_out)
       HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
-    else if (nq)
-      HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
-    HIPCHK(e, hipMemcpyAsync(&hm, d_meta, sizeof hm, hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipMemcpyAsync(e->vres_pin.p, d_meta, back, hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
+    VoteMeta hm;
+    memcpy(&hm, e->vres_pin.p, sizeof hm);
+    if (!d_keys_out && nq)
+      memcpy(keys.data(), e->vres_pin.as<char>() + sizeof(VoteMeta), sizeof(unsigned long long) * nq);
     static const bool dbg = getenv("TFP_DEBUG_VOTE") != nullptr;
     if (dbg) fprintf(stderr, "[tfp] vote: nq %d Qp %d C %d ku %d kp %d ok %d\n", nq, Qp, C, hm.ku, hm.kp, hm.ok);
     if (hm.ok) return TFP_OK;
@@ -1030,7 +1035,9 @@ struct tfp_stream {
   int64_t W = 0;                 // window samples
   int64_t wpos = 0;              // ring position of the oldest sample of every window
   std::vector<int64_t> filled;   // samples of history per channel (saturates at W)
-  DevBuf ring, tick, sbeg, send, foff, toff, tclip;
+  DevBuf ring, stage_d;          // stage_d: this tick's samples + window layout (one upload)
+  HostBuf stage_h;               // pinned source of that upload
+  bool stage_pending = false;    // stage_h may still be read by the last upload
 };
 
 // ring[c][2W]: every sample is written at p and p + W, so the last W samples of a channel are
@@ -1070,7 +1077,15 @@ int tfp_stream_create(tfp_engine* e, int32_t nch, int32_t sr, int64_t W, tfp_str
   return TFP_OK;
 }
 
-void tfp_stream_destroy(tfp_stream* st) { delete st; }
+void tfp_stream_destroy(tfp_stream* st) {
+  if (!st) return;
+  {
+    std::lock_guard<std::recursive_mutex> lk(st->eng->mu);
+    (void)hipSetDevice(st->eng->device);
+    (void)hipStreamSynchronize(st->eng->stream);  // the last tick's upload may still read stage_h
+  }
+  delete st;
+}
 
 int tfp_stream_reset(tfp_stream* st, int32_t ch) {
   if (!st || ch >= st->nch) return TFP_E_ARG;
@@ -1085,34 +1100,36 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   tfp_engine* e = st->eng;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
-  int rc = upload(e, st->tick, pcm, sizeof(int16_t) * (size_t)st->nch * T);
-  if (rc) return rc;
-  hipLaunchKernelGGL(stream_scatter_kernel, dim3(1024), dim3(256), 0, e->stream, st->tick.as<int16_t>(), T, st->W,
-                     st->wpos, st->nch, st->ring.as<int16_t>());
-  HIPCHK(e, hipGetLastError());
-  st->wpos = (st->wpos + T) % st->W;
-  for (auto& f : st->filled) f = std::min<int64_t>(st->W, f + T);
-  if (!P) return TFP_OK;
-  for (int32_t c = 0; c < st->nch; c++) {
-    memset(&out[c], 0, sizeof out[c]);
-    out[c].clip_id = -1;
-  }
-  if (!valid_params(P)) return TFP_OK;  // fp_handler.c:247-250: NULL
-  // full windows only
+  int rc;
+  // Windows to match after this tick: the channels whose history is full once it is in.
+  const int64_t wpos = (st->wpos + T) % st->W;
   std::vector<int32_t> act;
-  for (int32_t c = 0; c < st->nch; c++)
-    if (st->filled[c] >= st->W) act.push_back(c);
+  const bool match = P && valid_params(P);  // fp_handler.c:247-250: bad params -> NULL results
+  if (match)
+    for (int32_t c = 0; c < st->nch; c++)
+      if (std::min<int64_t>(st->W, st->filled[c] + T) >= st->W) act.push_back(c);
   const int32_t na = (int32_t)act.size();
-  if (!na) return TFP_OK;
-  const DspTables* Tb;
-  bool fx = false;
-  if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
   const int64_t F = tfp_frame_count(st->W);
   const int32_t tiles = (int32_t)((F + kFramesPerBlock - 1) / kFramesPerBlock);
-  std::vector<int64_t> sb(na), se(na), fo(na + 1);
-  std::vector<int32_t> to(na + 1), tc((size_t)na * tiles);
+  // One pinned upload per tick: the tick's samples, then the windows' layout (sbeg, send, foff,
+  // toff, tclip). The previous tick's upload must be done reading the pinned buffer.
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_pcm = al(sizeof(int16_t) * (size_t)st->nch * T), b_sb = al(sizeof(int64_t) * na),
+               b_fo = al(sizeof(int64_t) * (na + 1)), b_to = al(sizeof(int32_t) * (na + 1)),
+               b_tc = al(sizeof(int32_t) * (size_t)na * tiles);
+  const size_t total = b_pcm + 2 * b_sb + b_fo + b_to + b_tc;
+  if (st->stage_pending) HIPCHK(e, hipStreamSynchronize(e->stream));
+  HIPCHK(e, st->stage_h.reserve(total));
+  HIPCHK(e, st->stage_d.reserve(total));
+  char* h = st->stage_h.as<char>();
+  memcpy(h, pcm, sizeof(int16_t) * (size_t)st->nch * T);
+  int64_t* sb = reinterpret_cast<int64_t*>(h + b_pcm);
+  int64_t* se = reinterpret_cast<int64_t*>(h + b_pcm + b_sb);
+  int64_t* fo = reinterpret_cast<int64_t*>(h + b_pcm + 2 * b_sb);
+  int32_t* to = reinterpret_cast<int32_t*>(h + b_pcm + 2 * b_sb + b_fo);
+  int32_t* tc = reinterpret_cast<int32_t*>(h + b_pcm + 2 * b_sb + b_fo + b_to);
   for (int32_t i = 0; i < na; i++) {
-    sb[i] = (int64_t)act[i] * 2 * st->W + st->wpos;
+    sb[i] = (int64_t)act[i] * 2 * st->W + wpos;
     se[i] = sb[i] + st->W;
     fo[i] = (int64_t)i * F;
     to[i] = i * tiles;
@@ -1120,20 +1137,38 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   }
   fo[na] = (int64_t)na * F;
   to[na] = na * tiles;
-  if ((rc = upload(e, st->sbeg, sb.data(), sizeof(int64_t) * na)) || (rc = upload(e, st->send, se.data(), sizeof(int64_t) * na)) ||
-      (rc = upload(e, st->foff, fo.data(), sizeof(int64_t) * (na + 1))) ||
-      (rc = upload(e, st->toff, to.data(), sizeof(int32_t) * (na + 1))) ||
-      (rc = upload(e, st->tclip, tc.data(), sizeof(int32_t) * tc.size())))
-    return rc;
+  HIPCHK(e, hipMemcpyAsync(st->stage_d.p, h, total, hipMemcpyHostToDevice, e->stream));
+  st->stage_pending = true;
+  const char* d = st->stage_d.as<char>();
+  hipLaunchKernelGGL(stream_scatter_kernel, dim3(1024), dim3(256), 0, e->stream, reinterpret_cast<const int16_t*>(d), T,
+                     st->W, st->wpos, st->nch, st->ring.as<int16_t>());
+  HIPCHK(e, hipGetLastError());
+  st->wpos = wpos;
+  for (auto& f : st->filled) f = std::min<int64_t>(st->W, f + T);
+  if (!P) return TFP_OK;
+  for (int32_t c = 0; c < st->nch; c++) {
+    memset(&out[c], 0, sizeof out[c]);
+    out[c].clip_id = -1;
+  }
+  if (!match || !na) return TFP_OK;  // full windows only
+  const DspTables* Tb;
+  bool fx = false;
+  if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
-  HIPCHK(e, launch_fingerprint(Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), st->sbeg.as<int64_t>(), st->send.as<int64_t>(),
-                               st->foff.as<int64_t>(), st->toff.as<int32_t>(), st->tclip.as<int32_t>(), to[na], fo[na],
+  const int64_t* d_sb = reinterpret_cast<const int64_t*>(d + b_pcm);
+  HIPCHK(e, launch_fingerprint(Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), d_sb,
+                               reinterpret_cast<const int64_t*>(d + b_pcm + b_sb),
+                               reinterpret_cast<const int64_t*>(d + b_pcm + 2 * b_sb),
+                               reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo),
+                               reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo + b_to), to[na], fo[na],
                                e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+  const std::vector<int64_t> fov(fo, fo + na + 1);  // (the pinned buffer is rewritten next tick)
   std::vector<unsigned long long> keys;
-  if ((rc = search_core(e, fo.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
+  if ((rc = search_core(e, fov.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
+  st->stage_pending = false;  // search_core waited for e->stream
   std::vector<tfp_result> res(na);
-  fill_results(e, keys, fo.data(), na, res.data());
+  fill_results(e, keys, fov.data(), na, res.data());
   for (int32_t i = 0; i < na; i++) out[act[i]] = res[i];
   return TFP_OK;
 }
