@@ -1996,16 +1996,34 @@ hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteM
 // Pattern-class path: one wave per query, lanes over the patterns present; score = the query's
 // counts (A, exact in fp16) summed over the pattern's keys; key = score << 32 | tiekey of the
 // pattern's greatest column, max over patterns with a non-zero score.
+// The vote's last step, one wave per query: the pattern-class vote (meta->cls), or for the GEMM
+// path the max of the query's per-chunk keys (one launch for both: the path is known only on the
+// device).
 __global__ __launch_bounds__(256) void class_vote_kernel(const _Float16* __restrict__ A, int32_t Qp,
                                                          const VoteMeta* __restrict__ meta,
                                                          const _Float16* __restrict__ Bt,
                                                          const int32_t* __restrict__ tiekey,
+                                                         const unsigned long long* __restrict__ part, int32_t nchunks,
                                                          unsigned long long* __restrict__ best) {
   const int32_t Ku = meta->ku, Kp = meta->kp;
-  if (!meta->ok || !meta->cls) return;
+  if (!meta->ok) return;
   const int lane = threadIdx.x & 63;
   const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (q >= Qp) return;
+  if (!meta->cls) {  // GEMM path: max over the chunks' partial keys (score << 32 | tiekey)
+    unsigned long long b = 0;
+    for (int c = lane; c < nchunks; c += 64) {
+      const unsigned long long v = part[(int64_t)c * Qp + q];
+      b = v > b ? v : b;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      const unsigned long long o = __shfl_xor(b, off, 64);
+      b = o > b ? o : b;
+    }
+    if (lane == 0) best[q] = b;
+    return;
+  }
   const int32_t* cls = reinterpret_cast<const int32_t*>(Bt);
   int32_t cnt[kClassKuMax];
 #pragma unroll
@@ -2054,7 +2072,7 @@ __device__ __forceinline__ void vote_max_into(uintx16& m, const floatx16& acc) {
 }
 
 // The wave's 32 rows of its chunk's partial results (part = this chunk's row of [nchunks][Qp]):
-// plain stores, merged by vote_final_kernel. Device-scope atomics on shared addresses go past the
+// plain stores, merged by class_vote_kernel (GEMM branch). Device-scope atomics on shared addresses go past the
 // per-XCD L2s and serialise: 400 k of them cost ~50 us.
 __device__ __forceinline__ void vote_reduce_rows(const uintx16& m, int q0, int h, int r, int base,
                                                  const int32_t* __restrict__ tiekey,
@@ -2301,28 +2319,6 @@ __global__ __launch_bounds__(256) void vote_gemm_lds_kernel(const _Float16* __re
 
 // best[q] = max over the chunks' partial keys: 64 queries per block, 16 threads per query over
 // the chunks (one thread per query left the loads latency-bound: 24 us for 98 chunks).
-__global__ __launch_bounds__(1024) void vote_final_kernel(const unsigned long long* __restrict__ part, int32_t nchunks,
-                                                          int32_t Qp, const VoteMeta* __restrict__ meta,
-                                                          unsigned long long* __restrict__ best) {
-  if (!meta->ok || meta->cls) return;
-  __shared__ unsigned long long red[16][64];
-  const int ql = threadIdx.x & 63, cl = threadIdx.x >> 6;
-  const int q = blockIdx.x * 64 + ql;
-  unsigned long long b = 0;
-  if (q < Qp)
-    for (int c = cl; c < nchunks; c += 16) {
-      const unsigned long long v = part[(int64_t)c * Qp + q];
-      b = v > b ? v : b;
-    }
-  red[cl][ql] = b;
-  __syncthreads();
-  if (cl == 0 && q < Qp) {
-#pragma unroll
-    for (int i = 1; i < 16; i++) b = red[i][ql] > b ? red[i][ql] : b;
-    best[q] = b;
-  }
-}
-
 int32_t vote_chunks(int32_t Cp) { return (Cp + kVoteChunk - 1) / kVoteChunk; }
 
 hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
@@ -2334,9 +2330,8 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
   dim3 grid(nchunks, (Qp / 64 + 3) / 4);
   hipLaunchKernelGGL(vote_gemm_regs_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
   hipLaunchKernelGGL(vote_gemm_lds_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
-  hipLaunchKernelGGL(vote_final_kernel, dim3((unsigned)((Qp + 63) / 64)), dim3(1024), 0, s, d_part, nchunks, Qp, d_meta,
-                     d_best);
-  hipLaunchKernelGGL(class_vote_kernel, dim3((unsigned)(Qp / 4)), dim3(256), 0, s, d_A, Qp, d_meta, d_Bt, d_tiekey, d_best);
+  hipLaunchKernelGGL(class_vote_kernel, dim3((unsigned)(Qp / 4)), dim3(256), 0, s, d_A, Qp, d_meta, d_Bt, d_tiekey, d_part,
+                     nchunks, d_best);
   return hipGetLastError();
 }
 
