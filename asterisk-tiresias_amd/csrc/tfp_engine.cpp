@@ -120,6 +120,8 @@ struct tfp_engine {
   bool qoff_pending = false;
   DevBuf small_work, small_bk, key_rng;
   uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
+  int32_t small_cp4 = 0;     // row stride of the stamps in small_bk
+  int32_t small_rows = 0;    // rows stamped since the last clear (the max used-key count)
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
@@ -446,13 +448,16 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       const int32_t C = e->ncols, Cp4 = ((C + 3) / 4) * 4;
       HIPCHK(e, e->small_work.reserve(sizeof(SmallWork)));
       const size_t bk_bytes = (size_t)kKeyRange * Cp4;
-      if (bk_bytes > e->small_bk.bytes) {
+      if (bk_bytes > e->small_bk.bytes || Cp4 != e->small_cp4) {
         HIPCHK(e, e->small_bk.reserve(bk_bytes));
-        e->small_epoch = 255;  // force a clear below
+        e->small_cp4 = Cp4;
+        e->small_rows = kKeyRange;  // new buffer or row stride: clear it all below
+        e->small_epoch = 255;
       }
-      if (e->small_epoch == 255) {  // stamps wrap: clear once every 255 calls
-        HIPCHK(e, hipMemsetAsync(e->small_bk.p, 0, e->small_bk.bytes, s));
+      if (e->small_epoch == 255) {  // stamps wrap: clear, once every 255 calls, the rows stamped since
+        HIPCHK(e, hipMemsetAsync(e->small_bk.p, 0, (size_t)e->small_rows * Cp4, s));
         e->small_epoch = 0;
+        e->small_rows = 0;
       }
       const uint8_t epoch = ++e->small_epoch;
       SmallWork* w = e->small_work.as<SmallWork>();
@@ -479,9 +484,12 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       if (!seen) HIPCHK(e, hipStreamSynchronize(s));
       // the vote ran after the fingerprint kernel, which read the staged upload: it is free again
       e->stage_pending = false;
-      if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq)
+      if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq) {
+        e->small_rows = kKeyRange;  // unknown stamps: clear everything at the next wrap
         return fail(e, TFP_E_HIP, "small search: result of call %u not published", seq);
+      }
       if (!h->bad) {
+        e->small_rows = std::max<int32_t>(e->small_rows, (int32_t)h->ku);
         for (int32_t i = 0; i < nq; i++) keys[i] = h->best[i];
         return TFP_OK;
       }

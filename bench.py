@@ -330,6 +330,8 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         uuid_grank = {uuid_of(g): int(grank[g]) for g in range(args.db_clips)}
         kpin = torch.zeros(1, dtype=torch.int64).pin_memory()
         kdev = torch.zeros(1, dtype=torch.int64, device=dev)
+    for i in range(min(3, len(host_q))):  # untimed: first-call allocations of the small path
+        eng.search_pcm_batch(host_q[i], [0, qn], p)
     lat = []
     for i in range(len(host_q)):
         barrier()

@@ -420,3 +420,28 @@ def test_search_f32_equals_frame_search(engine, oracle, tfp_lib):
     r16, _ = engine.search_pcm_batch(q[0], [0, 40000], tfp_lib.params(1, 0.001))
     r32, _ = engine.search_f32_batch(xs[4], [0, 40000], tfp_lib.params(1, 0.001))
     assert r32 == r16
+
+
+def test_small_path_epoch_wrap(engine, oracle, tfp_lib):
+    """The small path stamps clips with a per-call epoch byte and clears only the rows stamped
+    since the last clear when the epoch wraps (every 255 calls): 600 calls (two wraps) over
+    queries with different used-key counts give the first calls' results, and so does a call
+    after the index (hence the stamp row stride) changes."""
+    _build_db(engine, oracle, tfp_lib, 80, 12)
+    qpcm = _queries(tfp_lib, 12, 80, 12, 5)
+    n = qpcm.shape[1]
+    ps = [tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.45), tfp_lib.params(1, 2.0)]
+    want = {}
+    for i in range(12):
+        for j, p in enumerate(ps):
+            r, _ = engine.search_pcm_batch(qpcm[i], [0, n], p)
+            want[i, j] = r[0]
+    for call in range(600):
+        i, j = call % 12, (call // 12) % 3
+        r, _ = engine.search_pcm_batch(qpcm[i], [0, n], ps[j])
+        assert r[0] == want[i, j], (call, i, j)
+    engine.index_add("ffffffff-0000-4000-8000-000000000000", np.array([1, 2], np.int32), np.array([3, 4], np.int32))
+    for i in range(12):
+        r, _ = engine.search_pcm_batch(qpcm[i], [0, n], ps[1])
+        big, _ = engine.search_pcm_batch(np.tile(qpcm[i], 9), np.arange(10) * n, ps[1])  # general path
+        assert r[0] == big[0]
