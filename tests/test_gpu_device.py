@@ -63,3 +63,39 @@ def test_device_fingerprint_and_search_equal_host(engine, tfp_lib, torch_cuda):
             assert int(k[i] >> np.uint64(32)) == res[i]["match_count"]
             assert engine.uuid_of_key(int(k[i] & np.uint64(0xffffffff))) == res[i]["audio_uuid"]
     engine.index_clear()
+
+
+def test_search_q_device_equals_search_device(engine, tfp_lib, torch_cuda):
+    """tfp_search_q_device on frame values fingerprinted in two halves (as two ranks of the
+    query-sharded configs[3] step would, concatenated) == tfp_search_device on the whole batch."""
+    torch = torch_cuda
+    nclips, n = 48, 8000 * 10
+    pcm = torch.empty((nclips, n), dtype=torch.int16, device="cuda")
+    engine.synth_device(0x7153A1, range(nclips), n, pcm.data_ptr())
+    plan = engine.plan(np.arange(nclips + 1, dtype=np.int64) * n)
+    micro = torch.empty((plan.nframes, 2), dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    engine.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, stream)
+    nf = plan.nframes // nclips
+    engine.index_clear()
+    engine.index_add_device(["%08x-0000-4000-8000-%012x" % (i * 31, i) for i in range(nclips)],
+                            np.arange(nclips + 1) * nf, micro.data_ptr(), stream)
+    nq, qn = 40, 8000 * 5
+    nfq = (qn + 255) // 256
+    qpcm = torch.empty((nq, qn), dtype=torch.int16, device="cuda")
+    engine.synth_device(0x7153A1, [i % nclips for i in range(nq)], qn, qpcm.data_ptr(),
+                        offsets=[256 * (i % 40) for i in range(nq)])
+    half = engine.plan(np.arange(nq // 2 + 1, dtype=np.int64) * qn)
+    q = torch.empty((nq * nfq, 2), dtype=torch.float64, device="cuda")
+    qm = torch.empty((nq * nfq, 2), dtype=torch.int32, device="cuda")
+    for h in range(2):
+        rows = slice(h * (nq // 2) * nfq, (h + 1) * (nq // 2) * nfq)
+        engine.fingerprint_device(half, qpcm[h * (nq // 2):].data_ptr(), qm[rows].data_ptr(), q[rows].data_ptr(), stream)
+    for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.5)):
+        k1 = torch.zeros(nq, dtype=torch.int64, device="cuda")
+        k2 = torch.zeros(nq, dtype=torch.int64, device="cuda")
+        engine.search_q_device(q.data_ptr(), np.arange(nq + 1) * nfq, p, k1.data_ptr(), stream)
+        engine.search_device(engine.plan(np.arange(nq + 1, dtype=np.int64) * qn), qpcm.data_ptr(), p, k2.data_ptr(), stream)
+        torch.cuda.synchronize()
+        assert torch.equal(k1, k2)
+    assert int((k2 != 0).sum()) > 0
