@@ -344,6 +344,24 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             sharding.combine(kdev, dist)
             kdev.item()
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
+    lat_py = list(lat)
+    harness = "python (ctypes) loop, max over ranks + 8-byte all_reduce" if dist else "python (ctypes) loop"
+    if not dist:
+        # the same calls from C (asterisk-tiresias_amd/bench/tfp_latency.c), as the Asterisk shim's
+        # channel threads make them: no Python/ctypes marshalling in the timed region
+        import ctypes
+        clat = ctypes.CDLL(os.path.join(os.path.dirname(T.LIB_PATH), "libtfp_latency.so"))
+        n_it = max(200, 10 * len(host_q))
+        out_ms = np.zeros(n_it, np.float64)
+        fnd = np.zeros(n_it, np.int32)
+        hq = np.ascontiguousarray(host_q, np.int16)
+        rc = clat.tfp_latency_search_pcm(eng.handle, ctypes.c_void_p(hq.ctypes.data), ctypes.c_int64(qn),
+                                         ctypes.c_int32(len(hq)), ctypes.c_int32(8000), ctypes.byref(p),
+                                         ctypes.c_int32(n_it), ctypes.c_void_p(out_ms.ctypes.data),
+                                         ctypes.c_void_p(fnd.ctypes.data))
+        if rc == 0:
+            lat = out_ms.tolist()
+            harness = "C loop over tfp_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries" % (n_it, len(hq))
     res = {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": (("all_gather of the query frame values (each rank fingerprints 1/%d of the queries), "
@@ -353,7 +371,8 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "db_build_s": t_build, "batch_queries": nq, "batch_warmup_calls": n_warm, "batch_ms": batch_ms,
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
-            "latency_samples": len(lat)}
+            "latency_samples": len(lat), "latency_harness": harness,
+            "latency_p50_ms_python": float(np.percentile(lat_py, 50))}
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = match_cpu_baseline(args, T)
     return res
