@@ -107,7 +107,7 @@ struct tfp_engine {
 
   // scratch
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
-  DevBuf pcm, q, qoff, boxes, vote_part, mask, maxc, keycols, kbounds, A, Bt, best, stamp, score, micro, db;
+  DevBuf pcm, q, qoff, boxes, vote_part, mask, maxc, A, Bt, best, stamp, score, micro, db;
   DevBuf soff, foff, toff, tclip, specs;
   // small host calls: packed upload + the small-batch search workspace
   HostBuf hstage;
@@ -536,16 +536,14 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     // vote-matrix path, no host round trip: key mask -> used-key compaction -> A (per-query
     // counts) and Bt -> GEMM
     const int32_t Cp = ((C + 31) / 32) * 32;
-    HIPCHK(e, e->keycols.reserve(sizeof(int32_t) * 2 * kKeyRange));
     HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * kKeyRange));
     HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
     HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
     VoteMeta* d_meta = reinterpret_cast<VoteMeta*>(d_mask + kMetaWord);
     if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
-    HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, s));
-    HIPCHK(e, launch_vote_compact(d_mask, d_max, e->rng_all.as<int64_t>(), e->keycols.as<int32_t>(),
-                                  e->key_rng.as<int64_t>(), d_meta, vote_class_ku_max(), s));
-    HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, e->keycols.as<int32_t>(), d_meta, e->A.as<_Float16>(), s));
+    HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, d_meta, s));
+    HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
+                             e->key_rng.as<int64_t>(), d_meta, vote_class_ku_max(), e->A.as<_Float16>(), s));
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),

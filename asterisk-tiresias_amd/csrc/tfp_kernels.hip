@@ -1775,7 +1775,9 @@ __device__ __forceinline__ bool frame_key(const double* __restrict__ q, int64_t 
 // query): bits set in a 32-word LDS mask per block, ORed into the global mask; a key outside the
 // vote range is reported through maxc as INT32_MAX (the batch then goes to the scan path).
 __global__ __launch_bounds__(256) void key_mask_kernel(const double* __restrict__ qv, SearchConsts sc, int64_t nf,
-                                                       uint32_t* __restrict__ mask, int32_t* __restrict__ maxc) {
+                                                       uint32_t* __restrict__ mask, int32_t* __restrict__ maxc,
+                                                       VoteMeta* __restrict__ meta) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) meta->ok = 1;  // build_A only ever clears it
   // one byte per key, set by plain stores (keys concentrate on a few values, so LDS atomics on a
   // few mask words would serialise), then folded to mask words by ballots
   __shared__ uint8_t used[kKeyRange];
@@ -1805,13 +1807,13 @@ __global__ __launch_bounds__(256) void key_mask_kernel(const double* __restrict_
 }
 
 hipError_t launch_key_mask(const double* d_q, SearchConsts sc, int64_t nf, uint32_t* d_mask, int32_t* d_maxc,
-                           hipStream_t s) {
-  if (nf <= 0) return hipSuccess;
+                           VoteMeta* d_meta, hipStream_t s) {
   // few blocks: each ORs its words into the same few global mask words, and same-address atomics
-  // serialise in L2 (4096 blocks cost ~50 us)
+  // serialise in L2 (4096 blocks cost ~50 us); at least one (it sets meta->ok)
   int64_t g = (nf + 255) / 256;
   if (g > 256) g = 256;
-  hipLaunchKernelGGL(key_mask_kernel, dim3((unsigned)g), dim3(256), 0, s, d_q, sc, nf, d_mask, d_maxc);
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(key_mask_kernel, dim3((unsigned)g), dim3(256), 0, s, d_q, sc, nf, d_mask, d_maxc, d_meta);
   return hipGetLastError();
 }
 
@@ -1830,72 +1832,73 @@ hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int
   return hipGetLastError();
 }
 
-// Used-key compaction on the GPU (no host round trip): the batch's key mask -> keycols (ascending
-// key order, the order the host used to build them), each key's "%f" box and its row range in the
-// m1-sorted index; meta = (Ku, Kp = padded Ku + 1, ok = counts exact in fp16).
-__global__ __launch_bounds__(1024) void vote_compact_kernel(const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
-                                                            const int64_t* __restrict__ rng_all,
-                                                            int32_t* __restrict__ keycols, int64_t* __restrict__ rng,
-                                                            VoteMeta* __restrict__ meta, int32_t class_ku_max) {
-  __shared__ int32_t scan[kKeyRange];
-  const int t = threadIdx.x;
-  const int used = (mask[t >> 5] >> (t & 31)) & 1;
-  scan[t] = used;
-  __syncthreads();
-  for (int off = 1; off < kKeyRange; off <<= 1) {
-    const int v = t >= off ? scan[t - off] : 0;
-    __syncthreads();
-    scan[t] += v;
-    __syncthreads();
-  }
-  keycols[kKeyRange + t] = used ? scan[t] - 1 : -1;  // key -> used-key column (build_A)
-  if (used) {
-    const int kc = scan[t] - 1;
-    keycols[kc] = t;
-    rng[2 * kc] = rng_all[2 * t];
-    rng[2 * kc + 1] = rng_all[2 * t + 1];
-  }
-  if (t == kKeyRange - 1) {
-    const int ku = scan[t];
-    meta->ku = ku;
-    meta->kp = ((ku + 1 + 15) / 16) * 16;
-    meta->ok = *maxc <= 2048 ? 1 : 0;  // every key in range (build_A clears it for a count > 2048)
-    meta->cls = ku <= class_ku_max && ku <= kClassKuMax ? 1 : 0;
-  }
-}
-
-hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int32_t* d_keycols,
-                               int64_t* d_rng, VoteMeta* d_meta, int32_t class_ku_max, hipStream_t s) {
-  hipLaunchKernelGGL(vote_compact_kernel, dim3(1), dim3(kKeyRange), 0, s, d_mask, d_maxc, d_rng_all, d_keycols, d_rng,
-                     d_meta, class_ku_max);
-  return hipGetLastError();
-}
-
+// Used-key compaction on the GPU (no host round trip), in every build_A block: the batch's key mask
+// -> column kc of each used key (ascending key order) by a prefix popcount of the 32 mask words;
+// block 0 writes meta = (Ku, Kp = padded Ku + 1, cls) and each used key's row range in the
+// m1-sorted index. (A separate one-block compaction launch cost ~5 us per batch.)
+//
 // One wave per query row of A: the query's frames counted per used key in LDS, then the row
 // written as fp16 (A[q][Ku] = 1 picks up Bt's column-position entry for vote_gemm's packed argmax;
 // rows q >= nq up to Qp are zero). A count above 2048 (not exact in fp16) clears meta->ok, before
 // vote_gemm reads it, and the host redoes the batch on the scan path.
 __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__ qv, SearchConsts sc,
                                                       const int64_t* __restrict__ qoff, int32_t nq, int32_t Qp,
-                                                      const int32_t* __restrict__ keycols, VoteMeta* __restrict__ meta,
+                                                      const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
+                                                      const int64_t* __restrict__ rng_all, int64_t* __restrict__ rng,
+                                                      VoteMeta* __restrict__ meta, int32_t class_ku_max,
                                                       _Float16* __restrict__ A) {
   __shared__ int32_t hist[4][kVoteKpMax];
+  __shared__ uint32_t mw[kKeyRange / 32];
+  __shared__ int32_t pre[kKeyRange / 32 + 1];  // used keys below mask word w; pre[32] = Ku
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  // used-key compaction (ascending key = column), derived by every block from the 32 mask words
+  if (threadIdx.x < 64) {
+    const uint32_t m = threadIdx.x < kKeyRange / 32 ? mask[threadIdx.x] : 0u;
+    const int c = __popc(m);
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    if (threadIdx.x < kKeyRange / 32) {
+      mw[threadIdx.x] = m;
+      pre[threadIdx.x] = incl - c;
+    }
+    if (threadIdx.x == kKeyRange / 32 - 1) pre[kKeyRange / 32] = incl;
+  }
+  __syncthreads();
+  const int32_t Ku = pre[kKeyRange / 32], Kp = ((Ku + 1 + 15) / 16) * 16;
+  if (blockIdx.x == 0) {  // the vote's metadata and the used keys' box row ranges (build_B)
+    if (threadIdx.x == 0) {
+      meta->ku = Ku;
+      meta->kp = Kp;
+      meta->cls = Ku <= class_ku_max && Ku <= kClassKuMax ? 1 : 0;
+      if (*maxc > 2048) meta->ok = 0;  // a key outside the vote range (key_mask)
+    }
+    for (int t = threadIdx.x; t < kKeyRange; t += blockDim.x) {
+      const uint32_t m = mw[t >> 5];
+      if ((m >> (t & 31)) & 1u) {
+        const int kc = pre[t >> 5] + __popc(m & ((1u << (t & 31)) - 1u));
+        rng[2 * kc] = rng_all[2 * t];
+        rng[2 * kc + 1] = rng_all[2 * t + 1];
+      }
+    }
+  }
   const int q = blockIdx.x * 4 + wave;
   if (q >= Qp) return;
-  const int32_t Ku = meta->ku, Kp = meta->kp;
   int32_t* h = hist[wave];
   for (int c = lane; c < Kp; c += 64) h[c] = 0;
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   if (q < nq) {
-    const int32_t* kmap = keycols + kKeyRange;
     for (int64_t i = qoff[q] + lane; i < qoff[q + 1]; i += 64) {
       int32_t k;
       if (!frame_key(qv, i, sc, k)) continue;
       const int64_t idx = (int64_t)k + kKeyOffset;
       if (idx < 0 || idx >= kKeyRange) continue;  // already flagged by key_mask (meta->ok = 0)
-      atomicAdd(&h[kmap[idx]], 1);
+      const uint32_t m = mw[idx >> 5];
+      atomicAdd(&h[pre[idx >> 5] + __popc(m & ((1u << (idx & 31)) - 1u))], 1);
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1912,9 +1915,10 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
 }
 
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
-                          const int32_t* d_keycols, VoteMeta* d_meta, _Float16* d_A, hipStream_t s) {
-  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, d_q, sc, d_qoff, nq, Qp, d_keycols,
-                     d_meta, d_A);
+                          const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int64_t* d_rng,
+                          VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A, hipStream_t s) {
+  hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, d_q, sc, d_qoff, nq, Qp, d_mask,
+                     d_maxc, d_rng_all, d_rng, d_meta, class_ku_max, d_A);
   return hipGetLastError();
 }
 

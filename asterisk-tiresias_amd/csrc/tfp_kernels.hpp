@@ -65,12 +65,15 @@ hipError_t radix_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* kin, 
 hipError_t launch_prep_boxes(const double* d_q, int64_t nframes, SearchConsts sc, FrameBox* boxes, uint32_t* zero_words,
                              int32_t nzero, hipStream_t s);
 // Used-key mask of all nf frames (d_mask zeroed); a key outside the vote range sets *d_maxc = INT32_MAX.
+struct VoteMeta;
+// Sets d_meta->ok (the vote's exactness flag, cleared later by build_A) as well.
 hipError_t launch_key_mask(const double* d_q, SearchConsts sc, int64_t nf, uint32_t* d_mask /*[kKeyRange/32]*/,
-                           int32_t* d_maxc /*zeroed*/, hipStream_t s);
+                           int32_t* d_maxc /*zeroed*/, VoteMeta* d_meta, hipStream_t s);
 // Row ranges of all kKeyRange keys' boxes at one tolerance (the engine caches them per index version).
 hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int64_t* d_rng_all /*[kKeyRange][2]*/,
                                  hipStream_t s);
-// Vote path bookkeeping computed on the GPU by vote_compact (read by the later kernels).
+// Vote path bookkeeping computed on the GPU by key_mask (ok) and build_A's block 0 (read by the
+// later kernels).
 struct VoteMeta {
   int32_t ku;  // used keys
   int32_t kp;  // GEMM K: Ku + 1 (the packed-argmax column) rounded up to 16
@@ -78,12 +81,12 @@ struct VoteMeta {
   int32_t cls; // pattern-class path (Ku <= class_ku_max) instead of the Bt GEMM
 };
 constexpr int32_t kVoteKpMax = ((kKeyRange + 1 + 15) / 16) * 16;
-hipError_t launch_vote_compact(const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
-                               int32_t* d_keycols /*[2][kKeyRange]: used keys, key -> column*/,
-                               int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max,
-                               hipStream_t s);
+// A[q][kc] per-query counts of the used keys (ascending key = column kc), derived by every block
+// from the key mask; block 0 writes VoteMeta (ku, kp, cls; ok cleared for an out-of-range key)
+// and the used keys' box row ranges d_rng[kc] (from the cached d_rng_all) for build_B.
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
-                          const int32_t* d_keycols /*vote_compact's [2][kKeyRange]*/, VoteMeta* d_meta, _Float16* d_A,
+                          const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
+                          int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A,
                           hipStream_t s);
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
                           _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
