@@ -1,9 +1,10 @@
-"""Copy one scripts/profile_round.sh run (gpurun_out/<R>_*) into profiles/r01/ and recompute
+"""Copy one scripts/profile_round.sh run (gpurun_out/<R>_*) into profiles/<ROUND>/ and recompute
 profiles/traffic_fingerprint.json from its PMC passes.
 
 Usage: python scripts/tools/refresh_profiles.py R WARMUP STEPS KERNEL_BUILD_NOTE
   R        the profile_round.sh tag (gpurun_out/R_trace, R_pmc_FETCH_SIZE, R_pmc_WRITE_SIZE)
   WARMUP, STEPS  the bench arguments of the traced run (C2 dispatch selection)
+  ROUND (env, default r02): the profiles/ subdirectory the summaries go to
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB), per MI355X_MICROARCH.md's gfx950
 correction for 16-B/lane streaming reads; averaged over the C2-sized dispatches."""
 import csv
@@ -17,7 +18,9 @@ import sys
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 R, warm, steps, note = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
 src = os.path.join(REPO, "gpurun_out")
-dst = os.path.join(REPO, "profiles", "r01")
+ROUND = os.environ.get("ROUND", "r02")
+dst = os.path.join(REPO, "profiles", ROUND)
+os.makedirs(dst, exist_ok=True)
 C2_FRAMES = 960512
 
 for f in ("bench_kernel_stats.csv", "bench_kernel_trace.csv", "bench_domain_stats.csv"):
@@ -61,7 +64,7 @@ out = {
               "FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section (gfx950 reports half the bytes of 16-B/lane "
               "streaming reads; the PCM is read with global_load_dwordx4); WRITE_SIZE as reported "
               "(uncalibrated for 4-B scattered stores)",
-    "round": "r01",
+    "round": ROUND,
     "kernel_build": note,
 }
 json.dump(out, open(os.path.join(REPO, "profiles", "traffic_fingerprint.json"), "w"), indent=1)
