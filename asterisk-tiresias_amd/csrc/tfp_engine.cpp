@@ -129,6 +129,11 @@ struct tfp_engine {
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
+  // launch configuration and test/A-B knobs, read once at engine creation
+  FpLaunchCfg fpcfg;
+  int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
+  bool small_sync = true;     // TFP_SMALL_SYNC=0: batch-1 spins on the published result instead of a stream sync
+  bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
   ~tfp_engine() {
     if (qoff_ev) (void)hipEventDestroy(qoff_ev);
   }
@@ -261,10 +266,10 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
     d_tclip = e->tclip.as<int32_t>();
   }
   if (f32)
-    HIPCHK(e, launch_fingerprint_f32(T, static_cast<const float*>(d_pcm), d_soff, d_soff + 1, d_foff, d_toff, d_tclip,
+    HIPCHK(e, launch_fingerprint_f32(e->fpcfg, T, static_cast<const float*>(d_pcm), d_soff, d_soff + 1, d_foff, d_toff, d_tclip,
                                      toff[nclips], e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
   else
-    HIPCHK(e, launch_fingerprint(T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
+    HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
                                  d_toff, d_tclip, toff[nclips], nf, e->micro.as<int32_t>(), e->db.as<double>(),
                                  e->stream));
   *nframes_out = nf;
@@ -331,8 +336,67 @@ int new_clip(tfp_engine* e, const char* uuid, int64_t nrows, int64_t off, int32_
   return TFP_OK;
 }
 
+// Staging rows of live clips, moved down over the rows of removed clips (clip ids and row order
+// kept): one block per run of rows.
+__global__ void compact_rows_kernel(const int64_t* __restrict__ runs /*[n][3]: src, dst, len*/, const int32_t* m1,
+                                    const int32_t* m2, const int32_t* cl, int32_t* o1, int32_t* o2, int32_t* oc) {
+  const int64_t src = runs[3 * blockIdx.x], dst = runs[3 * blockIdx.x + 1], len = runs[3 * blockIdx.x + 2];
+  for (int64_t i = threadIdx.x; i < len; i += blockDim.x) {
+    o1[dst + i] = m1[src + i];
+    o2[dst + i] = m2[src + i];
+    oc[dst + i] = cl[src + i];
+  }
+}
+
+// Drops the staging rows of removed clips once they outnumber a quarter of the live rows (else
+// delete/re-enrol cycles grow the staging area, and every rebuild sorts the dead rows too).
+int compact_staging(tfp_engine* e) {
+  int64_t live = 0;
+  for (const auto& c : e->clips)
+    if (c.alive) live += c.nrows;
+  const int64_t dead = e->n_staged - live;
+  if (dead <= std::max<int64_t>(1 << 16, live / 4)) return TFP_OK;
+  std::vector<int64_t> runs;
+  int64_t dst = 0;
+  for (auto& c : e->clips) {
+    if (!c.alive || !c.nrows) continue;
+    const size_t nr = runs.size();
+    if (nr && runs[nr - 3] + runs[nr - 1] == c.off && runs[nr - 2] + runs[nr - 1] == dst) runs[nr - 1] += c.nrows;
+    else runs.insert(runs.end(), {c.off, dst, c.nrows});
+    c.off = dst;
+    dst += c.nrows;
+  }
+  for (auto& c : e->clips)
+    if (!c.alive) c.nrows = 0, c.off = 0;
+  DevBuf n1, n2, nc, d_runs;
+  const int64_t cap = std::max<int64_t>(live, 1 << 16);
+  HIPCHK(e, n1.reserve(sizeof(int32_t) * cap));
+  HIPCHK(e, n2.reserve(sizeof(int32_t) * cap));
+  HIPCHK(e, nc.reserve(sizeof(int32_t) * cap));
+  const int32_t nruns = (int32_t)(runs.size() / 3);
+  if (nruns) {
+    int rc = upload(e, d_runs, runs.data(), sizeof(int64_t) * runs.size());
+    if (rc) return rc;
+    hipLaunchKernelGGL(compact_rows_kernel, dim3(nruns), dim3(256), 0, e->stream, d_runs.as<int64_t>(),
+                       e->st_m1.as<int32_t>(), e->st_m2.as<int32_t>(), e->st_clip.as<int32_t>(), n1.as<int32_t>(),
+                       n2.as<int32_t>(), nc.as<int32_t>());
+    HIPCHK(e, hipGetLastError());
+  }
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::swap(e->st_m1.p, n1.p); std::swap(e->st_m1.bytes, n1.bytes);
+  std::swap(e->st_m2.p, n2.p); std::swap(e->st_m2.bytes, n2.bytes);
+  std::swap(e->st_clip.p, nc.p); std::swap(e->st_clip.bytes, nc.bytes);
+  e->n_staged = live;
+  e->cap_staged = cap;
+  return TFP_OK;
+}
+
 int rebuild(tfp_engine* e) {
   if (!e->dirty) return TFP_OK;
+  int rc = compact_staging(e);
+  if (rc) return rc;
+  // the sort and the index rows use 32-bit row numbers
+  if (e->n_staged >= INT32_MAX) return fail(e, TFP_E_CAPACITY, "%lld staged rows (limit 2^31 - 1)", (long long)e->n_staged);
   // uuid order of live clips = columns (the tie-break order of SQLite's result sort)
   std::vector<int32_t> live;
   for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
@@ -344,13 +408,19 @@ int rebuild(tfp_engine* e) {
   e->col_clip = live;
   e->tiekey_host.assign(std::max<size_t>(live.size(), 1), 0);
   e->key_col.clear();
+  const bool ovr = !e->tiebreak_override.empty();
   for (size_t r = 0; r < live.size(); r++) {
     const int32_t clip = live[r];
-    const int32_t k = e->tiebreak_override.size() > (size_t)clip ? e->tiebreak_override[clip] : (int32_t)r;
+    // With an override every live clip needs its own key (a clip added after the override would
+    // otherwise take its local rank, which can equal another shard's global key).
+    if (ovr && (size_t)clip >= e->tiebreak_override.size())
+      return fail(e, TFP_E_ARG, "clip %s was added after tfp_index_set_tiebreak: set the tie-break keys again",
+                  e->clips[clip].uuid.c_str());
+    const int32_t k = ovr ? e->tiebreak_override[clip] : (int32_t)r;
+    if (!e->key_col.emplace(k, (int32_t)r).second)
+      return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
     e->tiekey_host[r] = k;
-    e->key_col[k] = (int32_t)r;
   }
-  int rc;
   if ((rc = upload(e, e->rank_of_clip, rank.data(), sizeof(int32_t) * rank.size()))) return rc;
   if ((rc = upload(e, e->tiekey, e->tiekey_host.data(), sizeof(int32_t) * e->tiekey_host.size()))) return rc;
   const int64_t n = e->n_staged;
@@ -404,20 +474,6 @@ int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
 }
 
 // ---- search core: frames' q values already on device (e->q, 2 doubles per frame) -----------
-
-// Used-key count up to which the vote takes the pattern-class path (test/A-B knob read per call:
-// TFP_VOTE_CLASS_MAX, default 10, the kernels' limit; -1 always runs the Bt GEMM).
-int32_t vote_class_ku_max() {
-  const char* s = getenv("TFP_VOTE_CLASS_MAX");
-  return s ? (int32_t)atoi(s) : (int32_t)10;
-}
-
-// Batch-1 completion wait (A/B knob read per call): 1 = hipStreamSynchronize (default; measured
-// 2 us faster at p50), 0 = spin on the published result.
-bool small_sync_mode() {
-  const char* v = getenv("TFP_SMALL_SYNC");
-  return !v || atoi(v) != 0;
-}
 
 int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* d_q, const tfp_search_params* P,
                 std::vector<unsigned long long>& keys, unsigned long long* d_keys_out, hipStream_t s) {
@@ -474,7 +530,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       // past it the stream is synchronised and the result read after that.
       const volatile SmallResult* h = e->small_res.as<SmallResult>();
       bool seen = false;
-      if (!small_sync_mode()) {
+      if (!e->small_sync) {
         const auto t0 = std::chrono::steady_clock::now();
         for (;;) {
           if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
@@ -543,7 +599,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
     HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, d_meta, s));
     HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
-                             e->key_rng.as<int64_t>(), d_meta, vote_class_ku_max(), e->A.as<_Float16>(), s));
+                             e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(), s));
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),
@@ -560,8 +616,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     memcpy(&hm, e->vres_pin.p, sizeof hm);
     if (!d_keys_out && nq)
       memcpy(keys.data(), e->vres_pin.as<char>() + sizeof(VoteMeta), sizeof(unsigned long long) * nq);
-    static const bool dbg = getenv("TFP_DEBUG_VOTE") != nullptr;
-    if (dbg) fprintf(stderr, "[tfp] vote: nq %d Qp %d C %d ku %d kp %d ok %d\n", nq, Qp, C, hm.ku, hm.kp, hm.ok);
+    if (e->dbg_vote) fprintf(stderr, "[tfp] vote: nq %d Qp %d C %d ku %d kp %d ok %d\n", nq, Qp, C, hm.ku, hm.kp, hm.ok);
     if (hm.ok) return TFP_OK;
     // a count above fp16's exact range or a key outside the vote range: the scan path below
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
@@ -584,6 +639,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   }
   if (d_keys_out) {
     HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+    // the scan kernels read and write engine scratch (boxes, stamp, score, best): the next call,
+    // on any stream or thread, may reuse it only once they are done
+    HIPCHK(e, hipStreamSynchronize(s));
     return TFP_OK;
   }
   if (nq) HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
@@ -641,6 +699,13 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   if (hipSetDevice(device) != hipSuccess) return TFP_E_HIP;
   tfp_engine* e = new tfp_engine();
   e->device = device;
+  if (fp_launch_config(device, &e->fpcfg) != hipSuccess) {
+    delete e;
+    return TFP_E_HIP;
+  }
+  if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
+  if (const char* v = getenv("TFP_SMALL_SYNC")) e->small_sync = atoi(v) != 0;
+  e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;
@@ -741,7 +806,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s));
   return TFP_OK;
@@ -1011,7 +1076,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
                                e->db.as<double>(), s));
@@ -1163,7 +1228,7 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
   const int64_t* d_sb = reinterpret_cast<const int64_t*>(d + b_pcm);
-  HIPCHK(e, launch_fingerprint(Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), d_sb,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), d_sb,
                                reinterpret_cast<const int64_t*>(d + b_pcm + b_sb),
                                reinterpret_cast<const int64_t*>(d + b_pcm + 2 * b_sb),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo),

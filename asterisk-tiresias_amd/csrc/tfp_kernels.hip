@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
     const DspTables* __restrict__ T, const Smp* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip,
-    int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, int32_t ablate) {
+    int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db) {
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
   const int tid = threadIdx.x;
@@ -353,19 +353,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   // Loop-invariant twiddles in registers (2 waves/SIMD leave VGPR room): dft16's W16^e and this
   // lane's inter-stage w256^(L k1), read from LDS once instead of every pass.
-#ifndef TFP_HOIST
-#define TFP_HOIST 3  // bit 0: dft16 twiddles, bit 1: inter-stage lane twiddles; 3 = 0.740 ms vs 0.772 (1), 0.757 (2), 0.771 (0)
-#endif
-#if TFP_HOIST & 1
   cf w16r[10];
 #pragma unroll
   for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
-#endif
-#if TFP_HOIST & 2
   cf ltw[15];
 #pragma unroll
   for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
-#endif
   const bool c_defer = S.c_defer != 0;
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
   {
@@ -402,7 +395,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
 
     for (int sub = 0; sub < 4; sub++) {
       const int row = sub * 4 + grp;
-      const int64_t f = cur_f0 + row;
       // stage this pass's PCM (prefetched; hop h at h * kHopStride) and prefetch the next pass
       wave_sync();  // the previous pass's readers of the scratch are done
       Smp* const stage = reinterpret_cast<Smp*>(kF32 ? (void*)M.pcmf : (void*)M.pcm);
@@ -428,15 +420,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       asm volatile("" : "+v"(oz));
       const float* __restrict__ win = S.window + oz;  // read per pass (registers: occupancy)
       cf z[16], Y[16];
-#if !(TFP_HOIST & 1)
-      cf w16r[10];
-#pragma unroll
-      for (int e = 0; e < 10; e++) w16r[e] = S.w16[e + oz];
-#endif
-      if (ablate & 1) {
-#pragma unroll
-        for (int n1 = 0; n1 < 16; n1++) { z[n1].x = win[n1 + L]; z[n1].y = (float)f; }
-      } else {
+      {
 #pragma unroll
         for (int n1 = 0; n1 < 16; n1++) {
           const int j = (32 * n1 + 2 * L + 256) & 511;
@@ -450,17 +434,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
           }
         }
       }
-      if (ablate & 2) {
-#pragma unroll
-        for (int k = 0; k < 16; k++) Y[k] = z[k];
-      } else {
+      {
         dft16(w16r, z, Y);
 #pragma unroll
-#if TFP_HOIST & 2
         for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
-#else
-        for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
-#endif
         wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
         for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
@@ -472,31 +449,19 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       wave_sync();  // every lane has read its column of the square: W is free for |X|
       // |X[k]| of the 512-point real FFT, k = L + 16 k2, needs Z[256 - k]: for L >= 1 that is
       // Y[15 - k2] of lane 16 - L, for L = 0 it is this lane's own Y[16 - k2] (Z[256] = Z[0]).
-      if (ablate & 4) {
-#pragma unroll
-        for (int k2 = 0; k2 < 16; k2++) N[L + 16 * k2] = Y[k2].x + Y[k2].y;
-        if (L == 0) N[256] = Y[0].x;
-      } else {
+      {
         // branch-free: generic split + corrected v_sqrt for every k; lanes whose |X|^2 falls
         // outside [2^-100, 2^100) redo that bin with the full IEEE sqrt below (wave-uniform
         // test, practically never taken); lane 0 then writes the two real bins 0 and 256.
         bool rare = false;
-#ifndef TFP_SPLIT_PERBIN
         cf P[16];  // every partner fetched before the first use: the 32 bpermutes overlap
-                   // (0.854 vs 0.865 ms per C2 launch fetched per bin)
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) P[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
-#endif
 #pragma unroll
         for (int k2 = 0; k2 < 16; k2++) {
           const int k = L + 16 * k2;
           const cf own = Y[(16 - k2) & 15];
-#ifndef TFP_SPLIT_PERBIN
           const cf Pk = cf{L == 0 ? own.x : P[k2].x, L == 0 ? own.y : P[k2].y};
-#else
-          const cf Pg = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
-          const cf Pk = cf{L == 0 ? own.x : Pg.x, L == 0 ? own.y : Pg.y};
-#endif
           const float x = split_power(Y[k2], Pk, S.tw512[k + oz]);
           rare |= !(x >= 0x1p-100f && x < 0x1p100f);
           N[k] = sqrtf_fast_cr(x);
@@ -520,19 +485,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
       // Filterbank: this lane's 3 filters (slots A, B, C) summed interleaved, each in ascending
       // bin order from 0 (fmat_vecmul); then fvec_log10 of each.
       float* lrow = M.logs + row * kLogStride;
-      if (ablate & 8) {
-        lrow[fA] = N[L];
-        if (fB >= 0) lrow[fB] = N[L + 16];
-        if (fC >= 0) lrow[fC] = N[L + 32];
-      } else {
+      {
         const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
         float aA = 0.f, aB = 0.f, aC = 0.f;
         const int oA = S.ms_woff[0] + 4 * L, oB = S.ms_woff[1] + 4 * L, oC = S.ms_woff[2] + 4 * L;
-#ifndef TFP_MEL_GENERIC
         if (ms_in_lds && lenA == 36 && lenB == 16 && lenC == 8)  // the 8 kHz schedule
-#else
-        if (false)
-#endif
           mel3_fixed<36, 16, 8>(N, S.ms_w + oA, S.ms_w + oB, S.ms_w + oC, stA, stB, stC, aA, aB, aC);
         else if (ms_in_lds)
           mel3(N, S.ms_w + oA, S.ms_w + oB, S.ms_w + oC, stA, stB, stC, lenA, lenB, lenC, aA, aB, aC);
@@ -564,11 +521,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
     }
     // Tail: lane = (frame row, coef) for the tile's 16 frames: DCT row (fmat_vecmul order),
     // 10*log10|c| (fp_handler.c:651), "%f" micro-units / NULL (db_ctx_handler.c:479-481).
-    if ((ablate & 16) && lane < 2 * kWaveFrames) {
-      const int row = lane >> 1, cf = lane & 1;
-      const int64_t f = cur_f0 + row;
-      if (f < nf) micro[2 * (foff[cur_c] + f) + cf] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cf]);
-    } else if (lane < 2 * kWaveFrames) {
+    if (lane < 2 * kWaveFrames) {
       const int row = lane >> 1, cf = lane & 1;
       const int64_t f = cur_f0 + row;
       if (f < nf) {
@@ -624,11 +577,8 @@ __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], 
   for (int k1 = 0; k1 < 4; k1++) dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
 }
 
-// Filterbank sum over LEN bins (multiple of 4) with pair products: acc = ((acc + n0 w0) + n1 w1) ...
-#ifndef TFP8_MEL_BATCH
-#define TFP8_MEL_BATCH 9  // 4-bin groups whose loads are issued together (register pressure vs latency)
-#endif
-// ... with the weights already in registers (loaded a phase early, TFP8_HOIST_W)
+// Filterbank sum over LEN bins (multiple of 4), weights already in registers, products in
+// pairs: acc = (((acc + n0 w0) + n1 w1) + n2 w2) + ... in ascending bin order.
 template <int LEN>
 __device__ __forceinline__ float mel_sum_w(const float* __restrict__ N, const float4 (&wv)[LEN / 4], int st) {
   float4 nv[LEN / 4];
@@ -649,113 +599,6 @@ __device__ __forceinline__ void load_w(const float* __restrict__ w, float4 (&wv)
   for (int i = 0; i < LEN / 4; i++) wv[i] = *reinterpret_cast<const float4*>(w + 64 * i);
 }
 
-template <int LEN>
-__device__ __forceinline__ float mel_sum(const float* __restrict__ N, const float* __restrict__ w, int st) {
-  constexpr int G = LEN / 4, B = TFP8_MEL_BATCH < G ? TFP8_MEL_BATCH : G;
-  float acc = 0.f;
-#pragma unroll
-  for (int i0 = 0; i0 < G; i0 += B) {
-    float4 wv[B], nv[B];
-#pragma unroll
-    for (int i = 0; i < B; i++) {
-      if (i0 + i < G) {
-        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
-        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < B; i++) {
-      if (i0 + i < G) {
-        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
-        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
-        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
-      }
-    }
-  }
-  return acc;
-}
-
-#ifndef TFP8_ABL
-#define TFP8_ABL 0  // timing-only phase ablation (wrong results): 1 FFT, 2 split, 4 mel, 8 logs, 16 tail
-#endif
-#ifndef TFP8_HOIST_TW
-#define TFP8_HOIST_TW 0  // 1: split twiddles read before the second-stage DFT16 (measured 0.604 vs 0.583 ms)
-#endif
-#ifndef TFP8_HOIST_W
-#define TFP8_HOIST_W 0  // filterbank weights read before the split: 1 = slots B+C, 2 = slot A, 3 = all (all slower)
-#endif
-#ifndef TFP8_GLDS
-#define TFP8_GLDS 0  // PCM staged by LDS-DMA into two per-wave buffers (vs registers + ds_write_b128)
-#endif
-#ifndef TFP8_MELB
-#define TFP8_MELB 0  // > 0: filterbank loads issued in groups of this many 4-bin steps (register pressure)
-#endif
-#ifndef TFP8_SPLIT_TAIL
-#define TFP8_SPLIT_TAIL 1  // the tile tail stores the DCT coefficient; dB and "%f" run in finish_db_kernel
-#endif
-#ifndef TFP8_RARE_AFTER
-#define TFP8_RARE_AFTER 1  // one wave-uniform rare test after the pair loop (not one branch per pair)
-#endif
-#ifndef TFP8_PAIRSPLIT
-#define TFP8_PAIRSPLIT 1  // real split per conjugate pair (k, 256 - k) on one lane (see the split)
-#endif
-#ifndef TFP8_DPP
-#define TFP8_DPP 0  // split partners by DPP row_mirror (VALU) instead of ds_bpermute (LDS)
-#endif
-// Second-stage column of lane L. With TFP8_DPP the columns are numbered so that the partner
-// column 16 - k1 of every k1 other than 0 and 8 sits on the mirror lane 15 - L (row_mirror):
-// sigma = 0..7 on lanes 0..7, 9..15 on lanes 8..14, 8 on lane 15.
-__device__ __forceinline__ int col_of_lane(int L) {
-#if TFP8_DPP
-  return L < 8 ? L : (L == 15 ? 8 : L + 1);
-#else
-  return L;
-#endif
-}
-
-__device__ __forceinline__ float mirror16(float v) {  // lane 15 - L of the 16-lane row
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x140, 0xf, 0xf, false));
-}
-
-template <int LEN, int BATCH>
-__device__ __forceinline__ float mel_sum_b(const float* __restrict__ N, const float* __restrict__ w, int st) {
-  constexpr int G = LEN / 4, B = BATCH < G ? BATCH : G;
-  float acc = 0.f;
-#pragma unroll
-  for (int i0 = 0; i0 < G; i0 += B) {
-    float4 wv[B], nv[B];
-#pragma unroll
-    for (int i = 0; i < B; i++)
-      if (i0 + i < G) {
-        wv[i] = *reinterpret_cast<const float4*>(w + 64 * (i0 + i));
-        nv[i] = *reinterpret_cast<const float4*>(N + st + 4 * (i0 + i));
-      }
-#pragma unroll
-    for (int i = 0; i < B; i++)
-      if (i0 + i < G) {
-        const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
-        const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
-        acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
-      }
-  }
-  return acc;
-}
-
-#ifndef TFP8_TIMING
-#define TFP8_TIMING 0  // 1: lane 0 of each of the first 64 tiles' waves records s_memtime at 8 points
-#endif
-#if TFP8_TIMING
-__device__ unsigned long long g_tfp8_t[64][8];
-#define TFP8_TS(i)                                                                          \
-  do {                                                                                      \
-    const int tb_ = blockIdx.x * kBlockWaves + (threadIdx.x >> 6);                          \
-    if ((threadIdx.x & 63) == 0 && tb_ < 64) g_tfp8_t[tb_][i] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define TFP8_TS(i) \
-  do {             \
-  } while (0)
-#endif
 // kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
 // small batches: 4x the waves on a short query, a quarter of the per-wave latency).
 template <int kPasses>
@@ -765,20 +608,15 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
     float rare_thr) {
   constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
-  // dB + "%f" in finish_db_kernel for throughput launches; in the tile tail for small ones (4-frame
-  // tiles, batch-1 latency), which saves a launch
-  constexpr bool kSplitTail = TFP8_SPLIT_TAIL && kPasses == 4;
+  // dB + "%f" in finish_db_kernel for throughput launches (full waves); in the tile tail for small
+  // ones (4-frame tiles, batch-1 latency), which saves a launch
+  constexpr bool kSplitTail = kPasses == 4;
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
-#if TFP8_GLDS
-  // two PCM staging buffers per wave, filled by LDS-DMA one pass ahead (hop h at h * kHopStride)
-  __shared__ __attribute__((aligned(16))) int16_t PB[kBlockWaves][2][5 * kHopStride];
-#endif
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
-  TFP8_TS(0);
   // Wave-uniform tile state (scalar registers): clip, first frame, clip sample range.
   struct Tile {
     int c;
@@ -794,7 +632,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   };
   // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
   auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
-    (void)pf;
     const int16_t* clip = pcm + t.s0;
     const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
     const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
@@ -819,29 +656,22 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   int4 pf[kChunkRounds];
   int b = blockIdx.x * kBlockWaves + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
-#if !TFP8_GLDS
   fetch(cur, 0, b < ntiles, pf);
-  TFP8_TS(1);
-#endif
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
   cf* winr = reinterpret_cast<cf*>(S.window);
   cf* twr = S.tw512;
   // Table staging: every global load below is issued before any LDS write (indices clamped,
   // writes predicated), so a block waits for one round trip instead of one per table: a small
-  // launch is latency-bound (fp_timing.py: 4200 -> cycles to here).
+  // launch is latency-bound.
   static_assert(kBlockThreads == 256, "one entry per thread per table");
   constexpr int kMsW = 16 * (LA + LB + LC);  // DspTables::fixed8k()'s ms_total
   const int wL = (tid >> 1) & 15, wn1 = 2 * (tid >> 5) + (tid & 1);
   const int wj = (32 * wn1 + 2 * wL + 256) & 511;
   const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
-#if TFP8_PAIRSPLIT
   // [k2][L] = (w512^k, w512^(256 - k)), k = L + 16 k2 (k2 < 8; lane 0 at k2 = 0: k = 128)
   const int tk2 = tid >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
   const int tk = (tid & 1) ? 256 - tkk : tkk;
-#else
-  const int tk = col_of_lane(wL) + 16 * wn1;
-#endif
   const float twre = T->tw512_re[tk], twim = T->tw512_im[tk];
   const int li = tid < 240 ? tid : 239, lk1 = 1 + li / 16, lL = li % 16;
   const float ltre = T->lane_tw_re[lk1][lL], ltim = T->lane_tw_im[lk1][lL];
@@ -880,15 +710,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   }
   const unsigned long long empty_filters = __ballot(lane < kFilters && mlen == 0);  // (log of 0 + 2e-42)
   __syncthreads();
-  TFP8_TS(2);
 
-  const int sg = col_of_lane(L);  // second-stage FFT column (= bins sg + 16 k2) of this lane
-#if TFP8_DPP
-  const bool selfpair = L == 0 || L == 15;
-  const int plane = selfpair ? L : 15 - L;  // partner lane in the 16-lane row
-#else
-  const int plane = (16 - L) & 15;
-#endif
   WaveLds& M = WL[wave];
   cf* W = M.scratch[grp];
   float* N = reinterpret_cast<float*>(W) + 16 * (grp & 1);  // |X| row (see fingerprint_kernel)
@@ -896,30 +718,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
-#ifndef TFP8_W16_REGS
-#define TFP8_W16_REGS 0  // 1: dft16 twiddles held in registers (20 VGPRs; 8 VGPRs spilled: 0.541 vs 0.539 ms)
-#endif
-#if TFP8_W16_REGS
-  cf w16r[10];
-#pragma unroll
-  for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
-#endif
-#ifndef TFP8_LTW_REGS
-#define TFP8_LTW_REGS 1  // inter-stage lane twiddles held in registers (30 VGPRs) vs read per pass
-#endif
-#if TFP8_LTW_REGS
+  // inter-stage lane twiddles w256^(L k1) held in registers (30 VGPRs) instead of read per pass
   cf ltw[15];
 #pragma unroll
   for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
-#endif
-#ifndef TFP8_WIN_REGS
-#define TFP8_WIN_REGS 0  // this lane's 16 window pairs held in registers (32 VGPRs) vs read per pass
-#endif
-#if TFP8_WIN_REGS
-  cf wreg[16];
-#pragma unroll
-  for (int n1 = 0; n1 < 16; n1++) wreg[n1] = winr[((n1 >> 1) * 16 + L) * 2 + (n1 & 1)];
-#endif
   {
     const float lempty = aubio_log10_fast(0.f, S.logf);
     for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
@@ -928,40 +730,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
   }
 
-#if TFP8_GLDS
-  // One pass's 5 hops into buf: interior passes by LDS-DMA (global_load_lds_dwordx4, one 32-lane
-  // instruction per hop so each lands in its padded row), edge passes by checked loads + ds_write.
-  auto issue = [&](const Tile& t, int sub, bool valid, int16_t* buf) {
-    if (!valid) return;
-    const int16_t* clip = pcm + t.s0;
-    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
-    const bool interior = ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
-    if (interior) {
-      if (lane < 32) {
-#pragma unroll
-        for (int h = 0; h < 5; h++)
-          __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(clip + sb + h * kHop + 8 * lane),
-                                           (__attribute__((address_space(3))) void*)(buf + h * kHopStride), 16, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        if (chunk < kPassChunks)
-          *reinterpret_cast<int4*>(buf + (chunk >> 5) * kHopStride + (chunk & 31) * 8) =
-              fetch_chunk_checked(clip, t.ns, sb + 8 * chunk);
-      }
-    }
-  };
-  int16_t* const pb0 = PB[wave][0];
-  int16_t* const pb1 = PB[wave][1];
-  int par = 0;
-#endif
-#if TFP8_GLDS
-  issue(cur, 0, b < ntiles, pb0);
-  (void)pf;
-  (void)fetch;
-#endif
   for (; b < ntiles; b += nwaves) {
     const int64_t nf = (cur.ns + kHop - 1) / kHop;
     const int bn = b + nwaves;
@@ -970,35 +738,19 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     for (int sub = 0; sub < kPasses; sub++) {
       const int row = sub * 4 + grp;
       wave_sync();  // the previous pass's readers of the scratch are done
-#if TFP8_GLDS
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this pass's hops have landed in LDS
-      int16_t* const pcur = par ? pb1 : pb0;
-      // the other buffer was read by the previous pass: refill it for the next pass now
-      if (sub < kPasses - 1) issue(cur, sub + 1, true, par ? pb0 : pb1);
-      else issue(nxt, 0, bn < ntiles, par ? pb0 : pb1);
-      par ^= 1;
-#else
-      if constexpr (!(TFP8_ABL & 32)) {
 #pragma unroll
-        for (int r = 0; r < kChunkRounds; r++) {
-          const int chunk = lane + 64 * r;
-          if (chunk < kPassChunks)
-            *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
-        }
-        if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
-        else fetch(nxt, 0, bn < ntiles, pf);
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        if (chunk < kPassChunks) *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
       }
-#endif
+      if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
+      else fetch(nxt, 0, bn < ntiles, pf);
       wave_sync();
-      TFP8_TS(3);
-#if TFP8_GLDS
-      const int16_t* hop0 = pcur + grp * kHopStride;
-#else
       const int16_t* hop0 = M.pcm + grp * kHopStride;
-#endif
+      // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
+      // them into registers for the whole kernel (occupancy).
       int oz = 0;
       asm volatile("" : "+v"(oz));
-#if !TFP8_WIN_REGS
       cf wreg[16];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -1006,12 +758,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         wreg[2 * i] = cf{w4.x, w4.y};
         wreg[2 * i + 1] = cf{w4.z, w4.w};
       }
-#endif
-#if !TFP8_W16_REGS
       cf w16r[10];
 #pragma unroll
       for (int e = 0; e < 10; e++) w16r[e] = S.w16[e + oz];
-#endif
+      // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
+      // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
+      // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
       cf z[16], Y[16];
 #pragma unroll
       for (int n1 = 0; n1 < 16; n1++) {
@@ -1020,71 +772,61 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
         z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
       }
-      if constexpr (TFP8_ABL & 1) {
-#pragma unroll
-        for (int k = 0; k < 16; k++) Y[k] = z[k];
-      } else {
       dft16q(w16r, z, Y);
 #pragma unroll
-#if TFP8_LTW_REGS
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
-#else
-      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], S.lane_tw[k1 - 1][L + oz]);
-#endif
-      }
-      wave_sync();
+      wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
 #pragma unroll
       for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
       wave_sync();
 #pragma unroll
-      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + sg];
-      cf tw[16];
-#if TFP8_HOIST_TW
+      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
+      dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
+      wave_sync();         // every lane has read its column of the square: W is free for |X|
+      // Real split per conjugate pair on one lane: lane L (k2 < 8) owns bins k = L + 16 k2 and
+      // 256 - k, whose Z values are its Y[k2] and Y[15 - k2] of lane 16 - L (8 ds_bpermute pairs).
+      // Column 0 pairs inside lane 0: (16 k2, 256 - 16 k2) for k2 = 1..7 and (128, 128) at k2 = 0;
+      // bins 0 and 256 come from Z[0] below. The spec's partner-side operands are exact sign
+      // flips of this side's: E' = (E.re, -E.im), O' = (-O.re, O.im) (a - b = -(b - a),
+      // a + b = b + a in IEEE), so E and O are formed once per pair; each bin then takes its
+      // own table twiddle (w512^k, w512^(256-k)) through the spec's T and S = E + T = 2X.
+      cf Pq[8];
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const float4 t4 = *reinterpret_cast<const float4*>(twr + (i * 16 + L) * 2 + oz);
-        tw[2 * i] = cf{t4.x, t4.y};
-        tw[2 * i + 1] = cf{t4.z, t4.w};
+      for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
+      // bins 0 and 256 (lane 0) from Z[0], taken now so Y[0] is not kept alive
+      const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
+      uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) {
+        cf own = Y[k2 == 0 ? 8 : 16 - k2];
+        asm("" : "+v"(own.x), "+v"(own.y));  // a value: the selects stay v_cndmask
+        cf y = Y[k2];
+        if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
+        const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
+        const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
+        const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
+        const cf E = addsub(y, p);
+        const cf O = subadd(y, p);
+        const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
+        const cf Sv = E + Tt;
+        const cf O2 = cf{-O.x, O.y};
+        const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
+        const cf S2 = cf{E.x, -E.y} + T2;
+        const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
+        const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
+        // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top) go to the spec's order below
+        umin = min(umin, min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u));
+        N[k] = sqrtf_fast_cr(x);
+        N[256 - k] = sqrtf_fast_cr(x2);
       }
-#endif
-      if constexpr (TFP8_ABL & 1) {
-#pragma unroll
-        for (int k = 0; k < 16; k++) Y[k] = z[k];
-      } else {
-        dft16q(w16r, z, Y);  // Y[k2] = Z[sg + 16 k2]
-      }
-      wave_sync();
-      TFP8_TS(4);
-      const float* wbase = S.ms_w + 4 * L + oz;
-      float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
-      if (TFP8_HOIST_W & 1) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
-      if (TFP8_HOIST_W & 2) load_w<LA>(wbase + S.ms_woff[0], wA);
-      if constexpr (TFP8_ABL & 2) {
-#pragma unroll
-        for (int k2 = 0; k2 < 16; k2++) N[sg + 16 * k2] = Y[k2].x + Y[k2].y;
-      } else if constexpr (TFP8_PAIRSPLIT) {
-        // Conjugate pairs on one lane: lane L (k2 < 8) owns bins k = L + 16 k2 and 256 - k, whose
-        // Z values are its Y[k2] and Y[15 - k2] of lane 16 - L (8 ds_bpermute pairs instead of 16).
-        // Column 0 pairs inside lane 0: (16 k2, 256 - 16 k2) for k2 = 1..7 and (128, 128) at k2 = 0;
-        // bins 0 and 256 come from Z[0] below. The spec's partner-side operands are exact sign
-        // flips of this side's: E' = (E.re, -E.im), O' = (-O.re, O.im) (a - b = -(b - a),
-        // a + b = b + a in IEEE), so E and O are formed once per pair; each bin then takes its
-        // own table twiddle (w512^k, w512^(256-k)) through the spec's T and S = E + T = 2X.
-        cf Pq[8];
-#pragma unroll
-        for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
-        // bins 0 and 256 (lane 0) from Z[0], taken now so Y[0] is not kept alive
-        const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
-        uint32_t umin = 0xffffffffu;
-        (void)umin;
+      if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
 #pragma unroll
         for (int k2 = 0; k2 < 8; k2++) {
-          cf own = Y[k2 == 0 ? 8 : 16 - k2];
-          asm("" : "+v"(own.x), "+v"(own.y));  // a value: the selects stay v_cndmask
+          const cf own = Y[k2 == 0 ? 8 : 16 - k2];
           cf y = Y[k2];
-          if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
-          const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
-          const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
+          if (k2 == 0 && L == 0) y = own;
+          const cf p = L == 0 ? own : Pq[k2];
+          const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2);
           const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
           const cf E = addsub(y, p);
           const cf O = subadd(y, p);
@@ -1093,147 +835,34 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           const cf O2 = cf{-O.x, O.y};
           const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
           const cf S2 = cf{E.x, -E.y} + T2;
-          const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
+          const float x = Sv.x * Sv.x + Sv.y * Sv.y, x2 = S2.x * S2.x + S2.y * S2.y;
           const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-          float nk = sqrtf_fast_cr(x), nk2 = sqrtf_fast_cr(x2);
-          // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order instead
-          const uint32_t m = min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u);
-#if TFP8_RARE_AFTER
-          umin = min(umin, m);
-#else
-          if (__builtin_expect(__any(m < rare_m1), 0)) {
-            if (x > 0.f && x < rare_thr) nk = 2.f * __builtin_sqrtf(split_power(y, p, w));
-            if (x2 > 0.f && x2 < rare_thr) nk2 = 2.f * __builtin_sqrtf(split_power(p, y, w2));
-          }
-#endif
-          N[k] = nk;
-          N[256 - k] = nk2;
+          if (x > 0.f && x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
+          if (x2 > 0.f && x2 < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
         }
-#if TFP8_RARE_AFTER
-        if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
-#pragma unroll
-          for (int k2 = 0; k2 < 8; k2++) {
-            const cf own = Y[k2 == 0 ? 8 : 16 - k2];
-            cf y = Y[k2];
-            if (k2 == 0 && L == 0) y = own;
-            const cf p = L == 0 ? own : Pq[k2];
-            const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2);
-            const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
-            const cf E = addsub(y, p);
-            const cf O = subadd(y, p);
-            const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-            const cf Sv = E + Tt;
-            const cf O2 = cf{-O.x, O.y};
-            const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
-            const cf S2 = cf{E.x, -E.y} + T2;
-            const float x = Sv.x * Sv.x + Sv.y * Sv.y, x2 = S2.x * S2.x + S2.y * S2.y;
-            const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-            if (x > 0.f && x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
-            if (x2 > 0.f && x2 < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
-          }
-        }
-#endif
-        if (L == 0) {
-          N[0] = n0;
-          N[256] = n256;
-        }
-      } else {
-        // P[k2] = Z[256 - k]: Y[15 - k2] of the partner lane; column 0 (lane 0) pairs with its
-        // own Y[16 - k2] (Z[256] = Z[0]), column 8 (lane 15 under TFP8_DPP) with its own Y[15 - k2]
-#if TFP8_DPP
-        // (formed per bin inside the split loop: VALU, no latency to cover)
-#else
-        cf P[16];
-#pragma unroll
-        for (int k2 = 0; k2 < 16; k2++) {
-          const cf own = Y[(16 - k2) & 15];
-          P[k2] = cf{L == 0 ? own.x : partner16(Y[15 - k2].x), L == 0 ? own.y : partner16(Y[15 - k2].y)};
-        }
-#endif
-#if !TFP8_HOIST_TW
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-          const float4 t4 = *reinterpret_cast<const float4*>(twr + (i * 16 + L) * 2 + oz);
-          tw[2 * i] = cf{t4.x, t4.y};
-          tw[2 * i + 1] = cf{t4.z, t4.w};
-        }
-#endif
-        uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
-#pragma unroll
-        for (int k2 = 0; k2 < 16; k2++) {
-          const int k = sg + 16 * k2;
-#if TFP8_DPP
-          cf y0 = Y[(16 - k2) & 15];
-          asm("" : "+v"(y0.x), "+v"(y0.y));  // a value, so the select below stays a v_cndmask
-          const cf own = L == 0 ? y0 : Y[15 - k2];
-          cf mir = cf{mirror16(Y[15 - k2].x), mirror16(Y[15 - k2].y)};
-          asm volatile("" : "+v"(mir.x), "+v"(mir.y));  // computed on every lane, then selected
-          const cf Pk = cf{selfpair ? own.x : mir.x, selfpair ? own.y : mir.y};
-#else
-          const cf Pk = P[k2];
-#endif
-          const cf w = tw[k2];
-          const cf E = addsub(Y[k2], Pk);
-          const cf O = subadd(Y[k2], Pk);
-          const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-          const cf Sv = E + Tt;  // = 2X exactly
-          const float x = hadd(Sv * Sv);
-          umin = min(umin, __builtin_bit_cast(uint32_t, x) - 1u);
-          N[k] = sqrtf_fast_cr(x);  // 2|X| for x = 0 and x >= 2^-98
-        }
-        if (__builtin_expect(__any(umin < rare_m1), 0)) {  // some 0 < |S|^2 < rare_thr
-#if TFP8_DPP
-#pragma unroll  // (rolled, Y[] would be indexed dynamically)
-#endif
-          for (int k2 = 0; k2 < 16; k2++) {
-            const int k = sg + 16 * k2;
-            cf Q = cf{__shfl(Y[15 - k2].x, plane, 16), __shfl(Y[15 - k2].y, plane, 16)};
-            if (L == 0) Q = Y[(16 - k2) & 15];
-            const cf w = twr[((k2 >> 1) * 16 + L) * 2 + (k2 & 1)];
-            const cf E = addsub(Y[k2], Q);
-            const cf O = subadd(Y[k2], Q);
-            const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-            const cf Sv = E + Tt;
-            const float xs = Sv.x * Sv.x + Sv.y * Sv.y;
-            if (xs > 0.f && xs < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(Y[k2], Q, w));
-          }
-        }
-        if (L == 0) {
-          N[0] = 2.f * fabsf(Y[0].x + Y[0].y);
-          N[256] = 2.f * fabsf(Y[0].x - Y[0].y);
-        }
+      }
+      if (L == 0) {
+        N[0] = n0;
+        N[256] = n256;
       }
       for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
       wave_sync();
-      TFP8_TS(5);
+      // Filterbank: this lane's 3 filters (slots A, B, C) from the half weights, then the logs
+      const float* wbase = S.ms_w + 4 * L + oz;
       float* lrow = M.logs + row * kLogStride;
-      if constexpr (TFP8_ABL & 4) {
-        lrow[fA] = N[L];
-        lrow[fB] = N[L + 16];
-        if (c_real) lrow[fC] = N[L + 32];
-      } else {
-        const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
-#if TFP8_MELB
-        (void)wA; (void)wB; (void)wC;
-        const float aC = mel_sum_b<LC, TFP8_MELB>(N, wbase + S.ms_woff[2], stC);
-        const float aB = mel_sum_b<LB, TFP8_MELB>(N, wbase + S.ms_woff[1], stB);
-        const float aA = mel_sum_b<LA, TFP8_MELB>(N, wbase + S.ms_woff[0], stA);
-#else
-        if (!(TFP8_HOIST_W & 1)) { load_w<LC>(wbase + S.ms_woff[2], wC); load_w<LB>(wbase + S.ms_woff[1], wB); }
-        if (!(TFP8_HOIST_W & 2)) load_w<LA>(wbase + S.ms_woff[0], wA);
-        const float aC = mel_sum_w<LC>(N, wC, stC);
-        const float aB = mel_sum_w<LB>(N, wB, stB);
-        const float aA = mel_sum_w<LA>(N, wA, stA);
-#endif
-        const float lA = (TFP8_ABL & 8) ? aA : aubio_log10_fast(aA, S.logf);
-        const float lB = (TFP8_ABL & 8) ? aB : aubio_log10_fast(aB, S.logf);
-        lrow[fA] = lA;
-        lrow[fB] = lB;
-        if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
-      }
+      const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+      float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
+      load_w<LC>(wbase + S.ms_woff[2], wC);
+      load_w<LB>(wbase + S.ms_woff[1], wB);
+      load_w<LA>(wbase + S.ms_woff[0], wA);
+      const float aC = mel_sum_w<LC>(N, wC, stC);
+      const float aB = mel_sum_w<LB>(N, wB, stB);
+      const float aA = mel_sum_w<LA>(N, wA, stA);
+      lrow[fA] = aubio_log10_fast(aA, S.logf);
+      lrow[fB] = aubio_log10_fast(aB, S.logf);
+      if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
     }
     wave_sync();
-    TFP8_TS(6);
     if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];
       if (f >= 0) {
@@ -1242,11 +871,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
-    if ((TFP8_ABL & 16) && lane < 2 * 4 * kPasses) {
-      const int row = lane >> 1, cfi = lane & 1;
-      const int64_t f = cur.f0 + row;
-      if (f < nf) micro[2 * (foff[cur.c] + f) + cfi] = __builtin_bit_cast(int32_t, M.logs[row * kLogStride + cfi]);
-    } else if (lane < 2 * 4 * kPasses) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
+    if (lane < 2 * 4 * kPasses) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
       const int row = lane >> 1, cfi = lane & 1;
       const int64_t f = cur.f0 + row;
       if (f < nf) {
@@ -1265,260 +890,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
     }
     wave_sync();
-    TFP8_TS(7);
     cur = nxt;
-  }
-}
-
-// ------------------------------------------------------------------------------------
-// Software-pipelined 8 kHz kernel: iteration g runs the FRONT of pass g (PCM, FFT, real split,
-// |X| into the wave's |X| buffer) and the BACK of pass g-1 (filterbank + logs from that buffer),
-// so the filterbank's LDS reads and the FFT's VALU work of two passes share one basic block and
-// overlap; a tile's tail (DCT, dB, "%f") runs after the back of its last pass. Arithmetic and
-// results are fingerprint8k_kernel's (same helpers, same order per value).
-#ifndef TFP8P_MEL_BATCH
-#define TFP8P_MEL_BATCH 1
-#endif
-constexpr int kNRow = 288;  // |X| row per frame: bins 0..271 read (8 kHz ms_maxbin = 272); 288 = 32 mod 64 banks
-struct WaveLds8P {
-  union {
-    cf scratch[4][kFrameStride];
-    alignas(16) int16_t pcm[5 * kHopStride];
-  };
-  alignas(16) float nbuf[4][kNRow];
-  float logs[kWaveFrames * kLogStride];
-};
-
-__global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_pipe_kernel(
-    const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
-    const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
-    const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
-    float rare_thr) {
-  constexpr int LA = 36, LB = 16, LC = 8;  // DspTables_fixed8k()
-  const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;
-  __shared__ __attribute__((aligned(16))) LdsTables S;
-  __shared__ __attribute__((aligned(16))) WaveLds8P WL[kBlockWaves];
-  const int tid = threadIdx.x;
-  cf* winr = reinterpret_cast<cf*>(S.window);  // [n1/2][L][2] window pairs (see fingerprint8k_kernel)
-  cf* twr = S.tw512;                           // [k2][L] = (w512^k, w512^(256-k)) pair-split twiddles
-  for (int i = tid; i < 256; i += kBlockThreads) {
-    const int L = (i >> 1) & 15, n1 = 2 * (i >> 5) + (i & 1);
-    const int j = (32 * n1 + 2 * L + 256) & 511;
-    winr[i] = cf{T->window_s[j], T->window_s[j + 1]};
-    const int k2 = i >> 5, kk = (L == 0 && k2 == 0) ? 128 : L + 16 * k2, kp = 256 - kk;
-    twr[i] = (i & 1) ? cf{T->tw512_re[kp], T->tw512_im[kp]} : cf{T->tw512_re[kk], T->tw512_im[kk]};
-  }
-  for (int i = tid; i < 15 * 16; i += kBlockThreads) {
-    const int k1 = 1 + i / 16, L = i % 16;
-    S.lane_tw[k1 - 1][L] = cf{T->lane_tw_re[k1][L], T->lane_tw_im[k1][L]};
-  }
-  for (int i = tid; i < 10; i += kBlockThreads) S.w16[i] = cf{T->tw256_re[16 * i], T->tw256_im[16 * i]};
-  for (int i = tid; i < kCoefs * kFilters; i += kBlockThreads) (&S.dct[0][0])[i] = (&T->dct[0][0])[i];
-  for (int i = tid; i < 48; i += kBlockThreads) {
-    (&S.ms_filter[0][0])[i] = (&T->ms_filter[0][0])[i];
-    (&S.ms_start[0][0])[i] = (&T->ms_start[0][0])[i];
-  }
-  if (tid < 3) { S.ms_len[tid] = T->ms_len[tid]; S.ms_woff[tid] = T->ms_woff[tid]; }
-  if (tid < 16) S.logf[tid] = logf_table()[tid];
-  if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
-  for (int i = tid; i < T->ms_total; i += kBlockThreads) S.ms_w[i] = 0.5f * T->ms_w[i];  // exact: w/2
-  __syncthreads();
-
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
-  WaveLds8P& M = WL[wave];
-  cf* W = M.scratch[grp];
-  float* Nf = M.nbuf[grp];
-  const int nwaves = gridDim.x * kBlockWaves;
-  const int maxbin = T->ms_maxbin;
-  const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
-  const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
-  cf w16r[10];
-#pragma unroll
-  for (int e = 0; e < 10; e++) w16r[e] = S.w16[e];
-  cf ltw[15];
-#pragma unroll
-  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
-  {
-    const float lempty = aubio_log10_fast(0.f, S.logf);
-    for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
-      const int j = i % kFilters;
-      if (T->mel_len[j] == 0) M.logs[(i / kFilters) * kLogStride + j] = lempty;
-    }
-    for (int i = lane; i < 4 * kNRow; i += 64) (&M.nbuf[0][0])[i] = 0.f;  // the first (dummy) back pass
-  }
-
-  struct Tile {
-    int c;
-    int64_t f0, s0, ns;
-  };
-  auto tile_of = [&](int b) {
-    Tile t;
-    t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
-    t.f0 = (int64_t)(b - toff[t.c]) * kWaveFrames;
-    t.s0 = sbeg[t.c];
-    t.ns = send[t.c] - t.s0;
-    return t;
-  };
-  auto fetch = [&](const Tile& t, int sub, bool valid, int4 (&pf)[kChunkRounds]) {
-    const int16_t* clip = pcm + t.s0;
-    const int64_t sb = (t.f0 + 4 * sub - 1) * kHop;
-    const bool interior = valid && ((reinterpret_cast<uintptr_t>(clip) & 15) == 0) && sb >= 0 && sb + kPassSamples <= t.ns;
-    if (interior) {
-      const int4* src = reinterpret_cast<const int4*>(clip + sb);
-#pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        pf[r] = (valid && chunk < kPassChunks) ? fetch_chunk_checked(clip, t.ns, sb + 8 * chunk) : make_int4(0, 0, 0, 0);
-      }
-    }
-  };
-
-  const int b0 = blockIdx.x * kBlockWaves + wave;
-  const int my_tiles = b0 < ntiles ? (ntiles - 1 - b0) / nwaves + 1 : 0;
-  const int npass = 4 * my_tiles;
-  int bf = b0, subf = 0;  // front pass: tile bf, pass subf
-  Tile tf = tile_of(b0 < ntiles ? b0 : 0);
-  Tile tn = (b0 + nwaves < ntiles) ? tile_of(b0 + nwaves) : tf;
-  Tile tb = tf;           // tile of the back pass
-  int4 pf[kChunkRounds];
-  fetch(tf, 0, b0 < ntiles, pf);
-  for (int g = 0; g <= npass; g++) {
-    const bool front_valid = g < npass;
-    const int subb = (g + 3) & 3;  // pass of the back half (g - 1)
-    wave_sync();  // the previous iteration's readers of the scratch are done
-#pragma unroll
-    for (int r = 0; r < kChunkRounds; r++) {
-      const int chunk = lane + 64 * r;
-      if (chunk < kPassChunks) *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
-    }
-    if (subf < 3) fetch(tf, subf + 1, front_valid, pf);
-    else fetch(tn, 0, front_valid && bf + nwaves < ntiles, pf);
-    wave_sync();
-    int oz = 0;
-    asm volatile("" : "+v"(oz));
-    // ---- FRONT (pass g): PCM -> window -> first DFT16 -> inter-stage twiddles
-    const int16_t* hop0 = M.pcm + grp * kHopStride;
-    cf wreg[16];
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const float4 w4 = *reinterpret_cast<const float4*>(winr + (i * 16 + L) * 2 + oz);
-      wreg[2 * i] = cf{w4.x, w4.y};
-      wreg[2 * i + 1] = cf{w4.z, w4.w};
-    }
-    cf z[16], Y[16];
-#pragma unroll
-    for (int n1 = 0; n1 < 16; n1++) {
-      const int j = (32 * n1 + 2 * L + 256) & 511;
-      const int hsel = n1 < 8 ? 1 : 0;
-      const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
-      z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
-    }
-    dft16q(w16r, z, Y);
-#pragma unroll
-    for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
-    // ---- BACK (pass g - 1): filterbank + logs from the |X| buffer (same basic block as the FFT)
-    {
-      const float* Nb = Nf;
-      float* lrow = M.logs + (subb * 4 + grp) * kLogStride;
-      const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
-      const float* wbase = S.ms_w + 4 * L + oz;
-      const float aC = mel_sum_b<LC, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[2], stC);
-      const float aB = mel_sum_b<LB, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[1], stB);
-      const float aA = mel_sum_b<LA, TFP8P_MEL_BATCH>(Nb, wbase + S.ms_woff[0], stA);
-      const float lA = aubio_log10_fast(aA, S.logf);
-      const float lB = aubio_log10_fast(aB, S.logf);
-      lrow[fA] = lA;
-      lrow[fB] = lB;
-      if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
-    }
-    wave_sync();
-    // ---- FRONT: transpose, second DFT16, real split -> |X| buffer
-#pragma unroll
-    for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
-    wave_sync();
-#pragma unroll
-    for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
-    dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
-    {
-      cf Pq[8];
-#pragma unroll
-      for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
-      const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
-#pragma unroll
-      for (int k2 = 0; k2 < 8; k2++) {
-        cf own = Y[k2 == 0 ? 8 : 16 - k2];
-        asm("" : "+v"(own.x), "+v"(own.y));
-        cf y = Y[k2];
-        if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
-        const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
-        const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
-        const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
-        const cf E = addsub(y, p);
-        const cf O = subadd(y, p);
-        const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-        const cf Sv = E + Tt;
-        const cf O2 = cf{-O.x, O.y};
-        const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
-        const cf S2 = cf{E.x, -E.y} + T2;
-        const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
-        const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-        float nk = sqrtf_fast_cr(x), nk2 = sqrtf_fast_cr(x2);
-        const uint32_t m = min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u);
-        if (__builtin_expect(__any(m < rare_m1), 0)) {
-          if (x > 0.f && x < rare_thr) nk = 2.f * __builtin_sqrtf(split_power(y, p, w));
-          if (x2 > 0.f && x2 < rare_thr) nk2 = 2.f * __builtin_sqrtf(split_power(p, y, w2));
-        }
-        Nf[k] = nk;
-        Nf[256 - k] = nk2;
-      }
-      if (L == 0) {
-        Nf[0] = n0;
-        Nf[256] = n256;
-      }
-      for (int i = 257 + L; i < maxbin; i += 16) Nf[i] = 0.f;
-    }
-    // ---- tail of the back tile after the back of its last pass
-    if (g >= 1 && subb == 3) {
-      wave_sync();
-      if (lane < 2 * kWaveFrames) {  // the deferred slot-2 logs: lane = (frame row, filter)
-        const int f = S.c_real[lane & 1];
-        if (f >= 0) {
-          float* p = M.logs + (lane >> 1) * kLogStride + f;
-          *p = aubio_log10_fast(*p, S.logf);
-        }
-      }
-      wave_sync();
-      if (lane < 2 * kWaveFrames) {  // DCT row, 10*log10|c|, "%f" micro-units / NULL
-        const int row = lane >> 1, cfi = lane & 1;
-        const int64_t f = tb.f0 + row;
-        const int64_t nfb = (tb.ns + kHop - 1) / kHop;
-        if (f < nfb) {
-          const float* lrow = M.logs + row * kLogStride;
-          float acc = 0.f;
-#pragma unroll 8
-          for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
-          const double q = db_of_coef(acc);
-          const int64_t gi = foff[tb.c] + f;
-          micro[2 * gi + cfi] = micro_of_db(q);
-          if (db) db[2 * gi + cfi] = q;
-        }
-      }
-    }
-    // advance: the back half of the next iteration is this iteration's front pass
-    tb = tf;
-    if (++subf == 4) {
-      subf = 0;
-      bf += nwaves;
-      tf = tn;
-      tn = (bf + nwaves < ntiles) ? tile_of(bf + nwaves) : tf;
-    }
   }
 }
 
@@ -1539,79 +911,67 @@ bool DspTables_fixed8k(const DspTables& t) {
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
 }
 
-hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t tile_frames, const int16_t* d_pcm,
-                              const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                              const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
-                              hipStream_t s) {
-  if (tile_frames != 16 && !(tile_frames == 4 && fixed8k)) return hipErrorInvalidValue;
-  if (ntiles <= 0) return hipSuccess;
-  static int grid_cap[2] = {0, 0};
-  // Test/A-B knobs, read per launch: TFP_GENERIC=1 runs the generic kernel at 8 kHz too;
-  // TFP_RARE_THR_LOG2=n (n >= -98) sends every bin with 0 < |S|^2 < 2^n through the spec-order
-  // slow path of the real split (any such threshold gives the same, exact, result).
+hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
+  int cus = 0, per = 0;
+  hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return e;
+  auto cap = [&](const void* k) {
+    per = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kBlockThreads, 0);
+    return cus * (per > 0 ? per : 1);
+  };
+  cfg->grid_cap_8k = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<4>));
+  cfg->grid_cap_generic = cap(reinterpret_cast<const void*>(fingerprint_kernel<int16_t>));
+  cfg->grid_cap_f32 = cap(reinterpret_cast<const void*>(fingerprint_kernel<float>));
   const char* g = getenv("TFP_GENERIC");
-  const int v = (fixed8k && !(g && atoi(g))) ? 1 : 0;
+  cfg->force_generic = g && atoi(g);
   const char* rt = getenv("TFP_RARE_THR_LOG2");
   int rl = rt ? atoi(rt) : -98;
-  rl = rl < -98 ? -98 : (rl > 100 ? 100 : rl);
-  const float rare_thr = ldexpf(1.f, rl);
-  if (!grid_cap[v]) {
-    int dev = 0, cus = 256, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (v) (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint8k_kernel<4>, kBlockThreads, 0);
-    else (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel<int16_t>, kBlockThreads, 0);
-    grid_cap[v] = cus * (per > 0 ? per : 1);
-  }
+  rl = rl < -98 ? -98 : (rl > 100 ? 100 : rl);  // any threshold >= 2^-98 gives the same, exact, result
+  cfg->rare_thr = ldexpf(1.f, rl);
+  return hipSuccess;
+}
+
+hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
+                              const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
+                              const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
+                              int32_t* d_micro, double* d_db, hipStream_t s) {
+  if (tile_frames != 16 && !(tile_frames == 4 && fixed8k)) return hipErrorInvalidValue;
+  if (ntiles <= 0) return hipSuccess;
+  const bool v8 = fixed8k && (tile_frames == 4 || !cfg.force_generic);
+  const int cap = v8 ? cfg.grid_cap_8k : cfg.grid_cap_generic;
+  if (cap <= 0) return hipErrorInvalidValue;
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
-  const int grid = want < grid_cap[v] ? want : grid_cap[v];
-  if (v) {
-    const char* pp = getenv("TFP_PIPE");
-    if (pp && atoi(pp) && tile_frames == 16)
-      hipLaunchKernelGGL(fingerprint8k_pipe_kernel, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
-    else {
-      if (tile_frames == 4)
-        hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                           d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
-      else
-        hipLaunchKernelGGL(fingerprint8k_kernel<4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                           d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, rare_thr);
-#if TFP8_SPLIT_TAIL
-      const int64_t nv = tile_frames == 16 ? 2 * nframes : 0;  // fingerprint8k_kernel<1> finishes its own tail
+  const int grid = want < cap ? want : cap;
+  if (v8) {
+    if (tile_frames == 4) {  // fingerprint8k_kernel<1> finishes its own tail
+      hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
+    } else {
+      hipLaunchKernelGGL(fingerprint8k_kernel<4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
+      const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;
       if (nv > 0) hipLaunchKernelGGL(finish_db_kernel, dim3((unsigned)g), dim3(256), 0, s, d_micro, d_db, nv);
-#endif
     }
     return hipGetLastError();
   }
-  static int ablate = -1;  // debug-only phase ablation for profiling (TFP_ABLATE bitmask); 0 in production
-  if (ablate < 0) {
-    const char* a = getenv("TFP_ABLATE");
-    ablate = a ? atoi(a) : 0;
-  }
   hipLaunchKernelGGL(fingerprint_kernel<int16_t>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, ablate);
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db);
   return hipGetLastError();
 }
 
-hipError_t launch_fingerprint_f32(const DspTables* d_tables, const float* d_x, const int64_t* d_sbeg,
-                                  const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                                  const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s) {
+hipError_t launch_fingerprint_f32(const FpLaunchCfg& cfg, const DspTables* d_tables, const float* d_x,
+                                  const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
+                                  const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro,
+                                  double* d_db, hipStream_t s) {
   if (ntiles <= 0) return hipSuccess;
-  static int grid_cap = 0;
-  if (!grid_cap) {
-    int dev = 0, cus = 256, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fingerprint_kernel<float>, kBlockThreads, 0);
-    grid_cap = cus * (per > 0 ? per : 1);
-  }
+  if (cfg.grid_cap_f32 <= 0) return hipErrorInvalidValue;
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;
-  const int grid = want < grid_cap ? want : grid_cap;
+  const int grid = want < cfg.grid_cap_f32 ? want : cfg.grid_cap_f32;
   hipLaunchKernelGGL(fingerprint_kernel<float>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_x, d_sbeg, d_send,
-                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, 0);
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db);
   return hipGetLastError();
 }
 
@@ -2628,8 +1988,3 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_b
 
 }  // namespace tfp
 
-#if TFP8_TIMING
-extern "C" int tfp_debug_fp_timing(unsigned long long* out) {  // 64 x 8 s_memtime stamps
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(tfp::g_tfp8_t), sizeof(tfp::g_tfp8_t)) == hipSuccess ? 0 : -2;
-}
-#endif

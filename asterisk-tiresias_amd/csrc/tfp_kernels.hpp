@@ -35,19 +35,31 @@ struct SynthSpecDev {
 // Fingerprint clips: clip c = samples [sbeg[c], send[c]) of d_pcm (for concatenated clips pass
 // send = soff + 1); frames of clip c are written from foff[c]; toff[nclips+1] are 16-frame tile
 // offsets (ntiles = toff[nclips]) and tclip[tile] the clip of each tile.
+// Per-engine launch configuration: read once when the engine is created (fp_launch_config),
+// grid caps from the engine's own device.
+struct FpLaunchCfg {
+  int32_t grid_cap_8k = 0;       // resident blocks of fingerprint8k_kernel on the device
+  int32_t grid_cap_generic = 0;  // resident blocks of fingerprint_kernel<int16_t>
+  int32_t grid_cap_f32 = 0;      // resident blocks of fingerprint_kernel<float>
+  bool force_generic = false;    // TFP_GENERIC=1: the generic kernel at 8 kHz too (tests)
+  float rare_thr = 0x1p-98f;     // TFP_RARE_THR_LOG2=n: bins with 0 < |S|^2 < 2^n take the spec-order path (tests)
+};
+// Fills cfg for `device` (occupancy queries + the test knobs from the environment).
+hipError_t fp_launch_config(int device, FpLaunchCfg* cfg);
 // fixed8k: the tables' filterbank schedule is the 8 kHz one (DspTables_fixed8k), so the
 // specialized fingerprint8k_kernel runs; otherwise the generic fingerprint_kernel.
 bool DspTables_fixed8k(const DspTables& t);
 // tile_frames: frames per wave tile in toff/tclip, 16 (any rate) or 4 (8 kHz only: small batches).
-hipError_t launch_fingerprint(const DspTables* d_tables, bool fixed8k, int32_t tile_frames, const int16_t* d_pcm, const int64_t* d_sbeg,
-                              const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                              const int32_t* d_tclip, int32_t ntiles, int64_t nframes, int32_t* d_micro, double* d_db,
-                              hipStream_t s);
+hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
+                              const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
+                              const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
+                              int32_t* d_micro, double* d_db, hipStream_t s);
 // fp32 samples (the values aubio_source_do produces: multichannel mean, 24/32-bit or float
 // WAV, tfp_wav_decode_f32) through the generic kernel, 16-frame tiles; same outputs as above.
-hipError_t launch_fingerprint_f32(const DspTables* d_tables, const float* d_x, const int64_t* d_sbeg,
-                                  const int64_t* d_send, const int64_t* d_foff, const int32_t* d_toff,
-                                  const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro, double* d_db, hipStream_t s);
+hipError_t launch_fingerprint_f32(const FpLaunchCfg& cfg, const DspTables* d_tables, const float* d_x,
+                                  const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
+                                  const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro,
+                                  double* d_db, hipStream_t s);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
 

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -87,9 +88,12 @@ class Engine:
         if rc != 0:
             raise TfpError(rc, f"cannot create engine on device {device}")
         self.device = device
+        self._streams = weakref.WeakSet()  # live Streams: destroyed before the engine (tiresias_fp.h)
 
     def close(self):
         if self._h:
+            for st in list(self._streams):
+                st.close()
             lib().tfp_engine_destroy(self._h)
             self._h = C.c_void_p()
 
@@ -277,6 +281,7 @@ class Stream:
                                          C.byref(self._h)))
         self.nchannels = nchannels
         self._res = (Result * nchannels)()
+        eng._streams.add(self)
 
     def reset(self, channel: int = -1):
         self._eng._chk(lib().tfp_stream_reset(self._h, int(channel)))
@@ -292,10 +297,18 @@ class Stream:
         return [None if not r.found else {"audio_uuid": r.uuid.decode(), "match_count": r.match_count,
                                           "frame_count": r.frame_count} for r in self._res]
 
-    def __del__(self):
-        if self._h:
+    def close(self):
+        # tfp_stream_destroy uses the engine: a stream outliving its engine's close() was already
+        # destroyed by it, so there is nothing left to free here
+        if self._h and self._eng._h:
             lib().tfp_stream_destroy(self._h)
-            self._h = C.c_void_p()
+        self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class Plan:

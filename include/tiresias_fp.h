@@ -87,7 +87,7 @@ typedef struct tfp_result {
 int tfp_abi_version(void);
 int tfp_device_count(int32_t* count);
 int tfp_engine_create(int32_t device, tfp_engine** out);
-void tfp_engine_destroy(tfp_engine* eng);
+void tfp_engine_destroy(tfp_engine* eng); /* destroy the engine's streams first */
 const char* tfp_engine_last_error(const tfp_engine* eng); /* eng == NULL: this thread's last
                                                           * engine-less error (tfp_wav_*) */
 int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
@@ -164,7 +164,10 @@ int tfp_index_stats(tfp_engine* eng, int64_t* nrows, int32_t* nclips);
 /* Rebuild the sorted device index now (otherwise done lazily by the next search). */
 int tfp_index_commit(tfp_engine* eng);
 /* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
- * this engine's uuids). keys[clip_id] must order like the uuids across all shards. */
+ * this engine's uuids). keys[clip_id] must order like the uuids across all shards and be
+ * distinct over live clips. A clip added after this call has no key: the next search (or
+ * tfp_index_commit) fails with TFP_E_ARG until the keys are set again; nclip_ids = 0 clears
+ * the override. */
 int tfp_index_set_tiebreak(tfp_engine* eng, const int32_t* keys, int32_t nclip_ids);
 
 /* ---- search: fp_search_fingerprint_info (fp_handler.c:207-408) ---------------------- */
@@ -204,7 +207,7 @@ int tfp_index_uuid_of_key(tfp_engine* eng, int32_t key, char* uuid, int32_t len)
 typedef struct tfp_stream tfp_stream;
 int tfp_stream_create(tfp_engine* eng, int32_t nchannels, int32_t sample_rate, int64_t window_samples,
                       tfp_stream** out);
-void tfp_stream_destroy(tfp_stream* st);
+void tfp_stream_destroy(tfp_stream* st); /* before tfp_engine_destroy of its engine */
 /* A new call on `channel` (< 0: every channel): its history restarts empty. */
 int tfp_stream_reset(tfp_stream* st, int32_t channel);
 /* pcm[nchannels][tick_samples] (host); tick_samples <= window_samples. params NULL: only

@@ -343,6 +343,38 @@ size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int6
  * NULL) reads back as 0.0. */
 static double json_real_get(double v) { return isfinite(v) ? v : 0.0; }
 
+/* One query frame's WHERE clause (fp_handler.c:287-351): 0 = the frame runs no SQL (ignored by
+ * freq_ignore_low/high, or a bound that "%f" cannot print as a SQL literal); else [L1, U1] on
+ * max1 and, when *has2, [L2, U2] on max2, in micro-units. */
+static int frame_box(double q1v, double q2v, int coefs, double tole, int low, int high, int64_t* L1,
+                     int64_t* U1, int* has2, int64_t* L2, int64_t* U2) {
+  double freq = (int)json_real_get(q1v); /* fp_handler.c:290 */
+  double lo1, hi1;
+  *has2 = 0;
+  if (low > 0 && freq < 10 * log10(low)) return 0;   /* :293-299 */
+  if (high > 0 && freq > 10 * log10(high)) return 0; /* :300-306 */
+  lo1 = freq - tole;
+  hi1 = freq + tole;
+  /* "%f" of nan/inf is not a SQL literal: the statement fails, nothing is inserted */
+  if (!isfinite(lo1) || !isfinite(hi1)) return 0;
+  *L1 = tfo_fmt6(lo1);
+  *U1 = tfo_fmt6(hi1);
+  if (coefs == 2) { /* :318-351, j = 1 */
+    double f2 = json_real_get(q2v);
+    int skip = 0;
+    if (low > 0 && f2 < 10 * log10(low)) skip = 1;
+    else if (high > 0 && f2 > 10 * log10(high)) skip = 1;
+    if (!skip) { /* a failing max2 ignore test drops only the max2 condition */
+      double lo2 = f2 - tole, hi2 = f2 + tole;
+      if (!isfinite(lo2) || !isfinite(hi2)) return 0;
+      *L2 = tfo_fmt6(lo2);
+      *U2 = tfo_fmt6(hi2);
+      *has2 = 1;
+    }
+  }
+  return 1;
+}
+
 int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, int64_t nrows,
                const char* const* uuids, int32_t nclips, const double* q1, const double* q2,
                int32_t nq, int coefs, double tolerance, int low, int high, int32_t* winner,
@@ -361,32 +393,9 @@ int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, in
   score = (int32_t*)calloc((size_t)(nclips > 0 ? nclips : 1), sizeof(int32_t));
   stamp = (int32_t*)calloc((size_t)(nclips > 0 ? nclips : 1), sizeof(int32_t));
   for (i = 0; i < nq; i++) {
-    double freq = (int)json_real_get(q1[i]); /* fp_handler.c:290 */
-    double lo1, hi1, lo2 = 0, hi2 = 0;
     int64_t L1, U1, L2 = 0, U2 = 0;
-    int has2 = 0;
-    if (low > 0 && freq < 10 * log10(low)) continue;   /* :293-299 */
-    if (high > 0 && freq > 10 * log10(high)) continue; /* :300-306 */
-    lo1 = freq - tole;
-    hi1 = freq + tole;
-    /* "%f" of nan/inf is not a SQL literal: the statement fails, nothing is inserted */
-    if (!isfinite(lo1) || !isfinite(hi1)) continue;
-    L1 = tfo_fmt6(lo1);
-    U1 = tfo_fmt6(hi1);
-    if (coefs == 2) { /* :318-351, j = 1 */
-      double f2 = json_real_get(q2[i]);
-      int skip = 0;
-      if (low > 0 && f2 < 10 * log10(low)) skip = 1;
-      else if (high > 0 && f2 > 10 * log10(high)) skip = 1;
-      if (!skip) {
-        lo2 = f2 - tole;
-        hi2 = f2 + tole;
-        if (!isfinite(lo2) || !isfinite(hi2)) continue;
-        L2 = tfo_fmt6(lo2);
-        U2 = tfo_fmt6(hi2);
-        has2 = 1;
-      }
-    }
+    int has2;
+    if (!frame_box(q1[i], q2[i], coefs, tole, low, high, &L1, &U1, &has2, &L2, &U2)) continue;
     /* insert into temp select * from audio_fingerprint where ... group by audio_uuid */
     for (r = 0; r < nrows; r++) {
       if (m1[r] == TFO_NULL) continue; /* NULL compares false */
@@ -411,4 +420,128 @@ int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, in
   free(score);
   free(stamp);
   return best >= 0;
+}
+
+/* ------------------------------------------------ large tables: sorted index ---------- */
+
+/* Rows ordered by max1 (the reference's B-tree idx_audio_fingerprint_max1, fp_handler.c:745-753):
+ * LSD radix sort on the order-preserving unsigned image of m1, stable, 4 passes of 8 bits. */
+int64_t tfo_sort_rows(const int32_t* m1, const int32_t* m2, const int32_t* clip, int64_t n, int32_t* om1,
+                      int32_t* om2, int32_t* oclip) {
+  uint32_t* ka = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+  uint32_t* kb = (uint32_t*)malloc(sizeof(uint32_t) * (size_t)(n > 0 ? n : 1));
+  int64_t* ia = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t* ib = (int64_t*)malloc(sizeof(int64_t) * (size_t)(n > 0 ? n : 1));
+  int64_t i;
+  int pass;
+  if (!ka || !kb || !ia || !ib) { free(ka); free(kb); free(ia); free(ib); return -1; }
+  for (i = 0; i < n; i++) { ka[i] = (uint32_t)m1[i] ^ 0x80000000u; ia[i] = i; }
+  for (pass = 0; pass < 4; pass++) {
+    int64_t cnt[257];
+    int sh = 8 * pass, d;
+    uint32_t* tk;
+    int64_t* ti;
+    memset(cnt, 0, sizeof cnt);
+    for (i = 0; i < n; i++) cnt[((ka[i] >> sh) & 255) + 1]++;
+    for (d = 0; d < 256; d++) cnt[d + 1] += cnt[d];
+    for (i = 0; i < n; i++) {
+      int64_t o = cnt[(ka[i] >> sh) & 255]++;
+      kb[o] = ka[i];
+      ib[o] = ia[i];
+    }
+    tk = ka; ka = kb; kb = tk;
+    ti = ia; ia = ib; ib = ti;
+  }
+  for (i = 0; i < n; i++) {
+    om1[i] = m1[ia[i]];
+    om2[i] = m2[ia[i]];
+    oclip[i] = clip[ia[i]];
+  }
+  free(ka); free(kb); free(ia); free(ib);
+  return n;
+}
+
+static int64_t lower_bound32(const int32_t* a, int64_t n, int64_t v) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    int64_t mid = lo + ((hi - lo) >> 1);
+    if ((int64_t)a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+typedef struct {
+  const int32_t *m1s, *m2s, *clip, *tiekey;
+  int64_t nrows;
+  int32_t nclips;
+  const double *q1, *q2;
+  const int64_t* qoff;
+  int32_t nq, coefs, low, high, tid, nthreads;
+  double tole;
+  int32_t *winner, *count;
+} sorted_arg;
+
+static void* sorted_worker(void* p) {
+  sorted_arg* a = (sorted_arg*)p;
+  int32_t* score = (int32_t*)calloc((size_t)(a->nclips > 0 ? a->nclips : 1), sizeof(int32_t));
+  int32_t* stamp = (int32_t*)calloc((size_t)(a->nclips > 0 ? a->nclips : 1), sizeof(int32_t));
+  int32_t* touched = (int32_t*)malloc(sizeof(int32_t) * (size_t)(a->nclips > 0 ? a->nclips : 1));
+  int32_t q, c, k;
+  int32_t epoch = 0;
+  for (q = a->tid; q < a->nq; q += a->nthreads) {
+    int64_t f;
+    int32_t nt = 0, best = -1;
+    for (f = a->qoff[q]; f < a->qoff[q + 1]; f++) {
+      int64_t L1, U1, L2 = 0, U2 = 0, r, lo, hi;
+      int has2;
+      epoch++;
+      if (!frame_box(a->q1[f], a->q2[f], a->coefs, a->tole, a->low, a->high, &L1, &U1, &has2, &L2, &U2)) continue;
+      lo = lower_bound32(a->m1s, a->nrows, L1);
+      hi = lower_bound32(a->m1s, a->nrows, U1 + 1);
+      for (r = lo; r < hi; r++) {
+        if (a->m1s[r] == TFO_NULL) continue; /* NULL compares false */
+        if (has2 && (a->m2s[r] == TFO_NULL || a->m2s[r] < L2 || a->m2s[r] > U2)) continue;
+        c = a->clip[r];
+        if (stamp[c] != epoch) { /* GROUP BY audio_uuid: at most 1 per clip per frame */
+          stamp[c] = epoch;
+          if (!score[c]++) touched[nt++] = c;
+        }
+      }
+    }
+    for (k = 0; k < nt; k++) { /* max count, ties to the greatest uuid (tiekey = uuid rank) */
+      c = touched[k];
+      if (best < 0 || score[c] > score[best] || (score[c] == score[best] && a->tiekey[c] > a->tiekey[best])) best = c;
+    }
+    a->winner[q] = best;
+    a->count[q] = best >= 0 ? score[best] : 0;
+    for (k = 0; k < nt; k++) score[touched[k]] = 0;
+  }
+  free(score); free(stamp); free(touched);
+  return NULL;
+}
+
+int tfo_search_sorted_batch(const int32_t* m1s, const int32_t* m2s, const int32_t* row_clip, int64_t nrows,
+                            const int32_t* tiekey, int32_t nclips, const double* q1, const double* q2,
+                            const int64_t* qoff, int32_t nq, int coefs, double tolerance, int low, int high,
+                            int32_t* winner, int32_t* match_count, int nthreads) {
+  pthread_t* th;
+  sorted_arg* args;
+  int i;
+  if (coefs < 1 || coefs > TFO_COEFS) { /* fp_handler.c:247-250 */
+    for (i = 0; i < nq; i++) { winner[i] = -1; match_count[i] = 0; }
+    return 0;
+  }
+  if (nthreads < 1) nthreads = 1;
+  th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
+  args = (sorted_arg*)malloc(sizeof(sorted_arg) * (size_t)nthreads);
+  for (i = 0; i < nthreads; i++) {
+    sorted_arg a = {m1s, m2s, row_clip, tiekey, nrows, nclips, q1, q2, qoff, nq, coefs, low, high, i, nthreads,
+                    tolerance < 0 ? 0.001 : tolerance, winner, match_count};
+    args[i] = a;
+    pthread_create(&th[i], NULL, sorted_worker, &args[i]);
+  }
+  for (i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+  free(th);
+  free(args);
+  return 0;
 }

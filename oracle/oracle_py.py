@@ -58,6 +58,12 @@ def lib():
                                  C.c_void_p, C.c_void_p, C.c_int32, C.c_int, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.tfo_search.restype = C.c_int
+        L.tfo_sort_rows.argtypes = [C.c_void_p] * 3 + [C.c_int64] + [C.c_void_p] * 3
+        L.tfo_sort_rows.restype = C.c_int64
+        L.tfo_search_sorted_batch.argtypes = ([C.c_void_p] * 3 + [C.c_int64, C.c_void_p, C.c_int32] + [C.c_void_p] * 3
+                                              + [C.c_int32, C.c_int, C.c_double, C.c_int, C.c_int, C.c_void_p,
+                                                 C.c_void_p, C.c_int])
+        L.tfo_search_sorted_batch.restype = C.c_int
         L.tfo_fmt6.argtypes = [C.c_double]
         L.tfo_fmt6.restype = C.c_int64
         _lib = L
@@ -157,6 +163,38 @@ def search(m1, m2, row_clip, uuids, q1, q2, coefs=1, tolerance=0.001, low=-1, hi
                              q1.ctypes.data, q2.ctypes.data, len(q1), coefs, float(tolerance), int(low), int(high),
                              C.byref(w), C.byref(mc), C.byref(fc))
     return bool(found), w.value, mc.value, fc.value
+
+
+class SortedIndex:
+    """The audio_fingerprint rows ordered by max1 (idx_audio_fingerprint_max1) for searches over
+    large tables; tiekey[clip] = rank of the clip's uuid (greatest wins a tie)."""
+
+    def __init__(self, m1, m2, row_clip, tiekey):
+        m1 = np.ascontiguousarray(m1, np.int32)
+        m2 = np.ascontiguousarray(m2, np.int32)
+        row_clip = np.ascontiguousarray(row_clip, np.int32)
+        n = len(m1)
+        self.m1 = np.empty(n, np.int32)
+        self.m2 = np.empty(n, np.int32)
+        self.clip = np.empty(n, np.int32)
+        if lib().tfo_sort_rows(m1.ctypes.data, m2.ctypes.data, row_clip.ctypes.data, n, self.m1.ctypes.data,
+                               self.m2.ctypes.data, self.clip.ctypes.data) != n:
+            raise MemoryError("tfo_sort_rows")
+        self.tiekey = np.ascontiguousarray(tiekey, np.int32)
+
+    def search_batch(self, q1, q2, qoff, coefs=1, tolerance=0.001, low=-1, high=-1, nthreads=8):
+        """-> (winner clip int32[nq] (-1 = NOTFOUND), match_count int32[nq])."""
+        q1 = np.ascontiguousarray(q1, np.float64)
+        q2 = np.ascontiguousarray(q2, np.float64)
+        qoff = np.ascontiguousarray(qoff, np.int64)
+        nq = len(qoff) - 1
+        w = np.zeros(nq, np.int32)
+        mc = np.zeros(nq, np.int32)
+        lib().tfo_search_sorted_batch(self.m1.ctypes.data, self.m2.ctypes.data, self.clip.ctypes.data, len(self.m1),
+                                      self.tiekey.ctypes.data, len(self.tiekey), q1.ctypes.data, q2.ctypes.data,
+                                      qoff.ctypes.data, nq, coefs, float(tolerance), int(low), int(high),
+                                      w.ctypes.data, mc.ctypes.data, int(nthreads))
+        return w, mc
 
 
 def fmt6(x: float) -> int:

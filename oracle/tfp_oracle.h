@@ -65,6 +65,18 @@ int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, in
                int32_t nqframes, int coefs, double tolerance, int freq_ignore_low,
                int freq_ignore_high, int32_t* winner, int32_t* match_count, int32_t* frame_count);
 
+/* Large tables (configs[2] size): the same search semantics over rows sorted by max1.
+ * tfo_sort_rows orders (m1, m2, clip) by m1 (stable LSD radix sort; returns n or -1).
+ * tfo_search_sorted_batch runs nq queries (frames qoff[q]..qoff[q+1]) over the sorted rows with
+ * a binary search per frame box, on nthreads threads; tiekey[clip] orders clips like their uuid
+ * strings (the greatest wins a tie). winner[q] = clip or -1 (NOTFOUND), match_count[q]. */
+int64_t tfo_sort_rows(const int32_t* m1, const int32_t* m2, const int32_t* clip, int64_t n, int32_t* om1,
+                      int32_t* om2, int32_t* oclip);
+int tfo_search_sorted_batch(const int32_t* m1s, const int32_t* m2s, const int32_t* row_clip, int64_t nrows,
+                            const int32_t* tiekey, int32_t nclips, const double* q1, const double* q2,
+                            const int64_t* qoff, int32_t nq, int coefs, double tolerance, int low, int high,
+                            int32_t* winner, int32_t* match_count, int nthreads);
+
 /* printf("%f") micro-units of x, parsed from the printed string. */
 int64_t tfo_fmt6(double x);
 

@@ -17,6 +17,20 @@ pytestmark = pytest.mark.gpu
 SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
 
 
+def _engine_with(tfp_lib, env):
+    """A fresh engine created with test knobs in the environment (the engine reads them once)."""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return tfp_lib.Engine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
 def _pcm_cases():
     rng = np.random.default_rng(11)
     cases = {
@@ -268,11 +282,11 @@ def test_fingerprint_kernel_variants_bit_exact(engine, oracle, tfp_lib, knob):
     lens = [80000] * 6 + [len(v) for v in _pcm_cases().values()]
     off = np.concatenate([[0], np.cumsum(lens)])
     micro, db = oracle.fingerprint_batch(flat, off, nthreads=8)
-    os.environ[knob[0]] = knob[1]
+    eng = _engine_with(tfp_lib, {knob[0]: knob[1]})  # knobs are read once, at engine creation
     try:
-        fr = engine.fingerprint_batch(flat, off)
+        fr = eng.fingerprint_batch(flat, off)
     finally:
-        del os.environ[knob[0]]
+        eng.close()
     _assert_frames_equal(fr, micro, db)
 
 
@@ -333,18 +347,18 @@ def test_vote_paths_vs_oracle(engine, oracle, tfp_lib, spread, class_max):
     """The coefs=1 vote: the pattern-class path (few used keys, Ku <= 10), the GEMM with A in
     registers (Kp <= 128) and the streamed GEMM (larger Kp). TFP_VOTE_CLASS_MAX=-1 forces the
     GEMM for every batch. Same (uuid, match_count) as the oracle's per-query search."""
-    uuids, m1, m2, clip = _many_key_index(engine, 700, spread, 17 + spread)
+    eng = _engine_with(tfp_lib, {"TFP_VOTE_CLASS_MAX": class_max})  # read once, at engine creation
+    uuids, m1, m2, clip = _many_key_index(eng, 700, spread, 17 + spread)
     rng = np.random.default_rng(spread)
     nq, lens = 40, rng.integers(1, 120, 40)
     qoff = np.concatenate([[0], np.cumsum(lens)])
     k = rng.integers(-spread, spread + 1, qoff[-1])
     q1 = k + rng.choice([0.2, 0.7, -0.3], qoff[-1]) * np.sign(k + 0.5)  # trunc(q1) == k
     q2 = np.zeros(qoff[-1])
-    os.environ["TFP_VOTE_CLASS_MAX"] = class_max
     try:
-        res, fcs = engine.search_batch(_frames_from_q(q1, q2), qoff, tfp_lib.params(1, 0.001))
+        res, fcs = eng.search_batch(_frames_from_q(q1, q2), qoff, tfp_lib.params(1, 0.001))
     finally:
-        del os.environ["TFP_VOTE_CLASS_MAX"]
+        eng.close()
     nfound = 0
     for i in range(nq):
         a, b = qoff[i], qoff[i + 1]

@@ -106,3 +106,61 @@ def test_oracle_batch_equals_single(oracle):
     micro, db = oracle.fingerprint_batch(pcm, off, nthreads=3)
     single = np.concatenate([oracle.fingerprint(c)[2] for c in clips])
     assert np.array_equal(micro, single)
+
+
+def test_sorted_index_search_matches_sqlite_golden(oracle):
+    """The sorted-index batch search (large tables) gives the SQLite-pinned results too: every
+    golden scenario, every query, ties by uuid rank."""
+    g = load_golden()
+    n = 0
+    for s in g["scenarios"]:
+        if not s["uuids"]:
+            continue
+        order = sorted(range(len(s["uuids"])), key=lambda c: s["uuids"][c])
+        rank = np.empty(len(order), np.int32)
+        rank[order] = np.arange(len(order))
+        idx = oracle.SortedIndex(s["m1"], s["m2"], s["clip"], rank)
+        assert np.all(np.diff(idx.m1.astype(np.int64)) >= 0)
+        groups = {}
+        for q in s["queries"]:  # one batch per parameter set
+            groups.setdefault((q["coefs"], q["tol"], q["low"], q["high"]), []).append(q)
+        for (coefs, tol, low, high), qs in groups.items():
+            q1 = np.concatenate([_q(q["q1"]) for q in qs]) if qs else np.zeros(0)
+            q2 = np.concatenate([_q(q["q2"]) for q in qs])
+            qoff = np.concatenate([[0], np.cumsum([len(q["q1"]) for q in qs])])
+            w, mc = idx.search_batch(q1, q2, qoff, coefs, tol if tol is not None else float("nan"), low, high, nthreads=3)
+            for i, q in enumerate(qs):
+                got = {"audio_uuid": s["uuids"][w[i]], "match_count": int(mc[i]), "frame_count": len(q["q1"])} \
+                    if w[i] >= 0 else None
+                assert got == q["expect"], (s["name"], coefs, tol, low, high)
+                n += 1
+    assert n > 900
+
+
+def test_sorted_index_search_equals_linear_scan(oracle):
+    """Random tables with NULL rows, coefs 1 and 2, ignore filters: sorted search == row scan."""
+    rng = np.random.default_rng(17)
+    nclips, nrows = 300, 40000
+    m1 = rng.integers(-5_000_000, 5_000_000, nrows).astype(np.int32)
+    m1[rng.random(nrows) < 0.05] = oracle.NULL_MICRO
+    m2 = rng.integers(-3_000_000, 3_000_000, nrows).astype(np.int32)
+    m2[rng.random(nrows) < 0.05] = oracle.NULL_MICRO
+    clip = rng.integers(0, nclips, nrows).astype(np.int32)
+    uuids = ["%08x-0000-4000-8000-%012x" % (int(rng.integers(1 << 30)), c) for c in range(nclips)]
+    order = sorted(range(nclips), key=lambda c: uuids[c])
+    rank = np.empty(nclips, np.int32)
+    rank[order] = np.arange(nclips)
+    idx = oracle.SortedIndex(m1, m2, clip, rank)
+    nq = 24
+    lens = rng.integers(0, 40, nq)
+    qoff = np.concatenate([[0], np.cumsum(lens)])
+    q1 = rng.uniform(-5.5, 5.5, qoff[-1])
+    q2 = rng.uniform(-3.5, 3.5, qoff[-1])
+    q1[rng.random(len(q1)) < 0.05] = np.inf
+    for coefs, tol, low, high in [(1, 0.001, -1, -1), (1, 0.4, -1, -1), (2, 0.3, -1, -1), (2, 0.05, 1, 3),
+                                  (1, -1.0, 1, -1), (3, 0.1, -1, -1)]:
+        w, mc = idx.search_batch(q1, q2, qoff, coefs, tol, low, high, nthreads=4)
+        for i in range(nq):
+            a, b = qoff[i], qoff[i + 1]
+            found, ww, mm, _ = oracle.search(m1, m2, clip, uuids, q1[a:b], q2[a:b], coefs, tol, low, high)
+            assert (w[i] >= 0) == found and (not found or (w[i], mc[i]) == (ww, mm)), (i, coefs, tol)
