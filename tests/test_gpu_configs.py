@@ -1,0 +1,305 @@
+"""GPU parity at the BASELINE.json configs' own sizes.
+
+Each test runs the device path the bench times, at the bench's size, and checks every result
+against the CPU oracle (oracle/, the reference path restated; reference semantics
+src/fp_handler.c:287-374 for the search, :577-671 for the fingerprint):
+
+  configs[1]  1,024 x 30 s clips in one launch: every one of the 960,512 stored (m1, m2) rows,
+              i.e. the persistent kernel's multi-tile loop (~29 tiles per wave) and its
+              next-tile prefetch, which smaller batches never reach.
+  configs[2]  the 100k-clip DB (93.8 M rows) and 5 s queries: the batch vote (class path and
+              the Bt GEMM over 98 1,024-clip chunks) and the batch-1 path, against the oracle's
+              sorted-index search over the same rows.
+  vote chunks ties straddling 1,024-clip chunk boundaries (the GEMM's cross-chunk max), with
+              the pattern-class vote and with the GEMM forced (TFP_VOTE_CLASS_MAX=-1).
+  configs[4]  512 live channels: one tick's results on sampled channels vs the oracle on each
+              channel's last window.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
+HOP = 256
+ORACLE_THREADS = 16  # the GPU box's CPU share
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+def _uuid_of(g: int) -> str:
+    """bench.py's deterministic uuid per global clip id."""
+    a = (g * 0x9E3779B97F4A7C15 + 0x7153A1) & (2**64 - 1)
+    b = (a * 0xBF58476D1CE4E5B9 + g) & (2**64 - 1)
+    s = "%032x" % ((a << 64) | b)
+    s = s[:12] + "4" + s[13:16] + "89ab"[int(s[16], 16) & 3] + s[17:]
+    return "%s-%s-%s-%s-%s" % (s[:8], s[8:12], s[12:16], s[16:20], s[20:32])
+
+
+def _engine_with(tfp_lib, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return tfp_lib.Engine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def test_configs1_full_batch_bit_exact(engine, oracle, torch_cuda):
+    """configs[1] as bench.py runs it: 1,024 x 30 s clips synthesised in HBM, one plan, one
+    tfp_fingerprint_device launch (+ finish_db). All 960,512 rows == the oracle's, bit for bit;
+    the frame values (q1, q2) of a second launch with d_db equal glibc's to the last bit or 1 ulp."""
+    torch = torch_cuda
+    nclips, n = 1024, 8000 * 30
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    pcm = torch.empty((nclips, n), dtype=torch.int16, device=dev)
+    engine.synth_device(SEED_DB, range(nclips), n, pcm.data_ptr(), stream=stream)
+    off = np.arange(nclips + 1, dtype=np.int64) * n
+    plan = engine.plan(off)
+    assert plan.nframes == 960512
+    micro = torch.empty((plan.nframes, 2), dtype=torch.int32, device=dev)
+    engine.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, stream)
+    torch.cuda.synchronize()
+    host = pcm.cpu().numpy().reshape(-1)
+    exp, db = oracle.fingerprint_batch(host, off, nthreads=ORACLE_THREADS)
+    got = micro.cpu().numpy()
+    bad = np.nonzero((got != exp).any(axis=1))[0]
+    assert len(bad) == 0, ("frames differing", len(bad), bad[:10])
+    # with the frame values (the query path's d_db)
+    micro.fill_(0)
+    qv = torch.empty((plan.nframes, 2), dtype=torch.float64, device=dev)
+    engine.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), qv.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(micro.cpu().numpy(), exp)
+    q = qv.cpu().numpy()
+    same = (q == db) | (np.isinf(q) & np.isinf(db))
+    assert np.all(same | (np.abs(q - db) <= np.abs(np.spacing(db))))
+
+
+def _chunk_tie_index(eng, nclips, nkeys, seed):
+    """nclips clips whose uuids sort like their numbers (column = uuid rank = clip number).
+    Groups g = 0..3 are the column pairs (1024 (g+1) - 1, 1024 (g+1)) on either side of a
+    1,024-clip vote chunk boundary, each with a row in every key's box but key g's; every other
+    clip has rows in a random ~30 % of the keys' boxes, never in more than two of the boxes of
+    keys 0..3 (so it cannot reach a group's count). Rows are added in shuffled order."""
+    rng = np.random.default_rng(seed)
+    uuids = ["%08x-0000-4000-8000-%012x" % (c, c) for c in range(nclips)]
+    group = {}
+    for g in range(4):
+        group[1024 * (g + 1) - 1] = g
+        group[1024 * (g + 1)] = g
+    m1s, m2s, clips = [], [], []
+    for c in range(nclips):
+        if c in group:
+            keys = [k for k in range(nkeys) if k != group[c]]
+        else:
+            drop = set(rng.choice(4, 2, replace=False).tolist())
+            keys = [k for k in range(nkeys) if k not in drop and rng.random() < 0.3]
+        keys = np.asarray(keys, np.int64)
+        m1s.append((keys * 1000000 + rng.integers(-900, 901, len(keys))).astype(np.int32))
+        m2s.append(rng.integers(-5000000, 5000000, len(keys)).astype(np.int32))
+        clips.append(np.full(len(keys), c, np.int32))
+    order = rng.permutation(nclips)
+    eng.index_clear()
+    fo = np.concatenate([[0], np.cumsum([len(m1s[c]) for c in order])])
+    eng.index_add_batch([uuids[c] for c in order], fo, np.concatenate([m1s[c] for c in order]),
+                        np.concatenate([m2s[c] for c in order]))
+    return uuids, np.concatenate(m1s), np.concatenate(m2s), np.concatenate(clips)
+
+
+@pytest.mark.parametrize("class_max", ["10", "-1"])
+@pytest.mark.parametrize("nkeys", [6, 12])
+def test_vote_ties_across_chunk_boundaries(oracle, tfp_lib, class_max, nkeys):
+    """>= 4 GEMM chunks (4,200 clips). Query q has frames on every group key but e (0..3), so
+    only group e reaches the query's full count: its two columns tie across the chunk boundary
+    and the later one (greater uuid) must win. nkeys = 6 takes the pattern-class vote unless
+    TFP_VOTE_CLASS_MAX=-1 forces the GEMM; nkeys = 12 always takes the GEMM."""
+    eng = _engine_with(tfp_lib, {"TFP_VOTE_CLASS_MAX": class_max})
+    try:
+        nclips = 4200
+        uuids, m1, m2, clip = _chunk_tie_index(eng, nclips, nkeys, 5 + nkeys)
+        rng = np.random.default_rng(nkeys)
+        q1s, qoff, expect_col = [], [0], []
+        for i in range(48):
+            e = i % 4 if i % 6 else int(rng.integers(4))
+            keys = [k for k in range(nkeys) if k != e and (k < 4 or rng.random() < 0.8)]
+            cnt = rng.integers(1, 6, len(keys))
+            q = np.repeat(np.asarray(keys, np.float64), cnt) + rng.choice([0.2, 0.6], int(cnt.sum()))
+            q1s.append(rng.permutation(q))
+            qoff.append(qoff[-1] + len(q))
+            expect_col.append(1024 * (e + 1))
+        q1 = np.concatenate(q1s)
+        q2 = np.zeros_like(q1)
+        fr = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                         ("q1", "<f8"), ("q2", "<f8")]))
+        fr["q1"], fr["q2"] = q1, q2
+        res, fcs = eng.search_batch(fr, np.asarray(qoff), tfp_lib.params(1, 0.001))
+        at_boundary = 0
+        for i in range(len(qoff) - 1):
+            a, b = qoff[i], qoff[i + 1]
+            found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[a:b], q2[a:b], 1, 0.001, -1, -1)
+            exp = (uuids[w], mc) if found else None
+            got = None if res[i] is None else (res[i]["audio_uuid"], res[i]["match_count"])
+            assert got == exp, (i, class_max, nkeys)
+            assert fcs[i] == fc == b - a
+            at_boundary += found and w == expect_col[i]
+        assert at_boundary == len(qoff) - 1  # the construction put every winner on a boundary
+    finally:
+        eng.close()
+
+
+def _enroll_db(eng, torch, dev, stream, ids, keep_rows=True, chunk=2048):
+    """bench.py's enrolment (synth -> fingerprint_device -> index_add_device, 2,048 clips at a
+    time) that also returns the rows it enrolled (host int32 [nclips * 938, 2])."""
+    n_db = 8000 * 30
+    nf_db = (n_db + HOP - 1) // HOP
+    buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
+    micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
+    rows = np.empty((len(ids) * nf_db, 2), np.int32) if keep_rows else None
+    eng.index_clear()
+    for s in range(0, len(ids), chunk):
+        part = ids[s:s + chunk]
+        k = len(part)
+        plan = eng.plan(np.arange(k + 1, dtype=np.int64) * n_db)
+        eng.synth_device(SEED_DB, part, n_db, buf.data_ptr(), stream=stream)
+        eng.fingerprint_device(plan, buf.data_ptr(), micro.data_ptr(), 0, stream)
+        eng.index_add_device([_uuid_of(g) for g in part], np.arange(k + 1, dtype=np.int64) * nf_db, micro.data_ptr(),
+                             stream)
+        if keep_rows:
+            torch.cuda.synchronize()
+            rows[s * nf_db:(s + k) * nf_db] = micro[:k * nf_db].cpu().numpy()
+    eng.index_commit()
+    torch.cuda.synchronize()
+    del buf, micro
+    torch.cuda.empty_cache()
+    return rows
+
+
+def _c3_queries(nq, db_clips, seed=SEED_Q):
+    """bench.py's configs[2] query mix: 75 % 5 s excerpts of DB clips at 256-aligned offsets,
+    25 % unrelated audio."""
+    rng = np.random.default_rng(seed)
+    n_db, qn = 8000 * 30, 8000 * 5
+    spec = []
+    for i in range(nq):
+        if i % 4 != 3:
+            spec.append((SEED_DB, int(rng.integers(db_clips)), 256 * int(rng.integers(0, (n_db - qn) // HOP))))
+        else:
+            spec.append((SEED_Q, i, 0))
+    return spec
+
+
+def test_configs2_full_db_vs_sorted_oracle(engine, oracle, tfp_lib, torch_cuda):
+    """configs[2]: 100,000 x 30 s clips (93.8 M rows) enrolled on the device as bench.py does,
+    5 s queries against all of them. Rows: a sample of 256 clips re-fingerprinted by the oracle.
+    Search: the batch device path (vote; tol 0.001 and 0.1) and the batch-1 host path, each
+    (count, uuid rank) == the oracle's sorted-index search over the same 93.8 M rows."""
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    db_clips, n_db, qn = 100_000, 8000 * 30, 8000 * 5
+    nf_db = (n_db + HOP - 1) // HOP
+    rows = _enroll_db(engine, torch, dev, stream, list(range(db_clips)))
+    nrows, nc = engine.index_stats()
+    assert nc == db_clips and nrows == db_clips * nf_db
+    # the enrolled rows are the oracle's fingerprints (sampled: the full-size batch test above
+    # covers the kernel at this launch size)
+    rng = np.random.default_rng(1)
+    sample = np.sort(rng.choice(db_clips, 256, replace=False))
+    pcm = tfp_lib.synth_pcm(SEED_DB, sample.tolist(), n_db)
+    exp, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(len(sample) + 1) * n_db, nthreads=ORACLE_THREADS,
+                                      want_db=False)
+    got = np.concatenate([rows[c * nf_db:(c + 1) * nf_db] for c in sample])
+    assert np.array_equal(got, exp)
+    # oracle index over the same rows; tie key = rank of the uuid among all clips
+    uuids = [_uuid_of(g) for g in range(db_clips)]
+    order = np.argsort(np.asarray(uuids))
+    rank = np.empty(db_clips, np.int32)
+    rank[order] = np.arange(db_clips, dtype=np.int32)
+    idx = oracle.SortedIndex(rows[:, 0], rows[:, 1], np.repeat(np.arange(db_clips, dtype=np.int32), nf_db), rank)
+    del rows
+    spec = _c3_queries(96, db_clips)
+    qpcm = np.stack([tfp_lib.synth_pcm(sd, [c], qn, offsets=[o])[0] for sd, c, o in spec])
+    nfq = (qn + HOP - 1) // HOP
+    qdb = np.concatenate([oracle.fingerprint(qpcm[i])[1] for i in range(len(spec))])
+    qoff = np.arange(len(spec) + 1, dtype=np.int64) * nfq
+    d_q = torch.from_numpy(qpcm).to(dev)
+    qplan = engine.plan(np.arange(len(spec) + 1, dtype=np.int64) * qn)
+    for tol in (0.001, 0.1):
+        w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, 1, tol, nthreads=ORACLE_THREADS)
+        keys = torch.zeros(len(spec), dtype=torch.int64, device=dev)
+        engine.search_device(qplan, d_q.data_ptr(), tfp_lib.params(1, tol), keys.data_ptr(), stream)
+        torch.cuda.synchronize()
+        k = keys.cpu().numpy().view(np.uint64)
+        expk = np.where(w >= 0, (mc.astype(np.uint64) << np.uint64(32)) | rank[np.maximum(w, 0)].astype(np.uint64), 0)
+        assert np.array_equal(k, expk.astype(np.uint64)), (tol, np.nonzero(k != expk)[0][:8])
+        assert (w >= 0).sum() >= len(spec) // 4
+    # batch-1 (small path), host PCM in -> result out, as the dialplan application calls it
+    w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, 1, 0.001, nthreads=ORACLE_THREADS)
+    for i in range(16):
+        res, fc = engine.search_pcm_batch(qpcm[i], [0, qn], tfp_lib.params(1, 0.001))
+        got = None if res[0] is None else (res[0]["audio_uuid"], res[0]["match_count"])
+        assert got == ((uuids[w[i]], int(mc[i])) if w[i] >= 0 else None), i
+        assert fc[0] == nfq
+    engine.index_clear()
+
+
+def test_configs4_512_channels_one_tick(engine, oracle, tfp_lib, torch_cuda):
+    """configs[4]: 512 live channels, 160-sample ticks, 3 s windows (94 frames). After the windows
+    fill, each tick's result of 32 sampled channels == the oracle's search on that channel's last
+    24,000 samples (the recording the dialplan application would have searched)."""
+    torch = torch_cuda
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    db_clips, n_db, W, tick = 3000, 8000 * 30, 24000, 160
+    nf_db = (n_db + HOP - 1) // HOP
+    rows = _enroll_db(engine, torch, dev, stream, list(range(db_clips)))
+    uuids = [_uuid_of(g) for g in range(db_clips)]
+    order = np.argsort(np.asarray(uuids))
+    rank = np.empty(db_clips, np.int32)
+    rank[order] = np.arange(db_clips, dtype=np.int32)
+    idx = oracle.SortedIndex(rows[:, 0], rows[:, 1], np.repeat(np.arange(db_clips, dtype=np.int32), nf_db), rank)
+    nch, ticks = 512, 3
+    rng = np.random.default_rng(44)
+    span = W + ticks * tick
+    src = [int(rng.integers(db_clips)) for _ in range(nch)]
+    offs = [256 * int(rng.integers(0, (n_db - span) // HOP)) + int(rng.integers(0, 4)) * 40 for _ in range(nch)]
+    pcm = tfp_lib.synth_pcm(SEED_DB, src, span, offsets=offs)
+    for c in range(3, nch, 4):  # unrelated audio on every 4th channel
+        pcm[c] = tfp_lib.synth_pcm(SEED_Q + 7, [c], span)[0]
+    st = tfp_lib.Stream(engine, nch, W)
+    p = tfp_lib.params(1, 0.001)
+    for t in range(W // tick):
+        st.push(np.ascontiguousarray(pcm[:, t * tick:(t + 1) * tick]))
+    checked = found = 0
+    for t in range(ticks):
+        s0 = W + t * tick
+        res = st.push(np.ascontiguousarray(pcm[:, s0:s0 + tick]), p)
+        chans = rng.choice(nch, 32, replace=False)
+        qdb = np.concatenate([oracle.fingerprint(pcm[c, s0 + tick - W:s0 + tick])[1] for c in chans])
+        nfw = (W + HOP - 1) // HOP
+        w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], np.arange(len(chans) + 1) * nfw, 1, 0.001,
+                                 nthreads=ORACLE_THREADS)
+        for i, c in enumerate(chans):
+            exp = {"audio_uuid": uuids[w[i]], "match_count": int(mc[i]), "frame_count": nfw} if w[i] >= 0 else None
+            assert res[c] == exp, (t, int(c))
+            checked += 1
+            found += w[i] >= 0
+    assert checked == 96 and found > 20
+    st.close()
+    engine.index_clear()

@@ -99,3 +99,95 @@ def test_search_q_device_equals_search_device(engine, tfp_lib, torch_cuda):
         torch.cuda.synchronize()
         assert torch.equal(k1, k2)
     assert int((k2 != 0).sum()) > 0
+
+
+def test_tiebreak_override_covers_every_live_clip(engine, tfp_lib):
+    """A clip added after tfp_index_set_tiebreak has no global key: the next search fails with
+    TFP_E_ARG instead of giving it a local rank that may collide; duplicate keys fail too."""
+    rng = np.random.default_rng(2)
+    engine.index_clear()
+    for c in range(4):
+        engine.index_add("u%d" % c, rng.integers(0, 9, 20) * 1000000, rng.integers(0, 9, 20) * 1000000)
+    engine.set_tiebreak(np.array([10, 40, 20, 30], np.int32))
+    engine.index_commit()
+    engine.index_add("u4", np.zeros(5, np.int32), np.zeros(5, np.int32))
+    with pytest.raises(tfp_lib.TfpError):
+        engine.index_commit()
+    engine.set_tiebreak(np.array([10, 40, 20, 30, 40], np.int32))  # duplicate 40
+    with pytest.raises(tfp_lib.TfpError):
+        engine.index_commit()
+    engine.set_tiebreak(np.array([10, 40, 20, 30, 50], np.int32))
+    engine.index_commit()
+    assert engine.uuid_of_key(50) == "u4"
+    engine.set_tiebreak(np.zeros(0, np.int32))  # cleared: uuid ranks again
+    engine.index_commit()
+    assert engine.uuid_of_key(4) == "u4"
+    engine.index_clear()
+
+
+def test_remove_readd_cycles_compact_staging(engine, oracle, tfp_lib):
+    """Delete / re-enrol cycles (tfp_index_remove + tfp_index_add) keep the search exact while the
+    staging rows of removed clips are compacted away."""
+    rng = np.random.default_rng(8)
+    engine.index_clear()
+    nclips, nrows = 40, 3000
+    rows = {}
+    for c in range(nclips):
+        rows[c] = ((rng.integers(-3, 4, nrows) * 1000000 + rng.integers(-900, 901, nrows)).astype(np.int32),
+                   rng.integers(-5000000, 5000000, nrows).astype(np.int32))
+        engine.index_add("clip-%03d" % c, *rows[c])
+    for cycle in range(30):  # ~30 x 20 x 3000 rows removed: several compactions
+        for c in rng.choice(nclips, 20, replace=False):
+            engine.index_remove("clip-%03d" % c)
+            rows[c] = ((rng.integers(-3, 4, nrows) * 1000000 + rng.integers(-900, 901, nrows)).astype(np.int32),
+                       rng.integers(-5000000, 5000000, nrows).astype(np.int32))
+            engine.index_add("clip-%03d" % c, *rows[c])
+        if cycle % 10 == 9:
+            uuids = ["clip-%03d" % c for c in range(nclips)]
+            m1 = np.concatenate([rows[c][0] for c in range(nclips)])
+            m2 = np.concatenate([rows[c][1] for c in range(nclips)])
+            clip = np.repeat(np.arange(nclips), nrows)
+            q1 = rng.integers(-3, 4, 50) + 0.4
+            fr = np.zeros(50, np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                        ("q1", "<f8"), ("q2", "<f8")]))
+            fr["q1"] = q1
+            res, _ = engine.search_batch(fr, [0, 50], tfp_lib.params(1, 0.001))
+            found, w, mc, _ = oracle.search(m1, m2, clip, uuids, q1, np.zeros(50), 1, 0.001)
+            assert (res[0]["audio_uuid"], res[0]["match_count"]) == (uuids[w], mc)
+            for c in (0, 17, 39):
+                a, b = engine.index_rows("clip-%03d" % c)
+                assert np.array_equal(a, rows[c][0]) and np.array_equal(b, rows[c][1])
+    assert engine.index_stats() == (nclips * nrows, nclips)
+    engine.index_clear()
+
+
+def test_scan_path_on_caller_stream_then_host_search(engine, tfp_lib, torch_cuda):
+    """tfp_search_q_device with coefs=2 (scan path) on a torch stream, immediately followed by a
+    host search on the engine's own stream: the shared scratch must not be overwritten while the
+    first search still runs (each result equals the same search run alone)."""
+    torch = torch_cuda
+    nclips, n = 32, 8000 * 10
+    pcm = tfp_lib.synth_pcm(0x7153A1, range(nclips), n)
+    fr = engine.fingerprint_batch(pcm.reshape(-1), np.arange(nclips + 1) * n)
+    nf = fr.shape[0] // nclips
+    engine.index_clear()
+    engine.index_add_batch(["s%03d" % c for c in range(nclips)], np.arange(nclips + 1) * nf, fr["m1"], fr["m2"])
+    nq, qn = 16, 8000 * 3
+    q = np.stack([pcm[i % nclips, 256 * i: 256 * i + qn] for i in range(nq)])
+    qfr = engine.fingerprint_batch(q.reshape(-1), np.arange(nq + 1) * qn)
+    nfq = qfr.shape[0] // nq
+    d_q = torch.from_numpy(np.stack([qfr["q1"], qfr["q2"]], 1).copy()).cuda()
+    p2 = tfp_lib.params(2, 0.5)
+    alone = torch.zeros(nq, dtype=torch.int64, device="cuda")
+    side = torch.cuda.Stream()
+    engine.search_q_device(d_q.data_ptr(), np.arange(nq + 1) * nfq, p2, alone.data_ptr(), side.cuda_stream)
+    torch.cuda.synchronize()
+    ref_host, _ = engine.search_batch(qfr, np.arange(nq + 1) * nfq, tfp_lib.params(1, 0.3))
+    for _ in range(5):
+        keys = torch.zeros(nq, dtype=torch.int64, device="cuda")
+        engine.search_q_device(d_q.data_ptr(), np.arange(nq + 1) * nfq, p2, keys.data_ptr(), side.cuda_stream)
+        host, _ = engine.search_batch(qfr, np.arange(nq + 1) * nfq, tfp_lib.params(1, 0.3))
+        torch.cuda.synchronize()
+        assert torch.equal(keys, alone)
+        assert host == ref_host
+    engine.index_clear()
