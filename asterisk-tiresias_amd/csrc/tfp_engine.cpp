@@ -129,6 +129,15 @@ struct tfp_engine {
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
+  // general path: clip-set cache at tolerance cell_tol (tfp_scan.hip), built on first use per
+  // index version and tolerance
+  CellCache cells;
+  double cell_tol = 0.0;
+  bool cell_fresh = false;
+  // scan scratch: stamp / score / touched nq x ncols int32 each, tcnt nq int32; kept all-zero
+  // by the scan kernels themselves
+  DevBuf touched, tcnt;
+  size_t scan_zeroed = 0;  // bytes of stamp / score / touched known to be zero
   // launch configuration and test/A-B knobs, read once at engine creation
   FpLaunchCfg fpcfg;
   int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
@@ -459,7 +468,8 @@ int rebuild(tfp_engine* e) {
     HIPCHK(e, e->cols.reserve(4));
   }
   e->dirty = false;
-  e->rng_valid = false;  // the key-range cache follows the index
+  e->rng_valid = false;  // the key-range and clip-set caches follow the index
+  e->cell_fresh = false;
   return TFP_OK;
 }
 
@@ -470,6 +480,20 @@ int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
   HIPCHK(e, launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, tole, e->rng_all.as<int64_t>(), s));
   e->rng_tol = tole;
   e->rng_valid = true;
+  return TFP_OK;
+}
+
+// The general path's clip-set cache at tolerance tole (after ensure_ranges at tole).
+int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
+  if (e->cell_fresh && memcmp(&e->cell_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  std::vector<int64_t> rng(2 * kKeyRange), off(kKeyRange + 1, 0);
+  HIPCHK(e, hipMemcpyAsync(rng.data(), e->rng_all.p, sizeof(int64_t) * rng.size(), hipMemcpyDeviceToHost, s));
+  HIPCHK(e, hipStreamSynchronize(s));
+  for (int k = 0; k < kKeyRange; k++) off[k + 1] = off[k] + std::max<int64_t>(0, rng[2 * k + 1] - rng[2 * k]);
+  HIPCHK(e, e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), e->ncols,
+                           e->nrows, tole, s));
+  e->cell_tol = tole;
+  e->cell_fresh = true;
   return TFP_OK;
 }
 
@@ -622,19 +646,29 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }
   if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
-    // general path, query chunks bounded to ~512 MB of stamp+score scratch
-    const int32_t Cp = C;
-    int64_t chunk = (int64_t)(512ll << 20) / (8ll * Cp);
-    chunk = std::max<int64_t>(4, std::min<int64_t>(chunk, nq));
-    HIPCHK(e, e->stamp.reserve(sizeof(int32_t) * chunk * Cp));
-    HIPCHK(e, e->score.reserve(sizeof(int32_t) * chunk * Cp));
+    // general path (tfp_scan.hip): queries in chunks of <= 256 MB of scratch per array
+    if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
+    int64_t chunk = (int64_t)(256ll << 20) / (4ll * C);
+    chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, nq));
+    const size_t bytes = sizeof(int32_t) * chunk * C;
+    if (bytes > e->scan_zeroed || bytes > e->stamp.bytes || bytes > e->score.bytes || bytes > e->touched.bytes ||
+        sizeof(int32_t) * chunk > e->tcnt.bytes) {
+      HIPCHK(e, e->stamp.reserve(bytes));
+      HIPCHK(e, e->score.reserve(bytes));
+      HIPCHK(e, e->touched.reserve(bytes));
+      HIPCHK(e, e->tcnt.reserve(sizeof(int32_t) * chunk));
+      const size_t z = std::min(std::min(e->stamp.bytes, e->score.bytes), e->touched.bytes);
+      HIPCHK(e, hipMemsetAsync(e->stamp.p, 0, z, s));
+      HIPCHK(e, hipMemsetAsync(e->score.p, 0, z, s));
+      HIPCHK(e, hipMemsetAsync(e->tcnt.p, 0, e->tcnt.bytes, s));
+      e->scan_zeroed = z;  // (touched is written before it is read)
+    }
     for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
       const int32_t n = (int32_t)std::min<int64_t>(chunk, nq - q0);
-      HIPCHK(e, hipMemsetAsync(e->stamp.p, 0, sizeof(int32_t) * n * Cp, s));
-      HIPCHK(e, hipMemsetAsync(e->score.p, 0, sizeof(int32_t) * n * Cp, s));
-      HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), (int32_t)q0, n, e->m1s.as<int32_t>(),
-                            e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->tiekey.as<int32_t>(), Cp,
-                            e->stamp.as<int32_t>(), e->score.as<int32_t>(), d_best, s));
+      HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), qo.data(), (int32_t)q0, n,
+                            e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, &e->cells,
+                            e->tiekey.as<int32_t>(), C, e->stamp.as<int32_t>(), e->score.as<int32_t>(),
+                            e->touched.as<int32_t>(), e->tcnt.as<int32_t>(), d_best, s));
     }
   }
   if (d_keys_out) {

@@ -1943,48 +1943,5 @@ hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, Search
 // ---- general path (any coefs / tolerance): one wave per query, frames in order; per frame the
 // rows with max1 in [L1, U1] (binary search on the sorted index) filtered by the max2 box; each
 // clip counts once per frame (stamp), i.e. the per-frame GROUP BY audio_uuid of :353.
-__global__ __launch_bounds__(256) void scan_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff,
-                                                   int32_t q_begin, int32_t nq, const int32_t* __restrict__ m1s,
-                                                   const int32_t* __restrict__ m2s, const int32_t* __restrict__ cols,
-                                                   int64_t R, const int32_t* __restrict__ tiekey, int32_t Cp,
-                                                   int32_t* __restrict__ stamp, int32_t* __restrict__ score,
-                                                   unsigned long long* __restrict__ best) {
-  const int wq = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (wq >= nq) return;
-  const int q = q_begin + wq;
-  int32_t* st = stamp + (int64_t)wq * Cp;
-  int32_t* sc = score + (int64_t)wq * Cp;
-  const int64_t fbeg = qoff[q], fend = qoff[q + 1];
-  for (int64_t i = fbeg; i < fend; i++) {
-    const FrameBox bx = boxes[i];
-    if (!(bx.flags & 1)) continue;
-    const int64_t lo = lower_bound_i32(m1s, R, bx.L1);
-    const int64_t hi = upper_bound_i32(m1s, R, bx.U1);
-    const int32_t tag = (int32_t)(i - fbeg) + 1;
-    for (int64_t rr = lo + lane; rr < hi; rr += 64) {
-      if (bx.flags & 2) {
-        const int32_t v = m2s[rr];
-        if (v == kNullMicro || (int64_t)v < bx.L2 || (int64_t)v > bx.U2) continue;
-      }
-      const int32_t col = cols[rr];
-      const int32_t old = atomicMax(&st[col], tag);
-      if (old < tag) {
-        const int32_t s = atomicAdd(&sc[col], 1) + 1;
-        atomicMax(&best[q], ((unsigned long long)(unsigned)s << 32) | (unsigned)tiekey[col]);
-      }
-    }
-  }
-}
-
-hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
-                       const int32_t* m2s, const int32_t* cols, int64_t R, const int32_t* d_tiekey, int32_t Cp,
-                       int32_t* d_stamp, int32_t* d_score, unsigned long long* d_best, hipStream_t s) {
-  if (nq <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, boxes, d_qoff, q_begin, nq, m1s, m2s, cols, R,
-                     d_tiekey, Cp, d_stamp, d_score, d_best);
-  return hipGetLastError();
-}
-
 }  // namespace tfp
 

@@ -140,8 +140,35 @@ hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, Search
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
                                uint32_t seq, hipStream_t s);
 
-hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, int32_t q_begin, int32_t nq, const int32_t* m1s,
-                       const int32_t* m2s, const int32_t* cols, int64_t R, const int32_t* d_tiekey, int32_t Cp,
-                       int32_t* d_stamp, int32_t* d_score, unsigned long long* d_best, hipStream_t s);
+// General path (coefs = 2 and the vote's fallbacks; tfp_scan.hip). Clip-set cache of one index
+// version and tolerance, built from the key boxes' row ranges (d_rng_all, h_off = host prefix of
+// the box sizes, h_off[kKeyRange] = S rows in all boxes): per (key, clip) group the clip's max2
+// values in the key's box ("points", ascending), and the cell entries (key, cell, clip) of the
+// max2 axis cut into cells of width w. Not built (valid = false) past its limits: then every
+// frame takes the row scan.
+struct CellCache {
+  static constexpr int32_t kMaxCols = 1 << 21;  // clip columns packed in 21 bits
+  int32_t* p_m2 = nullptr;                 // [S] points of each group, ascending
+  uint32_t* g_key = nullptr;               // [n1] key << 21 | column of each group, ascending
+  int32_t* g_beg = nullptr;                // [n1 + 1] first point of each group
+  unsigned long long* e_key = nullptr;     // [n2] key << 52 | cell << 21 | column, ascending
+  int32_t* e_grp = nullptr;                // [n2] group of each entry
+  int64_t S = 0, n1 = 0, n2 = 0, w = 0;
+  bool valid = false;
+  hipError_t build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
+                   int32_t ncols, int64_t nrows, double tole, hipStream_t s);
+  void release();
+  CellCache() = default;
+  CellCache(const CellCache&) = delete;
+  CellCache& operator=(const CellCache&) = delete;
+  ~CellCache() { release(); }
+};
+// Queries [q_begin, q_begin + nq) of the batch (frame boxes from prep_boxes, offsets d_qoff on the
+// device and h_qoff on the host); d_best[q] = (count << 32 | tie key), 0 = NOTFOUND.
+// d_stamp / d_score / d_touched: nq x C int32, d_tcnt: nq int32; all zero on entry and on return.
+hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64_t* h_qoff, int32_t q_begin, int32_t nq,
+                       const int32_t* m1s, const int32_t* m2s, const int32_t* cols, int64_t R, const CellCache* cells,
+                       const int32_t* d_tiekey, int32_t C, int32_t* d_stamp, int32_t* d_score, int32_t* d_touched,
+                       int32_t* d_tcnt, unsigned long long* d_best, hipStream_t s);
 
 }  // namespace tfp

@@ -10,8 +10,11 @@ Also reported (same JSON line):
   roofline      the fingerprint kernel: algorithmic 520 B/fingerprint (512 B PCM in + 8 B out,
                 SURVEY §8d) / average launch time measured with HIP events on the launch stream,
                 against 8 TB/s HBM; traffic = PMC-measured HBM bytes per launch if a profile exists.
+  strong        the same fixed 1,024-clip configs[1] batch split over the N ranks (strong scaling;
+                north_star's >= 6x at 8 GPUs is graded on this leg's value at N = 1 vs 8).
   cpu_baseline  the C oracle (oracle/, the reference path restated; `port`) on a bounded sample of
-                the same workload, all threads of this host.
+                the same workload: the host's CPU share (16 threads on a 1-GPU box; `nproc`
+                reported beside it) and 1 thread.
   match         configs[2]: 4,096 x 5 s queries vs a 100k-clip DB (93.8 M rows), coefs=1,
                 tolerance 0.001; batch-4096 time and batch-1 latency p50/p99 (host PCM in ->
                 result out); with N GPUs the DB is clip-sharded and the per-query keys are
@@ -66,6 +69,10 @@ def main():
     ap.add_argument("--latency-queries", type=int, default=40)
     ap.add_argument("--no-match", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-db-clips", type=int, default=1000,
+                    help="30 s clips in the SQLite DB of the match CPU baseline")
+    ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling leg")
+    ap.add_argument("--no-sweeps", action="store_true", help="skip the match leg's tolerance / coefs sweeps")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--clock-warmup-s", type=float, default=0.25,
                     help="untimed fingerprint steps before the timed region until this much wall time has passed")
@@ -185,27 +192,13 @@ def main():
     }
     del micro
 
+    # ---------------------------------------------------------------- strong scaling (C2 fixed)
+    if not args.no_strong:
+        out["strong"] = run_strong(args, eng, torch, dev, sh, pcm, nclips, n, rank, world, barrier, max_over_ranks)
+
     # ---------------------------------------------------------------- CPU baseline (oracle)
     if rank == 0 and world == 1 and not args.no_cpu:
-        import oracle_py
-        threads = min(os.cpu_count() or 1, 16)
-        k = min(nclips, 4 * threads)
-        host = pcm[:k].cpu().numpy().reshape(-1)
-        off = np.arange(k + 1) * n
-        oracle_py.fingerprint_batch(host[: 2 * n], off[:3], nthreads=1, want_db=False)  # load + tables
-        passes, t1 = 0, time.perf_counter()
-        while True:  # whole passes over the sample until ~cpu_seconds of work
-            oracle_py.fingerprint_batch(host, off, nthreads=threads, want_db=False)
-            passes += 1
-            dt = time.perf_counter() - t1
-            if dt >= args.cpu_seconds:
-                break
-        frames = passes * k * (F // nclips)
-        fps = frames / dt
-        out["cpu_baseline"] = {"value": fps, "unit": "fingerprints/s", "cores": threads, "kind": "port",
-                               "sample": f"{passes} passes over {k} of the {nclips} x {args.seconds} s clips "
-                                         f"({frames} frames), oracle/oracle.c, {threads} threads, {dt:.1f} s"}
-        log(f"cpu baseline {fps:.0f} fp/s on {threads} threads ({dt:.1f} s)")
+        out["cpu_baseline"] = fingerprint_cpu_baseline(args, pcm, nclips, n, F)
     del pcm
     torch.cuda.empty_cache()
 
@@ -219,6 +212,84 @@ def main():
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def run_strong(args, eng, torch, dev, sh, pcm, nclips, n, rank, world, barrier, max_over_ranks):
+    """Strong scaling: the fixed configs[1] batch (nclips clips in total, not per GPU) split over
+    the ranks in contiguous shares; each rank times K launches over its share (taken from the
+    weak leg's PCM, already in HBM), wall time max over ranks, value = the batch's frames per
+    second. At N = 1 this is the weak leg's workload, timed again."""
+    share = [(nclips * r) // world for r in range(world + 1)]
+    b, e = share[rank], share[rank + 1]
+    k = e - b
+    plan = eng.plan(np.arange(k + 1, dtype=np.int64) * n)
+    micro = torch.empty((max(plan.nframes, 1), 2), dtype=torch.int32, device=dev)
+    d_pcm = pcm[b:e].data_ptr() if k else pcm.data_ptr()
+
+    def step():
+        if k:
+            eng.fingerprint_device(plan, d_pcm, micro.data_ptr(), 0, sh)
+    for _ in range(max(args.warmup, 3)):
+        step()
+    torch.cuda.synchronize(dev)
+    t_w = time.perf_counter()
+    while time.perf_counter() - t_w < args.clock_warmup_s:  # clock warm-up, as for the weak leg
+        for _ in range(16):
+            step()
+        torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier()
+    torch.cuda.synchronize(dev)
+    wall = max_over_ranks(time.perf_counter() - t0)
+    total = nclips * ((n + HOP - 1) // HOP)
+    log(f"[rank {rank}] strong: {k} of {nclips} clips, {wall * 1e3 / args.steps:.3f} ms per step (max over ranks)")
+    return {"workload": f"configs[1] fixed: {nclips} x {args.seconds} s clips in total, split over {world} GPU(s)",
+            "scaling": "strong", "clips_total": nclips, "clips_per_gpu_max": max(share[r + 1] - share[r] for r in range(world)),
+            "frames_per_step": total, "ms_per_step": wall * 1e3 / args.steps, "value": total * args.steps / wall,
+            "unit": "fingerprints/s"}
+
+
+def fingerprint_cpu_baseline(args, pcm, nclips, n, F):
+    """The C oracle (the reference's create_audio_fingerprints restated, `port`: libaubio is not
+    in the image) on whole passes over a sample of the batch's clips, on the host's CPU share and
+    on one thread."""
+    import oracle_py
+    nproc = os.cpu_count() or 1
+    # the GPU box's CPU share (OMP_NUM_THREADS, 16 per GPU there); nproc counts the whole machine
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+    threads = max(1, min(nproc, share))
+    k = min(nclips, 4 * threads)
+    host = pcm[:k].cpu().numpy().reshape(-1)
+    off = np.arange(k + 1) * n
+    oracle_py.fingerprint_batch(host[: 2 * n], off[:3], nthreads=1, want_db=False)  # load + tables
+
+    def timed(nthreads, clips, seconds):
+        passes, t1 = 0, time.perf_counter()
+        while True:  # whole passes over the sample until ~seconds of work
+            oracle_py.fingerprint_batch(host[: clips * n], off[: clips + 1], nthreads=nthreads, want_db=False)
+            passes += 1
+            dt = time.perf_counter() - t1
+            if dt >= seconds:
+                return passes, dt
+    passes, dt = timed(threads, k, args.cpu_seconds)
+    frames = passes * k * (F // nclips)
+    fps = frames / dt
+    p1, dt1 = timed(1, 2, max(2.0, args.cpu_seconds / 3))
+    fps1 = p1 * 2 * (F // nclips) / dt1
+    log(f"cpu baseline {fps:.0f} fp/s on {threads} threads ({dt:.1f} s), {fps1:.0f} fp/s on 1 thread; nproc {nproc}")
+    return {"value": fps, "unit": "fingerprints/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} passes over {k} of the {nclips} x {args.seconds} s clips "
+                      f"({frames} frames), oracle/oracle.c, {threads} threads, {dt:.1f} s",
+            "nproc": nproc, "cores_policy": "the host's CPU share for this GPU (OMP_NUM_THREADS; 16 per GPU on "
+                                            "the GPU box), capped at nproc",
+            "one_core": {"value": fps1, "unit": "fingerprints/s", "cores": 1,
+                         "sample": f"{p1} passes over 2 clips ({p1 * 2 * (F // nclips)} frames), 1 thread, {dt1:.1f} s"},
+            "note": "libaubio is not installed: the oracle restates its algorithm in plain C (kind: port)"}
 
 
 def enroll(eng, torch, dev, sh, ids_all, chunk=2048):
@@ -321,6 +392,42 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     k = keys.cpu().numpy().view(np.uint64)
     found = int((k != 0).sum())
 
+    # SURVEY §8(d) sweeps on the same batch: tolerances, coefs = 2 (the general path), and the
+    # 100 / 3400 Hz ignore filter. First call untimed (it builds the tolerance's caches), then
+    # the median of up to 3 timed calls (1 when a call takes over 2 s).
+    sweeps = []
+    if not args.no_sweeps:
+        for coefs, tol, low, high in [(1, 0.01, -1, -1), (1, 0.1, -1, -1), (1, 0.45, -1, -1), (1, 0.001, 100, 3400),
+                                      (2, 0.001, -1, -1), (2, 0.01, -1, -1), (2, 0.1, -1, -1), (2, 0.45, -1, -1),
+                                      (2, 0.1, 100, 3400)]:
+            ps = T.params(coefs, tol, low, high)
+            log(f"sweep coefs={coefs} tol={tol} low/high={low}/{high} ...")
+
+            def sweep_batch():
+                if sharded:
+                    sharded(qpcm.data_ptr(), ps, keys, sh)
+                else:
+                    eng.search_device(qplan, qpcm.data_ptr(), ps, keys.data_ptr(), sh)
+                    sharding.combine(keys, dist)
+            sweep_batch()
+            torch.cuda.synchronize(dev)
+            ts = []
+            for _ in range(3):
+                barrier()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                sweep_batch()
+                torch.cuda.synchronize(dev)
+                ts.append(max_over_ranks(time.perf_counter() - t0))
+                if ts[-1] > 2.0:
+                    break
+            ks = keys.cpu().numpy().view(np.uint64)
+            sweeps.append({"coefs": coefs, "tolerance": tol, "freq_ignore_low": low, "freq_ignore_high": high,
+                           "batch_ms": float(np.median(ts)) * 1e3, "queries_per_s": nq / float(np.median(ts)),
+                           "found": int((ks != 0).sum()), "timed_calls": len(ts)})
+            log(f"sweep coefs={coefs} tol={tol} low/high={low}/{high}: {sweeps[-1]['batch_ms']:.2f} ms, "
+                f"found {sweeps[-1]['found']}")
+
     # batch-1 latency: host PCM in -> (uuid, match_count, frame_count) out
     # On N GPUs every rank runs the same small-batch path on its shard, turns its local winner into
     # the global key (match_count << 32 | global uuid rank) and one all_reduce(MAX) of 8 bytes
@@ -372,50 +479,73 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "queries_per_s": nq / (batch_ms / 1e3), "found": found,
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat), "latency_harness": harness,
-            "latency_p50_ms_python": float(np.percentile(lat_py, 50))}
+            "latency_p50_ms_python": float(np.percentile(lat_py, 50)),
+            "sweeps": sweeps}
     if rank == 0 and world == 1 and not args.no_cpu:
-        res["cpu_baseline"] = match_cpu_baseline(args, T)
+        res["cpu_baseline"] = match_cpu_baseline(args, T, eng, torch, dev, sh)
     return res
 
 
-def match_cpu_baseline(args, T, db_clips=200):
+def match_cpu_baseline(args, T, eng, torch, dev, sh):
     """The reference's own search path on the CPU: its SQL (oracle/sql_oracle.py restates
-    fp_handler.c:287-374 string for string) through SQLite 3.37, on a reduced DB — 200 of the
-    30 s clips inserted as db_ctx_insert does — with queries fingerprinted by the C oracle.
-    A smaller DB makes each range query cheaper, so this over-states the CPU's rate at C3."""
+    fp_handler.c:287-374 string for string) through SQLite 3.37, one connection, one thread, on
+    a DB of --cpu-db-clips of the 30 s clips (rows as db_ctx_insert writes them: "%f" literals,
+    NULL for absent keys; bulk-loaded, load not timed), queries fingerprinted by the C oracle.
+    Reported: per-query latency p50/p99 (= the dialplan application's search call) and the rows
+    the max1 index range scans visit per query. The GPU figures are against 100x the rows, and
+    the range scans grow with the DB, so this over-states the CPU at the C3 size."""
     import oracle_py
     from sql_oracle import SqlFingerprintDB
+    db_clips = args.cpu_db_clips
     n_db, qn = 8000 * 30, 8000 * 5
     nf_db = (n_db + HOP - 1) // HOP
     ids = list(range(db_clips))
-    pcm = T.synth_pcm(SEED_DB, ids, n_db)
+    buf = torch.empty((db_clips, n_db), dtype=torch.int16, device=dev)
+    eng.synth_device(SEED_DB, ids, n_db, buf.data_ptr(), stream=sh)  # same PCM as the host synth, faster
+    torch.cuda.synchronize(dev)
+    pcm = buf.cpu().numpy()
+    del buf
     micro, _ = oracle_py.fingerprint_batch(pcm.reshape(-1), np.arange(db_clips + 1) * n_db, nthreads=16, want_db=False)
     db = SqlFingerprintDB()
-    for i, g in enumerate(ids):
-        db.insert_rows("bench", uuid_of(g), micro[i * nf_db:(i + 1) * nf_db, 0], micro[i * nf_db:(i + 1) * nf_db, 1])
+    t_load = time.perf_counter()
+    db.insert_rows_bulk("bench", ((uuid_of(g), micro[i * nf_db:(i + 1) * nf_db, 0], micro[i * nf_db:(i + 1) * nf_db, 1])
+                                  for i, g in enumerate(ids)))
+    t_load = time.perf_counter() - t_load
+    m1_sorted = np.sort(micro[:, 0][micro[:, 0] != oracle_py.NULL_MICRO].astype(np.int64))
     rng = np.random.default_rng(SEED_Q + 2)
-    queries = []
-    for i in range(64):
+    queries, scanned = [], []
+    for i in range(32):
         if i % 4 != 3:
             q = T.synth_pcm(SEED_DB, [int(rng.integers(db_clips))], qn, offsets=[256 * int(rng.integers(0, (n_db - qn) // HOP))])[0]
         else:
             q = T.synth_pcm(SEED_Q, [100000 + i], qn)[0]
         _, qdb, _ = oracle_py.fingerprint(q)
-        queries.append(([None if not np.isfinite(v) else float(v) for v in qdb[:, 0]],
-                        [None if not np.isfinite(v) else float(v) for v in qdb[:, 1]]))
-    done, found, t0 = 0, 0, time.perf_counter()
+        q1 = [None if not np.isfinite(v) else float(v) for v in qdb[:, 0]]
+        queries.append((q1, [None if not np.isfinite(v) else float(v) for v in qdb[:, 1]]))
+        # rows of the max1 index range each frame's statement visits (coefs=1, tol 0.001)
+        keys = np.trunc(np.array([0.0 if v is None else v for v in q1]))
+        lo = np.array([oracle_py.fmt6(k - 0.001) for k in keys])
+        hi = np.array([oracle_py.fmt6(k + 0.001) for k in keys])
+        scanned.append(int((np.searchsorted(m1_sorted, hi, "right") - np.searchsorted(m1_sorted, lo, "left")).sum()))
+    lat, done, found, t0 = [], 0, 0, time.perf_counter()
     while True:
         q1, q2 = queries[done % len(queries)]
+        t1 = time.perf_counter()
         found += db.search(q1, q2, 1, 0.001, -1, -1) is not None
+        lat.append((time.perf_counter() - t1) * 1e3)
         done += 1
         dt = time.perf_counter() - t0
-        if dt >= args.cpu_seconds and done >= len(queries):
+        if dt >= args.cpu_seconds and done >= 8:
             break
-    log(f"match cpu baseline {done / dt:.1f} queries/s ({done} queries, {dt:.1f} s)")
+    log(f"match cpu baseline {done / dt:.1f} queries/s ({done} queries, {dt:.1f} s), p50 {np.percentile(lat, 50):.1f} ms")
     return {"value": done / dt, "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": f"{done} x 5 s queries (75 % excerpts) vs {db_clips} x 30 s clips "
+            "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
+            "db_clips": db_clips, "db_rows": db_clips * nf_db, "db_load_s": t_load,
+            "rows_scanned_per_query_mean": float(np.mean(scanned)),
+            "sample": f"{done} x 5 s queries (75 % excerpts, {found} found) vs {db_clips} x 30 s clips "
                       f"({db_clips * nf_db} rows) through the reference SQL in SQLite {__import__('sqlite3').sqlite_version}, "
-                      f"1 thread, {dt:.1f} s; the GPU figure is against {args.db_clips} clips"}
+                      f"1 thread, {dt:.1f} s; the GPU figures are against {args.db_clips} clips",
+            "note": "the reference's SQL restated string for string (fp_handler.c:287-374), run by this image's SQLite (kind: port)"}
 
 
 def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):

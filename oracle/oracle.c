@@ -481,30 +481,64 @@ typedef struct {
   int32_t *winner, *count;
 } sorted_arg;
 
+typedef struct {
+  int64_t L1, U1, L2, U2;
+  int has2, frames;
+} box_t;
+
+static int box_cmp(const void* a, const void* b) {
+  const box_t *x = (const box_t*)a, *y = (const box_t*)b;
+  if (x->L1 != y->L1) return x->L1 < y->L1 ? -1 : 1;
+  if (x->U1 != y->U1) return x->U1 < y->U1 ? -1 : 1;
+  if (x->has2 != y->has2) return x->has2 < y->has2 ? -1 : 1;
+  if (x->L2 != y->L2) return x->L2 < y->L2 ? -1 : 1;
+  if (x->U2 != y->U2) return x->U2 < y->U2 ? -1 : 1;
+  return 0;
+}
+
+/* Per query: every frame's WHERE clause; frames with the same clause insert the same rows (one
+ * per clip), so each distinct clause scans its rows once and adds its frame count per clip. */
 static void* sorted_worker(void* p) {
   sorted_arg* a = (sorted_arg*)p;
   int32_t* score = (int32_t*)calloc((size_t)(a->nclips > 0 ? a->nclips : 1), sizeof(int32_t));
   int32_t* stamp = (int32_t*)calloc((size_t)(a->nclips > 0 ? a->nclips : 1), sizeof(int32_t));
   int32_t* touched = (int32_t*)malloc(sizeof(int32_t) * (size_t)(a->nclips > 0 ? a->nclips : 1));
+  box_t* boxes = NULL;
+  int64_t cap = 0;
   int32_t q, c, k;
   int32_t epoch = 0;
   for (q = a->tid; q < a->nq; q += a->nthreads) {
-    int64_t f;
+    int64_t f, nb = 0, i, j;
     int32_t nt = 0, best = -1;
+    if (a->qoff[q + 1] - a->qoff[q] > cap) {
+      cap = a->qoff[q + 1] - a->qoff[q];
+      boxes = (box_t*)realloc(boxes, sizeof(box_t) * (size_t)cap);
+    }
     for (f = a->qoff[q]; f < a->qoff[q + 1]; f++) {
-      int64_t L1, U1, L2 = 0, U2 = 0, r, lo, hi;
-      int has2;
+      box_t b;
+      memset(&b, 0, sizeof b);
+      if (!frame_box(a->q1[f], a->q2[f], a->coefs, a->tole, a->low, a->high, &b.L1, &b.U1, &b.has2, &b.L2, &b.U2))
+        continue;
+      b.frames = 1;
+      boxes[nb++] = b;
+    }
+    if (nb > 1) qsort(boxes, (size_t)nb, sizeof(box_t), box_cmp);
+    for (i = 0; i < nb; i = j) {
+      int64_t r, lo, hi;
+      const box_t* b = &boxes[i];
+      int add = 0;
+      for (j = i; j < nb && box_cmp(&boxes[j], b) == 0; j++) add++;
       epoch++;
-      if (!frame_box(a->q1[f], a->q2[f], a->coefs, a->tole, a->low, a->high, &L1, &U1, &has2, &L2, &U2)) continue;
-      lo = lower_bound32(a->m1s, a->nrows, L1);
-      hi = lower_bound32(a->m1s, a->nrows, U1 + 1);
+      lo = lower_bound32(a->m1s, a->nrows, b->L1);
+      hi = lower_bound32(a->m1s, a->nrows, b->U1 + 1);
       for (r = lo; r < hi; r++) {
         if (a->m1s[r] == TFO_NULL) continue; /* NULL compares false */
-        if (has2 && (a->m2s[r] == TFO_NULL || a->m2s[r] < L2 || a->m2s[r] > U2)) continue;
+        if (b->has2 && (a->m2s[r] == TFO_NULL || a->m2s[r] < b->L2 || a->m2s[r] > b->U2)) continue;
         c = a->clip[r];
         if (stamp[c] != epoch) { /* GROUP BY audio_uuid: at most 1 per clip per frame */
           stamp[c] = epoch;
-          if (!score[c]++) touched[nt++] = c;
+          if (!score[c]) touched[nt++] = c;
+          score[c] += add;
         }
       }
     }
@@ -516,7 +550,7 @@ static void* sorted_worker(void* p) {
     a->count[q] = best >= 0 ? score[best] : 0;
     for (k = 0; k < nt; k++) score[touched[k]] = 0;
   }
-  free(score); free(stamp); free(touched);
+  free(boxes); free(score); free(stamp); free(touched);
   return NULL;
 }
 

@@ -60,6 +60,27 @@ class SqlFingerprintDB:
             c.execute("insert into audio_fingerprint(%s) values (%s);" % (", ".join(keys), ", ".join(vals)))
         self.db.commit()
 
+    def insert_rows_bulk(self, context: str, clips, null: int = -(2**31), per_stmt: int = 500):
+        """The same rows as insert_rows (same "%f" literals, same NULL rule), loaded in one
+        transaction with multi-row INSERT statements: for building large benchmark tables fast
+        (the load is not what the baseline times). clips: iterable of (uuid, m1s, m2s)."""
+        c = self.db.cursor()
+        c.execute("begin")
+        buf = []
+
+        def lit(m):
+            return "NULL" if m == null else micro_str(int(m))
+        for uuid, m1s, m2s in clips:
+            for idx, (m1, m2) in enumerate(zip(m1s, m2s)):
+                buf.append("('%s','%s',%d,%s,%s)" % (context, uuid, idx, lit(m1), lit(m2)))
+                if len(buf) == per_stmt:
+                    c.execute("insert into audio_fingerprint(context, audio_uuid, frame_idx, max1, max2) values "
+                              + ",".join(buf))
+                    buf = []
+        if buf:
+            c.execute("insert into audio_fingerprint(context, audio_uuid, frame_idx, max1, max2) values " + ",".join(buf))
+        self.db.commit()
+
     def search(self, q1s, q2s, coefs: int, tolerance: float, freq_ignore_low: int, freq_ignore_high: int):
         """fp_search_fingerprint_info on precomputed query fingerprints.
 

@@ -204,21 +204,20 @@ def _c3_queries(nq, db_clips, seed=SEED_Q):
     return spec
 
 
-def test_configs2_full_db_vs_sorted_oracle(engine, oracle, tfp_lib, torch_cuda):
-    """configs[2]: 100,000 x 30 s clips (93.8 M rows) enrolled on the device as bench.py does,
-    5 s queries against all of them. Rows: a sample of 256 clips re-fingerprinted by the oracle.
-    Search: the batch device path (vote; tol 0.001 and 0.1) and the batch-1 host path, each
-    (count, uuid rank) == the oracle's sorted-index search over the same 93.8 M rows."""
+@pytest.fixture(scope="module")
+def c3db(oracle, tfp_lib, torch_cuda):
+    """configs[2]'s DB: 100,000 x 30 s clips (93.8 M rows) enrolled on the device as bench.py does
+    (own engine), its rows checked on a 256-clip sample against the oracle's fingerprints, and the
+    oracle's sorted index over the same rows (tie key = rank of the uuid among all clips)."""
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
-    db_clips, n_db, qn = 100_000, 8000 * 30, 8000 * 5
+    eng = tfp_lib.Engine(0)
+    db_clips, n_db = 100_000, 8000 * 30
     nf_db = (n_db + HOP - 1) // HOP
-    rows = _enroll_db(engine, torch, dev, stream, list(range(db_clips)))
-    nrows, nc = engine.index_stats()
+    rows = _enroll_db(eng, torch, dev, stream, list(range(db_clips)))
+    nrows, nc = eng.index_stats()
     assert nc == db_clips and nrows == db_clips * nf_db
-    # the enrolled rows are the oracle's fingerprints (sampled: the full-size batch test above
-    # covers the kernel at this launch size)
     rng = np.random.default_rng(1)
     sample = np.sort(rng.choice(db_clips, 256, replace=False))
     pcm = tfp_lib.synth_pcm(SEED_DB, sample.tolist(), n_db)
@@ -226,37 +225,75 @@ def test_configs2_full_db_vs_sorted_oracle(engine, oracle, tfp_lib, torch_cuda):
                                       want_db=False)
     got = np.concatenate([rows[c * nf_db:(c + 1) * nf_db] for c in sample])
     assert np.array_equal(got, exp)
-    # oracle index over the same rows; tie key = rank of the uuid among all clips
     uuids = [_uuid_of(g) for g in range(db_clips)]
     order = np.argsort(np.asarray(uuids))
     rank = np.empty(db_clips, np.int32)
     rank[order] = np.arange(db_clips, dtype=np.int32)
     idx = oracle.SortedIndex(rows[:, 0], rows[:, 1], np.repeat(np.arange(db_clips, dtype=np.int32), nf_db), rank)
     del rows
-    spec = _c3_queries(96, db_clips)
+    yield {"eng": eng, "idx": idx, "uuids": uuids, "rank": rank, "db_clips": db_clips}
+    eng.close()
+
+
+def _c3_batch(c3db, tfp_lib, torch, nq, seed=SEED_Q):
+    qn = 8000 * 5
+    spec = _c3_queries(nq, c3db["db_clips"], seed)
     qpcm = np.stack([tfp_lib.synth_pcm(sd, [c], qn, offsets=[o])[0] for sd, c, o in spec])
-    nfq = (qn + HOP - 1) // HOP
-    qdb = np.concatenate([oracle.fingerprint(qpcm[i])[1] for i in range(len(spec))])
-    qoff = np.arange(len(spec) + 1, dtype=np.int64) * nfq
-    d_q = torch.from_numpy(qpcm).to(dev)
-    qplan = engine.plan(np.arange(len(spec) + 1, dtype=np.int64) * qn)
+    return qpcm, torch.from_numpy(qpcm).to("cuda")
+
+
+def _oracle_q(oracle, qpcm):
+    nfq = (qpcm.shape[1] + HOP - 1) // HOP
+    qdb = np.concatenate([oracle.fingerprint(qpcm[i])[1] for i in range(len(qpcm))])
+    return qdb, np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
+
+
+def _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, p, nthreads=ORACLE_THREADS):
+    eng, idx, rank = c3db["eng"], c3db["idx"], c3db["rank"]
+    w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, p.coefs, p.tolerance, p.freq_ignore_low, p.freq_ignore_high,
+                             nthreads=nthreads)
+    keys = torch.zeros(len(qpcm), dtype=torch.int64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    eng.search_device(eng.plan(np.arange(len(qpcm) + 1, dtype=np.int64) * qpcm.shape[1]), d_q.data_ptr(), p,
+                      keys.data_ptr(), stream)
+    torch.cuda.synchronize()
+    k = keys.cpu().numpy().view(np.uint64)
+    expk = np.where(w >= 0, (mc.astype(np.uint64) << np.uint64(32)) | rank[np.maximum(w, 0)].astype(np.uint64), 0)
+    assert np.array_equal(k, expk.astype(np.uint64)), (p.coefs, p.tolerance, np.nonzero(k != expk)[0][:8])
+    return w, mc
+
+
+def test_configs2_full_db_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
+    """configs[2]: 5 s queries against all 100,000 clips. The batch device path (vote; tol 0.001
+    and 0.1) and the batch-1 host path, each (count, uuid rank) == the oracle's sorted-index
+    search over the same 93.8 M rows."""
+    torch = torch_cuda
+    qpcm, d_q = _c3_batch(c3db, tfp_lib, torch, 96)
+    qdb, qoff = _oracle_q(oracle, qpcm)
     for tol in (0.001, 0.1):
-        w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, 1, tol, nthreads=ORACLE_THREADS)
-        keys = torch.zeros(len(spec), dtype=torch.int64, device=dev)
-        engine.search_device(qplan, d_q.data_ptr(), tfp_lib.params(1, tol), keys.data_ptr(), stream)
-        torch.cuda.synchronize()
-        k = keys.cpu().numpy().view(np.uint64)
-        expk = np.where(w >= 0, (mc.astype(np.uint64) << np.uint64(32)) | rank[np.maximum(w, 0)].astype(np.uint64), 0)
-        assert np.array_equal(k, expk.astype(np.uint64)), (tol, np.nonzero(k != expk)[0][:8])
-        assert (w >= 0).sum() >= len(spec) // 4
+        w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(1, tol))
+        assert (w >= 0).sum() >= len(qpcm) // 4
     # batch-1 (small path), host PCM in -> result out, as the dialplan application calls it
-    w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, 1, 0.001, nthreads=ORACLE_THREADS)
+    w, mc = c3db["idx"].search_batch(qdb[:, 0], qdb[:, 1], qoff, 1, 0.001, nthreads=ORACLE_THREADS)
+    nfq = int(qoff[1])
     for i in range(16):
-        res, fc = engine.search_pcm_batch(qpcm[i], [0, qn], tfp_lib.params(1, 0.001))
+        res, fc = c3db["eng"].search_pcm_batch(qpcm[i], [0, qpcm.shape[1]], tfp_lib.params(1, 0.001))
         got = None if res[0] is None else (res[0]["audio_uuid"], res[0]["match_count"])
-        assert got == ((uuids[w[i]], int(mc[i])) if w[i] >= 0 else None), i
+        assert got == ((c3db["uuids"][w[i]], int(mc[i])) if w[i] >= 0 else None), i
         assert fc[0] == nfq
-    engine.index_clear()
+
+
+@pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 64), (2, 0.01, -1, -1, 32), (2, 0.1, -1, -1, 16),
+                                                   (1, 0.45, -1, -1, 64), (1, 0.01, 100, 3400, 64),
+                                                   (2, 0.1, 100, 3400, 16)])
+def test_configs2_sweeps_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda, coefs, tol, low, high, nq):
+    """SURVEY §8(d)'s configs[2] sweeps at full DB size: coefs = 2 (the general path over the
+    m2-ordered key segments, src/fp_handler.c:318-351), wider tolerances and the 100/3400 Hz
+    ignore filter (:293-306, :324-337) — every key == the oracle's."""
+    torch = torch_cuda
+    qpcm, d_q = _c3_batch(c3db, tfp_lib, torch, nq, SEED_Q + coefs)
+    qdb, qoff = _oracle_q(oracle, qpcm)
+    _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(coefs, tol, low, high))
 
 
 def test_configs4_512_channels_one_tick(engine, oracle, tfp_lib, torch_cuda):
