@@ -71,7 +71,7 @@ struct Clip {
 }  // namespace
 
 struct tfp_plan {
-  int32_t nclips = 0, ntiles = 0, sample_rate = 0;
+  int32_t nclips = 0, ntiles = 0, sample_rate = 0, tile_frames = 0;
   int64_t nsamples = 0, nframes = 0;
   std::vector<int64_t> soff, foff;
   std::vector<int32_t> toff, tclip;
@@ -222,13 +222,14 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
   if (rc) return rc;
   std::vector<int64_t> soff, foff;
   std::vector<int32_t> toff, tclip;
-  // small batches at 8 kHz: 4-frame wave tiles (4x the waves, a quarter of the per-wave passes)
-  int tile_frames = kFramesPerBlock;
+  // small batches at 8 kHz: 4-frame wave tiles (more waves, fewer passes per wave)
+  bool small = false;
   if (fx && !f32) {
     int64_t nf16 = 0;
     for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(offsets[c + 1] - offsets[c]) + 15) / 16;
-    if (nf16 <= 256) tile_frames = 4;
+    small = nf16 <= 256;
   }
+  const int tile_frames = fp_tile_frames(e->fpcfg, fx, f32, small);
   layout(offsets, nclips, soff, foff, toff, &tclip, tile_frames);
   const int64_t ns = soff[nclips], nf = foff[nclips];
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
@@ -805,13 +806,15 @@ int tfp_plan_create(tfp_engine* e, const int64_t* offsets, int32_t nclips, int32
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
   const DspTables* T;
-  int rc = ensure_tables(e, sr, &T);
+  bool fx = false;
+  int rc = ensure_tables(e, sr, &T, &fx);
   if (rc) return rc;
   tfp_plan* p = new tfp_plan();
   p->eng = e;
   p->nclips = nclips;
   p->sample_rate = sr;
-  layout(offsets, nclips, p->soff, p->foff, p->toff, &p->tclip);
+  p->tile_frames = fp_tile_frames(e->fpcfg, fx, false, false);
+  layout(offsets, nclips, p->soff, p->foff, p->toff, &p->tclip, p->tile_frames);
   p->nsamples = p->soff[nclips];
   p->nframes = p->foff[nclips];
   p->ntiles = p->toff[nclips];
@@ -840,7 +843,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s));
   return TFP_OK;
@@ -1110,7 +1113,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, kFramesPerBlock, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
                                e->db.as<double>(), s));
@@ -1215,7 +1218,11 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
       if (std::min<int64_t>(st->W, st->filled[c] + T) >= st->W) act.push_back(c);
   const int32_t na = (int32_t)act.size();
   const int64_t F = tfp_frame_count(st->W);
-  const int32_t tiles = (int32_t)((F + kFramesPerBlock - 1) / kFramesPerBlock);
+  const DspTables* Tb;
+  bool fx = false;
+  if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
+  const int32_t tile = fp_tile_frames(e->fpcfg, fx, false, false);
+  const int32_t tiles = (int32_t)((F + tile - 1) / tile);
   // One pinned upload per tick: the tick's samples, then the windows' layout (sbeg, send, foff,
   // toff, tclip). The previous tick's upload must be done reading the pinned buffer.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1256,13 +1263,10 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
     out[c].clip_id = -1;
   }
   if (!match || !na) return TFP_OK;  // full windows only
-  const DspTables* Tb;
-  bool fx = false;
-  if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
   const int64_t* d_sb = reinterpret_cast<const int64_t*>(d + b_pcm);
-  HIPCHK(e, launch_fingerprint(e->fpcfg, Tb, fx, kFramesPerBlock, st->ring.as<int16_t>(), d_sb,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, Tb, fx, tile, st->ring.as<int16_t>(), d_sb,
                                reinterpret_cast<const int64_t*>(d + b_pcm + b_sb),
                                reinterpret_cast<const int64_t*>(d + b_pcm + 2 * b_sb),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo),

@@ -610,7 +610,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
   // dB + "%f" in finish_db_kernel for throughput launches (full waves); in the tile tail for small
   // ones (4-frame tiles, batch-1 latency), which saves a launch
-  constexpr bool kSplitTail = kPasses == 4;
+  constexpr bool kSplitTail = kPasses >= 2;
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
@@ -911,18 +911,42 @@ bool DspTables_fixed8k(const DspTables& t) {
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
 }
 
+// Resident 256-thread blocks per CU of kernel k: the occupancy query, capped by what the
+// kernel's VGPRs and LDS admit on gfx950 (512 VGPRs per SIMD lane in granules of 8, one wave of
+// a block per SIMD; 160 KiB of LDS per CU). The query alone over-counted once the LDS shrank
+// below a third of the CU while the VGPRs still admitted two waves: a grid of 3 blocks per CU
+// ran its last third as a tail (0.71 vs 0.54 ms per C2 launch).
+static int resident_blocks(const void* k) {
+  int per = 0;
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kBlockThreads, 0);
+  hipFuncAttributes a;
+  if (hipFuncGetAttributes(&a, k) == hipSuccess) {
+    const int vg = ((a.numRegs > 0 ? a.numRegs : 1) + 7) / 8 * 8;
+    int by_vgpr = 512 / vg;
+    if (by_vgpr > 8) by_vgpr = 8;
+    const int by_lds = a.sharedSizeBytes ? (int)((160 * 1024) / a.sharedSizeBytes) : 8;
+    const int own = by_vgpr < by_lds ? by_vgpr : by_lds;
+    if (per <= 0 || own < per) per = own;
+  }
+  return per > 0 ? per : 1;
+}
+
 hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
-  int cus = 0, per = 0;
+  int cus = 0;
   hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return e;
-  auto cap = [&](const void* k) {
-    per = 0;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kBlockThreads, 0);
-    return cus * (per > 0 ? per : 1);
-  };
-  cfg->grid_cap_8k = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<4>));
+  auto cap = [&](const void* k) { return cus * resident_blocks(k); };
+  cfg->grid_cap_8k = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>));
+  cfg->grid_cap_8k_small = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<1>));
   cfg->grid_cap_generic = cap(reinterpret_cast<const void*>(fingerprint_kernel<int16_t>));
   cfg->grid_cap_f32 = cap(reinterpret_cast<const void*>(fingerprint_kernel<float>));
+  if (getenv("TFP_DEBUG_OCC")) {
+    int per = 0;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>),
+                                                       kBlockThreads, 0);
+    fprintf(stderr, "[tfp] fingerprint8k_kernel<%d>: %d blocks/CU (occupancy query %d), grid cap %d\n", kTile8k / 4,
+            cfg->grid_cap_8k / cus, per, cfg->grid_cap_8k);
+  }
   const char* g = getenv("TFP_GENERIC");
   cfg->force_generic = g && atoi(g);
   const char* rt = getenv("TFP_RARE_THR_LOG2");
@@ -936,10 +960,10 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
                               int32_t* d_micro, double* d_db, hipStream_t s) {
-  if (tile_frames != 16 && !(tile_frames == 4 && fixed8k)) return hipErrorInvalidValue;
-  if (ntiles <= 0) return hipSuccess;
   const bool v8 = fixed8k && (tile_frames == 4 || !cfg.force_generic);
-  const int cap = v8 ? cfg.grid_cap_8k : cfg.grid_cap_generic;
+  if (v8 ? !(tile_frames == 4 || tile_frames == kTile8k) : tile_frames != kFramesPerBlock) return hipErrorInvalidValue;
+  if (ntiles <= 0) return hipSuccess;
+  const int cap = v8 ? (tile_frames == 4 ? cfg.grid_cap_8k_small : cfg.grid_cap_8k) : cfg.grid_cap_generic;
   if (cap <= 0) return hipErrorInvalidValue;
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
   const int grid = want < cap ? want : cap;
@@ -948,8 +972,8 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
       hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                          d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
     } else {
-      hipLaunchKernelGGL(fingerprint8k_kernel<4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
+      hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg,
+                         d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;

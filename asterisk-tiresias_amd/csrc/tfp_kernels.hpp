@@ -7,7 +7,12 @@
 
 namespace tfp {
 
-constexpr int kFramesPerBlock = 16;   // 16 lanes per frame x 16 frames = 256 threads
+constexpr int kFramesPerBlock = 16;   // frames per wave tile of the generic kernel (16 lanes per frame)
+// Frames per wave tile of fingerprint8k_kernel's throughput launches. 16: the tile tail (deferred
+// logs, DCT) amortised over 4 passes. Measured, not kept: 8-frame tiles with the smaller log
+// buffer that lets 3 workgroups (3 waves/SIMD at <= 168 VGPRs) share a CU: 0.565 ms per C2
+// launch vs 0.536 (the LDS array is ~50 % busy at 2 waves/SIMD; a third wave adds contention).
+constexpr int kTile8k = 16;
 constexpr int32_t kKeyOffset = 512;   // trunc(dB) key k stored at k + 512 (|k| <= 459)
 constexpr int32_t kKeyRange = 1024;
 
@@ -38,7 +43,8 @@ struct SynthSpecDev {
 // Per-engine launch configuration: read once when the engine is created (fp_launch_config),
 // grid caps from the engine's own device.
 struct FpLaunchCfg {
-  int32_t grid_cap_8k = 0;       // resident blocks of fingerprint8k_kernel on the device
+  int32_t grid_cap_8k = 0;       // resident blocks of fingerprint8k_kernel (kTile8k-frame tiles) on the device
+  int32_t grid_cap_8k_small = 0; // ... of its 4-frame-tile form (small batches)
   int32_t grid_cap_generic = 0;  // resident blocks of fingerprint_kernel<int16_t>
   int32_t grid_cap_f32 = 0;      // resident blocks of fingerprint_kernel<float>
   bool force_generic = false;    // TFP_GENERIC=1: the generic kernel at 8 kHz too (tests)
@@ -46,10 +52,16 @@ struct FpLaunchCfg {
 };
 // Fills cfg for `device` (occupancy queries + the test knobs from the environment).
 hipError_t fp_launch_config(int device, FpLaunchCfg* cfg);
+inline int32_t fp_tile_frames(const FpLaunchCfg& cfg, bool fixed8k, bool f32, bool small) {
+  if (!fixed8k || f32) return kFramesPerBlock;
+  if (small) return 4;
+  return cfg.force_generic ? kFramesPerBlock : kTile8k;
+}
 // fixed8k: the tables' filterbank schedule is the 8 kHz one (DspTables_fixed8k), so the
 // specialized fingerprint8k_kernel runs; otherwise the generic fingerprint_kernel.
 bool DspTables_fixed8k(const DspTables& t);
-// tile_frames: frames per wave tile in toff/tclip, 16 (any rate) or 4 (8 kHz only: small batches).
+// tile_frames: frames per wave tile in toff/tclip: fp_tile_frames() — kFramesPerBlock for the
+// generic kernel, kTile8k (or 4 for small batches) for fingerprint8k_kernel.
 hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
