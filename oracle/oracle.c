@@ -214,6 +214,58 @@ static void rfft512_norm(const tfo_tables* t, const float* x, float* norm) {
   }
 }
 
+/* ---------------------------------------- other valid fp32 FFT orders (sensitivity) ----- */
+/* The canonical FFT above is this project's spec; the reference build's FFT backend (fftw3f, or
+ * aubio's bundled Ooura code) cannot be reproduced here. These two textbook orders measure how
+ * much a different, equally valid fp32 evaluation moves the stored values:
+ *   1: iterative radix-2 decimation-in-time 256-point complex FFT + the canonical real split;
+ *   2: radix-2 decimation-in-time 512-point complex FFT of the real input (no real split),
+ *      |X_k| = sqrtf(re^2 + im^2). Twiddles: the same (float)cos / (float)-sin tables. */
+static void fft_radix2(cpx* a, int N, const float* wre, const float* wim, int wstride) {
+  int i, j, len, bits = 0;
+  for (i = N; i > 1; i >>= 1) bits++;
+  for (i = 0; i < N; i++) { /* bit-reversed input order */
+    int r = 0, b;
+    for (b = 0; b < bits; b++) r |= ((i >> b) & 1) << (bits - 1 - b);
+    if (r > i) { cpx tmp = a[i]; a[i] = a[r]; a[r] = tmp; }
+  }
+  for (len = 2; len <= N; len <<= 1) {
+    int half = len >> 1, step = (N / len) * wstride;
+    for (i = 0; i < N; i += len)
+      for (j = 0; j < half; j++) {
+        cpx u = a[i + j], v = cmul(a[i + j + half], wre[j * step], wim[j * step]);
+        a[i + j].re = u.re + v.re; a[i + j].im = u.im + v.im;
+        a[i + j + half].re = u.re - v.re; a[i + j + half].im = u.im - v.im;
+      }
+  }
+}
+
+static void rfft512_norm_variant(const tfo_tables* t, const float* x, float* norm, int variant) {
+  int m, k;
+  if (variant == 1) {
+    cpx Z[256];
+    for (m = 0; m < 256; m++) { Z[m].re = x[2 * m]; Z[m].im = x[2 * m + 1]; }
+    fft_radix2(Z, 256, t->tw256_re, t->tw256_im, 1);
+    norm[0] = fabsf(Z[0].re + Z[0].im);
+    norm[256] = fabsf(Z[0].re - Z[0].im);
+    for (k = 1; k < 256; k++) {
+      float a = Z[k].re, b = Z[k].im, c = Z[256 - k].re, d = Z[256 - k].im;
+      float Er = a + c, Ei = b - d, Or = a - c, Oi = b + d;
+      float wr = t->tw512_re[k], wi = t->tw512_im[k];
+      float tr = wr * Oi + wi * Or;
+      float ti = wr * Or - wi * Oi;
+      float Xr = 0.5f * (Er + tr);
+      float Xi = 0.5f * (Ei - ti);
+      norm[k] = sqrtf(Xr * Xr + Xi * Xi);
+    }
+  } else {
+    cpx X[512];
+    for (m = 0; m < 512; m++) { X[m].re = x[m]; X[m].im = 0.f; }
+    fft_radix2(X, 512, t->tw512_re, t->tw512_im, 1);
+    for (k = 0; k <= 256; k++) norm[k] = sqrtf(X[k].re * X[k].re + X[k].im * X[k].im);
+  }
+}
+
 /* ---------------------------------------------------------------- %f ---------------- */
 
 int64_t tfo_fmt6(double x) {
@@ -238,7 +290,7 @@ int64_t tfo_fmt6(double x) {
  * 16-bit sndfile/wavread conversion) or are given as fp32 (x: multichannel mean, 24/32-bit or
  * float data, as tfp_wav_decode_f32 restates aubio's source for them). */
 static size_t fingerprint_core(const tfo_tables* t, const int16_t* pcm, const float* xin, size_t n, float* coef,
-                               double* db, int32_t* micro) {
+                               double* db, int32_t* micro, int variant) {
   float data[TFO_WIN], dataold[TFO_WIN - TFO_HOP], x[TFO_WIN], norm[TFO_BINS];
   float band[TFO_FILTERS], out[TFO_COEFS];
   size_t nf = tfo_frame_count(n), f;
@@ -257,7 +309,8 @@ static size_t fingerprint_core(const tfo_tables* t, const int16_t* pcm, const fl
     for (i = 0; i < TFO_WIN - TFO_HOP; i++) dataold[i] = data[i + TFO_HOP];
     for (i = 0; i < TFO_WIN; i++) data[i] *= t->window[i];
     for (i = 0; i < TFO_WIN / 2; i++) { x[i] = data[i + TFO_WIN / 2]; x[i + TFO_WIN / 2] = data[i]; }
-    rfft512_norm(t, x, norm);
+    if (variant) rfft512_norm_variant(t, x, norm, variant);
+    else rfft512_norm(t, x, norm);
     /* aubio_mfcc_do: filterbank (fmat_vecmul), fvec_log10, DCT (fmat_vecmul) */
     for (j = 0; j < TFO_FILTERS; j++) band[j] = 0.f;
     for (i = 0; i < TFO_BINS; i++)
@@ -282,12 +335,12 @@ static size_t fingerprint_core(const tfo_tables* t, const int16_t* pcm, const fl
 
 size_t tfo_fingerprint(const tfo_tables* t, const int16_t* pcm, size_t n, float* coef, double* db,
                        int32_t* micro) {
-  return fingerprint_core(t, pcm, NULL, n, coef, db, micro);
+  return fingerprint_core(t, pcm, NULL, n, coef, db, micro, 0);
 }
 
 size_t tfo_fingerprint_f32(const tfo_tables* t, const float* x, size_t n, float* coef, double* db,
                            int32_t* micro) {
-  return fingerprint_core(t, NULL, x, n, coef, db, micro);
+  return fingerprint_core(t, NULL, x, n, coef, db, micro, 0);
 }
 
 typedef struct {
@@ -295,7 +348,7 @@ typedef struct {
   const int16_t* pcm;
   const int64_t* off;
   const int64_t* foff;
-  int nclips, tid, nthreads;
+  int nclips, tid, nthreads, variant;
   int32_t* micro;
   double* db;
 } batch_arg;
@@ -305,14 +358,14 @@ static void* batch_worker(void* p) {
   int c;
   for (c = a->tid; c < a->nclips; c += a->nthreads) {
     size_t n = (size_t)(a->off[c + 1] - a->off[c]);
-    tfo_fingerprint(a->t, a->pcm + a->off[c], n, NULL, a->db ? a->db + 2 * a->foff[c] : NULL,
-                    a->micro ? a->micro + 2 * a->foff[c] : NULL);
+    fingerprint_core(a->t, a->pcm + a->off[c], NULL, n, NULL, a->db ? a->db + 2 * a->foff[c] : NULL,
+                     a->micro ? a->micro + 2 * a->foff[c] : NULL, a->variant);
   }
   return NULL;
 }
 
-size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
-                             int nclips, int32_t* micro, double* db, int nthreads) {
+size_t tfo_fingerprint_batch_variant(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
+                                     int nclips, int32_t* micro, double* db, int nthreads, int variant) {
   int64_t* foff = (int64_t*)malloc(sizeof(int64_t) * (size_t)(nclips + 1));
   pthread_t* th;
   batch_arg* args;
@@ -325,7 +378,7 @@ size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int6
   th = (pthread_t*)malloc(sizeof(pthread_t) * (size_t)nthreads);
   args = (batch_arg*)malloc(sizeof(batch_arg) * (size_t)nthreads);
   for (i = 0; i < nthreads; i++) {
-    batch_arg a = {t, pcm, offsets, foff, nclips, i, nthreads, micro, db};
+    batch_arg a = {t, pcm, offsets, foff, nclips, i, nthreads, variant, micro, db};
     args[i] = a;
     pthread_create(&th[i], NULL, batch_worker, &args[i]);
   }
@@ -335,6 +388,11 @@ size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int6
   free(args);
   free(foff);
   return total;
+}
+
+size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
+                             int nclips, int32_t* micro, double* db, int nthreads) {
+  return tfo_fingerprint_batch_variant(t, pcm, offsets, nclips, micro, db, nthreads, 0);
 }
 
 /* ---------------------------------------------------------------- search ------------ */

@@ -54,6 +54,9 @@ def lib():
         L.tfo_fingerprint_f32.restype = C.c_size_t
         L.tfo_fingerprint_batch.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int]
         L.tfo_fingerprint_batch.restype = C.c_size_t
+        L.tfo_fingerprint_batch_variant.argtypes = [C.POINTER(Tables), C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                                    C.c_void_p, C.c_int, C.c_int]
+        L.tfo_fingerprint_batch_variant.restype = C.c_size_t
         L.tfo_search.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_char_p), C.c_int32,
                                  C.c_void_p, C.c_void_p, C.c_int32, C.c_int, C.c_double, C.c_int, C.c_int,
                                  C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
@@ -138,15 +141,17 @@ def wav_mono_f32(frames: np.ndarray, bits: int, is_float: bool = False) -> np.nd
 
 
 def fingerprint_batch(pcm: np.ndarray, offsets: np.ndarray, sample_rate: int = 8000, nthreads: int = 1,
-                      want_db: bool = True):
+                      want_db: bool = True, fft_variant: int = 0):
+    """fft_variant != 0: another valid fp32 FFT order (tfo_fingerprint_batch_variant)."""
     pcm = np.ascontiguousarray(pcm, dtype=np.int16)
     offsets = np.ascontiguousarray(offsets, dtype=np.int64)
     nclips = len(offsets) - 1
     total = int(sum(frame_count(int(offsets[i + 1] - offsets[i])) for i in range(nclips)))
     micro = np.zeros((total, 2), np.int32)
     db = np.zeros((total, 2), np.float64) if want_db else None
-    lib().tfo_fingerprint_batch(C.byref(tables(sample_rate)), pcm.ctypes.data, offsets.ctypes.data, nclips,
-                                micro.ctypes.data, db.ctypes.data if db is not None else None, nthreads)
+    lib().tfo_fingerprint_batch_variant(C.byref(tables(sample_rate)), pcm.ctypes.data, offsets.ctypes.data, nclips,
+                                        micro.ctypes.data, db.ctypes.data if db is not None else None, nthreads,
+                                        fft_variant)
     return micro, db
 
 

@@ -53,6 +53,12 @@ size_t tfo_fingerprint_f32(const tfo_tables* t, const float* x, size_t n, float*
 size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
                              int nclips, int32_t* micro, double* db, int nthreads);
 
+/* The same with another valid fp32 FFT order in place of the canonical one (0), to measure how
+ * much the unpinned FFT backend can move the stored values: 1 = radix-2 256-point complex FFT +
+ * the canonical real split, 2 = radix-2 512-point complex FFT of the real input. */
+size_t tfo_fingerprint_batch_variant(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
+                                     int nclips, int32_t* micro, double* db, int nthreads, int variant);
+
 /* fp_search_fingerprint_info over an in-memory audio_fingerprint table.
  *   rows:    m1/m2 micro-units (TFO_NULL = SQL NULL), row_clip = clip index
  *   uuids:   clip index -> audio_uuid string (tie-break: greatest string wins)

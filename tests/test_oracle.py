@@ -164,3 +164,20 @@ def test_sorted_index_search_equals_linear_scan(oracle):
             a, b = qoff[i], qoff[i + 1]
             found, ww, mm, _ = oracle.search(m1, m2, clip, uuids, q1[a:b], q2[a:b], coefs, tol, low, high)
             assert (w[i] >= 0) == found and (not found or (w[i], mc[i]) == (ww, mm)), (i, coefs, tol)
+
+
+@pytest.mark.parametrize("variant", [1, 2])
+def test_fft_order_variants_are_valid_dfts(oracle, variant):
+    """The sensitivity study's other FFT orders (scripts/fft_sensitivity.py) are correct DFTs: the
+    same float64 agreement as the canonical order, and stored values within a few micro-units."""
+    import dsp_f64
+    rng = np.random.default_rng(3)
+    t = np.arange(8000 * 4)
+    pcm = (6000 * np.sin(2 * np.pi * 440 * t / 8000) + 2500 * np.sin(2 * np.pi * 1234.5 * t / 8000)
+           + rng.normal(0, 800, len(t))).astype(np.int16)
+    base, db0 = oracle.fingerprint_batch(pcm, np.array([0, len(pcm)]))
+    mic, db = oracle.fingerprint_batch(pcm, np.array([0, len(pcm)]), fft_variant=variant)
+    ref = dsp_f64.fingerprint_f64(pcm, oracle.table_arrays())
+    np.testing.assert_allclose(10 ** (db / 10), np.abs(ref), rtol=3e-5, atol=2e-3)
+    assert np.abs(mic.astype(np.int64) - base.astype(np.int64)).max() <= 5
+    assert (mic != base).any()  # a different rounding pattern, not the same code path
