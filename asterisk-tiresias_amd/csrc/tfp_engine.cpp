@@ -143,6 +143,8 @@ struct tfp_engine {
   int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
   bool small_sync = true;     // TFP_SMALL_SYNC=0: batch-1 spins on the published result instead of a stream sync
   bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
+  DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
+  LogFix logfix{nullptr, nullptr, 0};
   ~tfp_engine() {
     if (qoff_ev) (void)hipEventDestroy(qoff_ev);
   }
@@ -167,7 +169,26 @@ int fail(tfp_engine* e, int code, const char* fmt, ...) {
     if (_st != hipSuccess) return fail((e), TFP_E_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
   } while (0)
 
+// The device copy of the glibc log correction table (frame values == glibc's 10*log10|c|).
+int ensure_logfix(tfp_engine* e) {
+  if (e->logfix.n) return TFP_OK;
+  const uint32_t* k;
+  const double* v;
+  int32_t n;
+  log_fix_table(&k, &v, &n);
+  if (n <= 0) return TFP_OK;
+  HIPCHK(e, e->logfix_key.reserve(sizeof(uint32_t) * n));
+  HIPCHK(e, e->logfix_val.reserve(sizeof(double) * n));
+  HIPCHK(e, hipMemcpyAsync(e->logfix_key.p, k, sizeof(uint32_t) * n, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->logfix_val.p, v, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  e->logfix = LogFix{e->logfix_key.as<uint32_t>(), e->logfix_val.as<double>(), n};
+  return TFP_OK;
+}
+
 int ensure_tables(tfp_engine* e, int sr, const DspTables** out, bool* fixed8k = nullptr) {
+  int rc0 = ensure_logfix(e);
+  if (rc0) return rc0;
   auto it = e->tables.find(sr);
   if (it == e->tables.end()) {
     DspTables host;
@@ -212,8 +233,10 @@ int upload(tfp_engine* e, DevBuf& d, const void* h, size_t bytes, hipStream_t s 
 
 // Fingerprint host samples (int16 PCM, or with f32 the fp32 values aubio_source produced);
 // leaves micro/db on the device in e->micro / e->db.
+// exact_q: the frame values (e->db) equal glibc's 10*log10|c| bit for bit (LogFix lookups); a
+// coefs = 1 search needs only their truncation, which is exact either way.
 int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nclips, int32_t sr,
-                     int64_t* nframes_out, std::vector<int64_t>* foff_out) {
+                     int64_t* nframes_out, std::vector<int64_t>* foff_out, bool exact_q = true) {
   const size_t ss = f32 ? sizeof(float) : sizeof(int16_t);
   const char* src = static_cast<const char*>(pcm);
   const DspTables* T;
@@ -277,11 +300,12 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
   }
   if (f32)
     HIPCHK(e, launch_fingerprint_f32(e->fpcfg, T, static_cast<const float*>(d_pcm), d_soff, d_soff + 1, d_foff, d_toff, d_tclip,
-                                     toff[nclips], e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+                                     toff[nclips], e->micro.as<int32_t>(), e->db.as<double>(), e->stream,
+                                     exact_q ? e->logfix : LogFix{}));
   else
     HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
                                  d_toff, d_tclip, toff[nclips], nf, e->micro.as<int32_t>(), e->db.as<double>(),
-                                 e->stream));
+                                 e->stream, exact_q ? e->logfix : LogFix{}));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
   return TFP_OK;
@@ -845,7 +869,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
-                               p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s));
+                               p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s, e->logfix));
   return TFP_OK;
 }
 
@@ -1081,7 +1105,7 @@ int search_samples_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t*
   std::vector<unsigned long long> keys(nq, 0ull);
   if (valid_params(P) && nq && foff[nq] > 0) {
     int64_t nf;
-    int rc = fingerprint_host(e, pcm, f32, offsets, nq, sr, &nf, nullptr);
+    int rc = fingerprint_host(e, pcm, f32, offsets, nq, sr, &nf, nullptr, P->coefs == 2);
     if (rc) return rc;
     if ((rc = search_core(e, foff.data(), nq, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
     e->stage_pending = false;  // search_core waited for e->stream (keys on the host)
@@ -1116,7 +1140,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
-                               e->db.as<double>(), s));
+                               e->db.as<double>(), s, P->coefs == 2 ? e->logfix : LogFix{}));
   std::vector<unsigned long long> keys;
   return search_core(e, p->foff.data(), p->nclips, e->db.as<double>(), P, keys,
                      reinterpret_cast<unsigned long long*>(d_keys), s);
@@ -1271,7 +1295,8 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
                                reinterpret_cast<const int64_t*>(d + b_pcm + 2 * b_sb),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo + b_to), to[na], fo[na],
-                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream));
+                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream,
+                               P->coefs == 2 ? e->logfix : LogFix{}));
   const std::vector<int64_t> fov(fo, fo + na + 1);  // (the pinned buffer is rewritten next tick)
   std::vector<unsigned long long> keys;
   if ((rc = search_core(e, fov.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;

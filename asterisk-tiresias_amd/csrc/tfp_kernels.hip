@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
     const DspTables* __restrict__ T, const Smp* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip,
-    int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db) {
+    int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db, LogFix fx) {
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
   const int tid = threadIdx.x;
@@ -385,6 +385,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
   int c = b < ntiles ? tclip[b] : 0;
   int64_t f0 = b < ntiles ? (int64_t)(b - toff[c]) * kWaveFrames : 0;
   fetch_pass(pass_src(c, f0, 0), b < ntiles, lane, pf);
+  uint32_t dense_rows = 0;  // rows of this tile redone by the dense filterbank (wave-uniform)
   for (; b < ntiles; b += nwaves) {
     const int64_t nf = (send[c] - sbeg[c] + kHop - 1) / kHop;
     const int cur_c = c;
@@ -506,11 +507,36 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
           const float lC = aubio_log10_fast(aC, S.logf);
           if (fC >= 0) lrow[fC] = lC;
         }
+        // A non-finite |X| bin or band sum (fp32 samples near FLT_MAX, or inf / NaN samples of a
+        // float WAV): aubio's dense fmat_vecmul multiplies every bin by every filter's weight, so
+        // 0 * inf = NaN reaches bands the sparse slots skip, and fvec_log10 passes NaN and inf
+        // through (the fast log assumes finite sums). Such frames are redone densely, in bin
+        // order, with the full clamped log (wave-uniform test, never taken for int16 PCM).
+        bool bad = !(aA <= 3.40282347e38f) || !(aB <= 3.40282347e38f) || !(aC <= 3.40282347e38f);
+        for (int i = L; i < kBins; i += 16) bad |= !(N[i] <= 3.40282347e38f);
+        const unsigned long long bm = __ballot(bad);
+        if (__builtin_expect(bm != 0, 0)) {
+          wave_sync();  // every lane's sparse results are in the row before it is rewritten
+          if ((bm >> (16 * grp)) & 0xffffull) {
+            for (int j = L; j < kFilters; j += 16) {
+              const int st = T->mel_start[j], len = T->mel_len[j], off = T->mel_off[j];
+              float acc = 0.f;
+              for (int i = 0; i < kBins; i++) {
+                const float w = (i >= st && i < st + len) ? T->mel_w[off + i - st] : 0.f;
+                acc = acc + N[i] * w;
+              }
+              lrow[j] = aubio_log10_clamped(acc, S.logf);
+            }
+          }
+#pragma unroll
+          for (int g = 0; g < 4; g++)
+            if ((bm >> (16 * g)) & 0xffffull) dense_rows |= 1u << (sub * 4 + g);
+        }
       }
     }
     wave_sync();
     if (c_defer) {  // the deferred slot-2 logs: lane = (frame row, filter)
-      if (lane < 2 * kWaveFrames) {
+      if (lane < 2 * kWaveFrames && !((dense_rows >> (lane >> 1)) & 1u)) {
         const int f = S.c_real[lane & 1];
         if (f >= 0) {
           float* p = M.logs + (lane >> 1) * kLogStride + f;
@@ -529,13 +555,22 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
         float acc = 0.f;
 #pragma unroll 8
         for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cf][i];
-        const double q = db_of_coef(acc);
+        const double q = db ? db_of_coef(acc, fx) : db_of_coef(acc);  // frame values glibc-exact
         const int64_t g = foff[cur_c] + f;
         micro[2 * g + cf] = micro_of_db(q);
         if (db) db[2 * g + cf] = q;
       }
     }
     wave_sync();  // the log buffer is rewritten by the next tile
+    if (__builtin_expect(dense_rows != 0, 0)) {  // dense rows overwrote the empty filters' constant
+      const float lempty = aubio_log10_fast(0.f, S.logf);
+      for (int i = lane; i < kWaveFrames * kFilters; i += 64) {
+        const int r = i / kFilters, j = i % kFilters;
+        if (((dense_rows >> r) & 1u) && T->mel_len[j] == 0) M.logs[r * kLogStride + j] = lempty;
+      }
+      dense_rows = 0;
+      wave_sync();
+    }
     c = cn;
     f0 = fn0;
   }
@@ -606,7 +641,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
-    float rare_thr) {
+    float rare_thr, LogFix fx) {
   constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
   // dB + "%f" in finish_db_kernel for throughput launches (full waves); in the tile tail for small
   // ones (4-frame tiles, batch-1 latency), which saves a launch
@@ -883,7 +918,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         if constexpr (kSplitTail) {
           micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
         } else {
-          const double q = db_of_coef(acc);
+          const double q = db ? db_of_coef(acc, fx) : db_of_coef(acc);  // frame values glibc-exact
           micro[2 * g + cfi] = micro_of_db(q);
           if (db) db[2 * g + cfi] = q;
         }
@@ -897,9 +932,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 // 10*log10|c| (fp_handler.c:651) and "%f" micro-units / NULL (db_ctx_handler.c:479-481) of every
 // coefficient fingerprint8k_kernel stored (as float bits) in micro[], in place, on full waves: the
 // kernel's tile tail would run this double-precision work on 32 of 64 lanes.
-__global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict__ db, int64_t nvals) {
+__global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict__ db, int64_t nvals, LogFix fx) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvals; i += (int64_t)gridDim.x * blockDim.x) {
-    const double q = db_of_coef(__builtin_bit_cast(float, micro[i]));
+    const float c = __builtin_bit_cast(float, micro[i]);
+    const double q = db ? db_of_coef(c, fx) : db_of_coef(c);  // frame values glibc-exact
     micro[i] = micro_of_db(q);
     if (db) db[i] = q;
   }
@@ -959,7 +995,7 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
 hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
-                              int32_t* d_micro, double* d_db, hipStream_t s) {
+                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx) {
   const bool v8 = fixed8k && (tile_frames == 4 || !cfg.force_generic);
   if (v8 ? !(tile_frames == 4 || tile_frames == kTile8k) : tile_frames != kFramesPerBlock) return hipErrorInvalidValue;
   if (ntiles <= 0) return hipSuccess;
@@ -970,32 +1006,32 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
   if (v8) {
     if (tile_frames == 4) {  // fingerprint8k_kernel<1> finishes its own tail
       hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx);
     } else {
       hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg,
-                         d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr);
+                         d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx);
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;
-      if (nv > 0) hipLaunchKernelGGL(finish_db_kernel, dim3((unsigned)g), dim3(256), 0, s, d_micro, d_db, nv);
+      if (nv > 0) hipLaunchKernelGGL(finish_db_kernel, dim3((unsigned)g), dim3(256), 0, s, d_micro, d_db, nv, fx);
     }
     return hipGetLastError();
   }
   hipLaunchKernelGGL(fingerprint_kernel<int16_t>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db);
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, fx);
   return hipGetLastError();
 }
 
 hipError_t launch_fingerprint_f32(const FpLaunchCfg& cfg, const DspTables* d_tables, const float* d_x,
                                   const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                                   const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro,
-                                  double* d_db, hipStream_t s) {
+                                  double* d_db, hipStream_t s, const LogFix& fx) {
   if (ntiles <= 0) return hipSuccess;
   if (cfg.grid_cap_f32 <= 0) return hipErrorInvalidValue;
   const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;
   const int grid = want < cfg.grid_cap_f32 ? want : cfg.grid_cap_f32;
   hipLaunchKernelGGL(fingerprint_kernel<float>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_x, d_sbeg, d_send,
-                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db);
+                     d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, fx);
   return hipGetLastError();
 }
 

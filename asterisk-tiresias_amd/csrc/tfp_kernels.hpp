@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tfp_math.hpp"
 #include "tfp_tables.hpp"
 
 namespace tfp {
@@ -65,13 +66,15 @@ bool DspTables_fixed8k(const DspTables& t);
 hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
-                              int32_t* d_micro, double* d_db, hipStream_t s);
+                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx);
+// fx: the glibc log correction table (device copy; tfp_math.hpp LogFix) used for d_db's frame
+// values, so they equal glibc's 10*log10|c| bit for bit (the stored micro-units need none).
 // fp32 samples (the values aubio_source_do produces: multichannel mean, 24/32-bit or float
 // WAV, tfp_wav_decode_f32) through the generic kernel, 16-frame tiles; same outputs as above.
 hipError_t launch_fingerprint_f32(const FpLaunchCfg& cfg, const DspTables* d_tables, const float* d_x,
                                   const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                                   const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int32_t* d_micro,
-                                  double* d_db, hipStream_t s);
+                                  double* d_db, hipStream_t s, const LogFix& fx);
 
 hipError_t launch_synth(const SynthSpecDev* d_specs, int32_t nclips, int64_t spc, int16_t* d_out, hipStream_t s);
 

@@ -180,8 +180,34 @@ TFP_HD double log_acc(double x) {
   return s + (err + lo);
 }
 
-// glibc 2.35 log10 = fdlibm e_log10.c wrapper; the inner log is log_acc() above.
-TFP_HD double log10_glibc_wrapper(double x) {
+// glibc's inner log differs from log_acc on 58,054 of the 2^24 reduced arguments the wrapper
+// below can see for a float input (the double of a float has 29 zero low mantissa bits; the
+// reduced argument is its mantissa in [1, 2) or [0.5, 1)). LogFix lists them, keyed
+// i << 23 | mantissa23 (i = 1 for [0.5, 1)), with glibc's value: built on the host from glibc
+// itself (tfp_tables.cpp build_log_fix), ascending keys. n = 0: no table (log_acc everywhere).
+struct LogFix {
+  const uint32_t* key;
+  const double* val;
+  int32_t n;
+};
+
+TFP_HD double log_fixed(double x, int32_t i, const LogFix& fx) {
+  if (fx.n > 0 && (d2u(x) & 0x1fffffffull) == 0) {  // (a float's double: the table's domain)
+    const uint32_t k = ((uint32_t)i << 23) | (uint32_t)((d2u(x) >> 29) & 0x7fffffu);
+    int32_t lo = 0, hi = fx.n;
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (fx.key[mid] < k) lo = mid + 1; else hi = mid;
+    }
+    if (lo < fx.n && fx.key[lo] == k) return fx.val[lo];
+  }
+  return log_acc(x);
+}
+
+// glibc 2.35 log10 = fdlibm e_log10.c wrapper; the inner log is log_acc() above, or glibc's own
+// value where the LogFix table lists it (then the result is glibc's, bit for bit, for every
+// double of a float: tests/native/check_logfix.cpp).
+TFP_HD double log10_glibc_wrapper(double x, const LogFix& fx = LogFix{nullptr, nullptr, 0}) {
   const double two54 = 1.80143985094819840000e+16;
   const double ivln10 = 4.34294481903251816668e-01;
   const double log10_2hi = 3.01029995663611771306e-01;
@@ -204,14 +230,16 @@ TFP_HD double log10_glibc_wrapper(double x) {
   hx = (hx & 0x000fffff) | ((0x3ff - i) << 20);
   const double y = (double)(k + i);
   x = u2d(((uint64_t)(uint32_t)hx << 32) | (d2u(x) & 0xffffffffull));
-  const double z = y * log10_2lo + ivln10 * log_acc(x);
+  const double z = y * log10_2lo + ivln10 * log_fixed(x, i, fx);
   return z + y * log10_2hi;
 }
 
-// `10 * log10(fabs((double)c))` of /root/reference/src/fp_handler.c:651.
-TFP_HD double db_of_coef(float c) {
+// `10 * log10(fabs((double)c))` of /root/reference/src/fp_handler.c:651. Without a LogFix table
+// the value may differ from glibc's in its last bit (152,867 floats), never in its "%f" micro-units
+// or its truncation (what the stored rows and the max1 keys use); with the table it is glibc's.
+TFP_HD double db_of_coef(float c, const LogFix& fx = LogFix{nullptr, nullptr, 0}) {
   const double a = (double)c;
-  return 10.0 * log10_glibc_wrapper(a < 0.0 ? -a : a);
+  return 10.0 * log10_glibc_wrapper(a < 0.0 ? -a : a, fx);
 }
 
 // ---------------------------------------------------------------------------------------

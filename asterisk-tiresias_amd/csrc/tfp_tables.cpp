@@ -1,7 +1,10 @@
 // tfp_tables.cpp — host construction of DspTables (see tfp_tables.hpp for provenance).
 // Compiled with -ffp-contract=off -fno-builtin so every float expression rounds where the
 // C source of libaubio rounds and cosf/powf are glibc's run-time functions.
+#include <mutex>
+#include <vector>
 #include "tfp_tables.hpp"
+#include "tfp_math.hpp"
 
 #include <math.h>
 #include <string.h>
@@ -234,6 +237,26 @@ bool build_tables(int sample_rate, DspTables* t) {
       t->lane_tw_im[k1][L] = t->tw256_im[(L * k1) & 255];
     }
   return true;
+}
+
+void log_fix_table(const uint32_t** keys, const double** vals, int32_t* n) {
+  static std::vector<uint32_t> K;
+  static std::vector<double> V;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (uint32_t i = 0; i < 2; i++)
+      for (uint32_t m = 0; m < (1u << 23); m++) {
+        const double x = u2d(((uint64_t)(0x3ff - i) << 52) | ((uint64_t)m << 29));
+        const double want = log(x);  // glibc (built with -fno-builtin: no compile-time folding)
+        if (d2u(log_acc(x)) != d2u(want)) {
+          K.push_back((i << 23) | m);
+          V.push_back(want);
+        }
+      }
+  });
+  *keys = K.data();
+  *vals = V.data();
+  *n = (int32_t)K.size();
 }
 
 }  // namespace tfp

@@ -54,5 +54,8 @@ struct DspTables {
 // Dense filterbank as aubio lays it out (40 x 257), for tests.
 void build_mel_dense(int sample_rate, float (*mel)[kBins]);
 bool build_tables(int sample_rate, DspTables* t);
+// The reduced arguments where log_acc differs from this host's glibc log, with glibc's value
+// (tfp_math.hpp LogFix), ascending keys; computed once per process (~0.3 s).
+void log_fix_table(const uint32_t** keys, const double** vals, int32_t* n);
 
 }  // namespace tfp

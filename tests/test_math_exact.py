@@ -28,3 +28,21 @@ def test_exhaustive_log_committed():
     assert "2139095039 floats" in log and "0 fmt6 mismatches, 0 trunc mismatches" in log
     assert "aubio_log10_fast vs aubio_log10_clamped : 0 / 2139095041 mismatches" in log
     assert log.strip().endswith("OK")
+
+
+def test_logfix_sampled(tmp_path):
+    """The frame values with the LogFix table == glibc's 10*log10|c| (sampled; the exhaustive
+    run over every positive float is tests/native/check_logfix_exhaustive.log)."""
+    exe = str(tmp_path / "check_logfix")
+    subprocess.run(["g++", "-O2", "-std=c++20", "-ffp-contract=off", "-fno-builtin", "-fopenmp",
+                    os.path.join(NATIVE, "check_logfix.cpp"),
+                    os.path.join(REPO, "asterisk-tiresias_amd", "csrc", "tfp_tables.cpp"), "-o", exe, "-lm"], check=True)
+    out = subprocess.run([exe, "997"], capture_output=True, text=True, timeout=300)
+    print(out.stdout)
+    assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout
+
+
+def test_logfix_exhaustive_log_committed():
+    log = open(os.path.join(NATIVE, "check_logfix_exhaustive.log")).read()
+    assert "10*log10|c| with LogFix vs glibc : 0 / 2139095039 mismatches" in log
+    assert log.strip().endswith("OK")
