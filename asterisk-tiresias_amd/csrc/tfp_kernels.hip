@@ -13,6 +13,7 @@
 
 #include "tfp_kernels.hpp"
 #include "tfp_math.hpp"
+#include "tfp_split.hpp"
 #include "tfp_synth.hpp"
 
 namespace tfp {
@@ -590,12 +591,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
 //     scalings; proof in DESIGN.md §4); bins with 0 < |S|^2 < 2^-98 (where the scaling or the
 //     fast sqrt could round differently) take the spec sequence in a wave-uniform slow path;
 //   * filterbank products formed in pairs (v_pk_mul_f32 on the b128 halves), sums sequential.
-__device__ __forceinline__ float hadd(cf v) {  // v.x + v.y as one v_add_f32 (no pair repacking)
-  float r;
-  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(v.x), "v"(v.y));
-  return r;
-}
-
 // dft16 with the W16^4 = (0, -1) multiply as (y, -x).
 __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], cf (&out)[16]) {
   cf A[4][4];
@@ -704,10 +699,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int wL = (tid >> 1) & 15, wn1 = 2 * (tid >> 5) + (tid & 1);
   const int wj = (32 * wn1 + 2 * wL + 256) & 511;
   const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
-  // [k2][L] = (w512^k, w512^(256 - k)), k = L + 16 k2 (k2 < 8; lane 0 at k2 = 0: k = 128)
+  // [k2][L] = (re w512^k, re w512^k', im w512^k, im w512^k'), k = L + 16 k2, k' = 256 - k (k2 < 8;
+  // lane 0 at k2 = 0: k = 128): the pair layout of split_pair_sq
   const int tk2 = tid >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
-  const int tk = (tid & 1) ? 256 - tkk : tkk;
-  const float twre = T->tw512_re[tk], twim = T->tw512_im[tk];
+  const float* tws = (tid & 1) ? T->tw512_im : T->tw512_re;
+  const float twk = tws[tkk], twk2 = tws[256 - tkk];
   const int li = tid < 240 ? tid : 239, lk1 = 1 + li / 16, lL = li % 16;
   const float ltre = T->lane_tw_re[lk1][lL], ltim = T->lane_tw_im[lk1][lL];
   const int i10 = tid < 10 ? tid : 9;
@@ -727,7 +723,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   }
   const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
   winr[tid] = cf{win0, win1};
-  twr[tid] = cf{twre, twim};
+  twr[tid] = cf{twk, twk2};
   if (tid < 240) S.lane_tw[lk1 - 1][lL] = cf{ltre, ltim};
   if (tid < 10) S.w16[tid] = cf{w16re, w16im};
   if (tid < kCoefs * kFilters) (&S.dct[0][0])[tid] = dctv;
@@ -830,30 +826,25 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       for (int k2 = 0; k2 < 8; k2++) Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};
       // bins 0 and 256 (lane 0) from Z[0], taken now so Y[0] is not kept alive
       const float n0 = 2.f * fabsf(Y[0].x + Y[0].y), n256 = 2.f * fabsf(Y[0].x - Y[0].y);
-      uint32_t umin = 0xffffffffu;  // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top
+      // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top. (On |S|^2 itself, not on its
+      // v_sqrt_f32: that returns 0 for denormal inputs; tests/native/check_fast_sqrt.hip.)
+      uint32_t umin = 0xffffffffu;
 #pragma unroll
       for (int k2 = 0; k2 < 8; k2++) {
-        cf own = Y[k2 == 0 ? 8 : 16 - k2];
-        asm("" : "+v"(own.x), "+v"(own.y));  // a value: the selects stay v_cndmask
+        const cf own = Y[k2 == 0 ? 8 : 16 - k2];
         cf y = Y[k2];
         if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
         const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
         const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
-        const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
-        const cf E = addsub(y, p);
-        const cf O = subadd(y, p);
-        const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-        const cf Sv = E + Tt;
-        const cf O2 = cf{-O.x, O.y};
-        const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
-        const cf S2 = cf{E.x, -E.y} + T2;
-        const float x = hadd(Sv * Sv), x2 = hadd(S2 * S2);
+        const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
+        float nk, nk2;
+        sqrt_pair_cr(sq, nk, nk2);
+        umin = min(umin, min(__builtin_bit_cast(uint32_t, sq.x) - 1u, __builtin_bit_cast(uint32_t, sq.y) - 1u));
         const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-        // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top) go to the spec's order below
-        umin = min(umin, min(__builtin_bit_cast(uint32_t, x) - 1u, __builtin_bit_cast(uint32_t, x2) - 1u));
-        N[k] = sqrtf_fast_cr(x);
-        N[256 - k] = sqrtf_fast_cr(x2);
+        N[k] = nk;
+        N[256 - k] = nk2;
       }
+      // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order below
       if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
 #pragma unroll
         for (int k2 = 0; k2 < 8; k2++) {
@@ -862,18 +853,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           if (k2 == 0 && L == 0) y = own;
           const cf p = L == 0 ? own : Pq[k2];
           const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2);
-          const cf w = cf{t4.x, t4.y}, w2 = cf{t4.z, t4.w};
-          const cf E = addsub(y, p);
-          const cf O = subadd(y, p);
-          const cf Tt = addsub(O * cf{w.y, w.y}, swap(O) * cf{w.x, w.x});
-          const cf Sv = E + Tt;
-          const cf O2 = cf{-O.x, O.y};
-          const cf T2 = addsub(O2 * cf{w2.y, w2.y}, swap(O2) * cf{w2.x, w2.x});
-          const cf S2 = cf{E.x, -E.y} + T2;
-          const float x = Sv.x * Sv.x + Sv.y * Sv.y, x2 = S2.x * S2.x + S2.y * S2.y;
+          const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
+          const cf w = cf{t4.x, t4.z}, w2 = cf{t4.y, t4.w};
           const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-          if (x > 0.f && x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
-          if (x2 > 0.f && x2 < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
+          if (sq.x > 0.f && sq.x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
+          if (sq.y > 0.f && sq.y < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
         }
       }
       if (L == 0) {
