@@ -591,7 +591,16 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint_kerne
 //     scalings; proof in DESIGN.md §4); bins with 0 < |S|^2 < 2^-98 (where the scaling or the
 //     fast sqrt could round differently) take the spec sequence in a wave-uniform slow path;
 //   * filterbank products formed in pairs (v_pk_mul_f32 on the b128 halves), sums sequential.
-// dft16 with the W16^4 = (0, -1) multiply as (y, -x).
+// dft16 with the W16^4 = (0, -1) multiply of A[2][2] as (y, -x), folded into the dft4 that takes
+// it as a2: t0 = a0 + (y, -x) = addsub(a0, swap(A)), t1 = a0 - (y, -x) = subadd(a0, swap(A)),
+// the same two roundings (c + (-p) == c - p), with no negation or move.
+__device__ __forceinline__ void dft4_rot_a2(cf a0, cf a1, cf A2, cf a3, cf& X0, cf& X1, cf& X2, cf& X3) {
+  const cf t0 = addsub(a0, swap(A2)), t1 = subadd(a0, swap(A2)), t2 = a1 + a3, t3 = a1 - a3;
+  X0 = t0 + t2;
+  X2 = t0 - t2;
+  X1 = addsub(t1, swap(t3));
+  X3 = subadd(t1, swap(t3));
+}
 __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], cf (&out)[16]) {
   cf A[4][4];
 #pragma unroll
@@ -599,16 +608,18 @@ __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], 
 #pragma unroll
   for (int n2 = 1; n2 < 4; n2++)
 #pragma unroll
-    for (int k1 = 1; k1 < 4; k1++) {
-      if (n2 * k1 == 4) A[n2][k1] = cf{A[n2][k1].y, -A[n2][k1].x};
-      else A[n2][k1] = cmul(A[n2][k1], w16[n2 * k1]);
-    }
+    for (int k1 = 1; k1 < 4; k1++)
+      if (n2 * k1 != 4) A[n2][k1] = cmul(A[n2][k1], w16[n2 * k1]);
 #pragma unroll
-  for (int k1 = 0; k1 < 4; k1++) dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
+  for (int k1 = 0; k1 < 4; k1++) {
+    if (k1 == 2) dft4_rot_a2(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
+    else dft4(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
+  }
 }
 
 // Filterbank sum over LEN bins (multiple of 4), weights already in registers, products in
-// pairs: acc = (((acc + n0 w0) + n1 w1) + n2 w2) + ... in ascending bin order.
+// pairs: acc = (((0 + n0 w0) + n1 w1) + n2 w2) + ... in ascending bin order. Every product is
+// >= +0 (half weights >= 0, |X| from sqrt of a sum of squares), so 0 + n0 w0 is n0 w0 bitwise.
 template <int LEN>
 __device__ __forceinline__ float mel_sum_w(const float* __restrict__ N, const float4 (&wv)[LEN / 4], int st) {
   float4 nv[LEN / 4];
@@ -619,7 +630,8 @@ __device__ __forceinline__ float mel_sum_w(const float* __restrict__ N, const fl
   for (int i = 0; i < LEN / 4; i++) {
     const cf p01 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].y};
     const cf p23 = cf{nv[i].z, nv[i].w} * cf{wv[i].z, wv[i].w};
-    acc = acc + p01.x; acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
+    acc = i == 0 ? p01.x : acc + p01.x;
+    acc = acc + p01.y; acc = acc + p23.x; acc = acc + p23.y;
   }
   return acc;
 }
@@ -829,13 +841,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top. (On |S|^2 itself, not on its
       // v_sqrt_f32: that returns 0 for denormal inputs; tests/native/check_fast_sqrt.hip.)
       uint32_t umin = 0xffffffffu;
+      const float4* tw4 = reinterpret_cast<const float4*>(twr + 2 * L + oz);  // + 16 k2: one base, immediate offsets
 #pragma unroll
       for (int k2 = 0; k2 < 8; k2++) {
         const cf own = Y[k2 == 0 ? 8 : 16 - k2];
         cf y = Y[k2];
         if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
         const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
-        const float4 t4 = *reinterpret_cast<const float4*>(twr + (k2 * 16 + L) * 2 + oz);
+        const float4 t4 = tw4[16 * k2];
         const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
         float nk, nk2;
         sqrt_pair_cr(sq, nk, nk2);

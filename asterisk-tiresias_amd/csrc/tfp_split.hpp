@@ -20,18 +20,18 @@ typedef float cf2 __attribute__((ext_vector_type(2)));
 // (|S_k|^2, |S_k'|^2) with S = 2X: (fl(S.re^2) + fl(S.im^2)) per bin.
 //   WX = (re w512^k, re w512^k'), WY = (im w512^k, im w512^k').
 __device__ __forceinline__ cf2 split_pair_sq(cf2 y, cf2 p, cf2 WX, cf2 WY) {
-  const cf2 EOr = __builtin_elementwise_fma(cf2{p.x, p.x}, cf2{1.f, -1.f}, cf2{y.x, y.x});  // (E.re, O.re)
-  const cf2 EOi = __builtin_elementwise_fma(cf2{p.y, p.y}, cf2{-1.f, 1.f}, cf2{y.y, y.y});  // (E.im, O.im)
-  const cf2 A1 = cf2{EOr.y, EOr.y} * WY;  // (O.re wy, O.re wy')
-  const cf2 A2 = cf2{EOi.y, EOi.y} * WX;  // (O.im wx, O.im wx')
-  const cf2 A3 = cf2{EOi.y, EOi.y} * WY;  // (O.im wy, O.im wy')
-  const cf2 A4 = cf2{EOr.y, EOr.y} * WX;  // (O.re wx, O.re wx')
+  const cf2 E = __builtin_elementwise_fma(p, cf2{1.f, -1.f}, y);  // (a + Px, b - Py)
+  const cf2 O = __builtin_elementwise_fma(p, cf2{-1.f, 1.f}, y);  // (a - Px, b + Py)
+  const cf2 A1 = cf2{O.x, O.x} * WY;  // (O.re wy, O.re wy')
+  const cf2 A2 = cf2{O.y, O.y} * WX;  // (O.im wx, O.im wx')
+  const cf2 A3 = cf2{O.y, O.y} * WY;  // (O.im wy, O.im wy')
+  const cf2 A4 = cf2{O.x, O.x} * WX;  // (O.re wx, O.re wx')
   // T.re = O.re wy + O.im wx;      T'.re = (-O.re) wy' + O.im wx'
   const cf2 TR = __builtin_elementwise_fma(A1, cf2{1.f, -1.f}, A2);
   // T.im = O.im wy - O.re wx;      T'.im = O.im wy' - (-O.re) wx'
   const cf2 TI = __builtin_elementwise_fma(A4, cf2{-1.f, 1.f}, A3);
-  const cf2 SR = cf2{EOr.x, EOr.x} + TR;                                      // E.re + T.re, E.re + T'.re
-  const cf2 SI = __builtin_elementwise_fma(cf2{EOi.x, EOi.x}, cf2{1.f, -1.f}, TI);  // E.im + T.im, -E.im + T'.im
+  const cf2 SR = cf2{E.x, E.x} + TR;                                        // E.re + T.re, E.re + T'.re
+  const cf2 SI = __builtin_elementwise_fma(cf2{E.y, E.y}, cf2{1.f, -1.f}, TI);  // E.im + T.im, -E.im + T'.im
   return SR * SR + SI * SI;
 }
 
