@@ -641,6 +641,16 @@ __device__ __forceinline__ void load_w(const float* __restrict__ w, float4 (&wv)
   for (int i = 0; i < LEN / 4; i++) wv[i] = *reinterpret_cast<const float4*>(w + 64 * i);
 }
 
+// Phase stamps (experiment builds only, -DTFP_STAMPS): per-wave s_memtime deltas at the pass's
+// existing wave_syncs (no extra waits), printed by a few waves at exit.
+#ifdef TFP_STAMPS
+#define TFP_STAMP(i) const uint64_t ts##i = __builtin_amdgcn_s_memtime()
+#define TFP_ACC(i, a, b) st[i] += ts##b - ts##a
+#else
+#define TFP_STAMP(i)
+#define TFP_ACC(i, a, b)
+#endif
+
 // kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
 // small batches: 4x the waves on a short query, a quarter of the per-wave latency).
 template <int kPasses>
@@ -694,7 +704,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   };
 
   // The first tile's bounds and PCM are requested before the tables are staged, so their
-  // latency overlaps the staging (most of a small launch's time).
+  // latency overlaps the staging (most of a small launch's time). The PCM is prefetched one pass
+  // ahead (a two-pass distance measured no faster: the pass is bound by LDS traffic and latency,
+  // not by the PCM loads).
   int4 pf[kChunkRounds];
   int b = blockIdx.x * kBlockWaves + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
@@ -761,6 +773,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
+  // dft16's twiddles W16^e (e = 1, 2, 3, 6, 9 used) are wave-uniform: scalar loads, held in SGPRs
+  // for the kernel (no LDS read per pass)
+  cf w16r[10];
+#pragma unroll
+  for (int e = 0; e < 10; e++)
+    w16r[e] = cf{T->tw256_re[16 * e], T->tw256_im[16 * e]};
   // inter-stage lane twiddles w256^(L k1) held in registers (30 VGPRs) instead of read per pass
   cf ltw[15];
 #pragma unroll
@@ -773,6 +791,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
   }
 
+#ifdef TFP_STAMPS
+  uint64_t st[7] = {0, 0, 0, 0, 0, 0, 0};
+  uint64_t tprev = __builtin_amdgcn_s_memtime();
+  const uint64_t tstart = tprev;
+  int npass = 0;
+#endif
   for (; b < ntiles; b += nwaves) {
     const int64_t nf = (cur.ns + kHop - 1) / kHop;
     const int bn = b + nwaves;
@@ -781,6 +805,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     for (int sub = 0; sub < kPasses; sub++) {
       const int row = sub * 4 + grp;
       wave_sync();  // the previous pass's readers of the scratch are done
+      TFP_STAMP(0);
 #pragma unroll
       for (int r = 0; r < kChunkRounds; r++) {
         const int chunk = lane + 64 * r;
@@ -789,6 +814,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
       else fetch(nxt, 0, bn < ntiles, pf);
       wave_sync();
+      TFP_STAMP(1);
       const int16_t* hop0 = M.pcm + grp * kHopStride;
       // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
       // them into registers for the whole kernel (occupancy).
@@ -801,9 +827,6 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         wreg[2 * i] = cf{w4.x, w4.y};
         wreg[2 * i + 1] = cf{w4.z, w4.w};
       }
-      cf w16r[10];
-#pragma unroll
-      for (int e = 0; e < 10; e++) w16r[e] = S.w16[e + oz];
       // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
       // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
       // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
@@ -819,6 +842,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #pragma unroll
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
       wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
+      TFP_STAMP(2);
 #pragma unroll
       for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
       wave_sync();
@@ -826,6 +850,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
       dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       wave_sync();         // every lane has read its column of the square: W is free for |X|
+      TFP_STAMP(3);
       // Real split per conjugate pair on one lane: lane L (k2 < 8) owns bins k = L + 16 k2 and
       // 256 - k, whose Z values are its Y[k2] and Y[15 - k2] of lane 16 - L (8 ds_bpermute pairs).
       // Column 0 pairs inside lane 0: (16 k2, 256 - 16 k2) for k2 = 1..7 and (128, 128) at k2 = 0;
@@ -841,6 +866,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       // min over bins of bits(|S|^2) - 1: exact zeros wrap to the top. (On |S|^2 itself, not on its
       // v_sqrt_f32: that returns 0 for denormal inputs; tests/native/check_fast_sqrt.hip.)
       uint32_t umin = 0xffffffffu;
+      float nk[8], nk2[8];
       const float4* tw4 = reinterpret_cast<const float4*>(twr + 2 * L + oz);  // + 16 k2: one base, immediate offsets
 #pragma unroll
       for (int k2 = 0; k2 < 8; k2++) {
@@ -850,13 +876,18 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
         const float4 t4 = tw4[16 * k2];
         const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
-        float nk, nk2;
-        sqrt_pair_cr(sq, nk, nk2);
+        sqrt_pair_cr(sq, nk[k2], nk2[k2]);
         umin = min(umin, min(__builtin_bit_cast(uint32_t, sq.x) - 1u, __builtin_bit_cast(uint32_t, sq.y) - 1u));
-        const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-        N[k] = nk;
-        N[256 - k] = nk2;
       }
+      // |X| rows, addressed as bins L + 16 k2 and 256 - that for every lane (paired ds_write2_b32);
+      // lane 0's k2 = 0 pair is bin 128 twice (the partner-side value stands, below): its writes to
+      // bins 0 and 256 are overwritten by n0 and n256.
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) N[L + 16 * k2] = nk[k2];
+      float* const nrev = N + (144 - L);  // bin 256 - L - 16 k2 = nrev[16 (7 - k2)]: one base, immediate offsets
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) nrev[16 * (7 - k2)] = nk2[k2];
+      if (L == 0) N[128] = nk2[0];  // before the slow path below, which may redo bin 128
       // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order below
       if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
 #pragma unroll
@@ -879,6 +910,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
       for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
       wave_sync();
+      TFP_STAMP(4);
       // Filterbank: this lane's 3 filters (slots A, B, C) from the half weights, then the logs
       const float* wbase = S.ms_w + 4 * L + oz;
       float* lrow = M.logs + row * kLogStride;
@@ -893,6 +925,17 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       lrow[fA] = aubio_log10_fast(aA, S.logf);
       lrow[fB] = aubio_log10_fast(aB, S.logf);
       if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+#ifdef TFP_STAMPS
+      const uint64_t ts5 = __builtin_amdgcn_s_memtime();
+      st[0] += ts0 - tprev;  // previous pass's end (or the tail) to this pass's first wave_sync
+      TFP_ACC(1, 0, 1);      // PCM staging (prefetched registers -> LDS), next pass's loads issued
+      TFP_ACC(2, 1, 2);      // PCM reads, window, DFT16, lane twiddles
+      TFP_ACC(3, 2, 3);      // transpose square write + read, DFT16
+      TFP_ACC(4, 3, 4);      // partner exchange, real split, sqrt, |X| writes, rare test
+      TFP_ACC(5, 4, 5);      // filterbank + logs
+      tprev = ts5;
+      npass++;
+#endif
     }
     wave_sync();
     if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
@@ -924,6 +967,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     wave_sync();
     cur = nxt;
   }
+#ifdef TFP_STAMPS
+  if (lane == 0 && (blockIdx.x & 63) == 0)
+    printf("stamps block %d wave %d passes %d total %lu | lead %lu stage %lu fft1 %lu fft2 %lu split %lu mel %lu\n",
+           (int)blockIdx.x, wave, npass, (unsigned long)(tprev - tstart), (unsigned long)st[0], (unsigned long)st[1],
+           (unsigned long)st[2], (unsigned long)st[3], (unsigned long)st[4], (unsigned long)st[5]);
+#endif
 }
 
 // 10*log10|c| (fp_handler.c:651) and "%f" micro-units / NULL (db_ctx_handler.c:479-481) of every
