@@ -118,6 +118,22 @@ struct WaveLds {
 static_assert(sizeof(float) * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride, "pcm alias fits");
 static_assert(16 * kSq <= kFrameStride && 16 + 500 <= 2 * kFrameStride, "square and |X| rows (ms_maxbin <= 500) fit");
 
+// The 8 kHz kernel's per-wave scratch: the transpose square stored column-major with a row pitch
+// of 18 complex (lane L writes Y[k1] to [k1][L]; reads its column as 8 contiguous ds_read_b128,
+// conflict-free: lane L's 16-B pieces start at dword 36 L + 4 j, 16 distinct bank quads per lane
+// group), frames 288 complex apart; the odd frames' |X| rows 48 floats in, which gives the
+// filterbank reads the banks of the 272-complex layout (frames 0, 48, 0, 48 mod 64).
+constexpr int kSq8 = 18;
+constexpr int kFrameStride8 = 16 * kSq8;
+struct WaveLds8 {
+  union {
+    cf scratch[4][kFrameStride8];
+    alignas(16) int16_t pcm[5 * kHopStride];
+  };
+  float logs[kWaveFrames * kLogStride];
+};
+static_assert(2 * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride8 && 48 + 260 <= 2 * kFrameStride8, "8 kHz scratch");
+
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
 template <typename Smp>
 struct PassSrc {
@@ -665,7 +681,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   constexpr bool kSplitTail = kPasses >= 2;
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
-  __shared__ __attribute__((aligned(16))) WaveLds WL[kBlockWaves];
+  __shared__ __attribute__((aligned(16))) WaveLds8 WL[kBlockWaves];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
@@ -766,9 +782,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const unsigned long long empty_filters = __ballot(lane < kFilters && mlen == 0);  // (log of 0 + 2e-42)
   __syncthreads();
 
-  WaveLds& M = WL[wave];
+  WaveLds8& M = WL[wave];
   cf* W = M.scratch[grp];
-  float* N = reinterpret_cast<float*>(W) + 16 * (grp & 1);  // |X| row (see fingerprint_kernel)
+  float* N = reinterpret_cast<float*>(W) + 48 * (grp & 1);  // |X| row (WaveLds8)
   const int nwaves = gridDim.x * kBlockWaves;
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
@@ -844,10 +860,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
       TFP_STAMP(2);
 #pragma unroll
-      for (int k1 = 0; k1 < 16; k1++) W[L * kSq + k1] = Y[k1];
+      for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
       wave_sync();
 #pragma unroll
-      for (int n2 = 0; n2 < 16; n2++) z[n2] = W[n2 * kSq + L];
+      for (int n2 = 0; n2 < 16; n2 += 2) {
+        const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
+        z[n2] = cf{v.x, v.y};
+        z[n2 + 1] = cf{v.z, v.w};
+      }
       dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       wave_sync();         // every lane has read its column of the square: W is free for |X|
       TFP_STAMP(3);
@@ -989,7 +1009,7 @@ __global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict
 
 bool DspTables_fixed8k(const DspTables& t) {
   return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total == 16 * (36 + 16 + 8) &&
-         t.ms_total <= kMsLds && t.ms_c_defer == 1 &&
+         t.ms_total <= kMsLds && t.ms_c_defer == 1 && t.ms_maxbin <= 2 * kFrameStride8 - 48 &&
          t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
 }
 
