@@ -324,7 +324,8 @@ __device__ __forceinline__ float sqrtf_fast_cr(float x) {
 
 // Value of lane (16 - L) & 15 of this lane's 16-lane row (L = lane & 15). ds_bpermute: measured
 // faster than the two-DPP-mov form (row_mirror + row_ror:1, 0.937 vs 0.911 ms per C2 launch),
-// whose chained DPP reads cost wait states.
+// whose chained DPP reads cost wait states, and no slower than one row_mirror with renumbered
+// second-stage columns plus selects for the two self-paired columns (round 2: 0.486 vs 0.484 ms).
 __device__ __forceinline__ float partner16(float v) { return __shfl(v, (16 - (int)(threadIdx.x & 15)) & 15, 16); }
 
 template <typename Smp>
