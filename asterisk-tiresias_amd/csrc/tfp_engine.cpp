@@ -112,7 +112,10 @@ struct tfp_engine {
   // small host calls: packed upload + the small-batch search workspace
   HostBuf hstage;
   DevBuf dstage;
-  bool stage_pending = false;  // hstage may still be read by a copy on e->stream
+  HostBuf zstage;                   // mapped + coherent: small 8 kHz calls are read by the kernel in place
+  void* zstage_host = nullptr;      // the allocation zstage_dev was taken for
+  char* zstage_dev = nullptr;
+  bool stage_pending = false;  // hstage / zstage may still be read by a copy or kernel on e->stream
   HostBuf qoff_pin;                   // pinned source of the qoff copy
   std::vector<int64_t> qoff_host;     // what e->qoff holds (copied on stream qoff_stream)
   hipStream_t qoff_stream = nullptr;
@@ -266,21 +269,34 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
   const int64_t *d_soff, *d_foff;
   const int32_t *d_toff, *d_tclip;
   if (total <= ((size_t)8 << 20)) {
-    // small call: pack every array into pinned staging, one H2D copy (batch-1 latency)
+    // small call: pack every array into pinned staging, one H2D copy. The 4-frame-tile calls
+    // (a query, batch-1 latency) skip the copy: the kernel reads the mapped, coherent staging in
+    // place (a copy plus its hand-off to the kernel cost ~16 us before the first kernel started).
     // Every caller waits for e->stream before it returns and then clears stage_pending, so the
     // staging buffer is free here; after an error return the stream is drained first.
     if (e->stage_pending) HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, e->hstage.reserve(total));
-    HIPCHK(e, e->dstage.reserve(total));
-    char* h = e->hstage.as<char>();
+    const bool zero_copy = small;
+    char* h;
+    if (zero_copy) {
+      HIPCHK(e, e->zstage.reserve(total, hipHostMallocMapped | hipHostMallocCoherent));
+      if (e->zstage.p != e->zstage_host) {
+        HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&e->zstage_dev), e->zstage.p, 0));
+        e->zstage_host = e->zstage.p;
+      }
+      h = e->zstage.as<char>();
+    } else {
+      HIPCHK(e, e->hstage.reserve(total));
+      HIPCHK(e, e->dstage.reserve(total));
+      h = e->hstage.as<char>();
+    }
     if (ns) memcpy(h, src + ss * offsets[0], ss * ns);
     memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
     memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
     memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
     memcpy(h + b_pcm + b_so + b_fo + b_to, tclip.data(), sizeof(int32_t) * tclip.size());
-    HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
+    if (!zero_copy) HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
     e->stage_pending = true;
-    char* d = e->dstage.as<char>();
+    char* d = zero_copy ? e->zstage_dev : e->dstage.as<char>();
     d_pcm = d;
     d_soff = reinterpret_cast<const int64_t*>(d + b_pcm);
     d_foff = reinterpret_cast<const int64_t*>(d + b_pcm + b_so);
@@ -1167,9 +1183,11 @@ struct tfp_stream {
   int64_t W = 0;                 // window samples
   int64_t wpos = 0;              // ring position of the oldest sample of every window
   std::vector<int64_t> filled;   // samples of history per channel (saturates at W)
-  DevBuf ring, stage_d;          // stage_d: this tick's samples + window layout (one upload)
-  HostBuf stage_h;               // pinned source of that upload
-  bool stage_pending = false;    // stage_h may still be read by the last upload
+  DevBuf ring;
+  HostBuf stage_h;               // this tick's samples + window layout: mapped, coherent pinned memory
+  void* stage_host = nullptr;    // the allocation stage_dev was taken for
+  char* stage_dev = nullptr;     // its device address: the kernels read it in place (no upload)
+  bool stage_pending = false;    // stage_h may still be read by the last tick's kernels
 };
 
 // ring[c][2W]: every sample is written at p and p + W, so the last W samples of a channel are
@@ -1214,7 +1232,7 @@ void tfp_stream_destroy(tfp_stream* st) {
   {
     std::lock_guard<std::recursive_mutex> lk(st->eng->mu);
     (void)hipSetDevice(st->eng->device);
-    (void)hipStreamSynchronize(st->eng->stream);  // the last tick's upload may still read stage_h
+    (void)hipStreamSynchronize(st->eng->stream);  // the last tick's kernels may still read stage_h
   }
   delete st;
 }
@@ -1247,16 +1265,20 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
   const int32_t tile = fp_tile_frames(e->fpcfg, fx, false, false);
   const int32_t tiles = (int32_t)((F + tile - 1) / tile);
-  // One pinned upload per tick: the tick's samples, then the windows' layout (sbeg, send, foff,
-  // toff, tclip). The previous tick's upload must be done reading the pinned buffer.
+  // One mapped pinned buffer per tick, read in place by the kernels: the tick's samples, then the
+  // windows' layout (sbeg, send, foff, toff, tclip). An upload and its hand-off to the first
+  // kernel cost ~16 us a tick. The previous tick's kernels must be done reading the buffer.
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t b_pcm = al(sizeof(int16_t) * (size_t)st->nch * T), b_sb = al(sizeof(int64_t) * na),
                b_fo = al(sizeof(int64_t) * (na + 1)), b_to = al(sizeof(int32_t) * (na + 1)),
                b_tc = al(sizeof(int32_t) * (size_t)na * tiles);
   const size_t total = b_pcm + 2 * b_sb + b_fo + b_to + b_tc;
   if (st->stage_pending) HIPCHK(e, hipStreamSynchronize(e->stream));
-  HIPCHK(e, st->stage_h.reserve(total));
-  HIPCHK(e, st->stage_d.reserve(total));
+  HIPCHK(e, st->stage_h.reserve(total, hipHostMallocMapped | hipHostMallocCoherent));
+  if (st->stage_h.p != st->stage_host) {
+    HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&st->stage_dev), st->stage_h.p, 0));
+    st->stage_host = st->stage_h.p;
+  }
   char* h = st->stage_h.as<char>();
   memcpy(h, pcm, sizeof(int16_t) * (size_t)st->nch * T);
   int64_t* sb = reinterpret_cast<int64_t*>(h + b_pcm);
@@ -1273,9 +1295,8 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   }
   fo[na] = (int64_t)na * F;
   to[na] = na * tiles;
-  HIPCHK(e, hipMemcpyAsync(st->stage_d.p, h, total, hipMemcpyHostToDevice, e->stream));
   st->stage_pending = true;
-  const char* d = st->stage_d.as<char>();
+  const char* d = st->stage_dev;
   hipLaunchKernelGGL(stream_scatter_kernel, dim3(1024), dim3(256), 0, e->stream, reinterpret_cast<const int16_t*>(d), T,
                      st->W, st->wpos, st->nch, st->ring.as<int16_t>());
   HIPCHK(e, hipGetLastError());
