@@ -128,7 +128,7 @@ struct tfp_engine {
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
-  uint32_t small_seq = 0;
+  void* small_res_host = nullptr;  // the allocation small_res_dev was taken for
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
@@ -144,7 +144,6 @@ struct tfp_engine {
   // launch configuration and test/A-B knobs, read once at engine creation
   FpLaunchCfg fpcfg;
   int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
-  bool small_sync = true;     // TFP_SMALL_SYNC=0: batch-1 spins on the published result instead of a stream sync
   bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
@@ -582,36 +581,32 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       }
       const uint8_t epoch = ++e->small_epoch;
       SmallWork* w = e->small_work.as<SmallWork>();
-      if (!e->small_res_dev) {
-        HIPCHK(e, e->small_res.reserve(sizeof(SmallResult), hipHostMallocMapped | hipHostMallocCoherent));
+      HIPCHK(e, e->small_res.reserve(small_result_bytes(C), hipHostMallocMapped | hipHostMallocCoherent));
+      if (e->small_res.p != e->small_res_host) {
         HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&e->small_res_dev), e->small_res.p, 0));
+        e->small_res_host = e->small_res.p;
       }
       if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
-      const uint32_t seq = ++e->small_seq;
       HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->rng_all.as<int64_t>(),
-                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), e->small_res_dev, seq, s));
-      // Wait for the end of the stream (default), or spin on the result itself: the publishing
-      // kernel stores seq after (ku, bad, best) with system-scope release. The spin is bounded;
-      // past it the stream is synchronised and the result read after that.
-      const volatile SmallResult* h = e->small_res.as<SmallResult>();
-      bool seen = false;
-      if (!e->small_sync) {
-        const auto t0 = std::chrono::steady_clock::now();
-        for (;;) {
-          if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) == seq) { seen = true; break; }
-          if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) break;
-        }
-      }
-      if (!seen) HIPCHK(e, hipStreamSynchronize(s));
+                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), e->small_res_dev, s));
+      const hipError_t sync_rc = hipStreamSynchronize(s);
+      if (sync_rc != hipSuccess) e->small_rows = kKeyRange;  // unknown stamps: clear everything at the next wrap
+      HIPCHK(e, sync_rc);
       // the vote ran after the fingerprint kernel, which read the staged upload: it is free again
       e->stage_pending = false;
-      if (__atomic_load_n(&h->seq, __ATOMIC_ACQUIRE) != seq) {
-        e->small_rows = kKeyRange;  // unknown stamps: clear everything at the next wrap
-        return fail(e, TFP_E_HIP, "small search: result of call %u not published", seq);
-      }
+      // the vote's blocks wrote their per-query maxima into host memory: the max over the blocks
+      SmallResult* h = e->small_res.as<SmallResult>();
       if (!h->bad) {
         e->small_rows = std::max<int32_t>(e->small_rows, (int32_t)h->ku);
-        for (int32_t i = 0; i < nq; i++) keys[i] = h->best[i];
+        if (h->ku > 0) {
+          const unsigned long long* part = small_result_parts(h);
+          const int32_t nb = small_vote_blocks(C);
+          for (int32_t i = 0; i < nq; i++) {
+            unsigned long long k = 0ull;
+            for (int32_t b = 0; b < nb; b++) k = std::max(k, part[(size_t)b * kSmallQ + i]);
+            keys[i] = k;
+          }
+        }
         return TFP_OK;
       }
       // a key outside the vote range: redo the batch on the general path below
@@ -779,7 +774,6 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
     return TFP_E_HIP;
   }
   if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
-  if (const char* v = getenv("TFP_SMALL_SYNC")) e->small_sync = atoi(v) != 0;
   e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;

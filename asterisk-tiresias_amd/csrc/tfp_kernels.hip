@@ -1828,12 +1828,6 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
 
 // ---- small-batch path (see tfp_kernels.hpp). Same sets and counts as key_hist + build_A/B +
 // vote_gemm: a query frame with trunc key k votes once for every clip with a row in k's box.
-#ifndef TFP_SMALL_PUBLISH
-// 0: small_vote's last block publishes the results (a done counter + fences in every block: the
-// vote measured 11.7 us); 1: a one-wave kernel after the vote (4.6 + 4.0 us, batch-1 p50 -5 us);
-// 2: as 1 without the system-scope fence (the host then waits for the stream, not on seq)
-#define TFP_SMALL_PUBLISH 1
-#endif
 // The batch's used keys (ascending key order = column order kc), derived by each block from the
 // query frames with frame_key's filter; bad = a key outside the vote range.
 struct SmallKeySet {
@@ -1894,9 +1888,7 @@ __global__ __launch_bounds__(256) void small_mark_kernel(const double* __restric
   small_keys(q, nf, sc, K);
   if (blockIdx.x == 0) {  // the vote's bookkeeping: counts per (query, used key), ku, bad
     const int ku = K.ku;
-    if (threadIdx.x <= kSmallQ) w->best[threadIdx.x] = 0ull;
     if (threadIdx.x == 0) {
-      w->done = 0u;
       w->ku = ku;
       w->bad = K.bad;
     }
@@ -1940,15 +1932,16 @@ __global__ __launch_bounds__(256) void small_mark_kernel(const double* __restric
 
 // Clip-parallel scores of every query (4 clips per thread: one 32-bit stamp word per key row);
 // the per-query max of score << 32 | tie key (a later uuid wins a tie, as SQLite's
-// ORDER BY count(*) DESC returns it), reduced per block before one atomicMax per block. The last
-// block to finish publishes (ku, bad, best[]) and the call's sequence number to host memory.
-__global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, SmallWork* __restrict__ w,
+// ORDER BY count(*) DESC returns it), reduced per block and written to the caller's host-mapped
+// result as this block's part; block 0 also writes (ku, bad). (Publishing the final max from the
+// device cost a one-wave kernel of ~4 us per call, or a done counter and fences in every block.)
+__global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, const SmallWork* __restrict__ w,
                                                          const uint8_t* __restrict__ bk, int32_t Cp, int32_t C,
                                                          const int32_t* __restrict__ tiekey, uint8_t epoch,
-                                                         SmallResult* __restrict__ out, uint32_t seq) {
+                                                         SmallResult* __restrict__ out) {
+  static_assert(4 * 256 == kSmallVoteClips, "4 clips per thread");
   __shared__ int32_t A[kSmallQ][kKeyRange];
   __shared__ unsigned long long bmax[kSmallQ][4];
-  __shared__ int32_t last;
   const int nq = sq.nq;
   const int ku = w->ku, bad = w->bad;
   if (!bad && ku > 0) {  // else every frame was ignored (NOTFOUND: best stays 0) or the caller redoes it
@@ -2008,62 +2001,23 @@ __global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, SmallW
     if (threadIdx.x < nq) {
       unsigned long long key = bmax[threadIdx.x][0];
       for (int i = 1; i < 4; i++) key = bmax[threadIdx.x][i] > key ? bmax[threadIdx.x][i] : key;
-      if (key) atomicMax(&w->best[threadIdx.x], key);
+      small_result_parts(out)[(int64_t)blockIdx.x * kSmallQ + threadIdx.x] = key;
     }
   }
-#if TFP_SMALL_PUBLISH == 0
-  // last block done: publish to host memory
-  __threadfence();
-  __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(&w->done, 1u) == gridDim.x - 1;
-  __syncthreads();
-  if (last) {
-    __threadfence();
-    if (threadIdx.x < kSmallQ)
-      out->best[threadIdx.x] = threadIdx.x < nq ? __hip_atomic_load(&w->best[threadIdx.x], __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                                : 0ull;
-    if (threadIdx.x == 0) {
-      out->ku = ku;
-      out->bad = bad;
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    out->ku = ku;
+    out->bad = bad;
   }
-#else
-  (void)out; (void)seq; (void)last;
-#endif
-}
-
-// TFP_SMALL_PUBLISH=1: the results are published by a one-wave kernel after the vote
-__global__ __launch_bounds__(64) void small_publish_kernel(const SmallWork* __restrict__ w, int32_t nq,
-                                                           SmallResult* __restrict__ out, uint32_t seq) {
-  const int t = threadIdx.x;
-  if (t < kSmallQ) out->best[t] = t < nq ? w->best[t] : 0ull;
-  if (t == 0) {
-    out->ku = w->ku;
-    out->bad = w->bad;
-  }
-#if TFP_SMALL_PUBLISH == 1
-  __threadfence_system();
-  if (t == 0) __hip_atomic_store(&out->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-#else
-  if (t == 0) out->seq = seq;
-#endif
 }
 
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
                                uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
-                               uint32_t seq, hipStream_t s) {
+                               hipStream_t s) {
   if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0 || !h_out) return hipErrorInvalidValue;
   hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_q, sq, sc, d_rng_all, d_bk, Cp, cols, epoch, d_work);
-  hipLaunchKernelGGL(small_vote_kernel, dim3((C + 1023) / 1024), dim3(256), 0, s, sq, d_work, d_bk, Cp, C,
-                     d_tiekey, epoch, h_out, seq);
-#if TFP_SMALL_PUBLISH >= 1
-  hipLaunchKernelGGL(small_publish_kernel, dim3(1), dim3(64), 0, s, d_work, sq.nq, h_out, seq);
-#endif
+  hipLaunchKernelGGL(small_vote_kernel, dim3(small_vote_blocks(C)), dim3(256), 0, s, sq, d_work, d_bk, Cp, C, d_tiekey,
+                     epoch, h_out);
   return hipGetLastError();
 }
 

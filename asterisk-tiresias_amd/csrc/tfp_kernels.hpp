@@ -127,8 +127,9 @@ hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Q
 // two launches, no host round trip and no copy back. Every block of small_mark derives the
 // batch's used keys from the query frames itself (a few KB of L2-resident reads) and stamps the
 // clips with a row in each used key's box (a byte per clip, key-major); its block 0 also writes
-// the per-query key counts. small_vote scores clip-parallel, arg-maxes, and its last block writes
-// the results straight into the caller's host-mapped SmallResult.
+// the per-query key counts. small_vote scores clip-parallel and arg-maxes per block; each block
+// writes its per-query maxima straight into the caller's host-mapped SmallResult, and the caller
+// takes the max over the blocks once the stream is done (no publishing kernel, no device atomics).
 constexpr int kSmallQ = 8;
 struct SmallQueries {
   int32_t nq;
@@ -139,21 +140,26 @@ struct SmallWork {                       // device workspace of the small path (
   int32_t A[kSmallQ][kKeyRange];         // A[q][kc]: query q's frames whose key is the kc-th used key
   int32_t ku;                            // used keys
   int32_t bad;                           // a key outside [-512, 511]
-  unsigned long long best[kSmallQ + 1];  // per query score << 32 | tie key; best[kSmallQ] unused
-  uint32_t done;                         // small_vote blocks finished (the last one publishes)
 };
-struct SmallResult {  // host-mapped (pinned) result of one small call
-  int32_t ku;         // used keys
-  int32_t bad;        // a key outside [-512, 511]: the caller redoes the batch generally
-  unsigned long long best[kSmallQ];
-  uint32_t seq;       // the call's sequence number, stored last
+// Host-mapped (pinned, coherent) result of one small call: the header, then small_vote's per-block
+// maxima part[block][query] (score << 32 | tie key, 0 = no hit) for the small_vote_blocks(C) blocks.
+// Written only when !bad and ku > 0; valid once the stream is done.
+struct SmallResult {
+  int32_t ku;   // used keys (0: every frame was ignored, NOTFOUND)
+  int32_t bad;  // a key outside [-512, 511]: the caller redoes the batch generally
 };
+constexpr int kSmallVoteClips = 1024;  // clips per small_vote block (4 per thread)
+inline int32_t small_vote_blocks(int32_t C) { return (C + kSmallVoteClips - 1) / kSmallVoteClips; }
+inline size_t small_result_bytes(int32_t C) {
+  return sizeof(SmallResult) + sizeof(unsigned long long) * kSmallQ * (size_t)small_vote_blocks(C);
+}
+TFP_HD unsigned long long* small_result_parts(SmallResult* r) { return reinterpret_cast<unsigned long long*>(r + 1); }
 // d_bk: [kKeyRange][Cp] bytes stamped with `epoch` (1..255, a new one per call; the caller clears
-// d_bk when the epoch wraps). h_out: host-mapped memory the device may write.
+// d_bk when the epoch wraps). h_out: host-mapped memory of small_result_bytes(C) the device writes.
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
                                uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
                                const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
-                               uint32_t seq, hipStream_t s);
+                               hipStream_t s);
 
 // General path (coefs = 2 and the vote's fallbacks; tfp_scan.hip). Clip-set cache of one index
 // version and tolerance, built from the key boxes' row ranges (d_rng_all, h_off = host prefix of
