@@ -115,6 +115,8 @@ struct tfp_engine {
   HostBuf zstage;                   // mapped + coherent: small 8 kHz calls are read by the kernel in place
   void* zstage_host = nullptr;      // the allocation zstage_dev was taken for
   char* zstage_dev = nullptr;
+  DevBuf zlayout;                   // device copy of the last zero-copy call's tile layout
+  std::vector<char> zlayout_host;   // ... and its bytes (re-uploaded when they change)
   bool stage_pending = false;  // hstage / zstage may still be read by a copy or kernel on e->stream
   HostBuf qoff_pin;                   // pinned source of the qoff copy
   std::vector<int64_t> qoff_host;     // what e->qoff holds (copied on stream qoff_stream)
@@ -297,10 +299,23 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
     e->stage_pending = true;
     char* d = zero_copy ? e->zstage_dev : e->dstage.as<char>();
     d_pcm = d;
-    d_soff = reinterpret_cast<const int64_t*>(d + b_pcm);
-    d_foff = reinterpret_cast<const int64_t*>(d + b_pcm + b_so);
-    d_toff = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo);
-    d_tclip = reinterpret_cast<const int32_t*>(d + b_pcm + b_so + b_fo + b_to);
+    const char* lay_d = d + b_pcm;  // the layout arrays' device address
+    if (zero_copy) {
+      // The tile layout is read first and in a dependent chain (tile -> clip -> its bounds -> the
+      // PCM address): keep it in device memory. It depends only on the query lengths, so it is
+      // uploaded only when it changes (from the pinned staging; the PCM stays in place).
+      const size_t lay = total - b_pcm;
+      if (e->zlayout_host.size() != lay || memcmp(e->zlayout_host.data(), h + b_pcm, lay) != 0) {
+        HIPCHK(e, e->zlayout.reserve(lay));
+        HIPCHK(e, hipMemcpyAsync(e->zlayout.p, h + b_pcm, lay, hipMemcpyHostToDevice, e->stream));
+        e->zlayout_host.assign(h + b_pcm, h + total);
+      }
+      lay_d = e->zlayout.as<char>();
+    }
+    d_soff = reinterpret_cast<const int64_t*>(lay_d);
+    d_foff = reinterpret_cast<const int64_t*>(lay_d + b_so);
+    d_toff = reinterpret_cast<const int32_t*>(lay_d + b_so + b_fo);
+    d_tclip = reinterpret_cast<const int32_t*>(lay_d + b_so + b_fo + b_to);
   } else {
     if ((rc = upload(e, e->pcm, src + ss * offsets[0], ss * ns))) return rc;
     if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
