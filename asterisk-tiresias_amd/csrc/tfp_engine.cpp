@@ -68,6 +68,27 @@ struct Clip {
   int64_t off = 0;  // first staging row (a clip's rows are contiguous, in frame order)
 };
 
+// tfp_host_alloc's buffers: host address -> (bytes, device address), so a call whose samples lie
+// inside one hands the GPU the samples in place.
+struct HostAllocs {
+  std::mutex mu;
+  std::map<uintptr_t, std::pair<size_t, char*>> m;
+  // device address of [p, p + n) if it lies inside one buffer, else nullptr
+  const char* find(const void* p, size_t n) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = m.upper_bound(a);
+    if (it == m.begin()) return nullptr;
+    --it;
+    if (a + n > it->first + it->second.first) return nullptr;
+    return it->second.second + (a - it->first);
+  }
+};
+HostAllocs& host_allocs() {
+  static HostAllocs h;
+  return h;
+}
+
 }  // namespace
 
 struct tfp_plan {
@@ -290,7 +311,9 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
       HIPCHK(e, e->dstage.reserve(total));
       h = e->hstage.as<char>();
     }
-    if (ns) memcpy(h, src + ss * offsets[0], ss * ns);
+    // samples already in a tfp_host_alloc buffer: read in place (no copy into the staging)
+    const char* in_place = zero_copy && ns ? host_allocs().find(src + ss * offsets[0], ss * ns) : nullptr;
+    if (ns && !in_place) memcpy(h, src + ss * offsets[0], ss * ns);
     memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
     memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
     memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
@@ -298,7 +321,7 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
     if (!zero_copy) HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
     e->stage_pending = true;
     char* d = zero_copy ? e->zstage_dev : e->dstage.as<char>();
-    d_pcm = d;
+    d_pcm = in_place ? in_place : d;
     const char* lay_d = d + b_pcm;  // the layout arrays' device address
     if (zero_copy) {
       // The tile layout is read first and in a dependent chain (tile -> clip -> its bounds -> the
@@ -809,6 +832,34 @@ void tfp_engine_destroy(tfp_engine* e) {
 
 __attribute__((visibility("hidden"))) const char* tfp_ingest_last_error();  // tfp_wav.cpp: engine-less errors of this thread
 const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : tfp_ingest_last_error(); }
+
+int tfp_host_alloc(size_t bytes, void** out) {
+  if (!bytes || !out) return TFP_E_ARG;
+  *out = nullptr;
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
+    return TFP_E_NOMEM;
+  char* d = nullptr;
+  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), p, 0) != hipSuccess) {
+    (void)hipHostFree(p);
+    return TFP_E_NOMEM;
+  }
+  HostAllocs& h = host_allocs();
+  std::lock_guard<std::mutex> lk(h.mu);
+  h.m[reinterpret_cast<uintptr_t>(p)] = {bytes, d};
+  *out = p;
+  return TFP_OK;
+}
+
+void tfp_host_free(void* p) {
+  if (!p) return;
+  HostAllocs& h = host_allocs();
+  {
+    std::lock_guard<std::mutex> lk(h.mu);
+    if (!h.m.erase(reinterpret_cast<uintptr_t>(p))) return;  // not ours
+  }
+  (void)hipHostFree(p);
+}
 
 namespace {
 int fingerprint_batch_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nclips,

@@ -52,6 +52,8 @@ _SIGS = {
     "tfp_engine_destroy": (None, [P]),
     "tfp_engine_last_error": (C.c_char_p, [P]),
     "tfp_frame_count": (C.c_int64, [C.c_int64]),
+    "tfp_host_alloc": (C.c_int, [C.c_size_t, C.POINTER(P)]),
+    "tfp_host_free": (None, [P]),
     "tfp_wav_decode": (C.c_int, [P, C.c_int64, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_wav_read": (C.c_int, [C.c_char_p, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_wav_decode_f32": (C.c_int, [P, C.c_int64, P, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),

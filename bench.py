@@ -468,7 +468,8 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
                                          ctypes.c_void_p(fnd.ctypes.data))
         if rc == 0:
             lat = out_ms.tolist()
-            harness = "C loop over tfp_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries" % (n_it, len(hq))
+            harness = ("C loop over tfp_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries held in a "
+                       "tfp_host_alloc buffer (read in place, as the shim's WAV reads)" % (n_it, len(hq)))
     res = {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": (("all_gather of the query frame values (each rank fingerprints 1/%d of the queries), "

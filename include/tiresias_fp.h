@@ -92,6 +92,17 @@ const char* tfp_engine_last_error(const tfp_engine* eng); /* eng == NULL: this t
                                                           * engine-less error (tfp_wav_*) */
 int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
 
+/* ---- host buffers the engine reads in place ------------------------------------------- */
+/* Pinned, device-mapped host memory for PCM (new in round 2). Samples handed to a query search
+ * (tfp_search_pcm_batch, tfp_search_pcm) or a small tfp_fingerprint_* call from inside such a
+ * buffer are read by the GPU where they lie: the call skips copying them into the engine's
+ * staging (a 5 s query is 80 KB, several microseconds of batch-1 latency). Any other caller memory
+ * works as before. Thread-safe, usable with every engine; the buffer must stay allocated until
+ * the call that reads it returns. The Asterisk shim reads WAV files straight into one.
+ * tfp_host_alloc: TFP_E_ARG for bytes == 0 or out == NULL, TFP_E_NOMEM when allocation fails. */
+int tfp_host_alloc(size_t bytes, void** out);
+void tfp_host_free(void* p); /* NULL is a no-op; p must come from tfp_host_alloc */
+
 /* ---- audio ingest: the aubio_source step of create_audio_fingerprints ------------------ */
 /* RIFF/WAVE -> mono int16 PCM at the file's native rate (fp_handler.c:37 DEF_AUBIO_SAMPLERATE 0,
  * :604, :633). Accepts integer PCM (format 1, or EXTENSIBLE with the PCM subformat), mono,

@@ -14,6 +14,7 @@
  * Every tfp_* call is serialised per engine, so the channel threads need no lock here. */
 #include "asterisk.h"
 
+#include <pthread.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -26,6 +27,7 @@
 #include "tiresias_fp.h"
 
 static tfp_engine* g_tfp = NULL; /* one engine (GPU 0) for the module */
+static void pcm_pool_drain(void);
 
 static bool load_clip(void* arg, const char* uuid, const int32_t* m1, const int32_t* m2, int64_t n)
 {
@@ -59,6 +61,7 @@ bool fp_init(void)
 bool fp_term(void)
 {
 	bool ret = fpc_db_term(); /* the rows were written to audio_fingerprint at enrolment */
+	pcm_pool_drain();
 	tfp_engine_destroy(g_tfp);
 	g_tfp = NULL;
 	if(ret == false) {
@@ -67,19 +70,85 @@ bool fp_term(void)
 	return ret;
 }
 
+/* int16 sample buffers in engine-mapped host memory (tfp_host_alloc), which the engine reads in
+ * place instead of copying into its staging. Pooled: pinning memory costs more than the copy it
+ * saves. The channel threads search concurrently, so the pool is locked. */
+#define PCM_POOL 32
+static struct {
+	int16_t* p;
+	int64_t cap;
+} g_pool[PCM_POOL];
+static int g_npool = 0;
+static pthread_mutex_t g_pool_lock = PTHREAD_MUTEX_INITIALIZER;
+
+static int16_t* pcm_get(int64_t n, int64_t* cap)
+{
+	int i, best = -1;
+	void* p = NULL;
+
+	pthread_mutex_lock(&g_pool_lock);
+	for(i = 0; i < g_npool; i++) {
+		if(g_pool[i].cap >= n && (best < 0 || g_pool[i].cap < g_pool[best].cap)) {
+			best = i;
+		}
+	}
+	if(best >= 0) {
+		int16_t* q = g_pool[best].p;
+		*cap = g_pool[best].cap;
+		g_pool[best] = g_pool[--g_npool];
+		pthread_mutex_unlock(&g_pool_lock);
+		return q;
+	}
+	pthread_mutex_unlock(&g_pool_lock);
+	*cap = n < 80000 ? 80000 : n; /* at least 10 s at 8 kHz */
+	if(tfp_host_alloc(sizeof(int16_t) * (size_t)*cap, &p) != TFP_OK) {
+		*cap = 0;
+		return NULL;
+	}
+	return (int16_t*)p;
+}
+
+static void pcm_put(int16_t* p, int64_t cap)
+{
+	if(p == NULL) {
+		return;
+	}
+	pthread_mutex_lock(&g_pool_lock);
+	if(g_npool < PCM_POOL) {
+		g_pool[g_npool].p = p;
+		g_pool[g_npool].cap = cap;
+		g_npool++;
+		p = NULL;
+	}
+	pthread_mutex_unlock(&g_pool_lock);
+	tfp_host_free(p); /* pool full (NULL: kept) */
+}
+
+static void pcm_pool_drain(void)
+{
+	pthread_mutex_lock(&g_pool_lock);
+	while(g_npool > 0) {
+		g_npool--;
+		tfp_host_free(g_pool[g_npool].p);
+	}
+	pthread_mutex_unlock(&g_pool_lock);
+}
+
 /* aubio_source (fp_handler.c:37,604,633): a WAV's mono hop values at its own rate — int16 PCM for
- * 8/16-bit mono (every Asterisk recording), else (TFP_E_FORMAT) the fp32 values (multichannel
- * mean, 24/32-bit, float). Exactly one of *pcm / *x is set. */
-static int read_audio(const char* filename, int16_t** pcm, float** x, int64_t* ns, int32_t* sr)
+ * 8/16-bit mono (every Asterisk recording; in a pooled pcm_get buffer of *cap samples), else
+ * (TFP_E_FORMAT) the fp32 values (multichannel mean, 24/32-bit, float). Exactly one of *pcm / *x
+ * is set; release with pcm_put(*pcm, *cap) and ast_free(*x). */
+static int read_audio(const char* filename, int16_t** pcm, int64_t* cap, float** x, int64_t* ns, int32_t* sr)
 {
 	int rc;
 
 	*pcm = NULL;
+	*cap = 0;
 	*x = NULL;
 	rc = tfp_wav_read(filename, NULL, 0, ns, sr);
 	if(rc == TFP_OK) {
-		*pcm = ast_malloc(sizeof(int16_t) * (*ns ? *ns : 1));
-		rc = *pcm ? tfp_wav_read(filename, *pcm, *ns, ns, sr) : TFP_E_NOMEM;
+		*pcm = pcm_get(*ns ? *ns : 1, cap);
+		rc = *pcm ? tfp_wav_read(filename, *pcm, *cap, ns, sr) : TFP_E_NOMEM;
 	}
 	else if(rc == TFP_E_FORMAT && (rc = tfp_wav_read_f32(filename, NULL, 0, ns, sr)) == TFP_OK) {
 		*x = ast_malloc(sizeof(float) * (*ns ? *ns : 1));
@@ -87,7 +156,7 @@ static int read_audio(const char* filename, int16_t** pcm, float** x, int64_t* n
 	}
 	if(rc != TFP_OK) {
 		ast_log(LOG_WARNING, "Could not read %s: %s\n", filename, tfp_engine_last_error(NULL));
-		ast_free(*pcm);
+		pcm_put(*pcm, *cap);
 		ast_free(*x);
 		*pcm = NULL;
 		*x = NULL;
@@ -102,13 +171,13 @@ static bool create_audio_fingerprint_info(const char* context, const char* filen
 {
 	int16_t* pcm;
 	float* x;
-	int64_t ns, n, i, off[2];
+	int64_t cap, ns, n, i, off[2];
 	int32_t sr, *m1, *m2;
 	tfp_frame* rows;
 	int rc;
 	bool ret;
 
-	if(read_audio(filename, &pcm, &x, &ns, &sr) != 0) {
+	if(read_audio(filename, &pcm, &cap, &x, &ns, &sr) != 0) {
 		return false;
 	}
 	n = tfp_frame_count(ns);
@@ -116,14 +185,14 @@ static bool create_audio_fingerprint_info(const char* context, const char* filen
 	m1 = ast_malloc(sizeof(int32_t) * (n ? n : 1));
 	m2 = ast_malloc(sizeof(int32_t) * (n ? n : 1));
 	if(rows == NULL || m1 == NULL || m2 == NULL) {
-		ast_free(pcm); ast_free(x); ast_free(rows); ast_free(m1); ast_free(m2);
+		pcm_put(pcm, cap); ast_free(x); ast_free(rows); ast_free(m1); ast_free(m2);
 		return false;
 	}
 	off[0] = 0;
 	off[1] = ns;
 	rc = pcm ? tfp_fingerprint_pcm(g_tfp, pcm, ns, sr, rows, n, &n)
 	         : tfp_fingerprint_f32_batch(g_tfp, x, off, 1, sr, rows, n, &n);
-	ast_free(pcm);
+	pcm_put(pcm, cap);
 	ast_free(x);
 	if(rc != TFP_OK) {
 		ast_log(LOG_ERROR, "Could not fingerprint %s: %s\n", filename, tfp_engine_last_error(g_tfp));
@@ -202,7 +271,7 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 {
 	int16_t* pcm;
 	float* x;
-	int64_t ns, off[2];
+	int64_t cap, ns, off[2];
 	int32_t sr;
 	int rc;
 	tfp_search_params p;
@@ -217,7 +286,7 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 		ast_log(LOG_WARNING, "Wrong coefs count. coefs[%d]\n", coefs);
 		return NULL;
 	}
-	if(read_audio(filename, &pcm, &x, &ns, &sr) != 0) {
+	if(read_audio(filename, &pcm, &cap, &x, &ns, &sr) != 0) {
 		return NULL;
 	}
 	memset(&p, 0, sizeof(p));
@@ -229,7 +298,7 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 	off[1] = ns;
 	rc = pcm ? tfp_search_pcm_batch(g_tfp, pcm, off, 1, sr, &p, &r)
 	         : tfp_search_f32_batch(g_tfp, x, off, 1, sr, &p, &r);
-	ast_free(pcm);
+	pcm_put(pcm, cap);
 	ast_free(x);
 	if(rc != TFP_OK) {
 		ast_log(LOG_ERROR, "Could not search %s: %s\n", filename, tfp_engine_last_error(g_tfp));

@@ -191,3 +191,45 @@ def test_scan_path_on_caller_stream_then_host_search(engine, tfp_lib, torch_cuda
         assert torch.equal(keys, alone)
         assert host == ref_host
     engine.index_clear()
+
+
+def test_host_alloc_buffers_read_in_place(engine, tfp_lib):
+    """tfp_host_alloc buffers, which the small path's kernel reads where they lie (no staging copy),
+    give the same results as ordinary memory: queries at the buffer's start and at two misaligned
+    sample offsets (checked loads), a single query, and a small fingerprint call."""
+    import ctypes
+    from tiresias_amd._lib import lib
+    L = lib()
+    nclips, n_db, qn = 24, 8000 * 10, 8000 * 3
+    db = tfp_lib.synth_pcm(0x7153A1, range(nclips), n_db)
+    fr = engine.fingerprint_batch(db.reshape(-1), np.arange(nclips + 1) * n_db)
+    nf = (n_db + 255) // 256
+    engine.index_clear()
+    engine.index_add_batch(["%08x-0000-4000-8000-%012x" % (i * 7919 % 65536, i) for i in range(nclips)],
+                           np.arange(nclips + 1) * nf, fr["m1"], fr["m2"])
+    q = tfp_lib.synth_pcm(0x7153A1, [3, 7, 11], qn, offsets=[256 * 5, 999, 0]).reshape(-1)
+    off = np.arange(4, dtype=np.int64) * qn
+    p = tfp_lib.params(1, 0.001)
+    ref, _ = engine.search_pcm_batch(q, off, p)
+    assert sum(r is not None for r in ref) == 3
+    ptr = ctypes.c_void_p()
+    total = 3 * qn + 8
+    assert L.tfp_host_alloc(2 * total, ctypes.byref(ptr)) == 0 and ptr.value
+    try:
+        buf = np.ctypeslib.as_array((ctypes.c_int16 * total).from_address(ptr.value))
+        for start in (0, 1, 7):
+            buf[start:start + 3 * qn] = q
+            got, _ = engine.search_pcm_batch(buf[start:start + 3 * qn], off, p)
+            assert got == ref, start
+            one, _ = engine.search_pcm_batch(buf[start:start + qn], [0, qn], p)
+            assert one[0] == ref[0], start
+        buf[:3 * qn] = q
+        fa = engine.fingerprint_batch(buf[:3 * qn], off)
+        fb = engine.fingerprint_batch(q, off)
+        assert np.array_equal(fa["m1"], fb["m1"]) and np.array_equal(fa["m2"], fb["m2"])
+    finally:
+        L.tfp_host_free(ptr)
+    bad = ctypes.c_void_p()
+    assert L.tfp_host_alloc(0, ctypes.byref(bad)) != 0
+    L.tfp_host_free(None)
+    engine.index_clear()
