@@ -284,15 +284,20 @@ def test_configs2_full_db_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
 
 @pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 64), (2, 0.01, -1, -1, 32), (2, 0.1, -1, -1, 16),
                                                    (1, 0.45, -1, -1, 64), (1, 0.01, 100, 3400, 64),
-                                                   (2, 0.1, 100, 3400, 16)])
+                                                   (2, 0.1, 100, 3400, 16), (1, 0.001, 50, 60, 64),
+                                                   (2, 0.01, 50, 60, 32)])
 def test_configs2_sweeps_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda, coefs, tol, low, high, nq):
     """SURVEY §8(d)'s configs[2] sweeps at full DB size: coefs = 2 (the general path over the
-    m2-ordered key segments, src/fp_handler.c:318-351), wider tolerances and the 100/3400 Hz
-    ignore filter (:293-306, :324-337) — every key == the oracle's."""
+    m2-ordered key segments, src/fp_handler.c:318-351), wider tolerances and the ignore filter
+    (:293-306, :324-337) — every key == the oracle's. 100/3400 Hz drops ~92% of the synthetic
+    frames (max1 ~17 dB < 20 dB) and matches nothing; 50/60 Hz (16.99/17.78 dB) keeps about a third
+    and still matches, so the filter's kept/dropped split is exercised on both sides."""
     torch = torch_cuda
     qpcm, d_q = _c3_batch(c3db, tfp_lib, torch, nq, SEED_Q + coefs)
     qdb, qoff = _oracle_q(oracle, qpcm)
-    _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(coefs, tol, low, high))
+    w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(coefs, tol, low, high))
+    if low == 50:
+        assert (w >= 0).sum() > 0  # the filter keeps frames that still match
 
 
 def test_configs4_512_channels_one_tick(engine, oracle, tfp_lib, torch_cuda):
