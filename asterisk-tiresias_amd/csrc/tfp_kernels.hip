@@ -96,7 +96,10 @@ struct LdsTables {
   int32_t ms_filter[3][16], ms_start[3][16];
   LogfEntry logf[16];
   int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
-  alignas(16) float ms_w[kMsLds];
+  union {
+    alignas(16) float ms_w[kMsLds];                  // slot schedule (fingerprint_kernel, fingerprint8k_kernel<1>)
+    alignas(16) float fbw[kFbSteps / 4 * kFbPatterns * 4];  // frame-pair schedule (fingerprint8k_kernel<4>)
+  };
 };
 
 constexpr int kPassSamples = 5 * kHop;           // one pass = 4 frames = hops f-1 .. f+3
@@ -123,16 +126,30 @@ static_assert(16 * kSq <= kFrameStride && 16 + 500 <= 2 * kFrameStride, "square 
 // conflict-free: lane L's 16-B pieces start at dword 36 L + 4 j, 16 distinct bank quads per lane
 // group), frames 288 complex apart; the odd frames' |X| rows 48 floats in, which gives the
 // filterbank reads the banks of the 272-complex layout (frames 0, 48, 0, 48 mod 64).
+//
+// The throughput kernel's filterbank runs once per two passes over frame pairs: a pass writes
+// each pair's |X| rows interleaved ([bin][2 frames], kFbRow floats per pair, the two pairs' rows
+// 32 banks apart), the even pass into xeven and the odd pass into the scratch (free after its
+// transpose), and 64 lanes = 4 pairs x 16 patterns (DspTables::fb_*) then sum all 8 frames.
+// Its raw sums land in logs as [2 (t % 8) + t / 8][kFbNf] for tile frame t (a pair's frames of
+// both double passes a few rows apart: immediate offsets), logged once per tile.
 constexpr int kSq8 = 18;
 constexpr int kFrameStride8 = 16 * kSq8;
+constexpr int kFbRow = 544;  // 258 bins x 2 frames, padded to 32 mod 64 banks
+constexpr int kFbNf = 34;    // non-empty filters at 8 kHz (DspTables::fb_nfilters), all below the empty ones
 struct WaveLds8 {
   union {
     cf scratch[4][kFrameStride8];
     alignas(16) int16_t pcm[5 * kHopStride];
   };
+  alignas(16) float xeven[2 * kFbRow];
   float logs[kWaveFrames * kLogStride];
 };
 static_assert(2 * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride8 && 48 + 260 <= 2 * kFrameStride8, "8 kHz scratch");
+static_assert(2 * kFbRow <= 2 * 4 * kFrameStride8 && 2 * kFbRowBins <= kFbRow && kWaveFrames * kFbNf <= kWaveFrames * kLogStride,
+              "frame-pair rows");
+static_assert(kFbSegs == 4, "fb_seg");
+constexpr int fb_seg(int s) { return s < kFbSegStart[1] ? 0 : s < kFbSegStart[2] ? 1 : s < kFbSegStart[3] ? 2 : 3; }
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
 template <typename Smp>
@@ -736,7 +753,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   // writes predicated), so a block waits for one round trip instead of one per table: a small
   // launch is latency-bound.
   static_assert(kBlockThreads == 256, "one entry per thread per table");
-  constexpr int kMsW = 16 * (LA + LB + LC);  // DspTables::fixed8k()'s ms_total
+  // filterbank weights: the frame-pair schedule (throughput) or the slot schedule (small tiles)
+  constexpr bool kPairFb = kPasses >= 2;
+  constexpr int kMsW = kPairFb ? kFbSteps * kFbPatterns : 16 * (LA + LB + LC);  // DspTables_fixed8k
+  const float* const wsrc = kPairFb ? &T->fb_w[0][0][0] : T->ms_w;
   const int wL = (tid >> 1) & 15, wn1 = 2 * (tid >> 5) + (tid & 1);
   const int wj = (32 * wn1 + 2 * wL + 256) & 511;
   const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
@@ -760,7 +780,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #pragma unroll
   for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
     const int idx = tid + kBlockThreads * r;
-    mw[r] = T->ms_w[idx < kMsW ? idx : kMsW - 1];
+    mw[r] = wsrc[idx < kMsW ? idx : kMsW - 1];
   }
   const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
   winr[tid] = cf{win0, win1};
@@ -800,11 +820,28 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   cf ltw[15];
 #pragma unroll
   for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
-  {
-    const float lempty = aubio_log10_fast(0.f, S.logf);
+  const float lempty = aubio_log10_fast(0.f, S.logf);  // log of an empty filter's clamped 0
+  if constexpr (!kPairFb) {
     for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
       const int j = i % kFilters;
       if ((empty_filters >> j) & 1) M.logs[(i / kFilters) * kLogStride + j] = lempty;
+    }
+  }
+  // Frame-pair filterbank (kPairFb): lane = pair grp x pattern L. Pair grp's rows: the even
+  // pass's pairs 0, 1 in xeven, the odd pass's in the scratch. Per segment k: the read base (step
+  // s reads the bins at fbb[k] + 2 s), where the job's raw sums go (frames 2 grp, 2 grp + 1 of
+  // double pass 0: rows 4 grp, 4 grp + 2; double pass 1 one row on), and 0 where the segment
+  // starts a job (acc = fma(acc, 0, p) = p; 1: acc + p).
+  const float* fbb[kFbSegs];
+  float* fbc[kFbSegs];
+  float fbk[kFbSegs];
+  if constexpr (kPairFb) {
+    const float* row = (grp < 2 ? M.xeven : reinterpret_cast<const float*>(M.scratch)) + (grp & 1) * kFbRow;
+#pragma unroll
+    for (int k = 0; k < kFbSegs; k++) {
+      fbb[k] = row + 2 * (T->fb_bin[L][k] - kFbSegStart[k]);
+      fbc[k] = M.logs + 4 * grp * kFbNf + T->fb_filter[L][k];
+      fbk[k] = T->fb_new[L][k] ? 0.f : 1.f;
     }
   }
 
@@ -902,13 +939,17 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
       // |X| rows, addressed as bins L + 16 k2 and 256 - that for every lane (paired ds_write2_b32);
       // lane 0's k2 = 0 pair is bin 128 twice (the partner-side value stands, below): its writes to
-      // bins 0 and 256 are overwritten by n0 and n256.
+      // bins 0 and 256 are overwritten by n0 and n256. Bin b of this frame is NX[kXs * b]: its own
+      // row (slot schedule) or its lane of the pair's interleaved row (frame-pair schedule).
+      constexpr int kXs = kPairFb ? 2 : 1;
+      float* const NX = kPairFb ? ((sub & 1) ? reinterpret_cast<float*>(M.scratch) : M.xeven) + (grp >> 1) * kFbRow + (grp & 1)
+                                : N;
 #pragma unroll
-      for (int k2 = 0; k2 < 8; k2++) N[L + 16 * k2] = nk[k2];
-      float* const nrev = N + (144 - L);  // bin 256 - L - 16 k2 = nrev[16 (7 - k2)]: one base, immediate offsets
+      for (int k2 = 0; k2 < 8; k2++) NX[kXs * (L + 16 * k2)] = nk[k2];
+      float* const nrev = NX + kXs * (144 - L);  // bin 256 - L - 16 k2 = nrev[16 (7 - k2)]: one base, immediate offsets
 #pragma unroll
-      for (int k2 = 0; k2 < 8; k2++) nrev[16 * (7 - k2)] = nk2[k2];
-      if (L == 0) N[128] = nk2[0];  // before the slow path below, which may redo bin 128
+      for (int k2 = 0; k2 < 8; k2++) nrev[kXs * 16 * (7 - k2)] = nk2[k2];
+      if (L == 0) NX[kXs * 128] = nk2[0];  // before the slow path below, which may redo bin 128
       // 0 < |S|^2 < rare_thr (bits - 1 wraps exact zeros to the top): the spec's order below
       if (__builtin_expect(__any(umin < rare_m1), 0)) {  // redo the affected bins in the spec's order
 #pragma unroll
@@ -921,31 +962,62 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
           const cf w = cf{t4.x, t4.z}, w2 = cf{t4.y, t4.w};
           const int k = (k2 == 0 && L == 0) ? 128 : L + 16 * k2;
-          if (sq.x > 0.f && sq.x < rare_thr) N[k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
-          if (sq.y > 0.f && sq.y < rare_thr) N[256 - k] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
+          if (sq.x > 0.f && sq.x < rare_thr) NX[kXs * k] = 2.f * __builtin_sqrtf(split_power(y, p, w));
+          if (sq.y > 0.f && sq.y < rare_thr) NX[kXs * (256 - k)] = 2.f * __builtin_sqrtf(split_power(p, y, w2));
         }
       }
       if (L == 0) {
-        N[0] = n0;
-        N[256] = n256;
+        NX[0] = n0;
+        NX[kXs * 256] = n256;
+        if constexpr (kPairFb) NX[kXs * 257] = 0.f;  // the zero pad a pattern's last pair of bins may read
       }
-      for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
+      if constexpr (!kPairFb)
+        for (int i = 257 + L; i < maxbin; i += 16) N[i] = 0.f;
       wave_sync();
       TFP_STAMP(4);
-      // Filterbank: this lane's 3 filters (slots A, B, C) from the half weights, then the logs
-      const float* wbase = S.ms_w + 4 * L + oz;
-      float* lrow = M.logs + row * kLogStride;
-      const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
-      float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
-      load_w<LC>(wbase + S.ms_woff[2], wC);
-      load_w<LB>(wbase + S.ms_woff[1], wB);
-      load_w<LA>(wbase + S.ms_woff[0], wA);
-      const float aC = mel_sum_w<LC>(N, wC, stC);
-      const float aB = mel_sum_w<LB>(N, wB, stB);
-      const float aA = mel_sum_w<LA>(N, wA, stA);
-      lrow[fA] = aubio_log10_fast(aA, S.logf);
-      lrow[fB] = aubio_log10_fast(aB, S.logf);
-      if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+      if constexpr (!kPairFb) {
+        // Filterbank: this lane's 3 filters (slots A, B, C) from the half weights, then the logs
+        const float* wbase = S.ms_w + 4 * L + oz;
+        float* lrow = M.logs + row * kLogStride;
+        const int stA = S.ms_start[0][L], stB = S.ms_start[1][L], stC = S.ms_start[2][L];
+        float4 wA[LA / 4], wB[LB / 4], wC[LC / 4];
+        load_w<LC>(wbase + S.ms_woff[2], wC);
+        load_w<LB>(wbase + S.ms_woff[1], wB);
+        load_w<LA>(wbase + S.ms_woff[0], wA);
+        const float aC = mel_sum_w<LC>(N, wC, stC);
+        const float aB = mel_sum_w<LB>(N, wB, stB);
+        const float aA = mel_sum_w<LA>(N, wA, stA);
+        lrow[fA] = aubio_log10_fast(aA, S.logf);
+        lrow[fB] = aubio_log10_fast(aB, S.logf);
+        if (c_real) lrow[fC] = aC;  // raw sum: its log is taken in the tile tail
+      } else if (sub & 1) {
+        // Frame-pair filterbank over this double pass's 8 frames: each step multiplies a pair of
+        // bins' (frame, frame) |X| by the pattern's half weight and adds both frames' products to
+        // their sums in one packed op (sums sequential in ascending bins from the job's first
+        // bin, as above); a job's raw sums go to the log rows at each of its segments' ends (the
+        // last write stands), their logs are taken in the tile tail.
+        const int doff = (sub >> 1) * kFbNf;
+        cf acc;
+        float4 wv;
+#pragma unroll
+        for (int st = 0; st < kFbSteps; st += 2) {
+          const int k = fb_seg(st);
+          if ((st & 3) == 0) wv = *reinterpret_cast<const float4*>(S.fbw + ((st >> 2) * kFbPatterns + L) * 4 + oz);
+          const float4 nv = *reinterpret_cast<const float4*>(fbb[k] + 2 * st);
+          const float w0 = (st & 3) ? wv.z : wv.x, w1 = (st & 3) ? wv.w : wv.y;
+          const cf p0 = cf{nv.x, nv.y} * cf{w0, w0};
+          const cf p1 = cf{nv.z, nv.w} * cf{w1, w1};
+          if (st == 0) acc = p0;
+          else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{fbk[k], fbk[k]}, p0);
+          else acc = acc + p0;
+          acc = acc + p1;
+          if (st + 2 == kFbSegStart[k + 1]) {
+            float* const c = fbc[k] + doff;
+            c[0] = acc.x;
+            c[2 * kFbNf] = acc.y;
+          }
+        }
+      }
 #ifdef TFP_STAMPS
       const uint64_t ts5 = __builtin_amdgcn_s_memtime();
       st[0] += ts0 - tprev;  // previous pass's end (or the tail) to this pass's first wave_sync
@@ -959,7 +1031,16 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #endif
     }
     wave_sync();
-    if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
+    if constexpr (kPairFb) {  // the tile's 16 x kFbNf band logs: 8.5 rounds over the wave
+#pragma unroll
+      for (int r = 0; r < (kWaveFrames * kFbNf + 63) / 64; r++) {
+        const int i = 64 * r + lane;
+        if (64 * r + 63 < kWaveFrames * kFbNf || i < kWaveFrames * kFbNf) {
+          float* p = M.logs + i;
+          *p = aubio_log10_fast(*p, S.logf);
+        }
+      }
+    } else if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];
       if (f >= 0) {
         float* p = M.logs + (lane >> 1) * kLogStride + f;
@@ -971,10 +1052,18 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       const int row = lane >> 1, cfi = lane & 1;
       const int64_t f = cur.f0 + row;
       if (f < nf) {
-        const float* lrow = M.logs + row * kLogStride;
         float acc = 0.f;
+        if constexpr (kPairFb) {
+          const float* lrow = M.logs + (2 * (row & 7) + (row >> 3)) * kFbNf;
+#pragma unroll 2
+          for (int i = 0; i < kFbNf; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+#pragma unroll
+          for (int i = kFbNf; i < kFilters; i++) acc = acc + lempty * S.dct[cfi][i];
+        } else {
+          const float* lrow = M.logs + row * kLogStride;
 #pragma unroll 8
-        for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+          for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+        }
         const int64_t g = foff[cur.c] + f;
         if constexpr (kSplitTail) {
           micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
@@ -1011,7 +1100,7 @@ __global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict
 bool DspTables_fixed8k(const DspTables& t) {
   return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total == 16 * (36 + 16 + 8) &&
          t.ms_total <= kMsLds && t.ms_c_defer == 1 && t.ms_maxbin <= 2 * kFrameStride8 - 48 &&
-         t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0;
+         t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0 && t.fb_ok == 1 && t.fb_nfilters == kFbNf;
 }
 
 // Resident 256-thread blocks per CU of kernel k: the occupancy query, capped by what the

@@ -147,6 +147,71 @@ void build_mel_dense(int sample_rate, float (*mel)[kBins]) {
   }
 }
 
+// The frame-pair schedule (DspTables::fb_*): best-fit decreasing. Filters, longest span first
+// (span = the filter's bins from its start rounded down to even, rounded up to even), each take
+// the run of consecutive free segments of an open pattern that fits them with the least slack,
+// or open a new pattern (up to 16) at the least-slack run. A job's window of bins starts at the
+// filter's even-rounded start, moved down when the window would pass bin 257, so every read is a
+// bin of the |X| row or its zero pad.
+static void build_fb_schedule(DspTables* t) {
+  t->fb_ok = 0;
+  int nf = 0;
+  while (nf < kFilters && t->mel_len[nf] > 0) nf++;
+  for (int f = nf; f < kFilters; f++)
+    if (t->mel_len[f] > 0) return;  // the kernel keeps the logs of filters [0, nf) only
+  t->fb_nfilters = nf;
+  int order[kFilters], span[kFilters];
+  for (int f = 0; f < nf; f++) {
+    span[f] = (t->mel_start[f] & 1) + t->mel_len[f];
+    span[f] += span[f] & 1;
+    order[f] = f;
+  }
+  for (int a = 0; a < nf; a++)  // stable selection sort, longest span first
+    for (int b = a + 1; b < nf; b++)
+      if (span[order[b]] > span[order[a]]) { const int x = order[a]; order[a] = order[b]; order[b] = x; }
+  int owner[kFbPatterns][kFbSegs];
+  for (auto& o : owner)
+    for (int& v : o) v = -1;
+  int npat = 0;
+  memset(t->fb_w, 0, sizeof t->fb_w);
+  for (int q = 0; q < nf; q++) {
+    const int f = order[q], need = span[f];
+    int bp = -1, bk0 = 0, bk1 = 0, bw = 1 << 30;
+    auto scan = [&](int p) {
+      for (int k0 = 0; k0 < kFbSegs; k0++)
+        for (int k1 = k0; k1 < kFbSegs && owner[p][k1] < 0; k1++) {
+          const int cap = kFbSegStart[k1 + 1] - kFbSegStart[k0];
+          if (cap >= need && cap - need < bw) { bw = cap - need; bp = p; bk0 = k0; bk1 = k1; }
+        }
+    };
+    for (int p = 0; p < npat; p++) scan(p);
+    if (bp < 0) {
+      if (npat == kFbPatterns) return;
+      scan(npat++);
+      if (bp < 0) return;  // longer than a whole pattern
+    }
+    const int cap = kFbSegStart[bk1 + 1] - kFbSegStart[bk0];
+    const int start = t->mel_start[f], len = t->mel_len[f];
+    int b0 = start & ~1;
+    if (b0 + cap > kFbRowBins) b0 = (kFbRowBins - cap) & ~1;
+    if (b0 < 0 || b0 > start || b0 + cap < start + len) return;
+    for (int k = bk0; k <= bk1; k++) {
+      owner[bp][k] = f;
+      t->fb_bin[bp][k] = b0 + kFbSegStart[k] - kFbSegStart[bk0];
+      t->fb_new[bp][k] = k == bk0;
+      t->fb_filter[bp][k] = f;
+    }
+    for (int s = kFbSegStart[bk0]; s < kFbSegStart[bk1 + 1]; s++) {
+      const int b = b0 + s - kFbSegStart[bk0];
+      t->fb_w[s / 4][bp][s % 4] = (b >= start && b < start + len) ? t->mel_w[t->mel_off[f] + b - start] : 0.f;
+    }
+  }
+  for (int p = 0; p < kFbPatterns; p++)
+    for (int k = 0; k < kFbSegs; k++)
+      if (owner[p][k] < 0) return;  // the kernel has no idle lanes
+  t->fb_ok = 1;
+}
+
 bool build_tables(int sample_rate, DspTables* t) {
   if (sample_rate <= 0 || !t) return false;
   memset(t, 0, sizeof *t);
@@ -230,6 +295,7 @@ bool build_tables(int sample_rate, DspTables* t) {
     for (int L = 0; L < 16; L++)
       if (t->ms_start[sl][L] + t->ms_len[sl] > t->ms_maxbin) t->ms_maxbin = t->ms_start[sl][L] + t->ms_len[sl];
   if (t->ms_maxbin > 500) return false;  // the kernel's per-frame |X| row holds 528 floats
+  build_fb_schedule(t);
   for (int i = 0; i < kWin; i++) t->window_s[i] = t->window[i] * 0x1p-15f;
   for (int k1 = 0; k1 < 16; k1++)
     for (int L = 0; L < 16; L++) {

@@ -16,6 +16,12 @@ namespace tfp {
 
 constexpr int kHop = 256, kWin = 512, kBins = 257, kFilters = 40, kCoefs = 2;
 
+// Frame-pair filterbank schedule of the 8 kHz throughput kernel (fingerprint8k_kernel<4>): 16
+// patterns of kFbSteps steps in kFbSegs fixed segments [kFbSegStart[k], kFbSegStart[k + 1]).
+constexpr int kFbSteps = 36, kFbSegs = 4, kFbPatterns = 16;
+constexpr int kFbSegStart[kFbSegs + 1] = {0, 10, 20, 26, 36};
+constexpr int kFbRowBins = 258;  // bins a pattern step may read: 0..257 (257 reads the zero pad)
+
 // Device-resident table block (one per sample rate). Mel filters are stored sparse:
 // filter j covers bins [mel_start[j], mel_start[j] + mel_len[j]) with weights at mel_w[mel_off[j] ...].
 struct DspTables {
@@ -49,6 +55,18 @@ struct DspTables {
   // log per lane per pass; empty filters' log rows hold the constant log of the clamped 0.
   int32_t ms_c_defer;       // 1 when slot 2 qualifies
   int32_t ms_c_real[2];     // its non-empty filter ids (-1: none)
+  // The frame-pair schedule (kFbSteps above). A lane sums one pattern for two frames at once
+  // (packed), reading their interleaved |X| rows: step s of segment k reads bin
+  // fb_bin[j][k] + s - kFbSegStart[k]. Every segment belongs to a job: one filter's sequential
+  // sum over one or more consecutive segments, restarted where fb_new is set. Weights outside the
+  // filter's bins are zero (exact +0 terms, as for the slots). fb_ok = 0: no such schedule
+  // (more than 16 patterns needed, or a segment left uncovered).
+  int32_t fb_ok;
+  int32_t fb_nfilters;                          // non-empty filters, all below every empty one
+  int32_t fb_bin[kFbPatterns][kFbSegs];
+  int32_t fb_new[kFbPatterns][kFbSegs];
+  int32_t fb_filter[kFbPatterns][kFbSegs];
+  alignas(16) float fb_w[kFbSteps / 4][kFbPatterns][4];  // [step / 4][pattern][step % 4]
 };
 
 // Dense filterbank as aubio lays it out (40 x 257), for tests.
