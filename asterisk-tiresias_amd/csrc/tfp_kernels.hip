@@ -10,8 +10,10 @@
 // oracle (oracle/oracle.c) performs, in the same order, so results are bit-identical.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 
 #include "tfp_kernels.hpp"
+#include "tfp_log.hpp"
 #include "tfp_math.hpp"
 #include "tfp_split.hpp"
 #include "tfp_synth.hpp"
@@ -95,10 +97,11 @@ struct LdsTables {
   int32_t ms_len[3], ms_woff[3];
   int32_t ms_filter[3][16], ms_start[3][16];
   LogfEntry logf[16];
+  LogfEntry logf2[kLogf2Entries];  // (invc, y0) for aubio_log10_frexp (tfp_log.hpp)
   int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
   union {
     alignas(16) float ms_w[kMsLds];                  // slot schedule (fingerprint_kernel, fingerprint8k_kernel<1>)
-    alignas(16) float fbw[kFbSteps / 4 * kFbPatterns * 4];  // frame-pair schedule (fingerprint8k_kernel<4>)
+    alignas(16) float fbw[kFbSteps * kFbPatterns];  // frame-pair schedule (fingerprint8k_kernel<4>)
   };
 };
 
@@ -133,6 +136,7 @@ static_assert(16 * kSq <= kFrameStride && 16 + 500 <= 2 * kFrameStride, "square 
 // transpose), and 64 lanes = 4 pairs x 16 patterns (DspTables::fb_*) then sum all 8 frames.
 // Its raw sums land in logs as [2 (t % 8) + t / 8][kFbNf] for tile frame t (a pair's frames of
 // both double passes a few rows apart: immediate offsets), logged once per tile.
+typedef float f4v __attribute__((ext_vector_type(4)));
 constexpr int kSq8 = 18;
 constexpr int kFrameStride8 = 16 * kSq8;
 constexpr int kFbRow = 544;  // 258 bins x 2 frames, padded to 32 mod 64 banks
@@ -794,6 +798,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   }
   if (tid < 3) { S.ms_len[tid] = msl; S.ms_woff[tid] = mso; }
   if (tid < 16) S.logf[tid] = lge;
+  if (kPairFb && tid < kLogf2Entries) S.logf2[tid] = logf2_entry(tid, logf_table());
   if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
 #pragma unroll
   for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
@@ -995,28 +1000,33 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         // bins' (frame, frame) |X| by the pattern's half weight and adds both frames' products to
         // their sums in one packed op (sums sequential in ascending bins from the job's first
         // bin, as above); a job's raw sums go to the log rows at each of its segments' ends (the
-        // last write stands), their logs are taken in the tile tail.
-        const int doff = (sub >> 1) * kFbNf;
-        cf acc;
-        float4 wv;
+        // last write stands), their logs are taken in the tile tail. One copy per double pass,
+        // so the row offset of its sums is an immediate.
+        auto pair_fb = [&](auto dp) {
+          constexpr int doff = decltype(dp)::value * kFbNf;
+          cf acc;
+          // a step pair's weights: one ds_read_b64 each, whose halves the packed multiplies
+          // broadcast with op_sel (a b128 of 4 steps made the compiler move the halves apart)
+          const cf* const wfb = reinterpret_cast<const cf*>(S.fbw) + L + oz;
 #pragma unroll
-        for (int st = 0; st < kFbSteps; st += 2) {
-          const int k = fb_seg(st);
-          if ((st & 3) == 0) wv = *reinterpret_cast<const float4*>(S.fbw + ((st >> 2) * kFbPatterns + L) * 4 + oz);
-          const float4 nv = *reinterpret_cast<const float4*>(fbb[k] + 2 * st);
-          const float w0 = (st & 3) ? wv.z : wv.x, w1 = (st & 3) ? wv.w : wv.y;
-          const cf p0 = cf{nv.x, nv.y} * cf{w0, w0};
-          const cf p1 = cf{nv.z, nv.w} * cf{w1, w1};
-          if (st == 0) acc = p0;
-          else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{fbk[k], fbk[k]}, p0);
-          else acc = acc + p0;
-          acc = acc + p1;
-          if (st + 2 == kFbSegStart[k + 1]) {
-            float* const c = fbc[k] + doff;
-            c[0] = acc.x;
-            c[2 * kFbNf] = acc.y;
+          for (int st = 0; st < kFbSteps; st += 2) {
+            const int k = fb_seg(st);
+            const cf wv = wfb[(st >> 1) * kFbPatterns];
+            const f4v nv = *reinterpret_cast<const f4v*>(fbb[k] + 2 * st);
+            const cf p0 = cf{nv.x, nv.y} * cf{wv.x, wv.x};
+            const cf p1 = cf{nv.z, nv.w} * cf{wv.y, wv.y};
+            if (st == 0) acc = p0;
+            else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{fbk[k], fbk[k]}, p0);
+            else acc = acc + p0;
+            acc = acc + p1;
+            if (st + 2 == kFbSegStart[k + 1]) {
+              fbc[k][doff] = acc.x;
+              fbc[k][doff + 2 * kFbNf] = acc.y;
+            }
           }
-        }
+        };
+        if (sub == 1) pair_fb(std::integral_constant<int, 0>{});
+        else pair_fb(std::integral_constant<int, 1>{});
       }
 #ifdef TFP_STAMPS
       const uint64_t ts5 = __builtin_amdgcn_s_memtime();
@@ -1037,7 +1047,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const int i = 64 * r + lane;
         if (64 * r + 63 < kWaveFrames * kFbNf || i < kWaveFrames * kFbNf) {
           float* p = M.logs + i;
-          *p = aubio_log10_fast(*p, S.logf);
+          *p = aubio_log10_frexp(*p, S.logf2);
         }
       }
     } else if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)

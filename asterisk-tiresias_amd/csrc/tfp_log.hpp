@@ -1,0 +1,56 @@
+// tfp_log.hpp — the 8 kHz throughput kernel's band log (device code; included by tfp_kernels.hip
+// and tests/native/check_log_fast.hip): aubio_log10_fast (tfp_math.hpp) with fewer instructions.
+//
+//   * glibc log10f's argument split (k = unbiased exponent, i = k < 0, m = the mantissa with
+//     exponent 0x7f - i, y = k + i; the 2^25 rescale of subnormals) is v_frexp: a = mt 2^e with
+//     mt in [0.5, 1), so k = e - 1 and, with c = (e >= 1), m = mt 2^c and y = e - c, exactly;
+//   * logf's y0 = logc + k Ln2 (k in {-1, 0, 1} on [0.5, 2)) comes from a 64-entry table indexed
+//     by bits 19..24 of tmp = bits(m) - 0x3f330000, built with the same double operations.
+// tests/native/check_log_fast.hip compares it with aubio_log10_fast on the GPU for every
+// non-negative finite float.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "tfp_math.hpp"
+
+namespace tfp {
+
+constexpr int kLogf2Entries = 64;
+
+// Entry idx of the 64-entry table: (invc, y0) of logf_glibc's table entry idx & 15 and its
+// exponent k = bits 23..24 of tmp as a signed field (idx >> 4: 0 -> 0, 1 -> 1, 3 -> -1; 2 is
+// unused). y0 = logc + (double)k * Ln2, the two roundings of logf_glibc.
+__device__ inline LogfEntry logf2_entry(int idx, const LogfEntry* T16) {
+  const double Ln2 = 0x1.62e42fefa39efp-1;
+  const LogfEntry e = T16[idx & 15];
+  const int k = ((idx >> 4) ^ 2) - 2;
+  return LogfEntry{e.invc, e.logc + (double)k * Ln2};
+}
+
+// == aubio_log10_fast(x) for every x >= +0 (finite; the filterbank sums). T64: logf2_entry(0..63).
+__device__ __forceinline__ float aubio_log10_frexp(float x, const LogfEntry* T64) {
+  const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const float c = (float)2.e-42;
+  const float a = x > c ? x : c;  // aubio's clamp (a double compare, equal to this for any non-NaN x)
+  const int e = __builtin_amdgcn_frexp_expf(a);
+  const float mt = __builtin_amdgcn_frexp_mantf(a);
+  const int c1 = min(max(e, 0), 1);
+  const float m = __builtin_amdgcn_ldexpf(mt, c1);  // glibc's x (exact)
+  const float y = (float)(e - c1);                  // glibc's y = k + i
+  const uint32_t ix = f2u(m);
+  const uint32_t tmp = ix - 0x3f330000u;
+  const LogfEntry en = T64[(tmp >> 19) & 63u];
+  const uint32_t iz = ix - (tmp & 0xff800000u);
+  const double z = (double)u2f(iz);
+  const double r = z * en.invc - 1.0;
+  const double r2 = r * r;
+  double yy = A1 * r + A2;
+  yy = A0 * r2 + yy;
+  yy = yy * r2 + (en.logc + r);  // en.logc holds y0
+  const float l = (float)yy;
+  const float zz = y * log10_2lo + ivln10 * l;
+  return zz + y * log10_2hi;
+}
+
+}  // namespace tfp

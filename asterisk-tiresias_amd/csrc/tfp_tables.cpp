@@ -147,6 +147,76 @@ void build_mel_dense(int sample_rate, float (*mel)[kBins]) {
   }
 }
 
+// Pattern-to-lane order of the frame-pair schedule with few LDS bank conflicts. Lane 16 p + j
+// reads its pattern's bins (b, b + 1) of pair p's interleaved row as one 16-B slot b / 2, the odd
+// pairs' rows 8 slots further round the banks (kFbRow); a ds_read_b128 is served in the four
+// 16-lane groups of bank_cost, each mixing 8 lanes of an even pair with 8 of an odd one. Same
+// search as lane_order_for_banks over which pattern each j runs.
+static int fb_bank_cost(const DspTables* t, const int* perm) {
+  static const int G[2][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                               {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31}};  // (groups 2, 3 alike)
+  int extra = 0;
+  for (int s = 0; s < kFbSteps; s += 2) {
+    int k = 0;
+    while (s >= kFbSegStart[k + 1]) k++;
+    for (const auto& g : G) {
+      int slot_of_bank[16], cnt[16], worst = 0;
+      for (int b = 0; b < 16; b++) { slot_of_bank[b] = -1; cnt[b] = 0; }
+      for (int l : g) {
+        const int p = l >> 4, pat = perm[l & 15];
+        const int sl = (t->fb_bin[pat][k] + s - kFbSegStart[k]) / 2 + 8 * (p & 1);
+        const int b = sl & 15;
+        if (slot_of_bank[b] != sl) { cnt[b]++; slot_of_bank[b] = sl; }  // a rough count, as bank_cost
+        if (cnt[b] > worst) worst = cnt[b];
+      }
+      extra += worst - 1;
+    }
+  }
+  return extra;
+}
+
+static void fb_order_for_banks(DspTables* t) {
+  int best[kFbPatterns], perm[kFbPatterns];
+  for (int j = 0; j < kFbPatterns; j++) best[j] = j;
+  int best_cost = fb_bank_cost(t, best);
+  uint32_t rng = 0x9e3779b9u;
+  for (int rs = 0; rs < 64 && best_cost > 0; rs++) {
+    for (int j = 0; j < kFbPatterns; j++) perm[j] = j;
+    for (int j = kFbPatterns - 1; j > 0; j--) {  // Fisher-Yates with an LCG: deterministic
+      rng = rng * 1664525u + 1013904223u;
+      const int r = (int)((rng >> 8) % (uint32_t)(j + 1));
+      const int x = perm[j]; perm[j] = perm[r]; perm[r] = x;
+    }
+    int c = fb_bank_cost(t, perm);
+    for (bool improved = true; improved;) {
+      improved = false;
+      for (int a = 0; a < kFbPatterns; a++)
+        for (int b = a + 1; b < kFbPatterns; b++) {
+          int x = perm[a]; perm[a] = perm[b]; perm[b] = x;
+          const int c2 = fb_bank_cost(t, perm);
+          if (c2 < c) { c = c2; improved = true; }
+          else { x = perm[a]; perm[a] = perm[b]; perm[b] = x; }
+        }
+    }
+    if (c < best_cost) { best_cost = c; for (int j = 0; j < kFbPatterns; j++) best[j] = perm[j]; }
+  }
+  int bin[kFbPatterns][kFbSegs], nw[kFbPatterns][kFbSegs], fil[kFbPatterns][kFbSegs];
+  float w[kFbSteps / 2][kFbPatterns][2];
+  memcpy(bin, t->fb_bin, sizeof bin);
+  memcpy(nw, t->fb_new, sizeof nw);
+  memcpy(fil, t->fb_filter, sizeof fil);
+  memcpy(w, t->fb_w, sizeof w);
+  for (int j = 0; j < kFbPatterns; j++) {
+    for (int k = 0; k < kFbSegs; k++) {
+      t->fb_bin[j][k] = bin[best[j]][k];
+      t->fb_new[j][k] = nw[best[j]][k];
+      t->fb_filter[j][k] = fil[best[j]][k];
+    }
+    for (int q = 0; q < kFbSteps / 2; q++)
+      for (int i = 0; i < 2; i++) t->fb_w[q][j][i] = w[q][best[j]][i];
+  }
+}
+
 // The frame-pair schedule (DspTables::fb_*): best-fit decreasing. Filters, longest span first
 // (span = the filter's bins from its start rounded down to even, rounded up to even), each take
 // the run of consecutive free segments of an open pattern that fits them with the least slack,
@@ -203,12 +273,13 @@ static void build_fb_schedule(DspTables* t) {
     }
     for (int s = kFbSegStart[bk0]; s < kFbSegStart[bk1 + 1]; s++) {
       const int b = b0 + s - kFbSegStart[bk0];
-      t->fb_w[s / 4][bp][s % 4] = (b >= start && b < start + len) ? t->mel_w[t->mel_off[f] + b - start] : 0.f;
+      t->fb_w[s / 2][bp][s % 2] = (b >= start && b < start + len) ? t->mel_w[t->mel_off[f] + b - start] : 0.f;
     }
   }
   for (int p = 0; p < kFbPatterns; p++)
     for (int k = 0; k < kFbSegs; k++)
       if (owner[p][k] < 0) return;  // the kernel has no idle lanes
+  fb_order_for_banks(t);
   t->fb_ok = 1;
 }
 

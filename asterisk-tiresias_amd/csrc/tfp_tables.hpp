@@ -66,7 +66,7 @@ struct DspTables {
   int32_t fb_bin[kFbPatterns][kFbSegs];
   int32_t fb_new[kFbPatterns][kFbSegs];
   int32_t fb_filter[kFbPatterns][kFbSegs];
-  alignas(16) float fb_w[kFbSteps / 4][kFbPatterns][4];  // [step / 4][pattern][step % 4]
+  alignas(16) float fb_w[kFbSteps / 2][kFbPatterns][2];  // [step / 2][pattern][step % 2]
 };
 
 // Dense filterbank as aubio lays it out (40 x 257), for tests.

@@ -19,3 +19,15 @@ def test_fast_sqrt_exhaustive():
     print(r.stdout)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "fast_mismatch 0, zero_bad 0, rare_missed 0, rare_spurious 0;" in r.stdout
+
+
+def test_band_log_exhaustive():
+    """The throughput kernel's band log (csrc/tfp_log.hpp: v_frexp reduction, 64-entry (invc, y0)
+    table) == aubio_log10_fast (aubio's clamped glibc log10f, tests/native/check_math.cpp) on every
+    non-negative finite float, both on this GPU (tests/native/check_log_fast.hip)."""
+    exe = os.path.join(PKG, "bin", "check_log_fast")
+    assert os.path.exists(exe), "build with make -C asterisk-tiresias_amd"
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    print(r.stdout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "aubio_log10_fast on 0\n" in r.stdout
