@@ -1042,13 +1042,18 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
     wave_sync();
     if constexpr (kPairFb) {  // the tile's 16 x kFbNf band logs: 8.5 rounds over the wave
+      constexpr int kFull = kWaveFrames * kFbNf / 64;  // 8 full rounds, all table reads issued up front
+      LogArg g[kFull];
+      LogfEntry en[kFull];
 #pragma unroll
-      for (int r = 0; r < (kWaveFrames * kFbNf + 63) / 64; r++) {
-        const int i = 64 * r + lane;
-        if (64 * r + 63 < kWaveFrames * kFbNf || i < kWaveFrames * kFbNf) {
-          float* p = M.logs + i;
-          *p = aubio_log10_frexp(*p, S.logf2);
-        }
+      for (int r = 0; r < kFull; r++) g[r] = log_reduce(M.logs[64 * r + lane]);
+#pragma unroll
+      for (int r = 0; r < kFull; r++) en[r] = S.logf2[g[r].idx];
+#pragma unroll
+      for (int r = 0; r < kFull; r++) M.logs[64 * r + lane] = log_finish(g[r], en[r]);
+      if (64 * kFull + lane < kWaveFrames * kFbNf) {
+        float* p = M.logs + 64 * kFull + lane;
+        *p = aubio_log10_frexp(*p, S.logf2);
       }
     } else if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];

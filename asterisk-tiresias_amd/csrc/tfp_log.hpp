@@ -28,29 +28,40 @@ __device__ inline LogfEntry logf2_entry(int idx, const LogfEntry* T16) {
 }
 
 // == aubio_log10_fast(x) for every x >= +0 (finite; the filterbank sums). T64: logf2_entry(0..63).
-__device__ __forceinline__ float aubio_log10_frexp(float x, const LogfEntry* T64) {
-  const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
-  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+// In two halves, so a caller with several logs can issue all their table reads before it needs
+// any of them: log_reduce (argument split + table index) and log_finish.
+struct LogArg {
+  float y;      // glibc's y = k + i
+  uint32_t iz;  // logf's z bits
+  uint32_t idx; // table index
+};
+__device__ __forceinline__ LogArg log_reduce(float x) {
   const float c = (float)2.e-42;
   const float a = x > c ? x : c;  // aubio's clamp (a double compare, equal to this for any non-NaN x)
   const int e = __builtin_amdgcn_frexp_expf(a);
   const float mt = __builtin_amdgcn_frexp_mantf(a);
   const int c1 = min(max(e, 0), 1);
   const float m = __builtin_amdgcn_ldexpf(mt, c1);  // glibc's x (exact)
-  const float y = (float)(e - c1);                  // glibc's y = k + i
   const uint32_t ix = f2u(m);
   const uint32_t tmp = ix - 0x3f330000u;
-  const LogfEntry en = T64[(tmp >> 19) & 63u];
-  const uint32_t iz = ix - (tmp & 0xff800000u);
-  const double z = (double)u2f(iz);
+  return LogArg{(float)(e - c1), ix - (tmp & 0xff800000u), (tmp >> 19) & 63u};
+}
+__device__ __forceinline__ float log_finish(const LogArg& g, const LogfEntry& en) {
+  const float ivln10 = 4.3429449201e-01f, log10_2hi = 3.0102920532e-01f, log10_2lo = 7.9034151668e-07f;
+  const double A0 = -0x1.00ea348b88334p-2, A1 = 0x1.5575b0be00b6ap-2, A2 = -0x1.ffffef20a4123p-2;
+  const double z = (double)u2f(g.iz);
   const double r = z * en.invc - 1.0;
   const double r2 = r * r;
   double yy = A1 * r + A2;
   yy = A0 * r2 + yy;
   yy = yy * r2 + (en.logc + r);  // en.logc holds y0
   const float l = (float)yy;
-  const float zz = y * log10_2lo + ivln10 * l;
-  return zz + y * log10_2hi;
+  const float zz = g.y * log10_2lo + ivln10 * l;
+  return zz + g.y * log10_2hi;
+}
+__device__ __forceinline__ float aubio_log10_frexp(float x, const LogfEntry* T64) {
+  const LogArg g = log_reduce(x);
+  return log_finish(g, T64[g.idx]);
 }
 
 }  // namespace tfp
