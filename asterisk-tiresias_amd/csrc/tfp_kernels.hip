@@ -1070,7 +1070,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         float acc = 0.f;
         if constexpr (kPairFb) {
           const float* lrow = M.logs + (2 * (row & 7) + (row >> 3)) * kFbNf;
-#pragma unroll 2
+#pragma unroll
           for (int i = 0; i < kFbNf; i++) acc = acc + lrow[i] * S.dct[cfi][i];
 #pragma unroll
           for (int i = kFbNf; i < kFilters; i++) acc = acc + lempty * S.dct[cfi][i];
