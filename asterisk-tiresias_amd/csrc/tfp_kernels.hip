@@ -840,7 +840,11 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const float* fbb[kFbSegs];
   float* fbc[kFbSegs];
   float fbk[kFbSegs];
+  cf dctl, dct9;  // the DCT weights (rows 0, 1) of this lane's filter in the tail's log rounds
   if constexpr (kPairFb) {
+    const int lf = lane < kFbNf ? lane : lane - kFbNf, l9 = kFbNf - 4 + (lane & 3);
+    dctl = cf{S.dct[0][lf], S.dct[1][lf]};
+    dct9 = cf{S.dct[0][l9], S.dct[1][l9]};
     const float* row = (grp < 2 ? M.xeven : reinterpret_cast<const float*>(M.scratch)) + (grp & 1) * kFbRow;
 #pragma unroll
     for (int k = 0; k < kFbSegs; k++) {
@@ -1041,19 +1045,30 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #endif
     }
     wave_sync();
-    if constexpr (kPairFb) {  // the tile's 16 x kFbNf band logs: 8.5 rounds over the wave
-      constexpr int kFull = kWaveFrames * kFbNf / 64;  // 8 full rounds, all table reads issued up front
+    if constexpr (kPairFb) {
+      // The tile's 16 x kFbNf band logs, each times its two DCT weights (the DCT rows' products,
+      // formed here once per log instead of per row term): round r < 8, lane l takes log row pair
+      // (2r, 2r + 1) = frames r, r + 8 at filter l (l < 34) or l - 34, one filter per lane in
+      // every round; the 32 left (filters 30..33 of frames 8..15) go to round 8. Products to the
+      // free scratch as (c0, c1) pairs at the raw sum's index. All table reads issued up front.
+      constexpr int kFull = 8;
+      static_assert(kWaveFrames * kFbNf == kFull * 2 * kFbNf && 2 * kFbNf - 64 == 4, "log rounds");
+      cf* const prod = reinterpret_cast<cf*>(M.scratch);
       LogArg g[kFull];
       LogfEntry en[kFull];
 #pragma unroll
-      for (int r = 0; r < kFull; r++) g[r] = log_reduce(M.logs[64 * r + lane]);
+      for (int r = 0; r < kFull; r++) g[r] = log_reduce(M.logs[2 * kFbNf * r + lane]);
 #pragma unroll
       for (int r = 0; r < kFull; r++) en[r] = S.logf2[g[r].idx];
 #pragma unroll
-      for (int r = 0; r < kFull; r++) M.logs[64 * r + lane] = log_finish(g[r], en[r]);
-      if (64 * kFull + lane < kWaveFrames * kFbNf) {
-        float* p = M.logs + 64 * kFull + lane;
-        *p = aubio_log10_frexp(*p, S.logf2);
+      for (int r = 0; r < kFull; r++) {
+        const float l = log_finish(g[r], en[r]);
+        prod[2 * kFbNf * r + lane] = cf{l, l} * dctl;
+      }
+      if (lane < kWaveFrames * 2) {
+        const int i = 2 * kFbNf * (lane >> 2) + 64 + (lane & 3);
+        const float l = aubio_log10_frexp(M.logs[i], S.logf2);
+        prod[i] = cf{l, l} * dct9;
       }
     } else if (lane < 2 * 4 * kPasses) {  // the deferred slot-2 logs: lane = (frame row, filter)
       const int f = S.c_real[lane & 1];
@@ -1069,9 +1084,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       if (f < nf) {
         float acc = 0.f;
         if constexpr (kPairFb) {
-          const float* lrow = M.logs + (2 * (row & 7) + (row >> 3)) * kFbNf;
+          const float* prow = reinterpret_cast<const float*>(M.scratch) + 2 * (2 * (row & 7) + (row >> 3)) * kFbNf + cfi;
 #pragma unroll
-          for (int i = 0; i < kFbNf; i++) acc = acc + lrow[i] * S.dct[cfi][i];
+          for (int i = 0; i < kFbNf; i++) acc = acc + prow[2 * i];
 #pragma unroll
           for (int i = kFbNf; i < kFilters; i++) acc = acc + lempty * S.dct[cfi][i];
         } else {
