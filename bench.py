@@ -187,7 +187,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "fingerprint8k_kernel + finish_db_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_unit": BYTES_PER_FP, "units_per_launch": F, "avg_launch_ms": avg_launch_s * 1e3,
-                     "limiter": "not HBM: instruction issue at 2 waves/SIMD (~192 wave64 VALU + ~30 LDS + ~14 SALU per fingerprint) "
+                     "limiter": "not HBM: instruction issue at 2 waves/SIMD (~170 wave64 VALU + ~24 LDS + ~13 SALU per fingerprint) "
                                 "(bit-exact fp32 DSP + glibc-exact logs); DESIGN.md §4"},
     }
     del micro
