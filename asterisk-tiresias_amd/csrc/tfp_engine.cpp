@@ -158,6 +158,8 @@ struct tfp_engine {
   // general path: clip-set cache at tolerance cell_tol (tfp_scan.hip), built on first use per
   // index version and tolerance
   CellCache cells;
+  WideScratch wide;         // the general path's sweep by groups
+  double wide_min_tol = 0;  // TFP_WIDE_MIN_TOL: general-path batches below it take the clip-set cells (tests)
   double cell_tol = 0.0;
   bool cell_fresh = false;
   // scan scratch: stamp / score / touched nq x ncols int32 each, tcnt nq int32; kept all-zero
@@ -719,6 +721,19 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     // a count above fp16's exact range or a key outside the vote range: the scan path below
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }
+  if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
+    // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
+    if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
+    if (e->cells.valid) {
+      HIPCHK(e, e->wide.reserve(nf, nq, C, s));
+      bool ok = false;
+      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, &e->wide, &ok, s));
+      if (ok) {
+        HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
+        done = true;
+      }
+    }
+  }
   if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
     // general path (tfp_scan.hip): queries in chunks of <= 256 MB of scratch per array
     if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
@@ -813,6 +828,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   }
   if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
   e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
+  if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;

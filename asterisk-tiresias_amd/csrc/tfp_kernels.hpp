@@ -174,6 +174,7 @@ struct CellCache {
   int32_t* g_beg = nullptr;                // [n1 + 1] first point of each group
   unsigned long long* e_key = nullptr;     // [n2] key << 52 | cell << 21 | column, ascending
   int32_t* e_grp = nullptr;                // [n2] group of each entry
+  int32_t* k_gbeg = nullptr;               // [kKeyRange + 1] first group of each key
   int64_t S = 0, n1 = 0, n2 = 0, w = 0;
   bool valid = false;
   hipError_t build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
@@ -191,5 +192,41 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64
                        const int32_t* m1s, const int32_t* m2s, const int32_t* cols, int64_t R, const CellCache* cells,
                        const int32_t* d_tiekey, int32_t C, int32_t* d_stamp, int32_t* d_score, int32_t* d_touched,
                        int32_t* d_tcnt, unsigned long long* d_best, hipStream_t s);
+
+// The general path's sweep by groups (tfp_scan.hip): every query frame of
+// the batch sorted by (64-query chunk, key, max2 window); per chunk, one wave per clip group of
+// each key the chunk uses counts, for the chunk's 64 queries at once, the frames whose window
+// holds one of the group's points (prefix counts over the sorted frames), so its work follows
+// the groups, not the hits. Needs every frame's key inside the clip-set cache.
+struct WideScratch {
+  static constexpr int32_t kChunk = 64;  // queries per chunk: one per lane
+  // all sized by wide_reserve for nf frames, nq queries, C clips
+  unsigned long long *ka = nullptr, *kb = nullptr;  // sort keys
+  uint32_t *ua = nullptr, *ub = nullptr;
+  int32_t *va = nullptr, *vb = nullptr;             // frame indices
+  int32_t *L2s = nullptr, *U2s = nullptr;           // sorted windows
+  uint8_t* qis = nullptr;                            // sorted frames' query within its chunk
+  int32_t* P = nullptr;                              // [nf][kChunk] in-segment prefix counts
+  int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
+  int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix
+  int32_t* score = nullptr;                          // [C][kChunk], zero between calls
+  int32_t* info = nullptr;                           // [2]: frames kept, ineligible frames
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  int64_t cap_nf = 0, cap_nch = 0, cap_c = 0;
+  hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
+  void release();
+  WideScratch() = default;
+  WideScratch(const WideScratch&) = delete;
+  WideScratch& operator=(const WideScratch&) = delete;
+  ~WideScratch() { release(); }
+};
+// Sorts the batch's frames; *eligible = false (nothing else queued) when a frame needs the row
+// scan (key outside the cache, window outside int32), the caller then takes launch_scan.
+hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
+                                    WideScratch* ws, bool* eligible, hipStream_t s);
+// After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
+hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
+                            WideScratch* ws, unsigned long long* d_best, hipStream_t s);
 
 }  // namespace tfp

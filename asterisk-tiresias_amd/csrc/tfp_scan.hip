@@ -106,6 +106,12 @@ __global__ void cells_entries_kernel(const int32_t* __restrict__ p_m2, const uin
   }
 }
 
+// First group of every key (groups are sorted by key << 21 | column).
+__global__ void key_gbeg_kernel(const uint32_t* __restrict__ g_key, int64_t n1, int32_t* __restrict__ k_gbeg) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t <= kKeyRange) k_gbeg[t] = (int32_t)lower_bound_t<uint32_t>(g_key, n1, (uint32_t)t << kColBits);
+}
+
 inline unsigned grid_for(int64_t n) {
   int64_t g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -121,13 +127,14 @@ hipError_t dmalloc(T** p, int64_t n) {
 }  // namespace
 
 void CellCache::release() {
-  for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp})
+  for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp, (void*)k_gbeg})
     if (p) (void)hipFree(p);
   p_m2 = nullptr;
   g_key = nullptr;
   g_beg = nullptr;
   e_key = nullptr;
   e_grp = nullptr;
+  k_gbeg = nullptr;
   S = n1 = n2 = 0;
   valid = false;
 }
@@ -194,6 +201,9 @@ hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, cons
   TFP_TRY(dmalloc(&g_beg, n1 + 1));
   TFP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, glen, g_beg, (int)n1, s));
   TFP_TRY(hipMemcpyAsync(g_beg + n1, &S, sizeof(int32_t), hipMemcpyHostToDevice, s));  // S < 2^31
+  TFP_TRY(dmalloc(&k_gbeg, kKeyRange + 1));
+  hipLaunchKernelGGL(key_gbeg_kernel, dim3((kKeyRange + 256) / 256), dim3(256), 0, s, g_key, n1, k_gbeg);
+  TFP_TRY(hipGetLastError());
   (void)hipFree(glen);
   glen = nullptr;
   TFP_TRY(dmalloc(&ea, 2 * S));
@@ -381,6 +391,356 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64
                      cols, R, C, d_stamp, d_score, d_touched, d_tcnt);
   hipLaunchKernelGGL(scan_final_kernel, dim3((nq + 3) / 4), dim3(256), 0, s, q_begin, nq, d_tiekey, C, d_stamp, d_score,
                      d_touched, d_tcnt, d_best);
+  return hipGetLastError();
+}
+
+
+// ---- wide max2 windows: sweep by groups ----------------------------------------------------
+//
+// A coefs = 2 frame hits clip c's group of its key iff one of the group's points v lies in its
+// window [L2, U2]. Within one (chunk, key) segment the frames sorted by (L2, U2) have both bounds
+// non-decreasing (both are monotone functions of the frame's max2 value), so the frames a point v
+// hits are one contiguous run [A(v), B(v)] (A: first U2 >= v, B: last L2 <= v), and A(v), B(v)
+// grow with v: the union over the group's ascending points is a few merged runs, and a query's
+// count is its frames inside them: differences of in-segment prefix counts P[i][q]. Frames
+// without a max2 condition (the ignore filter dropped it) hit every group of their key: their
+// own segment, counted whole. Scores go to a per-chunk [clip][query] array (64 lanes = 64
+// queries, one coalesced add per group), then one pass per chunk takes each query's best key.
+
+namespace {
+
+constexpr int kWideCh = WideScratch::kChunk;
+constexpr int kWideSegs = 2 * kKeyRange;  // per chunk: key k with a max2 window, k | 1024 without
+static_assert(kWideCh == 64, "one query per lane");
+
+__global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t nf, uint32_t* __restrict__ uk,
+                                   int32_t* __restrict__ fv, int32_t* __restrict__ info) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    const FrameBox bx = boxes[i];
+    uint32_t u = 0xffffffffu;
+    if (bx.flags & 1) {
+      const int64_t kk = (int64_t)bx.k + kKeyOffset;
+      bool bad = kk < 0 || kk >= kKeyRange;
+      if (bx.flags & 2) {
+        bad = bad || bx.L2 <= (int64_t)INT32_MIN || bx.L2 > (int64_t)INT32_MAX || bx.U2 < (int64_t)INT32_MIN ||
+              bx.U2 > (int64_t)INT32_MAX;
+        u = (uint32_t)(int32_t)bx.U2 ^ 0x80000000u;  // offset binary: unsigned order == signed order
+      } else {
+        u = 0;
+      }
+      if (bad) atomicAdd(&info[1], 1);
+    }
+    uk[i] = u;
+    fv[i] = (int32_t)i;
+  }
+}
+
+// Composite key (chunk << 43 | segment key << 32 | L2) of each frame in the U2 order; frames that
+// take no part get ~0 and sort last.
+__global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
+                                   int64_t nf, const int32_t* __restrict__ fv, unsigned long long* __restrict__ ck,
+                                   int32_t* __restrict__ info) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t f = fv[i];
+    const FrameBox bx = boxes[f];
+    unsigned long long key = ~0ull;
+    const int64_t kk = (int64_t)bx.k + kKeyOffset;
+    if ((bx.flags & 1) && kk >= 0 && kk < kKeyRange) {
+      int lo = 0, hi = nq;  // the frame's query: the last q with qoff[q] <= f
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (qoff[mid] <= f) lo = mid; else hi = mid;
+      }
+      const unsigned long long ch = (unsigned long long)(lo / kWideCh);
+      const unsigned long long sk = (bx.flags & 2) ? (unsigned long long)kk : (unsigned long long)kk | kKeyRange;
+      const unsigned long long l2 = (bx.flags & 2) ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
+      key = (ch << 43) | (sk << 32) | l2;
+      atomicAdd(&info[0], 1);
+    }
+    ck[i] = key;
+  }
+}
+
+// Sorted frames' windows and queries; the segment table [chunk][segment key] = [begin, end).
+__global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
+                                   int64_t n, const unsigned long long* __restrict__ ck,
+                                   const int32_t* __restrict__ fv, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
+                                   uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t f = fv[i];
+    const FrameBox bx = boxes[f];
+    L2s[i] = (int32_t)bx.L2;
+    U2s[i] = (int32_t)bx.U2;
+    int lo = 0, hi = nq;
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (qoff[mid] <= f) lo = mid; else hi = mid;
+    }
+    qis[i] = (uint8_t)(lo % kWideCh);
+    const unsigned long long sg = ck[i] >> 32;  // chunk << 11 | segment key
+    if (i == 0 || (ck[i - 1] >> 32) != sg) seg[2 * sg] = (int32_t)i;
+    if (i == n - 1 || (ck[i + 1] >> 32) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
+  }
+}
+
+// In-segment prefix counts: one wave per segment, lane q counts query q's frames.
+__global__ __launch_bounds__(256) void wide_prefix_kernel(int64_t nsegs, const int32_t* __restrict__ seg,
+                                                          const uint8_t* __restrict__ qis, int32_t* __restrict__ P) {
+  const int lane = threadIdx.x & 63;
+  for (int64_t sgi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; sgi < nsegs;
+       sgi += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int32_t b = seg[2 * sgi], e = seg[2 * sgi + 1];
+    int32_t run = 0;
+    for (int32_t i = b; i < e; i++) {
+      run += qis[i] == lane;
+      P[(int64_t)i * kWideCh + lane] = run;
+    }
+  }
+}
+
+// Per chunk: the work list over the groups of every key the chunk's frames use (exclusive prefix
+// of the keys' group counts), one block per chunk.
+__global__ __launch_bounds__(256) void wide_work_kernel(const int32_t* __restrict__ seg, const int32_t* __restrict__ k_gbeg,
+                                                        int32_t* __restrict__ wpre) {
+  __shared__ int32_t part[256];
+  const int ch = blockIdx.x, t = threadIdx.x;
+  const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
+  int32_t n[kKeyRange / 256], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kKeyRange / 256; j++) {
+    const int kk = t * (kKeyRange / 256) + j;
+    const bool used = sg[2 * kk + 1] > sg[2 * kk] || sg[2 * (kk | kKeyRange) + 1] > sg[2 * (kk | kKeyRange)];
+    n[j] = used ? k_gbeg[kk + 1] - k_gbeg[kk] : 0;
+    sum += n[j];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread sums
+    const int32_t y = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += y;
+    __syncthreads();
+  }
+  int32_t run = part[t] - sum;
+  int32_t* wp = wpre + (int64_t)ch * (kKeyRange + 1);
+#pragma unroll
+  for (int j = 0; j < kKeyRange / 256; j++) {
+    wp[t * (kKeyRange / 256) + j] = run;
+    run += n[j];
+  }
+  if (t == 255) wp[kKeyRange] = part[255];
+}
+
+__device__ __forceinline__ int32_t lb32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] >= v
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] > v
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// One wave per (key, clip group) of the chunk's work list; lane q = query q0 + q.
+__global__ __launch_bounds__(256) void wide_groups_kernel(const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
+                                                          CellView cv, const int32_t* __restrict__ k_gbeg,
+                                                          const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s,
+                                                          const int32_t* __restrict__ P, int32_t* __restrict__ score) {
+  const int lane = threadIdx.x & 63;
+  const int32_t W = wpre[kKeyRange];
+  for (int32_t t = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); t < W;
+       t += (int32_t)((gridDim.x * blockDim.x) >> 6)) {
+    int lo = 0, hi = kKeyRange;  // the item's key: the last kk with wpre[kk] <= t
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (wpre[mid] <= t) lo = mid; else hi = mid;
+    }
+    const int kk = lo;
+    const int32_t g = k_gbeg[kk] + (t - wpre[kk]);
+    const int32_t col = (int32_t)(cv.g_key[g] & kColMask);
+    const int32_t sb = seg[2 * kk], se = seg[2 * kk + 1];
+    const int32_t fb = seg[2 * (kk | kKeyRange)], fe = seg[2 * (kk | kKeyRange) + 1];
+    int32_t cnt = fe > fb ? P[(int64_t)(fe - 1) * kWideCh + lane] : 0;
+    if (se > sb) {
+      const int32_t pb = cv.g_beg[g], pn = cv.g_beg[g + 1] - pb;
+      int32_t carry = -2;  // the largest B of the valid runs so far (-2: none)
+      bool open = false;
+      int32_t aopen = 0;
+      auto close = [&](int32_t a, int32_t b) {
+        cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : 0);
+      };
+      for (int32_t base = 0; base < pn; base += 64) {
+        const int32_t i = base + lane;
+        int32_t A = INT32_MAX, B = -2;
+        if (i < pn) {
+          const int32_t v = cv.p_m2[pb + i];
+          A = sb + lb32(U2s + sb, se - sb, v);      // first frame with U2 >= v
+          B = sb + ub32(L2s + sb, se - sb, v) - 1;  // last frame with L2 <= v
+        }
+        const bool ok = A <= B;
+        int32_t bm = ok ? B : -2;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {  // inclusive running max of B over the valid runs
+          const int32_t y = __shfl_up(bm, o, 64);
+          if (lane >= o) bm = max(bm, y);
+        }
+        int32_t pe = __shfl_up(bm, 1, 64);
+        if (lane == 0) pe = -2;
+        pe = max(pe, carry);  // the largest B before this lane's run
+        unsigned long long starts = __ballot(ok && A > pe + 1);  // a gap before it: a new merged run
+        while (starts) {
+          const int sl = __ffsll((long long)starts) - 1;
+          starts &= starts - 1;
+          const int32_t as = __shfl(A, sl, 64), ps = __shfl(pe, sl, 64);
+          if (open) close(aopen, ps);
+          open = true;
+          aopen = as;
+        }
+        carry = max(carry, __shfl(bm, 63, 64));
+      }
+      if (open) close(aopen, carry);
+    }
+    if (cnt) atomicAdd(&score[(int64_t)col * kWideCh + lane], cnt);
+  }
+}
+
+// Per chunk: each query's max over clips of (count << 32 | tie key); the score rows back to zero.
+__global__ __launch_bounds__(256) void wide_final_kernel(int32_t q0, int32_t nq, int32_t C,
+                                                         const int32_t* __restrict__ tiekey, int32_t* __restrict__ score,
+                                                         unsigned long long* __restrict__ best) {
+  __shared__ unsigned long long red[4][kWideCh];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  unsigned long long run = 0;
+  for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < C; c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
+    const int32_t v = score[c * kWideCh + lane];
+    if (v) {
+      const unsigned long long k = ((unsigned long long)(uint32_t)v << 32) | (uint32_t)tiekey[c];
+      run = k > run ? k : run;
+      score[c * kWideCh + lane] = 0;
+    }
+  }
+  red[wave][lane] = run;
+  __syncthreads();
+  if (wave == 0) {
+    unsigned long long m = red[0][lane];
+    for (int w = 1; w < 4; w++) m = red[w][lane] > m ? red[w][lane] : m;
+    if (m && q0 + lane < nq) atomicMax(&best[q0 + lane], m);
+  }
+}
+
+}  // namespace
+
+void WideScratch::release() {
+  for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
+                  (void*)P, (void*)seg, (void*)wpre, (void*)score, (void*)info, tmp})
+    if (p) (void)hipFree(p);
+  ka = kb = nullptr;
+  ua = ub = nullptr;
+  va = vb = L2s = U2s = P = seg = wpre = score = info = nullptr;
+  qis = nullptr;
+  tmp = nullptr;
+  tmp_bytes = 0;
+  cap_nf = cap_nch = cap_c = 0;
+}
+
+hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s) {
+  const int64_t nch = (nq + kWideCh - 1) / kWideCh;
+  hipError_t e = hipSuccess;
+  if (nf > cap_nf) {
+    for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
+                    (void*)P, tmp})
+      if (p) (void)hipFree(p);
+    ka = kb = nullptr;
+    ua = ub = nullptr;
+    va = vb = L2s = U2s = P = nullptr;
+    qis = nullptr;
+    tmp = nullptr;
+    cap_nf = 0;
+    if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
+        (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
+        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideCh)))
+      return e;
+    size_t t1 = 0, t2 = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, ua, ub, va, vb, (int)nf, 0, 32, s)) ||
+        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, t2, ka, kb, va, vb, (int)nf, 0, 64, s)))
+      return e;
+    tmp_bytes = t1 > t2 ? t1 : t2;
+    if ((e = hipMalloc(&tmp, tmp_bytes > 0 ? tmp_bytes : 1))) return e;
+    cap_nf = nf;
+  }
+  if (nch > cap_nch) {
+    if (seg) (void)hipFree(seg);
+    if (wpre) (void)hipFree(wpre);
+    seg = wpre = nullptr;
+    cap_nch = 0;
+    if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1)))) return e;
+    cap_nch = nch;
+  }
+  if (C > cap_c) {
+    if (score) (void)hipFree(score);
+    score = nullptr;
+    cap_c = 0;
+    if ((e = dmalloc(&score, (int64_t)C * kWideCh))) return e;
+    if ((e = hipMemsetAsync(score, 0, sizeof(int32_t) * (size_t)C * kWideCh, s))) return e;  // kept zero by wide_final
+    cap_c = C;
+  }
+  if (!info && (e = dmalloc(&info, 2))) return e;
+  return hipSuccess;
+}
+
+hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
+                                    WideScratch* ws, bool* eligible, hipStream_t s) {
+  *eligible = false;
+  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 21)) return hipSuccess;
+  hipError_t e;
+  const int64_t nch = (nq + kWideCh - 1) / kWideCh;
+  if ((e = hipMemsetAsync(ws->info, 0, 2 * sizeof(int32_t), s))) return e;
+  hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
+  size_t tb = ws->tmp_bytes;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, (int)nf, 0, 32, s))) return e;
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf, ws->vb, ws->ka, ws->info);
+  tb = ws->tmp_bytes;
+  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, (int)nf, 0, 64, s))) return e;
+  int32_t info[2] = {0, 0};
+  if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
+  if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
+  const int64_t n = info[0];
+  if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
+  if (n > 0)
+    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, d_qoff, nq, n, ws->kb, ws->va, ws->L2s,
+                       ws->U2s, ws->qis, ws->seg);
+  const int64_t nsegs = nch * kWideSegs;
+  hipLaunchKernelGGL(wide_prefix_kernel, dim3(grid_for(nsegs * 64)), dim3(256), 0, s, nsegs, ws->seg, ws->qis, ws->P);
+  if ((e = hipGetLastError())) return e;
+  *eligible = true;
+  return hipSuccess;
+}
+
+hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
+                            WideScratch* ws, unsigned long long* d_best, hipStream_t s) {
+  if (nq <= 0 || !cells || !cells->valid || !cells->k_gbeg) return hipErrorInvalidValue;
+  (void)nf;
+  const int64_t nch = (nq + kWideCh - 1) / kWideCh;
+  CellView cv;
+  memset(&cv, 0, sizeof cv);
+  cv.p_m2 = cells->p_m2;
+  cv.g_key = cells->g_key;
+  cv.g_beg = cells->g_beg;
+  cv.valid = 1;
+  hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
+  for (int64_t ch = 0; ch < nch; ch++) {
+    hipLaunchKernelGGL(wide_groups_kernel, dim3(4096), dim3(256), 0, s, ws->wpre + ch * (kKeyRange + 1),
+                       ws->seg + ch * kWideSegs * 2, cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, ws->score);
+    hipLaunchKernelGGL(wide_final_kernel, dim3(1024), dim3(256), 0, s, (int32_t)(ch * kWideCh), nq, C, d_tiekey, ws->score,
+                       d_best);
+  }
   return hipGetLastError();
 }
 

@@ -192,8 +192,47 @@ def test_search_pcm_vs_oracle(engine, oracle, tfp_lib, coefs, tol, low, high):
         assert fcs[i] == fc == 157
 
 
-def test_search_scan_fallback_many_frames_one_key(engine, oracle, tfp_lib):
-    """> 2048 frames with the same key exceed fp16-exact counts: the scan path must take over."""
+@pytest.mark.parametrize("path", ["sweep", "cells"])
+@pytest.mark.parametrize("tol,low,high", [(0.001, -1, -1), (0.01, -1, -1), (0.1, 50, 60), (0.45, -1, -1)])
+def test_general_paths_vs_oracle(oracle, tfp_lib, path, tol, low, high):
+    """coefs=2 through the general path both ways (csrc/tfp_scan.hip): the sweep by groups (the
+    default) and the clip-set cells (forced with TFP_WIDE_MIN_TOL, read at engine creation).
+    150 queries = three 64-query chunks of the sweep, the last partial; the 50/60 Hz filter leaves
+    frames whose max2 condition is dropped (they hit every clip of their key,
+    src/fp_handler.c:324-337). == the oracle."""
+    eng = _engine_with(tfp_lib, {"TFP_WIDE_MIN_TOL": "0" if path == "sweep" else "1e9"})
+    try:
+        uuids, micro, clip = _build_db(eng, oracle, tfp_lib, 120, 12)
+        qpcm = _queries(tfp_lib, 150, 120, 12, 5)
+        off = np.arange(151) * qpcm.shape[1]
+        res, fcs = eng.search_pcm_batch(qpcm.reshape(-1), off, tfp_lib.params(2, tol, low, high))
+        nfound = 0
+        for i in range(150):
+            _, qdb, _ = oracle.fingerprint(qpcm[i])
+            found, w, mc, fc = oracle.search(micro[:, 0], micro[:, 1], clip, uuids, qdb[:, 0], qdb[:, 1],
+                                             2, tol, low, high)
+            exp = {"audio_uuid": uuids[w], "match_count": mc} if found else None
+            got = None if res[i] is None else {"audio_uuid": res[i]["audio_uuid"], "match_count": res[i]["match_count"]}
+            assert got == exp, (i, tol)
+            assert fcs[i] == fc
+            nfound += found
+        assert nfound > 0
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("path", ["sweep", "cells"])
+def test_search_scan_fallback_many_frames_one_key(oracle, tfp_lib, path):
+    """> 2048 frames with the same key exceed fp16-exact counts: the general path must take over
+    (both of its forms: the sweep by groups, the clip-set cells)."""
+    engine = _engine_with(tfp_lib, {"TFP_WIDE_MIN_TOL": "0" if path == "sweep" else "1e9"})
+    try:
+        _fallback_case(engine, oracle, tfp_lib)
+    finally:
+        engine.close()
+
+
+def _fallback_case(engine, oracle, tfp_lib):
     uuids, micro, clip = _build_db(engine, oracle, tfp_lib, 40, 6)
     q = np.zeros(2100 * 256, np.int16)  # silence: every frame has the same trunc key
     res, fcs = engine.search_pcm_batch(q, [0, len(q)], tfp_lib.params(1, 0.45))
