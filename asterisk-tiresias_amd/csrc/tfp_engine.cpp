@@ -360,7 +360,7 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
   else
     HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
                                  d_toff, d_tclip, toff[nclips], nf, e->micro.as<int32_t>(), e->db.as<double>(),
-                                 e->stream, exact_q ? e->logfix : LogFix{}));
+                                 e->stream, exact_q ? e->logfix : LogFix{}, nclips == 1 && soff[0] == 0 ? soff[1] : -1));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
   return TFP_OK;

@@ -192,6 +192,20 @@ __device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns
   return make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
 }
 
+// The same, inline (the 8 kHz kernel's edge passes): a call makes the caller wait for every
+// outstanding load first, and a batch-1 query's PCM is read across PCIe from mapped host memory.
+__device__ __forceinline__ int4 fetch_chunk_inline(const int16_t* clip, int64_t ns, int64_t s) {
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; e++) {
+    const int64_t a = s + 2 * e;
+    const uint32_t lo = (a >= 0 && a < ns) ? (uint16_t)clip[a] : 0u;
+    const uint32_t hi = (a + 1 >= 0 && a + 1 < ns) ? (uint16_t)clip[a + 1] : 0u;
+    w[e] = lo | (hi << 16);
+  }
+  return make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+}
+
 // 16-byte chunks of a pass into registers, issued one pass ahead of use.
 template <typename Smp>
 __device__ __forceinline__ void fetch_pass(const PassSrc<Smp>& p, bool valid, int lane,
@@ -696,11 +710,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
-    float rare_thr, LogFix fx) {
+    float rare_thr, LogFix fx, int64_t single_ns) {
   constexpr int LA = 36, LB = 16, LC = 8;  // DspTables::fixed8k()
   // dB + "%f" in finish_db_kernel for throughput launches (full waves); in the tile tail for small
   // ones (4-frame tiles, batch-1 latency), which saves a launch
   constexpr bool kSplitTail = kPasses >= 2;
+#ifdef TFP_STAMPS
+  const uint64_t t_entry = __builtin_amdgcn_s_memtime();
+#endif
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveLds8 WL[kBlockWaves];
@@ -714,6 +731,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   };
   auto tile_of = [&](int b) {
     Tile t;
+    if (single_ns >= 0) {  // one clip at d_pcm[0]: no layout loads
+      t.c = 0;
+      t.f0 = (int64_t)b * (4 * kPasses);
+      t.s0 = 0;
+      t.ns = single_ns;
+      return t;
+    }
     t.c = __builtin_amdgcn_readfirstlane(tclip[b]);
     t.f0 = (int64_t)(b - toff[t.c]) * (4 * kPasses);
     t.s0 = sbeg[t.c];
@@ -732,7 +756,22 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const int chunk = lane + 64 * r;
         pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
       }
-    } else {
+    } else if constexpr (kPasses == 1) {
+      // clip edges of a small launch (its PCM may be across PCIe): chunks wholly inside are one
+      // 16-byte load, wholly outside zeros, no call (a call waits for every outstanding load)
+      const bool aligned = (reinterpret_cast<uintptr_t>(clip) & 15) == 0;
+#pragma unroll
+      for (int r = 0; r < kChunkRounds; r++) {
+        const int chunk = lane + 64 * r;
+        const int64_t s0 = sb + 8 * chunk;
+        int4 v = make_int4(0, 0, 0, 0);
+        if (valid && chunk < kPassChunks && s0 + 8 > 0 && s0 < t.ns) {
+          if (aligned && s0 >= 0 && s0 + 8 <= t.ns) v = *reinterpret_cast<const int4*>(clip + s0);
+          else v = fetch_chunk_inline(clip, t.ns, s0);  // straddling the end, or an unaligned clip
+        }
+        pf[r] = v;
+      }
+    } else {  // (throughput launches: 2 edge passes per clip, their latency hidden; less code in the loop)
 #pragma unroll
       for (int r = 0; r < kChunkRounds; r++) {
         const int chunk = lane + 64 * r;
@@ -741,14 +780,14 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     }
   };
 
-  // The first tile's bounds and PCM are requested before the tables are staged, so their
-  // latency overlaps the staging (most of a small launch's time). The PCM is prefetched one pass
-  // ahead (a two-pass distance measured no faster: the pass is bound by LDS traffic and latency,
-  // not by the PCM loads).
+  // The first tile's bounds are known before the tables are staged (a one-clip launch passes
+  // them as an argument), and its PCM is requested right after the table loads, so its latency
+  // overlaps the staging (most of a small launch's time). The PCM is prefetched one pass ahead
+  // (a two-pass distance measured no faster: the pass is bound by instruction issue, not by the
+  // PCM loads).
   int4 pf[kChunkRounds];
   int b = blockIdx.x * kBlockWaves + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
-  fetch(cur, 0, b < ntiles, pf);
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
   cf* winr = reinterpret_cast<cf*>(S.window);
@@ -787,6 +826,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     mw[r] = wsrc[idx < kMsW ? idx : kMsW - 1];
   }
   const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
+  // the first pass's PCM after the table loads (loads complete in order, so the tables' waits
+  // would otherwise include the PCM's: a batch-1 query's is read across PCIe)
+  fetch(cur, 0, b < ntiles, pf);
   winr[tid] = cf{win0, win1};
   twr[tid] = cf{twk, twk2};
   if (tid < 240) S.lane_tw[lk1 - 1][lL] = cf{ltre, ltim};
@@ -807,6 +849,9 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   }
   const unsigned long long empty_filters = __ballot(lane < kFilters && mlen == 0);  // (log of 0 + 2e-42)
   __syncthreads();
+#ifdef TFP_STAMPS
+  const uint64_t t_staged = __builtin_amdgcn_s_memtime();
+#endif
 
   WaveLds8& M = WL[wave];
   cf* W = M.scratch[grp];
@@ -1094,7 +1139,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
 #pragma unroll 8
           for (int i = 0; i < kFilters; i++) acc = acc + lrow[i] * S.dct[cfi][i];
         }
-        const int64_t g = foff[cur.c] + f;
+        const int64_t g = (single_ns >= 0 ? 0 : foff[cur.c]) + f;
         if constexpr (kSplitTail) {
           micro[2 * g + cfi] = __builtin_bit_cast(int32_t, acc);  // finish_db_kernel: dB + "%f" on full waves
         } else {
@@ -1108,9 +1153,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
     cur = nxt;
   }
 #ifdef TFP_STAMPS
+  const uint64_t t_end = __builtin_amdgcn_s_memtime();
   if (lane == 0 && (blockIdx.x & 63) == 0)
-    printf("stamps block %d wave %d passes %d total %lu | lead %lu stage %lu fft1 %lu fft2 %lu split %lu mel %lu\n",
-           (int)blockIdx.x, wave, npass, (unsigned long)(tprev - tstart), (unsigned long)st[0], (unsigned long)st[1],
+    printf("stamps<%d> block %d wave %d passes %d | entry->staged %lu staged->loop %lu loop %lu after-last-pass %lu | "
+           "lead %lu stage %lu fft1 %lu fft2 %lu split %lu mel %lu\n",
+           kPasses, (int)blockIdx.x, wave, npass, (unsigned long)(t_staged - t_entry), (unsigned long)(tstart - t_staged),
+           (unsigned long)(tprev - tstart), (unsigned long)(t_end - tprev), (unsigned long)st[0], (unsigned long)st[1],
            (unsigned long)st[2], (unsigned long)st[3], (unsigned long)st[4], (unsigned long)st[5]);
 #endif
 }
@@ -1181,7 +1229,7 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
 hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
-                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx) {
+                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx, int64_t single_ns) {
   const bool v8 = fixed8k && (tile_frames == 4 || !cfg.force_generic);
   if (v8 ? !(tile_frames == 4 || tile_frames == kTile8k) : tile_frames != kFramesPerBlock) return hipErrorInvalidValue;
   if (ntiles <= 0) return hipSuccess;
@@ -1192,10 +1240,10 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
   if (v8) {
     if (tile_frames == 4) {  // fingerprint8k_kernel<1> finishes its own tail
       hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
-                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx);
+                         d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx, single_ns);
     } else {
       hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg,
-                         d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx);
+                         d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx, single_ns);
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;

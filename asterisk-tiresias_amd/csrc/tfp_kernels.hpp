@@ -66,7 +66,11 @@ bool DspTables_fixed8k(const DspTables& t);
 hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables, bool fixed8k, int32_t tile_frames,
                               const int16_t* d_pcm, const int64_t* d_sbeg, const int64_t* d_send, const int64_t* d_foff,
                               const int32_t* d_toff, const int32_t* d_tclip, int32_t ntiles, int64_t nframes,
-                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx);
+                              int32_t* d_micro, double* d_db, hipStream_t s, const LogFix& fx,
+                              int64_t single_ns = -1);
+// single_ns >= 0 (8 kHz kernel): the batch is one clip of single_ns samples at d_pcm[0], frames from
+// 0, so the kernel takes its tile bounds from the argument instead of a chain of layout loads
+// (batch-1: the first PCM request goes out at the kernel's first instruction).
 // fx: the glibc log correction table (device copy; tfp_math.hpp LogFix) used for d_db's frame
 // values, so they equal glibc's 10*log10|c| bit for bit (the stored micro-units need none).
 // fp32 samples (the values aubio_source_do produces: multichannel mean, 24/32-bit or float
