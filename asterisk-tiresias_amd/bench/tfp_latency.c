@@ -39,3 +39,38 @@ int tfp_latency_search_pcm(tfp_engine* eng, const int16_t* pcm, int64_t n, int32
   tfp_host_free(hq);
   return rc;
 }
+
+/* Stream ticks from C, as the shim's channel threads would push them: ticks
+ * t < nticks of pcm (int16 [nchannels][total] row-major, tick samples each, starting at sample
+ * first), one tfp_stream_push per tick with results into one caller array; wall time per tick in
+ * ms -> out_ms[t]; *found_last = the channels found on the last tick. */
+int tfp_latency_stream(tfp_stream* st, const int16_t* pcm, int32_t nchannels, int64_t total, int64_t first,
+                       int32_t tick, int32_t nticks, const tfp_search_params* params, double* out_ms,
+                       int32_t* found_last) {
+  int32_t t, c;
+  int rc = TFP_OK;
+  int16_t* blk;
+  tfp_result* res;
+  if (!st || !pcm || nchannels <= 0 || tick <= 0 || nticks < 0 || !params || !out_ms || !found_last ||
+      first < 0 || first + (int64_t)tick * nticks > total)
+    return TFP_E_ARG;
+  if (tfp_host_alloc(sizeof(int16_t) * (size_t)nchannels * (size_t)tick, (void**)&blk) != TFP_OK) return TFP_E_NOMEM;
+  if (tfp_host_alloc(sizeof(tfp_result) * (size_t)nchannels, (void**)&res) != TFP_OK) {
+    tfp_host_free(blk);
+    return TFP_E_NOMEM;
+  }
+  *found_last = 0;
+  for (t = 0; t < nticks && rc == TFP_OK; t++) {
+    double t0, t1;
+    for (c = 0; c < nchannels; c++)  /* the tick's samples arrive: untimed, as the channel audio */
+      memcpy(blk + (int64_t)c * tick, pcm + (int64_t)c * total + first + (int64_t)t * tick, sizeof(int16_t) * (size_t)tick);
+    t0 = now_ms();
+    rc = tfp_stream_push(st, blk, tick, params, res);
+    t1 = now_ms();
+    out_ms[t] = t1 - t0;
+  }
+  for (c = 0; c < nchannels; c++) *found_last += res[c].found;
+  tfp_host_free(res);
+  tfp_host_free(blk);
+  return rc;
+}

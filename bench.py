@@ -25,6 +25,7 @@ Also reported (same JSON line):
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -458,7 +459,6 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     if not dist:
         # the same calls from C (asterisk-tiresias_amd/bench/tfp_latency.c), as the Asterisk shim's
         # channel threads make them: no Python/ctypes marshalling in the timed region
-        import ctypes
         clat = ctypes.CDLL(os.path.join(os.path.dirname(T.LIB_PATH), "libtfp_latency.so"))
         n_it = max(200, 10 * len(host_q))
         out_ms = np.zeros(n_it, np.float64)
@@ -554,7 +554,9 @@ def match_cpu_baseline(args, T, eng, torch, dev, sh):
 def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):
     """configs[4] (C5): live channels, 160-sample SLIN ticks, 3000 ms window (24000 samples =
     94 frames), rolling fingerprint + match against the DB. Latency = host tick in -> every
-    channel's result on the host (tfp_stream_push, application_handler.c:152-185).
+    channel's result on the host (tfp_stream_push, application_handler.c:152-185), timed from C
+    (bench/tfp_latency.c, as the shim's threads call it); the same ticks through the Python
+    mirror (result dicts for every channel) are reported beside it.
     N GPUs: the channels are split round-robin over the ranks and every rank holds the whole DB
     (1.13 GB at 100k clips), so a tick needs no collective; the reported per-tick
     latency is the max over ranks."""
@@ -565,7 +567,7 @@ def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):
         enroll(eng, torch, dev, sh, list(range(args.db_clips)))
         eng.index_commit()
     rng = np.random.default_rng(SEED_Q + 1)
-    span = W + nt * tick
+    span = W + 2 * nt * tick  # the C-timed ticks, then the Python-timed ones
     clips = [int(rng.integers(args.db_clips)) for _ in range(nch)]
     offs = [256 * int(rng.integers(0, (n_db - span) // HOP)) for _ in range(nch)]
     mine = list(range(rank, nch, world))
@@ -577,21 +579,34 @@ def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):
     p = T.params(1, 0.001)
     for t in range(W // tick):  # fill the windows (ingest only)
         st.push(pcm[:, t * tick:(t + 1) * tick])
-    lat, found = [], 0
     base = W // tick
-    for t in range(nt):
-        s0 = (base + t) * tick
+    clat = ctypes.CDLL(os.path.join(os.path.dirname(T.LIB_PATH), "libtfp_latency.so"))
+    clat.tfp_latency_stream.restype = ctypes.c_int
+    pcm = np.ascontiguousarray(pcm, np.int16)
+    cms = np.zeros(nt, np.float64)
+    cfound = ctypes.c_int32()
+    barrier()
+    rc = clat.tfp_latency_stream(st._h, ctypes.c_void_p(pcm.ctypes.data), ctypes.c_int32(len(mine)), ctypes.c_int64(span),
+                                 ctypes.c_int64(W), ctypes.c_int32(tick), ctypes.c_int32(nt), ctypes.byref(p),
+                                 ctypes.c_void_p(cms.ctypes.data), ctypes.byref(cfound))
+    assert rc == 0, rc
+    found = cfound.value
+    lat = cms
+    plat = []
+    for t in range(nt):  # the same through the Python mirror (ctypes + a result dict per channel)
+        s0 = (base + nt + t) * tick
         blk = np.ascontiguousarray(pcm[:, s0:s0 + tick])
-        barrier()
         t0 = time.perf_counter()
-        res = st.push(blk, p)
-        lat.append((time.perf_counter() - t0) * 1e3)
-        found = sum(r is not None for r in res)
-    lat = np.array(lat)
+        st.push(blk, p)
+        plat.append((time.perf_counter() - t0) * 1e3)
+    plat = np.array(plat)
     if dist:
         tl = torch.tensor(lat, dtype=torch.float64, device=dev)
         dist.all_reduce(tl, op=dist.ReduceOp.MAX)
         lat = tl.cpu().numpy()
+        tl = torch.tensor(plat, dtype=torch.float64, device=dev)
+        dist.all_reduce(tl, op=dist.ReduceOp.MAX)
+        plat = tl.cpu().numpy()
         tf = torch.tensor([found], dtype=torch.int64, device=dev)
         dist.all_reduce(tf)
         found = int(tf.item())
@@ -601,6 +616,8 @@ def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):
                         + ("1 GPU" if world == 1 else f"{world} GPUs, channels split round-robin, DB replicated, no collective"),
             "ticks_timed": len(lat), "tick_latency_p50_ms": float(np.percentile(lat, 50)),
             "tick_latency_p99_ms": float(np.percentile(lat, 99)), "tick_budget_ms": 1e3 * tick / 8000,
+            "tick_harness": "C loop over tfp_stream_push (bench/tfp_latency.c), the tick's samples in a tfp_host_alloc buffer",
+            "tick_latency_p50_ms_python": float(np.percentile(plat, 50)),
             "fingerprints_per_tick": nch * ((W + HOP - 1) // HOP), "channels_found_last_tick": found}
 
 
