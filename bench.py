@@ -190,6 +190,10 @@ def main():
                      "bytes_per_unit": BYTES_PER_FP, "units_per_launch": F, "avg_launch_ms": avg_launch_s * 1e3,
                      "limiter": "not HBM: instruction issue at 2 waves/SIMD (~170 wave64 VALU + ~24 LDS + ~13 SALU per fingerprint) "
                                 "(bit-exact fp32 DSP + glibc-exact logs); DESIGN.md §4"},
+        # the same throughput as clips/s and as multiples of real time (a fingerprint
+        # is one 256-sample hop of 8 kHz audio)
+        "derived": {"clips_per_s": value * nclips / (F or 1), "x_realtime": value * HOP / 8000.0,
+                    "clip_seconds": n / 8000.0},
     }
     del micro
 
