@@ -37,3 +37,17 @@ def test_product_tables_equal_oracle(oracle, tmp_path, sr):
     assert np.array_equal(tw512_im.view(np.uint32), as_(t.tw512_im))
     assert np.array_equal(dct.view(np.uint32), np.ctypeslib.as_array(t.dct).reshape(2, 40).view(np.uint32))
     assert np.array_equal(mel.view(np.uint32), np.ctypeslib.as_array(t.mel).reshape(40, 257).view(np.uint32))
+
+
+def test_frame_pair_schedule_8k(tmp_path):
+    """The throughput kernel's frame-pair filterbank schedule (csrc/tfp_tables.cpp
+    build_fb_schedule) rebuilds every 8 kHz filter's dense row bit for bit, one job per filter."""
+    exe = str(tmp_path / "fb")
+    src = os.path.join(REPO, "tests", "native", "check_fb_schedule.cpp")
+    tab = os.path.join(REPO, "asterisk-tiresias_amd", "csrc", "tfp_tables.cpp")
+    inc = os.path.join(REPO, "asterisk-tiresias_amd", "csrc")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-builtin", "-I", inc, src, tab, "-o", exe],
+                   check=True)
+    r = subprocess.run([exe, "8000"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("OK: 34 filters")
