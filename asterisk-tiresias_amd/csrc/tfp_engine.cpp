@@ -727,7 +727,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     if (e->cells.valid) {
       HIPCHK(e, e->wide.reserve(nf, nq, C, s));
       bool ok = false;
-      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, &e->wide, &ok, s));
+      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, &e->wide, &ok,
+                                               s));
       if (ok) {
         HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
         done = true;

@@ -210,14 +210,17 @@ struct WideScratch {
   int32_t *va = nullptr, *vb = nullptr;             // frame indices
   int32_t *L2s = nullptr, *U2s = nullptr;           // sorted windows
   uint8_t* qis = nullptr;                            // sorted frames' query within its chunk
-  int32_t* P = nullptr;                              // [nf][kChunk] in-segment prefix counts
+  int32_t* P = nullptr;                              // [nf][kChunk] in-chunk prefix counts
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
   int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix
-  int32_t* score = nullptr;                          // [C][kChunk], zero between calls
+  int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk
+  int64_t* chw = nullptr;                            // [nchunks + 1] first work item of each chunk
+  uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
   int32_t* info = nullptr;                           // [2]: frames kept, ineligible frames
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  int64_t cap_nf = 0, cap_nch = 0, cap_c = 0;
+  int64_t cap_nf = 0, cap_nch = 0, cap_score = 0;
+  int32_t slab = 0;                                  // chunks per groups launch
   hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
   void release();
   WideScratch() = default;
@@ -226,9 +229,10 @@ struct WideScratch {
   ~WideScratch() { release(); }
 };
 // Sorts the batch's frames; *eligible = false (nothing else queued) when a frame needs the row
-// scan (key outside the cache, window outside int32), the caller then takes launch_scan.
+// scan (key outside the cache, window outside int32) or a query has 2^16 frames or more (the
+// score rows hold 16-bit counts), the caller then takes launch_scan.
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    WideScratch* ws, bool* eligible, hipStream_t s);
+                                    int64_t max_qframes, WideScratch* ws, bool* eligible, hipStream_t s);
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s);

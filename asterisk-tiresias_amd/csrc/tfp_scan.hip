@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "tfp_kernels.hpp"
 #include "tfp_math.hpp"
 
@@ -483,17 +485,42 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
   }
 }
 
-// In-segment prefix counts: one wave per segment, lane q counts query q's frames.
-__global__ __launch_bounds__(256) void wide_prefix_kernel(int64_t nsegs, const int32_t* __restrict__ seg,
-                                                          const uint8_t* __restrict__ qis, int32_t* __restrict__ P) {
-  const int lane = threadIdx.x & 63;
-  for (int64_t sgi = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; sgi < nsegs;
-       sgi += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int32_t b = seg[2 * sgi], e = seg[2 * sgi + 1];
-    int32_t run = 0;
-    for (int32_t i = b; i < e; i++) {
-      run += qis[i] == lane;
-      P[(int64_t)i * kWideCh + lane] = run;
+// Chunk boundaries in the sorted frames: cbeg[ch] = first frame of chunk ch (n for ch >= chunks).
+__global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, int64_t n, int64_t nch,
+                                 int32_t* __restrict__ cbeg) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << 43);
+}
+
+// In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i]: one 16-wave workgroup per
+// chunk, each wave over a contiguous 64-aligned share (its counts first, then the writes, offset
+// by the waves before it). Lane q counts query q among 64 frames by reading their queries out of
+// the lanes (no per-frame memory dependency).
+__global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg,
+                                                           const uint8_t* __restrict__ qis, int32_t* __restrict__ P) {
+  __shared__ int32_t tot[16][kWideCh];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int32_t b = cbeg[blockIdx.x], n = cbeg[blockIdx.x + 1] - b;
+  const int32_t per = (n + 16 * 64 - 1) / (16 * 64) * 64;
+  const int32_t r0 = min(n, wv * per), r1 = min(n, r0 + per);
+  int32_t cnt = 0;
+  for (int32_t i = r0; i < r1; i += 64) {
+    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
+#pragma unroll
+    for (int j = 0; j < 64; j++) cnt += __builtin_amdgcn_readlane(x, j) == lane;
+  }
+  tot[wv][lane] = cnt;
+  __syncthreads();
+  int32_t run = 0;
+  for (int w = 0; w < wv; w++) run += tot[w][lane];
+  for (int32_t i = r0; i < r1; i += 64) {
+    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
+    int32_t* row = P + ((int64_t)b + i) * kWideCh + lane;
+    const int m = min(64, r1 - i);
+#pragma unroll
+    for (int j = 0; j < 64; j++) {
+      run += __builtin_amdgcn_readlane(x, j) == lane;
+      if (j < m) row[(int64_t)j * kWideCh] = run;
     }
   }
 }
@@ -531,6 +558,30 @@ __global__ __launch_bounds__(256) void wide_work_kernel(const int32_t* __restric
   if (t == 255) wp[kKeyRange] = part[255];
 }
 
+// Exclusive prefix of the chunks' work counts (wpre[ch][kKeyRange]): chw[0..nch], one block.
+__global__ __launch_bounds__(1024) void wide_chw_kernel(const int32_t* __restrict__ wpre, int64_t nch,
+                                                        int64_t* __restrict__ chw) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  int64_t carry = 0;
+  for (int64_t c0 = 0; c0 < nch; c0 += 1024) {
+    const int64_t c = c0 + t;
+    const int64_t v = c < nch ? (int64_t)wpre[c * (kKeyRange + 1) + kKeyRange] : 0;
+    part[t] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int64_t y = t >= o ? part[t - o] : 0;
+      __syncthreads();
+      part[t] += y;
+      __syncthreads();
+    }
+    if (c < nch) chw[c] = carry + part[t] - v;
+    carry += part[1023];
+    __syncthreads();
+  }
+  if (t == 0) chw[nch] = carry;
+}
+
 __device__ __forceinline__ int32_t lb32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] >= v
   int32_t lo = 0, hi = n;
   while (lo < hi) {
@@ -548,36 +599,79 @@ __device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) 
   return lo;
 }
 
-// One wave per (key, clip group) of the chunk's work list; lane q = query q0 + q.
-__global__ __launch_bounds__(256) void wide_groups_kernel(const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
-                                                          CellView cv, const int32_t* __restrict__ k_gbeg,
-                                                          const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s,
-                                                          const int32_t* __restrict__ P, int32_t* __restrict__ score) {
+// The work items (chunk, key, clip group) of chunks [ch0, ch1), in chunk and key order; each wave
+// takes a contiguous share, so it locates its first item by binary search and then steps through
+// keys and chunks. Lane q = query 64 ch + q. A group's counts go to the slab's score rows as 16-bit
+// pairs (query 2i low, 2i + 1 high: a count is at most the query's frames, < 2^16).
+__global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t ch1, const int64_t* __restrict__ chw,
+                                                          const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
+                                                          const int32_t* __restrict__ cbeg, CellView cv,
+                                                          const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
+                                                          const int32_t* __restrict__ U2s, const int32_t* __restrict__ P,
+                                                          int32_t C, uint32_t* __restrict__ score) {
   const int lane = threadIdx.x & 63;
-  const int32_t W = wpre[kKeyRange];
-  for (int32_t t = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6); t < W;
-       t += (int32_t)((gridDim.x * blockDim.x) >> 6)) {
-    int lo = 0, hi = kKeyRange;  // the item's key: the last kk with wpre[kk] <= t
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (wpre[mid] <= t) lo = mid; else hi = mid;
+  const int64_t W0 = chw[ch0], W1 = chw[ch1];
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t per = (W1 - W0 + nw - 1) / nw;
+  int64_t t = W0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * per;
+  const int64_t tend = min(W1, t + per);
+  if (t >= tend) return;
+  int ch = ch0;
+  {
+    int hi = ch1;  // the last chunk with chw[ch] <= t
+    while (hi - ch > 1) {
+      const int mid = (ch + hi) >> 1;
+      if (chw[mid] <= t) ch = mid; else hi = mid;
     }
-    const int kk = lo;
-    const int32_t g = k_gbeg[kk] + (t - wpre[kk]);
+  }
+  const int32_t* wp = wpre + (int64_t)ch * (kKeyRange + 1);
+  int32_t tt = (int32_t)(t - chw[ch]);
+  int kk = 0;
+  {
+    int hi = kKeyRange;  // the last key with wp[kk] <= tt
+    while (hi - kk > 1) {
+      const int mid = (kk + hi) >> 1;
+      if (wp[mid] <= tt) kk = mid; else hi = mid;
+    }
+  }
+  int32_t kend = wp[kk + 1];
+  bool fresh = true;
+  int32_t sb = 0, se = 0, base = 0, fcnt = 0, gk0 = 0;
+  for (; t < tend; t++, tt++) {
+    while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
+      if (++kk == kKeyRange) {
+        ++ch;
+        wp += kKeyRange + 1;
+        tt = (int32_t)(t - chw[ch]);
+        kk = 0;
+      }
+      kend = wp[kk + 1];
+      fresh = true;
+    }
+    if (fresh) {
+      fresh = false;
+      const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
+      const int32_t cb = cbeg[ch];
+      sb = sg[2 * kk];
+      se = sg[2 * kk + 1];
+      const int32_t fb = sg[2 * (kk | kKeyRange)], fe = sg[2 * (kk | kKeyRange) + 1];
+      base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
+      fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
+      gk0 = k_gbeg[kk] - wp[kk];
+    }
+    const int32_t g = gk0 + tt;
     const int32_t col = (int32_t)(cv.g_key[g] & kColMask);
-    const int32_t sb = seg[2 * kk], se = seg[2 * kk + 1];
-    const int32_t fb = seg[2 * (kk | kKeyRange)], fe = seg[2 * (kk | kKeyRange) + 1];
-    int32_t cnt = fe > fb ? P[(int64_t)(fe - 1) * kWideCh + lane] : 0;
+    int32_t cnt = fcnt;
     if (se > sb) {
       const int32_t pb = cv.g_beg[g], pn = cv.g_beg[g + 1] - pb;
       int32_t carry = -2;  // the largest B of the valid runs so far (-2: none)
       bool open = false;
       int32_t aopen = 0;
       auto close = [&](int32_t a, int32_t b) {
-        cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : 0);
+        cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : base);
       };
-      for (int32_t base = 0; base < pn; base += 64) {
-        const int32_t i = base + lane;
+      for (int32_t pbase = 0; pbase < pn; pbase += 64) {
+        const int32_t i = pbase + lane;
         int32_t A = INT32_MAX, B = -2;
         if (i < pn) {
           const int32_t v = cv.p_m2[pb + i];
@@ -607,31 +701,57 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(const int32_t* __restr
       }
       if (open) close(aopen, carry);
     }
-    if (cnt) atomicAdd(&score[(int64_t)col * kWideCh + lane], cnt);
+    const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
+    const uint32_t v = (uint32_t)cnt | (hi16 << 16);
+    if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
   }
 }
 
-// Per chunk: each query's max over clips of (count << 32 | tie key); the score rows back to zero.
-__global__ __launch_bounds__(256) void wide_final_kernel(int32_t q0, int32_t nq, int32_t C,
-                                                         const int32_t* __restrict__ tiekey, int32_t* __restrict__ score,
+// Per chunk of the slab (blockIdx.y): each query's max over clips of (count << 32 | tie key),
+// and the score rows back to zero. A wave reads two clips' rows per step (32 words each).
+__global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq, int32_t C,
+                                                         const int32_t* __restrict__ tiekey, uint32_t* __restrict__ score,
                                                          unsigned long long* __restrict__ best) {
   __shared__ unsigned long long red[4][kWideCh];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long run = 0;
-  for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < C; c += ((int64_t)gridDim.x * blockDim.x) >> 6) {
-    const int32_t v = score[c * kWideCh + lane];
-    if (v) {
-      const unsigned long long k = ((unsigned long long)(uint32_t)v << 32) | (uint32_t)tiekey[c];
-      run = k > run ? k : run;
-      score[c * kWideCh + lane] = 0;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, wl = lane & 31;
+  uint32_t* rows = score + (int64_t)blockIdx.y * C * (kWideCh / 2);
+  unsigned long long rlo = 0, rhi = 0;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t c0 = 2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); c0 < C; c0 += 8 * nw) {
+    uint32_t w[4];
+    int64_t cc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      cc[u] = c0 + 2 * nw * u + half;
+      w[u] = cc[u] < C ? rows[cc[u] * (kWideCh / 2) + wl] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      if (w[u]) {
+        const unsigned long long tk = (uint32_t)tiekey[cc[u]];
+        const unsigned long long klo = ((unsigned long long)(w[u] & 0xffffu) << 32) | tk;
+        const unsigned long long khi = ((unsigned long long)(w[u] >> 16) << 32) | tk;
+        if (w[u] & 0xffffu) rlo = klo > rlo ? klo : rlo;
+        if (w[u] >> 16) rhi = khi > rhi ? khi : rhi;
+        rows[cc[u] * (kWideCh / 2) + wl] = 0u;
+      }
     }
   }
-  red[wave][lane] = run;
+  {
+    const unsigned long long olo = __shfl_xor(rlo, 32, 64), ohi = __shfl_xor(rhi, 32, 64);
+    rlo = olo > rlo ? olo : rlo;
+    rhi = ohi > rhi ? ohi : rhi;
+  }
+  if (half == 0) {
+    red[wave][2 * wl] = rlo;
+    red[wave][2 * wl + 1] = rhi;
+  }
   __syncthreads();
   if (wave == 0) {
     unsigned long long m = red[0][lane];
-    for (int w = 1; w < 4; w++) m = red[w][lane] > m ? red[w][lane] : m;
-    if (m && q0 + lane < nq) atomicMax(&best[q0 + lane], m);
+    for (int w2 = 1; w2 < 4; w2++) m = red[w2][lane] > m ? red[w2][lane] : m;
+    const int32_t q = (ch0 + (int32_t)blockIdx.y) * kWideCh + lane;
+    if (m && q < nq) atomicMax(&best[q], m);
   }
 }
 
@@ -639,15 +759,18 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t q0, int32_t nq,
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)score, (void*)info, tmp})
+                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, tmp})
     if (p) (void)hipFree(p);
   ka = kb = nullptr;
   ua = ub = nullptr;
-  va = vb = L2s = U2s = P = seg = wpre = score = info = nullptr;
+  va = vb = L2s = U2s = P = seg = wpre = cbeg = info = nullptr;
+  chw = nullptr;
+  score = nullptr;
   qis = nullptr;
   tmp = nullptr;
   tmp_bytes = 0;
-  cap_nf = cap_nch = cap_c = 0;
+  cap_nf = cap_nch = cap_score = 0;
+  slab = 0;
 }
 
 hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s) {
@@ -676,29 +799,37 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    if (seg) (void)hipFree(seg);
-    if (wpre) (void)hipFree(wpre);
-    seg = wpre = nullptr;
+    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw})
+      if (p) (void)hipFree(p);
+    seg = wpre = cbeg = nullptr;
+    chw = nullptr;
     cap_nch = 0;
-    if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1)))) return e;
+    if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
+        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)))
+      return e;
     cap_nch = nch;
   }
-  if (C > cap_c) {
+  // score rows for a slab of chunks at once: [slab][C][kChunk / 2] 16-bit pairs, at most ~1 GiB
+  const int64_t row = (int64_t)(C > 0 ? C : 1) * (kWideCh / 2) * (int64_t)sizeof(uint32_t);
+  slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
+  const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * (kWideCh / 2);
+  if (ns > cap_score) {
     if (score) (void)hipFree(score);
     score = nullptr;
-    cap_c = 0;
-    if ((e = dmalloc(&score, (int64_t)C * kWideCh))) return e;
-    if ((e = hipMemsetAsync(score, 0, sizeof(int32_t) * (size_t)C * kWideCh, s))) return e;  // kept zero by wide_final
-    cap_c = C;
+    cap_score = 0;
+    if ((e = dmalloc(&score, ns))) return e;
+    if ((e = hipMemsetAsync(score, 0, sizeof(uint32_t) * (size_t)ns, s))) return e;  // kept zero by wide_final
+    cap_score = ns;
   }
   if (!info && (e = dmalloc(&info, 2))) return e;
   return hipSuccess;
 }
 
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    WideScratch* ws, bool* eligible, hipStream_t s) {
+                                    int64_t max_qframes, WideScratch* ws, bool* eligible, hipStream_t s) {
   *eligible = false;
-  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 21)) return hipSuccess;
+  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 21) || max_qframes >= 65536)
+    return hipSuccess;
   hipError_t e;
   const int64_t nch = (nq + kWideCh - 1) / kWideCh;
   if ((e = hipMemsetAsync(ws->info, 0, 2 * sizeof(int32_t), s))) return e;
@@ -716,8 +847,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   if (n > 0)
     hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, d_qoff, nq, n, ws->kb, ws->va, ws->L2s,
                        ws->U2s, ws->qis, ws->seg);
-  const int64_t nsegs = nch * kWideSegs;
-  hipLaunchKernelGGL(wide_prefix_kernel, dim3(grid_for(nsegs * 64)), dim3(256), 0, s, nsegs, ws->seg, ws->qis, ws->P);
+  hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, n, nch, ws->cbeg);
+  hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->P);
   if ((e = hipGetLastError())) return e;
   *eligible = true;
   return hipSuccess;
@@ -735,11 +866,15 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   cv.g_beg = cells->g_beg;
   cv.valid = 1;
   hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
-  for (int64_t ch = 0; ch < nch; ch++) {
-    hipLaunchKernelGGL(wide_groups_kernel, dim3(4096), dim3(256), 0, s, ws->wpre + ch * (kKeyRange + 1),
-                       ws->seg + ch * kWideSegs * 2, cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, ws->score);
-    hipLaunchKernelGGL(wide_final_kernel, dim3(1024), dim3(256), 0, s, (int32_t)(ch * kWideCh), nq, C, d_tiekey, ws->score,
-                       d_best);
+  hipLaunchKernelGGL(wide_chw_kernel, dim3(1), dim3(1024), 0, s, ws->wpre, nch, ws->chw);
+  const int32_t slab = ws->slab > 0 ? ws->slab : 1;
+  const unsigned fx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (C + 2047) / 2048));
+  for (int64_t c0 = 0; c0 < nch; c0 += slab) {
+    const int32_t c1 = (int32_t)std::min<int64_t>(nch, c0 + slab);
+    hipLaunchKernelGGL(wide_groups_kernel, dim3(8192), dim3(256), 0, s, (int32_t)c0, c1, ws->chw, ws->wpre, ws->seg, ws->cbeg,
+                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score);
+    hipLaunchKernelGGL(wide_final_kernel, dim3(fx, (unsigned)(c1 - c0)), dim3(256), 0, s, (int32_t)c0, nq, C, d_tiekey,
+                       ws->score, d_best);
   }
   return hipGetLastError();
 }
