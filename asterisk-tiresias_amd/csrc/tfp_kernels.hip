@@ -653,6 +653,18 @@ __device__ __forceinline__ void dft4_rot_a2(cf a0, cf a1, cf A2, cf a3, cf& X0, 
   X1 = addsub(t1, swap(t3));
   X3 = subadd(t1, swap(t3));
 }
+// The two 45-degree twiddles in two ops instead of three. W16^2 = (c, -c) and W16^6 = (d, d)
+// (DspTables_fixed8k checks the table halves are equal in magnitude). With p = a c = (a.x c, a.y c):
+// the spec's (a.x c - a.y (-c), a.x (-c) + a.y c) is (p.x + p.y, p.y - p.x) bitwise (b (-c) =
+// -(b c) exactly, x - (-y) == x + y), and (a.x d - a.y d, a.x d + a.y d) is (p.x - p.y, p.y + p.x).
+__device__ __forceinline__ cf cmul_w2(cf a, float c) {
+  const cf p = a * cf{c, c};
+  return addsub(p, swap(p));
+}
+__device__ __forceinline__ cf cmul_w6(cf a, float d) {
+  const cf p = a * cf{d, d};
+  return subadd(p, swap(p));
+}
 __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], cf (&out)[16]) {
   cf A[4][4];
 #pragma unroll
@@ -660,8 +672,12 @@ __device__ __forceinline__ void dft16q(const cf (&w16)[10], const cf (&in)[16], 
 #pragma unroll
   for (int n2 = 1; n2 < 4; n2++)
 #pragma unroll
-    for (int k1 = 1; k1 < 4; k1++)
-      if (n2 * k1 != 4) A[n2][k1] = cmul(A[n2][k1], w16[n2 * k1]);
+    for (int k1 = 1; k1 < 4; k1++) {
+      const int e = n2 * k1;
+      if (e == 2) A[n2][k1] = cmul_w2(A[n2][k1], w16[2].x);
+      else if (e == 6) A[n2][k1] = cmul_w6(A[n2][k1], w16[6].x);
+      else if (e != 4) A[n2][k1] = cmul(A[n2][k1], w16[e]);
+    }
 #pragma unroll
   for (int k1 = 0; k1 < 4; k1++) {
     if (k1 == 2) dft4_rot_a2(A[0][k1], A[1][k1], A[2][k1], A[3][k1], out[k1], out[k1 + 4], out[k1 + 8], out[k1 + 12]);
@@ -989,7 +1005,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         const float4 t4 = tw4[16 * k2];
         const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
         sqrt_pair_cr(sq, nk[k2], nk2[k2]);
-        umin = min(umin, min(__builtin_bit_cast(uint32_t, sq.x) - 1u, __builtin_bit_cast(uint32_t, sq.y) - 1u));
+        umin = min(umin, rare_key_pair(sq));
       }
       // |X| rows, addressed as bins L + 16 k2 and 256 - that for every lane (paired ds_write2_b32);
       // lane 0's k2 = 0 pair is bin 128 twice (the partner-side value stands, below): its writes to
@@ -1178,7 +1194,8 @@ __global__ void finish_db_kernel(int32_t* __restrict__ micro, double* __restrict
 bool DspTables_fixed8k(const DspTables& t) {
   return t.ms_len[0] == 36 && t.ms_len[1] == 16 && t.ms_len[2] == 8 && t.ms_total == 16 * (36 + 16 + 8) &&
          t.ms_total <= kMsLds && t.ms_c_defer == 1 && t.ms_maxbin <= 2 * kFrameStride8 - 48 &&
-         t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0 && t.fb_ok == 1 && t.fb_nfilters == kFbNf;
+         t.ms_filter[0][15] >= 0 && t.ms_filter[1][15] >= 0 && t.fb_ok == 1 && t.fb_nfilters == kFbNf &&
+         t.tw256_im[32] == -t.tw256_re[32] && t.tw256_im[96] == t.tw256_re[96];  // dft16q's cmul_w2 / cmul_w6
 }
 
 // Resident 256-thread blocks per CU of kernel k: the occupancy query, capped by what the

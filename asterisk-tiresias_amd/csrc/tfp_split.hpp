@@ -52,6 +52,15 @@ __device__ __forceinline__ void step_tuckerman(uint32_t m0, uint32_t m1, cf2 rp,
   n0 = __builtin_bit_cast(float, a0);
   n1 = __builtin_bit_cast(float, a1);
 }
+// The kernel's rare-bin key of a pair: min over both bins of bits(|S|^2) - 1 (exact zeros wrap to
+// the top), so a wave holds a bin with 0 < |S|^2 < thr iff its min key < bits(thr) - 1. The
+// elements go through scalars first: clang's __builtin_bit_cast of an ext_vector element
+// expression (`sq.y`) reads element 0, which left every bin 256 - k out of the test.
+__device__ __forceinline__ uint32_t rare_key_pair(cf2 sq) {
+  const float a = sq.x, b = sq.y;
+  return min(__builtin_bit_cast(uint32_t, a) - 1u, __builtin_bit_cast(uint32_t, b) - 1u);
+}
+
 // Correctly rounded sqrtf of x (= SSE sqrtss, glibc's sqrtf) for x = 0 and x in [2^-100, 2^100):
 // v_sqrt_f32 (within 1 ulp) moved to the neighbour whose Tuckerman interval holds x:
 //   +1 ulp when x - yp y > 0, -1 ulp when x - ym y <= 0 (ym, yp: y's neighbours),

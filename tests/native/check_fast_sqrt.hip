@@ -1,9 +1,11 @@
 // check_fast_sqrt.hip — exhaustive gfx950 check of the 8 kHz kernel's sqrt sequence
 // (asterisk-tiresias_amd/csrc/tfp_split.hpp: sqrt_pair_cr) over every non-negative finite float:
 //   * x = 0 and x in [2^-100, 2^100): the result equals the correctly rounded sqrtf, bitwise;
-//   * 0 < x < 2^-98 (denormals included): the kernel's rare-bin flag, bits(x) - 1 < bits(2^-98) - 1,
-//     is raised, so those bins take the spec-order slow path (and it is not raised for x = 0 or
-//     the fast range). Also counted: x whose v_sqrt_f32 is 0 (denormal inputs, flushed).
+//   * 0 < x < 2^-98 (denormals included): the kernel's rare-bin flag (tfp_split.hpp:
+//     rare_key_pair(pair) < bits(2^-98) - 1) is raised, so those bins take the spec-order slow
+//     path, and it is not raised for x = 0 or the fast range; the pair key is checked with the
+//     candidate in either element (bin k or bin 256 - k). Also counted: x whose v_sqrt_f32 is 0
+//     (denormal inputs, flushed).
 // The device's IEEE __builtin_sqrtf is the reference; it is pinned to the host's sqrtf (SSE
 // sqrtss, glibc) on a strided sample copied back. Prints the counts; exit status 0 iff all are 0.
 #include <hip/hip_runtime.h>
@@ -45,12 +47,15 @@ __global__ void check_kernel(Counts* c, uint32_t rare_m1, float* sample) {
       const bool fast = xi == 0.f || (xi >= 0x1p-100f && xi < 0x1p100f);
       if (fast && __builtin_bit_cast(uint32_t, r[i]) != __builtin_bit_cast(uint32_t, ref)) bad++;
       if (xi == 0.f && __builtin_bit_cast(uint32_t, r[i]) != 0u) zbad++;
-      const bool flag = bx[i] - 1u < rare_m1;  // fingerprint8k_kernel's umin test
-      if (xi > 0.f && xi < 0x1p-98f && !flag) missed++;
-      if (!(xi > 0.f && xi < 0x1p-98f) && flag) spur++;
       if (xi > 0.f && __builtin_amdgcn_sqrtf(xi) == 0.f) flushed++;
       n++;
     }
+    // fingerprint8k_kernel's rare test on the pair, with x.x (the low half's candidate; x.y is
+    // never in (0, 2^-98)) as bin k and as bin 256 - k
+    const bool want = (x.x > 0.f && x.x < 0x1p-98f) || (x.y > 0.f && x.y < 0x1p-98f);
+    const bool f01 = tfp::rare_key_pair(x) < rare_m1, f10 = tfp::rare_key_pair(tfp::cf2{x.y, x.x}) < rare_m1;
+    missed += (want && !f01) + (want && !f10);
+    spur += (!want && f01) + (!want && f10);
   }
   if (bad) atomicAdd(&c->fast_mismatch, bad);
   if (missed) atomicAdd(&c->rare_missed, missed);
