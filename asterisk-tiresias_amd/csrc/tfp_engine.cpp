@@ -699,7 +699,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
     HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, d_meta, s));
     HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
-                             e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(), s));
+                             e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(),
+                             e->Bt.as<_Float16>(), Cp, s));
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),

@@ -1517,7 +1517,7 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
                                                       const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
                                                       const int64_t* __restrict__ rng_all, int64_t* __restrict__ rng,
                                                       VoteMeta* __restrict__ meta, int32_t class_ku_max,
-                                                      _Float16* __restrict__ A) {
+                                                      _Float16* __restrict__ A, _Float16* __restrict__ Bt, int32_t Cp) {
   __shared__ int32_t hist[4][kVoteKpMax];
   __shared__ uint32_t mw[kKeyRange / 32];
   __shared__ int32_t pre[kKeyRange / 32 + 1];  // used keys below mask word w; pre[32] = Ku
@@ -1540,11 +1540,21 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
   }
   __syncthreads();
   const int32_t Ku = pre[kKeyRange / 32], Kp = ((Ku + 1 + 15) / 16) * 16;
+  const int32_t cls = Ku <= class_ku_max && Ku <= kClassKuMax ? 1 : 0;
+  // the region of Bt build_B marks, cleared over the whole grid (each block knows the path: a
+  // separate clearing launch cost ~5 us per batch)
+  {
+    const int64_t n16 = cls ? (1 << kClassKuMax) / 4 + (int64_t)Cp  // 16-byte units
+                            : (int64_t)Cp * Kp / 8;                  // (Kp is a multiple of 16)
+    uint4* p = reinterpret_cast<uint4*>(Bt);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+      p[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
   if (blockIdx.x == 0) {  // the vote's metadata and the used keys' box row ranges (build_B)
     if (threadIdx.x == 0) {
       meta->ku = Ku;
       meta->kp = Kp;
-      meta->cls = Ku <= class_ku_max && Ku <= kClassKuMax ? 1 : 0;
+      meta->cls = cls;
       if (*maxc > 2048) meta->ok = 0;  // a key outside the vote range (key_mask)
     }
     for (int t = threadIdx.x; t < kKeyRange; t += blockDim.x) {
@@ -1587,14 +1597,15 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
 
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
                           const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int64_t* d_rng,
-                          VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A, hipStream_t s) {
+                          VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A, _Float16* d_Bt, int32_t Cp,
+                          hipStream_t s) {
   hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, d_q, sc, d_qoff, nq, Qp, d_mask,
-                     d_maxc, d_rng_all, d_rng, d_meta, class_ku_max, d_A);
+                     d_maxc, d_rng_all, d_rng, d_meta, class_ku_max, d_A, d_Bt, Cp);
   return hipGetLastError();
 }
 
 // Bt[clip][key] = kVoteScale for every row in the key's box, Bt[clip][Ku] = clip mod 1024 (the
-// clip's position in its vote_gemm chunk), 0 elsewhere: zero_bt clears the [Cp][Kp] region the
+// clip's position in its vote_gemm chunk), 0 elsewhere: build_A clears the [Cp][Kp] region the
 // GEMM reads, then build_B marks.
 //
 // Few used keys (meta->cls: Ku <= kClassKuMax) take the pattern-class path instead, in the same
@@ -1604,14 +1615,6 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
 // most 2^Ku - 1 classes per query instead of over every clip. Layout: cls[2^kClassKuMax] int32
 // (greatest column + 1 per pattern, 0 = none), then flags[Cp][16] bytes (flag k: the clip has a
 // row in the k-th used key's box; plain byte stores, since a box can hold ~10^5 rows).
-__global__ void zero_bt_kernel(_Float16* __restrict__ Bt, int32_t Cp, const VoteMeta* __restrict__ meta) {
-  const int64_t n16 = meta->cls ? (1 << kClassKuMax) / 4 + (int64_t)Cp  // 16-byte units
-                                : (int64_t)Cp * meta->kp / 8;            // (Kp is a multiple of 16)
-  uint4* p = reinterpret_cast<uint4*>(Bt);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = make_uint4(0u, 0u, 0u, 0u);
-}
-
 // The rows of all keys are spread over the whole grid (a box can hold a large share of the index
 // when fingerprints concentrate).
 __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
@@ -1637,16 +1640,16 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
 
 // Pattern-class path: every clip's pattern from its flags, the greatest column per pattern
 // reduced in LDS per block first (many clips share a pattern; same-address global atomics
-// serialise), then merged with one global atomicMax per pattern present in the block.
-__global__ __launch_bounds__(256) void class_max_kernel(int32_t Cp, const VoteMeta* __restrict__ meta,
-                                                        _Float16* __restrict__ Bt) {
-  if (!meta->cls) return;
-  __shared__ int32_t best[1 << kClassKuMax];
+// serialise, so only the first kClassMaxBlocks blocks take part), then merged with one global
+// atomicMax per pattern present in the block. Run by vote_gemm_regs_kernel's blocks when
+// meta->cls (its GEMM is not needed then): a launch of its own cost ~4.5 us per batch.
+constexpr int kClassMaxBlocks = 64;
+__device__ void class_max_block(int blk, int nblk, int32_t Cp, _Float16* __restrict__ Bt, int32_t* best) {
   for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x) best[i] = 0;
   __syncthreads();
   int32_t* cls = reinterpret_cast<int32_t*>(Bt);
   const uint4* flags = reinterpret_cast<const uint4*>(cls + (1 << kClassKuMax));
-  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < Cp; c += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t c = (int64_t)blk * blockDim.x + threadIdx.x; c < Cp; c += (int64_t)nblk * blockDim.x) {
     const uint4 f = flags[c];
     const uint32_t w[4] = {f.x, f.y, f.z, f.w};
     uint32_t pat = 0;
@@ -1661,10 +1664,7 @@ __global__ __launch_bounds__(256) void class_max_kernel(int32_t Cp, const VoteMe
 
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt,
                           hipStream_t s) {
-  hipLaunchKernelGGL(zero_bt_kernel, dim3(2048), dim3(256), 0, s, d_Bt, Cp, d_meta);
   hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, d_meta, Cp, d_Bt);
-  hipLaunchKernelGGL(class_max_kernel, dim3((unsigned)std::min<int64_t>(64, (Cp + 255) / 256)), dim3(256), 0, s, Cp,
-                     d_meta, d_Bt);
   return hipGetLastError();
 }
 
@@ -1948,12 +1948,19 @@ __device__ __forceinline__ void vote_tile_stream(const _Float16* __restrict__ A,
 // in registers, more waves per SIMD) and Kp > 128 (fragments streamed) in the kernel without
 // LDS, 32 < Kp <= 128 in the LDS-staged one.
 __global__ __launch_bounds__(256) void vote_gemm_regs_kernel(const _Float16* __restrict__ A,
-                                                              const _Float16* __restrict__ Bt, int32_t Qp, int32_t Cp,
+                                                              _Float16* __restrict__ Bt, int32_t Qp, int32_t Cp,
                                                               const VoteMeta* __restrict__ meta,
                                                               const int32_t* __restrict__ tiekey,
                                                               unsigned long long* __restrict__ part) {
   const int32_t Kp = meta->kp;
-  if (!meta->ok || meta->cls || (Kp > 32 && Kp <= 128)) return;
+  if (meta->cls) {  // the pattern-class path's per-pattern maxima instead of a GEMM
+    __shared__ int32_t cbest[1 << kClassKuMax];
+    const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+    const int nblk = min((int)(gridDim.x * gridDim.y), min(kClassMaxBlocks, (Cp + 255) / 256));
+    if (blk < nblk) class_max_block(blk, nblk, Cp, Bt, cbest);
+    return;
+  }
+  if (!meta->ok || (Kp > 32 && Kp <= 128)) return;
   const int q0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * 64;
   if (q0 >= Qp) return;
   unsigned long long* __restrict__ best = part + (int64_t)blockIdx.x * Qp;
@@ -1996,7 +2003,7 @@ __global__ __launch_bounds__(256) void vote_gemm_lds_kernel(const _Float16* __re
 // the chunks (one thread per query left the loads latency-bound: 24 us for 98 chunks).
 int32_t vote_chunks(int32_t Cp) { return (Cp + kVoteChunk - 1) / kVoteChunk; }
 
-hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
+hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
                             hipStream_t s) {
   if (Qp <= 0 || Cp <= 0) return hipSuccess;

@@ -114,16 +114,17 @@ struct VoteMeta {
 constexpr int32_t kVoteKpMax = ((kKeyRange + 1 + 15) / 16) * 16;
 // A[q][kc] per-query counts of the used keys (ascending key = column kc), derived by every block
 // from the key mask; block 0 writes VoteMeta (ku, kp, cls; ok cleared for an out-of-range key)
-// and the used keys' box row ranges d_rng[kc] (from the cached d_rng_all) for build_B.
+// and the used keys' box row ranges d_rng[kc] (from the cached d_rng_all) for build_B; the grid
+// clears the part of d_Bt build_B marks.
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
                           const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
                           int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A,
-                          hipStream_t s);
+                          _Float16* d_Bt /*[Cp][kVoteKpMax]: cleared where build_B marks*/, int32_t Cp, hipStream_t s);
 hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
                           _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
 // Partial results: d_part holds vote_chunks(Cp) x Qp keys.
 int32_t vote_chunks(int32_t Cp);
-hipError_t launch_vote_gemm(const _Float16* d_A, const _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
+hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
                             hipStream_t s);
 

@@ -15,7 +15,7 @@ for r in rows:
         groups.append(cur)
     elif cur is not None:
         cur.append(r)
-names = ["key_mask", "vote_compact", "build_A", "zero_bt", "build_B", "class_max", "vote_gemm", "class_vote"]
+names = ["key_mask", "vote_compact", "build_A", "zero_bt", "build_B", "class_max", "vote_gemm", "class_vote"]  # zero_bt / class_max: traces before r02z (folded into build_A / vote_gemm_regs)
 for gi, g in enumerate(groups):
     seq = [r for r in g if any(k in r["Kernel_Name"] for k in names)]
     nsearch = sum("key_mask" in r["Kernel_Name"] for r in seq)
