@@ -144,10 +144,9 @@ struct tfp_engine {
   hipStream_t qoff_stream = nullptr;
   hipEvent_t qoff_ev = nullptr;
   bool qoff_pending = false;
-  DevBuf small_work, small_bk, key_rng;
-  uint8_t small_epoch = 0;  // last stamp written into small_bk (0 = cleared)
-  int32_t small_cp4 = 0;     // row stride of the stamps in small_bk
-  int32_t small_rows = 0;    // rows stamped since the last clear (the max used-key count)
+  DevBuf key_rng;
+  DevBuf key_bits;           // key-presence bitsets at tolerance rng_tol (launch_key_bits; small path)
+  bool key_bits_valid = false;
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
@@ -560,6 +559,16 @@ int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
   HIPCHK(e, launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, tole, e->rng_all.as<int64_t>(), s));
   e->rng_tol = tole;
   e->rng_valid = true;
+  e->key_bits_valid = false;
+  return TFP_OK;
+}
+
+// The small path's key-presence bitsets, from the cached row ranges (after ensure_ranges).
+int ensure_key_bits(tfp_engine* e, hipStream_t s) {
+  if (e->key_bits_valid) return TFP_OK;
+  HIPCHK(e, e->key_bits.reserve(sizeof(uint32_t) * (size_t)kKeyRange * key_bits_words(e->ncols)));
+  HIPCHK(e, launch_key_bits(e->rng_all.as<int64_t>(), e->cols.as<int32_t>(), e->ncols, e->key_bits.as<uint32_t>(), s));
+  e->key_bits_valid = true;
   return TFP_OK;
 }
 
@@ -597,7 +606,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   std::vector<int64_t> qo(h_qoff, h_qoff + nq + 1);
   for (auto& v : qo) v -= h_qoff[0];
   if (!d_keys_out && sc.coefs == 1 && nq >= 1 && nq <= kSmallQ && e->ncols > 0 && e->nrows > 0) {
-    // small batch (batch-1 latency): mark + vote + publish kernels, results into host-mapped memory
+    // small batch (batch-1 latency): one vote launch over the cached key bitsets, results into
+    // host-mapped memory
     bool fits = true;
     for (int32_t i = 0; i < nq; i++) fits &= qo[i + 1] - qo[i] <= 2048;  // counts bounded like the fp16 path
     if (fits) {
@@ -605,39 +615,21 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       memset(&sq, 0, sizeof sq);
       sq.nq = nq;
       for (int32_t i = 0; i <= nq; i++) sq.qoff[i] = qo[i];
-      const int32_t C = e->ncols, Cp4 = ((C + 3) / 4) * 4;
-      HIPCHK(e, e->small_work.reserve(sizeof(SmallWork)));
-      const size_t bk_bytes = (size_t)kKeyRange * Cp4;
-      if (bk_bytes > e->small_bk.bytes || Cp4 != e->small_cp4) {
-        HIPCHK(e, e->small_bk.reserve(bk_bytes));
-        e->small_cp4 = Cp4;
-        e->small_rows = kKeyRange;  // new buffer or row stride: clear it all below
-        e->small_epoch = 255;
-      }
-      if (e->small_epoch == 255) {  // stamps wrap: clear, once every 255 calls, the rows stamped since
-        HIPCHK(e, hipMemsetAsync(e->small_bk.p, 0, (size_t)e->small_rows * Cp4, s));
-        e->small_epoch = 0;
-        e->small_rows = 0;
-      }
-      const uint8_t epoch = ++e->small_epoch;
-      SmallWork* w = e->small_work.as<SmallWork>();
+      const int32_t C = e->ncols;
       HIPCHK(e, e->small_res.reserve(small_result_bytes(C), hipHostMallocMapped | hipHostMallocCoherent));
       if (e->small_res.p != e->small_res_host) {
         HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&e->small_res_dev), e->small_res.p, 0));
         e->small_res_host = e->small_res.p;
       }
-      if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
-      HIPCHK(e, launch_search_small(d_q, sq, sc, w, e->small_bk.as<uint8_t>(), Cp4, epoch, e->rng_all.as<int64_t>(),
-                                    e->cols.as<int32_t>(), C, e->tiekey.as<int32_t>(), e->small_res_dev, s));
-      const hipError_t sync_rc = hipStreamSynchronize(s);
-      if (sync_rc != hipSuccess) e->small_rows = kKeyRange;  // unknown stamps: clear everything at the next wrap
-      HIPCHK(e, sync_rc);
+      if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_key_bits(e, s))) return rc;
+      HIPCHK(e, launch_search_small(d_q, sq, sc, e->key_bits.as<uint32_t>(), C, e->tiekey.as<int32_t>(), e->small_res_dev,
+                                    s));
+      HIPCHK(e, hipStreamSynchronize(s));
       // the vote ran after the fingerprint kernel, which read the staged upload: it is free again
       e->stage_pending = false;
       // the vote's blocks wrote their per-query maxima into host memory: the max over the blocks
       SmallResult* h = e->small_res.as<SmallResult>();
       if (!h->bad) {
-        e->small_rows = std::max<int32_t>(e->small_rows, (int32_t)h->ku);
         if (h->ku > 0) {
           const unsigned long long* part = small_result_parts(h);
           const int32_t nb = small_vote_blocks(C);

@@ -2067,110 +2067,110 @@ __device__ __forceinline__ int small_kc(const SmallKeySet& K, int key) {
   return K.pre[w] + __popc(K.mask[w] & ((1u << (key & 31)) - 1u));
 }
 
-// Stamp the clips with a row in each used key's box: bk[kc][clip] = epoch (a per-call byte, so
-// rows of earlier calls never need clearing). Every key's rows are spread over the whole grid.
-// Block 0 also resets the vote's workspace (small_vote runs after this launch on the stream).
-__global__ __launch_bounds__(256) void small_mark_kernel(const double* __restrict__ q, SmallQueries sq, SearchConsts sc,
-                                                         const int64_t* __restrict__ rng_all, uint8_t* __restrict__ bk,
-                                                         int32_t Cp, const int32_t* __restrict__ cols, uint8_t epoch,
-                                                         SmallWork* __restrict__ w) {
-  const int64_t nf = sq.qoff[sq.nq];
-  __shared__ SmallKeySet K;
-  small_keys(q, nf, sc, K);
-  if (blockIdx.x == 0) {  // the vote's bookkeeping: counts per (query, used key), ku, bad
-    const int ku = K.ku;
-    if (threadIdx.x == 0) {
-      w->ku = ku;
-      w->bad = K.bad;
-    }
-    if (!K.bad) {
-      for (int i = threadIdx.x; i < sq.nq * ku; i += blockDim.x) w->A[i / ku][i % ku] = 0;
-      __syncthreads();
-      // per 64 frames of a wave: one ballot per distinct (query, key) among them, one add per
-      // ballot (keys concentrate on a few values, where per-frame atomics would serialise)
-      for (int64_t base = threadIdx.x & ~63; base < nf; base += blockDim.x) {
-        const int64_t i = base + (threadIdx.x & 63);
-        int32_t k = 0;
-        int slot = -1;  // qi * kKeyRange + kc of this frame, -1 if ignored
-        if (i < nf && frame_key(q, i, sc, k)) {
-          int qi = 0;
-          while (qi + 1 < sq.nq && sq.qoff[qi + 1] <= i) qi++;
-          slot = qi * kKeyRange + small_kc(K, k + kKeyOffset);
-        }
-        unsigned long long todo = __ballot(slot >= 0);
-        while (todo) {
-          const int lead = __builtin_ctzll(todo);
-          const int ls = __shfl(slot, lead, 64);
-          const unsigned long long same = __ballot(slot == ls);
-          if ((threadIdx.x & 63) == lead) atomicAdd(&w->A[0][0] + ls, (int)__popcll(same));
-          todo &= ~same;
-        }
-      }
-    }
-  }
-  if (K.bad) return;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int kc = 0;
-  for (int wd = 0; wd < kKeyRange / 32; wd++) {
-    for (uint32_t m = K.mask[wd]; m; m &= m - 1u, kc++) {
-      const int key = 32 * wd + __builtin_ctz(m);
-      uint8_t* row = bk + (int64_t)kc * Cp;
-      const int64_t lo = rng_all[2 * key], hi = rng_all[2 * key + 1];
-      for (int64_t r = lo + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < hi; r += stride) row[cols[r]] = epoch;
-    }
+// Key-presence bitsets: one block row-range share per (key, slice); rows of a box spread over
+// kKeyBitsSlices blocks (a box can hold most of the index at wide tolerances).
+constexpr int kKeyBitsSlices = 16;
+__global__ __launch_bounds__(256) void key_bits_kernel(const int64_t* __restrict__ rng_all, const int32_t* __restrict__ cols,
+                                                       int32_t W, uint32_t* __restrict__ bits) {
+  const int key = blockIdx.x;
+  const int64_t lo = rng_all[2 * key], hi = rng_all[2 * key + 1];
+  uint32_t* row = bits + (int64_t)key * W;
+  const int64_t stride = (int64_t)kKeyBitsSlices * blockDim.x;
+  for (int64_t r = lo + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; r < hi; r += stride) {
+    const int32_t c = cols[r];
+    atomicOr(&row[c >> 5], 1u << (c & 31));
   }
 }
 
-// Clip-parallel scores of every query (4 clips per thread: one 32-bit stamp word per key row);
-// the per-query max of score << 32 | tie key (a later uuid wins a tie, as SQLite's
-// ORDER BY count(*) DESC returns it), reduced per block and written to the caller's host-mapped
-// result as this block's part; block 0 also writes (ku, bad). (Publishing the final max from the
-// device cost a one-wave kernel of ~4 us per call, or a done counter and fences in every block.)
-__global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, const SmallWork* __restrict__ w,
-                                                         const uint8_t* __restrict__ bk, int32_t Cp, int32_t C,
-                                                         const int32_t* __restrict__ tiekey, uint8_t epoch,
+hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, uint32_t* d_bits, hipStream_t s) {
+  const int32_t W = key_bits_words(C);
+  hipError_t e = hipMemsetAsync(d_bits, 0, sizeof(uint32_t) * (size_t)kKeyRange * W, s);
+  if (e) return e;
+  hipLaunchKernelGGL(key_bits_kernel, dim3(kKeyRange, kKeyBitsSlices), dim3(256), 0, s, d_rng_all, cols, W, d_bits);
+  return hipGetLastError();
+}
+
+// Every block: the batch's used keys and per-(query, used key) frame counts from the query frames
+// (per 64 frames of a wave: one ballot per distinct (query, key) among them and one LDS add per
+// ballot, since keys concentrate on a few values), then clip-parallel scores of every query (4
+// clips per thread: one bitset word per used key) and the per-query max of score << 32 | tie key
+// (a later uuid wins a tie, as SQLite's ORDER BY count(*) DESC returns it), reduced per block and
+// written to the caller's host-mapped result as this block's part; block 0 also writes (ku, bad).
+// (The clips used to be stamped per call by a separate marking launch over the used keys' boxes;
+// publishing the final max from the device cost a one-wave kernel of ~4 us per call, or a done
+// counter and fences in every block.)
+__global__ __launch_bounds__(256) void small_vote_kernel(const double* __restrict__ q, SmallQueries sq, SearchConsts sc,
+                                                         const uint32_t* __restrict__ bits, int32_t C,
+                                                         const int32_t* __restrict__ tiekey,
                                                          SmallResult* __restrict__ out) {
   static_assert(4 * 256 == kSmallVoteClips, "4 clips per thread");
+  __shared__ SmallKeySet K;
   __shared__ int32_t A[kSmallQ][kKeyRange];
+  __shared__ int16_t kkey[kKeyRange];  // kc -> key index (row of bits)
   __shared__ unsigned long long bmax[kSmallQ][4];
   const int nq = sq.nq;
-  const int ku = w->ku, bad = w->bad;
+  const int64_t nf = sq.qoff[nq];
+  small_keys(q, nf, sc, K);
+  const int ku = K.ku, bad = K.bad;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (!bad && ku > 0) {  // else every frame was ignored (NOTFOUND: best stays 0) or the caller redoes it
-    for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = w->A[i / ku][i % ku];
+    for (int i = threadIdx.x; i < nq * ku; i += blockDim.x) A[i / ku][i % ku] = 0;
+    if (threadIdx.x < kKeyRange / 32) {  // used keys in ascending order
+      int kc = K.pre[threadIdx.x];
+      for (uint32_t m = K.mask[threadIdx.x]; m; m &= m - 1u) kkey[kc++] = (int16_t)(32 * threadIdx.x + __builtin_ctz(m));
+    }
+    __syncthreads();
+    for (int64_t base = threadIdx.x & ~63; base < nf; base += blockDim.x) {
+      const int64_t i = base + lane;
+      int32_t k = 0;
+      int slot = -1;  // qi * kKeyRange + kc of this frame, -1 if ignored
+      if (i < nf && frame_key(q, i, sc, k)) {
+        int qi = 0;
+        while (qi + 1 < nq && sq.qoff[qi + 1] <= i) qi++;
+        slot = qi * kKeyRange + small_kc(K, k + kKeyOffset);
+      }
+      unsigned long long todo = __ballot(slot >= 0);
+      while (todo) {
+        const int lead = __builtin_ctzll(todo);
+        const int ls = __shfl(slot, lead, 64);
+        const unsigned long long same = __ballot(slot == ls);
+        if (lane == lead) atomicAdd(&A[0][0] + ls, (int)__popcll(same));
+        todo &= ~same;
+      }
+    }
     __syncthreads();
     const int c4 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);  // first of this thread's 4 clips
+    const int W = key_bits_words(C);
     int32_t sc4[kSmallQ][4];
 #pragma unroll
     for (int qi = 0; qi < kSmallQ; qi++)
 #pragma unroll
       for (int j = 0; j < 4; j++) sc4[qi][j] = 0;
     if (c4 < C) {
-      const uint32_t ep4 = 0x01010101u * epoch;
+      const uint32_t* col = bits + (c4 >> 5);
+      const int sh = c4 & 31;
       int kc = 0;
-      for (; kc + 4 <= ku; kc += 4) {  // 4 independent row loads in flight
+      for (; kc + 4 <= ku; kc += 4) {  // 4 independent bitset loads in flight
         uint32_t v[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint32_t*>(bk + (int64_t)(kc + u) * Cp + c4);
+        for (int u = 0; u < 4; u++) v[u] = col[(int64_t)kkey[kc + u] * W] >> sh;
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const uint32_t x = v[u] ^ ep4;  // byte j == 0 <=> clip c4 + j stamped this call
+        for (int u = 0; u < 4; u++)
 #pragma unroll
           for (int j = 0; j < 4; j++)
-            if (((x >> (8 * j)) & 0xffu) == 0u)
+            if ((v[u] >> j) & 1u)
 #pragma unroll
               for (int qi = 0; qi < kSmallQ; qi++) sc4[qi][j] += qi < nq ? A[qi][kc + u] : 0;
-        }
       }
       for (; kc < ku; kc++) {
-        const uint32_t x = *reinterpret_cast<const uint32_t*>(bk + (int64_t)kc * Cp + c4) ^ ep4;
+        const uint32_t x = col[(int64_t)kkey[kc] * W] >> sh;
 #pragma unroll
         for (int j = 0; j < 4; j++)
-          if (((x >> (8 * j)) & 0xffu) == 0u)
+          if ((x >> j) & 1u)
 #pragma unroll
             for (int qi = 0; qi < kSmallQ; qi++) sc4[qi][j] += qi < nq ? A[qi][kc] : 0;
       }
     }
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int qi = 0; qi < nq; qi++) {
       unsigned long long key = 0ull;
 #pragma unroll
@@ -2201,14 +2201,11 @@ __global__ __launch_bounds__(256) void small_vote_kernel(SmallQueries sq, const 
   }
 }
 
-hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
-                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
-                               hipStream_t s) {
-  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || Cp < C || epoch == 0 || !h_out) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(small_mark_kernel, dim3(256), dim3(256), 0, s, d_q, sq, sc, d_rng_all, d_bk, Cp, cols, epoch, d_work);
-  hipLaunchKernelGGL(small_vote_kernel, dim3(small_vote_blocks(C)), dim3(256), 0, s, sq, d_work, d_bk, Cp, C, d_tiekey,
-                     epoch, h_out);
+hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, const uint32_t* d_bits,
+                               int32_t C, const int32_t* d_tiekey, SmallResult* h_out, hipStream_t s) {
+  if (sq.nq <= 0 || sq.nq > kSmallQ || C <= 0 || !h_out) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(small_vote_kernel, dim3(small_vote_blocks(C)), dim3(256), 0, s, d_q, sq, sc, d_bits, C, d_tiekey,
+                     h_out);
   return hipGetLastError();
 }
 

@@ -129,22 +129,18 @@ hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int
                             hipStream_t s);
 
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
-// two launches, no host round trip and no copy back. Every block of small_mark derives the
-// batch's used keys from the query frames itself (a few KB of L2-resident reads) and stamps the
-// clips with a row in each used key's box (a byte per clip, key-major); its block 0 also writes
-// the per-query key counts. small_vote scores clip-parallel and arg-maxes per block; each block
-// writes its per-query maxima straight into the caller's host-mapped SmallResult, and the caller
-// takes the max over the blocks once the stream is done (no publishing kernel, no device atomics).
+// one launch after the queries' fingerprint launch, no host round trip and no copy back. Every
+// block of small_vote derives the batch's used keys and per-query key counts from the query
+// frames itself (a few KB of L2-resident reads) and scores its clips from the key-presence
+// bitsets (launch_key_bits: bit c of key k's row = clip column c has a row in k's box, cached per
+// index version and tolerance, as the boxes' row ranges are); it arg-maxes per block and writes
+// its per-query maxima straight into the caller's host-mapped SmallResult, and the caller takes
+// the max over the blocks once the stream is done (no publishing kernel, no device atomics).
 constexpr int kSmallQ = 8;
 struct SmallQueries {
   int32_t nq;
   int32_t pad;
   int64_t qoff[kSmallQ + 1];  // frame offsets of the queries in d_q (relative)
-};
-struct SmallWork {                       // device workspace of the small path (written by small_mark)
-  int32_t A[kSmallQ][kKeyRange];         // A[q][kc]: query q's frames whose key is the kc-th used key
-  int32_t ku;                            // used keys
-  int32_t bad;                           // a key outside [-512, 511]
 };
 // Host-mapped (pinned, coherent) result of one small call: the header, then small_vote's per-block
 // maxima part[block][query] (score << 32 | tie key, 0 = no hit) for the small_vote_blocks(C) blocks.
@@ -159,12 +155,14 @@ inline size_t small_result_bytes(int32_t C) {
   return sizeof(SmallResult) + sizeof(unsigned long long) * kSmallQ * (size_t)small_vote_blocks(C);
 }
 TFP_HD unsigned long long* small_result_parts(SmallResult* r) { return reinterpret_cast<unsigned long long*>(r + 1); }
-// d_bk: [kKeyRange][Cp] bytes stamped with `epoch` (1..255, a new one per call; the caller clears
-// d_bk when the epoch wraps). h_out: host-mapped memory of small_result_bytes(C) the device writes.
-hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, SmallWork* d_work,
-                               uint8_t* d_bk, int32_t Cp, uint8_t epoch, const int64_t* d_rng_all,
-                               const int32_t* cols, int32_t C, const int32_t* d_tiekey, SmallResult* h_out,
-                               hipStream_t s);
+// Key-presence bitsets: d_bits[k][w] (kKeyRange rows of W = key_bits_words(C) words), bit c of row
+// k set iff column c has an index row in key k's box (d_rng_all, the cached row ranges). Cleared
+// and rebuilt on the stream.
+TFP_HD int32_t key_bits_words(int32_t C) { return (C + 127) / 128 * 4; }  // rows 16-byte aligned
+hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, uint32_t* d_bits, hipStream_t s);
+// h_out: host-mapped memory of small_result_bytes(C) the device writes.
+hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, const uint32_t* d_bits,
+                               int32_t C, const int32_t* d_tiekey, SmallResult* h_out, hipStream_t s);
 
 // General path (coefs = 2 and the vote's fallbacks; tfp_scan.hip). Clip-set cache of one index
 // version and tolerance, built from the key boxes' row ranges (d_rng_all, h_off = host prefix of
