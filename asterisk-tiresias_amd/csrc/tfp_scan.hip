@@ -599,6 +599,24 @@ __device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) 
   return lo;
 }
 
+// Coarse sample of a segment's sorted bounds across the wave's lanes: lane j holds a[sb + j step]
+// (j < ns samples). Returns [lo, hi) of a that holds the first index whose value is >= v (ge) or
+// > v (!ge): every sample before it fails the test and the next one passes, so the search is
+// over at most step entries. Lanes search their own v among the samples through ds_bpermute, by
+// binary lifting in 7 uniform steps (every lane takes part in every exchange: call it converged).
+__device__ __forceinline__ void coarse_range(int32_t samp, int32_t ns, int32_t step, int32_t sb, int32_t se, int32_t v,
+                                             bool ge, int32_t& lo, int32_t& hi) {
+  int32_t a = 0;  // count of samples that fail (value < v, or <= v); the samples are sorted
+#pragma unroll
+  for (int bit = 64; bit >= 1; bit >>= 1) {
+    const int32_t cand = a + bit;
+    const int32_t x = __shfl(samp, min(cand, 64) - 1, 64);
+    if (cand <= ns && (ge ? x < v : x <= v)) a = cand;
+  }
+  lo = a ? sb + (a - 1) * step + 1 : sb;
+  hi = a < ns ? sb + a * step + 1 : se;
+}
+
 // The work items (chunk, key, clip group) of chunks [ch0, ch1), in chunk and key order; each wave
 // takes a contiguous share, so it locates its first item by binary search and then steps through
 // keys and chunks. Lane q = query 64 ch + q. A group's counts go to the slab's score rows as 16-bit
@@ -637,6 +655,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
   int32_t kend = wp[kk + 1];
   bool fresh = true;
   int32_t sb = 0, se = 0, base = 0, fcnt = 0, gk0 = 0;
+  int32_t step = 1, nsamp = 0, sU = 0, sL = 0;  // the segment's coarse sample (coarse_range)
   for (; t < tend; t++, tt++) {
     while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
       if (++kk == kKeyRange) {
@@ -658,6 +677,12 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
       fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
       gk0 = k_gbeg[kk] - wp[kk];
+      const int32_t S = se - sb;
+      step = S > 64 ? (S + 63) / 64 : 1;
+      nsamp = S > 0 ? (S + step - 1) / step : 0;
+      const int32_t js = sb + (lane < nsamp ? lane : 0) * step;
+      sU = S > 0 ? U2s[js] : 0;
+      sL = S > 0 ? L2s[js] : 0;
     }
     const int32_t g = gk0 + tt;
     const int32_t col = (int32_t)(cv.g_key[g] & kColMask);
@@ -673,10 +698,13 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       for (int32_t pbase = 0; pbase < pn; pbase += 64) {
         const int32_t i = pbase + lane;
         int32_t A = INT32_MAX, B = -2;
+        const int32_t v = i < pn ? cv.p_m2[pb + i] : 0;
+        int32_t loA, hiA, loB, hiB;
+        coarse_range(sU, nsamp, step, sb, se, v, true, loA, hiA);
+        coarse_range(sL, nsamp, step, sb, se, v, false, loB, hiB);
         if (i < pn) {
-          const int32_t v = cv.p_m2[pb + i];
-          A = sb + lb32(U2s + sb, se - sb, v);      // first frame with U2 >= v
-          B = sb + ub32(L2s + sb, se - sb, v) - 1;  // last frame with L2 <= v
+          A = loA + lb32(U2s + loA, hiA - loA, v);      // first frame with U2 >= v
+          B = loB + ub32(L2s + loB, hiB - loB, v) - 1;  // last frame with L2 <= v
         }
         const bool ok = A <= B;
         int32_t bm = ok ? B : -2;
