@@ -688,7 +688,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
     HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
     VoteMeta* d_meta = reinterpret_cast<VoteMeta*>(d_mask + kMetaWord);
-    if ((rc = ensure_ranges(e, sc.tole, s))) return rc;
+    if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_key_bits(e, s))) return rc;
     HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, d_meta, s));
     HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
                              e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(),
@@ -696,7 +696,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),
-                               e->vote_part.as<unsigned long long>(), d_best, s));
+                               e->vote_part.as<unsigned long long>(), d_best, d_mask, e->key_bits.as<uint32_t>(), C, s));
     // the results go out before the ok flag is known (one host wait); a redo overwrites them.
     // Host results: (VoteMeta, best[nq]) in one copy into pinned memory.
     const size_t back = sizeof(VoteMeta) + (d_keys_out ? 0 : sizeof(unsigned long long) * nq);

@@ -1544,8 +1544,8 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
   // the region of Bt build_B marks, cleared over the whole grid (each block knows the path: a
   // separate clearing launch cost ~5 us per batch)
   {
-    const int64_t n16 = cls ? (1 << kClassKuMax) / 4 + (int64_t)Cp  // 16-byte units
-                            : (int64_t)Cp * Kp / 8;                  // (Kp is a multiple of 16)
+    const int64_t n16 = cls ? (1 << kClassKuMax) / 4     // 16-byte units: the pattern maxima
+                            : (int64_t)Cp * Kp / 8;      // (Kp is a multiple of 16)
     uint4* p = reinterpret_cast<uint4*>(Bt);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
       p[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -1613,8 +1613,8 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
 // of the clip, so it depends only on that key set (the clip's pattern, Ku bits). Per pattern only
 // the greatest column matters (a tie goes to the greatest uuid), so the vote is an argmax over at
 // most 2^Ku - 1 classes per query instead of over every clip. Layout: cls[2^kClassKuMax] int32
-// (greatest column + 1 per pattern, 0 = none), then flags[Cp][16] bytes (flag k: the clip has a
-// row in the k-th used key's box; plain byte stores, since a box can hold ~10^5 rows).
+// (greatest column + 1 per pattern, 0 = none); a clip's pattern comes from the cached key-presence
+// bitsets (launch_key_bits), one bit per used key.
 // The rows of all keys are spread over the whole grid (a box can hold a large share of the index
 // when fingerprints concentrate).
 __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
@@ -1623,14 +1623,7 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
   const int32_t Ku = meta->ku, Kp = meta->kp;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (meta->cls) {
-    uint8_t* flags = reinterpret_cast<uint8_t*>(reinterpret_cast<int32_t*>(Bt) + (1 << kClassKuMax));
-    for (int k = 0; k < Ku; k++) {
-      const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
-      for (int64_t r = lo + t0; r < hi; r += stride) flags[(int64_t)cols[r] * 16 + k] = 1;
-    }
-    return;
-  }
+  if (meta->cls) return;  // the class path reads the cached key bitsets instead
   for (int64_t c = t0; c < Cp; c += stride) Bt[c * Kp + Ku] = (_Float16)(float)(c & (kVoteColsPerBlock - 1));
   for (int k = 0; k < Ku; k++) {
     const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
@@ -1644,17 +1637,21 @@ __global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict_
 // atomicMax per pattern present in the block. Run by vote_gemm_regs_kernel's blocks when
 // meta->cls (its GEMM is not needed then): a launch of its own cost ~4.5 us per batch.
 constexpr int kClassMaxBlocks = 64;
-__device__ void class_max_block(int blk, int nblk, int32_t Cp, _Float16* __restrict__ Bt, int32_t* best) {
+__device__ void class_max_block(int blk, int nblk, int32_t Ku, const uint32_t* __restrict__ mask,
+                                const uint32_t* __restrict__ bits, int32_t C, _Float16* __restrict__ Bt, int32_t* best,
+                                int32_t* kk) {
   for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x) best[i] = 0;
+  if (threadIdx.x == 0) {  // the used keys, ascending (= columns kc)
+    int n = 0;
+    for (int w = 0; w < kKeyRange / 32 && n < Ku; w++)
+      for (uint32_t m = mask[w]; m && n < Ku; m &= m - 1u) kk[n++] = 32 * w + __builtin_ctz(m);
+  }
   __syncthreads();
   int32_t* cls = reinterpret_cast<int32_t*>(Bt);
-  const uint4* flags = reinterpret_cast<const uint4*>(cls + (1 << kClassKuMax));
-  for (int64_t c = (int64_t)blk * blockDim.x + threadIdx.x; c < Cp; c += (int64_t)nblk * blockDim.x) {
-    const uint4 f = flags[c];
-    const uint32_t w[4] = {f.x, f.y, f.z, f.w};
+  const int32_t W = key_bits_words(C);
+  for (int64_t c = (int64_t)blk * blockDim.x + threadIdx.x; c < C; c += (int64_t)nblk * blockDim.x) {
     uint32_t pat = 0;
-#pragma unroll
-    for (int k = 0; k < kClassKuMax; k++) pat |= ((w[k >> 2] >> (8 * (k & 3))) & 1u) << k;
+    for (int k = 0; k < Ku; k++) pat |= ((bits[(int64_t)kk[k] * W + (c >> 5)] >> (c & 31)) & 1u) << k;
     if (pat) atomicMax(&best[pat], (int32_t)c + 1);
   }
   __syncthreads();
@@ -1951,13 +1948,16 @@ __global__ __launch_bounds__(256) void vote_gemm_regs_kernel(const _Float16* __r
                                                               _Float16* __restrict__ Bt, int32_t Qp, int32_t Cp,
                                                               const VoteMeta* __restrict__ meta,
                                                               const int32_t* __restrict__ tiekey,
-                                                              unsigned long long* __restrict__ part) {
+                                                              unsigned long long* __restrict__ part,
+                                                              const uint32_t* __restrict__ mask,
+                                                              const uint32_t* __restrict__ bits, int32_t C) {
   const int32_t Kp = meta->kp;
   if (meta->cls) {  // the pattern-class path's per-pattern maxima instead of a GEMM
     __shared__ int32_t cbest[1 << kClassKuMax];
+    __shared__ int32_t ckk[kClassKuMax];
     const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-    const int nblk = min((int)(gridDim.x * gridDim.y), min(kClassMaxBlocks, (Cp + 255) / 256));
-    if (blk < nblk) class_max_block(blk, nblk, Cp, Bt, cbest);
+    const int nblk = min((int)(gridDim.x * gridDim.y), min(kClassMaxBlocks, (C + 255) / 256));
+    if (blk < nblk) class_max_block(blk, nblk, meta->ku, mask, bits, C, Bt, cbest, ckk);
     return;
   }
   if (!meta->ok || (Kp > 32 && Kp <= 128)) return;
@@ -2005,12 +2005,13 @@ int32_t vote_chunks(int32_t Cp) { return (Cp + kVoteChunk - 1) / kVoteChunk; }
 
 hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
-                            hipStream_t s) {
+                            const uint32_t* d_mask, const uint32_t* d_bits, int32_t C, hipStream_t s) {
   if (Qp <= 0 || Cp <= 0) return hipSuccess;
   if (Qp % 128 || Cp % 32) return hipErrorInvalidValue;  // the tiles assume these paddings
   const int32_t nchunks = vote_chunks(Cp);
   dim3 grid(nchunks, (Qp / 64 + 3) / 4);
-  hipLaunchKernelGGL(vote_gemm_regs_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
+  hipLaunchKernelGGL(vote_gemm_regs_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part, d_mask,
+                     d_bits, C);
   hipLaunchKernelGGL(vote_gemm_lds_kernel, grid, dim3(256), 0, s, d_A, d_Bt, Qp, Cp, d_meta, d_tiekey, d_part);
   hipLaunchKernelGGL(class_vote_kernel, dim3((unsigned)(Qp / 4)), dim3(256), 0, s, d_A, Qp, d_meta, d_Bt, d_tiekey, d_part,
                      nchunks, d_best);

@@ -126,7 +126,8 @@ hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteM
 int32_t vote_chunks(int32_t Cp);
 hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
                             const int32_t* d_tiekey, unsigned long long* d_part, unsigned long long* d_best,
-                            hipStream_t s);
+                            const uint32_t* d_mask /*key mask words*/, const uint32_t* d_bits /*launch_key_bits*/,
+                            int32_t C, hipStream_t s);
 
 // ---- small-batch search (batch-1 latency path; coefs = 1, nq <= kSmallQ, <= 2048 frames per query):
 // one launch after the queries' fingerprint launch, no host round trip and no copy back. Every
