@@ -85,6 +85,54 @@ def test_fingerprint_synthetic_clips_bit_exact(engine, oracle, tfp_lib):
     assert len(fr) == 24 * 313
 
 
+def _sparse_cases(nclips=256, n=4096, seed=21):
+    """Spectra with exact zeros and tiny cancellation residues in both halves of the bins: sparse
+    +-1..3 impulses (near the window's tails too), impulse pairs half a window apart, integer
+    tones on exact bins, short periods dividing 512, and isolated full-scale spikes."""
+    rng = np.random.default_rng(seed)
+    clips = []
+    t = np.arange(n)
+    for c in range(nclips):
+        kind = c % 5
+        x = np.zeros(n, np.int32)
+        if kind == 0:
+            pos = rng.choice(n, size=int(rng.integers(1, 24)), replace=False)
+            x[pos] = rng.choice([-3, -2, -1, 1, 2, 3], size=len(pos))
+        elif kind == 1:
+            for _ in range(int(rng.integers(1, 8))):
+                p = int(rng.integers(0, n - 256))
+                v = int(rng.choice([-2, -1, 1, 2]))
+                x[p] = v
+                x[p + 256] = v if rng.random() < 0.5 else -v
+        elif kind == 2:
+            k = int(rng.integers(1, 256))
+            a = float(rng.choice([1.0, 2.0, 3.0, 30000.0]))
+            x = np.rint(a * np.cos(2 * np.pi * k * t / 512 + float(rng.random()) * 2 * np.pi)).astype(np.int32)
+        elif kind == 3:
+            per = int(rng.choice([2, 4, 8, 16, 32, 64, 128, 256, 512]))
+            base = rng.integers(-3, 4, per)
+            x = base[t % per].astype(np.int32)
+        else:
+            x[int(rng.integers(0, n))] = int(rng.choice([-32768, 32767]))
+        clips.append(np.clip(x, -32768, 32767).astype(np.int16))
+    return clips
+
+
+def test_fingerprint_sparse_and_cancelling_spectra_bit_exact(engine, oracle):
+    """The throughput launch and the small launch on spectra full of exact zeros and rounding
+    residues (the rare-bin test and both elements of every conjugate pair)."""
+    clips = _sparse_cases()
+    flat = np.concatenate(clips)
+    off = np.concatenate([[0], np.cumsum([len(c) for c in clips])]).astype(np.int64)
+    fr = engine.fingerprint_batch(flat, off)
+    micro, db = oracle.fingerprint_batch(flat, off, nthreads=8)
+    _assert_frames_equal(fr, micro, db)
+    for c in clips[:10]:
+        fr1 = engine.fingerprint(c)
+        _, db1, micro1 = oracle.fingerprint(c)
+        _assert_frames_equal(fr1, micro1, db1)
+
+
 def test_fingerprint_ragged_batch_equals_single(engine, tfp_lib):
     rng = np.random.default_rng(2)
     lens = [0, 17, 256, 511, 4096, 4097, 12345, 0, 80000]
