@@ -693,7 +693,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
                              e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(),
                              e->Bt.as<_Float16>(), Cp, s));
-    HIPCHK(e, launch_build_B(e->key_rng.as<int64_t>(), e->cols.as<int32_t>(), d_meta, Cp, e->Bt.as<_Float16>(), s));
+    HIPCHK(e, launch_build_B(d_mask, e->key_bits.as<uint32_t>(), C, d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),
                                e->vote_part.as<unsigned long long>(), d_best, d_mask, e->key_bits.as<uint32_t>(), C, s));

@@ -1544,8 +1544,8 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
   // the region of Bt build_B marks, cleared over the whole grid (each block knows the path: a
   // separate clearing launch cost ~5 us per batch)
   {
-    const int64_t n16 = cls ? (1 << kClassKuMax) / 4     // 16-byte units: the pattern maxima
-                            : (int64_t)Cp * Kp / 8;      // (Kp is a multiple of 16)
+    const int64_t n16 = cls ? (1 << kClassKuMax) / 4 : 0;  // 16-byte units: the pattern maxima
+                                                             // (build_B writes all of the GEMM's Bt)
     uint4* p = reinterpret_cast<uint4*>(Bt);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
       p[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -1604,9 +1604,9 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
   return hipGetLastError();
 }
 
-// Bt[clip][key] = kVoteScale for every row in the key's box, Bt[clip][Ku] = clip mod 1024 (the
-// clip's position in its vote_gemm chunk), 0 elsewhere: build_A clears the [Cp][Kp] region the
-// GEMM reads, then build_B marks.
+// Bt[clip][kc] = kVoteScale when the clip has a row in the kc-th used key's box, Bt[clip][Ku] =
+// clip mod 1024 (the clip's position in its vote_gemm chunk), 0 elsewhere: build_B writes the
+// [Cp][Kp] region the GEMM reads from the cached key bitsets.
 //
 // Few used keys (meta->cls: Ku <= kClassKuMax) take the pattern-class path instead, in the same
 // buffer: a clip's score for query q is the sum of q's counts over the keys whose boxes hold a row
@@ -1615,19 +1615,52 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
 // most 2^Ku - 1 classes per query instead of over every clip. Layout: cls[2^kClassKuMax] int32
 // (greatest column + 1 per pattern, 0 = none); a clip's pattern comes from the cached key-presence
 // bitsets (launch_key_bits), one bit per used key.
-// The rows of all keys are spread over the whole grid (a box can hold a large share of the index
-// when fingerprints concentrate).
-__global__ __launch_bounds__(256) void build_B_kernel(const int64_t* __restrict__ rng, const int32_t* __restrict__ cols,
-                                                      const VoteMeta* __restrict__ meta, int32_t Cp,
+// GEMM path: every row of Bt written whole from the cached key bitsets (one thread per clip,
+// 16-byte stores), so nothing needs clearing first and the work does not grow with the boxes'
+// rows. Against clearing plus marking the boxes' rows (scattered 2-byte stores): 42 -> 33 us at
+// 81 used keys and 280 -> 199 us at 601 (scripts/vote_bench.py under rocprofv3, C3 size).
+typedef _Float16 bt8 __attribute__((ext_vector_type(8)));
+__global__ __launch_bounds__(256) void build_B_kernel(const uint32_t* __restrict__ mask, const uint32_t* __restrict__ bits,
+                                                      int32_t C, const VoteMeta* __restrict__ meta, int32_t Cp,
                                                       _Float16* __restrict__ Bt) {
+  if (meta->cls) return;  // the class path reads the cached key bitsets itself
   const int32_t Ku = meta->ku, Kp = meta->kp;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t t0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (meta->cls) return;  // the class path reads the cached key bitsets instead
-  for (int64_t c = t0; c < Cp; c += stride) Bt[c * Kp + Ku] = (_Float16)(float)(c & (kVoteColsPerBlock - 1));
-  for (int k = 0; k < Ku; k++) {
-    const int64_t lo = rng[2 * k], hi = rng[2 * k + 1];
-    for (int64_t r = lo + t0; r < hi; r += stride) Bt[(int64_t)cols[r] * Kp + k] = (_Float16)kVoteScale;
+  __shared__ int16_t kk[kKeyRange];  // used keys, ascending (= columns kc)
+  __shared__ int32_t pre[kKeyRange / 32];
+  if (threadIdx.x < 64) {  // exclusive prefix of the mask words' popcounts
+    const int lane = threadIdx.x;
+    const int c = lane < kKeyRange / 32 ? __popc(mask[lane]) : 0;
+    int incl = c;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if (lane >= off) incl += v;
+    }
+    if (lane < kKeyRange / 32) pre[lane] = incl - c;
+  }
+  __syncthreads();
+  if (threadIdx.x < kKeyRange / 32) {
+    int kc = pre[threadIdx.x];
+    for (uint32_t m = mask[threadIdx.x]; m; m &= m - 1u) kk[kc++] = (int16_t)(32 * threadIdx.x + __builtin_ctz(m));
+  }
+  __syncthreads();
+  const int32_t W = key_bits_words(C);
+  for (int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; c < Cp; c += (int64_t)gridDim.x * blockDim.x) {
+    bt8* row = reinterpret_cast<bt8*>(Bt + c * Kp);
+    const uint32_t* col = bits + (c >> 5);
+    const int sh = (int)(c & 31);
+    for (int k0 = 0; k0 < Kp; k0 += 8) {
+      bt8 v;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int kc = k0 + j;
+        float x = 0.f;
+        if (kc < Ku) x = ((col[(int64_t)kk[kc] * W] >> sh) & 1u) ? kVoteScale : 0.f;
+        else if (kc == Ku) x = (float)(c & (kVoteColsPerBlock - 1));
+        v[j] = (_Float16)x;
+      }
+      row[k0 / 8] = v;
+    }
   }
 }
 
@@ -1659,9 +1692,9 @@ __device__ void class_max_block(int blk, int nblk, int32_t Ku, const uint32_t* _
     if (best[i]) atomicMax(&cls[i], best[i]);
 }
 
-hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt,
-                          hipStream_t s) {
-  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_rng, cols, d_meta, Cp, d_Bt);
+hipError_t launch_build_B(const uint32_t* d_mask, const uint32_t* d_bits, int32_t C, const VoteMeta* d_meta, int32_t Cp,
+                          _Float16* d_Bt, hipStream_t s) {
+  hipLaunchKernelGGL(build_B_kernel, dim3(1024), dim3(256), 0, s, d_mask, d_bits, C, d_meta, Cp, d_Bt);
   return hipGetLastError();
 }
 

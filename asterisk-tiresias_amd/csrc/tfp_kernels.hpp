@@ -120,8 +120,9 @@ hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_q
                           const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
                           int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A,
                           _Float16* d_Bt /*[Cp][kVoteKpMax]: cleared where build_B marks*/, int32_t Cp, hipStream_t s);
-hipError_t launch_build_B(const int64_t* d_rng, const int32_t* cols, const VoteMeta* d_meta, int32_t Cp,
-                          _Float16* d_Bt /*[Cp][kVoteKpMax]*/, hipStream_t s);
+hipError_t launch_build_B(const uint32_t* d_mask /*key mask words*/, const uint32_t* d_bits /*launch_key_bits*/,
+                          int32_t C, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt /*[Cp][kVoteKpMax]*/,
+                          hipStream_t s);
 // Partial results: d_part holds vote_chunks(Cp) x Qp keys.
 int32_t vote_chunks(int32_t Cp);
 hipError_t launch_vote_gemm(const _Float16* d_A, _Float16* d_Bt, int32_t Qp, int32_t Cp, const VoteMeta* d_meta,
