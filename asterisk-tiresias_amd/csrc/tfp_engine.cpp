@@ -144,7 +144,6 @@ struct tfp_engine {
   hipStream_t qoff_stream = nullptr;
   hipEvent_t qoff_ev = nullptr;
   bool qoff_pending = false;
-  DevBuf key_rng;
   DevBuf key_bits;           // key-presence bitsets at tolerance rng_tol (launch_key_bits; small path)
   bool key_bits_valid = false;
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
@@ -684,15 +683,13 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     // vote-matrix path, no host round trip: key mask -> used-key compaction -> A (per-query
     // counts) and Bt -> GEMM
     const int32_t Cp = ((C + 31) / 32) * 32;
-    HIPCHK(e, e->key_rng.reserve(sizeof(int64_t) * 2 * kKeyRange));
     HIPCHK(e, e->A.reserve(sizeof(_Float16) * (size_t)Qp * kVoteKpMax));
     HIPCHK(e, e->Bt.reserve(sizeof(_Float16) * (size_t)Cp * kVoteKpMax));
     VoteMeta* d_meta = reinterpret_cast<VoteMeta*>(d_mask + kMetaWord);
     if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_key_bits(e, s))) return rc;
     HIPCHK(e, launch_key_mask(d_q, sc, nf, d_mask, d_max, d_meta, s));
-    HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, e->rng_all.as<int64_t>(),
-                             e->key_rng.as<int64_t>(), d_meta, e->class_ku_max, e->A.as<_Float16>(),
-                             e->Bt.as<_Float16>(), Cp, s));
+    HIPCHK(e, launch_build_A(d_q, sc, e->qoff.as<int64_t>(), nq, Qp, d_mask, d_max, d_meta, e->class_ku_max,
+                             e->A.as<_Float16>(), e->Bt.as<_Float16>(), Cp, s));
     HIPCHK(e, launch_build_B(d_mask, e->key_bits.as<uint32_t>(), C, d_meta, Cp, e->Bt.as<_Float16>(), s));
     HIPCHK(e, e->vote_part.reserve(sizeof(unsigned long long) * (size_t)vote_chunks(Cp) * Qp));
     HIPCHK(e, launch_vote_gemm(e->A.as<_Float16>(), e->Bt.as<_Float16>(), Qp, Cp, d_meta, e->tiekey.as<int32_t>(),

@@ -1505,8 +1505,8 @@ hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int
 
 // Used-key compaction on the GPU (no host round trip), in every build_A block: the batch's key mask
 // -> column kc of each used key (ascending key order) by a prefix popcount of the 32 mask words;
-// block 0 writes meta = (Ku, Kp = padded Ku + 1, cls) and each used key's row range in the
-// m1-sorted index. (A separate one-block compaction launch cost ~5 us per batch.)
+// block 0 writes meta = (Ku, Kp = padded Ku + 1, cls). (A separate one-block compaction launch
+// cost ~5 us per batch.)
 //
 // One wave per query row of A: the query's frames counted per used key in LDS, then the row
 // written as fp16 (A[q][Ku] = 1 picks up Bt's column-position entry for vote_gemm's packed argmax;
@@ -1515,7 +1515,6 @@ hipError_t launch_key_ranges_all(const int32_t* m1s, int64_t R, double tole, int
 __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__ qv, SearchConsts sc,
                                                       const int64_t* __restrict__ qoff, int32_t nq, int32_t Qp,
                                                       const uint32_t* __restrict__ mask, const int32_t* __restrict__ maxc,
-                                                      const int64_t* __restrict__ rng_all, int64_t* __restrict__ rng,
                                                       VoteMeta* __restrict__ meta, int32_t class_ku_max,
                                                       _Float16* __restrict__ A, _Float16* __restrict__ Bt, int32_t Cp) {
   __shared__ int32_t hist[4][kVoteKpMax];
@@ -1550,21 +1549,11 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
       p[i] = make_uint4(0u, 0u, 0u, 0u);
   }
-  if (blockIdx.x == 0) {  // the vote's metadata and the used keys' box row ranges (build_B)
-    if (threadIdx.x == 0) {
-      meta->ku = Ku;
-      meta->kp = Kp;
-      meta->cls = cls;
-      if (*maxc > 2048) meta->ok = 0;  // a key outside the vote range (key_mask)
-    }
-    for (int t = threadIdx.x; t < kKeyRange; t += blockDim.x) {
-      const uint32_t m = mw[t >> 5];
-      if ((m >> (t & 31)) & 1u) {
-        const int kc = pre[t >> 5] + __popc(m & ((1u << (t & 31)) - 1u));
-        rng[2 * kc] = rng_all[2 * t];
-        rng[2 * kc + 1] = rng_all[2 * t + 1];
-      }
-    }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the vote's metadata
+    meta->ku = Ku;
+    meta->kp = Kp;
+    meta->cls = cls;
+    if (*maxc > 2048) meta->ok = 0;  // a key outside the vote range (key_mask)
   }
   const int q = blockIdx.x * 4 + wave;
   if (q >= Qp) return;
@@ -1596,11 +1585,11 @@ __global__ __launch_bounds__(256) void build_A_kernel(const double* __restrict__
 }
 
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
-                          const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all, int64_t* d_rng,
+                          const uint32_t* d_mask, const int32_t* d_maxc,
                           VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A, _Float16* d_Bt, int32_t Cp,
                           hipStream_t s) {
   hipLaunchKernelGGL(build_A_kernel, dim3((unsigned)((Qp + 3) / 4)), dim3(256), 0, s, d_q, sc, d_qoff, nq, Qp, d_mask,
-                     d_maxc, d_rng_all, d_rng, d_meta, class_ku_max, d_A, d_Bt, Cp);
+                     d_maxc, d_meta, class_ku_max, d_A, d_Bt, Cp);
   return hipGetLastError();
 }
 

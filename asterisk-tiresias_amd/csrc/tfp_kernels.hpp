@@ -113,13 +113,12 @@ struct VoteMeta {
 };
 constexpr int32_t kVoteKpMax = ((kKeyRange + 1 + 15) / 16) * 16;
 // A[q][kc] per-query counts of the used keys (ascending key = column kc), derived by every block
-// from the key mask; block 0 writes VoteMeta (ku, kp, cls; ok cleared for an out-of-range key)
-// and the used keys' box row ranges d_rng[kc] (from the cached d_rng_all) for build_B; the grid
-// clears the part of d_Bt build_B marks.
+// from the key mask; block 0 writes VoteMeta (ku, kp, cls; ok cleared for an out-of-range key);
+// on the class path the grid clears the pattern maxima at the head of d_Bt.
 hipError_t launch_build_A(const double* d_q, SearchConsts sc, const int64_t* d_qoff, int32_t nq, int32_t Qp,
-                          const uint32_t* d_mask, const int32_t* d_maxc, const int64_t* d_rng_all,
-                          int64_t* d_rng /*[kKeyRange][2]*/, VoteMeta* d_meta, int32_t class_ku_max, _Float16* d_A,
-                          _Float16* d_Bt /*[Cp][kVoteKpMax]: cleared where build_B marks*/, int32_t Cp, hipStream_t s);
+                          const uint32_t* d_mask, const int32_t* d_maxc, VoteMeta* d_meta, int32_t class_ku_max,
+                          _Float16* d_A, _Float16* d_Bt /*the class path's pattern maxima are cleared*/, int32_t Cp,
+                          hipStream_t s);
 hipError_t launch_build_B(const uint32_t* d_mask /*key mask words*/, const uint32_t* d_bits /*launch_key_bits*/,
                           int32_t C, const VoteMeta* d_meta, int32_t Cp, _Float16* d_Bt /*[Cp][kVoteKpMax]*/,
                           hipStream_t s);
