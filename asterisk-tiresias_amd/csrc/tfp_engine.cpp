@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/tiresias_fp.h"
+#include "tfp_index.hpp"
 #include "tfp_kernels.hpp"
 #include "tfp_math.hpp"
 #include "tfp_synth.hpp"
@@ -68,20 +69,25 @@ struct Clip {
   int64_t off = 0;  // first staging row (a clip's rows are contiguous, in frame order)
 };
 
-// tfp_host_alloc's buffers: host address -> (bytes, device address), so a call whose samples lie
-// inside one hands the GPU the samples in place.
+// tfp_host_alloc's buffers: host address -> (bytes, generation), so a call whose samples lie
+// inside one hands the GPU the samples in place. The device address is resolved per engine
+// (hipHostGetDevicePointer on the engine's own device, cached by base and generation), not taken
+// from whichever device was current at allocation.
 struct HostAllocs {
   std::mutex mu;
-  std::map<uintptr_t, std::pair<size_t, char*>> m;
-  // device address of [p, p + n) if it lies inside one buffer, else nullptr
-  const char* find(const void* p, size_t n) {
+  std::map<uintptr_t, std::pair<size_t, uint64_t>> m;
+  uint64_t next_gen = 1;
+  // the buffer holding [p, p + n): its base and generation, or false
+  bool find(const void* p, size_t n, uintptr_t* base, uint64_t* gen) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);
     std::lock_guard<std::mutex> lk(mu);
     auto it = m.upper_bound(a);
-    if (it == m.begin()) return nullptr;
+    if (it == m.begin()) return false;
     --it;
-    if (a + n > it->first + it->second.first) return nullptr;
-    return it->second.second + (a - it->first);
+    if (a + n > it->first + it->second.first) return false;
+    *base = it->first;
+    *gen = it->second.second;
+    return true;
   }
 };
 HostAllocs& host_allocs() {
@@ -119,6 +125,15 @@ struct tfp_engine {
 
   // sorted index
   DevBuf m1s, m2s, cols, rank_of_clip, tiekey;
+  // incremental maintenance (merge_index): the last build's clips and staged rows, the merge's
+  // output buffers (swapped with m1s/m2s/cols) and scratch
+  bool built = false;        // m1s/m2s/cols/col_clip describe clips [0, built_clips) as of the last build
+  bool force_full = false;   // TFP_INDEX_FULL: every update is a full build (A/B, tests)
+  size_t built_clips = 0;
+  int64_t built_staged = 0;
+  int64_t n_merges = 0, n_full_builds = 0;
+  DevBuf m1s_b, m2s_b, cols_b, remap;
+  MergeScratch merge;
   int64_t nrows = 0;       // rows that can match (live clip, non-NULL max1)
   int32_t ncols = 0;       // live clips
   std::vector<int32_t> col_clip;                 // column (uuid rank) -> clip id
@@ -139,6 +154,7 @@ struct tfp_engine {
   DevBuf zlayout;                   // device copy of the last zero-copy call's tile layout
   std::vector<char> zlayout_host;   // ... and its bytes (re-uploaded when they change)
   bool stage_pending = false;  // hstage / zstage may still be read by a copy or kernel on e->stream
+  std::unordered_map<uintptr_t, std::pair<uint64_t, char*>> host_dev;  // tfp_host_alloc base -> (generation, device address)
   HostBuf qoff_pin;                   // pinned source of the qoff copy
   std::vector<int64_t> qoff_host;     // what e->qoff holds (copied on stream qoff_stream)
   hipStream_t qoff_stream = nullptr;
@@ -168,6 +184,7 @@ struct tfp_engine {
   FpLaunchCfg fpcfg;
   int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
   bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
+  int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
   ~tfp_engine() {
@@ -256,6 +273,25 @@ int upload(tfp_engine* e, DevBuf& d, const void* h, size_t bytes, hipStream_t s 
   return TFP_OK;
 }
 
+// The engine's device address of [p, p + n) if it lies inside one tfp_host_alloc buffer, else
+// nullptr. Resolved on the engine's device (current here) once per buffer and cached.
+const char* engine_host_ptr(tfp_engine* e, const void* p, size_t n) {
+  uintptr_t base;
+  uint64_t gen;
+  if (!host_allocs().find(p, n, &base, &gen)) return nullptr;
+  auto& slot = e->host_dev[base];
+  if (slot.first != gen) {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(base), 0) != hipSuccess) {
+      (void)hipGetLastError();
+      e->host_dev.erase(base);
+      return nullptr;  // (the call copies the samples instead)
+    }
+    slot = {gen, static_cast<char*>(d)};
+  }
+  return slot.second + (reinterpret_cast<uintptr_t>(p) - base);
+}
+
 // Fingerprint host samples (int16 PCM, or with f32 the fp32 values aubio_source produced);
 // leaves micro/db on the device in e->micro / e->db.
 // exact_q: the frame values (e->db) equal glibc's 10*log10|c| bit for bit (LogFix lookups); a
@@ -312,7 +348,7 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
       h = e->hstage.as<char>();
     }
     // samples already in a tfp_host_alloc buffer: read in place (no copy into the staging)
-    const char* in_place = zero_copy && ns ? host_allocs().find(src + ss * offsets[0], ss * ns) : nullptr;
+    const char* in_place = zero_copy && ns ? engine_host_ptr(e, src + ss * offsets[0], ss * ns) : nullptr;
     if (ns && !in_place) memcpy(h, src + ss * offsets[0], ss * ns);
     memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
     memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
@@ -443,24 +479,29 @@ int compact_staging(tfp_engine* e) {
     if (c.alive) live += c.nrows;
   const int64_t dead = e->n_staged - live;
   if (dead <= std::max<int64_t>(1 << 16, live / 4)) return TFP_OK;
-  std::vector<int64_t> runs;
+  // The new layout is built aside and written into e->clips only once the copy has succeeded: a
+  // failure below (allocation, launch) leaves the staging rows and every clip's offset as they were.
+  std::vector<int64_t> runs, new_off(e->clips.size(), 0);
   int64_t dst = 0;
-  for (auto& c : e->clips) {
+  for (size_t i = 0; i < e->clips.size(); i++) {
+    const Clip& c = e->clips[i];
     if (!c.alive || !c.nrows) continue;
     const size_t nr = runs.size();
     if (nr && runs[nr - 3] + runs[nr - 1] == c.off && runs[nr - 2] + runs[nr - 1] == dst) runs[nr - 1] += c.nrows;
     else runs.insert(runs.end(), {c.off, dst, c.nrows});
-    c.off = dst;
+    new_off[i] = dst;
     dst += c.nrows;
   }
-  for (auto& c : e->clips)
-    if (!c.alive) c.nrows = 0, c.off = 0;
   DevBuf n1, n2, nc, d_runs;
   const int64_t cap = std::max<int64_t>(live, 1 << 16);
   HIPCHK(e, n1.reserve(sizeof(int32_t) * cap));
   HIPCHK(e, n2.reserve(sizeof(int32_t) * cap));
   HIPCHK(e, nc.reserve(sizeof(int32_t) * cap));
   const int32_t nruns = (int32_t)(runs.size() / 3);
+  if (e->fail_compact > 0) {  // TFP_TEST_FAIL_COMPACT: an allocation failure here, for the tests
+    e->fail_compact--;
+    return fail(e, TFP_E_NOMEM, "compact_staging: injected allocation failure");
+  }
   if (nruns) {
     int rc = upload(e, d_runs, runs.data(), sizeof(int64_t) * runs.size());
     if (rc) return rc;
@@ -473,28 +514,125 @@ int compact_staging(tfp_engine* e) {
   std::swap(e->st_m1.p, n1.p); std::swap(e->st_m1.bytes, n1.bytes);
   std::swap(e->st_m2.p, n2.p); std::swap(e->st_m2.bytes, n2.bytes);
   std::swap(e->st_clip.p, nc.p); std::swap(e->st_clip.bytes, nc.bytes);
+  for (size_t i = 0; i < e->clips.size(); i++) {
+    Clip& c = e->clips[i];
+    if (c.alive) c.off = new_off[i];
+    else c.nrows = 0, c.off = 0;
+  }
   e->n_staged = live;
   e->cap_staged = cap;
   return TFP_OK;
 }
 
+// Live clips in uuid order (the columns: the tie-break order of SQLite's result sort) and each
+// clip's rank (-1 when dead). Incremental: the previous build's order with the clips added since
+// merged in (no re-sort of every uuid).
+void live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* live, std::vector<int32_t>* rank) {
+  auto by_uuid = [&](int32_t a, int32_t b) { return e->clips[a].uuid < e->clips[b].uuid; };
+  live->clear();
+  if (incremental) {
+    std::vector<int32_t> old, add;
+    old.reserve(e->col_clip.size());
+    for (int32_t c : e->col_clip)
+      if (e->clips[c].alive) old.push_back(c);
+    for (int32_t i = (int32_t)e->built_clips; i < (int32_t)e->clips.size(); i++)
+      if (e->clips[i].alive) add.push_back(i);
+    std::sort(add.begin(), add.end(), by_uuid);
+    live->resize(old.size() + add.size());
+    std::merge(old.begin(), old.end(), add.begin(), add.end(), live->begin(), by_uuid);
+  } else {
+    for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
+      if (e->clips[i].alive) live->push_back(i);
+    std::sort(live->begin(), live->end(), by_uuid);
+  }
+  rank->assign(std::max<size_t>(e->clips.size(), 1), -1);
+  for (size_t r = 0; r < live->size(); r++) (*rank)[(*live)[r]] = (int32_t)r;
+}
+
+// Sorted (m1, m2, col) of staging rows [b, b + n) whose clip is live and max1 non-NULL: m1 in
+// keys_b, m2 in vals_a, col in keys_a (the first *valid entries). Synchronous.
+int sort_staged_rows(tfp_engine* e, int64_t b, int64_t n, int64_t* valid) {
+  HIPCHK(e, e->keys_a.reserve(sizeof(int32_t) * (n + 1)));
+  HIPCHK(e, e->keys_b.reserve(sizeof(int32_t) * (n + 1)));
+  HIPCHK(e, e->vals_a.reserve(sizeof(int32_t) * (n + 1)));
+  HIPCHK(e, e->vals_b.reserve(sizeof(int32_t) * (n + 1)));
+  HIPCHK(e, launch_index_keys(e->st_m1.as<int32_t>() + b, e->st_clip.as<int32_t>() + b, e->rank_of_clip.as<int32_t>(), n,
+                              e->keys_a.as<int32_t>(), e->vals_a.as<int32_t>(), e->stream));
+  size_t tb = 0;
+  HIPCHK(e, radix_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, e->stream));
+  HIPCHK(e, e->sort_tmp.reserve(tb));
+  HIPCHK(e, radix_sort_pairs(e->sort_tmp.p, &tb, e->keys_a.as<int32_t>(), e->keys_b.as<int32_t>(),
+                             e->vals_a.as<int32_t>(), e->vals_b.as<int32_t>(), n, e->stream));
+  HIPCHK(e, e->cnt.reserve(sizeof(int64_t)));
+  HIPCHK(e, launch_count_below(e->keys_b.as<int32_t>(), n, INT32_MAX, e->cnt.as<int64_t>(), e->stream));
+  HIPCHK(e, hipMemcpyAsync(valid, e->cnt.p, sizeof *valid, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  if (*valid)
+    HIPCHK(e, launch_index_gather(e->vals_b.as<int32_t>(), e->st_m2.as<int32_t>() + b, e->st_clip.as<int32_t>() + b,
+                                  e->rank_of_clip.as<int32_t>(), *valid, e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(),
+                                  e->stream));
+  return TFP_OK;
+}
+
+// Index update without a full re-sort (tfp_index.hip): the rows staged since the last build are
+// sorted alone and merged into (m1s, m2s, cols) in one pass that also drops removed clips' rows
+// and renumbers the columns around the inserted / removed uuids. Commits nothing on failure.
+int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
+  const int64_t b = e->built_staged, n = e->n_staged - e->built_staged;
+  // old column -> new column (-1: the clip was removed)
+  std::vector<int32_t> remap(std::max<size_t>(e->col_clip.size(), 1), -1);
+  bool removed = false;
+  for (size_t c = 0; c < e->col_clip.size(); c++) {
+    remap[c] = rank[e->col_clip[c]];
+    removed |= remap[c] < 0;
+  }
+  if (n == 0 && !removed) return TFP_OK;  // (e.g. new tie-break keys only: the rows are unchanged)
+  int rc = upload(e, e->remap, remap.data(), sizeof(int32_t) * remap.size());
+  if (rc) return rc;
+  int64_t valid = 0;
+  if (n > 0 && (rc = sort_staged_rows(e, b, n, &valid))) return rc;
+  const int64_t R = e->nrows;
+  HIPCHK(e, e->m1s_b.reserve(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->m2s_b.reserve(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->cols_b.reserve(sizeof(int32_t) * (R + valid + 1)));
+  int64_t kept = R;
+  HIPCHK(e, launch_merge_update(e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->remap.as<int32_t>(),
+                                removed, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
+                                &e->merge, e->m1s_b.as<int32_t>(), e->m2s_b.as<int32_t>(), e->cols_b.as<int32_t>(), &kept,
+                                e->stream));
+  HIPCHK(e, hipStreamSynchronize(e->stream));
+  std::swap(e->m1s.p, e->m1s_b.p); std::swap(e->m1s.bytes, e->m1s_b.bytes);
+  std::swap(e->m2s.p, e->m2s_b.p); std::swap(e->m2s.bytes, e->m2s_b.bytes);
+  std::swap(e->cols.p, e->cols_b.p); std::swap(e->cols.bytes, e->cols_b.bytes);
+  e->nrows = kept + valid;
+  return TFP_OK;
+}
+
+int full_index(tfp_engine* e);
+
 int rebuild(tfp_engine* e) {
   if (!e->dirty) return TFP_OK;
-  int rc = compact_staging(e);
-  if (rc) return rc;
-  // the sort and the index rows use 32-bit row numbers
-  if (e->n_staged >= INT32_MAX) return fail(e, TFP_E_CAPACITY, "%lld staged rows (limit 2^31 - 1)", (long long)e->n_staged);
-  // uuid order of live clips = columns (the tie-break order of SQLite's result sort)
-  std::vector<int32_t> live;
-  for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
-    if (e->clips[i].alive) live.push_back(i);
-  std::sort(live.begin(), live.end(), [&](int32_t a, int32_t b) { return e->clips[a].uuid < e->clips[b].uuid; });
-  std::vector<int32_t> rank(std::max<size_t>(e->clips.size(), 1), -1);
-  for (size_t r = 0; r < live.size(); r++) rank[live[r]] = (int32_t)r;
-  e->ncols = (int32_t)live.size();
-  e->col_clip = live;
-  e->tiekey_host.assign(std::max<size_t>(live.size(), 1), 0);
-  e->key_col.clear();
+  int rc;
+  // Incremental (merge) when there is an index to merge into, the new rows are few next to it, and
+  // the staging area needs no compaction (the staged rows since the last build are then exactly
+  // rows [built_staged, n_staged)); otherwise the full build.
+  int64_t live_rows = 0;
+  for (const auto& c : e->clips)
+    if (c.alive) live_rows += c.nrows;
+  const int64_t dead = e->n_staged - live_rows, fresh = e->n_staged - e->built_staged;
+  const bool incremental = e->built && !e->force_full && fresh <= std::max<int64_t>(e->nrows / 2, 0) &&
+                           dead <= std::max<int64_t>(1 << 16, live_rows / 4) && e->n_staged < INT32_MAX;
+  if (!incremental) {
+    e->built = false;  // a failure below leaves the next attempt a full build as well
+    if ((rc = compact_staging(e))) return rc;
+    // the sort and the index rows use 32-bit row numbers
+    if (e->n_staged >= INT32_MAX)
+      return fail(e, TFP_E_CAPACITY, "%lld staged rows (limit 2^31 - 1)", (long long)e->n_staged);
+  }
+  std::vector<int32_t> live, rank;
+  live_order(e, incremental, &live, &rank);
+  std::vector<int32_t> tiekey(std::max<size_t>(live.size(), 1), 0);
+  std::unordered_map<int32_t, int32_t> key_col;
   const bool ovr = !e->tiebreak_override.empty();
   for (size_t r = 0; r < live.size(); r++) {
     const int32_t clip = live[r];
@@ -504,50 +642,50 @@ int rebuild(tfp_engine* e) {
       return fail(e, TFP_E_ARG, "clip %s was added after tfp_index_set_tiebreak: set the tie-break keys again",
                   e->clips[clip].uuid.c_str());
     const int32_t k = ovr ? e->tiebreak_override[clip] : (int32_t)r;
-    if (!e->key_col.emplace(k, (int32_t)r).second)
-      return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
-    e->tiekey_host[r] = k;
+    if (!key_col.emplace(k, (int32_t)r).second) return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
+    tiekey[r] = k;
   }
   if ((rc = upload(e, e->rank_of_clip, rank.data(), sizeof(int32_t) * rank.size()))) return rc;
-  if ((rc = upload(e, e->tiekey, e->tiekey_host.data(), sizeof(int32_t) * e->tiekey_host.size()))) return rc;
+  if ((rc = upload(e, e->tiekey, tiekey.data(), sizeof(int32_t) * tiekey.size()))) return rc;
+  if (incremental) {
+    if ((rc = merge_index(e, rank))) return rc;
+    e->n_merges++;
+  } else {
+    e->nrows = 0;
+    if ((rc = full_index(e))) return rc;
+    e->n_full_builds++;
+  }
+  e->ncols = (int32_t)live.size();
+  e->col_clip = std::move(live);
+  e->tiekey_host = std::move(tiekey);
+  e->key_col = std::move(key_col);
+  e->built = true;
+  e->built_clips = e->clips.size();
+  e->built_staged = e->n_staged;
+  e->dirty = false;
+  e->rng_valid = false;  // the key-range and clip-set caches follow the index
+  e->cell_fresh = false;
+  return TFP_OK;
+}
+
+// The full build: every staged row of a live clip, radix-sorted by m1 (the sorted arrays become
+// the index buffers).
+int full_index(tfp_engine* e) {
   const int64_t n = e->n_staged;
-  e->nrows = 0;
+  int64_t valid = 0;
   if (n > 0) {
-    HIPCHK(e, e->keys_a.reserve(sizeof(int32_t) * n));
-    HIPCHK(e, e->keys_b.reserve(sizeof(int32_t) * n));
-    HIPCHK(e, e->vals_a.reserve(sizeof(int32_t) * n));
-    HIPCHK(e, e->vals_b.reserve(sizeof(int32_t) * n));
-    HIPCHK(e, launch_index_keys(e->st_m1.as<int32_t>(), e->st_clip.as<int32_t>(), e->rank_of_clip.as<int32_t>(), n,
-                                e->keys_a.as<int32_t>(), e->vals_a.as<int32_t>(), e->stream));
-    size_t tb = 0;
-    HIPCHK(e, radix_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, e->stream));
-    HIPCHK(e, e->sort_tmp.reserve(tb));
-    HIPCHK(e, radix_sort_pairs(e->sort_tmp.p, &tb, e->keys_a.as<int32_t>(), e->keys_b.as<int32_t>(),
-                               e->vals_a.as<int32_t>(), e->vals_b.as<int32_t>(), n, e->stream));
-    HIPCHK(e, e->cnt.reserve(sizeof(int64_t)));
-    HIPCHK(e, launch_count_below(e->keys_b.as<int32_t>(), n, INT32_MAX, e->cnt.as<int64_t>(), e->stream));
-    int64_t valid = 0;
-    HIPCHK(e, hipMemcpyAsync(&valid, e->cnt.p, sizeof valid, hipMemcpyDeviceToHost, e->stream));
+    int rc = sort_staged_rows(e, 0, n, &valid);
+    if (rc) return rc;
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, e->m1s.reserve(sizeof(int32_t) * (valid + 1)));
-    HIPCHK(e, e->m2s.reserve(sizeof(int32_t) * (valid + 1)));
-    HIPCHK(e, e->cols.reserve(sizeof(int32_t) * (valid + 1)));
-    if (valid) {
-      HIPCHK(e, hipMemcpyAsync(e->m1s.p, e->keys_b.p, sizeof(int32_t) * valid, hipMemcpyDeviceToDevice, e->stream));
-      HIPCHK(e, launch_index_gather(e->vals_b.as<int32_t>(), e->st_m2.as<int32_t>(), e->st_clip.as<int32_t>(),
-                                    e->rank_of_clip.as<int32_t>(), valid, e->m2s.as<int32_t>(), e->cols.as<int32_t>(),
-                                    e->stream));
-    }
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->nrows = valid;
+    std::swap(e->m1s.p, e->keys_b.p); std::swap(e->m1s.bytes, e->keys_b.bytes);
+    std::swap(e->m2s.p, e->vals_a.p); std::swap(e->m2s.bytes, e->vals_a.bytes);
+    std::swap(e->cols.p, e->keys_a.p); std::swap(e->cols.bytes, e->keys_a.bytes);
   } else {
     HIPCHK(e, e->m1s.reserve(4));
     HIPCHK(e, e->m2s.reserve(4));
     HIPCHK(e, e->cols.reserve(4));
   }
-  e->dirty = false;
-  e->rng_valid = false;  // the key-range and clip-set caches follow the index
-  e->cell_fresh = false;
+  e->nrows = valid;
   return TFP_OK;
 }
 
@@ -578,8 +716,16 @@ int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
   HIPCHK(e, hipMemcpyAsync(rng.data(), e->rng_all.p, sizeof(int64_t) * rng.size(), hipMemcpyDeviceToHost, s));
   HIPCHK(e, hipStreamSynchronize(s));
   for (int k = 0; k < kKeyRange; k++) off[k + 1] = off[k] + std::max<int64_t>(0, rng[2 * k + 1] - rng[2 * k]);
-  HIPCHK(e, e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), e->ncols,
-                           e->nrows, tole, s));
+  // The cache is optional: if building it fails (an allocation or a hipcub call), the batch takes
+  // the row scan, which needs none of it (tfp_scan.hip). The failed build has released its buffers.
+  const hipError_t st = e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(),
+                                       e->ncols, e->nrows, tole, s);
+  if (st != hipSuccess) {
+    (void)hipGetLastError();
+    if (e->dbg_vote) fprintf(stderr, "[tfp] clip-set cache not built (%s): row scan\n", hipGetErrorString(st));
+    e->cells.release();
+    HIPCHK(e, hipStreamSynchronize(s));
+  }
   e->cell_tol = tole;
   e->cell_fresh = true;
   return TFP_OK;
@@ -819,6 +965,8 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   }
   if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
   e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
+  if (const char* v = getenv("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
+  e->force_full = getenv("TFP_INDEX_FULL") != nullptr;
   if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
@@ -844,16 +992,12 @@ int tfp_host_alloc(size_t bytes, void** out) {
   if (!bytes || !out) return TFP_E_ARG;
   *out = nullptr;
   void* p = nullptr;
+  // portable: pinned for every device; each engine maps it on its own device (engine_host_ptr)
   if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) != hipSuccess)
     return TFP_E_NOMEM;
-  char* d = nullptr;
-  if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d), p, 0) != hipSuccess) {
-    (void)hipHostFree(p);
-    return TFP_E_NOMEM;
-  }
   HostAllocs& h = host_allocs();
   std::lock_guard<std::mutex> lk(h.mu);
-  h.m[reinterpret_cast<uintptr_t>(p)] = {bytes, d};
+  h.m[reinterpret_cast<uintptr_t>(p)] = {bytes, h.next_gen++};
   *out = p;
   return TFP_OK;
 }
@@ -1108,6 +1252,10 @@ int tfp_index_clear(tfp_engine* e) {
   e->by_uuid.clear();
   e->tiebreak_override.clear();
   e->n_staged = 0;
+  e->built = false;
+  e->built_clips = 0;
+  e->built_staged = 0;
+  e->col_clip.clear();
   e->dirty = true;
   return TFP_OK;
 }
@@ -1129,6 +1277,14 @@ int tfp_index_commit(tfp_engine* e) {
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
   return rebuild(e);
+}
+
+int tfp_index_build_stats(tfp_engine* e, int64_t* full_builds, int64_t* merges) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (full_builds) *full_builds = e->n_full_builds;
+  if (merges) *merges = e->n_merges;
+  return TFP_OK;
 }
 
 int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {

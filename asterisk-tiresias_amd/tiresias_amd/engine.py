@@ -190,6 +190,12 @@ class Engine:
     def index_commit(self):
         self._chk(lib().tfp_index_commit(self._h))
 
+    def index_build_stats(self):
+        """(full builds, incremental merges) of the sorted index so far."""
+        f, m = C.c_int64(), C.c_int64()
+        self._chk(lib().tfp_index_build_stats(self._h, C.byref(f), C.byref(m)))
+        return f.value, m.value
+
     def set_tiebreak(self, keys):
         keys = np.ascontiguousarray(keys, np.int32)
         self._chk(lib().tfp_index_set_tiebreak(self._h, keys.ctypes.data, len(keys)))

@@ -319,6 +319,31 @@ def enroll(eng, torch, dev, sh, ids_all, chunk=2048):
     torch.cuda.empty_cache()
 
 
+def c3_queries(eng, torch, dev, sh, nq, db_clips, qn=8000 * 5):
+    """configs[2]'s query batch on the device, int16 [nq, qn]: 75 % excerpts of DB clips at
+    256-aligned offsets, 25 % unrelated audio (the same on every rank; tests reuse it)."""
+    n_db = 8000 * 30
+    rng = np.random.default_rng(SEED_Q)
+    seeds, clips, offs = [], [], []
+    for i in range(nq):
+        if i % 4 != 3:
+            clips.append(int(rng.integers(db_clips)))
+            offs.append(256 * int(rng.integers(0, (n_db - qn) // HOP)))
+            seeds.append(SEED_DB)
+        else:
+            clips.append(i)
+            offs.append(0)
+            seeds.append(SEED_Q)
+    qpcm = torch.empty((nq, qn), dtype=torch.int16, device=dev)
+    for sd in (SEED_DB, SEED_Q):
+        idx = [i for i in range(nq) if seeds[i] == sd]
+        tmp = torch.empty((len(idx), qn), dtype=torch.int16, device=dev)
+        eng.synth_device(sd, [clips[i] for i in idx], qn, tmp.data_ptr(), offsets=[offs[i] for i in idx], stream=sh)
+        qpcm[torch.tensor(idx, device=dev)] = tmp
+    torch.cuda.synchronize(dev)
+    return qpcm
+
+
 def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T):
     from tiresias_amd import sharding
     n_db = 8000 * 30
@@ -336,25 +361,8 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     t_build = time.perf_counter() - t_build
     rows, nclips_local = eng.index_stats()
 
-    # queries: 75 % excerpts of DB clips at 256-aligned offsets, 25 % unrelated
-    rng = np.random.default_rng(SEED_Q)
     nq, qn = args.queries, 8000 * 5
-    seeds, clips, offs = [], [], []
-    for i in range(nq):
-        if i % 4 != 3:
-            clips.append(int(rng.integers(args.db_clips)))
-            offs.append(256 * int(rng.integers(0, (n_db - qn) // HOP)))
-            seeds.append(SEED_DB)
-        else:
-            clips.append(i)
-            offs.append(0)
-            seeds.append(SEED_Q)
-    qpcm = torch.empty((nq, qn), dtype=torch.int16, device=dev)
-    for sd in (SEED_DB, SEED_Q):
-        idx = [i for i in range(nq) if seeds[i] == sd]
-        tmp = torch.empty((len(idx), qn), dtype=torch.int16, device=dev)
-        eng.synth_device(sd, [clips[i] for i in idx], qn, tmp.data_ptr(), offsets=[offs[i] for i in idx], stream=sh)
-        qpcm[torch.tensor(idx, device=dev)] = tmp
+    qpcm = c3_queries(eng, torch, dev, sh, nq, args.db_clips)
     qplan = eng.plan(np.arange(nq + 1, dtype=np.int64) * qn)
     keys = torch.zeros(nq, dtype=torch.int64, device=dev)
     p = T.params(1, 0.001)

@@ -172,8 +172,15 @@ int tfp_index_rows(tfp_engine* eng, const char* uuid, int32_t* m1, int32_t* m2, 
 int tfp_index_remove(tfp_engine* eng, const char* uuid);
 int tfp_index_clear(tfp_engine* eng);
 int tfp_index_stats(tfp_engine* eng, int64_t* nrows, int32_t* nclips);
-/* Rebuild the sorted device index now (otherwise done lazily by the next search). */
+/* Rebuild the sorted device index now (otherwise done lazily by the next search). After the first
+ * build, adds and removals are merged into the sorted index in one pass over it (the added rows
+ * alone are sorted), as the reference's INSERTs update its max1 B-tree (fp_handler.c:559-571,
+ * :745-753); a full re-sort happens only for the first build, after many removals (staging
+ * compaction) or when the new rows outnumber half the index. */
 int tfp_index_commit(tfp_engine* eng);
+/* How the index was brought up to date so far: full sorts and incremental merges (new in round 3;
+ * either pointer may be NULL). */
+int tfp_index_build_stats(tfp_engine* eng, int64_t* full_builds, int64_t* merges);
 /* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
  * this engine's uuids). keys[clip_id] must order like the uuids across all shards and be
  * distinct over live clips. A clip added after this call has no key: the next search (or

@@ -162,14 +162,17 @@ def test_vote_ties_across_chunk_boundaries(oracle, tfp_lib, class_max, nkeys):
         eng.close()
 
 
-def _enroll_db(eng, torch, dev, stream, ids, keep_rows=True, chunk=2048):
+def _enroll_db(eng, torch, dev, stream, ids, keep_rows=True, chunk=2048, oracle=None, check_every=0):
     """bench.py's enrolment (synth -> fingerprint_device -> index_add_device, 2,048 clips at a
-    time) that also returns the rows it enrolled (host int32 [nclips * 938, 2])."""
+    time) that also returns the rows it enrolled (host int32 [nclips * 938, 2]). With an oracle,
+    every check_every-th clip's enrolled rows are compared with the oracle's fingerprints of the
+    same PCM (copied back from the device buffer the kernel read). Returns (rows, clips checked)."""
     n_db = 8000 * 30
     nf_db = (n_db + HOP - 1) // HOP
     buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
     micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
     rows = np.empty((len(ids) * nf_db, 2), np.int32) if keep_rows else None
+    checked = 0
     eng.index_clear()
     for s in range(0, len(ids), chunk):
         part = ids[s:s + chunk]
@@ -179,14 +182,25 @@ def _enroll_db(eng, torch, dev, stream, ids, keep_rows=True, chunk=2048):
         eng.fingerprint_device(plan, buf.data_ptr(), micro.data_ptr(), 0, stream)
         eng.index_add_device([_uuid_of(g) for g in part], np.arange(k + 1, dtype=np.int64) * nf_db, micro.data_ptr(),
                              stream)
-        if keep_rows:
+        if keep_rows or check_every:
             torch.cuda.synchronize()
-            rows[s * nf_db:(s + k) * nf_db] = micro[:k * nf_db].cpu().numpy()
+            got = micro[:k * nf_db].cpu().numpy()
+            if keep_rows:
+                rows[s * nf_db:(s + k) * nf_db] = got
+            if check_every:
+                sel = [i for i in range(k) if part[i] % check_every == 0]
+                pcm = buf[torch.tensor(sel, device=dev)].cpu().numpy().reshape(-1)
+                exp, _ = oracle.fingerprint_batch(pcm, np.arange(len(sel) + 1) * n_db, nthreads=ORACLE_THREADS,
+                                                  want_db=False)
+                g = np.concatenate([got[i * nf_db:(i + 1) * nf_db] for i in sel])
+                bad = np.nonzero((g != exp).any(axis=1))[0]
+                assert len(bad) == 0, ("enrolled rows differ from the oracle", s, len(bad))
+                checked += len(sel)
     eng.index_commit()
     torch.cuda.synchronize()
     del buf, micro
     torch.cuda.empty_cache()
-    return rows
+    return rows, checked
 
 
 def _c3_queries(nq, db_clips, seed=SEED_Q):
@@ -206,20 +220,23 @@ def _c3_queries(nq, db_clips, seed=SEED_Q):
 @pytest.fixture(scope="module")
 def c3db(oracle, tfp_lib, torch_cuda):
     """configs[2]'s DB: 100,000 x 30 s clips (93.8 M rows) enrolled on the device as bench.py does
-    (own engine), its rows checked on a 256-clip sample against the oracle's fingerprints, and the
-    oracle's sorted index over the same rows (tie key = rank of the uuid among all clips)."""
+    (own engine), the rows of every 16th clip (6,250 clips, 5.9 M rows) checked against the
+    oracle's fingerprints of the same PCM, a 64-clip sample of the host synthesiser's PCM against
+    the device's, and the oracle's sorted index over the same rows (tie key = rank of the uuid
+    among all clips)."""
     torch = torch_cuda
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     eng = tfp_lib.Engine(0)
     db_clips, n_db = 100_000, 8000 * 30
     nf_db = (n_db + HOP - 1) // HOP
-    rows = _enroll_db(eng, torch, dev, stream, list(range(db_clips)))
+    rows, checked = _enroll_db(eng, torch, dev, stream, list(range(db_clips)), oracle=oracle, check_every=16)
+    assert checked == 6250
     nrows, nc = eng.index_stats()
     assert nc == db_clips and nrows == db_clips * nf_db
     rng = np.random.default_rng(1)
-    sample = np.sort(rng.choice(db_clips, 256, replace=False))
-    pcm = tfp_lib.synth_pcm(SEED_DB, sample.tolist(), n_db)
+    sample = np.sort(rng.choice(db_clips, 64, replace=False))
+    pcm = tfp_lib.synth_pcm(SEED_DB, sample.tolist(), n_db)  # host synthesiser (the oracle's PCM above came from the device)
     exp, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(len(sample) + 1) * n_db, nthreads=ORACLE_THREADS,
                                       want_db=False)
     got = np.concatenate([rows[c * nf_db:(c + 1) * nf_db] for c in sample])
@@ -243,8 +260,10 @@ def _c3_batch(c3db, tfp_lib, torch, nq, seed=SEED_Q):
 
 def _oracle_q(oracle, qpcm):
     nfq = (qpcm.shape[1] + HOP - 1) // HOP
-    qdb = np.concatenate([oracle.fingerprint(qpcm[i])[1] for i in range(len(qpcm))])
-    return qdb, np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
+    qoff = np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
+    _, qdb = oracle.fingerprint_batch(np.ascontiguousarray(qpcm).reshape(-1), np.arange(len(qpcm) + 1) * qpcm.shape[1],
+                                      nthreads=ORACLE_THREADS)
+    return qdb, qoff
 
 
 def _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, p, nthreads=ORACLE_THREADS):
@@ -309,7 +328,7 @@ def test_configs4_512_channels_one_tick(engine, oracle, tfp_lib, torch_cuda):
     stream = torch.cuda.current_stream().cuda_stream
     db_clips, n_db, W, tick = 3000, 8000 * 30, 24000, 160
     nf_db = (n_db + HOP - 1) // HOP
-    rows = _enroll_db(engine, torch, dev, stream, list(range(db_clips)))
+    rows, _ = _enroll_db(engine, torch, dev, stream, list(range(db_clips)))
     uuids = [_uuid_of(g) for g in range(db_clips)]
     order = np.argsort(np.asarray(uuids))
     rank = np.empty(db_clips, np.int32)
@@ -344,3 +363,30 @@ def test_configs4_512_channels_one_tick(engine, oracle, tfp_lib, torch_cuda):
     assert checked == 96 and found > 20
     st.close()
     engine.index_clear()
+
+
+def _bench_batch(c3db, torch, nq=4096):
+    """The exact query batch bench.py times at configs[2] (bench.c3_queries), device and host."""
+    import sys
+    sys.path.insert(0, REPO)
+    import bench
+    dev = torch.device("cuda", 0)
+    d_q = bench.c3_queries(c3db["eng"], torch, dev, torch.cuda.current_stream().cuda_stream, nq, c3db["db_clips"])
+    return d_q.cpu().numpy(), d_q
+
+
+@pytest.mark.timeout(900)
+def test_configs2_timed_batch_all_4096_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
+    """The batch bench.py times (4,096 x 5 s queries, coefs = 1, tolerance 0.001, the vote path),
+    every one of its keys == the oracle's sorted-index search over the same 93.8 M rows; and the
+    bench's coefs = 2 tolerance 0.001 sweep on its first 256 queries (4 sweep chunks of 64 queries
+    in one slab of the general path, src/fp_handler.c:318-351) at full DB size."""
+    torch = torch_cuda
+    qpcm, d_q = _bench_batch(c3db, torch)
+    qdb, qoff = _oracle_q(oracle, qpcm)
+    w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(1, 0.001))
+    assert (w >= 0).sum() >= 1000  # (the bench reports ~1,500 found)
+    k = 256
+    w2, _ = _check_keys(c3db, tfp_lib, torch, qpcm[:k], d_q[:k].contiguous(), qdb[:k * int(qoff[1])], qoff[:k + 1],
+                        tfp_lib.params(2, 0.001))
+    assert (w2 >= 0).sum() > 0

@@ -1,0 +1,212 @@
+"""Incremental maintenance of the device index (csrc/tfp_index.hip) on the GPU.
+
+The reference's enrolment INSERTs a clip's rows into audio_fingerprint, whose max1 B-tree makes
+them searchable at once (src/fp_handler.c:559-571, :745-753); a delete removes them
+(:115-159). After the first build the engine merges adds and removals into its m1-sorted index in
+one pass (the new rows alone are sorted; columns renumbered around the inserted / removed uuids)
+instead of re-sorting every staged row. Every step below is searched on all paths (batch vote,
+batch-1 small path, coefs = 2 general path) and must equal the oracle over the live rows
+(count(*) DESC, ties to the greatest audio_uuid, :367-374) and an engine that rebuilds fully
+(TFP_INDEX_FULL=1); the merge count proves no full sort ran.
+
+Also the staging compaction's failure path (advisor finding, round 2): an allocation failure
+inside compact_staging must leave every clip's rows readable and the next build correct."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
+HOP = 256
+
+
+def _engine_with(tfp_lib, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return tfp_lib.Engine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _uuids(rng, n):
+    out = []
+    for _ in range(n):
+        h = "%032x" % int.from_bytes(rng.bytes(16), "little")
+        out.append("%s-%s-4%s-a%s-%s" % (h[:8], h[8:12], h[13:16], h[17:20], h[20:32]))
+    return out
+
+
+class Mirror:
+    """The live audio_fingerprint rows (uuid -> (m1, m2)) the engines should hold."""
+
+    def __init__(self):
+        self.rows = {}
+
+    def search(self, oracle, q1, q2, qoff, p):
+        uu = sorted(self.rows)
+        m1 = np.concatenate([self.rows[u][0] for u in uu]) if uu else np.zeros(0, np.int32)
+        m2 = np.concatenate([self.rows[u][1] for u in uu]) if uu else np.zeros(0, np.int32)
+        clip = np.concatenate([np.full(len(self.rows[u][0]), i, np.int32) for i, u in enumerate(uu)]) if uu else \
+            np.zeros(0, np.int32)
+        # the sorted-index oracle (checked against the reference SQL in test_oracle.py); uu is in
+        # uuid order, so the tie key of clip i is i
+        idx = oracle.SortedIndex(m1, m2, clip, np.arange(max(len(uu), 1), dtype=np.int32))
+        w, mc = idx.search_batch(q1, q2, qoff, p.coefs, p.tolerance, p.freq_ignore_low, p.freq_ignore_high,
+                                 nthreads=16)
+        return [(uu[w[i]], int(mc[i])) if w[i] >= 0 else None for i in range(len(qoff) - 1)]
+
+
+def _frames(tfp_lib, qdb):
+    fr = np.zeros(len(qdb), tfp_lib.FRAME_DTYPE)
+    fr["q1"], fr["q2"] = qdb[:, 0], qdb[:, 1]
+    return fr
+
+
+def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
+    rng = np.random.default_rng(31)
+    n, nclips = 8000 * 10, 420
+    nf = (n + HOP - 1) // HOP
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(nclips), n)
+    micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(nclips + 1) * n, nthreads=16, want_db=False)
+    rows = [(micro[c * nf:(c + 1) * nf, 0].copy(), micro[c * nf:(c + 1) * nf, 1].copy()) for c in range(nclips)]
+    uuids = _uuids(rng, nclips)
+    uuids[410] = "00000000-0000-4000-8000-000000000000"  # sorts before every other uuid
+    uuids[411] = "ffffffff-ffff-4fff-bfff-ffffffffffff"  # ... and after
+    # queries: 3 s excerpts of clips (enrolled at various steps) and unrelated audio
+    qn = 8000 * 3
+    qsrc = [int(rng.integers(nclips)) if i % 4 != 3 else -1 for i in range(40)]
+    qsrc[:6] = [300, 305, 410, 411, 2, 415]
+    qpcm = np.stack([tfp_lib.synth_pcm(SEED_DB, [c], qn, offsets=[256 * int(rng.integers(0, 150))])[0] if c >= 0
+                     else tfp_lib.synth_pcm(SEED_Q, [i], qn)[0] for i, c in enumerate(qsrc)])
+    qdb = np.concatenate([oracle.fingerprint(q)[1] for q in qpcm])
+    nfq = (qn + HOP - 1) // HOP
+    qoff = np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
+    frames = _frames(tfp_lib, qdb)
+
+    inc = tfp_lib.Engine(0)
+    full = _engine_with(tfp_lib, {"TFP_INDEX_FULL": "1"})
+    mir = Mirror()
+    engines = (inc, full)
+
+    def add(cs, uu=None):
+        uu = uu or [uuids[c] for c in cs]
+        fo = np.concatenate([[0], np.cumsum([len(rows[c][0]) for c in cs])])
+        for e in engines:
+            if len(cs) == 1:
+                e.index_add(uu[0], rows[cs[0]][0], rows[cs[0]][1])
+            else:
+                e.index_add_batch(uu, fo, np.concatenate([rows[c][0] for c in cs]),
+                                  np.concatenate([rows[c][1] for c in cs]))
+        for u, c in zip(uu, cs):
+            mir.rows[u] = rows[c]
+
+    def remove(u):
+        for e in engines:
+            e.index_remove(u)
+        del mir.rows[u]
+
+    def check(step):
+        for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05)):
+            exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+            for e in engines:
+                res, fcs = e.search_batch(frames, qoff, p)
+                got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+                assert got == exp, (step, p.coefs, p.tolerance, [i for i in range(len(exp)) if got[i] != exp[i]][:5])
+                assert all(f == nfq for f in fcs)
+        # batch-1 (small path) on the first queries
+        p = tfp_lib.params(1, 0.001)
+        exp = mir.search(oracle, qdb[:6 * nfq, 0], qdb[:6 * nfq, 1], qoff[:7], p)
+        for i in range(6):
+            r, _ = inc.search(frames[qoff[i]:qoff[i + 1]], p)
+            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
+        return sum(x is not None for x in exp)
+
+    add(list(range(300)))
+    for e in engines:
+        e.index_commit()
+    assert inc.index_build_stats() == (1, 0)
+    check("initial")
+    steps = 0
+    add([300]); steps += 1
+    check("one clip")
+    add([301]); steps += 1
+    check("another clip")
+    add(list(range(302, 340))); steps += 1
+    check("batch of 38")
+    for c in (0, 17, 150, 299):
+        remove(uuids[c])
+    steps += 1
+    check("4 removed")
+    remove(uuids[301]); steps += 1
+    check("a merged clip removed")
+    add([17], [uuids[17]]); steps += 1          # a removed uuid re-enrolled (same rows)
+    add([340], [uuids[0]]); steps += 1          # ... and one with other rows
+    check("re-added")
+    add([410]); add([411]); steps += 1
+    check("first and last uuid")
+    add([412]); remove(uuids[412]); add([413]); steps += 1   # added and removed between builds
+    check("transient clip")
+    for c in range(341, 356):                   # one clip per build, searched each time (the bench's enrolment loop)
+        add([c]); steps += 1
+        if c % 5 == 0:
+            check("stream of adds %d" % c)
+    assert check("final") > 10
+    fb, merges = inc.index_build_stats()
+    assert fb == 1 and merges == steps, (fb, merges, steps)   # no full sort after the first build
+    assert full.index_build_stats()[1] == 0
+    for e in engines:
+        assert e.index_stats() == (sum(len(r[0]) for r in mir.rows.values()), len(mir.rows))
+        e.close()
+
+
+def test_compaction_failure_leaves_index_intact(tfp_lib, oracle):
+    """compact_staging fails (injected allocation failure) after many removals: the call returns
+    TFP_E_NOMEM, every live clip's rows read back unchanged, and the next commit succeeds and
+    searches equal the oracle (the advisor's round-2 finding at tfp_engine.cpp:453)."""
+    rng = np.random.default_rng(5)
+    n, nclips = 8000 * 30, 200
+    nf = (n + HOP - 1) // HOP
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(nclips), n)
+    micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(nclips + 1) * n, nthreads=16, want_db=False)
+    uuids = _uuids(rng, nclips)
+    eng = _engine_with(tfp_lib, {"TFP_TEST_FAIL_COMPACT": "1"})
+    eng.index_add_batch(uuids, np.arange(nclips + 1) * nf, micro[:, 0], micro[:, 1])
+    eng.index_commit()
+    mir = Mirror()
+    for c in range(nclips):
+        mir.rows[uuids[c]] = (micro[c * nf:(c + 1) * nf, 0], micro[c * nf:(c + 1) * nf, 1])
+    for c in range(0, nclips, 4):   # interleaved live / dead runs
+        for k in range(3):
+            if c + k < nclips:
+                eng.index_remove(uuids[c + k])
+                del mir.rows[uuids[c + k]]
+    with pytest.raises(tfp_lib.TfpError) as ei:
+        eng.index_commit()  # dead rows > 1/4 of the live ones: compaction, which fails
+    assert ei.value.code == -3
+    for u, (m1, m2) in mir.rows.items():
+        g1, g2 = eng.index_rows(u)
+        assert np.array_equal(g1, m1) and np.array_equal(g2, m2), u
+    eng.index_commit()
+    for u, (m1, m2) in mir.rows.items():
+        g1, g2 = eng.index_rows(u)
+        assert np.array_equal(g1, m1) and np.array_equal(g2, m2), u
+    qn = 8000 * 3
+    live = [c for c in range(nclips) if uuids[c] in mir.rows]
+    qpcm = np.stack([tfp_lib.synth_pcm(SEED_DB, [live[i * 7 % len(live)]], qn, offsets=[256 * 40])[0]
+                     for i in range(12)])
+    qdb = np.concatenate([oracle.fingerprint(q)[1] for q in qpcm])
+    nfq = (qn + HOP - 1) // HOP
+    qoff = np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
+    p = tfp_lib.params(1, 0.001)
+    res, _ = eng.search_batch(_frames(tfp_lib, qdb), qoff, p)
+    got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+    exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+    assert got == exp and sum(x is not None for x in exp) >= 8
+    eng.close()
