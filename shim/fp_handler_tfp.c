@@ -24,45 +24,58 @@
 #include "asterisk/utils.h"
 
 #include "fp_catalog.h"
+#include "fp_handler_tfp.h"
 #include "tiresias_fp.h"
 
 static tfp_engine* g_tfp = NULL; /* one engine (GPU 0) for the module */
 static void pcm_pool_drain(void);
 
-static bool load_clip(void* arg, const char* uuid, const int32_t* m1, const int32_t* m2, int64_t n)
-{
-	(void)arg;
-	if(tfp_index_add(g_tfp, uuid, m1, m2, (int32_t)n, NULL) != TFP_OK) {
-		ast_log(LOG_WARNING, "Could not index audio %s: %s\n", uuid, tfp_engine_last_error(g_tfp));
-	}
-	return true;
-}
-
+/* fp_init (fp_handler.c:68-90): the catalog (init_database + the backup's tables), the engine, and
+ * the GPU index from the restored audio_fingerprint table in one tfp_index_add_batch. A failure
+ * closes whatever was opened, without writing the backup. */
 bool fp_init(void)
 {
+	fpc_rows rows;
+
 	if(fpc_db_init() == false) {
 		ast_log(LOG_ERROR, "Could not initiate database.\n");
 		return false;
 	}
 	if(tfp_engine_create(0, &g_tfp) != TFP_OK) {
 		ast_log(LOG_ERROR, "Could not create the MI355X fingerprint engine.\n");
+		g_tfp = NULL;
+		fpc_db_close();
 		return false;
 	}
-	/* the GPU index from the restored audio_fingerprint table */
-	if(fpc_for_each_fingerprint_clip(load_clip, NULL) == false || tfp_index_commit(g_tfp) != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not load the fingerprint index: %s\n", tfp_engine_last_error(g_tfp));
+	if(fpc_load_fingerprints(&rows) == false) {
+		ast_log(LOG_ERROR, "Could not load the database data.\n");
 		tfp_engine_destroy(g_tfp);
 		g_tfp = NULL;
+		fpc_db_close();
 		return false;
 	}
+	if(tfp_index_add_batch(g_tfp, rows.nclips, (const char* const*)rows.uuids, rows.frame_offsets, rows.m1, rows.m2)
+			!= TFP_OK || tfp_index_commit(g_tfp) != TFP_OK) {
+		ast_log(LOG_ERROR, "Could not load the fingerprint index: %s\n", tfp_engine_last_error(g_tfp));
+		fpc_rows_free(&rows);
+		tfp_engine_destroy(g_tfp);
+		g_tfp = NULL;
+		fpc_db_close();
+		return false;
+	}
+	fpc_rows_free(&rows);
 	return true;
 }
 
+/* fp_term (fp_handler.c:92-108): the backup (the rows were written to audio_fingerprint at
+ * enrolment), then the engine */
 bool fp_term(void)
 {
-	bool ret = fpc_db_term(); /* the rows were written to audio_fingerprint at enrolment */
+	bool ret = fpc_db_term();
 	pcm_pool_drain();
-	tfp_engine_destroy(g_tfp);
+	if(g_tfp != NULL) {
+		tfp_engine_destroy(g_tfp);
+	}
 	g_tfp = NULL;
 	if(ret == false) {
 		ast_log(LOG_ERROR, "Could not write database.\n");
@@ -264,6 +277,274 @@ bool fp_craete_audio_list_info(const char* context, const char* filename)
 	}
 	ast_free(uuid);
 	return true;
+}
+
+/* ---- batched enrolment: app_tiresias.c:365-424's directory scan onto the GPU ----------------
+ * The reference calls fp_craete_audio_list_info once per file of a context's directory (scandir,
+ * alphasort). fp_create_audio_list_infos takes the whole list: the catalog rows are written in
+ * the same order with the same per-context MD5 dedup (a file repeated within the list counts as
+ * already enrolled), and the audio of all new files is fingerprinted by one tfp_fingerprint_batch
+ * (per sample rate and sample format, and per ENROL_BATCH_SAMPLES) and indexed by one
+ * tfp_index_add_batch, instead of a GPU round trip per file. */
+#define ENROL_GROUPS 4
+#define ENROL_BATCH_SAMPLES ((int64_t)1 << 27) /* 256 MB of int16 per batch */
+
+typedef struct {
+	int32_t sr;
+	bool f32;
+	int n, cap;
+	int* file;         /* index into the caller's list */
+	char** uuid;
+	int64_t* off;      /* [n + 1] sample offsets */
+	int64_t scap;      /* samples allocated */
+	void* x;           /* int16 PCM or fp32 hop values */
+} enrol_group;
+
+static void group_reset(enrol_group* g)
+{
+	int i;
+	for(i = 0; i < g->n; i++) {
+		ast_free(g->uuid[i]);
+	}
+	g->n = 0;
+	if(g->off) {
+		g->off[0] = 0;
+	}
+}
+
+static void group_free(enrol_group* g)
+{
+	group_reset(g);
+	ast_free(g->file);
+	ast_free(g->uuid);
+	ast_free(g->off);
+	ast_free(g->x);
+	memset(g, 0, sizeof(*g));
+}
+
+/* fingerprint, store and index one group; returns the clips enrolled */
+static int group_flush(const char* context, enrol_group* g, bool* ok)
+{
+	int64_t nf = 0, got = 0, i;
+	int c, kept = 0, done = 0;
+	tfp_frame* rows = NULL;
+	int32_t *m1 = NULL, *m2 = NULL;
+	int64_t* foff = NULL;
+	const char** uu = NULL;
+	int rc;
+
+	if(g->n == 0) {
+		return 0;
+	}
+	for(c = 0; c < g->n; c++) {
+		nf += tfp_frame_count(g->off[c + 1] - g->off[c]);
+	}
+	rows = ast_calloc(nf ? nf : 1, sizeof(tfp_frame));
+	m1 = ast_malloc(sizeof(int32_t) * (nf ? nf : 1));
+	m2 = ast_malloc(sizeof(int32_t) * (nf ? nf : 1));
+	foff = ast_malloc(sizeof(int64_t) * (g->n + 1));
+	uu = ast_malloc(sizeof(char*) * g->n);
+	rc = TFP_E_NOMEM;
+	if(rows && m1 && m2 && foff && uu) {
+		rc = g->f32 ? tfp_fingerprint_f32_batch(g_tfp, (const float*)g->x, g->off, g->n, g->sr, rows, nf, &got)
+		            : tfp_fingerprint_batch(g_tfp, (const int16_t*)g->x, g->off, g->n, g->sr, rows, nf, &got);
+	}
+	if(rc != TFP_OK) {
+		ast_log(LOG_ERROR, "Could not fingerprint %d files: %s\n", g->n, tfp_engine_last_error(g_tfp));
+	}
+	else {
+		/* the audio_fingerprint rows of each clip; a clip whose rows could not be stored is dropped */
+		int64_t src = 0;
+		foff[0] = 0;
+		for(c = 0; c < g->n; c++) {
+			const int64_t n = tfp_frame_count(g->off[c + 1] - g->off[c]);
+			int32_t* a = m1 + foff[kept];
+			int32_t* b = m2 + foff[kept];
+			for(i = 0; i < n; i++) {
+				a[i] = rows[src + i].m1;
+				b[i] = rows[src + i].m2;
+			}
+			src += n;
+			if(fpc_store_fingerprints(context, g->uuid[c], a, b, n) == false) {
+				ast_log(LOG_NOTICE, "Could not create audio fingerprint info.\n");
+				fpc_delete_audio_list_info(g->uuid[c]);
+				continue;
+			}
+			uu[kept] = g->uuid[c];
+			foff[kept + 1] = foff[kept] + n;
+			g->file[kept] = g->file[c];
+			kept++;
+		}
+		if(tfp_index_add_batch(g_tfp, kept, (const char* const*)uu, foff, m1, m2) != TFP_OK) {
+			ast_log(LOG_ERROR, "Could not index %d files: %s\n", kept, tfp_engine_last_error(g_tfp));
+			for(c = 0; c < kept; c++) {
+				fpc_delete_audio_list_info(uu[c]);
+			}
+		}
+		else {
+			for(c = 0; c < kept; c++) {
+				if(ok) {
+					ok[g->file[c]] = true;
+				}
+			}
+			done = kept;
+		}
+	}
+	if(rc != TFP_OK) {
+		for(c = 0; c < g->n; c++) {
+			fpc_delete_audio_list_info(g->uuid[c]);
+		}
+	}
+	ast_free(rows);
+	ast_free(m1);
+	ast_free(m2);
+	ast_free(foff);
+	ast_free(uu);
+	group_reset(g);
+	return done;
+}
+
+/* appends file f's audio (ns samples at rate sr) to g; false on allocation or read errors */
+static bool group_add(enrol_group* g, int f, const char* filename, char* uuid, int64_t ns)
+{
+	const size_t ss = g->f32 ? sizeof(float) : sizeof(int16_t);
+	const int64_t at = g->off[g->n];
+	int64_t got = 0;
+	int32_t sr = 0;
+	int rc;
+	if(g->n + 1 >= g->cap) {
+		int nc = g->cap ? 2 * g->cap : 64;
+		int* nf = realloc(g->file, sizeof(int) * (size_t)nc);
+		char** nu = nf ? realloc(g->uuid, sizeof(char*) * (size_t)nc) : NULL;
+		int64_t* no = nu ? realloc(g->off, sizeof(int64_t) * ((size_t)nc + 1)) : NULL;
+		if(nf) g->file = nf;
+		if(nu) g->uuid = nu;
+		if(no) g->off = no;
+		if(no == NULL) {
+			return false;
+		}
+		g->cap = nc;
+	}
+	if(at + ns + 1 > g->scap) {
+		int64_t nc = g->scap ? g->scap : (int64_t)1 << 20;
+		void* nx;
+		while(nc < at + ns + 1) {
+			nc *= 2;
+		}
+		nx = realloc(g->x, ss * (size_t)nc);
+		if(nx == NULL) {
+			return false;
+		}
+		g->x = nx;
+		g->scap = nc;
+	}
+	rc = g->f32 ? tfp_wav_read_f32(filename, (float*)g->x + at, ns, &got, &sr)
+	            : tfp_wav_read(filename, (int16_t*)g->x + at, ns, &got, &sr);
+	if(rc != TFP_OK || got != ns || sr != g->sr) {
+		return false;
+	}
+	g->file[g->n] = f;
+	g->uuid[g->n] = uuid;
+	g->off[g->n + 1] = at + ns;
+	g->n++;
+	return true;
+}
+
+int fp_create_audio_list_infos(const char* context, const char* const* filenames, int count, bool* ok)
+{
+	enrol_group groups[ENROL_GROUPS];
+	int i, k, enrolled = 0;
+
+	if((context == NULL) || (filenames == NULL) || (count < 0)) {
+		ast_log(LOG_WARNING, "Wrong input parameter.\n");
+		return -1;
+	}
+	memset(groups, 0, sizeof(groups));
+	for(i = 0; i < count; i++) {
+		const char* f = filenames[i];
+		char* uuid;
+		int ret;
+		int64_t ns = 0;
+		int32_t sr = 0;
+		bool f32 = false;
+		enrol_group* g = NULL;
+
+		if(ok) {
+			ok[i] = false;
+		}
+		if(f == NULL) {
+			continue;
+		}
+		uuid = fp_generate_uuid();
+		if(uuid == NULL) {
+			continue;
+		}
+		ret = fpc_create_audio_list_info(context, f, uuid);
+		if(ret < 0) {
+			ast_log(LOG_WARNING, "Could not create audio_list info. context[%s], filename[%s]\n", context, f);
+			ast_free(uuid);
+			continue;
+		}
+		if(ret == 0) {
+			ast_log(LOG_VERBOSE, "The given audio file is already exist in the list. context[%s], filename[%s]\n",
+					context, f);
+			ast_free(uuid);
+			if(ok) {
+				ok[i] = true;
+			}
+			continue;
+		}
+		/* aubio_source at the native rate: int16 PCM, else the fp32 hop values (read_audio) */
+		if(tfp_wav_read(f, NULL, 0, &ns, &sr) != TFP_OK) {
+			f32 = true;
+			if(tfp_wav_read_f32(f, NULL, 0, &ns, &sr) != TFP_OK) {
+				ast_log(LOG_WARNING, "Could not read %s: %s\n", f, tfp_engine_last_error(NULL));
+				ast_log(LOG_NOTICE, "Could not create audio fingerprint info.\n");
+				fpc_delete_audio_list_info(uuid);
+				ast_free(uuid);
+				continue;
+			}
+		}
+		for(k = 0; k < ENROL_GROUPS; k++) {
+			if(groups[k].off != NULL && groups[k].sr == sr && groups[k].f32 == f32) {
+				g = &groups[k];
+				break;
+			}
+		}
+		if(g == NULL) {
+			for(k = 0; k < ENROL_GROUPS && groups[k].off != NULL; k++) {
+			}
+			if(k == ENROL_GROUPS) { /* many formats in one scan: flush them all */
+				for(k = 0; k < ENROL_GROUPS; k++) {
+					enrolled += group_flush(context, &groups[k], ok);
+					group_free(&groups[k]);
+				}
+				k = 0;
+			}
+			g = &groups[k];
+			g->sr = sr;
+			g->f32 = f32;
+			g->off = ast_calloc(1, sizeof(int64_t));
+			if(g->off == NULL) {
+				fpc_delete_audio_list_info(uuid);
+				ast_free(uuid);
+				continue;
+			}
+		}
+		if(g->n > 0 && g->off[g->n] + ns > ENROL_BATCH_SAMPLES) {
+			enrolled += group_flush(context, g, ok);
+		}
+		if(group_add(g, i, f, uuid, ns) == false) {
+			ast_log(LOG_WARNING, "Could not read %s: %s\n", f, tfp_engine_last_error(NULL));
+			fpc_delete_audio_list_info(uuid);
+			ast_free(uuid);
+		}
+	}
+	for(k = 0; k < ENROL_GROUPS; k++) {
+		enrolled += group_flush(context, &groups[k], ok);
+		group_free(&groups[k]);
+	}
+	return enrolled;
 }
 
 struct ast_json* fp_search_fingerprint_info(const char* context, const char* filename, const int coefs,

@@ -1,0 +1,33 @@
+/* fp_handler_tfp.h — the engine facade of the module (src/fp_handler.h:13-38, unchanged
+ * signatures) as built from shim/fp_handler_tfp.c (hot half) + shim/fp_catalog.c (catalog half),
+ * plus what the MI355X engine adds for the module's callers. */
+#ifndef FP_HANDLER_TFP_H
+#define FP_HANDLER_TFP_H
+
+#include <stdbool.h>
+
+struct ast_json;
+
+/* src/fp_handler.h:13-38 */
+bool fp_init(void);
+bool fp_term(void);
+bool fp_create_context_list_info(const char* name, const char* directory, bool replace);
+bool fp_delete_context_list_info(const char* name);
+struct ast_json* fp_get_context_lists_all(void);
+struct ast_json* fp_get_context_list_info(const char* name);
+struct ast_json* fp_get_audio_lists_all(void);
+struct ast_json* fp_get_audio_lists_by_contextname(const char* name);
+bool fp_craete_audio_list_info(const char* context, const char* filename);
+bool fp_delete_audio_list_info(const char* uuid);
+struct ast_json* fp_search_fingerprint_info(const char* context, const char* filename, const int coefs,
+		const double tolerance, const int freq_ignore_low, const int freq_ignore_high);
+char* fp_generate_uuid(void);
+char* fp_create_hash(const char* filename);
+
+/* New: fp_craete_audio_list_info over a list of files of one context, as app_tiresias.c's
+ * create_new_audio_info (:365-424) calls it file by file for its directory scan. ok[i] (ok may be
+ * NULL) receives what fp_craete_audio_list_info(context, filenames[i]) would return. Returns the
+ * number of files newly enrolled, or -1 for bad arguments. */
+int fp_create_audio_list_infos(const char* context, const char* const* filenames, int count, bool* ok);
+
+#endif

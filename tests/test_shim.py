@@ -1,9 +1,12 @@
-"""The compiled Asterisk-side shim (shim/fp_handler_tfp.c): the reference's facade
-src/fp_handler.h:13-38 over the C-ABI, built with -pedantic -Werror against test stubs of the
+"""The compiled Asterisk-side shim: shim/fp_handler_tfp.c (hot half, over the C-ABI) +
+shim/fp_catalog.c (the reference's SQLite catalog and audio_recongition.db backup), together the
+reference's facade src/fp_handler.h:13-38, built with -pedantic -Werror against test stubs of the
 Asterisk headers (tests/native/asterisk_stub) and driven from C by tests/native/shim_harness.c the
-way the dialplan application calls it (src/application_handler.c:180-236): enrolment, a duplicate
-file, FOUND / NOTFOUND, bad coefs, a NULL context, delete, and a restart that reloads the index
-from the backup. Results equal the oracle's search over the same rows."""
+way the module calls it (application_handler.c:180-236, app_tiresias.c:365-424): enrolment, a
+duplicate file, FOUND / NOTFOUND, bad coefs, a NULL context, delete, a restart that reloads the
+index from the backup file; batched directory enrolment == the reference's file-by-file loop; and
+backup files interchangeable with tiresias_amd/dbio.py's in both directions. Results equal the
+oracle's search over the same rows."""
 import json
 import os
 import subprocess
@@ -14,17 +17,21 @@ import pytest
 
 from conftest import PKG, REPO
 
-SHIM_SRC = [os.path.join(REPO, "shim", "fp_handler_tfp.c"), os.path.join(REPO, "tests", "native", "shim_harness.c")]
-INC = ["-I" + os.path.join(REPO, d) for d in ("shim", "include", "tests/native/asterisk_stub")]
+SHIM_SRC = [os.path.join(REPO, "shim", "fp_handler_tfp.c"), os.path.join(REPO, "shim", "fp_catalog.c"),
+            os.path.join(REPO, "tests", "native", "shim_harness.c")]
+INC = ["-I" + os.path.join(REPO, d) for d in ("shim", "include", "tests/native/asterisk_stub")] + \
+    ["-idirafter", "/opt/conda/include"]  # sqlite3.h (the image has libsqlite3.so.0 but no dev package)
+LIBS = ["-l:libsqlite3.so.0", "-lcrypto", "-lm"]
 
 
 def _build(tmp_path, tfp_lib):
     lib = os.path.dirname(tfp_lib.LIB_PATH)
     exe = str(tmp_path / "shim_driver")
-    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic", *INC, "-c", SHIM_SRC[0], "-o",
-                    str(tmp_path / "shim.o")], check=True)
+    for src in SHIM_SRC[:2]:
+        subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic", *INC, "-c", src, "-o",
+                        str(tmp_path / (os.path.basename(src) + ".o"))], check=True)
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", *INC, *SHIM_SRC, "-o", exe, "-L" + lib,
-                    "-ltiresias_fp", "-Wl,-rpath," + lib], check=True)
+                    "-ltiresias_fp", "-Wl,-rpath," + lib, *LIBS], check=True)
     return exe
 
 
@@ -59,7 +66,7 @@ def _run(exe, snap, *cmd):
 @pytest.mark.gpu
 def test_shim_end_to_end_vs_oracle(tmp_path, tfp_lib, oracle):
     exe = _build(tmp_path, tfp_lib)
-    snap = str(tmp_path / "snapshot.txt")
+    snap = str(tmp_path / "audio_recongition.db")
     n, nclips = 8000 * 8, 6
     pcm = tfp_lib.synth_pcm(0x7153A1, range(nclips), n)
     files = []
@@ -136,3 +143,112 @@ def test_shim_end_to_end_vs_oracle(tmp_path, tfp_lib, oracle):
     assert out2[0] == {"init": True}
     assert sub(out2[1]) == sub(s[0])
     assert sub(out2[2]) == expect([0, 1, 2, 3, 5], "q5", 0.45)
+
+
+def _db_rows_by_name(path):
+    """{audio_list name: (context, hash, [(m1 REAL or None, m2 REAL or None) in frame order])}"""
+    import sqlite3
+    con = sqlite3.connect(path)
+    out = {}
+    for uuid, name, ctx, h in con.execute("select uuid, name, context, hash from audio_list"):
+        rows = con.execute("select max1, max2 from audio_fingerprint where audio_uuid = ? order by frame_idx",
+                           (uuid,)).fetchall()
+        out[name] = (ctx, h, rows)
+    con.close()
+    return out
+
+
+@pytest.mark.gpu
+def test_shim_batched_directory_enrolment_equals_per_file(tmp_path, tfp_lib, oracle):
+    """app_tiresias.c:365-424's scan of a context directory (alphasort): fp_create_audio_list_infos
+    (one GPU batch per sample format) leaves the same catalog and audio_fingerprint rows and gives
+    the same search results as fp_craete_audio_list_info file by file, including a repeated file
+    (already enrolled), a non-audio file (not enrolled), stereo (fp32 path) and 16 kHz audio."""
+    exe = _build(tmp_path, tfp_lib)
+    d = tmp_path / "dir"
+    d.mkdir()
+    n = 8000 * 6
+    pcm = tfp_lib.synth_pcm(0x7153A1, range(7), n)
+    for c in range(5):
+        _write_wav(str(d / ("c%02d.wav" % c)), pcm[c])
+    _write_wav(str(d / "c05_copy.wav"), pcm[1])                       # same bytes as c01: deduplicated
+    st = np.stack([pcm[5], (pcm[5] // 3).astype(np.int16)], 1)
+    _write_wav(str(d / "c06_stereo.wav"), st.reshape(-1), channels=2)
+    _write_wav(str(d / "c07_16k.wav"), tfp_lib.synth_pcm(0x7153A1, [6], 16000 * 5)[0], rate=16000)
+    (d / "c08_notes.txt").write_text("not audio")
+    q = str(tmp_path / "q.wav")
+    _write_wav(q, pcm[3, 256 * 30: 256 * 30 + 16000])
+    res = {}
+    for mode in ("enrolldir", "enrolldir1"):
+        db = str(tmp_path / (mode + ".db"))
+        out = _run(exe, db, "init", mode, "ctx", str(d), "search", "ctx", q, "1", "0.45", "-1", "-1",
+                   "search", "ctx", q, "1", "0.001", "-1", "-1", "term")
+        assert out[0] == {"init": True} and out[-1] == {"term": True}
+        res[mode] = (out[1], [o for o in out if "TIRSTATUS" in o], _db_rows_by_name(db))
+    b, f = res["enrolldir"], res["enrolldir1"]
+    assert b[0]["ok"] == f[0]["ok"] == [True] * 8 + [False]
+    assert b[0]["enrolled"] == 7
+    strip = [{k: v for k, v in o.items() if k not in ("TIRFILEUUID",)} for o in b[1]]
+    assert strip == [{k: v for k, v in o.items() if k not in ("TIRFILEUUID",)} for o in f[1]]
+    assert b[1][0]["TIRSTATUS"] == "FOUND" and b[1][0]["TIRFILENAME"] == "c03.wav"
+    assert b[2] == f[2] and sorted(b[2]) == ["c%02d.wav" % c for c in range(5)] + ["c06_stereo.wav", "c07_16k.wav"]
+    # the stored rows are the oracle's "%f" values
+    _, _, micro = oracle.fingerprint(pcm[2])
+    rows = b[2]["c02.wav"][2]
+    assert len(rows) == len(micro)
+    assert all((None if m == -(2**31) else round(r * 1e6)) == (None if m == -(2**31) else int(m))
+               for (r, _), m in zip(rows, micro[:, 0]))
+
+
+@pytest.mark.gpu
+def test_shim_backup_interchangeable_with_dbio(tmp_path, tfp_lib):
+    """A backup the C module writes (fp_term) loads through the Python mirror (FpHandler ->
+    dbio.load_backup) with the same search results, and one the mirror writes loads through the
+    C module (fp_init) with the same results."""
+    exe = _build(tmp_path, tfp_lib)
+    n = 8000 * 6
+    pcm = tfp_lib.synth_pcm(0x7153A1, range(6), n)
+    files = []
+    for c in range(6):
+        files.append(str(tmp_path / ("w%d.wav" % c)))
+        _write_wav(files[-1], pcm[c])
+    qs = []
+    for i, c in enumerate((0, 2, 4, 5)):
+        qs.append(str(tmp_path / ("q%d.wav" % i)))
+        _write_wav(qs[-1], pcm[c, 256 * (5 + 7 * i): 256 * (5 + 7 * i) + 16000])
+
+    def searches_c(db, enrol):
+        cmd = ["init"]
+        for f in enrol:
+            cmd += ["enroll", "ctx", f]
+        for q in qs:
+            cmd += ["search", "ctx", q, "1", "0.45", "-1", "-1", "search", "ctx", q, "2", "0.3", "-1", "-1"]
+        out = _run(exe, db, *(cmd + ["term"]))
+        return [{k: v for k, v in o.items() if k != "file"} for o in out if "TIRSTATUS" in o]
+
+    def searches_py(db, enrol):
+        h = tfp_lib.FpHandler(0, backup_path=db)
+        assert h.fp_init()
+        for f in enrol:
+            assert h.fp_craete_audio_list_info("ctx", f)
+        out = []
+        for q in qs:
+            for coefs, tol in ((1, 0.45), (2, 0.3)):
+                r = h.fp_search_fingerprint_info("ctx", q, coefs, tol, -1, -1)
+                out.append({"TIRSTATUS": "NOTFOUND"} if r is None else
+                           {"TIRSTATUS": "FOUND", "TIRFRAMECOUNT": r["frame_count"], "TIRMATCHCOUNT": r["match_count"],
+                            "TIRFILEUUID": r["uuid"], "TIRFILENAME": r["name"], "TIRCONTEXT": r["context"],
+                            "TIRFILEHASH": r["hash"]})
+        assert h.fp_term()
+        return out
+
+    c_db = str(tmp_path / "c.db")
+    c_first = searches_c(c_db, files)
+    assert sum(o["TIRSTATUS"] == "FOUND" for o in c_first) >= 4
+    assert searches_py(c_db, []) == c_first          # C writes, Python reads
+    py_db = str(tmp_path / "py.db")
+    py_first = searches_py(py_db, files)
+    py_uuids = {o["TIRFILENAME"]: o["TIRFILEUUID"] for o in py_first if o["TIRSTATUS"] == "FOUND"}
+    assert searches_c(py_db, []) == py_first         # Python writes, C reads
+    strip = lambda v: [{k: x for k, x in o.items() if k != "TIRFILEUUID"} for o in v]  # noqa: E731
+    assert strip(py_first) == strip(c_first) and py_uuids
