@@ -1,0 +1,671 @@
+// tfp_group.cpp — several engines (one per GPU of the node) behind one index and one search
+// (include/tiresias_fp.h, "device groups").
+//
+// The reference's fp_search_fingerprint_info is one SQL pipeline over the whole audio_fingerprint
+// table (fp_handler.c:287-374). Here the enrolled clips are sharded over the engines — a clip is
+// never split, because the per-frame GROUP BY audio_uuid (:353) is not additive over a split clip —
+// and every search runs on all shards in parallel, one worker thread per engine. Each shard's
+// per-query winner is the key (count << 32 | global uuid rank): the engines carry the group-wide
+// uuid ranks as their tie-break keys (tfp_index_set_tiebreak), so the greatest key over the shards
+// is the reference's winner (count(*) DESC, ties to the greatest audio_uuid, :367-374) and the
+// combine is an integer max on the host (the results leave the GPUs for the caller anyway).
+//
+// Batches of host PCM large enough to be throughput-bound are query-sharded: shard s fingerprints
+// queries [s·nq/N, (s+1)·nq/N) on its GPU, the frame values are exchanged device to device
+// (hipMemcpyPeerAsync over xGMI; a plain device copy when a device repeats), and every shard
+// searches the whole batch against its clips (tfp_search_q_device). Smaller batches (batch-1
+// latency) and stream ticks are fingerprinted by every shard itself: no exchange on the latency
+// path. Stream channels run on every shard's engine (the windows are fingerprinted per shard, a
+// few tens of microseconds of GPU time), each shard matching them against its clips.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tiresias_fp.h"
+
+namespace {
+
+// One worker thread per shard but the first (which runs on the caller); run() executes f(s) for
+// every shard in parallel and returns when all are done.
+class ShardPool {
+ public:
+  explicit ShardPool(int n) : n_(n), rc_(n, 0) {
+    for (int s = 1; s < n; s++) th_.emplace_back([this, s] { loop(s); });
+  }
+  ~ShardPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  // first nonzero return code (shard order), its shard in *bad
+  int run(const std::function<int(int)>& f, int* bad = nullptr) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      f_ = &f;
+      pending_ = n_ - 1;
+      gen_++;
+    }
+    cv_.notify_all();
+    rc_[0] = f(0);
+    {
+      std::unique_lock<std::mutex> lk(m_);
+      done_.wait(lk, [this] { return pending_ == 0; });
+      f_ = nullptr;
+    }
+    for (int s = 0; s < n_; s++)
+      if (rc_[s]) {
+        if (bad) *bad = s;
+        return rc_[s];
+      }
+    return TFP_OK;
+  }
+
+ private:
+  void loop(int s) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<int(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(m_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        f = f_;
+      }
+      const int rc = (*f)(s);
+      std::lock_guard<std::mutex> lk(m_);
+      rc_[s] = rc;
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  int n_;
+  std::vector<int> rc_;
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<int(int)>* f_ = nullptr;
+  uint64_t gen_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+struct Member {
+  std::string uuid;
+  int32_t shard;
+  int32_t id;  // the engine's clip id
+};
+
+// Device buffers of the query-sharded batch path, one set per shard.
+struct ShardBufs {
+  void* pcm = nullptr;      // this shard's queries (int16)
+  void* micro = nullptr;    // their stored values (unused by the search, written by the kernel)
+  void* q = nullptr;        // the whole batch's frame values (2 doubles per frame)
+  void* keys = nullptr;     // per-query keys
+  size_t b_pcm = 0, b_micro = 0, b_q = 0, b_keys = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t fp_done = nullptr;
+  tfp_plan* plan = nullptr;  // this shard's share of the last batch shape (k queries of qn samples)
+  int64_t plan_k = -1, plan_qn = -1;
+  int32_t plan_sr = 0;
+};
+
+hipError_t grow(void** p, size_t* have, size_t want) {
+  if (want <= *have) return hipSuccess;
+  if (*p) (void)hipFree(*p);
+  *p = nullptr;
+  *have = 0;
+  hipError_t e = hipMalloc(p, want);
+  if (e == hipSuccess) *have = want;
+  return e;
+}
+
+}  // namespace
+
+struct tfp_group {
+  std::vector<tfp_engine*> eng;
+  std::vector<int32_t> dev;
+  ShardPool* pool = nullptr;
+  std::recursive_mutex mu;
+  std::string err;
+  std::unordered_map<std::string, int32_t> where;     // uuid -> index in members
+  std::vector<Member> members;                         // every clip ever added (uuid "" once removed)
+  std::vector<std::vector<int32_t>> id2member;         // [shard][engine clip id] -> member index (-1 removed)
+  std::vector<int64_t> rows;                           // live rows per shard (placement)
+  std::vector<int32_t> by_uuid;                        // live members in uuid order (global ranks)
+  std::vector<int32_t> member_rank;                    // member -> its global rank (valid when !ranks_dirty)
+  bool ranks_dirty = true;
+  std::vector<ShardBufs> bufs;
+  ~tfp_group() {
+    delete pool;
+    for (size_t s = 0; s < bufs.size(); s++) {
+      (void)hipSetDevice(dev[s]);
+      for (void* p : {bufs[s].pcm, bufs[s].micro, bufs[s].q, bufs[s].keys})
+        if (p) (void)hipFree(p);
+      if (bufs[s].fp_done) (void)hipEventDestroy(bufs[s].fp_done);
+      tfp_plan_destroy(bufs[s].plan);
+      if (bufs[s].stream) (void)hipStreamDestroy(bufs[s].stream);
+    }
+    for (auto* e : eng) tfp_engine_destroy(e);
+  }
+};
+
+struct tfp_group_stream {
+  tfp_group* g = nullptr;
+  std::vector<tfp_stream*> st;  // one per shard, every channel
+  int32_t nch = 0;
+  std::vector<std::vector<tfp_result>> res;
+};
+
+namespace {
+
+int gfail(tfp_group* g, int code, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+int gfail(tfp_group* g, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (g) g->err = buf;
+  return code;
+}
+
+// The error of shard s's failed call, into the group's message.
+int shard_fail(tfp_group* g, int rc, int s) {
+  return gfail(g, rc, "shard %d (device %d): %s", s, g->dev[s], tfp_engine_last_error(g->eng[s]));
+}
+
+int run_all(tfp_group* g, const std::function<int(int)>& f) {
+  int bad = 0;
+  const int rc = g->pool->run(f, &bad);
+  return rc ? shard_fail(g, rc, bad) : TFP_OK;
+}
+
+// Group-wide uuid ranks as every engine's tie-break keys (before any search after a change).
+int refresh_ranks(tfp_group* g) {
+  if (!g->ranks_dirty) return TFP_OK;
+  const int n = (int)g->eng.size();
+  std::vector<std::vector<int32_t>> keys(n);
+  for (int s = 0; s < n; s++) keys[s].assign(std::max<size_t>(g->id2member[s].size(), 1), -1);
+  g->member_rank.assign(g->members.size(), -1);
+  for (size_t r = 0; r < g->by_uuid.size(); r++) {
+    const Member& m = g->members[g->by_uuid[r]];
+    keys[m.shard][m.id] = (int32_t)r;
+    g->member_rank[g->by_uuid[r]] = (int32_t)r;
+  }
+  const int rc = run_all(g, [&](int s) {
+    return tfp_index_set_tiebreak(g->eng[s], keys[s].data(), (int32_t)g->id2member[s].size());
+  });
+  if (rc) return rc;
+  g->ranks_dirty = false;
+  return TFP_OK;
+}
+
+bool uuid_less(const tfp_group* g, int32_t a, int32_t b) { return g->members[a].uuid < g->members[b].uuid; }
+
+void insert_live(tfp_group* g, int32_t mi) {
+  auto it = std::lower_bound(g->by_uuid.begin(), g->by_uuid.end(), mi,
+                             [&](int32_t a, int32_t b) { return uuid_less(g, a, b); });
+  g->by_uuid.insert(it, mi);
+  g->ranks_dirty = true;
+}
+
+void erase_live(tfp_group* g, int32_t mi) {
+  auto it = std::lower_bound(g->by_uuid.begin(), g->by_uuid.end(), mi,
+                             [&](int32_t a, int32_t b) { return uuid_less(g, a, b); });
+  if (it != g->by_uuid.end() && *it == mi) g->by_uuid.erase(it);
+  g->ranks_dirty = true;
+}
+
+int32_t lightest(const tfp_group* g) {
+  return (int32_t)(std::min_element(g->rows.begin(), g->rows.end()) - g->rows.begin());
+}
+
+// A shard's result -> its key (count << 32 | global rank); 0 = no hit.
+unsigned long long key_of(const tfp_group* g, int s, const tfp_result& r) {
+  if (!r.found || r.clip_id < 0 || (size_t)r.clip_id >= g->id2member[s].size()) return 0ull;
+  const int32_t mi = g->id2member[s][r.clip_id];
+  if (mi < 0 || g->member_rank[mi] < 0) return 0ull;
+  return ((unsigned long long)(uint32_t)r.match_count << 32) | (uint32_t)g->member_rank[mi];
+}
+
+// Per query, the greatest key over the shards' results -> the group's result.
+void combine(tfp_group* g, const std::vector<std::vector<tfp_result>>& res, int32_t nq, tfp_result* out) {
+  for (int32_t i = 0; i < nq; i++) {
+    int best_s = -1;
+    unsigned long long best = 0ull;
+    for (size_t s = 0; s < res.size(); s++) {
+      const unsigned long long k = key_of(g, (int)s, res[s][i]);
+      if (k > best) best = k, best_s = (int)s;
+    }
+    out[i] = best_s >= 0 ? res[best_s][i] : res[0][i];
+    if (best_s >= 0) out[i].clip_id = best_s;  // the shard holding the winner
+    else out[i].found = 0, out[i].match_count = 0, out[i].clip_id = -1, out[i].uuid[0] = 0;
+  }
+}
+
+// Global key -> result (uuid, count) for the query-sharded path.
+void fill_from_key(const tfp_group* g, unsigned long long k, int32_t frame_count, tfp_result* r) {
+  memset(r, 0, sizeof *r);
+  r->frame_count = frame_count;
+  r->clip_id = -1;
+  const uint32_t rank = (uint32_t)(k & 0xffffffffu);
+  if (!k || rank >= g->by_uuid.size()) return;
+  const Member& m = g->members[g->by_uuid[rank]];
+  r->found = 1;
+  r->match_count = (int32_t)(k >> 32);
+  r->clip_id = m.shard;
+  snprintf(r->uuid, sizeof r->uuid, "%s", m.uuid.c_str());
+}
+
+bool valid_params(const tfp_search_params* P) { return P && P->coefs >= 1 && P->coefs <= 2; }
+
+int add_members(tfp_group* g, int32_t s, int32_t n, const char* const* uuids) {
+  // the engine assigns clip ids in order of addition (tfp_index_add / _add_batch)
+  for (int32_t c = 0; c < n; c++) {
+    const int32_t mi = (int32_t)g->members.size();
+    g->members.push_back(Member{uuids[c], s, (int32_t)g->id2member[s].size()});
+    g->id2member[s].push_back(mi);
+    g->where[uuids[c]] = mi;
+    insert_live(g, mi);
+  }
+  return TFP_OK;
+}
+
+// Query-sharded batch over host int16 PCM of equal-length queries: shard s fingerprints its share,
+// the frame values are exchanged, every shard searches the whole batch.
+int search_sharded(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nq, int32_t sr,
+                   const tfp_search_params* P, tfp_result* out) {
+  const int n = (int)g->eng.size();
+  const int64_t qn = offsets[1] - offsets[0];
+  const int64_t nfq = tfp_frame_count(qn), nf = nfq * nq;
+  std::vector<int32_t> share(n + 1);
+  for (int s = 0; s <= n; s++) share[s] = (int32_t)(((int64_t)nq * s) / n);
+  std::vector<int64_t> qoff(nq + 1);
+  for (int32_t i = 0; i <= nq; i++) qoff[i] = nfq * i;
+  std::vector<std::vector<unsigned long long>> keys(n, std::vector<unsigned long long>(nq));
+  // 1: each shard fingerprints its queries into its part of its own q buffer
+  int rc = run_all(g, [&](int s) -> int {
+    ShardBufs& b = g->bufs[s];
+    if (hipSetDevice(g->dev[s]) != hipSuccess) return TFP_E_HIP;
+    if (!b.stream && hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking) != hipSuccess) return TFP_E_HIP;
+    if (!b.fp_done && hipEventCreateWithFlags(&b.fp_done, hipEventDisableTiming) != hipSuccess) return TFP_E_HIP;
+    const int32_t k = share[s + 1] - share[s];
+    if (grow(&b.pcm, &b.b_pcm, sizeof(int16_t) * (size_t)(k * qn + 1)) != hipSuccess ||
+        grow(&b.micro, &b.b_micro, sizeof(int32_t) * 2 * (size_t)(k * nfq + 1)) != hipSuccess ||
+        grow(&b.q, &b.b_q, sizeof(double) * 2 * (size_t)(nf + 1)) != hipSuccess ||
+        grow(&b.keys, &b.b_keys, sizeof(unsigned long long) * (size_t)(nq + 1)) != hipSuccess)
+      return TFP_E_NOMEM;
+    if (!k) return hipEventRecord(b.fp_done, b.stream) == hipSuccess ? TFP_OK : TFP_E_HIP;
+    if (hipMemcpyAsync(b.pcm, pcm + offsets[share[s]] - offsets[0], sizeof(int16_t) * (size_t)(k * qn),
+                       hipMemcpyHostToDevice, b.stream) != hipSuccess)
+      return TFP_E_HIP;
+    if (!b.plan || b.plan_k != k || b.plan_qn != qn || b.plan_sr != sr) {
+      std::vector<int64_t> off(k + 1);
+      for (int32_t i = 0; i <= k; i++) off[i] = qn * i;
+      tfp_plan_destroy(b.plan);
+      b.plan = nullptr;
+      const int r = tfp_plan_create(g->eng[s], off.data(), k, sr, &b.plan);
+      if (r) return r;
+      b.plan_k = k, b.plan_qn = qn, b.plan_sr = sr;
+    }
+    const int r = tfp_fingerprint_device(g->eng[s], b.plan, (const int16_t*)b.pcm, (int32_t*)b.micro,
+                                         (double*)b.q + 2 * nfq * share[s], b.stream);
+    if (r) return r;
+    if (hipEventRecord(b.fp_done, b.stream) != hipSuccess || hipStreamSynchronize(b.stream) != hipSuccess)
+      return TFP_E_HIP;
+    return TFP_OK;
+  });
+  if (rc) return rc;
+  // 2: every shard pulls the other shards' frame values, searches the batch, keys to the host
+  rc = run_all(g, [&](int s) -> int {
+    ShardBufs& b = g->bufs[s];
+    if (hipSetDevice(g->dev[s]) != hipSuccess) return TFP_E_HIP;
+    for (int o = 0; o < n; o++) {
+      const int32_t k = share[o + 1] - share[o];
+      if (o == s || !k) continue;
+      const size_t off = sizeof(double) * 2 * (size_t)(nfq * share[o]), bytes = sizeof(double) * 2 * (size_t)(nfq * k);
+      if (hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], (const char*)g->bufs[o].q + off, g->dev[o], bytes, b.stream) !=
+          hipSuccess)
+        return TFP_E_HIP;
+    }
+    int r = tfp_search_q_device(g->eng[s], (const double*)b.q, qoff.data(), nq, P, (uint64_t*)b.keys, b.stream);
+    if (r) return r;
+    if (hipMemcpyAsync(keys[s].data(), b.keys, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, b.stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(b.stream) != hipSuccess)
+      return TFP_E_HIP;
+    return TFP_OK;
+  });
+  if (rc) return rc;
+  for (int32_t i = 0; i < nq; i++) {
+    unsigned long long k = 0ull;
+    for (int s = 0; s < n; s++) k = std::max(k, keys[s][i]);
+    fill_from_key(g, k, (int32_t)nfq, &out[i]);
+  }
+  return TFP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tfp_group_create(const int32_t* devices, int32_t n, tfp_group** out) {
+  if (!devices || n <= 0 || !out) return TFP_E_ARG;
+  *out = nullptr;
+  tfp_group* g = new tfp_group();
+  for (int32_t s = 0; s < n; s++) {
+    tfp_engine* e = nullptr;
+    const int rc = tfp_engine_create(devices[s], &e);
+    if (rc) {
+      delete g;
+      return rc;
+    }
+    g->eng.push_back(e);
+    g->dev.push_back(devices[s]);
+  }
+  // peer access between the distinct devices (xGMI), for the query-sharded batches
+  for (int32_t a = 0; a < n; a++)
+    for (int32_t b = 0; b < n; b++) {
+      int can = 0;
+      if (devices[a] != devices[b] && hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can &&
+          hipSetDevice(devices[a]) == hipSuccess) {
+        const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
+        if (e != hipSuccess) (void)hipGetLastError();  // (already enabled: fine; else copies stage through the host)
+      }
+    }
+  g->id2member.assign(n, {});
+  g->rows.assign(n, 0);
+  g->bufs.resize(n);
+  g->pool = new ShardPool(n);
+  *out = g;
+  return TFP_OK;
+}
+
+void tfp_group_destroy(tfp_group* g) { delete g; }
+
+int32_t tfp_group_size(const tfp_group* g) { return g ? (int32_t)g->eng.size() : 0; }
+
+const char* tfp_group_last_error(const tfp_group* g) { return g ? g->err.c_str() : ""; }
+
+tfp_engine* tfp_group_engine(tfp_group* g, int32_t shard) {
+  return g && shard >= 0 && shard < (int32_t)g->eng.size() ? g->eng[shard] : nullptr;
+}
+
+namespace {
+int group_fingerprint(tfp_group* g, const void* x, bool f32, const int64_t* offsets, int32_t nclips, int32_t sr,
+                      tfp_frame* out, int64_t cap, int64_t* nframes) {
+  if (!g || !offsets || nclips < 0 || !nframes) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  const int n = (int)g->eng.size();
+  std::vector<int64_t> foff(nclips + 1, 0);
+  for (int32_t c = 0; c < nclips; c++) {
+    if (offsets[c + 1] < offsets[c]) return gfail(g, TFP_E_ARG, "offsets not monotone");
+    foff[c + 1] = foff[c] + tfp_frame_count(offsets[c + 1] - offsets[c]);
+  }
+  *nframes = foff[nclips];
+  if (foff[nclips] > 0 && (!out || cap < foff[nclips])) return gfail(g, TFP_E_CAPACITY, "need %lld frames", (long long)foff[nclips]);
+  if (!foff[nclips]) return TFP_OK;
+  // contiguous clip ranges with about equal frames per shard
+  std::vector<int32_t> cut(n + 1, nclips);
+  cut[0] = 0;
+  for (int s = 1; s < n; s++)
+    cut[s] = (int32_t)(std::lower_bound(foff.begin(), foff.end(), foff[nclips] * s / n) - foff.begin());
+  for (int s = 1; s <= n; s++) cut[s] = std::max(cut[s], cut[s - 1]);
+  return run_all(g, [&](int s) -> int {
+    const int32_t a = cut[s], b = cut[s + 1];
+    if (a >= b) return TFP_OK;
+    int64_t got = 0;
+    return f32 ? tfp_fingerprint_f32_batch(g->eng[s], (const float*)x, offsets + a, b - a, sr, out + foff[a],
+                                           foff[b] - foff[a], &got)
+               : tfp_fingerprint_batch(g->eng[s], (const int16_t*)x, offsets + a, b - a, sr, out + foff[a],
+                                       foff[b] - foff[a], &got);
+  });
+}
+}  // namespace
+
+int tfp_group_fingerprint_batch(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nclips, int32_t sr,
+                                tfp_frame* out, int64_t cap, int64_t* nframes) {
+  return group_fingerprint(g, pcm, false, offsets, nclips, sr, out, cap, nframes);
+}
+
+int tfp_group_fingerprint_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nclips, int32_t sr,
+                                    tfp_frame* out, int64_t cap, int64_t* nframes) {
+  return group_fingerprint(g, x, true, offsets, nclips, sr, out, cap, nframes);
+}
+
+int tfp_group_index_add(tfp_group* g, const char* uuid, const int32_t* m1, const int32_t* m2, int32_t nframes) {
+  if (!g) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  if (!uuid || g->where.count(uuid)) return gfail(g, uuid ? TFP_E_EXISTS : TFP_E_ARG, "uuid %s already indexed", uuid ? uuid : "(null)");
+  const int32_t s = lightest(g);
+  int32_t id = -1;
+  const int rc = tfp_index_add(g->eng[s], uuid, m1, m2, nframes, &id);
+  if (rc) return shard_fail(g, rc, s);
+  if (id != (int32_t)g->id2member[s].size()) return gfail(g, TFP_E_HIP, "shard %d clip id %d out of step", s, id);
+  g->rows[s] += nframes;
+  return add_members(g, s, 1, &uuid);
+}
+
+int tfp_group_index_add_batch(tfp_group* g, int32_t nclips, const char* const* uuids, const int64_t* foff,
+                              const int32_t* m1, const int32_t* m2) {
+  if (!g || nclips < 0 || !uuids || !foff) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  const int n = (int)g->eng.size();
+  std::unordered_map<std::string, int> seen;
+  for (int32_t c = 0; c < nclips; c++) {
+    if (!uuids[c] || !*uuids[c] || strlen(uuids[c]) >= 64) return gfail(g, TFP_E_ARG, "bad uuid %d", c);
+    if (foff[c + 1] < foff[c]) return gfail(g, TFP_E_ARG, "frame_offsets not monotone at %d", c);
+    if (g->where.count(uuids[c]) || !seen.emplace(uuids[c], c).second)
+      return gfail(g, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
+  }
+  // each clip to the shard with the fewest rows so far; per shard one tfp_index_add_batch
+  std::vector<std::vector<int32_t>> pick(n);
+  std::vector<int64_t> rows = g->rows;
+  for (int32_t c = 0; c < nclips; c++) {
+    const int32_t s = (int32_t)(std::min_element(rows.begin(), rows.end()) - rows.begin());
+    pick[s].push_back(c);
+    rows[s] += foff[c + 1] - foff[c];
+  }
+  std::vector<std::vector<const char*>> uu(n);
+  std::vector<std::vector<int64_t>> fo(n);
+  std::vector<std::vector<int32_t>> a1(n), a2(n);
+  for (int s = 0; s < n; s++) {
+    fo[s].push_back(0);
+    for (int32_t c : pick[s]) {
+      uu[s].push_back(uuids[c]);
+      a1[s].insert(a1[s].end(), m1 + foff[c], m1 + foff[c + 1]);
+      a2[s].insert(a2[s].end(), m2 + foff[c], m2 + foff[c + 1]);
+      fo[s].push_back((int64_t)a1[s].size());
+    }
+  }
+  std::vector<int> rcs(n, TFP_OK);
+  const int rc = run_all(g, [&](int s) -> int {
+    if (uu[s].empty()) return TFP_OK;
+    return rcs[s] = tfp_index_add_batch(g->eng[s], (int32_t)uu[s].size(), uu[s].data(), fo[s].data(), a1[s].data(),
+                                        a2[s].data());
+  });
+  // (arguments were checked above, so a shard fails only on a device error; the shards that
+  // succeeded keep their clips, as the engine's own add_batch is all-or-nothing per call)
+  for (int s = 0; s < n; s++)
+    if (!uu[s].empty() && rcs[s] == TFP_OK) {
+      add_members(g, s, (int32_t)uu[s].size(), uu[s].data());
+      g->rows[s] += fo[s].back();
+    }
+  return rc;
+}
+
+int tfp_group_index_remove(tfp_group* g, const char* uuid) {
+  if (!g || !uuid) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  auto it = g->where.find(uuid);
+  if (it == g->where.end()) return gfail(g, TFP_E_NOENT, "uuid %s not indexed", uuid);
+  const int32_t mi = it->second;
+  Member& m = g->members[mi];
+  int64_t nr = 0;
+  (void)tfp_index_rows(g->eng[m.shard], uuid, nullptr, nullptr, 0, &nr);
+  const int rc = tfp_index_remove(g->eng[m.shard], uuid);
+  if (rc) return shard_fail(g, rc, m.shard);
+  erase_live(g, mi);
+  g->rows[m.shard] -= nr;
+  g->id2member[m.shard][m.id] = -1;
+  g->where.erase(it);
+  m.uuid.clear();
+  return TFP_OK;
+}
+
+int tfp_group_index_clear(tfp_group* g) {
+  if (!g) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  const int rc = run_all(g, [&](int s) { return tfp_index_clear(g->eng[s]); });
+  g->where.clear();
+  g->members.clear();
+  g->by_uuid.clear();
+  for (auto& v : g->id2member) v.clear();
+  std::fill(g->rows.begin(), g->rows.end(), 0);
+  g->ranks_dirty = true;
+  return rc;
+}
+
+int tfp_group_index_rows(tfp_group* g, const char* uuid, int32_t* m1, int32_t* m2, int64_t cap, int64_t* nframes) {
+  if (!g || !uuid) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  auto it = g->where.find(uuid);
+  if (it == g->where.end()) return gfail(g, TFP_E_NOENT, "uuid %s not indexed", uuid);
+  const int s = g->members[it->second].shard;
+  const int rc = tfp_index_rows(g->eng[s], uuid, m1, m2, cap, nframes);
+  return rc ? shard_fail(g, rc, s) : TFP_OK;
+}
+
+int tfp_group_index_stats(tfp_group* g, int64_t* nrows, int32_t* nclips) {
+  if (!g) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  int64_t r = 0;
+  int32_t c = 0;
+  for (auto* e : g->eng) {
+    int64_t a = 0;
+    int32_t b = 0;
+    const int rc = tfp_index_stats(e, &a, &b);
+    if (rc) return rc;
+    r += a;
+    c += b;
+  }
+  if (nrows) *nrows = r;
+  if (nclips) *nclips = c;
+  return TFP_OK;
+}
+
+int tfp_group_index_commit(tfp_group* g) {
+  if (!g) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  int rc = refresh_ranks(g);
+  if (rc) return rc;
+  return run_all(g, [&](int s) { return tfp_index_commit(g->eng[s]); });
+}
+
+int tfp_group_search_batch(tfp_group* g, const tfp_frame* frames, const int64_t* qoff, int32_t nq,
+                           const tfp_search_params* P, tfp_result* out) {
+  if (!g || !qoff || nq < 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  int rc = refresh_ranks(g);
+  if (rc) return rc;
+  const int n = (int)g->eng.size();
+  std::vector<std::vector<tfp_result>> res(n, std::vector<tfp_result>(std::max(nq, 1)));
+  rc = run_all(g, [&](int s) { return tfp_search_batch(g->eng[s], frames, qoff, nq, P, res[s].data()); });
+  if (rc) return rc;
+  combine(g, res, nq, out);
+  return TFP_OK;
+}
+
+namespace {
+int group_search_samples(tfp_group* g, const void* x, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
+                         const tfp_search_params* P, tfp_result* out) {
+  if (!g || !offsets || nq < 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  int rc = refresh_ranks(g);
+  if (rc) return rc;
+  const int n = (int)g->eng.size();
+  // throughput batches of equal-length int16 queries: query-sharded (fingerprint once, exchange)
+  bool equal = nq > 0;
+  for (int32_t i = 0; i < nq && equal; i++) equal = offsets[i + 1] - offsets[i] == offsets[1] - offsets[0];
+  if (!f32 && n > 1 && equal && nq >= 64 * n && offsets[1] > offsets[0] && valid_params(P) && x)
+    return search_sharded(g, (const int16_t*)x, offsets, nq, sr, P, out);
+  std::vector<std::vector<tfp_result>> res(n, std::vector<tfp_result>(std::max(nq, 1)));
+  rc = run_all(g, [&](int s) {
+    return f32 ? tfp_search_f32_batch(g->eng[s], (const float*)x, offsets, nq, sr, P, res[s].data())
+               : tfp_search_pcm_batch(g->eng[s], (const int16_t*)x, offsets, nq, sr, P, res[s].data());
+  });
+  if (rc) return rc;
+  combine(g, res, nq, out);
+  return TFP_OK;
+}
+}  // namespace
+
+int tfp_group_search_pcm_batch(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nq, int32_t sr,
+                               const tfp_search_params* P, tfp_result* out) {
+  return group_search_samples(g, pcm, false, offsets, nq, sr, P, out);
+}
+
+int tfp_group_search_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nq, int32_t sr,
+                               const tfp_search_params* P, tfp_result* out) {
+  return group_search_samples(g, x, true, offsets, nq, sr, P, out);
+}
+
+int tfp_group_stream_create(tfp_group* g, int32_t nch, int32_t sr, int64_t W, tfp_group_stream** out) {
+  if (!g || nch <= 0 || W <= 0 || !out) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  *out = nullptr;
+  tfp_group_stream* st = new tfp_group_stream();
+  st->g = g;
+  st->nch = nch;
+  st->st.assign(g->eng.size(), nullptr);
+  const int rc = run_all(g, [&](int s) { return tfp_stream_create(g->eng[s], nch, sr, W, &st->st[s]); });
+  if (rc) {
+    for (auto* p : st->st) tfp_stream_destroy(p);
+    delete st;
+    return rc;
+  }
+  st->res.assign(g->eng.size(), std::vector<tfp_result>(nch));
+  *out = st;
+  return TFP_OK;
+}
+
+void tfp_group_stream_destroy(tfp_group_stream* st) {
+  if (!st) return;
+  for (auto* p : st->st) tfp_stream_destroy(p);
+  delete st;
+}
+
+int tfp_group_stream_reset(tfp_group_stream* st, int32_t ch) {
+  if (!st || ch >= st->nch) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(st->g->mu);
+  return run_all(st->g, [&](int s) { return tfp_stream_reset(st->st[s], ch); });
+}
+
+int tfp_group_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t tick, const tfp_search_params* P,
+                          tfp_result* out) {
+  if (!st || !pcm || tick <= 0 || (P && !out)) return TFP_E_ARG;
+  tfp_group* g = st->g;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  int rc = P ? refresh_ranks(g) : TFP_OK;
+  if (rc) return rc;
+  rc = run_all(g, [&](int s) { return tfp_stream_push(st->st[s], pcm, tick, P, P ? st->res[s].data() : nullptr); });
+  if (rc || !P) return rc;
+  combine(g, st->res, st->nch, out);
+  return TFP_OK;
+}
+
+}  // extern "C"

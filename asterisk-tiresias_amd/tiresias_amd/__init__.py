@@ -4,5 +4,6 @@ The compute lives in lib/libtiresias_fp.so (HIP, gfx950) behind include/tiresias
 this package is its ctypes binding plus a mirror of the reference's fp_handler interface.
 """
 from ._lib import LIB_PATH, NULL_MICRO, TfpError, header_symbols, lib  # noqa: F401
-from .engine import FRAME_DTYPE, Engine, Plan, Stream, device_count, frame_count, params, synth_pcm  # noqa: F401
+from .engine import (FRAME_DTYPE, Engine, Group, GroupStream, Plan, Stream, device_count, frame_count,  # noqa: F401
+                     params, synth_pcm)
 from .fp_handler import FpHandler  # noqa: F401

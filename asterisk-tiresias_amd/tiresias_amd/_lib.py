@@ -89,6 +89,27 @@ _SIGS = {
     "tfp_synth_pcm": (C.c_int, [P, C.c_int32, C.c_int64, P]),
     "tfp_synth_pcm_device": (C.c_int, [P, P, C.c_int32, C.c_int64, P, P]),
     "tfp_synchronize": (C.c_int, [P, P]),
+    "tfp_group_create": (C.c_int, [P, C.c_int32, C.POINTER(P)]),
+    "tfp_group_destroy": (None, [P]),
+    "tfp_group_size": (C.c_int32, [P]),
+    "tfp_group_last_error": (C.c_char_p, [P]),
+    "tfp_group_engine": (P, [P, C.c_int32]),
+    "tfp_group_fingerprint_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
+    "tfp_group_fingerprint_f32_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),
+    "tfp_group_index_add": (C.c_int, [P, C.c_char_p, P, P, C.c_int32]),
+    "tfp_group_index_add_batch": (C.c_int, [P, C.c_int32, C.POINTER(C.c_char_p), P, P, P]),
+    "tfp_group_index_remove": (C.c_int, [P, C.c_char_p]),
+    "tfp_group_index_clear": (C.c_int, [P]),
+    "tfp_group_index_rows": (C.c_int, [P, C.c_char_p, P, P, C.c_int64, C.POINTER(C.c_int64)]),
+    "tfp_group_index_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "tfp_group_index_commit": (C.c_int, [P]),
+    "tfp_group_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_group_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_group_search_f32_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_group_stream_create": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]),
+    "tfp_group_stream_destroy": (None, [P]),
+    "tfp_group_stream_reset": (C.c_int, [P, C.c_int32]),
+    "tfp_group_stream_push": (C.c_int, [P, P, C.c_int32, C.POINTER(SearchParams), P]),
 }
 
 _lib = None

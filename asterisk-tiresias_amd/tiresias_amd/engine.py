@@ -334,3 +334,164 @@ class Plan:
         if self._h:
             lib().tfp_plan_destroy(self._h)
             self._h = C.c_void_p()
+
+
+class Group:
+    """tfp_group: one engine per listed device (a device may repeat), the enrolled clips sharded
+    over them, searches combined on the host (tiresias_fp.h, device groups)."""
+
+    def __init__(self, devices):
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        self._h = C.c_void_p()
+        rc = lib().tfp_group_create(devs, len(devices), C.byref(self._h))
+        if rc != 0:
+            raise TfpError(rc, f"cannot create a group on devices {list(devices)}")
+        self.devices = list(devices)
+        self._streams = weakref.WeakSet()
+
+    def close(self):
+        if self._h:
+            for st in list(self._streams):
+                st.close()
+            lib().tfp_group_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise TfpError(rc, lib().tfp_group_last_error(self._h).decode())
+        return rc
+
+    def size(self) -> int:
+        return int(lib().tfp_group_size(self._h))
+
+    def engine_stats(self):
+        """[(rows, clips)] of every shard's engine."""
+        out = []
+        for s in range(self.size()):
+            r, c = C.c_int64(), C.c_int32()
+            check(lib().tfp_index_stats(lib().tfp_group_engine(self._h, s), C.byref(r), C.byref(c)))
+            out.append((r.value, c.value))
+        return out
+
+    def fingerprint_batch(self, pcm, offsets, sample_rate: int = 8000) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nclips = len(offsets) - 1
+        n = sum(frame_count(int(offsets[i + 1] - offsets[i])) for i in range(nclips))
+        out = np.zeros(max(n, 1), FRAME_DTYPE)
+        got = C.c_int64()
+        self._chk(lib().tfp_group_fingerprint_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nclips, sample_rate,
+                                                    out.ctypes.data, n, C.byref(got)))
+        return out[:n]
+
+    def index_add(self, uuid: str, m1, m2):
+        m1 = np.ascontiguousarray(m1, np.int32)
+        m2 = np.ascontiguousarray(m2, np.int32)
+        self._chk(lib().tfp_group_index_add(self._h, uuid.encode(), m1.ctypes.data, m2.ctypes.data, len(m1)))
+
+    def index_add_batch(self, uuids, frame_offsets, m1, m2):
+        frame_offsets = np.ascontiguousarray(frame_offsets, np.int64)
+        m1 = np.ascontiguousarray(m1, np.int32)
+        m2 = np.ascontiguousarray(m2, np.int32)
+        arr = (C.c_char_p * max(1, len(uuids)))(*[u.encode() for u in uuids])
+        self._chk(lib().tfp_group_index_add_batch(self._h, len(uuids), arr, frame_offsets.ctypes.data, m1.ctypes.data,
+                                                  m2.ctypes.data))
+
+    def index_remove(self, uuid: str):
+        self._chk(lib().tfp_group_index_remove(self._h, uuid.encode()))
+
+    def index_clear(self):
+        self._chk(lib().tfp_group_index_clear(self._h))
+
+    def index_rows(self, uuid: str):
+        n = C.c_int64()
+        rc = lib().tfp_group_index_rows(self._h, uuid.encode(), None, None, 0, C.byref(n))
+        if rc not in (0, -5):
+            self._chk(rc)
+        m1 = np.zeros(max(n.value, 1), np.int32)
+        m2 = np.zeros(max(n.value, 1), np.int32)
+        self._chk(lib().tfp_group_index_rows(self._h, uuid.encode(), m1.ctypes.data, m2.ctypes.data, n.value,
+                                             C.byref(n)))
+        return m1[:n.value], m2[:n.value]
+
+    def index_stats(self):
+        r, c = C.c_int64(), C.c_int32()
+        self._chk(lib().tfp_group_index_stats(self._h, C.byref(r), C.byref(c)))
+        return r.value, c.value
+
+    def index_commit(self):
+        self._chk(lib().tfp_group_index_commit(self._h))
+
+    def search_batch(self, frames: np.ndarray, qoffsets, p: SearchParams):
+        frames = np.ascontiguousarray(frames, FRAME_DTYPE)
+        qoffsets = np.ascontiguousarray(qoffsets, np.int64)
+        nq = len(qoffsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_group_search_batch(self._h, frames.ctypes.data, qoffsets.ctypes.data, nq, C.byref(p), res))
+        return Engine._results(res, nq)
+
+    def search_pcm_batch(self, pcm, offsets, p: SearchParams, sample_rate: int = 8000):
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nq = len(offsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_group_search_pcm_batch(self._h, pcm.ctypes.data, offsets.ctypes.data, nq, sample_rate,
+                                                   C.byref(p), res))
+        return Engine._results(res, nq)
+
+    def search_f32_batch(self, x, offsets, p: SearchParams, sample_rate: int = 8000):
+        x = np.ascontiguousarray(x, np.float32)
+        offsets = np.ascontiguousarray(offsets, np.int64)
+        nq = len(offsets) - 1
+        res = (Result * max(1, nq))()
+        self._chk(lib().tfp_group_search_f32_batch(self._h, x.ctypes.data, offsets.ctypes.data, nq, sample_rate,
+                                                   C.byref(p), res))
+        return Engine._results(res, nq)
+
+
+class GroupStream:
+    """tfp_group_stream: live channels matched against every shard of a Group."""
+
+    def __init__(self, g: Group, nchannels: int, window_samples: int, sample_rate: int = 8000):
+        self._g = g
+        self._h = C.c_void_p()
+        g._chk(lib().tfp_group_stream_create(g.handle, int(nchannels), int(sample_rate), int(window_samples),
+                                             C.byref(self._h)))
+        self.nchannels = nchannels
+        self._res = (Result * nchannels)()
+        g._streams.add(self)
+
+    def reset(self, channel: int = -1):
+        self._g._chk(lib().tfp_group_stream_reset(self._h, int(channel)))
+
+    def push(self, pcm: np.ndarray, p: SearchParams = None):
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        assert pcm.shape[0] == self.nchannels
+        self._g._chk(lib().tfp_group_stream_push(self._h, pcm.ctypes.data, pcm.shape[1],
+                                                 C.byref(p) if p is not None else None,
+                                                 self._res if p is not None else None))
+        if p is None:
+            return None
+        return [None if not r.found else {"audio_uuid": r.uuid.decode(), "match_count": r.match_count,
+                                          "frame_count": r.frame_count} for r in self._res]
+
+    def close(self):
+        if self._h and self._g._h:
+            lib().tfp_group_stream_destroy(self._h)
+        self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -233,6 +233,54 @@ int tfp_stream_reset(tfp_stream* st, int32_t channel);
 int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t tick_samples, const tfp_search_params* params,
                     tfp_result* out);
 
+/* ---- device groups: the node's GPUs behind one index (new in round 3) -------------------
+ * The module's enrolled DB sharded over one engine per listed device (the reference
+ * has one SQLite DB, fp_handler.c:30): each clip lives on one engine (the one holding the fewest
+ * rows when it is added) and is never split, since the per-frame GROUP BY audio_uuid of
+ * fp_handler.c:353 is not additive over a split clip. Every search runs on all engines in parallel
+ * (a worker thread per engine); the engines carry the group-wide uuid ranks as tie-break keys, so
+ * the per-query key (match_count << 32 | rank) of each shard combines by an integer max into the
+ * reference's winner (count(*) DESC, ties to the greatest audio_uuid, fp_handler.c:367-374).
+ * Batches of >= 64 equal-length int16 queries per engine are query-sharded: each engine
+ * fingerprints its share and the frame values are exchanged GPU to GPU (peer copies over xGMI);
+ * smaller batches and stream ticks are fingerprinted by every engine, so the latency path has no
+ * exchange. A device may be listed more than once (shards sharing a GPU). Results as the engine
+ * calls, except tfp_result.clip_id = the index of the engine holding the winner. Thread-safe
+ * (calls are serialised per group); errors through tfp_group_last_error. */
+typedef struct tfp_group tfp_group;
+int tfp_group_create(const int32_t* devices, int32_t ndevices, tfp_group** out);
+void tfp_group_destroy(tfp_group* g); /* destroy its streams first */
+int32_t tfp_group_size(const tfp_group* g);
+const char* tfp_group_last_error(const tfp_group* g);
+tfp_engine* tfp_group_engine(tfp_group* g, int32_t shard); /* for stats; do not change its index */
+int tfp_group_fingerprint_batch(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nclips,
+                                int32_t sample_rate, tfp_frame* out, int64_t cap, int64_t* nframes);
+int tfp_group_fingerprint_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nclips,
+                                    int32_t sample_rate, tfp_frame* out, int64_t cap, int64_t* nframes);
+int tfp_group_index_add(tfp_group* g, const char* uuid, const int32_t* m1, const int32_t* m2, int32_t nframes);
+int tfp_group_index_add_batch(tfp_group* g, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
+                              const int32_t* m1, const int32_t* m2);
+int tfp_group_index_remove(tfp_group* g, const char* uuid);
+int tfp_group_index_clear(tfp_group* g);
+int tfp_group_index_rows(tfp_group* g, const char* uuid, int32_t* m1, int32_t* m2, int64_t cap, int64_t* nframes);
+int tfp_group_index_stats(tfp_group* g, int64_t* nrows, int32_t* nclips);
+int tfp_group_index_commit(tfp_group* g);
+int tfp_group_search_batch(tfp_group* g, const tfp_frame* frames, const int64_t* qoffsets, int32_t nqueries,
+                           const tfp_search_params* params, tfp_result* out);
+int tfp_group_search_pcm_batch(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nqueries,
+                               int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+int tfp_group_search_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nqueries,
+                               int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+/* Live channels on a group: every engine keeps every channel's window and matches it against its
+ * clips each tick; out[nchannels] = the combined results (as tfp_stream_push). */
+typedef struct tfp_group_stream tfp_group_stream;
+int tfp_group_stream_create(tfp_group* g, int32_t nchannels, int32_t sample_rate, int64_t window_samples,
+                            tfp_group_stream** out);
+void tfp_group_stream_destroy(tfp_group_stream* st);
+int tfp_group_stream_reset(tfp_group_stream* st, int32_t channel);
+int tfp_group_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t tick_samples,
+                          const tfp_search_params* params, tfp_result* out);
+
 /* ---- deterministic synthetic PCM (benchmark / test data; identical host and device) -- */
 /* One spec per clip: samples s of clip = synth(seed, clip, offset + s). */
 typedef struct tfp_synth_spec {

@@ -1,0 +1,144 @@
+"""Device groups (tfp_group_*, csrc/tfp_group.cpp): the enrolled DB sharded over several engines
+in one process, searched on all of them in parallel and combined on the host.
+
+On this one-GPU box the group is three engines on device 0 (the same code path as three GPUs,
+with device-to-device copies in place of xGMI peer copies). Every search — batch-1 (each shard
+fingerprints the queries), a batch (each shard's vote), a query-sharded batch of >= 64 queries per
+shard (fingerprint shares exchanged between shards) and coefs = 2 — and every stream tick must
+equal the single engine over the same clips and the oracle (count(*) DESC, ties to the greatest
+audio_uuid: src/fp_handler.c:367-374; clip-aligned shards: :353), including ties whose clips sit on
+different shards."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED_DB, SEED_Q = 0x7153A1, 0x7153B2
+HOP = 256
+
+
+def _uuids(rng, n):
+    out = []
+    for _ in range(n):
+        h = "%032x" % int.from_bytes(rng.bytes(16), "little")
+        out.append("%s-%s-4%s-a%s-%s" % (h[:8], h[8:12], h[13:16], h[17:20], h[20:32]))
+    return out
+
+
+def _oracle_search(oracle, live, q1, q2, qoff, p):
+    uu = sorted(live)
+    m1 = np.concatenate([live[u][0] for u in uu])
+    m2 = np.concatenate([live[u][1] for u in uu])
+    clip = np.concatenate([np.full(len(live[u][0]), i, np.int32) for i, u in enumerate(uu)])
+    idx = oracle.SortedIndex(m1, m2, clip, np.arange(len(uu), dtype=np.int32))
+    w, mc = idx.search_batch(q1, q2, qoff, p.coefs, p.tolerance, p.freq_ignore_low, p.freq_ignore_high, nthreads=16)
+    return [(uu[w[i]], int(mc[i])) if w[i] >= 0 else None for i in range(len(qoff) - 1)]
+
+
+def _pairs(res):
+    return [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+
+
+def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
+    rng = np.random.default_rng(8)
+    n, nsrc = 8000 * 10, 200
+    nf = (n + HOP - 1) // HOP
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(nsrc), n)
+    micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(nsrc + 1) * n, nthreads=16, want_db=False)
+    rows = [(micro[c * nf:(c + 1) * nf, 0].copy(), micro[c * nf:(c + 1) * nf, 1].copy()) for c in range(nsrc)]
+    # 230 clips: 0..199 plus copies of 0..29 under other uuids (ties, likely on other shards)
+    src = list(range(nsrc)) + list(range(30))
+    uuids = _uuids(rng, len(src))
+    g = tfp_lib.Group([0, 0, 0])
+    e = tfp_lib.Engine(0)
+    assert g.size() == 3
+    live = {}
+    fo = np.concatenate([[0], np.cumsum([nf] * 180)])
+    for t in (g, e):
+        t.index_add_batch(uuids[:180], fo, np.concatenate([rows[src[c]][0] for c in range(180)]),
+                          np.concatenate([rows[src[c]][1] for c in range(180)]))
+    for c in range(180, len(src)):
+        for t in (g, e):
+            t.index_add(uuids[c], rows[src[c]][0], rows[src[c]][1])
+    for c in range(len(src)):
+        live[uuids[c]] = rows[src[c]]
+    for c in (3, 77, 181):
+        for t in (g, e):
+            t.index_remove(uuids[c])
+        del live[uuids[c]]
+    assert g.index_stats() == e.index_stats() == (len(live) * nf, len(live))
+    per = g.engine_stats()
+    assert sum(r for r, _ in per) == len(live) * nf and max(r for r, _ in per) - min(r for r, _ in per) <= 2 * nf
+    for c in (0, 150, 229):
+        a, b = g.index_rows(uuids[c])
+        assert np.array_equal(a, rows[src[c]][0]) and np.array_equal(b, rows[src[c]][1])
+
+    # fingerprinting split over the shards == one engine
+    off = np.array([0, 5000, 5001, 24000, 24000, 80000, 80255, 160000], np.int64)
+    flat = pcm[:2].reshape(-1)
+    assert np.array_equal(g.fingerprint_batch(flat, off), e.fingerprint_batch(flat, off))
+
+    # queries: 3 s excerpts (several of tied clips) and unrelated audio
+    qn = 8000 * 3
+    nq = 3 * 64  # >= 64 per shard: the query-sharded path
+    qsrc = [int(rng.integers(nsrc)) if i % 4 != 3 else -1 for i in range(nq)]
+    qsrc[:8] = [0, 1, 2, 3, 4, 150, 199, 29]
+    qpcm = np.stack([tfp_lib.synth_pcm(SEED_DB, [c], qn, offsets=[256 * int(rng.integers(0, 150))])[0] if c >= 0
+                     else tfp_lib.synth_pcm(SEED_Q, [i], qn)[0] for i, c in enumerate(qsrc)])
+    _, qdb = oracle.fingerprint_batch(qpcm.reshape(-1), np.arange(nq + 1) * qn, nthreads=16)
+    nfq = (qn + HOP - 1) // HOP
+    qoff = np.arange(nq + 1, dtype=np.int64) * nfq
+    soff = np.arange(nq + 1, dtype=np.int64) * qn
+    frames = np.zeros(len(qdb), tfp_lib.FRAME_DTYPE)
+    frames["q1"], frames["q2"] = qdb[:, 0], qdb[:, 1]
+    found = 0
+    for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05)):
+        exp = _oracle_search(oracle, live, qdb[:, 0], qdb[:, 1], qoff, p)
+        found = max(found, sum(x is not None for x in exp))
+        rs, fcs = g.search_pcm_batch(qpcm.reshape(-1), soff, p)          # query-sharded
+        assert _pairs(rs) == exp and all(f == nfq for f in fcs), (p.coefs, p.tolerance)
+        assert all(r is None or 0 <= r["clip_id"] < 3 for r in rs)
+        assert _pairs(e.search_pcm_batch(qpcm.reshape(-1), soff, p)[0]) == exp
+        rb, _ = g.search_batch(frames[:24 * nfq], qoff[:25], p)           # each shard's batch search
+        assert _pairs(rb) == exp[:24]
+        r1, _ = g.search_pcm_batch(qpcm[:4].reshape(-1), soff[:5], p)     # batch-1 path on every shard
+        assert _pairs(r1) == exp[:4]
+        for i in range(4):
+            r, fc = g.search_pcm_batch(qpcm[i], [0, qn], p)
+            assert _pairs(r) == exp[i:i + 1] and fc[0] == nfq
+    assert found >= 40
+    # ties across shards: a copied clip and its original hold the same rows
+    p = tfp_lib.params(1, 0.3)
+    exp = _oracle_search(oracle, live, qdb[:8 * nfq, 0], qdb[:8 * nfq, 1], qoff[:9], p)
+    tied = [i for i, c in enumerate(qsrc[:8]) if c < 30 and c != 3 and exp[i] is not None]
+    assert tied and all(exp[i][0] == max(uuids[qsrc[i]], uuids[200 + qsrc[i]]) for i in tied)
+
+    # live channels: every tick == the single engine's stream == the oracle on the window
+    nch, W, tick = 12, 24000, 160
+    span = W + 3 * tick
+    chs = [int(rng.integers(nsrc)) for _ in range(nch)]
+    spcm = tfp_lib.synth_pcm(SEED_DB, chs, span, offsets=[256 * int(rng.integers(0, 100)) for _ in range(nch)])
+    spcm[3] = tfp_lib.synth_pcm(SEED_Q + 5, [3], span)[0]
+    gs = tfp_lib.GroupStream(g, nch, W)
+    es = tfp_lib.Stream(e, nch, W)
+    for t in range(W // tick):
+        blk = np.ascontiguousarray(spcm[:, t * tick:(t + 1) * tick])
+        gs.push(blk)
+        es.push(blk)
+    p = tfp_lib.params(1, 0.001)
+    nfw = (W + HOP - 1) // HOP
+    for t in range(3):
+        s0 = W + t * tick
+        blk = np.ascontiguousarray(spcm[:, s0:s0 + tick])
+        rg = gs.push(blk, p)
+        assert rg == es.push(blk, p)
+        _, wdb = oracle.fingerprint_batch(np.ascontiguousarray(spcm[:, s0 + tick - W:s0 + tick]).reshape(-1),
+                                          np.arange(nch + 1) * W, nthreads=16)
+        exp = _oracle_search(oracle, live, wdb[:, 0], wdb[:, 1], np.arange(nch + 1) * nfw, p)
+        assert [None if r is None else (r["audio_uuid"], r["match_count"]) for r in rg] == exp
+    gs.close()
+    es.close()
+    g.index_clear()
+    assert g.index_stats() == (0, 0)
+    g.close()
+    e.close()
