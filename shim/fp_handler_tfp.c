@@ -54,8 +54,8 @@ bool fp_init(void)
 		fpc_db_close();
 		return false;
 	}
-	if(tfp_index_add_batch(g_tfp, rows.nclips, (const char* const*)rows.uuids, rows.frame_offsets, rows.m1, rows.m2)
-			!= TFP_OK || tfp_index_commit(g_tfp) != TFP_OK) {
+	if((rows.nclips > 0 && tfp_index_add_batch(g_tfp, rows.nclips, (const char* const*)rows.uuids, rows.frame_offsets,
+			rows.m1, rows.m2) != TFP_OK) || tfp_index_commit(g_tfp) != TFP_OK) {
 		ast_log(LOG_ERROR, "Could not load the fingerprint index: %s\n", tfp_engine_last_error(g_tfp));
 		fpc_rows_free(&rows);
 		tfp_engine_destroy(g_tfp);

@@ -107,11 +107,17 @@ def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
             r, fc = g.search_pcm_batch(qpcm[i], [0, qn], p)
             assert _pairs(r) == exp[i:i + 1] and fc[0] == nfq
     assert found >= 40
-    # ties across shards: a copied clip and its original hold the same rows
-    p = tfp_lib.params(1, 0.3)
-    exp = _oracle_search(oracle, live, qdb[:8 * nfq, 0], qdb[:8 * nfq, 1], qoff[:9], p)
-    tied = [i for i, c in enumerate(qsrc[:8]) if c < 30 and c != 3 and exp[i] is not None]
-    assert tied and all(exp[i][0] == max(uuids[qsrc[i]], uuids[200 + qsrc[i]]) for i in tied)
+    # ties across shards: a clip and its copy (added later, one at a time: another shard, as a rule)
+    # score alike, so whenever either wins, it must be the greater uuid of the two
+    pairs = 0
+    for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05)):
+        exp = _oracle_search(oracle, live, qdb[:, 0], qdb[:, 1], qoff, p)
+        got = _pairs(g.search_pcm_batch(qpcm.reshape(-1), soff, p)[0])
+        for i, c in enumerate(qsrc):
+            if 0 <= c < 30 and c != 3 and got[i] is not None and got[i][0] in (uuids[c], uuids[200 + c]):
+                assert got[i][0] == max(uuids[c], uuids[200 + c]) and got[i] == exp[i]
+                pairs += 1
+    assert pairs > 0
 
     # live channels: every tick == the single engine's stream == the oracle on the window
     nch, W, tick = 12, 24000, 160
