@@ -1,21 +1,24 @@
 /* fp_handler_tfp.c — the hot half of the reference's engine facade (src/fp_handler.h:13-38) on
- * the MI355X engine (include/tiresias_fp.h). Built into app_tiresias.so in place of the
- * reference's create/search code; the catalog half stays (shim/fp_catalog.h).
+ * the MI355X engines (include/tiresias_fp.h): a device group over the node's GPUs, the enrolled
+ * clips sharded over them. Built into app_tiresias.so with shim/fp_catalog.c (the catalog half:
+ * the reference's SQLite tables and backup) in place of the reference's fp_handler.c and
+ * db_ctx_handler.c.
  *
- *   fp_init / fp_term                fp_handler.c:68-108   + the GPU engine and its index
+ *   fp_init / fp_term                fp_handler.c:68-108   + the GPU engines and their index
  *   fp_craete_audio_list_info        fp_handler.c:161-197  (sic "craete": the reference's name)
- *   fp_delete_audio_list_info        fp_handler.c:115-159  + tfp_index_remove
+ *   fp_delete_audio_list_info        fp_handler.c:115-159  + tfp_group_index_remove
  *   fp_search_fingerprint_info       fp_handler.c:207-408
  *
  * Conventions kept: false / NULL plus ast_log on errors; the search returns NULL both for
  * NOTFOUND and for errors (application_handler.c:180-191 maps both to TIRSTATUS=NOTFOUND);
  * a file already enrolled in the context is a success (fp_handler.c:181-185); the result is
  * {uuid, name, context, hash, frame_count, match_count}, owned by the caller (ast_json_unref).
- * Every tfp_* call is serialised per engine, so the channel threads need no lock here. */
+ * Every tfp_group_* call is serialised per group, so the channel threads need no lock here. */
 #include "asterisk.h"
 
 #include <pthread.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -27,11 +30,57 @@
 #include "fp_handler_tfp.h"
 #include "tiresias_fp.h"
 
-static tfp_engine* g_tfp = NULL; /* one engine (GPU 0) for the module */
+static tfp_group* g_tfp = NULL; /* the module's engines: one per configured GPU (fp_set_gpu_devices) */
+static char g_devices[256] = ""; /* "" : every visible GPU */
 static void pcm_pool_drain(void);
 
+/* fp_set_gpu_devices: "0,2,5", "0-7", or "" / NULL for every visible GPU (a device may repeat) */
+void fp_set_gpu_devices(const char* list)
+{
+	snprintf(g_devices, sizeof(g_devices), "%s", list ? list : "");
+}
+
+static bool create_group(void)
+{
+	int32_t dev[64], n = 0, count = 0, a, b;
+	const char* p = g_devices;
+	char* end;
+
+	if(tfp_device_count(&count) != TFP_OK || count <= 0) {
+		return false;
+	}
+	while(*p != '\0' && n < 64) {
+		if(*p == ',' || *p == ' ') {
+			p++;
+			continue;
+		}
+		a = (int32_t)strtol(p, &end, 10);
+		if(end == p) {
+			return false;
+		}
+		b = a;
+		if(*end == '-') {
+			p = end + 1;
+			b = (int32_t)strtol(p, &end, 10);
+			if(end == p) {
+				return false;
+			}
+		}
+		for(; a <= b && n < 64; a++) {
+			dev[n++] = a;
+		}
+		p = end;
+	}
+	if(n == 0) {
+		for(a = 0; a < count && a < 64; a++) {
+			dev[n++] = a;
+		}
+	}
+	return tfp_group_create(dev, n, &g_tfp) == TFP_OK;
+}
+
 /* fp_init (fp_handler.c:68-90): the catalog (init_database + the backup's tables), the engine, and
- * the GPU index from the restored audio_fingerprint table in one tfp_index_add_batch. A failure
+ * the GPU index from the restored audio_fingerprint table in one tfp_group_index_add_batch. A failure
  * closes whatever was opened, without writing the backup. */
 bool fp_init(void)
 {
@@ -41,24 +90,24 @@ bool fp_init(void)
 		ast_log(LOG_ERROR, "Could not initiate database.\n");
 		return false;
 	}
-	if(tfp_engine_create(0, &g_tfp) != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not create the MI355X fingerprint engine.\n");
+	if(create_group() == false) {
+		ast_log(LOG_ERROR, "Could not create the MI355X fingerprint engines. devices[%s]\n", g_devices);
 		g_tfp = NULL;
 		fpc_db_close();
 		return false;
 	}
 	if(fpc_load_fingerprints(&rows) == false) {
 		ast_log(LOG_ERROR, "Could not load the database data.\n");
-		tfp_engine_destroy(g_tfp);
+		tfp_group_destroy(g_tfp);
 		g_tfp = NULL;
 		fpc_db_close();
 		return false;
 	}
-	if((rows.nclips > 0 && tfp_index_add_batch(g_tfp, rows.nclips, (const char* const*)rows.uuids, rows.frame_offsets,
-			rows.m1, rows.m2) != TFP_OK) || tfp_index_commit(g_tfp) != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not load the fingerprint index: %s\n", tfp_engine_last_error(g_tfp));
+	if((rows.nclips > 0 && tfp_group_index_add_batch(g_tfp, rows.nclips, (const char* const*)rows.uuids,
+			rows.frame_offsets, rows.m1, rows.m2) != TFP_OK) || tfp_group_index_commit(g_tfp) != TFP_OK) {
+		ast_log(LOG_ERROR, "Could not load the fingerprint index: %s\n", tfp_group_last_error(g_tfp));
 		fpc_rows_free(&rows);
-		tfp_engine_destroy(g_tfp);
+		tfp_group_destroy(g_tfp);
 		g_tfp = NULL;
 		fpc_db_close();
 		return false;
@@ -73,9 +122,7 @@ bool fp_term(void)
 {
 	bool ret = fpc_db_term();
 	pcm_pool_drain();
-	if(g_tfp != NULL) {
-		tfp_engine_destroy(g_tfp);
-	}
+	tfp_group_destroy(g_tfp);
 	g_tfp = NULL;
 	if(ret == false) {
 		ast_log(LOG_ERROR, "Could not write database.\n");
@@ -203,12 +250,12 @@ static bool create_audio_fingerprint_info(const char* context, const char* filen
 	}
 	off[0] = 0;
 	off[1] = ns;
-	rc = pcm ? tfp_fingerprint_pcm(g_tfp, pcm, ns, sr, rows, n, &n)
-	         : tfp_fingerprint_f32_batch(g_tfp, x, off, 1, sr, rows, n, &n);
+	rc = pcm ? tfp_group_fingerprint_batch(g_tfp, pcm, off, 1, sr, rows, n, &n)
+	         : tfp_group_fingerprint_f32_batch(g_tfp, x, off, 1, sr, rows, n, &n);
 	pcm_put(pcm, cap);
 	ast_free(x);
 	if(rc != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not fingerprint %s: %s\n", filename, tfp_engine_last_error(g_tfp));
+		ast_log(LOG_ERROR, "Could not fingerprint %s: %s\n", filename, tfp_group_last_error(g_tfp));
 		ast_free(rows); ast_free(m1); ast_free(m2);
 		return false;
 	}
@@ -217,8 +264,8 @@ static bool create_audio_fingerprint_info(const char* context, const char* filen
 		m2[i] = rows[i].m2;
 	}
 	ret = fpc_store_fingerprints(context, uuid, m1, m2, n);
-	if(ret == true && tfp_index_add(g_tfp, uuid, m1, m2, (int32_t)n, NULL) != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not index %s: %s\n", filename, tfp_engine_last_error(g_tfp));
+	if(ret == true && tfp_group_index_add(g_tfp, uuid, m1, m2, (int32_t)n) != TFP_OK) {
+		ast_log(LOG_ERROR, "Could not index %s: %s\n", filename, tfp_group_last_error(g_tfp));
 		ret = false;
 	}
 	ast_free(rows);
@@ -236,7 +283,7 @@ bool fp_delete_audio_list_info(const char* uuid)
 	if(fpc_delete_audio_list_info(uuid) == false) {
 		return false;
 	}
-	if(tfp_index_remove(g_tfp, uuid) != TFP_OK) {
+	if(tfp_group_index_remove(g_tfp, uuid) != TFP_OK) {
 		ast_log(LOG_NOTICE, "Audio %s was not in the GPU index.\n", uuid);
 	}
 	return true;
@@ -283,9 +330,9 @@ bool fp_craete_audio_list_info(const char* context, const char* filename)
  * The reference calls fp_craete_audio_list_info once per file of a context's directory (scandir,
  * alphasort). fp_create_audio_list_infos takes the whole list: the catalog rows are written in
  * the same order with the same per-context MD5 dedup (a file repeated within the list counts as
- * already enrolled), and the audio of all new files is fingerprinted by one tfp_fingerprint_batch
+ * already enrolled), and the audio of all new files is fingerprinted by one tfp_group_fingerprint_batch
  * (per sample rate and sample format, and per ENROL_BATCH_SAMPLES) and indexed by one
- * tfp_index_add_batch, instead of a GPU round trip per file. */
+ * tfp_group_index_add_batch, instead of a GPU round trip per file. */
 #define ENROL_GROUPS 4
 #define ENROL_BATCH_SAMPLES ((int64_t)1 << 27) /* 256 MB of int16 per batch */
 
@@ -346,11 +393,11 @@ static int group_flush(const char* context, enrol_group* g, bool* ok)
 	uu = ast_malloc(sizeof(char*) * g->n);
 	rc = TFP_E_NOMEM;
 	if(rows && m1 && m2 && foff && uu) {
-		rc = g->f32 ? tfp_fingerprint_f32_batch(g_tfp, (const float*)g->x, g->off, g->n, g->sr, rows, nf, &got)
-		            : tfp_fingerprint_batch(g_tfp, (const int16_t*)g->x, g->off, g->n, g->sr, rows, nf, &got);
+		rc = g->f32 ? tfp_group_fingerprint_f32_batch(g_tfp, (const float*)g->x, g->off, g->n, g->sr, rows, nf, &got)
+		            : tfp_group_fingerprint_batch(g_tfp, (const int16_t*)g->x, g->off, g->n, g->sr, rows, nf, &got);
 	}
 	if(rc != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not fingerprint %d files: %s\n", g->n, tfp_engine_last_error(g_tfp));
+		ast_log(LOG_ERROR, "Could not fingerprint %d files: %s\n", g->n, tfp_group_last_error(g_tfp));
 	}
 	else {
 		/* the audio_fingerprint rows of each clip; a clip whose rows could not be stored is dropped */
@@ -375,8 +422,8 @@ static int group_flush(const char* context, enrol_group* g, bool* ok)
 			g->file[kept] = g->file[c];
 			kept++;
 		}
-		if(tfp_index_add_batch(g_tfp, kept, (const char* const*)uu, foff, m1, m2) != TFP_OK) {
-			ast_log(LOG_ERROR, "Could not index %d files: %s\n", kept, tfp_engine_last_error(g_tfp));
+		if(tfp_group_index_add_batch(g_tfp, kept, (const char* const*)uu, foff, m1, m2) != TFP_OK) {
+			ast_log(LOG_ERROR, "Could not index %d files: %s\n", kept, tfp_group_last_error(g_tfp));
 			for(c = 0; c < kept; c++) {
 				fpc_delete_audio_list_info(uu[c]);
 			}
@@ -577,12 +624,12 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 	p.freq_ignore_high = freq_ignore_high;
 	off[0] = 0;
 	off[1] = ns;
-	rc = pcm ? tfp_search_pcm_batch(g_tfp, pcm, off, 1, sr, &p, &r)
-	         : tfp_search_f32_batch(g_tfp, x, off, 1, sr, &p, &r);
+	rc = pcm ? tfp_group_search_pcm_batch(g_tfp, pcm, off, 1, sr, &p, &r)
+	         : tfp_group_search_f32_batch(g_tfp, x, off, 1, sr, &p, &r);
 	pcm_put(pcm, cap);
 	ast_free(x);
 	if(rc != TFP_OK) {
-		ast_log(LOG_ERROR, "Could not search %s: %s\n", filename, tfp_engine_last_error(g_tfp));
+		ast_log(LOG_ERROR, "Could not search %s: %s\n", filename, tfp_group_last_error(g_tfp));
 		return NULL;
 	}
 	if(r.found == 0) {

@@ -30,4 +30,9 @@ char* fp_create_hash(const char* filename);
  * number of files newly enrolled, or -1 for bad arguments. */
 int fp_create_audio_list_infos(const char* context, const char* const* filenames, int count, bool* ok);
 
+/* New: the GPUs the module's engines run on (tfp_group: the enrolled clips sharded over them,
+ * every search on all of them), before fp_init — e.g. from a "devices" option of tiresias.conf:
+ * "0-7", "0,2,5", or "" / NULL for every visible GPU (the default). */
+void fp_set_gpu_devices(const char* list);
+
 #endif

@@ -23,6 +23,7 @@ struct ast_json* fp_search_fingerprint_info(const char* c, const char* f, const 
   return NULL;
 }
 bool fp_delete_audio_list_info(const char* uuid) { return fpc_delete_audio_list_info(uuid); }
+void fp_set_gpu_devices(const char* list) { (void)list; }
 
 static void print_ints(const int32_t* v, int64_t n) {
   int64_t k;

@@ -6,7 +6,7 @@
  *   shim_driver BACKUP_DB CMD...   with CMD one of
  *     init | term | enroll CONTEXT FILE | enrolldir CONTEXT DIR | enrolldir1 CONTEXT DIR |
  *     delete UUID | search CONTEXT FILE COEFS TOL LOW HIGH | ctx NAME DIR | ctxdel NAME |
- *     lists | hash FILE
+ *     lists | hash FILE | devices LIST
  * enrolldir batches the scan through fp_create_audio_list_infos, enrolldir1 calls
  * fp_craete_audio_list_info per file as the reference does. Each command prints one JSON line. */
 #define _GNU_SOURCE
@@ -217,6 +217,10 @@ int main(int argc, char** argv) {
       char* h = fp_create_hash(argv[i]);
       printf("{\"hash\": \"%s\"}\n", h ? h : "");
       free(h);
+      i += 1;
+    } else if (!strcmp(cmd, "devices") && i < argc) {
+      fp_set_gpu_devices(argv[i]);
+      printf("{\"devices\": \"%s\"}\n", argv[i]);
       i += 1;
     } else {
       fprintf(stderr, "bad command %s\n", cmd);

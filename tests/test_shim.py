@@ -40,8 +40,8 @@ def test_shim_compiles_and_links(tmp_path, tfp_lib):
     exe = _build(tmp_path, tfp_lib)
     out = subprocess.run(["nm", "-u", exe], capture_output=True, text=True, check=True).stdout
     used = {l.split()[-1] for l in out.splitlines() if l.split()[-1].startswith("tfp_")}
-    assert {"tfp_engine_create", "tfp_search_pcm_batch", "tfp_fingerprint_pcm", "tfp_index_add",
-            "tfp_wav_read"} <= used
+    assert {"tfp_group_create", "tfp_group_search_pcm_batch", "tfp_group_fingerprint_batch", "tfp_group_index_add",
+            "tfp_group_index_add_batch", "tfp_wav_read", "tfp_host_alloc"} <= used
     assert used <= set(tfp_lib.header_symbols())
 
 
@@ -169,8 +169,9 @@ def _db_rows_by_name(path):
 @pytest.mark.gpu
 def test_shim_batched_directory_enrolment_equals_per_file(tmp_path, tfp_lib, oracle):
     """app_tiresias.c:365-424's scan of a context directory (alphasort): fp_create_audio_list_infos
-    (one GPU batch per sample format) leaves the same catalog and audio_fingerprint rows and gives
-    the same search results as fp_craete_audio_list_info file by file, including a repeated file
+    (one GPU batch per sample format, on a 3-engine device group) leaves the same catalog and
+    audio_fingerprint rows and gives the oracle's search results, as fp_craete_audio_list_info file
+    by file on one engine does, including a repeated file
     (already enrolled), a non-audio file (not enrolled), stereo (fp32 path) and 16 kHz audio."""
     exe = _build(tmp_path, tfp_lib)
     d = tmp_path / "dir"
@@ -189,8 +190,10 @@ def test_shim_batched_directory_enrolment_equals_per_file(tmp_path, tfp_lib, ora
     res = {}
     for mode in ("enrolldir", "enrolldir1"):
         db = str(tmp_path / (mode + ".db"))
-        out = _run(exe, db, "init", mode, "ctx", str(d), "search", "ctx", q, "1", "0.45", "-1", "-1",
-                   "search", "ctx", q, "1", "0.001", "-1", "-1", "term")
+        # the batched run on a 3-engine group (shards on GPU 0), the per-file run on one engine
+        devs = "0,0,0" if mode == "enrolldir" else "0"
+        out = _run(exe, db, "devices", devs, "init", mode, "ctx", str(d), "search", "ctx", q, "1", "0.45", "-1", "-1",
+                   "search", "ctx", q, "1", "0.001", "-1", "-1", "term")[1:]
         assert out[0] == {"init": True} and out[-1] == {"term": True}
         res[mode] = (out[1], [o for o in out if "TIRSTATUS" in o], _db_rows_by_name(db))
     b, f = res["enrolldir"], res["enrolldir1"]
