@@ -301,7 +301,9 @@ bool build_tables(int sample_rate, DspTables* t) {
     t->dct[0][i] = (float)((double)t->dct[0][i] * row0);
   }
 
-  static float mel[kFilters][kBins];
+  // (per call, not static: engines of a device group build their tables in parallel threads)
+  std::vector<float> mel_buf((size_t)kFilters * kBins);
+  float (*mel)[kBins] = reinterpret_cast<float (*)[kBins]>(mel_buf.data());
   build_mel_dense(sample_rate, mel);
   int off = 0;
   for (int j = 0; j < kFilters; j++) {
