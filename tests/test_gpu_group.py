@@ -107,17 +107,26 @@ def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
             r, fc = g.search_pcm_batch(qpcm[i], [0, qn], p)
             assert _pairs(r) == exp[i:i + 1] and fc[0] == nfq
     assert found >= 40
-    # ties across shards: a clip and its copy (added later, one at a time: another shard, as a rule)
-    # score alike, so whenever either wins, it must be the greater uuid of the two
-    pairs = 0
-    for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05)):
-        exp = _oracle_search(oracle, live, qdb[:, 0], qdb[:, 1], qoff, p)
-        got = _pairs(g.search_pcm_batch(qpcm.reshape(-1), soff, p)[0])
-        for i, c in enumerate(qsrc):
-            if 0 <= c < 30 and c != 3 and got[i] is not None and got[i][0] in (uuids[c], uuids[200 + c]):
-                assert got[i][0] == max(uuids[c], uuids[200 + c]) and got[i] == exp[i]
-                pairs += 1
-    assert pairs > 0
+    # ties across shards: a clip and its copy under another uuid, added one after the other to an
+    # empty group (so they land on different shards, each the lightest at its turn): the query's
+    # count ties and the greater uuid wins whichever shard holds it
+    t = tfp_lib.Group([0, 0, 0])
+    lo_u, hi_u = "10000000-0000-4000-8000-000000000000", "f0000000-0000-4000-8000-000000000000"
+    for first, second in ((lo_u, hi_u), (hi_u, lo_u)):
+        t.index_clear()
+        t.index_add(first, rows[5][0], rows[5][1])
+        t.index_add(second, rows[5][0], rows[5][1])
+        t.index_add("80000000-0000-4000-8000-000000000000", rows[6][0], rows[6][1])
+        assert sorted(r for r, _ in t.engine_stats()) == [nf, nf, nf]  # one clip per shard
+        _, q5 = oracle.fingerprint_batch(pcm[5, :qn], np.array([0, qn]), nthreads=1)
+        fr = np.zeros(len(q5), tfp_lib.FRAME_DTYPE)
+        fr["q1"], fr["q2"] = q5[:, 0], q5[:, 1]
+        for p in (tfp_lib.params(1, 0.45), tfp_lib.params(2, 0.45)):
+            r, _ = t.search_batch(fr, [0, len(fr)], p)
+            assert r[0] is not None and r[0]["audio_uuid"] == hi_u
+            r2, _ = t.search_pcm_batch(pcm[5, :qn], [0, qn], p)
+            assert r2[0] == r[0]
+    t.close()
 
     # live channels: every tick == the single engine's stream == the oracle on the window
     nch, W, tick = 12, 24000, 160
