@@ -75,6 +75,7 @@ def main():
     ap.add_argument("--no-strong", action="store_true", help="skip the strong-scaling leg")
     ap.add_argument("--no-sweeps", action="store_true", help="skip the match leg's tolerance / coefs sweeps")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-enrol", action="store_true", help="skip the enrol-then-first-search latency")
     ap.add_argument("--clock-warmup-s", type=float, default=0.25,
                     help="untimed fingerprint steps before the timed region until this much wall time has passed")
     ap.add_argument("--stream-channels", type=int, default=512)
@@ -166,6 +167,18 @@ def main():
             tj = json.load(f)
         if tj.get("frames_per_launch") == F:
             traffic = tj.get("hbm_bytes_per_launch")
+    issue = None
+    ipath = os.path.join(REPO, "profiles", "issue_fingerprint.json")
+    if os.path.exists(ipath):
+        with open(ipath) as f:
+            ij = json.load(f)
+        if ij.get("frames_per_launch") == F:
+            valu_s = ij["valu_per_frame"] * F / avg_launch_s
+            issue = {"bound": "valu_issue", "achieved": valu_s, "peak": ij["valu_issue_peak_per_s"],
+                     "unit": "wave64 VALU instructions/s", "frac": valu_s / ij["valu_issue_peak_per_s"],
+                     "valu_per_unit": ij["valu_per_frame"], "lds_per_unit": ij["lds_per_frame"],
+                     "wave_cycle_split": ij["wave_cycle_split"], "peak_method": ij["peak_method"],
+                     "counts_from": ij["source"]}
     log(f"[rank {rank}] fingerprint: {F} fp/launch, avg launch {avg_launch_s*1e3:.3f} ms, {F/avg_launch_s/1e9:.3f} Gfp/s")
 
     out = {
@@ -188,8 +201,9 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "fingerprint8k_kernel + finish_db_kernel", "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "bytes_per_unit": BYTES_PER_FP, "units_per_launch": F, "avg_launch_ms": avg_launch_s * 1e3,
-                     "limiter": "not HBM: instruction issue at 2 waves/SIMD (~170 wave64 VALU + ~24 LDS + ~13 SALU per fingerprint) "
-                                "(bit-exact fp32 DSP + glibc-exact logs); DESIGN.md §4"},
+                     "limiter": "not HBM: per-wave issue and latency at 2 waves/SIMD (~170 wave64 VALU + ~24 LDS + ~13 SALU "
+                                "per fingerprint; bit-exact fp32 DSP + glibc-exact logs); see `issue` and DESIGN.md §4",
+                     "issue": issue},
         # the same throughput as clips/s and as multiples of real time (a fingerprint
         # is one 256-sample hop of 8 kHz audio)
         "derived": {"clips_per_s": value * nclips / (F or 1), "x_realtime": value * HOP / 8000.0,
@@ -253,10 +267,44 @@ def run_strong(args, eng, torch, dev, sh, pcm, nclips, n, rank, world, barrier, 
     wall = max_over_ranks(time.perf_counter() - t0)
     total = nclips * ((n + HOP - 1) // HOP)
     log(f"[rank {rank}] strong: {k} of {nclips} clips, {wall * 1e3 / args.steps:.3f} ms per step (max over ranks)")
-    return {"workload": f"configs[1] fixed: {nclips} x {args.seconds} s clips in total, split over {world} GPU(s)",
-            "scaling": "strong", "clips_total": nclips, "clips_per_gpu_max": max(share[r + 1] - share[r] for r in range(world)),
-            "frames_per_step": total, "ms_per_step": wall * 1e3 / args.steps, "value": total * args.steps / wall,
-            "unit": "fingerprints/s"}
+    res = {"workload": f"configs[1] fixed: {nclips} x {args.seconds} s clips in total, split over {world} GPU(s)",
+           "scaling": "strong", "clips_total": nclips, "clips_per_gpu_max": max(share[r + 1] - share[r] for r in range(world)),
+           "frames_per_step": total, "ms_per_step": wall * 1e3 / args.steps, "value": total * args.steps / wall,
+           "unit": "fingerprints/s"}
+    if world == 1:
+        res["projected"] = strong_projection(args, eng, torch, dev, sh, pcm, nclips, n, wall / args.steps)
+    return res
+
+
+def strong_projection(args, eng, torch, dev, sh, pcm, nclips, n, t_full):
+    """One GPU's share of the fixed batch at N = 2, 4, 8 (1,024 / N clips), timed on this GPU with
+    HIP events over K launches: the strong leg's per-rank work, so t(1,024 clips) / t(share) is the
+    speedup N GPUs can reach before collectives and launch skew (the fingerprint leg has none)."""
+    out = {}
+    for N in (2, 4, 8):
+        k = nclips // N
+        plan = eng.plan(np.arange(k + 1, dtype=np.int64) * n)
+        micro = torch.empty((max(plan.nframes, 1), 2), dtype=torch.int32, device=dev)
+        for _ in range(3):
+            eng.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, sh)
+        t_w = time.perf_counter()
+        while time.perf_counter() - t_w < args.clock_warmup_s:
+            for _ in range(16):
+                eng.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, sh)
+            torch.cuda.synchronize(dev)
+        reps = max(args.steps, 20)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            eng.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, sh)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        t_share = e0.elapsed_time(e1) / 1e3 / reps
+        out[str(N)] = {"clips_per_gpu": k, "ms_per_step": t_share * 1e3, "projected_speedup": t_full / t_share,
+                       "projected_efficiency": t_full / t_share / N}
+        log(f"strong projection N={N}: {k} clips {t_share * 1e3:.3f} ms -> x{t_full / t_share:.2f}")
+        del micro
+    return out
 
 
 def fingerprint_cpu_baseline(args, pcm, nclips, n, F):
@@ -286,7 +334,21 @@ def fingerprint_cpu_baseline(args, pcm, nclips, n, F):
     fps = frames / dt
     p1, dt1 = timed(1, 2, max(2.0, args.cpu_seconds / 3))
     fps1 = p1 * 2 * (F // nclips) / dt1
-    log(f"cpu baseline {fps:.0f} fp/s on {threads} threads ({dt:.1f} s), {fps1:.0f} fp/s on 1 thread; nproc {nproc}")
+    # every core the machine reports (nproc), beside the share: on a shared GPU box the extra
+    # threads compete for the share's cores, so this is the figure for a dedicated host
+    ka = min(nclips, max(k, nproc))
+    host_all = pcm[:ka].cpu().numpy().reshape(-1) if ka > k else host
+    off_all = np.arange(ka + 1) * n
+    pa, ta = 0, time.perf_counter()
+    while True:
+        oracle_py.fingerprint_batch(host_all[: ka * n], off_all, nthreads=nproc, want_db=False)
+        pa += 1
+        dta = time.perf_counter() - ta
+        if dta >= max(2.0, args.cpu_seconds / 2):
+            break
+    fpsa = pa * ka * (F // nclips) / dta
+    log(f"cpu baseline {fps:.0f} fp/s on {threads} threads ({dt:.1f} s), {fps1:.0f} fp/s on 1 thread, "
+        f"{fpsa:.0f} fp/s on {nproc} threads; nproc {nproc}")
     return {"value": fps, "unit": "fingerprints/s", "cores": threads, "kind": "port",
             "sample": f"{passes} passes over {k} of the {nclips} x {args.seconds} s clips "
                       f"({frames} frames), oracle/oracle.c, {threads} threads, {dt:.1f} s",
@@ -294,6 +356,9 @@ def fingerprint_cpu_baseline(args, pcm, nclips, n, F):
                                             "the GPU box), capped at nproc",
             "one_core": {"value": fps1, "unit": "fingerprints/s", "cores": 1,
                          "sample": f"{p1} passes over 2 clips ({p1 * 2 * (F // nclips)} frames), 1 thread, {dt1:.1f} s"},
+            "all_cores": {"value": fpsa, "unit": "fingerprints/s", "cores": nproc,
+                          "sample": f"{pa} passes over {ka} clips ({pa * ka * (F // nclips)} frames), {nproc} threads "
+                                    f"(nproc), {dta:.1f} s"},
             "note": "libaubio is not installed: the oracle restates its algorithm in plain C (kind: port)"}
 
 
@@ -484,6 +549,12 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             lat = out_ms.tolist()
             harness = ("C loop over tfp_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries held in a "
                        "tfp_host_alloc buffer (read in place, as the shim's WAV reads)" % (n_it, len(hq)))
+    # SURVEY §8(d)'s match roofline: one pass over the index per batch (12 B per row) plus the
+    # query frames (16 B each) against HBM; the vote path reads only the used keys' boxes, so a
+    # fraction above 1 means the batch costs less than one index pass
+    match_bytes = 12 * rows + 16 * nq * ((qn + HOP - 1) // HOP)
+    for sw in sweeps:
+        sw["roofline_frac"] = match_bytes / (sw["batch_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS
     res = {"workload": f"configs[{2 if world == 1 else 3}]: {nq} x 5 s queries vs {args.db_clips} x 30 s clips"
                         f" ({'sharded x%d, %s all_reduce MAX' % (world, 'RCCL' if args.dist_backend == 'nccl' else args.dist_backend) if world > 1 else '1 GPU'})",
             "collective": (("all_gather of the query frame values (each rank fingerprints 1/%d of the queries), "
@@ -495,10 +566,67 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat), "latency_harness": harness,
             "latency_p50_ms_python": float(np.percentile(lat_py, 50)),
+            "roofline": {"bound": "hbm", "definition": "one index pass per batch: 12 B x index rows + 16 B x query frames "
+                                                       "(SURVEY 8d)", "bytes": match_bytes,
+                         "achieved": match_bytes / (batch_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": match_bytes / (batch_ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+                         "note": "the coefs=1 vote reads only the used keys' boxes: frac > 1 = under one index pass"},
             "sweeps": sweeps}
+    if world == 1 and not args.no_enrol:
+        res["enrol_then_search"] = enrol_latency(args, eng, T, torch, dev, sh, p)
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = match_cpu_baseline(args, T, eng, torch, dev, sh)
     return res
+
+
+def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
+    """Enrol-then-first-search at configs[2]'s 100k-clip DB: one new 30 s clip's rows added
+    (tfp_index_add, as the shim's fp_craete_audio_list_info does) and a batch-1 search of an excerpt
+    of it right after, timed together: the first search pays the index update. The engine merges
+    the new rows into the sorted index (tfp_index.hip); a second engine built with TFP_INDEX_FULL=1
+    (a full re-sort per update, the round-2 behaviour) gives the figure to compare against. The
+    reference's INSERT updates its B-tree per row (fp_handler.c:559-571, :745-753)."""
+    n_db, qn = 8000 * 30, 8000 * 5
+    nf_db = (n_db + HOP - 1) // HOP
+    ids = list(range(args.db_clips, args.db_clips + n_add))
+    pcm = T.synth_pcm(SEED_DB, ids, n_db)
+    fr = eng.fingerprint_batch(pcm.reshape(-1), np.arange(n_add + 1) * n_db)
+
+    def run(e, tag):
+        out = []
+        for i, g in enumerate(ids):
+            q = np.ascontiguousarray(pcm[i, 256 * 100: 256 * 100 + qn])
+            t0 = time.perf_counter()
+            e.index_add(uuid_of(g), fr["m1"][i * nf_db:(i + 1) * nf_db], fr["m2"][i * nf_db:(i + 1) * nf_db])
+            res, _ = e.search_pcm_batch(q, [0, qn], p)
+            out.append((time.perf_counter() - t0) * 1e3)
+            assert res[0] is not None and res[0]["audio_uuid"] == uuid_of(g), (tag, i, res[0])
+        for g in ids:
+            e.index_remove(uuid_of(g))
+        e.index_commit()
+        log(f"enrol-then-search ({tag}): p50 {np.percentile(out, 50):.2f} ms")
+        return out
+
+    fb0, mg0 = eng.index_build_stats()
+    inc = run(eng, "merge")
+    fb1, mg1 = eng.index_build_stats()
+    os.environ["TFP_INDEX_FULL"] = "1"
+    try:
+        full_eng = T.Engine(eng.device)
+    finally:
+        del os.environ["TFP_INDEX_FULL"]
+    enroll(full_eng, torch, dev, sh, list(range(args.db_clips)))
+    full_eng.index_commit()
+    full = run(full_eng, "full re-sort")
+    full_eng.close()
+    torch.cuda.empty_cache()
+    return {"workload": f"{n_add} x (tfp_index_add of one 30 s clip + batch-1 search of a 5 s excerpt of it) on the "
+                        f"{args.db_clips}-clip DB, host PCM",
+            "p50_ms": float(np.percentile(inc, 50)), "max_ms": float(np.max(inc)), "samples_ms": inc,
+            "index_updates": {"merges": mg1 - mg0, "full_sorts": fb1 - fb0},
+            "full_resort": {"p50_ms": float(np.percentile(full, 50)), "max_ms": float(np.max(full)), "samples_ms": full,
+                            "how": "same calls on an engine with TFP_INDEX_FULL=1 (every update a full radix sort of all "
+                                   "staged rows + a uuid sort), the round-2 behaviour"}}
 
 
 def match_cpu_baseline(args, T, eng, torch, dev, sh):
