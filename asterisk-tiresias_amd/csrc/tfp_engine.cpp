@@ -860,15 +860,18 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
     // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
     if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
+    if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
     if (e->cells.valid) {
       HIPCHK(e, e->wide.reserve(nf, nq, C, s));
       bool ok = false;
-      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, &e->wide, &ok,
-                                               s));
+      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
+                                         &e->wide, &ok, s));
       if (ok) {
         HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
         done = true;
       }
+      if (e->dbg_vote) fprintf(stderr, "[tfp] general path: nq %d nf %lld C %d tol %g -> %s\n", nq, (long long)nf, C, sc.tole,
+                               ok ? "sweep by groups" : "cells / row scan");
     }
   }
   if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {

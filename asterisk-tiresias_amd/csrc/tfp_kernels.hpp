@@ -216,7 +216,10 @@ struct WideScratch {
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk
   int64_t* chw = nullptr;                            // [nchunks + 1] first work item of each chunk
   uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
-  int32_t* info = nullptr;                           // [2]: frames kept, ineligible frames
+  uint32_t* tbits = nullptr;                         // [slab][ceil(C / 32)] clips touched per chunk, zero between calls
+  int32_t* tcnt = nullptr;                           // [slab] touched clips per chunk
+  int32_t* tlist = nullptr;                          // [slab][C] the touched clips (wide_final's work list)
+  int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   int64_t cap_nf = 0, cap_nch = 0, cap_score = 0;
@@ -232,7 +235,7 @@ struct WideScratch {
 // scan (key outside the cache, window outside int32) or a query has 2^16 frames or more (the
 // score rows hold 16-bit counts), the caller then takes launch_scan.
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    int64_t max_qframes, WideScratch* ws, bool* eligible, hipStream_t s);
+                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s);
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s);

@@ -415,8 +415,12 @@ constexpr int kWideCh = WideScratch::kChunk;
 constexpr int kWideSegs = 2 * kKeyRange;  // per chunk: key k with a max2 window, k | 1024 without
 static_assert(kWideCh == 64, "one query per lane");
 
+// Bad frames (a key outside the cache's range or a window outside int32: the row scan takes the
+// batch) into info[1]; with uk, the U2 (offset binary: unsigned order == signed order) of each frame
+// and fv = the identity, for the two-sort form.
 __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t nf, uint32_t* __restrict__ uk,
                                    int32_t* __restrict__ fv, int32_t* __restrict__ info) {
+  int32_t nbad = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
     const FrameBox bx = boxes[i];
     uint32_t u = 0xffffffffu;
@@ -426,24 +430,35 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
       if (bx.flags & 2) {
         bad = bad || bx.L2 <= (int64_t)INT32_MIN || bx.L2 > (int64_t)INT32_MAX || bx.U2 < (int64_t)INT32_MIN ||
               bx.U2 > (int64_t)INT32_MAX;
-        u = (uint32_t)(int32_t)bx.U2 ^ 0x80000000u;  // offset binary: unsigned order == signed order
+        u = (uint32_t)(int32_t)bx.U2 ^ 0x80000000u;
       } else {
         u = 0;
       }
-      if (bad) atomicAdd(&info[1], 1);
+      nbad += bad;
     }
-    uk[i] = u;
-    fv[i] = (int32_t)i;
+    if (uk) {
+      uk[i] = u;
+      fv[i] = (int32_t)i;
+    }
   }
+  for (int o = 32; o > 0; o >>= 1) nbad += __shfl_xor(nbad, o, 64);
+  if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(&info[1], nbad);
 }
 
-// Composite key (chunk << 43 | segment key << 32 | L2) of each frame in the U2 order; frames that
-// take no part get ~0 and sort last.
+// Composite sort key of a frame: chunk << 46 | segment key << 35 | L2 << 3 | d, with d = U2 - L2 -
+// dbase in [0, 8) (U2 - L2 is fmt6(q2 + tol) - fmt6(q2 - tol): within a few micro-units of 2 tol).
+// One sort by it orders each (chunk, key) segment by L2, then U2. Frames that take no part get ~0
+// and sort last. fv: the frame of each position (nullptr: position i is frame i). A width outside
+// [dbase, dbase + 8) counts in info[2]; the caller then sorts by U2 first and passes dbase = -1
+// (d = 0: that stable pre-sort orders equal L2 by U2 instead).
+constexpr int kWideDeltaBits = 3, kWideSegShift = 32 + kWideDeltaBits, kWideChunkShift = kWideSegShift + 11;
 __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
-                                   int64_t nf, const int32_t* __restrict__ fv, unsigned long long* __restrict__ ck,
+                                   int64_t nf, const int32_t* __restrict__ fv, int64_t dbase,
+                                   unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
                                    int32_t* __restrict__ info) {
+  int32_t kept = 0, wide = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t f = fv[i];
+    const int32_t f = fv ? fv[i] : (int32_t)i;
     const FrameBox bx = boxes[f];
     unsigned long long key = ~0ull;
     const int64_t kk = (int64_t)bx.k + kKeyOffset;
@@ -454,12 +469,29 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
         if (qoff[mid] <= f) lo = mid; else hi = mid;
       }
       const unsigned long long ch = (unsigned long long)(lo / kWideCh);
-      const unsigned long long sk = (bx.flags & 2) ? (unsigned long long)kk : (unsigned long long)kk | kKeyRange;
-      const unsigned long long l2 = (bx.flags & 2) ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
-      key = (ch << 43) | (sk << 32) | l2;
-      atomicAdd(&info[0], 1);
+      const bool w2 = bx.flags & 2;
+      const unsigned long long sk = w2 ? (unsigned long long)kk : (unsigned long long)kk | kKeyRange;
+      const unsigned long long l2 = w2 ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
+      unsigned long long d = 0;
+      if (w2 && dbase >= 0) {
+        const int64_t dd = bx.U2 - bx.L2 - dbase;
+        if (dd < 0 || dd >= (1 << kWideDeltaBits)) wide++;
+        else d = (unsigned long long)dd;
+      }
+      key = (ch << kWideChunkShift) | (sk << kWideSegShift) | (l2 << kWideDeltaBits) | d;
+      kept++;
     }
     ck[i] = key;
+    if (fo) fo[i] = f;
+  }
+  // one atomic per wave (same-address atomics serialise in L2: one per frame cost ~0.13 ms at C3)
+  for (int o = 32; o > 0; o >>= 1) {
+    kept += __shfl_xor(kept, o, 64);
+    wide += __shfl_xor(wide, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    if (kept) atomicAdd(&info[0], kept);
+    if (wide) atomicAdd(&info[2], wide);
   }
 }
 
@@ -479,9 +511,9 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
       if (qoff[mid] <= f) lo = mid; else hi = mid;
     }
     qis[i] = (uint8_t)(lo % kWideCh);
-    const unsigned long long sg = ck[i] >> 32;  // chunk << 11 | segment key
-    if (i == 0 || (ck[i - 1] >> 32) != sg) seg[2 * sg] = (int32_t)i;
-    if (i == n - 1 || (ck[i + 1] >> 32) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
+    const unsigned long long sg = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
+    if (i == 0 || (ck[i - 1] >> kWideSegShift) != sg) seg[2 * sg] = (int32_t)i;
+    if (i == n - 1 || (ck[i + 1] >> kWideSegShift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
   }
 }
 
@@ -489,7 +521,7 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
 __global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, int64_t n, int64_t nch,
                                  int32_t* __restrict__ cbeg) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << 43);
+  if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << kWideChunkShift);
 }
 
 // In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i]: one 16-wave workgroup per
@@ -626,7 +658,9 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
                                                           const int32_t* __restrict__ cbeg, CellView cv,
                                                           const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
                                                           const int32_t* __restrict__ U2s, const int32_t* __restrict__ P,
-                                                          int32_t C, uint32_t* __restrict__ score) {
+                                                          int32_t C, uint32_t* __restrict__ score, uint32_t* __restrict__ tbits,
+                                                          int32_t* __restrict__ tcnt, int32_t* __restrict__ tlist) {
+  const int32_t tw = (C + 31) >> 5;  // words of a chunk's touched-clip bitmap
   const int lane = threadIdx.x & 63;
   const int64_t W0 = chw[ch0], W1 = chw[ch1];
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -732,37 +766,54 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
     const uint32_t v = (uint32_t)cnt | (hi16 << 16);
     if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
+    // the chunk's touched-clip list: the first group to score a clip appends it (wide_final reads
+    // and clears only the listed rows)
+    if (__ballot(!(lane & 1) && v) && lane == 0) {
+      const uint32_t bit = 1u << (col & 31);
+      if (!(atomicOr(&tbits[(int64_t)(ch - ch0) * tw + (col >> 5)], bit) & bit))
+        tlist[(int64_t)(ch - ch0) * C + atomicAdd(&tcnt[ch - ch0], 1)] = col;
+    }
   }
 }
 
-// Per chunk of the slab (blockIdx.y): each query's max over clips of (count << 32 | tie key),
-// and the score rows back to zero. A wave reads two clips' rows per step (32 words each).
+// Per chunk of the slab (blockIdx.y): each query's max over the chunk's touched clips of
+// (count << 32 | tie key), and those score rows and bitmap words back to zero. A wave reads two
+// listed clips' rows per step (32 words each); the work follows the touched clips, not C.
 __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq, int32_t C,
                                                          const int32_t* __restrict__ tiekey, uint32_t* __restrict__ score,
+                                                         uint32_t* __restrict__ tbits, const int32_t* __restrict__ tcnt,
+                                                         const int32_t* __restrict__ tlist,
                                                          unsigned long long* __restrict__ best) {
   __shared__ unsigned long long red[4][kWideCh];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, wl = lane & 31;
+  const int32_t tw = (C + 31) >> 5;
   uint32_t* rows = score + (int64_t)blockIdx.y * C * (kWideCh / 2);
+  uint32_t* bits = tbits + (int64_t)blockIdx.y * tw;
+  const int32_t* list = tlist + (int64_t)blockIdx.y * C;
+  const int32_t n = tcnt[blockIdx.y];
   unsigned long long rlo = 0, rhi = 0;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c0 = 2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); c0 < C; c0 += 8 * nw) {
+  for (int64_t i0 = 2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); i0 < n; i0 += 8 * nw) {
     uint32_t w[4];
-    int64_t cc[4];
+    int32_t cc[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      cc[u] = c0 + 2 * nw * u + half;
-      w[u] = cc[u] < C ? rows[cc[u] * (kWideCh / 2) + wl] : 0u;
+      const int64_t i = i0 + 2 * nw * u + half;
+      cc[u] = i < n ? list[i] : -1;
+      w[u] = cc[u] >= 0 ? rows[(int64_t)cc[u] * (kWideCh / 2) + wl] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < 4; u++) {
+      if (cc[u] < 0) continue;
       if (w[u]) {
         const unsigned long long tk = (uint32_t)tiekey[cc[u]];
         const unsigned long long klo = ((unsigned long long)(w[u] & 0xffffu) << 32) | tk;
         const unsigned long long khi = ((unsigned long long)(w[u] >> 16) << 32) | tk;
         if (w[u] & 0xffffu) rlo = klo > rlo ? klo : rlo;
         if (w[u] >> 16) rhi = khi > rhi ? khi : rhi;
-        rows[cc[u] * (kWideCh / 2) + wl] = 0u;
+        rows[(int64_t)cc[u] * (kWideCh / 2) + wl] = 0u;
       }
+      if (wl == 0) bits[cc[u] >> 5] = 0u;  // (every set bit of the word belongs to a listed clip)
     }
   }
   {
@@ -787,8 +838,11 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, tmp})
+                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)tbits,
+                  (void*)tcnt, (void*)tlist, tmp})
     if (p) (void)hipFree(p);
+  tbits = nullptr;
+  tcnt = tlist = nullptr;
   ka = kb = nullptr;
   ua = ub = nullptr;
   va = vb = L2s = U2s = P = seg = wpre = cbeg = info = nullptr;
@@ -842,38 +896,69 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
   slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
   const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * (kWideCh / 2);
   if (ns > cap_score) {
-    if (score) (void)hipFree(score);
+    for (void* p : {(void*)score, (void*)tbits, (void*)tcnt, (void*)tlist})
+      if (p) (void)hipFree(p);
     score = nullptr;
+    tbits = nullptr;
+    tcnt = tlist = nullptr;
     cap_score = 0;
-    if ((e = dmalloc(&score, ns))) return e;
-    if ((e = hipMemsetAsync(score, 0, sizeof(uint32_t) * (size_t)ns, s))) return e;  // kept zero by wide_final
+    const int64_t tw = ((C > 0 ? C : 1) + 31) / 32;
+    if ((e = dmalloc(&score, ns)) || (e = dmalloc(&tbits, (int64_t)slab * tw)) || (e = dmalloc(&tcnt, (int64_t)slab)) ||
+        (e = dmalloc(&tlist, (int64_t)slab * (C > 0 ? C : 1))))
+      return e;
+    // kept zero by wide_final (rows and bitmaps; the counts are cleared per launch)
+    if ((e = hipMemsetAsync(score, 0, sizeof(uint32_t) * (size_t)ns, s)) ||
+        (e = hipMemsetAsync(tbits, 0, sizeof(uint32_t) * (size_t)(slab * tw), s)))
+      return e;
     cap_score = ns;
   }
-  if (!info && (e = dmalloc(&info, 2))) return e;
+  if (!info && (e = dmalloc(&info, 4))) return e;
   return hipSuccess;
 }
 
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    int64_t max_qframes, WideScratch* ws, bool* eligible, hipStream_t s) {
+                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s) {
   *eligible = false;
-  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 21) || max_qframes >= 65536)
+  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
     return hipSuccess;
   hipError_t e;
   const int64_t nch = (nq + kWideCh - 1) / kWideCh;
-  if ((e = hipMemsetAsync(ws->info, 0, 2 * sizeof(int32_t), s))) return e;
-  hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
+  int cb = 1;  // chunk bits: every chunk number below 2^cb - 1, so no key reaches the ~0 of unused frames
+  while (((int64_t)1 << cb) - 1 <= nch) cb++;
+  const int end_bit = kWideChunkShift + cb;
+  // U2 - L2 lies within a few micro-units of 2 tol (fmt6 rounds both ends): d = U2 - L2 - dbase
+  const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
+  if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
+  // the bad-frame check (a key or a window outside what the cache and the int32 windows hold)
+  hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
+                     ws->info);
+  // one sort by (chunk, key, L2, U2 - L2)
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf,
+                     (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, (int)nf, 0, 32, s))) return e;
-  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf, ws->vb, ws->ka, ws->info);
-  tb = ws->tmp_bytes;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, (int)nf, 0, 64, s))) return e;
-  int32_t info[2] = {0, 0};
+  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, (int)nf, 0, end_bit, s))) return e;
+  int32_t info[3] = {0, 0, 0};
   if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
   if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
+  const int32_t* order = ws->vb;
+  if (info[2] > 0 || dbase < 0) {
+    // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
+    if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
+    hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
+    tb = ws->tmp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, (int)nf, 0, 32, s))) return e;
+    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf, ws->vb, (int64_t)-1,
+                       ws->ka, (int32_t*)nullptr, ws->info);
+    tb = ws->tmp_bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, (int)nf, 0, end_bit, s)))
+      return e;
+    if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
+    order = ws->va;
+  }
   const int64_t n = info[0];
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
   if (n > 0)
-    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, d_qoff, nq, n, ws->kb, ws->va, ws->L2s,
+    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, d_qoff, nq, n, ws->kb, order, ws->L2s,
                        ws->U2s, ws->qis, ws->seg);
   hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, n, nch, ws->cbeg);
   hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->P);
@@ -899,10 +984,12 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   const unsigned fx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (C + 2047) / 2048));
   for (int64_t c0 = 0; c0 < nch; c0 += slab) {
     const int32_t c1 = (int32_t)std::min<int64_t>(nch, c0 + slab);
+    hipError_t e = hipMemsetAsync(ws->tcnt, 0, sizeof(int32_t) * (size_t)(c1 - c0), s);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(wide_groups_kernel, dim3(8192), dim3(256), 0, s, (int32_t)c0, c1, ws->chw, ws->wpre, ws->seg, ws->cbeg,
-                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score);
+                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->tbits, ws->tcnt, ws->tlist);
     hipLaunchKernelGGL(wide_final_kernel, dim3(fx, (unsigned)(c1 - c0)), dim3(256), 0, s, (int32_t)c0, nq, C, d_tiekey,
-                       ws->score, d_best);
+                       ws->score, ws->tbits, ws->tcnt, ws->tlist, d_best);
   }
   return hipGetLastError();
 }
