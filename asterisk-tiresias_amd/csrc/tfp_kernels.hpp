@@ -216,9 +216,7 @@ struct WideScratch {
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk
   int64_t* chw = nullptr;                            // [nchunks + 1] first work item of each chunk
   uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
-  uint32_t* tbits = nullptr;                         // [slab][ceil(C / 32)] clips touched per chunk, zero between calls
-  int32_t* tcnt = nullptr;                           // [slab] touched clips per chunk
-  int32_t* tlist = nullptr;                          // [slab][C] the touched clips (wide_final's work list)
+  uint8_t* touch = nullptr;                          // [slab][C] 1 = the chunk scored the clip; zero between calls
   int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
   void* tmp = nullptr;
   size_t tmp_bytes = 0;

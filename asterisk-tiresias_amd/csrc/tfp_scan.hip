@@ -658,9 +658,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
                                                           const int32_t* __restrict__ cbeg, CellView cv,
                                                           const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
                                                           const int32_t* __restrict__ U2s, const int32_t* __restrict__ P,
-                                                          int32_t C, uint32_t* __restrict__ score, uint32_t* __restrict__ tbits,
-                                                          int32_t* __restrict__ tcnt, int32_t* __restrict__ tlist) {
-  const int32_t tw = (C + 31) >> 5;  // words of a chunk's touched-clip bitmap
+                                                          int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch) {
   const int lane = threadIdx.x & 63;
   const int64_t W0 = chw[ch0], W1 = chw[ch1];
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -766,54 +764,46 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
     const uint32_t v = (uint32_t)cnt | (hi16 << 16);
     if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
-    // the chunk's touched-clip list: the first group to score a clip appends it (wide_final reads
-    // and clears only the listed rows)
-    if (__ballot(!(lane & 1) && v) && lane == 0) {
-      const uint32_t bit = 1u << (col & 31);
-      if (!(atomicOr(&tbits[(int64_t)(ch - ch0) * tw + (col >> 5)], bit) & bit))
-        tlist[(int64_t)(ch - ch0) * C + atomicAdd(&tcnt[ch - ch0], 1)] = col;
-    }
+    // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
+    if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
   }
 }
 
 // Per chunk of the slab (blockIdx.y): each query's max over the chunk's touched clips of
-// (count << 32 | tie key), and those score rows and bitmap words back to zero. A wave reads two
-// listed clips' rows per step (32 words each); the work follows the touched clips, not C.
+// (count << 32 | tie key), and those score rows and touch bytes back to zero. A wave reads the
+// touch bytes of 64 clips per step (64 B) and only the touched clips' rows (128 B each, two clips
+// per step, one per half-wave): the row traffic follows the hits, not C.
 __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq, int32_t C,
                                                          const int32_t* __restrict__ tiekey, uint32_t* __restrict__ score,
-                                                         uint32_t* __restrict__ tbits, const int32_t* __restrict__ tcnt,
-                                                         const int32_t* __restrict__ tlist,
-                                                         unsigned long long* __restrict__ best) {
+                                                         uint8_t* __restrict__ touch, unsigned long long* __restrict__ best) {
   __shared__ unsigned long long red[4][kWideCh];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, wl = lane & 31;
-  const int32_t tw = (C + 31) >> 5;
   uint32_t* rows = score + (int64_t)blockIdx.y * C * (kWideCh / 2);
-  uint32_t* bits = tbits + (int64_t)blockIdx.y * tw;
-  const int32_t* list = tlist + (int64_t)blockIdx.y * C;
-  const int32_t n = tcnt[blockIdx.y];
+  uint8_t* tch = touch + (int64_t)blockIdx.y * C;
   unsigned long long rlo = 0, rhi = 0;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i0 = 2 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); i0 < n; i0 += 8 * nw) {
-    uint32_t w[4];
-    int32_t cc[4];
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int64_t i = i0 + 2 * nw * u + half;
-      cc[u] = i < n ? list[i] : -1;
-      w[u] = cc[u] >= 0 ? rows[(int64_t)cc[u] * (kWideCh / 2) + wl] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-      if (cc[u] < 0) continue;
-      if (w[u]) {
-        const unsigned long long tk = (uint32_t)tiekey[cc[u]];
-        const unsigned long long klo = ((unsigned long long)(w[u] & 0xffffu) << 32) | tk;
-        const unsigned long long khi = ((unsigned long long)(w[u] >> 16) << 32) | tk;
-        if (w[u] & 0xffffu) rlo = klo > rlo ? klo : rlo;
-        if (w[u] >> 16) rhi = khi > rhi ? khi : rhi;
-        rows[(int64_t)cc[u] * (kWideCh / 2) + wl] = 0u;
+  for (int64_t c0 = 64 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); c0 < C; c0 += 64 * nw) {
+    const bool t = c0 + lane < C && tch[c0 + lane];
+    unsigned long long m = __ballot(t);
+    if (t) tch[c0 + lane] = 0;
+    while (m) {  // two touched clips per step, one per half-wave
+      const int b0 = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int b1 = m ? __ffsll((long long)m) - 1 : -1;
+      if (m) m &= m - 1;
+      const int b = half ? b1 : b0;
+      if (b >= 0) {
+        const int64_t c = c0 + b;
+        const uint32_t w = rows[c * (kWideCh / 2) + wl];
+        if (w) {
+          const unsigned long long tk = (uint32_t)tiekey[c];
+          const unsigned long long klo = ((unsigned long long)(w & 0xffffu) << 32) | tk;
+          const unsigned long long khi = ((unsigned long long)(w >> 16) << 32) | tk;
+          if (w & 0xffffu) rlo = klo > rlo ? klo : rlo;
+          if (w >> 16) rhi = khi > rhi ? khi : rhi;
+          rows[c * (kWideCh / 2) + wl] = 0u;
+        }
       }
-      if (wl == 0) bits[cc[u] >> 5] = 0u;  // (every set bit of the word belongs to a listed clip)
     }
   }
   {
@@ -838,11 +828,9 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)tbits,
-                  (void*)tcnt, (void*)tlist, tmp})
+                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, tmp})
     if (p) (void)hipFree(p);
-  tbits = nullptr;
-  tcnt = tlist = nullptr;
+  touch = nullptr;
   ka = kb = nullptr;
   ua = ub = nullptr;
   va = vb = L2s = U2s = P = seg = wpre = cbeg = info = nullptr;
@@ -896,19 +884,15 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
   slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
   const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * (kWideCh / 2);
   if (ns > cap_score) {
-    for (void* p : {(void*)score, (void*)tbits, (void*)tcnt, (void*)tlist})
+    for (void* p : {(void*)score, (void*)touch})
       if (p) (void)hipFree(p);
     score = nullptr;
-    tbits = nullptr;
-    tcnt = tlist = nullptr;
+    touch = nullptr;
     cap_score = 0;
-    const int64_t tw = ((C > 0 ? C : 1) + 31) / 32;
-    if ((e = dmalloc(&score, ns)) || (e = dmalloc(&tbits, (int64_t)slab * tw)) || (e = dmalloc(&tcnt, (int64_t)slab)) ||
-        (e = dmalloc(&tlist, (int64_t)slab * (C > 0 ? C : 1))))
-      return e;
-    // kept zero by wide_final (rows and bitmaps; the counts are cleared per launch)
+    if ((e = dmalloc(&score, ns)) || (e = dmalloc(&touch, (int64_t)slab * (C > 0 ? C : 1)))) return e;
+    // kept zero by wide_final (score rows and touch bytes)
     if ((e = hipMemsetAsync(score, 0, sizeof(uint32_t) * (size_t)ns, s)) ||
-        (e = hipMemsetAsync(tbits, 0, sizeof(uint32_t) * (size_t)(slab * tw), s)))
+        (e = hipMemsetAsync(touch, 0, (size_t)slab * (C > 0 ? C : 1), s)))
       return e;
     cap_score = ns;
   }
@@ -984,12 +968,10 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   const unsigned fx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (C + 2047) / 2048));
   for (int64_t c0 = 0; c0 < nch; c0 += slab) {
     const int32_t c1 = (int32_t)std::min<int64_t>(nch, c0 + slab);
-    hipError_t e = hipMemsetAsync(ws->tcnt, 0, sizeof(int32_t) * (size_t)(c1 - c0), s);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(wide_groups_kernel, dim3(8192), dim3(256), 0, s, (int32_t)c0, c1, ws->chw, ws->wpre, ws->seg, ws->cbeg,
-                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->tbits, ws->tcnt, ws->tlist);
+                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->touch);
     hipLaunchKernelGGL(wide_final_kernel, dim3(fx, (unsigned)(c1 - c0)), dim3(256), 0, s, (int32_t)c0, nq, C, d_tiekey,
-                       ws->score, ws->tbits, ws->tcnt, ws->tlist, d_best);
+                       ws->score, ws->touch, d_best);
   }
   return hipGetLastError();
 }
