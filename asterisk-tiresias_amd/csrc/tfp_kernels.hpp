@@ -210,6 +210,7 @@ struct WideScratch {
   int32_t *va = nullptr, *vb = nullptr;             // frame indices
   int32_t *L2s = nullptr, *U2s = nullptr;           // sorted windows
   uint8_t* qis = nullptr;                            // sorted frames' query within its chunk
+  int32_t* fq = nullptr;                             // [nf] each frame's query
   int32_t* P = nullptr;                              // [nf][kChunk] in-chunk prefix counts
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
   int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix

@@ -445,6 +445,15 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
   if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(&info[1], nbad);
 }
 
+// fq[f] = the query of frame f (one thread per query writes its frames' entries): the key and
+// gather passes read it instead of searching qoff per frame.
+__global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq) {
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t b = qoff[q] - qoff[0], e = qoff[q + 1] - qoff[0];
+    for (int64_t f = b; f < e; f++) fq[f] = (int32_t)q;
+  }
+}
+
 // Composite sort key of a frame: chunk << 46 | segment key << 35 | L2 << 3 | d, with d = U2 - L2 -
 // dbase in [0, 8) (U2 - L2 is fmt6(q2 + tol) - fmt6(q2 - tol): within a few micro-units of 2 tol).
 // One sort by it orders each (chunk, key) segment by L2, then U2. Frames that take no part get ~0
@@ -452,7 +461,7 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
 // [dbase, dbase + 8) counts in info[2]; the caller then sorts by U2 first and passes dbase = -1
 // (d = 0: that stable pre-sort orders equal L2 by U2 instead).
 constexpr int kWideDeltaBits = 3, kWideSegShift = 32 + kWideDeltaBits, kWideChunkShift = kWideSegShift + 11;
-__global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
+__global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    int64_t nf, const int32_t* __restrict__ fv, int64_t dbase,
                                    unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
                                    int32_t* __restrict__ info) {
@@ -463,12 +472,7 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
     unsigned long long key = ~0ull;
     const int64_t kk = (int64_t)bx.k + kKeyOffset;
     if ((bx.flags & 1) && kk >= 0 && kk < kKeyRange) {
-      int lo = 0, hi = nq;  // the frame's query: the last q with qoff[q] <= f
-      while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (qoff[mid] <= f) lo = mid; else hi = mid;
-      }
-      const unsigned long long ch = (unsigned long long)(lo / kWideCh);
+      const unsigned long long ch = (unsigned long long)(fq[f] / kWideCh);
       const bool w2 = bx.flags & 2;
       const unsigned long long sk = w2 ? (unsigned long long)kk : (unsigned long long)kk | kKeyRange;
       const unsigned long long l2 = w2 ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
@@ -496,7 +500,7 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
 }
 
 // Sorted frames' windows and queries; the segment table [chunk][segment key] = [begin, end).
-__global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int64_t* __restrict__ qoff, int32_t nq,
+__global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    int64_t n, const unsigned long long* __restrict__ ck,
                                    const int32_t* __restrict__ fv, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
                                    uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
@@ -505,12 +509,7 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
     const FrameBox bx = boxes[f];
     L2s[i] = (int32_t)bx.L2;
     U2s[i] = (int32_t)bx.U2;
-    int lo = 0, hi = nq;
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (qoff[mid] <= f) lo = mid; else hi = mid;
-    }
-    qis[i] = (uint8_t)(lo % kWideCh);
+    qis[i] = (uint8_t)(fq[f] % kWideCh);
     const unsigned long long sg = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
     if (i == 0 || (ck[i - 1] >> kWideSegShift) != sg) seg[2 * sg] = (int32_t)i;
     if (i == n - 1 || (ck[i + 1] >> kWideSegShift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
@@ -688,7 +687,17 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
   bool fresh = true;
   int32_t sb = 0, se = 0, base = 0, fcnt = 0, gk0 = 0;
   int32_t step = 1, nsamp = 0, sU = 0, sL = 0;  // the segment's coarse sample (coarse_range)
-  for (; t < tend; t++, tt++) {
+  auto add_score = [&](int32_t col, int32_t cnt) {
+    const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
+    const uint32_t v = (uint32_t)cnt | (hi16 << 16);
+    if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
+    // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
+    if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
+  };
+  auto close_run = [&](int32_t& cnt, int32_t a, int32_t b) {
+    cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : base);
+  };
+  while (t < tend) {
     while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
       if (++kk == kKeyRange) {
         ++ch;
@@ -716,21 +725,32 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       sU = S > 0 ? U2s[js] : 0;
       sL = S > 0 ? L2s[js] : 0;
     }
-    const int32_t g = gk0 + tt;
-    const int32_t col = (int32_t)(cv.g_key[g] & kColMask);
-    int32_t cnt = fcnt;
-    if (se > sb) {
-      const int32_t pb = cv.g_beg[g], pn = cv.g_beg[g + 1] - pb;
-      int32_t carry = -2;  // the largest B of the valid runs so far (-2: none)
+    const int32_t g0 = gk0 + tt;
+    if (se <= sb) {  // no frame of the segment has a max2 window: every group scores the rest
+      add_score((int32_t)(cv.g_key[g0] & kColMask), fcnt);
+      t++, tt++;
+      continue;
+    }
+    // A batch of consecutive groups of this segment whose points fit the 64 lanes: lane j holds
+    // group j's point range [pj0, pj1) relative to the first point pb0.
+    const int64_t left = min(tend - t, (int64_t)(kend - tt));
+    const int32_t pb0 = cv.g_beg[g0];
+    int32_t pj0 = 0, pj1 = INT32_MAX, colj = 0;
+    if (lane < left) {
+      pj0 = cv.g_beg[g0 + lane] - pb0;
+      pj1 = cv.g_beg[g0 + lane + 1] - pb0;
+      colj = (int32_t)(cv.g_key[g0 + lane] & kColMask);
+    }
+    const int nG = __popcll(__ballot(lane < left && pj1 <= 64));  // (pj1 grows with j: a prefix)
+    if (nG == 0) {
+      // one group with more than 64 points: its points 64 at a time, runs merged across the steps
+      const int32_t pn = __shfl(pj1, 0, 64);
+      int32_t cnt = fcnt, carry = -2, aopen = 0;
       bool open = false;
-      int32_t aopen = 0;
-      auto close = [&](int32_t a, int32_t b) {
-        cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : base);
-      };
       for (int32_t pbase = 0; pbase < pn; pbase += 64) {
         const int32_t i = pbase + lane;
         int32_t A = INT32_MAX, B = -2;
-        const int32_t v = i < pn ? cv.p_m2[pb + i] : 0;
+        const int32_t v = i < pn ? cv.p_m2[pb0 + i] : 0;
         int32_t loA, hiA, loB, hiB;
         coarse_range(sU, nsamp, step, sb, se, v, true, loA, hiA);
         coarse_range(sL, nsamp, step, sb, se, v, false, loB, hiB);
@@ -753,19 +773,68 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
           const int sl = __ffsll((long long)starts) - 1;
           starts &= starts - 1;
           const int32_t as = __shfl(A, sl, 64), ps = __shfl(pe, sl, 64);
-          if (open) close(aopen, ps);
+          if (open) close_run(cnt, aopen, ps);
           open = true;
           aopen = as;
         }
         carry = max(carry, __shfl(bm, 63, 64));
       }
-      if (open) close(aopen, carry);
+      if (open) close_run(cnt, aopen, carry);
+      add_score(__shfl(colj, 0, 64), cnt);
+      t++, tt++;
+      continue;
     }
-    const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
-    const uint32_t v = (uint32_t)cnt | (hi16 << 16);
-    if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
-    // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
-    if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
+    // every point of the batch on its own lane: its group (the last j < nG with pj0 <= lane, by
+    // binary lifting over the lanes' starts) and its run [A, B] of the segment's frames
+    const int32_t npts = __shfl(pj1, nG - 1, 64);
+    int gi = 0;
+#pragma unroll
+    for (int bit = 32; bit >= 1; bit >>= 1) {
+      const int cand = gi + bit;
+      const int32_t x = __shfl(pj0, min(cand, 63), 64);
+      if (cand < nG && x <= lane) gi = cand;
+    }
+    const int32_t gst = __shfl(pj0, gi, 64);  // the first point lane of this lane's group
+    int32_t A = INT32_MAX, B = -2;
+    const int32_t v = lane < npts ? cv.p_m2[pb0 + lane] : 0;
+    {
+      int32_t loA, hiA, loB, hiB;
+      coarse_range(sU, nsamp, step, sb, se, v, true, loA, hiA);
+      coarse_range(sL, nsamp, step, sb, se, v, false, loB, hiB);
+      if (lane < npts) {
+        A = loA + lb32(U2s + loA, hiA - loA, v);
+        B = loB + ub32(L2s + loB, hiB - loB, v) - 1;
+      }
+    }
+    const bool ok = lane < npts && A <= B;
+    int32_t bm = ok ? B : -2;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // running max of B within each group (segmented by gst)
+      const int32_t y = __shfl_up(bm, o, 64);
+      if (lane - o >= gst) bm = max(bm, y);
+    }
+    int32_t pe = __shfl_up(bm, 1, 64);
+    if (lane == gst) pe = -2;
+    const unsigned long long starts = __ballot(ok && A > pe + 1);
+    for (int j = 0; j < nG; j++) {  // per group: its merged runs, counted per query lane
+      const int32_t a0 = __shfl(pj0, j, 64), a1 = __shfl(pj1, j, 64);
+      const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
+      unsigned long long m = starts & rng;
+      int32_t cnt = fcnt, aopen = 0;
+      bool open = false;
+      while (m) {
+        const int sl = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int32_t as = __shfl(A, sl, 64), ps = __shfl(pe, sl, 64);
+        if (open) close_run(cnt, aopen, ps);
+        open = true;
+        aopen = as;
+      }
+      if (open) close_run(cnt, aopen, __shfl(bm, a1 - 1, 64));
+      add_score(__shfl(colj, j, 64), cnt);
+    }
+    t += nG;
+    tt += nG;
   }
 }
 
@@ -828,9 +897,11 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, tmp})
+                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch,
+                  (void*)fq, tmp})
     if (p) (void)hipFree(p);
   touch = nullptr;
+  fq = nullptr;
   ka = kb = nullptr;
   ua = ub = nullptr;
   va = vb = L2s = U2s = P = seg = wpre = cbeg = info = nullptr;
@@ -848,17 +919,17 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
   hipError_t e = hipSuccess;
   if (nf > cap_nf) {
     for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                    (void*)P, tmp})
+                    (void*)P, (void*)fq, tmp})
       if (p) (void)hipFree(p);
     ka = kb = nullptr;
     ua = ub = nullptr;
-    va = vb = L2s = U2s = P = nullptr;
+    va = vb = L2s = U2s = P = fq = nullptr;
     qis = nullptr;
     tmp = nullptr;
     cap_nf = 0;
     if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
         (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
-        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideCh)))
+        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideCh)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
     if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, ua, ub, va, vb, (int)nf, 0, 32, s)) ||
@@ -913,12 +984,14 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   // U2 - L2 lies within a few micro-units of 2 tol (fmt6 rounds both ends): d = U2 - L2 - dbase
   const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
   if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
+  hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(1024, (nq + 255) / 256)), dim3(256), 0, s,
+                     d_qoff, nq, ws->fq);
   // the bad-frame check (a key or a window outside what the cache and the int32 windows hold)
   hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
                      ws->info);
   // one sort by (chunk, key, L2, U2 - L2)
-  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf,
-                     (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, nf, (const int32_t*)nullptr,
+                     dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
   if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, (int)nf, 0, end_bit, s))) return e;
   int32_t info[3] = {0, 0, 0};
@@ -931,7 +1004,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
     hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
     tb = ws->tmp_bytes;
     if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, (int)nf, 0, 32, s))) return e;
-    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, d_qoff, nq, nf, ws->vb, (int64_t)-1,
+    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
                        ws->ka, (int32_t*)nullptr, ws->info);
     tb = ws->tmp_bytes;
     if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, (int)nf, 0, end_bit, s)))
@@ -942,7 +1015,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int64_t n = info[0];
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
   if (n > 0)
-    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, d_qoff, nq, n, ws->kb, order, ws->L2s,
+    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, ws->fq, n, ws->kb, order, ws->L2s,
                        ws->U2s, ws->qis, ws->seg);
   hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, n, nch, ws->cbeg);
   hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->P);
