@@ -286,6 +286,15 @@ int64_t tfo_fmt6(double x) {
 
 /* ---------------------------------------------------------------- per-clip DSP ------ */
 
+/* sum of a[i] * b[i] in 8 interleaved fp32 partial sums, combined as ((s0+s4)+(s2+s6)) +
+ * ((s1+s5)+(s3+s7)): the shape of a vectorised sgemv row dot (sensitivity variants only) */
+static float blocked_dot8(const float* a, const float* b, int n) {
+  float p[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int i;
+  for (i = 0; i < n; i++) p[i & 7] += a[i] * b[i];
+  return ((p[0] + p[4]) + (p[2] + p[6])) + ((p[1] + p[5]) + (p[3] + p[7]));
+}
+
 /* One clip whose aubio_source_do hop values come either from int16 PCM (pcm: s / 32768.f, the
  * 16-bit sndfile/wavread conversion) or are given as fp32 (x: multichannel mean, 24/32-bit or
  * float data, as tfp_wav_decode_f32 restates aubio's source for them). */
@@ -309,19 +318,29 @@ static size_t fingerprint_core(const tfo_tables* t, const int16_t* pcm, const fl
     for (i = 0; i < TFO_WIN - TFO_HOP; i++) dataold[i] = data[i + TFO_HOP];
     for (i = 0; i < TFO_WIN; i++) data[i] *= t->window[i];
     for (i = 0; i < TFO_WIN / 2; i++) { x[i] = data[i + TFO_WIN / 2]; x[i + TFO_WIN / 2] = data[i]; }
-    if (variant) rfft512_norm_variant(t, x, norm, variant);
+    if (variant & 3) rfft512_norm_variant(t, x, norm, variant & 3);
     else rfft512_norm(t, x, norm);
     /* aubio_mfcc_do: filterbank (fmat_vecmul), fvec_log10, DCT (fmat_vecmul) */
-    for (j = 0; j < TFO_FILTERS; j++) band[j] = 0.f;
-    for (i = 0; i < TFO_BINS; i++)
-      for (j = 0; j < TFO_FILTERS; j++) band[j] += norm[i] * t->mel[j][i];
+    if (variant & TFO_VARIANT_FB_BLOCKED) {
+      /* sensitivity variant: a BLAS-style sgemv row dot, 8 interleaved partial sums combined as a
+       * tree (the order a vectorised cblas_sgemv uses instead of fmat_vecmul's sequential sum) */
+      for (j = 0; j < TFO_FILTERS; j++) band[j] = blocked_dot8(norm, t->mel[j], TFO_BINS);
+    } else {
+      for (j = 0; j < TFO_FILTERS; j++) band[j] = 0.f;
+      for (i = 0; i < TFO_BINS; i++)
+        for (j = 0; j < TFO_FILTERS; j++) band[j] += norm[i] * t->mel[j][i];
+    }
     for (j = 0; j < TFO_FILTERS; j++) {
       double v = 2.e-42, b = band[j];
       band[j] = log10f((float)(v > b ? v : b));
     }
-    for (j = 0; j < TFO_COEFS; j++) out[j] = 0.f;
-    for (i = 0; i < TFO_FILTERS; i++)
-      for (j = 0; j < TFO_COEFS; j++) out[j] += band[i] * t->dct[j][i];
+    if (variant & TFO_VARIANT_DCT_BLOCKED) {
+      for (j = 0; j < TFO_COEFS; j++) out[j] = blocked_dot8(band, t->dct[j], TFO_FILTERS);
+    } else {
+      for (j = 0; j < TFO_COEFS; j++) out[j] = 0.f;
+      for (i = 0; i < TFO_FILTERS; i++)
+        for (j = 0; j < TFO_COEFS; j++) out[j] += band[i] * t->dct[j][i];
+    }
     /* fp_handler.c:649-652 */
     for (j = 0; j < TFO_COEFS; j++) {
       double q = 10 * log10(fabs(out[j]));

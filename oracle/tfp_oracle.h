@@ -56,6 +56,11 @@ size_t tfo_fingerprint_batch(const tfo_tables* t, const int16_t* pcm, const int6
 /* The same with another valid fp32 FFT order in place of the canonical one (0), to measure how
  * much the unpinned FFT backend can move the stored values: 1 = radix-2 256-point complex FFT +
  * the canonical real split, 2 = radix-2 512-point complex FFT of the real input. */
+/* variant bits (sensitivity study, scripts/fft_sensitivity.py): (variant & 3) = 1 radix-2 256-point
+ * complex FFT + canonical split, 2 = radix-2 512-point complex FFT of the real input; FB_BLOCKED and
+ * DCT_BLOCKED sum the filterbank / DCT rows in a vectorised-sgemv order instead of fmat_vecmul's */
+#define TFO_VARIANT_FB_BLOCKED 4
+#define TFO_VARIANT_DCT_BLOCKED 8
 size_t tfo_fingerprint_batch_variant(const tfo_tables* t, const int16_t* pcm, const int64_t* offsets,
                                      int nclips, int32_t* micro, double* db, int nthreads, int variant);
 

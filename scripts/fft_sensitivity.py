@@ -1,9 +1,12 @@
-"""How unpinned is the DSP? The canonical FFT against two other valid fp32 FFT
-orders (oracle tfo_fingerprint_batch_variant: 1 = radix-2 256-point complex FFT + the canonical
-real split, 2 = radix-2 512-point complex FFT of the real input), on configs[1]'s data
-(1,024 x 30 s synthetic clips, 960,512 frames) and on configs[2]-style searches.
+"""How unpinned is the DSP? The canonical pipeline against other valid fp32 operation
+orders of the parts a real libaubio build may compute differently (oracle
+tfo_fingerprint_batch_variant): the FFT (1 = radix-2 256-point complex FFT + the canonical real split,
+2 = radix-2 512-point complex FFT of the real input), the filterbank's and the DCT's summation
+order (4 / 8: a vectorised-sgemv row dot, 8 interleaved partial sums combined as a tree, in place of
+aubio's sequential fmat_vecmul, src/fp_handler.c:642 -> aubio_mfcc_do), and their combinations; on
+configs[1]'s data (1,024 x 30 s synthetic clips, 960,512 frames) and on configs[2]-style searches.
 
-Usage: python scripts/fft_sensitivity.py [--clips 1024] [--out profiles/r02/fft_sensitivity.json]"""
+Usage: python scripts/fft_sensitivity.py [--clips 1024] [--out profiles/r03/fft_sensitivity.json]"""
 import argparse
 import json
 import os
@@ -21,6 +24,15 @@ import tiresias_amd as T  # noqa: E402
 NULL = oracle_py.NULL_MICRO
 
 
+VARIANTS = {1: "FFT: radix-2 256-point complex FFT + canonical real split",
+            2: "FFT: radix-2 512-point complex FFT of the real input",
+            4: "filterbank: sgemv-style blocked sum (8 partial sums, tree)",
+            8: "DCT: sgemv-style blocked sum (8 partial sums, tree)",
+            12: "filterbank + DCT blocked",
+            13: "FFT 1 + filterbank + DCT blocked",
+            14: "FFT 2 + filterbank + DCT blocked"}
+
+
 def box_member(m, tol_micro=1000):
     """Would a stored max1 of m micro-units fall in its own integer key's box at tol 0.001?"""
     r = np.round(m / 1e6) * 1e6
@@ -33,7 +45,7 @@ def main():
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--db-clips", type=int, default=2000)
     ap.add_argument("--queries", type=int, default=256)
-    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r02", "fft_sensitivity.json"))
+    ap.add_argument("--out", default=os.path.join(REPO, "profiles", "r03", "fft_sensitivity.json"))
     a = ap.parse_args()
     n = 8000 * 30
     t0 = time.time()
@@ -41,8 +53,7 @@ def main():
     off = np.arange(a.clips + 1, dtype=np.int64) * n
     base, dbase = oracle_py.fingerprint_batch(pcm.reshape(-1), off, nthreads=a.threads)
     res = {"workload": f"configs[1] data: {a.clips} x 30 s synthetic clips ({len(base)} frames)", "variants": {}}
-    for v, name in ((1, "radix-2 256-point complex FFT + canonical real split"),
-                    (2, "radix-2 512-point complex FFT of the real input")):
+    for v, name in VARIANTS.items():
         mic, db = oracle_py.fingerprint_batch(pcm.reshape(-1), off, nthreads=a.threads, fft_variant=v)
         d1 = base[:, 0] != mic[:, 0]
         d2 = base[:, 1] != mic[:, 1]
@@ -51,7 +62,7 @@ def main():
         delta = np.abs(base.astype(np.int64) - mic.astype(np.int64))[both.all(1)]
         k0 = np.trunc(np.where(np.isfinite(dbase[:, 0]), dbase[:, 0], 0.0))
         k1 = np.trunc(np.where(np.isfinite(db[:, 0]), db[:, 0], 0.0))
-        res["variants"][name] = {
+        res["variants"][name] = {"variant": v,
             "frames_m1_differs": float(d1.mean()), "frames_m2_differs": float(d2.mean()),
             "frames_any_differs": float((d1 | d2).mean()),
             "null_status_differs": float(nullflip.any(1).mean()),
@@ -73,7 +84,7 @@ def main():
     qoff = np.arange(nq + 1, dtype=np.int64) * qn
     rank = np.arange(nd, dtype=np.int32)
     out = {}
-    for v in (0, 1, 2):
+    for v in (0, *VARIANTS):
         dm, _ = oracle_py.fingerprint_batch(dpcm.reshape(-1), doff, nthreads=a.threads, want_db=False, fft_variant=v)
         _, qdb = oracle_py.fingerprint_batch(qpcm, qoff, nthreads=a.threads, fft_variant=v)
         idx = oracle_py.SortedIndex(dm[:, 0], dm[:, 1], np.repeat(np.arange(nd, dtype=np.int32), len(dm) // nd), rank)
@@ -82,13 +93,13 @@ def main():
             w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], np.arange(nq + 1) * nfq, coefs, tol, nthreads=a.threads)
             out.setdefault((coefs, tol), {})[v] = (w, mc)
     res["search"] = {"workload": f"{nq} x 5 s queries (75 % excerpts) vs {nd} x 30 s clips, DB and queries "
-                                 f"fingerprinted with each FFT order"}
+                                 f"fingerprinted with each variant (variant numbers as in 'variants')"}
     for (coefs, tol), r in out.items():
         w0, m0 = r[0]
         res["search"][f"coefs={coefs} tol={tol}"] = {
             "found_canonical": int((w0 >= 0).sum()),
-            **{f"result_differs_variant{v}": float(((r[v][0] != w0) | (r[v][1] != m0)).mean()) for v in (1, 2)},
-            **{f"winner_differs_variant{v}": float((r[v][0] != w0).mean()) for v in (1, 2)}}
+            **{f"result_differs_variant{v}": float(((r[v][0] != w0) | (r[v][1] != m0)).mean()) for v in VARIANTS},
+            **{f"winner_differs_variant{v}": float((r[v][0] != w0).mean()) for v in VARIANTS}}
     res["seconds"] = time.time() - t0
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(res, open(a.out, "w"), indent=1)
