@@ -43,6 +43,9 @@ struct DevBuf {
     if (e == hipSuccess) bytes = want;
     return e;
   }
+  // for buffers that grow a little per call (the merged index): 1/8 headroom, so a run of
+  // enrolments does not free and reallocate hundreds of MB each time
+  hipError_t reserve_grow(size_t n) { return n <= bytes ? hipSuccess : reserve(n + n / 8); }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
@@ -138,7 +141,8 @@ struct tfp_engine {
   int32_t ncols = 0;       // live clips
   std::vector<int32_t> col_clip;                 // column (uuid rank) -> clip id
   std::vector<int32_t> tiekey_host;              // column -> tie-break key
-  std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> column
+  std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> column (with an override)
+  bool key_identity = true;                      // no override: key == column
   std::vector<int32_t> tiebreak_override;        // clip id -> key (empty = uuid rank)
 
   // scratch
@@ -184,6 +188,7 @@ struct tfp_engine {
   FpLaunchCfg fpcfg;
   int32_t class_ku_max = 10;  // TFP_VOTE_CLASS_MAX: pattern-class vote up to this many used keys (-1: always the GEMM)
   bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
+  bool dbg_index = false;     // TFP_DEBUG_INDEX: log each index update's phases (host ms)
   int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
@@ -538,8 +543,18 @@ void live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* liv
     for (int32_t i = (int32_t)e->built_clips; i < (int32_t)e->clips.size(); i++)
       if (e->clips[i].alive) add.push_back(i);
     std::sort(add.begin(), add.end(), by_uuid);
-    live->resize(old.size() + add.size());
-    std::merge(old.begin(), old.end(), add.begin(), add.end(), live->begin(), by_uuid);
+    // each new uuid's place by binary search, the old runs between them copied whole: log C
+    // string compares per new clip instead of a linear merge (each compare is two uuid strings
+    // on the heap, a cache miss apiece: ~10 ms at 100k clips)
+    live->reserve(old.size() + add.size());
+    auto from = old.begin();
+    for (int32_t a : add) {
+      const auto at = std::lower_bound(from, old.end(), a, by_uuid);
+      live->insert(live->end(), from, at);
+      live->push_back(a);
+      from = at;
+    }
+    live->insert(live->end(), from, old.end());
   } else {
     for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
       if (e->clips[i].alive) live->push_back(i);
@@ -592,9 +607,9 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
   int64_t valid = 0;
   if (n > 0 && (rc = sort_staged_rows(e, b, n, &valid))) return rc;
   const int64_t R = e->nrows;
-  HIPCHK(e, e->m1s_b.reserve(sizeof(int32_t) * (R + valid + 1)));
-  HIPCHK(e, e->m2s_b.reserve(sizeof(int32_t) * (R + valid + 1)));
-  HIPCHK(e, e->cols_b.reserve(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->m1s_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->m2s_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->cols_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
   int64_t kept = R;
   HIPCHK(e, launch_merge_update(e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->remap.as<int32_t>(),
                                 removed, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
@@ -613,6 +628,9 @@ int full_index(tfp_engine* e);
 int rebuild(tfp_engine* e) {
   if (!e->dirty) return TFP_OK;
   int rc;
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
   // Incremental (merge) when there is an index to merge into, the new rows are few next to it, and
   // the staging area needs no compaction (the staged rows since the last build are then exactly
   // rows [built_staged, n_staged)); otherwise the full build.
@@ -631,22 +649,32 @@ int rebuild(tfp_engine* e) {
   }
   std::vector<int32_t> live, rank;
   live_order(e, incremental, &live, &rank);
+  const double t_order = ms_since(t0);
   std::vector<int32_t> tiekey(std::max<size_t>(live.size(), 1), 0);
+  // key -> column: the identity without an override (the key is the uuid rank), so no map is built
+  // (a 100k-entry hash map was most of an enrolment's host time); with one, a map that also
+  // rejects a key given twice
   std::unordered_map<int32_t, int32_t> key_col;
   const bool ovr = !e->tiebreak_override.empty();
+  if (ovr) key_col.reserve(live.size());
   for (size_t r = 0; r < live.size(); r++) {
     const int32_t clip = live[r];
+    if (!ovr) {
+      tiekey[r] = (int32_t)r;
+      continue;
+    }
     // With an override every live clip needs its own key (a clip added after the override would
     // otherwise take its local rank, which can equal another shard's global key).
-    if (ovr && (size_t)clip >= e->tiebreak_override.size())
+    if ((size_t)clip >= e->tiebreak_override.size())
       return fail(e, TFP_E_ARG, "clip %s was added after tfp_index_set_tiebreak: set the tie-break keys again",
                   e->clips[clip].uuid.c_str());
-    const int32_t k = ovr ? e->tiebreak_override[clip] : (int32_t)r;
+    const int32_t k = e->tiebreak_override[clip];
     if (!key_col.emplace(k, (int32_t)r).second) return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
     tiekey[r] = k;
   }
   if ((rc = upload(e, e->rank_of_clip, rank.data(), sizeof(int32_t) * rank.size()))) return rc;
   if ((rc = upload(e, e->tiekey, tiekey.data(), sizeof(int32_t) * tiekey.size()))) return rc;
+  const double t_keys = ms_since(t0);
   if (incremental) {
     if ((rc = merge_index(e, rank))) return rc;
     e->n_merges++;
@@ -659,12 +687,16 @@ int rebuild(tfp_engine* e) {
   e->col_clip = std::move(live);
   e->tiekey_host = std::move(tiekey);
   e->key_col = std::move(key_col);
+  e->key_identity = !ovr;
   e->built = true;
   e->built_clips = e->clips.size();
   e->built_staged = e->n_staged;
   e->dirty = false;
   e->rng_valid = false;  // the key-range and clip-set caches follow the index
   e->cell_fresh = false;
+  if (e->dbg_index)
+    fprintf(stderr, "[tfp] index %s: %lld rows, %d clips; order %.3f keys %.3f total %.3f ms\n",
+            incremental ? "merge" : "full build", (long long)e->nrows, e->ncols, t_order, t_keys, ms_since(t0));
   return TFP_OK;
 }
 
@@ -912,6 +944,13 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   return TFP_OK;
 }
 
+// The index column of a tie-break key (-1: none).
+int32_t col_of_key(const tfp_engine* e, int32_t k) {
+  if (e->key_identity) return k >= 0 && (size_t)k < e->col_clip.size() ? k : -1;
+  auto it = e->key_col.find(k);
+  return it == e->key_col.end() ? -1 : it->second;
+}
+
 void fill_results(tfp_engine* e, const std::vector<unsigned long long>& keys, const int64_t* qoff, int32_t nq,
                   tfp_result* out) {
   for (int32_t i = 0; i < nq; i++) {
@@ -921,9 +960,9 @@ void fill_results(tfp_engine* e, const std::vector<unsigned long long>& keys, co
     r.clip_id = -1;
     const unsigned long long k = keys[i];
     if (!k) continue;
-    auto it = e->key_col.find((int32_t)(uint32_t)(k & 0xffffffffu));
-    if (it == e->key_col.end()) continue;
-    const int32_t clip = e->col_clip[it->second];
+    const int32_t col = col_of_key(e, (int32_t)(uint32_t)(k & 0xffffffffu));
+    if (col < 0) continue;
+    const int32_t clip = e->col_clip[col];
     r.found = 1;
     r.match_count = (int32_t)(k >> 32);
     r.clip_id = clip;
@@ -968,6 +1007,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   }
   if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
   e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
+  e->dbg_index = getenv("TFP_DEBUG_INDEX") != nullptr;
   if (const char* v = getenv("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
   e->force_full = getenv("TFP_INDEX_FULL") != nullptr;
   if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
@@ -1301,9 +1341,9 @@ int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {
 int tfp_index_uuid_of_key(tfp_engine* e, int32_t key, char* uuid, int32_t len) {
   if (!e || !uuid || len <= 0) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
-  auto it = e->key_col.find(key);
-  if (it == e->key_col.end()) return fail(e, TFP_E_NOENT, "no clip with key %d", key);
-  snprintf(uuid, len, "%s", e->clips[e->col_clip[it->second]].uuid.c_str());
+  const int32_t col = col_of_key(e, key);
+  if (col < 0) return fail(e, TFP_E_NOENT, "no clip with key %d", key);
+  snprintf(uuid, len, "%s", e->clips[e->col_clip[col]].uuid.c_str());
   return TFP_OK;
 }
 
