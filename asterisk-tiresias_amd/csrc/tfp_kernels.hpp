@@ -211,7 +211,7 @@ struct WideScratch {
   int32_t *L2s = nullptr, *U2s = nullptr;           // sorted windows
   uint8_t* qis = nullptr;                            // sorted frames' query within its chunk
   int32_t* fq = nullptr;                             // [nf] each frame's query
-  int32_t* P = nullptr;                              // [nf][kChunk] in-chunk prefix counts
+  uint16_t* P = nullptr;                             // [nf][kChunk] in-chunk prefix counts (< 2^16: every query < 65536 frames)
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
   int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk

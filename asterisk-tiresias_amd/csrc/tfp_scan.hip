@@ -114,6 +114,16 @@ __global__ void key_gbeg_kernel(const uint32_t* __restrict__ g_key, int64_t n1, 
   if (t <= kKeyRange) k_gbeg[t] = (int32_t)lower_bound_t<uint32_t>(g_key, n1, (uint32_t)t << kColBits);
 }
 
+// The sweep's frame sorts (0.6 M pairs at C3): hipCUB's dispatch (a merge sort below 2^20 items,
+// 0.17 ms at C3). rocPRIM's onesweep forced instead measured slower there (6 digit passes of
+// 23 us: 0.18 ms).
+template <class K>
+hipError_t sweep_sort_pairs(void* tmp, size_t& bytes, const K* kin, K* kout, const int32_t* vin, int32_t* vout, int64_t n,
+                            unsigned end_bit, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, (int)end_bit, s);
+}
+
+constexpr unsigned kKeysBlocks = 512;  // wide_keys_c_kernel's grid cap (one atomic per block)
 inline unsigned grid_for(int64_t n) {
   int64_t g = (n + 255) / 256;
   if (g > 8192) g = 8192;
@@ -488,14 +498,23 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
     ck[i] = key;
     if (fo) fo[i] = f;
   }
-  // one atomic per wave (same-address atomics serialise in L2: one per frame cost ~0.13 ms at C3)
+  // one atomic per block, on a grid of at most kKeysBlocks blocks: same-address atomics serialise in
+  // L2 (one per frame cost ~0.13 ms at C3, and one per wave still ~0.1 ms: 10k waves)
+  __shared__ int32_t red[2][256 / 64];
   for (int o = 32; o > 0; o >>= 1) {
     kept += __shfl_xor(kept, o, 64);
     wide += __shfl_xor(wide, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
-    if (kept) atomicAdd(&info[0], kept);
-    if (wide) atomicAdd(&info[2], wide);
+    red[0][threadIdx.x >> 6] = kept;
+    red[1][threadIdx.x >> 6] = wide;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t k = 0, w = 0;
+    for (int i = 0; i < 256 / 64; i++) k += red[0][i], w += red[1][i];
+    if (k) atomicAdd(&info[0], k);
+    if (w) atomicAdd(&info[2], w);
   }
 }
 
@@ -528,7 +547,7 @@ __global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, int6
 // by the waves before it). Lane q counts query q among 64 frames by reading their queries out of
 // the lanes (no per-frame memory dependency).
 __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg,
-                                                           const uint8_t* __restrict__ qis, int32_t* __restrict__ P) {
+                                                           const uint8_t* __restrict__ qis, uint16_t* __restrict__ P) {
   __shared__ int32_t tot[16][kWideCh];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int32_t b = cbeg[blockIdx.x], n = cbeg[blockIdx.x + 1] - b;
@@ -546,12 +565,12 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   for (int w = 0; w < wv; w++) run += tot[w][lane];
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
-    int32_t* row = P + ((int64_t)b + i) * kWideCh + lane;
+    uint16_t* row = P + ((int64_t)b + i) * kWideCh + lane;
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
       run += __builtin_amdgcn_readlane(x, j) == lane;
-      if (j < m) row[(int64_t)j * kWideCh] = run;
+      if (j < m) row[(int64_t)j * kWideCh] = (uint16_t)run;
     }
   }
 }
@@ -656,7 +675,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
                                                           const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
                                                           const int32_t* __restrict__ cbeg, CellView cv,
                                                           const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
-                                                          const int32_t* __restrict__ U2s, const int32_t* __restrict__ P,
+                                                          const int32_t* __restrict__ U2s, const uint16_t* __restrict__ P,
                                                           int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch) {
   const int lane = threadIdx.x & 63;
   const int64_t W0 = chw[ch0], W1 = chw[ch1];
@@ -695,7 +714,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
   };
   auto close_run = [&](int32_t& cnt, int32_t a, int32_t b) {
-    cnt += P[(int64_t)b * kWideCh + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideCh + lane] : base);
+    cnt += (int32_t)P[(int64_t)b * kWideCh + lane] - (a > sb ? (int32_t)P[(int64_t)(a - 1) * kWideCh + lane] : base);
   };
   while (t < tend) {
     while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
@@ -715,8 +734,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       sb = sg[2 * kk];
       se = sg[2 * kk + 1];
       const int32_t fb = sg[2 * (kk | kKeyRange)], fe = sg[2 * (kk | kKeyRange) + 1];
-      base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
-      fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
+      base = se > sb && sb > cb ? (int32_t)P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
+      fcnt = fe > fb ? (int32_t)P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? (int32_t)P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
       gk0 = k_gbeg[kk] - wp[kk];
       const int32_t S = se - sb;
       step = S > 64 ? (S + 63) / 64 : 1;
@@ -904,7 +923,8 @@ void WideScratch::release() {
   fq = nullptr;
   ka = kb = nullptr;
   ua = ub = nullptr;
-  va = vb = L2s = U2s = P = seg = wpre = cbeg = info = nullptr;
+  va = vb = L2s = U2s = seg = wpre = cbeg = info = nullptr;
+  P = nullptr;
   chw = nullptr;
   score = nullptr;
   qis = nullptr;
@@ -923,7 +943,8 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
       if (p) (void)hipFree(p);
     ka = kb = nullptr;
     ua = ub = nullptr;
-    va = vb = L2s = U2s = P = fq = nullptr;
+    va = vb = L2s = U2s = fq = nullptr;
+    P = nullptr;
     qis = nullptr;
     tmp = nullptr;
     cap_nf = 0;
@@ -932,8 +953,8 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
         (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideCh)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, t1, ua, ub, va, vb, (int)nf, 0, 32, s)) ||
-        (e = hipcub::DeviceRadixSort::SortPairs(nullptr, t2, ka, kb, va, vb, (int)nf, 0, 64, s)))
+    if ((e = sweep_sort_pairs<uint32_t>(nullptr, t1, ua, ub, va, vb, nf, 32, s)) ||
+        (e = sweep_sort_pairs<unsigned long long>(nullptr, t2, ka, kb, va, vb, nf, 64, s)))
       return e;
     tmp_bytes = t1 > t2 ? t1 : t2;
     if ((e = hipMalloc(&tmp, tmp_bytes > 0 ? tmp_bytes : 1))) return e;
@@ -990,10 +1011,10 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
                      ws->info);
   // one sort by (chunk, key, L2, U2 - L2)
-  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, nf, (const int32_t*)nullptr,
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, (const int32_t*)nullptr,
                      dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
-  if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, (int)nf, 0, end_bit, s))) return e;
+  if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
   int32_t info[3] = {0, 0, 0};
   if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
   if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
@@ -1003,11 +1024,11 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
     if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
     hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
     tb = ws->tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, (int)nf, 0, 32, s))) return e;
-    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
+    if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
+    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
                        ws->ka, (int32_t*)nullptr, ws->info);
     tb = ws->tmp_bytes;
-    if ((e = hipcub::DeviceRadixSort::SortPairs(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, (int)nf, 0, end_bit, s)))
+    if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, end_bit, s)))
       return e;
     if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
     order = ws->va;
