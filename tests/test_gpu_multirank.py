@@ -4,7 +4,11 @@ shard, joined by gloo. Each rank: tfp_index_set_tiebreak with the global uuid ra
 QueryShardedSearch (fingerprint 1/N of the queries, all_gather of the frame values,
 tfp_search_q_device on the local clips, all_reduce(MAX) of the keys) and the batch-1 key
 combine. Every key must equal the unsharded engine's and the oracle's (count(*) DESC, ties to the
-greatest audio_uuid: src/fp_handler.c:367-374)."""
+greatest audio_uuid: src/fp_handler.c:367-374).
+
+World 1 runs the same step over RCCL (backend "nccl"), the backend bench.py's N-GPU runs use: its
+all_gather_into_tensor of the frame values and an explicit int64 all_reduce(MAX) of the keys
+(identities at one rank, but the RCCL calls, dtypes and tensor shapes of the N-GPU path)."""
 import json
 import os
 import socket
@@ -27,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_path):
+def _worker(rank, world, port, out_path, backend="gloo"):
     import sys
     sys.path.insert(0, PKG)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -37,9 +41,9 @@ def _worker(rank, world, port, out_path):
     import tiresias_amd as T
     from tiresias_amd import sharding
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     stream = torch.cuda.current_stream().cuda_stream
     nclips, n_db, qn = 60, 8000 * 10, 8000 * 3
     nf_db = (n_db + 255) // 256
@@ -55,7 +59,7 @@ def _worker(rank, world, port, out_path):
     fr = eng.fingerprint_batch(pcm[mine].reshape(-1), np.arange(len(mine) + 1) * n_db)
     eng.index_add_batch([uuids[c] for c in mine], np.arange(len(mine) + 1) * nf_db, fr["m1"], fr["m2"])
     eng.set_tiebreak(grank[mine])
-    nq = 12 * world
+    nq = 12 * max(world, 2)
     qsrc = [(SEED_DB, src[int(rng.integers(nclips))], 256 * int(rng.integers(0, 100)) + int(rng.integers(0, 3)) * 17)
             if i % 4 != 3 else (SEED_Q, i, 0) for i in range(nq)]
     qpcm = np.stack([T.synth_pcm(sd, [c], qn, offsets=[o])[0] for sd, c, o in qsrc])
@@ -65,6 +69,8 @@ def _worker(rank, world, port, out_path):
         keys = torch.zeros(nq, dtype=torch.int64, device=dev)
         qs = sharding.QueryShardedSearch(eng, torch, dev, dist, nq, qn)
         qs(d_q.data_ptr(), p, keys, stream)
+        if backend == "nccl":  # sharding.combine skips a 1-rank group: run the RCCL reduction anyway
+            dist.all_reduce(keys, op=dist.ReduceOp.MAX)
         torch.cuda.synchronize()
         out["batch"].append([int(v) for v in keys.cpu().numpy().view(np.uint64)])
     # batch-1: local small-path result -> global key -> 8-byte all_reduce(MAX)
@@ -72,7 +78,7 @@ def _worker(rank, world, port, out_path):
         res, _ = eng.search_pcm_batch(qpcm[i], [0, qn], T.params(1, 0.001))
         r = res[0]
         k = torch.tensor([sharding.make_key(r["match_count"], grank[uuids.index(r["audio_uuid"])]) if r else 0],
-                         dtype=torch.int64)
+                         dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         sharding.combine(k, dist)
         out["single"].append(int(k.item()))
     if rank == 0:
@@ -106,12 +112,12 @@ def _worker(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_hip_engine_equals_unsharded(tmp_path, world):
+@pytest.mark.parametrize("world,backend", [(1, "nccl"), (2, "gloo"), (3, "gloo")])
+def test_sharded_hip_engine_equals_unsharded(tmp_path, world, backend):
     torch = pytest.importorskip("torch")
     import torch.multiprocessing as mp
     out = str(tmp_path / "res.json")
-    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), out, backend), nprocs=world, join=True)
     r = json.load(open(out))
     assert r["batch"] == r["expect_oracle"] == r["expect_engine"]
     assert r["single"] == r["expect_oracle"][0][:6]
