@@ -10,7 +10,8 @@ import os
 import re
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libtiresias_fp.so")
+# TFP_LIB_PATH: another build of the same library (kernel A/B experiments, scripts/ab_libs.sh)
+LIB_PATH = os.environ.get("TFP_LIB_PATH") or os.path.join(PKG_ROOT, "lib", "libtiresias_fp.so")
 HEADER = os.path.join(os.path.dirname(PKG_ROOT), "include", "tiresias_fp.h")
 
 TFP_OK = 0
