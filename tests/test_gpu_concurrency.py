@@ -68,3 +68,82 @@ def test_concurrent_searches_equal_serial(engine, oracle, tfp_lib):
     assert not any(th.is_alive() for th in threads), "a caller thread did not finish"
     assert not errors, errors[:5]
     assert any(v[0] is not None for v in want.values())
+
+
+def test_group_concurrent_searches_during_enrolment(oracle, tfp_lib):
+    """The shim's device group (tfp_group_*) under the module's real mix: channel threads
+    searching while the load / CLI thread enrols and deletes (src/app_tiresias.c:413,
+    src/cli_handler.c). The enrolled-and-deleted clips hold only NULL rows (a file whose every
+    coefficient printed as inf: src/fp_handler.c:649-652), which no box ever matches, so every
+    search must equal its serial answer whatever the interleaving, while each enrolment and
+    deletion forces an index merge on a shard between the searches."""
+    g = tfp_lib.Group([0, 0, 0])
+    class _Rows:  # _build_db's rows and uuids, added to the group below instead of an engine
+        def index_clear(self):
+            pass
+
+        def index_add(self, *a):
+            pass
+
+    uuids, micro, _ = _build_db(_Rows(), oracle, tfp_lib, 120, 12)
+    nf = len(micro) // 120
+    for c in range(120):
+        g.index_add(uuids[c], micro[c * nf:(c + 1) * nf, 0], micro[c * nf:(c + 1) * nf, 1])
+    g.index_commit()
+    qpcm = _queries(tfp_lib, 24, 120, 12, 5)
+    n = qpcm.shape[1]
+    params = [tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.1), tfp_lib.params(2, 0.5)]
+    want = {}
+    for pi, p in enumerate(params):
+        r, f = g.search_pcm_batch(qpcm.reshape(-1), np.arange(25) * n, p)
+        for q in range(24):
+            want[pi, q] = (_key(r[q]), f[q])
+    assert any(v[0] is not None for v in want.values())
+    null_rows = np.full(nf, tfp_lib.NULL_MICRO, np.int32)
+    errors, stop = [], threading.Event()
+
+    def searcher(t):
+        rng = np.random.default_rng(200 + t)
+        try:
+            for it in range(10):
+                pi = int(rng.integers(len(params)))
+                q0 = int(rng.integers(0, 22))
+                k = 1 if it % 2 else 3
+                r, f = g.search_pcm_batch(qpcm[q0:q0 + k].reshape(-1), np.arange(k + 1) * n, params[pi])
+                got = [(_key(a), b) for a, b in zip(r, f)]
+                exp = [want[pi, q] for q in range(q0, q0 + k)]
+                if got != exp:
+                    errors.append((t, it, pi, q0, got, exp))
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append((t, repr(ex)))
+
+    def enroller():
+        i = 0
+        try:
+            while not stop.is_set() and i < 200:
+                u = "%08x-0000-4000-8000-%012x" % (0xE0000000 + i, i)
+                g.index_add(u, null_rows, null_rows)
+                if i % 3 == 2:
+                    g.index_remove(u)
+                i += 1
+        except Exception as ex:  # pragma: no cover
+            errors.append(("enrol", repr(ex)))
+
+    threads = [threading.Thread(target=searcher, args=(t,)) for t in range(6)]
+    en = threading.Thread(target=enroller)
+    en.start()
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join(timeout=200)
+    stop.set()
+    en.join(timeout=100)
+    assert not any(th.is_alive() for th in threads + [en]), "a caller thread did not finish"
+    assert not errors, errors[:5]
+    # the NULL-row clips are enrolled (and counted) but never match
+    nrows, nclips = g.index_stats()
+    assert nclips > 120
+    for pi, p in enumerate(params):
+        r, f = g.search_pcm_batch(qpcm.reshape(-1), np.arange(25) * n, p)
+        assert [(_key(r[q]), f[q]) for q in range(24)] == [want[pi, q] for q in range(24)]
+    g.close()
