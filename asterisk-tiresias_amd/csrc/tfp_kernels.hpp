@@ -219,9 +219,13 @@ struct WideScratch {
   uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
   uint8_t* touch = nullptr;                          // [slab][C] 1 = the chunk scored the clip; zero between calls
   int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
+  int32_t* doff = nullptr;                           // [nchunks * kKeyRange + 1] each window segment's directory offset
+  int32_t* dtab = nullptr;                           // [<= 4 nf] segment directories: first frame per L2 / U2 bucket
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  int64_t cap_nf = 0, cap_nch = 0, cap_score = 0;
+  void* dtmp = nullptr;                              // the directory offsets' scan
+  size_t dtmp_bytes = 0;
+  int64_t cap_nf = 0, cap_nch = 0, cap_score = 0, cap_dtab = 0;
   int32_t slab = 0;                                  // chunks per groups launch
   hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
   void release();

@@ -542,6 +542,92 @@ __global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, int6
   if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << kWideChunkShift);
 }
 
+// Segment directories. A window segment's S frames are sorted by L2 (and U2); its directory has
+// NB = 2^ceil(log2 S) buckets over each bound's range: TL[b] = the first frame whose L2 >=
+// L2min + (b << shift), TU[b] the same for U2 (se if none), shift the least that fits the wider
+// range into NB buckets. A point v's first U2 >= v and first L2 > v then lie inside one bucket's
+// [T[b], T[b + 1]] (b = v's bucket): one table load and a search over the bucket's few frames,
+// instead of a search over the whole segment.
+#ifndef TFP_DIR_SCALE
+#define TFP_DIR_SCALE 2
+#endif
+constexpr int kDirScale = TFP_DIR_SCALE;  // NB = 2^(ceil(log2 S) + kDirScale)
+__device__ __forceinline__ int dir_log2(int32_t S) { return (S <= 1 ? 0 : 32 - __clz(S - 1)) + kDirScale; }
+__device__ __forceinline__ int dir_shift(int64_t range, int lg) {
+  const int bits = range > 0 ? 64 - __clzll((unsigned long long)range) : 0;
+  return bits > lg ? bits - lg : 0;
+}
+
+// Directory sizes: nb[ch * kKeyRange + k] = 2 NB of chunk ch's window segment of key k (0: empty);
+// nb[nch * kKeyRange] = 0 (the scan's total).
+__global__ void wide_dir_count_kernel(const int32_t* __restrict__ seg, int64_t nch, int32_t* __restrict__ nb) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t > nch * kKeyRange) return;
+  int32_t v = 0;
+  if (t < nch * kKeyRange) {
+    const int64_t ch = t / kKeyRange, k = t % kKeyRange;
+    const int32_t* sg = seg + ch * kWideSegs * 2 + 2 * k;
+    const int32_t S = sg[1] - sg[0];
+    v = S > 0 ? 2 << dir_log2(S) : 0;
+  }
+  nb[t] = v;
+}
+
+// The directories, from the sorted frames: frame i of a window segment is the first frame of the
+// buckets after its predecessor's bucket up to its own (each bucket written once), the last frame
+// also fills the buckets after its own with se. Lanes write short runs themselves; a long run (a
+// sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
+// buckets per step, so no lane loops over thousands of buckets alone.
+__global__ void wide_dir_fill_kernel(int64_t n, const unsigned long long* __restrict__ ck, const int32_t* __restrict__ seg,
+                                     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s,
+                                     const int32_t* __restrict__ doff, int32_t* __restrict__ dtab) {
+  constexpr int32_t kShort = 8;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; i0 < n; i0 += nw * 64) {
+    const int64_t i = i0 + lane;
+    // this lane's runs: [lo, hi] of table entries at base + (lo..hi), value v (up to 4: L2, U2, tails)
+    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
+    if (i < n) {
+      const unsigned long long sgk = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
+      const int32_t skey = (int32_t)(sgk & (kWideSegs - 1));
+      if (skey < kKeyRange) {  // (no max2 window: no searches, no directory)
+        const int64_t ch = (int64_t)(sgk >> 11);
+        const int32_t sb = seg[2 * sgk], se = seg[2 * sgk + 1];
+        const int lg = dir_log2(se - sb);
+        const int32_t nbk = 1 << lg;
+        const int32_t l2min = L2s[sb], u2min = U2s[sb];
+        const int shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
+        const int32_t t0 = doff[ch * kKeyRange + skey];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int32_t* X = h ? U2s : L2s;
+          const int64_t mn = h ? u2min : l2min;
+          const int32_t bi = (int32_t)(((int64_t)X[i] - mn) >> shf);
+          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)X[i - 1] - mn) >> shf);
+          base[h] = base[2 + h] = t0 + h * nbk;
+          lo[h] = bp + 1, hi[h] = bi, val[h] = (int32_t)i;
+          if (i == se - 1) lo[2 + h] = bi + 1, hi[2 + h] = nbk - 1, val[2 + h] = se;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int32_t len = hi[r] - lo[r] + 1;
+      if (len > 0 && len <= kShort)
+        for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
+      unsigned long long m = __ballot(len > kShort);
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64),
+                      o = __shfl(base[r], l, 64);
+        for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
+      }
+    }
+  }
+}
+
 // In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i]: one 16-wave workgroup per
 // chunk, each wave over a contiguous 64-aligned share (its counts first, then the writes, offset
 // by the waves before it). Lane q counts query q among 64 frames by reading their queries out of
@@ -649,24 +735,6 @@ __device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) 
   return lo;
 }
 
-// Coarse sample of a segment's sorted bounds across the wave's lanes: lane j holds a[sb + j step]
-// (j < ns samples). Returns [lo, hi) of a that holds the first index whose value is >= v (ge) or
-// > v (!ge): every sample before it fails the test and the next one passes, so the search is
-// over at most step entries. Lanes search their own v among the samples through ds_bpermute, by
-// binary lifting in 7 uniform steps (every lane takes part in every exchange: call it converged).
-__device__ __forceinline__ void coarse_range(int32_t samp, int32_t ns, int32_t step, int32_t sb, int32_t se, int32_t v,
-                                             bool ge, int32_t& lo, int32_t& hi) {
-  int32_t a = 0;  // count of samples that fail (value < v, or <= v); the samples are sorted
-#pragma unroll
-  for (int bit = 64; bit >= 1; bit >>= 1) {
-    const int32_t cand = a + bit;
-    const int32_t x = __shfl(samp, min(cand, 64) - 1, 64);
-    if (cand <= ns && (ge ? x < v : x <= v)) a = cand;
-  }
-  lo = a ? sb + (a - 1) * step + 1 : sb;
-  hi = a < ns ? sb + a * step + 1 : se;
-}
-
 // The work items (chunk, key, clip group) of chunks [ch0, ch1), in chunk and key order; each wave
 // takes a contiguous share, so it locates its first item by binary search and then steps through
 // keys and chunks. Lane q = query 64 ch + q. A group's counts go to the slab's score rows as 16-bit
@@ -676,7 +744,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
                                                           const int32_t* __restrict__ cbeg, CellView cv,
                                                           const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
                                                           const int32_t* __restrict__ U2s, const uint16_t* __restrict__ P,
-                                                          int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch) {
+                                                          int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch,
+                                                          const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab) {
   const int lane = threadIdx.x & 63;
   const int64_t W0 = chw[ch0], W1 = chw[ch1];
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -705,13 +774,33 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
   int32_t kend = wp[kk + 1];
   bool fresh = true;
   int32_t sb = 0, se = 0, base = 0, fcnt = 0, gk0 = 0;
-  int32_t step = 1, nsamp = 0, sU = 0, sL = 0;  // the segment's coarse sample (coarse_range)
+  int32_t nbk = 1, shf = 0, l2min = 0, u2min = 0;  // the segment's directory
+  const int32_t* TL = dtab;
   auto add_score = [&](int32_t col, int32_t cnt) {
     const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
     const uint32_t v = (uint32_t)cnt | (hi16 << 16);
     if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
     // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
     if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
+  };
+  // v's run in the segment: A = first frame with U2 >= v, B = last frame with L2 <= v
+  auto find_ab = [&](int32_t v, int32_t& A, int32_t& B) {
+    const int64_t dv = (int64_t)v - l2min;
+    if (dv < 0) {
+      B = sb - 1;
+    } else {
+      const int32_t b = (int32_t)min<int64_t>(dv >> shf, nbk - 1);
+      const int32_t lo = TL[b], hi = b + 1 < nbk ? TL[b + 1] : se;
+      B = lo + ub32(L2s + lo, hi - lo, v) - 1;
+    }
+    const int64_t du = (int64_t)v - u2min;
+    if (du <= 0) {
+      A = sb;
+    } else {
+      const int32_t b = (int32_t)min<int64_t>(du >> shf, nbk - 1);
+      const int32_t lo = TL[nbk + b], hi = b + 1 < nbk ? TL[nbk + b + 1] : se;
+      A = lo + lb32(U2s + lo, hi - lo, v);
+    }
   };
   auto close_run = [&](int32_t& cnt, int32_t a, int32_t b) {
     cnt += (int32_t)P[(int64_t)b * kWideCh + lane] - (a > sb ? (int32_t)P[(int64_t)(a - 1) * kWideCh + lane] : base);
@@ -737,12 +826,14 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       base = se > sb && sb > cb ? (int32_t)P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
       fcnt = fe > fb ? (int32_t)P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? (int32_t)P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
       gk0 = k_gbeg[kk] - wp[kk];
-      const int32_t S = se - sb;
-      step = S > 64 ? (S + 63) / 64 : 1;
-      nsamp = S > 0 ? (S + step - 1) / step : 0;
-      const int32_t js = sb + (lane < nsamp ? lane : 0) * step;
-      sU = S > 0 ? U2s[js] : 0;
-      sL = S > 0 ? L2s[js] : 0;
+      if (se > sb) {
+        const int lg = dir_log2(se - sb);
+        nbk = 1 << lg;
+        l2min = L2s[sb];
+        u2min = U2s[sb];
+        shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
+        TL = dtab + doff[(int64_t)ch * kKeyRange + kk];
+      }
     }
     const int32_t g0 = gk0 + tt;
     if (se <= sb) {  // no frame of the segment has a max2 window: every group scores the rest
@@ -769,14 +860,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       for (int32_t pbase = 0; pbase < pn; pbase += 64) {
         const int32_t i = pbase + lane;
         int32_t A = INT32_MAX, B = -2;
-        const int32_t v = i < pn ? cv.p_m2[pb0 + i] : 0;
-        int32_t loA, hiA, loB, hiB;
-        coarse_range(sU, nsamp, step, sb, se, v, true, loA, hiA);
-        coarse_range(sL, nsamp, step, sb, se, v, false, loB, hiB);
-        if (i < pn) {
-          A = loA + lb32(U2s + loA, hiA - loA, v);      // first frame with U2 >= v
-          B = loB + ub32(L2s + loB, hiB - loB, v) - 1;  // last frame with L2 <= v
-        }
+        if (i < pn) find_ab(cv.p_m2[pb0 + i], A, B);
         const bool ok = A <= B;
         int32_t bm = ok ? B : -2;
 #pragma unroll
@@ -815,16 +899,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     }
     const int32_t gst = __shfl(pj0, gi, 64);  // the first point lane of this lane's group
     int32_t A = INT32_MAX, B = -2;
-    const int32_t v = lane < npts ? cv.p_m2[pb0 + lane] : 0;
-    {
-      int32_t loA, hiA, loB, hiB;
-      coarse_range(sU, nsamp, step, sb, se, v, true, loA, hiA);
-      coarse_range(sL, nsamp, step, sb, se, v, false, loB, hiB);
-      if (lane < npts) {
-        A = loA + lb32(U2s + loA, hiA - loA, v);
-        B = loB + ub32(L2s + loB, hiB - loB, v) - 1;
-      }
-    }
+    if (lane < npts) find_ab(cv.p_m2[pb0 + lane], A, B);
     const bool ok = lane < npts && A <= B;
     int32_t bm = ok ? B : -2;
 #pragma unroll
@@ -917,10 +992,14 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch,
-                  (void*)fq, tmp})
+                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
     if (p) (void)hipFree(p);
   touch = nullptr;
   fq = nullptr;
+  doff = dtab = nullptr;
+  dtmp = nullptr;
+  dtmp_bytes = 0;
+  cap_dtab = 0;
   ka = kb = nullptr;
   ua = ub = nullptr;
   va = vb = L2s = U2s = seg = wpre = cbeg = info = nullptr;
@@ -961,15 +1040,31 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw})
+    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, dtmp})
       if (p) (void)hipFree(p);
-    seg = wpre = cbeg = nullptr;
+    seg = wpre = cbeg = doff = nullptr;
     chw = nullptr;
+    dtmp = nullptr;
+    dtmp_bytes = 0;
     cap_nch = 0;
     if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
-        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)))
+        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)))
       return e;
+    size_t tb = 0;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
+    if ((e = hipMalloc(&dtmp, tb > 0 ? tb : 1))) return e;
+    dtmp_bytes = tb;
     cap_nch = nch;
+  }
+  // the directory table: sum over segments of 2 NB <= 4 S (NB < 2 S), so <= 4 nf entries; it first
+  // holds the size pass's nch * kKeyRange + 1 entries (scanned into doff before the fill)
+  const int64_t need_d = std::max<int64_t>((4 << kDirScale) * nf + 8, nch * kKeyRange + 1);
+  if (need_d > cap_dtab) {
+    if (dtab) (void)hipFree(dtab);
+    dtab = nullptr;
+    cap_dtab = 0;
+    if ((e = dmalloc(&dtab, need_d))) return e;
+    cap_dtab = need_d;
   }
   // score rows for a slab of chunks at once: [slab][C][kChunk / 2] 16-bit pairs, at most ~1 GiB
   const int64_t row = (int64_t)(C > 0 ? C : 1) * (kWideCh / 2) * (int64_t)sizeof(uint32_t);
@@ -995,7 +1090,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
                                     int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s) {
   *eligible = false;
-  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
+  if (nq <= 0 || nf <= 0 || nf >= INT32_MAX / (4 << kDirScale) - 8 || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
     return hipSuccess;
   hipError_t e;
   const int64_t nch = (nq + kWideCh - 1) / kWideCh;
@@ -1039,6 +1134,14 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
     hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, ws->fq, n, ws->kb, order, ws->L2s,
                        ws->U2s, ws->qis, ws->seg);
   hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, n, nch, ws->cbeg);
+  // the window segments' directories (sizes, offsets, then filled from the sorted frames)
+  const int64_t nd = nch * kKeyRange + 1;
+  hipLaunchKernelGGL(wide_dir_count_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, ws->seg, nch, ws->dtab);
+  size_t db = ws->dtmp_bytes;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(ws->dtmp, db, ws->dtab, ws->doff, (int)nd, s))) return e;
+  if (n > 0)
+    hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, ws->kb, ws->seg, ws->L2s, ws->U2s,
+                       ws->doff, ws->dtab);
   hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->P);
   if ((e = hipGetLastError())) return e;
   *eligible = true;
@@ -1063,7 +1166,7 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   for (int64_t c0 = 0; c0 < nch; c0 += slab) {
     const int32_t c1 = (int32_t)std::min<int64_t>(nch, c0 + slab);
     hipLaunchKernelGGL(wide_groups_kernel, dim3(8192), dim3(256), 0, s, (int32_t)c0, c1, ws->chw, ws->wpre, ws->seg, ws->cbeg,
-                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->touch);
+                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->touch, ws->doff, ws->dtab);
     hipLaunchKernelGGL(wide_final_kernel, dim3(fx, (unsigned)(c1 - c0)), dim3(256), 0, s, (int32_t)c0, nq, C, d_tiekey,
                        ws->score, ws->touch, d_best);
   }
