@@ -179,7 +179,15 @@ struct CellCache {
   unsigned long long* e_key = nullptr;     // [n2] key << 52 | cell << 21 | column, ascending
   int32_t* e_grp = nullptr;                // [n2] group of each entry
   int32_t* k_gbeg = nullptr;               // [kKeyRange + 1] first group of each key
-  int64_t S = 0, n1 = 0, n2 = 0, w = 0;
+  // Clusters (the sweep's form of the points): a group's points cut where consecutive points are
+  // more than dgap micro-units apart, each kept as its (first, last) point. A window of width >=
+  // dgap - 1 that reaches from a cluster's first to its last point holds one of its points, so
+  // the sweep searches 2 bounds per cluster instead of 2 per point. dgap = max(0, floor(2 tol 1e6)
+  // - 3), the least window width at this tolerance (launch_scan_wide checks every frame's).
+  int32_t* c_lo = nullptr;                 // [nc] first point of each cluster
+  int32_t* c_hi = nullptr;                 // [nc] last point of each cluster
+  int32_t* c_beg = nullptr;                // [n1 + 1] first cluster of each group
+  int64_t S = 0, n1 = 0, n2 = 0, w = 0, nc = 0, dgap = 0;
   bool valid = false;
   hipError_t build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
                    int32_t ncols, int64_t nrows, double tole, hipStream_t s);
@@ -227,6 +235,8 @@ struct WideScratch {
   size_t dtmp_bytes = 0;
   int64_t cap_nf = 0, cap_nch = 0, cap_score = 0, cap_dtab = 0;
   int32_t slab = 0;                                  // chunks per groups launch
+  int64_t min_width = -1;                            // prepare: every max2 window is at least this wide (-1: unknown)
+  bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
   hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
   void release();
   WideScratch() = default;

@@ -114,6 +114,30 @@ __global__ void key_gbeg_kernel(const uint32_t* __restrict__ g_key, int64_t n1, 
   if (t <= kKeyRange) k_gbeg[t] = (int32_t)lower_bound_t<uint32_t>(g_key, n1, (uint32_t)t << kColBits);
 }
 
+// Clusters of each group's points (CellCache::c_lo/c_hi/c_beg): point i starts one when it starts
+// its group or lies more than dgap above its predecessor.
+__global__ void cluster_flag_kernel(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32, int64_t S,
+                                    int64_t dgap, int32_t* __restrict__ flag) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (int64_t)gridDim.x * blockDim.x)
+    flag[i] = i == 0 || k32[i] != k32[i - 1] || (int64_t)p_m2[i] - (int64_t)p_m2[i - 1] > dgap;
+}
+// cidx = exclusive prefix of the flags: point i is in cluster cidx[i] + flag[i] - 1.
+__global__ void cluster_write_kernel(const int32_t* __restrict__ p_m2, const int32_t* __restrict__ flag,
+                                     const int32_t* __restrict__ cidx, int64_t S, int32_t* __restrict__ c_lo,
+                                     int32_t* __restrict__ c_hi) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < S; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t c = cidx[i] + flag[i] - 1;
+    if (flag[i]) c_lo[c] = p_m2[i];
+    if (i == S - 1 || flag[i + 1]) c_hi[c] = p_m2[i];
+  }
+}
+// c_beg[g] = the cluster of group g's first point (a cluster start), c_beg[n1] = nc.
+__global__ void cluster_gbeg_kernel(const int32_t* __restrict__ g_beg, const int32_t* __restrict__ cidx, int64_t n1,
+                                    int64_t S, int64_t nc, int32_t* __restrict__ c_beg) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g <= n1; g += (int64_t)gridDim.x * blockDim.x)
+    c_beg[g] = g < n1 && g_beg[g] < S ? cidx[g_beg[g]] : (int32_t)nc;
+}
+
 // The sweep's frame sorts (0.6 M pairs at C3): hipCUB's dispatch (a merge sort below 2^20 items,
 // 0.17 ms at C3). rocPRIM's onesweep forced instead measured slower there (6 digit passes of
 // 23 us: 0.18 ms).
@@ -139,8 +163,11 @@ hipError_t dmalloc(T** p, int64_t n) {
 }  // namespace
 
 void CellCache::release() {
-  for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp, (void*)k_gbeg})
+  for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp, (void*)k_gbeg, (void*)c_lo,
+                  (void*)c_hi, (void*)c_beg})
     if (p) (void)hipFree(p);
+  c_lo = c_hi = c_beg = nullptr;
+  nc = dgap = 0;
   p_m2 = nullptr;
   g_key = nullptr;
   g_beg = nullptr;
@@ -218,6 +245,30 @@ hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, cons
   TFP_TRY(hipGetLastError());
   (void)hipFree(glen);
   glen = nullptr;
+  // the sweep's clusters: flags into ga, their prefix into gb (both reallocated below)
+  dgap = std::max<int64_t>(0, (int64_t)floor(2.0 * tole * 1e6) - 3);
+  TFP_TRY(dmalloc(&ga, S));
+  TFP_TRY(dmalloc(&gb, S));
+  hipLaunchKernelGGL(cluster_flag_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, k32, S, dgap, ga);
+  TFP_TRY(hipGetLastError());
+  TFP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ga, gb, (int)S, s));
+  {
+    int32_t last[2] = {0, 0};
+    TFP_TRY(hipMemcpyAsync(&last[0], gb + S - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    TFP_TRY(hipMemcpyAsync(&last[1], ga + S - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    TFP_TRY(hipStreamSynchronize(s));
+    nc = (int64_t)last[0] + last[1];
+  }
+  TFP_TRY(dmalloc(&c_lo, nc));
+  TFP_TRY(dmalloc(&c_hi, nc));
+  TFP_TRY(dmalloc(&c_beg, n1 + 1));
+  hipLaunchKernelGGL(cluster_write_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, ga, gb, S, c_lo, c_hi);
+  hipLaunchKernelGGL(cluster_gbeg_kernel, dim3(grid_for(n1 + 1)), dim3(256), 0, s, g_beg, gb, n1, S, nc, c_beg);
+  TFP_TRY(hipGetLastError());
+  TFP_TRY(hipStreamSynchronize(s));
+  (void)hipFree(ga);
+  (void)hipFree(gb);
+  ga = gb = nullptr;
   TFP_TRY(dmalloc(&ea, 2 * S));
   TFP_TRY(dmalloc(&eb, 2 * S));
   TFP_TRY(dmalloc(&ga, 2 * S));
@@ -249,6 +300,7 @@ namespace {
 
 struct CellView {
   const int32_t* p_m2;
+  const int32_t* p_hi;  // the sweep: each item's last point (its cluster's; p_m2 when items are points)
   const uint32_t* g_key;
   const int32_t* g_beg;
   const unsigned long long* e_key;
@@ -783,8 +835,10 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
     if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
   };
-  // v's run in the segment: A = first frame with U2 >= v, B = last frame with L2 <= v
-  auto find_ab = [&](int32_t v, int32_t& A, int32_t& B) {
+  // an item's run in the segment: A = first frame with U2 >= va, B = last frame with L2 <= vb (an
+  // item is a point, va = vb, or a cluster, va its first and vb its last point)
+  auto find_ab = [&](int32_t va, int32_t vb, int32_t& A, int32_t& B) {
+    const int32_t v = vb;
     const int64_t dv = (int64_t)v - l2min;
     if (dv < 0) {
       B = sb - 1;
@@ -793,13 +847,13 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       const int32_t lo = TL[b], hi = b + 1 < nbk ? TL[b + 1] : se;
       B = lo + ub32(L2s + lo, hi - lo, v) - 1;
     }
-    const int64_t du = (int64_t)v - u2min;
+    const int64_t du = (int64_t)va - u2min;
     if (du <= 0) {
       A = sb;
     } else {
       const int32_t b = (int32_t)min<int64_t>(du >> shf, nbk - 1);
       const int32_t lo = TL[nbk + b], hi = b + 1 < nbk ? TL[nbk + b + 1] : se;
-      A = lo + lb32(U2s + lo, hi - lo, v);
+      A = lo + lb32(U2s + lo, hi - lo, va);
     }
   };
   auto close_run = [&](int32_t& cnt, int32_t a, int32_t b) {
@@ -860,7 +914,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       for (int32_t pbase = 0; pbase < pn; pbase += 64) {
         const int32_t i = pbase + lane;
         int32_t A = INT32_MAX, B = -2;
-        if (i < pn) find_ab(cv.p_m2[pb0 + i], A, B);
+        if (i < pn) find_ab(cv.p_m2[pb0 + i], cv.p_hi[pb0 + i], A, B);
         const bool ok = A <= B;
         int32_t bm = ok ? B : -2;
 #pragma unroll
@@ -899,7 +953,7 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     }
     const int32_t gst = __shfl(pj0, gi, 64);  // the first point lane of this lane's group
     int32_t A = INT32_MAX, B = -2;
-    if (lane < npts) find_ab(cv.p_m2[pb0 + lane], A, B);
+    if (lane < npts) find_ab(cv.p_m2[pb0 + lane], cv.p_hi[pb0 + lane], A, B);
     const bool ok = lane < npts && A <= B;
     int32_t bm = ok ? B : -2;
 #pragma unroll
@@ -1114,6 +1168,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
   if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
   const int32_t* order = ws->vb;
+  ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase
   if (info[2] > 0 || dbase < 0) {
     // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
     if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
@@ -1155,9 +1210,17 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   const int64_t nch = (nq + kWideCh - 1) / kWideCh;
   CellView cv;
   memset(&cv, 0, sizeof cv);
-  cv.p_m2 = cells->p_m2;
   cv.g_key = cells->g_key;
-  cv.g_beg = cells->g_beg;
+  // clusters when every window of the batch is at least dgap wide (CellCache), else points
+  if (cells->c_beg && !ws->points_only && (cells->dgap == 0 || (ws->min_width >= 0 && ws->min_width >= cells->dgap))) {
+    cv.p_m2 = cells->c_lo;
+    cv.p_hi = cells->c_hi;
+    cv.g_beg = cells->c_beg;
+  } else {
+    cv.p_m2 = cells->p_m2;
+    cv.p_hi = cells->p_m2;
+    cv.g_beg = cells->g_beg;
+  }
   cv.valid = 1;
   hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
   hipLaunchKernelGGL(wide_chw_kernel, dim3(1), dim3(1024), 0, s, ws->wpre, nch, ws->chw);

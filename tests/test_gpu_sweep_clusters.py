@@ -1,0 +1,126 @@
+"""The coefs=2 sweep over clusters of points (csrc/tfp_scan.hip, CellCache::c_lo/c_hi/c_beg).
+
+A group's points closer than dgap = floor(2 tol 1e6) - 3 micro-units (the least max2 window width
+at the tolerance) merge into one cluster, and the sweep searches only a cluster's first and last
+point. These cases put max2 points at gaps just below, at and above dgap, duplicates, and windows
+placed inside every gap and on both ends of it, with q2 at several sub-micro offsets so the windows'
+"%f" rounding takes both widths. Each clip has its own key (one query per clip reads that clip's
+exact frame count back as match_count), and all clips also share one key, where the groups batch
+per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
+(src/fp_handler.c:308-374) and == the point form (TFP_WIDE_POINTS).
+"""
+import math
+import os
+import uuid as uuidlib
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SHARED_KEY = 30
+
+
+def _engine_with(tfp_lib, env):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        return tfp_lib.Engine(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+def _points(dgap, base, kind):
+    """Ascending max2 points (micro-units) of one clip's group."""
+    if kind == "many":  # > 64 clusters: every gap wider than any window
+        return [base + i * (2 * dgap + 40) for i in range(100)]
+    gaps = [max(dgap - 1, 0), dgap, dgap + 1, dgap + 2, dgap + 3, 0, 2 * dgap + 9, 1, dgap + 4, max(dgap - 2, 0), dgap]
+    if kind == "b":
+        gaps = gaps[::-1] + [3 * dgap + 11]
+    pts = [base]
+    for g in gaps:
+        pts.append(pts[-1] + g)
+    return pts
+
+
+def _frames_for(pts, tol, k):
+    """Query frames of trunc key k whose max2 windows sit at every gap's inner ends and middle."""
+    t = tol * 1e6
+    xs = set()
+    for a, b in zip(pts[:-1], pts[1:]):
+        for v in (a, b):
+            for d in range(-4, 5):
+                xs.add(v + t + d)   # L2 around v
+                xs.add(v - t + d)   # U2 around v
+        mid = (a + b) // 2
+        for d in range(-3, 4):
+            xs.add(mid + d)
+    xs.add(pts[0] - t - 50)
+    xs.add(pts[-1] + t + 50)
+    q2 = []
+    for x in sorted(xs):
+        for frac in (0.0, 0.25, 0.5, 0.7):
+            q2.append((x + frac) / 1e6)
+    return np.full(len(q2), k + 0.5), np.asarray(q2)
+
+
+@pytest.mark.parametrize("tol", [0.0, 0.000004, 0.001, 0.0105, 0.1, 0.45])
+def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
+    dgap = max(0, math.floor(2 * tol * 1e6) - 3)
+    kinds = ["a", "b", "a", "many", "b"]
+    rng = np.random.default_rng(7)
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in kinds]
+    m1, m2, clip = [], [], []
+    groups = []
+    for c, kind in enumerate(kinds):
+        own = 10 + c
+        base = 5_000_000 + c * 37
+        pts = _points(dgap, base, kind)
+        shared_base = 10_000_000 + c * (200 * dgap + 10_000_000)
+        spts = _points(dgap, shared_base, kind)
+        for k, p in ((own, pts), (SHARED_KEY, spts)):
+            m1 += [k * 1_000_000] * len(p)
+            m2 += p
+            clip += [c] * len(p)
+        groups.append((own, pts, spts))
+    m1 = np.asarray(m1, np.int32)
+    m2 = np.asarray(m2, np.int32)
+    clip = np.asarray(clip, np.int32)
+    queries = []
+    for c, (own, pts, spts) in enumerate(groups):
+        queries.append(_frames_for(pts, tol, own))
+        queries.append(_frames_for(spts, tol, SHARED_KEY))
+    q1 = np.concatenate([q[0] for q in queries])
+    q2 = np.concatenate([q[1] for q in queries])
+    qoff = np.concatenate([[0], np.cumsum([len(q[0]) for q in queries])])
+    assert qoff[-1] < 2**31 and max(len(q[0]) for q in queries) < 65536
+    frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                         ("q1", "<f8"), ("q2", "<f8")]))
+    frames["q1"], frames["q2"] = q1, q2
+    expect = []
+    for i in range(len(queries)):
+        s = slice(qoff[i], qoff[i + 1])
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, -1, -1)
+        expect.append((uuids[w], mc) if found else None)
+    got = {}
+    for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"})):
+        eng = _engine_with(tfp_lib, env)
+        try:
+            for c in range(len(kinds)):
+                sel = clip == c
+                eng.index_add(uuids[c], m1[sel], m2[sel])
+            res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol))
+            got[form] = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+            assert list(fcs) == list(np.diff(qoff))
+        finally:
+            eng.close()
+    assert got["clusters"] == expect, tol
+    assert got["points"] == expect, tol
+    # every query found its own clip with a partial count: windows in the gaps missed, others hit
+    for i, e in enumerate(expect):
+        assert e is not None and e[0] == uuids[i // 2]
+        assert 0 < e[1] < qoff[i + 1] - qoff[i]
