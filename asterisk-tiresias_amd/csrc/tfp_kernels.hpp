@@ -206,12 +206,12 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64
                        int32_t* d_tcnt, unsigned long long* d_best, hipStream_t s);
 
 // The general path's sweep by groups (tfp_scan.hip): every query frame of
-// the batch sorted by (64-query chunk, key, max2 window); per chunk, one wave per clip group of
-// each key the chunk uses counts, for the chunk's 64 queries at once, the frames whose window
+// the batch sorted by (128-query chunk, key, max2 window); per chunk, one wave per clip group of
+// each key the chunk uses counts, for the chunk's 128 queries at once, the frames whose window
 // holds one of the group's points (prefix counts over the sorted frames), so its work follows
 // the groups, not the hits. Needs every frame's key inside the clip-set cache.
 struct WideScratch {
-  static constexpr int32_t kChunk = 64;  // queries per chunk: one per lane
+  static constexpr int32_t kChunk = 128;  // queries per chunk: two per lane (a word of two 16-bit counts)
   // all sized by wide_reserve for nf frames, nq queries, C clips
   unsigned long long *ka = nullptr, *kb = nullptr;  // sort keys
   uint32_t *ua = nullptr, *ub = nullptr;
@@ -219,7 +219,8 @@ struct WideScratch {
   int32_t *L2s = nullptr, *U2s = nullptr;           // sorted windows
   uint8_t* qis = nullptr;                            // sorted frames' query within its chunk
   int32_t* fq = nullptr;                             // [nf] each frame's query
-  uint16_t* P = nullptr;                             // [nf][kChunk] in-chunk prefix counts (< 2^16: every query < 65536 frames)
+  uint32_t* P = nullptr;                             // [nf][kChunk / 2] in-chunk prefix counts, 16-bit pairs (< 2^16: every query < 65536 frames)
+  uint32_t* ptot = nullptr;                          // [nchunks][256][kChunk / 2] the prefix counts' per-share totals, then their prefix
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
   int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk

@@ -468,14 +468,19 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64
 // grow with v: the union over the group's ascending points is a few merged runs, and a query's
 // count is its frames inside them: differences of in-segment prefix counts P[i][q]. Frames
 // without a max2 condition (the ignore filter dropped it) hit every group of their key: their
-// own segment, counted whole. Scores go to a per-chunk [clip][query] array (64 lanes = 64
-// queries, one coalesced add per group), then one pass per chunk takes each query's best key.
+// own segment, counted whole. Scores go to a per-chunk [clip][query] array (lane l = queries 2l,
+// 2l + 1 as one word of two 16-bit counts, one coalesced add per group), then one pass per chunk
+// takes each query's best key.
 
 namespace {
 
 constexpr int kWideCh = WideScratch::kChunk;
 constexpr int kWideSegs = 2 * kKeyRange;  // per chunk: key k with a max2 window, k | 1024 without
-static_assert(kWideCh == 64, "one query per lane");
+static_assert(kWideCh == 128, "two queries per lane");
+// Per-lane counts are pairs of 16-bit counts in one word, (query 2l) | (query 2l + 1) << 16: a count
+// is at most its query's frames (< 2^16), and prefix counts only grow, so the differences and sums
+// below never borrow or carry across the halves.
+constexpr int kWideW = kWideCh / 2;  // words per P row and per score row
 
 // Bad frames (a key outside the cache's range or a window outside int32: the row scan takes the
 // batch) into info[1]; with uk, the U2 (offset binary: unsigned order == signed order) of each frame
@@ -680,35 +685,72 @@ __global__ void wide_dir_fill_kernel(int64_t n, const unsigned long long* __rest
   }
 }
 
-// In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i]: one 16-wave workgroup per
-// chunk, each wave over a contiguous 64-aligned share (its counts first, then the writes, offset
-// by the waves before it). Lane q counts query q among 64 frames by reading their queries out of
-// the lanes (no per-frame memory dependency).
-__global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg,
-                                                           const uint8_t* __restrict__ qis, uint16_t* __restrict__ P) {
-  __shared__ int32_t tot[16][kWideCh];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int32_t b = cbeg[blockIdx.x], n = cbeg[blockIdx.x + 1] - b;
-  const int32_t per = (n + 16 * 64 - 1) / (16 * 64) * 64;
-  const int32_t r0 = min(n, wv * per), r1 = min(n, r0 + per);
-  int32_t cnt = 0;
+// In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i], in three launches over
+// kPortions 64-aligned shares per chunk (one wave each: a chunk's ~20 k frames at C3 spread over
+// 256 waves instead of the 16 of one workgroup): each share's counts, their exclusive prefix per
+// chunk, then each share's rows from its prefix. Lane l counts queries 2l and 2l + 1 (one word
+// of two 16-bit counts) among 64 frames by reading their queries out of the lanes (no per-frame
+// memory dependency).
+constexpr int kPortions = 256;
+__device__ __forceinline__ void portion_range(const int32_t* cbeg, int ch, int p, int32_t& b, int32_t& r0, int32_t& r1) {
+  b = cbeg[ch];
+  const int32_t n = cbeg[ch + 1] - b;
+  const int32_t per = (n + kPortions * 64 - 1) / (kPortions * 64) * 64;
+  r0 = min(n, p * per);
+  r1 = min(n, r0 + per);
+}
+// frame x's increment for lane l: 1 (query 2l), 1 << 16 (query 2l + 1) or 0; 255 pads
+__device__ __forceinline__ uint32_t prefix_inc(int32_t x, int lane) {
+  return (x >> 1) == lane ? (x & 1 ? 0x10000u : 1u) : 0u;
+}
+__global__ __launch_bounds__(1024) void wide_pcount_kernel(const int32_t* __restrict__ cbeg,
+                                                           const uint8_t* __restrict__ qis, uint32_t* __restrict__ ptot) {
+  const int lane = threadIdx.x & 63, p = blockIdx.y * 16 + (threadIdx.x >> 6);
+  int32_t b, r0, r1;
+  portion_range(cbeg, blockIdx.x, p, b, r0, r1);
+  uint32_t cnt = 0;
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
 #pragma unroll
-    for (int j = 0; j < 64; j++) cnt += __builtin_amdgcn_readlane(x, j) == lane;
+    for (int j = 0; j < 64; j++) cnt += prefix_inc(__builtin_amdgcn_readlane(x, j), lane);
   }
-  tot[wv][lane] = cnt;
+  ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane] = cnt;
+}
+// Exclusive prefix of the shares' counts per chunk, in place: wave w scans shares 16w .. 16w + 15.
+__global__ __launch_bounds__(1024) void wide_pscan_kernel(uint32_t* __restrict__ ptot) {
+  __shared__ uint32_t tot[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t* t = ptot + ((int64_t)blockIdx.x * kPortions + 16 * wv) * 64 + lane;
+  uint32_t v[16], run = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) v[j] = t[64 * j];
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t x = v[j];
+    v[j] = run;
+    run += x;
+  }
+  tot[wv][lane] = run;
   __syncthreads();
-  int32_t run = 0;
-  for (int w = 0; w < wv; w++) run += tot[w][lane];
+  uint32_t base = 0;
+  for (int w = 0; w < wv; w++) base += tot[w][lane];
+#pragma unroll
+  for (int j = 0; j < 16; j++) t[64 * j] = base + v[j];
+}
+__global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg, const uint8_t* __restrict__ qis,
+                                                           const uint32_t* __restrict__ ptot, uint32_t* __restrict__ P) {
+  const int lane = threadIdx.x & 63, p = blockIdx.y * 16 + (threadIdx.x >> 6);
+  int32_t b, r0, r1;
+  portion_range(cbeg, blockIdx.x, p, b, r0, r1);
+  uint32_t run = ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane];
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
-    uint16_t* row = P + ((int64_t)b + i) * kWideCh + lane;
+    uint32_t* row = P + ((int64_t)b + i) * kWideW + lane;
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
-      run += __builtin_amdgcn_readlane(x, j) == lane;
-      if (j < m) row[(int64_t)j * kWideCh] = (uint16_t)run;
+      run += prefix_inc(__builtin_amdgcn_readlane(x, j), lane);
+      if (j < m) row[(int64_t)j * kWideW] = run;
     }
   }
 }
@@ -789,13 +831,13 @@ __device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) 
 
 // The work items (chunk, key, clip group) of chunks [ch0, ch1), in chunk and key order; each wave
 // takes a contiguous share, so it locates its first item by binary search and then steps through
-// keys and chunks. Lane q = query 64 ch + q. A group's counts go to the slab's score rows as 16-bit
-// pairs (query 2i low, 2i + 1 high: a count is at most the query's frames, < 2^16).
+// keys and chunks. Lane l = queries 128 ch + 2l, 128 ch + 2l + 1 (a word of two 16-bit counts). A
+// group's counts go to the slab's score rows as those words.
 __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t ch1, const int64_t* __restrict__ chw,
                                                           const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
                                                           const int32_t* __restrict__ cbeg, CellView cv,
                                                           const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
-                                                          const int32_t* __restrict__ U2s, const uint16_t* __restrict__ P,
+                                                          const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
                                                           int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch,
                                                           const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab) {
   const int lane = threadIdx.x & 63;
@@ -825,15 +867,18 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
   }
   int32_t kend = wp[kk + 1];
   bool fresh = true;
-  int32_t sb = 0, se = 0, base = 0, fcnt = 0, gk0 = 0;
+  int32_t sb = 0, se = 0, gk0 = 0;
+  uint32_t base = 0, fcnt = 0;
   int32_t nbk = 1, shf = 0, l2min = 0, u2min = 0;  // the segment's directory
   const int32_t* TL = dtab;
-  auto add_score = [&](int32_t col, int32_t cnt) {
-    const uint32_t hi16 = (uint32_t)__shfl_down(cnt, 1, 64);
-    const uint32_t v = (uint32_t)cnt | (hi16 << 16);
-    if (!(lane & 1) && v) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * (kWideCh / 2) + (lane >> 1)], v);
+  auto add_score = [&](int32_t col, uint32_t cnt) {
+#ifdef TFP_EXP_NO_SCORE  // timing experiment only (wrong results): the groups' work without its score writes
+    if (cnt == 12345u) score[0] = col;
+    return;
+#endif
+    if (cnt) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * kWideW + lane], cnt);
     // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
-    if (__ballot(!(lane & 1) && v) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
+    if (__ballot(cnt != 0) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
   };
   // an item's run in the segment: A = first frame with U2 >= va, B = last frame with L2 <= vb (an
   // item is a point, va = vb, or a cluster, va its first and vb its last point)
@@ -856,8 +901,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       A = lo + lb32(U2s + lo, hi - lo, va);
     }
   };
-  auto close_run = [&](int32_t& cnt, int32_t a, int32_t b) {
-    cnt += (int32_t)P[(int64_t)b * kWideCh + lane] - (a > sb ? (int32_t)P[(int64_t)(a - 1) * kWideCh + lane] : base);
+  auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
+    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
   };
   while (t < tend) {
     while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
@@ -877,8 +922,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       sb = sg[2 * kk];
       se = sg[2 * kk + 1];
       const int32_t fb = sg[2 * (kk | kKeyRange)], fe = sg[2 * (kk | kKeyRange) + 1];
-      base = se > sb && sb > cb ? (int32_t)P[(int64_t)(sb - 1) * kWideCh + lane] : 0;
-      fcnt = fe > fb ? (int32_t)P[(int64_t)(fe - 1) * kWideCh + lane] - (fb > cb ? (int32_t)P[(int64_t)(fb - 1) * kWideCh + lane] : 0) : 0;
+      base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
+      fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
       gk0 = k_gbeg[kk] - wp[kk];
       if (se > sb) {
         const int lg = dir_log2(se - sb);
@@ -909,7 +954,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
     if (nG == 0) {
       // one group with more than 64 points: its points 64 at a time, runs merged across the steps
       const int32_t pn = __shfl(pj1, 0, 64);
-      int32_t cnt = fcnt, carry = -2, aopen = 0;
+      uint32_t cnt = fcnt;
+      int32_t carry = -2, aopen = 0;
       bool open = false;
       for (int32_t pbase = 0; pbase < pn; pbase += 64) {
         const int32_t i = pbase + lane;
@@ -968,7 +1014,8 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
       const int32_t a0 = __shfl(pj0, j, 64), a1 = __shfl(pj1, j, 64);
       const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
       unsigned long long m = starts & rng;
-      int32_t cnt = fcnt, aopen = 0;
+      uint32_t cnt = fcnt;
+      int32_t aopen = 0;
       bool open = false;
       while (m) {
         const int sl = __ffsll((long long)m) - 1;
@@ -988,56 +1035,54 @@ __global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t c
 
 // Per chunk of the slab (blockIdx.y): each query's max over the chunk's touched clips of
 // (count << 32 | tie key), and those score rows and touch bytes back to zero. A wave reads the
-// touch bytes of 64 clips per step (64 B) and only the touched clips' rows (128 B each, two clips
-// per step, one per half-wave): the row traffic follows the hits, not C.
+// touch bytes of 64 clips per step (64 B) and only the touched clips' rows (256 B each, one per
+// load, the loads of 32 clips issued before the first use): the row traffic follows the hits, not C.
 __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq, int32_t C,
                                                          const int32_t* __restrict__ tiekey, uint32_t* __restrict__ score,
                                                          uint8_t* __restrict__ touch, unsigned long long* __restrict__ best) {
   __shared__ unsigned long long red[4][kWideCh];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5, wl = lane & 31;
-  uint32_t* rows = score + (int64_t)blockIdx.y * C * (kWideCh / 2);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* rows = score + (int64_t)blockIdx.y * C * kWideW;
   uint8_t* tch = touch + (int64_t)blockIdx.y * C;
-  unsigned long long rlo = 0, rhi = 0;
+  unsigned long long rlo = 0, rhi = 0;  // queries 2 lane, 2 lane + 1
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t c0 = 64 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); c0 < C; c0 += 64 * nw) {
     const bool t = c0 + lane < C && tch[c0 + lane];
-    unsigned long long m = __ballot(t);
+    const unsigned long long m = __ballot(t);
+    if (!m) continue;
     if (t) tch[c0 + lane] = 0;
-    while (m) {  // two touched clips per step, one per half-wave
-      const int b0 = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int b1 = m ? __ffsll((long long)m) - 1 : -1;
-      if (m) m &= m - 1;
-      const int b = half ? b1 : b0;
-      if (b >= 0) {
-        const int64_t c = c0 + b;
-        const uint32_t w = rows[c * (kWideCh / 2) + wl];
-        if (w) {
-          const unsigned long long tk = (uint32_t)tiekey[c];
-          const unsigned long long klo = ((unsigned long long)(w & 0xffffu) << 32) | tk;
-          const unsigned long long khi = ((unsigned long long)(w >> 16) << 32) | tk;
-          if (w & 0xffffu) rlo = klo > rlo ? klo : rlo;
-          if (w >> 16) rhi = khi > rhi ? khi : rhi;
-          rows[c * (kWideCh / 2) + wl] = 0u;
+    const int32_t tkl = t ? tiekey[c0 + lane] : 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (!((m >> (32 * h)) & 0xffffffffull)) continue;
+      uint32_t w[32];
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const int b = 32 * h + j;
+        w[j] = (m >> b) & 1 ? rows[(c0 + b) * kWideW + lane] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < 32; j++) {
+        const int b = 32 * h + j;
+        if ((m >> b) & 1) {
+          const unsigned long long tk = (uint32_t)__builtin_amdgcn_readlane(tkl, b);
+          const unsigned long long klo = ((unsigned long long)(w[j] & 0xffffu) << 32) | tk;
+          const unsigned long long khi = ((unsigned long long)(w[j] >> 16) << 32) | tk;
+          if (w[j] & 0xffffu) rlo = klo > rlo ? klo : rlo;
+          if (w[j] >> 16) rhi = khi > rhi ? khi : rhi;
+          if (w[j]) rows[(c0 + b) * kWideW + lane] = 0u;
         }
       }
     }
   }
-  {
-    const unsigned long long olo = __shfl_xor(rlo, 32, 64), ohi = __shfl_xor(rhi, 32, 64);
-    rlo = olo > rlo ? olo : rlo;
-    rhi = ohi > rhi ? ohi : rhi;
-  }
-  if (half == 0) {
-    red[wave][2 * wl] = rlo;
-    red[wave][2 * wl + 1] = rhi;
-  }
+  red[wave][2 * lane] = rlo;
+  red[wave][2 * lane + 1] = rhi;
   __syncthreads();
-  if (wave == 0) {
-    unsigned long long m = red[0][lane];
-    for (int w2 = 1; w2 < 4; w2++) m = red[w2][lane] > m ? red[w2][lane] : m;
-    const int32_t q = (ch0 + (int32_t)blockIdx.y) * kWideCh + lane;
-    if (m && q < nq) atomicMax(&best[q], m);
+  if (threadIdx.x < kWideCh) {
+    unsigned long long mm = red[0][threadIdx.x];
+    for (int w2 = 1; w2 < 4; w2++) mm = red[w2][threadIdx.x] > mm ? red[w2][threadIdx.x] : mm;
+    const int32_t q = (ch0 + (int32_t)blockIdx.y) * kWideCh + (int32_t)threadIdx.x;
+    if (mm && q < nq) atomicMax(&best[q], mm);
   }
 }
 
@@ -1045,10 +1090,11 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch,
+                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, (void*)ptot,
                   (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
     if (p) (void)hipFree(p);
   touch = nullptr;
+  ptot = nullptr;
   fq = nullptr;
   doff = dtab = nullptr;
   dtmp = nullptr;
@@ -1083,7 +1129,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = 0;
     if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
         (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
-        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideCh)) || (e = dmalloc(&fq, nf)))
+        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideW)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
     if ((e = sweep_sort_pairs<uint32_t>(nullptr, t1, ua, ub, va, vb, nf, 32, s)) ||
@@ -1094,15 +1140,17 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, dtmp})
+    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, (void*)ptot, dtmp})
       if (p) (void)hipFree(p);
     seg = wpre = cbeg = doff = nullptr;
+    ptot = nullptr;
     chw = nullptr;
     dtmp = nullptr;
     dtmp_bytes = 0;
     cap_nch = 0;
     if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
-        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)))
+        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
+        (e = dmalloc(&ptot, nch * kPortions * 64)))
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1121,9 +1169,9 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_dtab = need_d;
   }
   // score rows for a slab of chunks at once: [slab][C][kChunk / 2] 16-bit pairs, at most ~1 GiB
-  const int64_t row = (int64_t)(C > 0 ? C : 1) * (kWideCh / 2) * (int64_t)sizeof(uint32_t);
+  const int64_t row = (int64_t)(C > 0 ? C : 1) * kWideW * (int64_t)sizeof(uint32_t);
   slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
-  const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * (kWideCh / 2);
+  const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * kWideW;
   if (ns > cap_score) {
     for (void* p : {(void*)score, (void*)touch})
       if (p) (void)hipFree(p);
@@ -1197,7 +1245,10 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   if (n > 0)
     hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, ws->kb, ws->seg, ws->L2s, ws->U2s,
                        ws->doff, ws->dtab);
-  hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->P);
+  hipLaunchKernelGGL(wide_pcount_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
+  hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
+  hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot,
+                     ws->P);
   if ((e = hipGetLastError())) return e;
   *eligible = true;
   return hipSuccess;
