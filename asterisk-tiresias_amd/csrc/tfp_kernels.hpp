@@ -187,6 +187,13 @@ struct CellCache {
   int32_t* c_lo = nullptr;                 // [nc] first point of each cluster
   int32_t* c_hi = nullptr;                 // [nc] last point of each cluster
   int32_t* c_beg = nullptr;                // [n1 + 1] first cluster of each group
+  // the clip-major sweep's directory: kdir[k][w] = first group of key k with column >= kWin w
+#ifndef TFP_CLIP_WIN
+#define TFP_CLIP_WIN 32
+#endif
+  static constexpr int32_t kWin = TFP_CLIP_WIN;
+  int32_t* kdir = nullptr;                 // [kKeyRange][nwin + 1]
+  int32_t nwin = 0;                        // ceil(columns / kWin)
   int64_t S = 0, n1 = 0, n2 = 0, w = 0, nc = 0, dgap = 0;
   bool valid = false;
   hipError_t build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
@@ -238,6 +245,10 @@ struct WideScratch {
   int32_t slab = 0;                                  // chunks per groups launch
   int64_t min_width = -1;                            // prepare: every max2 window is at least this wide (-1: unknown)
   bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
+  bool groups_form = false;                          // TFP_WIDE_GROUPS (tests, A/B): the key-major sweep with score rows
+  int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
+  int32_t* nuk = nullptr;                            // [nchunks] their number
+  unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima
   hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
   void release();
   WideScratch() = default;

@@ -138,6 +138,20 @@ __global__ void cluster_gbeg_kernel(const int32_t* __restrict__ g_beg, const int
     c_beg[g] = g < n1 && g_beg[g] < S ? cidx[g_beg[g]] : (int32_t)nc;
 }
 
+// kdir[k][w] = the first group of key k whose column is >= kWin w (the key's end for w = nwin):
+// the clip-major sweep's per-window group ranges.
+__global__ void cluster_kdir_kernel(const uint32_t* __restrict__ g_key, const int32_t* __restrict__ k_gbeg, int32_t nwin,
+                                    int32_t* __restrict__ kdir) {
+  const int64_t n = (int64_t)kKeyRange * (nwin + 1);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / (nwin + 1)), w = (int)(i % (nwin + 1));
+    const int32_t lo = k_gbeg[k], hi = k_gbeg[k + 1];
+    kdir[i] = w == nwin ? hi
+                        : lo + (int32_t)lower_bound_t<uint32_t>(g_key + lo, hi - lo,
+                                                                ((uint32_t)k << kColBits) | (uint32_t)(CellCache::kWin * w));
+  }
+}
+
 // The sweep's frame sorts (0.6 M pairs at C3): hipCUB's dispatch (a merge sort below 2^20 items,
 // 0.17 ms at C3). rocPRIM's onesweep forced instead measured slower there (6 digit passes of
 // 23 us: 0.18 ms).
@@ -164,9 +178,10 @@ hipError_t dmalloc(T** p, int64_t n) {
 
 void CellCache::release() {
   for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp, (void*)k_gbeg, (void*)c_lo,
-                  (void*)c_hi, (void*)c_beg})
+                  (void*)c_hi, (void*)c_beg, (void*)kdir})
     if (p) (void)hipFree(p);
-  c_lo = c_hi = c_beg = nullptr;
+  c_lo = c_hi = c_beg = kdir = nullptr;
+  nwin = 0;
   nc = dgap = 0;
   p_m2 = nullptr;
   g_key = nullptr;
@@ -264,6 +279,11 @@ hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, cons
   TFP_TRY(dmalloc(&c_beg, n1 + 1));
   hipLaunchKernelGGL(cluster_write_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, ga, gb, S, c_lo, c_hi);
   hipLaunchKernelGGL(cluster_gbeg_kernel, dim3(grid_for(n1 + 1)), dim3(256), 0, s, g_beg, gb, n1, S, nc, c_beg);
+  TFP_TRY(hipGetLastError());
+  nwin = (ncols + kWin - 1) / kWin;
+  TFP_TRY(dmalloc(&kdir, (int64_t)kKeyRange * (nwin + 1)));
+  hipLaunchKernelGGL(cluster_kdir_kernel, dim3(grid_for((int64_t)kKeyRange * (nwin + 1))), dim3(256), 0, s, g_key, k_gbeg, nwin,
+                     kdir);
   TFP_TRY(hipGetLastError());
   TFP_TRY(hipStreamSynchronize(s));
   (void)hipFree(ga);
@@ -481,6 +501,7 @@ static_assert(kWideCh == 128, "two queries per lane");
 // is at most its query's frames (< 2^16), and prefix counts only grow, so the differences and sums
 // below never borrow or carry across the halves.
 constexpr int kWideW = kWideCh / 2;  // words per P row and per score row
+constexpr int kPartWaves = 1024;     // clip-major sweep: at most this many waves per chunk
 
 // Bad frames (a key outside the cache's range or a window outside int32: the row scan takes the
 // batch) into info[1]; with uk, the U2 (offset binary: unsigned order == signed order) of each frame
@@ -1086,15 +1107,260 @@ __global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq
   }
 }
 
+// ---- clip-major sweep ------------------------------------------------------------------------
+// The same per-group work as wide_groups, ordered by clip instead of by key: a wave takes windows of
+// kWin consecutive clip columns of one chunk and, for each key the chunk uses, the groups of those
+// clips (two kdir loads per key, no search), so every count a clip gets in the chunk lands in the
+// wave's own LDS row for it. After a window's keys the wave takes each query's best (count << 32 |
+// tie key) over the window's clips in registers: no score rows in memory, no atomics, no
+// wide_final pass. Per-wave maxima go to part[ch][x][query], reduced by wide_part_max.
+constexpr int kWin = CellCache::kWin;
+constexpr int kClipWaves = 4;  // waves per workgroup
+
+// The used keys of each chunk, ascending: ukeys[ch][0 .. nuk[ch]).
+__global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restrict__ seg, int32_t* __restrict__ ukeys,
+                                                          int32_t* __restrict__ nuk) {
+  __shared__ int32_t wcnt[16];
+  const int ch = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
+  const bool used = sg[2 * t + 1] > sg[2 * t] || sg[2 * (t | kKeyRange) + 1] > sg[2 * (t | kKeyRange)];
+  const unsigned long long m = __ballot(used);
+  if (lane == 0) wcnt[wv] = __popcll(m);
+  __syncthreads();
+  int32_t off = 0;
+  for (int w = 0; w < wv; w++) off += wcnt[w];
+  if (used) ukeys[(int64_t)ch * kKeyRange + off + __popcll(m & ((1ull << lane) - 1))] = t;
+  if (t == 0) {
+    int32_t n = 0;
+    for (int w = 0; w < 16; w++) n += wcnt[w];
+    nuk[ch] = n;
+  }
+}
+
+__global__ __launch_bounds__(64 * kClipWaves) void wide_clips_kernel(
+    int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
+    const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
+    const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
+    const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
+    unsigned long long* __restrict__ part) {
+  __shared__ uint32_t accs[kClipWaves][kWin * 64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * kClipWaves + wv;
+  const int ch = (int)(gw / xw), x = (int)(gw % xw);
+  uint32_t* acc = accs[wv];
+  const int32_t per = (nwin + xw - 1) / xw;
+  const int32_t w0 = min(nwin, x * per), w1 = min(nwin, w0 + per);
+  const int32_t nu = nuk[ch];
+  const int32_t* uk = ukeys + (int64_t)ch * kKeyRange;
+  const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
+  const int32_t cb = cbeg[ch];
+  unsigned long long rlo = 0, rhi = 0;  // queries 128 ch + 2 lane, + 1
+  int32_t sb = 0, se = 0;
+  uint32_t base = 0, fcnt = 0;
+  int32_t nbk = 1, shf = 0, l2min = 0, u2min = 0;
+  const int32_t* TL = dtab;
+  auto find_ab = [&](int32_t va, int32_t vb, int32_t& A, int32_t& B) {
+    const int64_t dv = (int64_t)vb - l2min;
+    if (dv < 0) {
+      B = sb - 1;
+    } else {
+      const int32_t b = (int32_t)min<int64_t>(dv >> shf, nbk - 1);
+      const int32_t lo = TL[b], hi = b + 1 < nbk ? TL[b + 1] : se;
+      B = lo + ub32(L2s + lo, hi - lo, vb) - 1;
+    }
+    const int64_t du = (int64_t)va - u2min;
+    if (du <= 0) {
+      A = sb;
+    } else {
+      const int32_t b = (int32_t)min<int64_t>(du >> shf, nbk - 1);
+      const int32_t lo = TL[nbk + b], hi = b + 1 < nbk ? TL[nbk + b + 1] : se;
+      A = lo + lb32(U2s + lo, hi - lo, va);
+    }
+  };
+  auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
+    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
+  };
+  for (int32_t w = w0; w < w1; w++) {
+    const int32_t c0 = kWin * w;
+#pragma unroll
+    for (int j = 0; j < kWin; j++) acc[j * 64 + lane] = 0u;
+    auto add = [&](int32_t col, uint32_t cnt) { acc[(col - c0) * 64 + lane] += cnt; };
+    for (int32_t u0 = 0; u0 < nu; u0 += 64) {
+      // the used keys with groups in this window, 64 keys a step
+      int32_t kk = 0, ga = 0, gb = 0;
+      if (u0 + lane < nu) {
+        kk = uk[u0 + lane];
+        ga = kdir[(int64_t)kk * (nwin + 1) + w];
+        gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
+      }
+      unsigned long long km = __ballot(gb > ga);
+      while (km) {
+        const int sl = __ffsll((long long)km) - 1;
+        km &= km - 1;
+        const int k = __builtin_amdgcn_readlane(kk, sl);
+        const int32_t g1 = __builtin_amdgcn_readlane(gb, sl);
+        int32_t g = __builtin_amdgcn_readlane(ga, sl);
+        // the key's window segment and its frames without a max2 window (as in wide_groups)
+        sb = sg[2 * k];
+        se = sg[2 * k + 1];
+        const int32_t fb = sg[2 * (k | kKeyRange)], fe = sg[2 * (k | kKeyRange) + 1];
+        base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
+        fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
+        if (se <= sb) {  // no frame of the key has a max2 window: every group scores the rest
+          for (; g < g1; g++) add((int32_t)(cv.g_key[g] & kColMask), fcnt);
+          continue;
+        }
+        {
+          const int lg = dir_log2(se - sb);
+          nbk = 1 << lg;
+          l2min = L2s[sb];
+          u2min = U2s[sb];
+          shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
+          TL = dtab + doff[(int64_t)ch * kKeyRange + k];
+        }
+        while (g < g1) {
+          const int32_t left = g1 - g;
+          const int32_t pb0 = cv.g_beg[g];
+          int32_t pj0 = 0, pj1 = INT32_MAX, colj = 0;
+          if (lane < left) {
+            pj0 = cv.g_beg[g + lane] - pb0;
+            pj1 = cv.g_beg[g + lane + 1] - pb0;
+            colj = (int32_t)(cv.g_key[g + lane] & kColMask);
+          }
+          const int nG = __popcll(__ballot(lane < left && pj1 <= 64));
+          if (nG == 0) {  // one group with more than 64 items: 64 at a time, runs merged across the steps
+            const int32_t pn = __shfl(pj1, 0, 64);
+            uint32_t cnt = fcnt;
+            int32_t carry = -2, aopen = 0;
+            bool open = false;
+            for (int32_t pbase = 0; pbase < pn; pbase += 64) {
+              const int32_t i = pbase + lane;
+              int32_t A = INT32_MAX, B = -2;
+              if (i < pn) find_ab(cv.p_m2[pb0 + i], cv.p_hi[pb0 + i], A, B);
+              const bool ok = A <= B;
+              int32_t bm = ok ? B : -2;
+#pragma unroll
+              for (int o = 1; o < 64; o <<= 1) {
+                const int32_t y = __shfl_up(bm, o, 64);
+                if (lane >= o) bm = max(bm, y);
+              }
+              int32_t pe = __shfl_up(bm, 1, 64);
+              if (lane == 0) pe = -2;
+              pe = max(pe, carry);
+              unsigned long long starts = __ballot(ok && A > pe + 1);
+              while (starts) {
+                const int s2 = __ffsll((long long)starts) - 1;
+                starts &= starts - 1;
+                const int32_t as = __shfl(A, s2, 64), ps = __shfl(pe, s2, 64);
+                if (open) close_run(cnt, aopen, ps);
+                open = true;
+                aopen = as;
+              }
+              carry = max(carry, __shfl(bm, 63, 64));
+            }
+            if (open) close_run(cnt, aopen, carry);
+            add(__shfl(colj, 0, 64), cnt);
+            g++;
+            continue;
+          }
+          const int32_t npts = __shfl(pj1, nG - 1, 64);
+          int gi = 0;
+#pragma unroll
+          for (int bit = 32; bit >= 1; bit >>= 1) {
+            const int cand = gi + bit;
+            const int32_t xx = __shfl(pj0, min(cand, 63), 64);
+            if (cand < nG && xx <= lane) gi = cand;
+          }
+          const int32_t gst = __shfl(pj0, gi, 64);
+          int32_t A = INT32_MAX, B = -2;
+          if (lane < npts) find_ab(cv.p_m2[pb0 + lane], cv.p_hi[pb0 + lane], A, B);
+          const bool ok = lane < npts && A <= B;
+          int32_t bm = ok ? B : -2;
+#pragma unroll
+          for (int o = 1; o < 64; o <<= 1) {
+            const int32_t y = __shfl_up(bm, o, 64);
+            if (lane - o >= gst) bm = max(bm, y);
+          }
+          int32_t pe = __shfl_up(bm, 1, 64);
+          if (lane == gst) pe = -2;
+          const unsigned long long starts = __ballot(ok && A > pe + 1);
+          for (int j = 0; j < nG; j++) {
+            const int32_t a0 = __shfl(pj0, j, 64), a1 = __shfl(pj1, j, 64);
+            const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
+            unsigned long long mm = starts & rng;
+            uint32_t cnt = fcnt;
+            int32_t aopen = 0;
+            bool open = false;
+            while (mm) {
+              const int s2 = __ffsll((long long)mm) - 1;
+              mm &= mm - 1;
+              const int32_t as = __shfl(A, s2, 64), ps = __shfl(pe, s2, 64);
+              if (open) close_run(cnt, aopen, ps);
+              open = true;
+              aopen = as;
+            }
+            if (open) close_run(cnt, aopen, __shfl(bm, a1 - 1, 64));
+            add(__shfl(colj, j, 64), cnt);
+          }
+          g += nG;
+        }
+      }
+    }
+    // the window's clips: each query's best (count << 32 | tie key)
+    const int32_t tk = c0 + lane < C && lane < kWin ? tiekey[c0 + lane] : 0;
+#pragma unroll
+    for (int j = 0; j < kWin; j++) {
+      const uint32_t v = acc[j * 64 + lane];
+      const unsigned long long t = (uint32_t)__builtin_amdgcn_readlane(tk, j);
+      const unsigned long long klo = ((unsigned long long)(v & 0xffffu) << 32) | t;
+      const unsigned long long khi = ((unsigned long long)(v >> 16) << 32) | t;
+      if (v & 0xffffu) rlo = klo > rlo ? klo : rlo;
+      if (v >> 16) rhi = khi > rhi ? khi : rhi;
+    }
+  }
+  // the workgroup's maxima (its waves share the chunk: xw is a multiple of kClipWaves)
+  __shared__ unsigned long long red[kClipWaves][kWideCh];
+  red[wv][2 * lane] = rlo;
+  red[wv][2 * lane + 1] = rhi;
+  __syncthreads();
+  if (threadIdx.x < kWideCh) {
+    unsigned long long m = red[0][threadIdx.x];
+    for (int w2 = 1; w2 < kClipWaves; w2++) m = red[w2][threadIdx.x] > m ? red[w2][threadIdx.x] : m;
+    part[((int64_t)ch * (xw / kClipWaves) + x / kClipWaves) * kWideCh + threadIdx.x] = m;
+  }
+}
+
+// best[q] = max over the chunk's nb per-workgroup maxima (one workgroup per chunk: query t & 127,
+// every 8th maximum from t >> 7, then the 8 slices in LDS).
+__global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long long* __restrict__ part, int32_t nb,
+                                                             int32_t nq, unsigned long long* __restrict__ best) {
+  __shared__ unsigned long long red[8][kWideCh];
+  const int ch = blockIdx.x, t = threadIdx.x & (kWideCh - 1), sl = threadIdx.x >> 7;
+  const unsigned long long* pp = part + (int64_t)ch * nb * kWideCh + t;
+  unsigned long long m = 0;
+#pragma unroll 4
+  for (int32_t x = sl; x < nb; x += 8) m = pp[(int64_t)x * kWideCh] > m ? pp[(int64_t)x * kWideCh] : m;
+  red[sl][t] = m;
+  __syncthreads();
+  if (sl == 0) {
+    for (int j = 1; j < 8; j++) m = red[j][t] > m ? red[j][t] : m;
+    const int32_t q = ch * kWideCh + t;
+    if (m && q < nq) best[q] = m > best[q] ? m : best[q];
+  }
+}
+
 }  // namespace
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, (void*)ptot,
+                  (void*)ukeys, (void*)nuk, (void*)part,
                   (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
     if (p) (void)hipFree(p);
   touch = nullptr;
   ptot = nullptr;
+  ukeys = nuk = nullptr;
+  part = nullptr;
   fq = nullptr;
   doff = dtab = nullptr;
   dtmp = nullptr;
@@ -1140,17 +1406,20 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, (void*)ptot, dtmp})
+    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk,
+                    (void*)part, dtmp})
       if (p) (void)hipFree(p);
-    seg = wpre = cbeg = doff = nullptr;
+    seg = wpre = cbeg = doff = ukeys = nuk = nullptr;
     ptot = nullptr;
+    part = nullptr;
     chw = nullptr;
     dtmp = nullptr;
     dtmp_bytes = 0;
     cap_nch = 0;
     if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
         (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
-        (e = dmalloc(&ptot, nch * kPortions * 64)))
+        (e = dmalloc(&ptot, nch * kPortions * 64)) || (e = dmalloc(&ukeys, nch * kKeyRange)) || (e = dmalloc(&nuk, nch)) ||
+        (e = dmalloc(&part, nch * kPartWaves * kWideCh)))
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1273,6 +1542,19 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
     cv.g_beg = cells->g_beg;
   }
   cv.valid = 1;
+  if (cells->kdir && !ws->groups_form) {
+    // clip-major: xw waves per chunk (a multiple of the workgroup's), ~32 k waves in all
+    int64_t xw = std::max<int64_t>(1, 32768 / nch);
+    xw = std::min<int64_t>(xw, std::min<int64_t>(kPartWaves, cells->nwin));
+    xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
+    hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
+    hipLaunchKernelGGL(wide_clips_kernel, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       C, ws->doff, ws->dtab, ws->part);
+    hipLaunchKernelGGL(wide_part_max_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves), nq,
+                       d_best);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
   hipLaunchKernelGGL(wide_chw_kernel, dim3(1), dim3(1024), 0, s, ws->wpre, nch, ws->chw);
   const int32_t slab = ws->slab > 0 ? ws->slab : 1;

@@ -7,7 +7,8 @@ placed inside every gap and on both ends of it, with q2 at several sub-micro off
 "%f" rounding takes both widths. Each clip has its own key (one query per clip reads that clip's
 exact frame count back as match_count), and all clips also share one key, where the groups batch
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
-(src/fp_handler.c:308-374) and == the point form (TFP_WIDE_POINTS).
+(src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
+(TFP_WIDE_POINTS) and in the key-major form with score rows (TFP_WIDE_GROUPS).
 """
 import math
 import os
@@ -107,7 +108,8 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
         found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, -1, -1)
         expect.append((uuids[w], mc) if found else None)
     got = {}
-    for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"})):
+    for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(len(kinds)):
@@ -120,6 +122,7 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
             eng.close()
     assert got["clusters"] == expect, tol
     assert got["points"] == expect, tol
+    assert got["key-major"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
