@@ -1441,7 +1441,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
   const int64_t row = (int64_t)(C > 0 ? C : 1) * kWideW * (int64_t)sizeof(uint32_t);
   slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
   const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * kWideW;
-  if (ns > cap_score) {
+  if (groups_form && ns > cap_score) {  // (the clip-major sweep keeps its counts in LDS)
     for (void* p : {(void*)score, (void*)touch})
       if (p) (void)hipFree(p);
     score = nullptr;
