@@ -189,7 +189,7 @@ struct CellCache {
   int32_t* c_beg = nullptr;                // [n1 + 1] first cluster of each group
   // the clip-major sweep's directory: kdir[k][w] = first group of key k with column >= kWin w
 #ifndef TFP_CLIP_WIN
-#define TFP_CLIP_WIN 32
+#define TFP_CLIP_WIN 16
 #endif
   static constexpr int32_t kWin = TFP_CLIP_WIN;
   int32_t* kdir = nullptr;                 // [kKeyRange][nwin + 1]
