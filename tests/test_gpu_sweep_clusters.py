@@ -127,3 +127,55 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
         assert 0 < e[1] < qoff[i + 1] - qoff[i]
+
+
+@pytest.mark.parametrize("tol", [0.001, 0.05, 0.3])
+def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
+    """Chunks that use more than 64 keys (the clip-major sweep takes them 64 per step), frames
+    with and without max2 windows (a 3400 Hz ignore filter drops max2 conditions), two 128-query
+    chunks, a last clip window only partly filled, and NULL max2 rows: every form == the oracle."""
+    rng = np.random.default_rng(int(tol * 1e4) + 5)
+    nclips, rows = 70, 260
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
+    keys = rng.integers(-5, 120, nclips * rows)
+    m1 = (keys * 1_000_000 + rng.integers(-350_000, 350_000, nclips * rows)).astype(np.int32)
+    m2 = rng.integers(0, 40_000_000, nclips * rows).astype(np.int32)
+    m2[rng.random(nclips * rows) < 0.02] = np.iinfo(np.int32).min  # NULL max2 (never matches a max2 window)
+    clip = np.repeat(np.arange(nclips), rows).astype(np.int32)
+    nq = 150
+    q1s, q2s, qoff = [], [], [0]
+    for i in range(nq):
+        c = int(rng.integers(nclips))
+        n = int(rng.integers(20, 120))
+        src = rng.integers(c * rows, (c + 1) * rows, n)
+        q1 = m1[src] / 1e6 + rng.normal(0, 0.02, n)
+        q2 = np.where(m2[src] == np.iinfo(np.int32).min, 20.0, m2[src] / 1e6) + rng.normal(0, 0.02, n)
+        q1s.append(q1)
+        q2s.append(q2)
+        qoff.append(qoff[-1] + n)
+    q1 = np.concatenate(q1s)
+    q2 = np.concatenate(q2s)
+    qoff = np.asarray(qoff, np.int64)
+    frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                         ("q1", "<f8"), ("q2", "<f8")]))
+    frames["q1"], frames["q2"] = q1, q2
+    low, high = -1, 3400  # 10 log10(3400) = 35.3: frames with q2 above it keep only their max1 box
+    expect = []
+    for i in range(nq):
+        s = slice(qoff[i], qoff[i + 1])
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, low, high)
+        expect.append((uuids[w], mc) if found else None)
+    assert sum(e is not None for e in expect) > nq // 2
+    for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
+        eng = _engine_with(tfp_lib, env)
+        try:
+            for c in range(nclips):
+                sel = clip == c
+                eng.index_add(uuids[c], m1[sel], m2[sel])
+            res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol, low, high))
+            got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+            assert got == expect, (form, tol, [i for i in range(nq) if got[i] != expect[i]][:5])
+            assert list(fcs) == list(np.diff(qoff))
+        finally:
+            eng.close()
