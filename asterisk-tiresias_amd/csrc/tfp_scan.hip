@@ -1137,7 +1137,10 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
   }
 }
 
-__global__ __launch_bounds__(64 * kClipWaves) void wide_clips_kernel(
+#ifndef TFP_CLIP_OCC
+#define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spills 12 VGPRs)
+#endif
+__global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
