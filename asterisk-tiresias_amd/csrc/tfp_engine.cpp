@@ -165,6 +165,7 @@ struct tfp_engine {
   hipEvent_t qoff_ev = nullptr;
   bool qoff_pending = false;
   DevBuf key_bits;           // key-presence bitsets at tolerance rng_tol (launch_key_bits; small path)
+  DevBuf key_bits_b;         // the other buffer of an update carried across a merge (merge_index)
   bool key_bits_valid = false;
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
@@ -592,7 +593,8 @@ int sort_staged_rows(tfp_engine* e, int64_t b, int64_t n, int64_t* valid) {
 // Index update without a full re-sort (tfp_index.hip): the rows staged since the last build are
 // sorted alone and merged into (m1s, m2s, cols) in one pass that also drops removed clips' rows
 // and renumbers the columns around the inserted / removed uuids. Commits nothing on failure.
-int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
+int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, int32_t new_cols, bool* carried) {
+  *carried = false;
   const int64_t b = e->built_staged, n = e->n_staged - e->built_staged;
   // old column -> new column (-1: the clip was removed)
   std::vector<int32_t> remap(std::max<size_t>(e->col_clip.size(), 1), -1);
@@ -602,7 +604,19 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
     removed |= remap[c] < 0;
   }
   if (n == 0 && !removed) return TFP_OK;  // (e.g. new tie-break keys only: the rows are unchanged)
-  int rc = upload(e, e->remap, remap.data(), sizeof(int32_t) * remap.size());
+  // without removals remap[c] - c only steps up (uuid order is kept): its breakpoints, when few
+  MergeBreaks brk;
+  brk.n = removed ? -1 : 0;
+  for (size_t c = 0, shift = 0; brk.n >= 0 && c < e->col_clip.size(); c++)
+    while ((size_t)remap[c] - c > shift) {
+      if (brk.n == kMergeBreaks) {
+        brk.n = -1;
+        break;
+      }
+      brk.p[brk.n++] = (int32_t)c;
+      shift++;
+    }
+  int rc = brk.n >= 0 ? TFP_OK : upload(e, e->remap, remap.data(), sizeof(int32_t) * remap.size());  // (table: only when gathered)
   if (rc) return rc;
   int64_t valid = 0;
   if (n > 0 && (rc = sort_staged_rows(e, b, n, &valid))) return rc;
@@ -612,7 +626,7 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
   HIPCHK(e, e->cols_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
   int64_t kept = R;
   HIPCHK(e, launch_merge_update(e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->remap.as<int32_t>(),
-                                removed, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
+                                removed, brk, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
                                 &e->merge, e->m1s_b.as<int32_t>(), e->m2s_b.as<int32_t>(), e->cols_b.as<int32_t>(), &kept,
                                 e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -620,6 +634,27 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank) {
   std::swap(e->m2s.p, e->m2s_b.p); std::swap(e->m2s.bytes, e->m2s_b.bytes);
   std::swap(e->cols.p, e->cols_b.p); std::swap(e->cols.bytes, e->cols_b.bytes);
   e->nrows = kept + valid;
+  // The small path's key ranges and bitsets, carried to the merged index at their tolerance
+  // instead of rebuilt from every box row (tfp_index.hpp): the ranges are searched again, the
+  // bitsets get zero columns at the breakpoints (highest first) and the new rows' bits. Only
+  // without removals, with few breakpoints and the same row width; best effort (else rebuilt).
+  const int32_t W = key_bits_words(new_cols);
+  if (brk.n >= 0 && e->rng_valid && e->key_bits_valid && key_bits_words((int32_t)e->col_clip.size()) == W &&
+      e->key_bits.bytes >= sizeof(uint32_t) * (size_t)kKeyRange * W) {
+    hipStream_t s = e->stream;
+    bool ok = launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, e->rng_tol, e->rng_all.as<int64_t>(), s) == hipSuccess &&
+              e->key_bits_b.reserve(e->key_bits.bytes) == hipSuccess;
+    for (int j = brk.n - 1; ok && j >= 0; j--) {
+      ok = launch_key_bits_insert(e->key_bits.as<uint32_t>(), e->key_bits_b.as<uint32_t>(), W, brk.p[j], s) == hipSuccess;
+      std::swap(e->key_bits.p, e->key_bits_b.p);
+      std::swap(e->key_bits.bytes, e->key_bits_b.bytes);
+    }
+    if (ok && valid > 0)
+      ok = launch_key_bits_add(e->rng_all.as<int64_t>(), e->m1s.as<int32_t>(), e->keys_b.as<int32_t>(), e->keys_a.as<int32_t>(),
+                               valid, W, e->key_bits.as<uint32_t>(), s) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    *carried = ok;
+  }
   return TFP_OK;
 }
 
@@ -675,8 +710,9 @@ int rebuild(tfp_engine* e) {
   if ((rc = upload(e, e->rank_of_clip, rank.data(), sizeof(int32_t) * rank.size()))) return rc;
   if ((rc = upload(e, e->tiekey, tiekey.data(), sizeof(int32_t) * tiekey.size()))) return rc;
   const double t_keys = ms_since(t0);
+  bool carried = false;
   if (incremental) {
-    if ((rc = merge_index(e, rank))) return rc;
+    if ((rc = merge_index(e, rank, (int32_t)live.size(), &carried))) return rc;
     e->n_merges++;
   } else {
     e->nrows = 0;
@@ -692,7 +728,8 @@ int rebuild(tfp_engine* e) {
   e->built_clips = e->clips.size();
   e->built_staged = e->n_staged;
   e->dirty = false;
-  e->rng_valid = false;  // the key-range and clip-set caches follow the index
+  e->rng_valid = carried;  // the key-range and clip-set caches follow the index (merge_index may carry the ranges and bitsets)
+  e->key_bits_valid = carried && e->key_bits_valid;
   e->cell_fresh = false;
   if (e->dbg_index)
     fprintf(stderr, "[tfp] index %s: %lld rows, %d clips; order %.3f keys %.3f total %.3f ms\n",

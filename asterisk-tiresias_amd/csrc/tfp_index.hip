@@ -25,6 +25,7 @@
 #include <algorithm>
 
 #include "tfp_index.hpp"
+#include "tfp_kernels.hpp"
 
 namespace tfp {
 namespace {
@@ -59,6 +60,14 @@ __global__ void merge_pos_kernel(const int32_t* __restrict__ m1s, int64_t R, con
     pos[j] = upper_bound_m1(m1s, R, nm1[j]);
 }
 
+// jbeg[t] = the first new row whose insertion point is >= t * 4096 (t = 0..ntiles): each tile's new
+// rows are [jbeg[t], jbeg[t + 1]). Searched once per tile here, so merge_write starts with two
+// loads instead of a chain of dependent ones.
+__global__ void merge_tiles_kernel(const int64_t* __restrict__ pos, int64_t n, int32_t ntiles, int64_t* __restrict__ jbeg) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= ntiles; t += (int64_t)gridDim.x * blockDim.x)
+    jbeg[t] = lower_bound_pos(pos, n, t * kMergeTile);
+}
+
 // kept[t] = old rows of tile t whose clip survives (remap[col] >= 0); kept[ntiles] = 0 (the scan's
 // total lands in base[ntiles]).
 __global__ __launch_bounds__(kThreads) void merge_count_kernel(const int32_t* __restrict__ cols, int64_t R,
@@ -87,40 +96,57 @@ __global__ __launch_bounds__(kThreads) void merge_count_kernel(const int32_t* __
 // base[t]: surviving old rows before tile t (nullptr: nothing removed, base = b0).
 __global__ __launch_bounds__(kThreads) void merge_write_kernel(
     const int32_t* __restrict__ m1s, const int32_t* __restrict__ m2s, const int32_t* __restrict__ cols, int64_t R,
-    const int32_t* __restrict__ remap, const int32_t* __restrict__ base, const int32_t* __restrict__ nm1,
-    const int32_t* __restrict__ nm2, const int32_t* __restrict__ ncol, const int64_t* __restrict__ pos, int64_t n,
-    int32_t* __restrict__ o1, int32_t* __restrict__ o2, int32_t* __restrict__ oc) {
+    const int32_t* __restrict__ remap, MergeBreaks brk, const int32_t* __restrict__ base, const int32_t* __restrict__ nm1,
+    const int32_t* __restrict__ nm2, const int32_t* __restrict__ ncol, const int64_t* __restrict__ pos,
+    const int64_t* __restrict__ jbeg, int32_t* __restrict__ o1, int32_t* __restrict__ o2, int32_t* __restrict__ oc) {
   __shared__ int32_t pref[kMergeTile + 1];          // surviving rows of the tile before each row
   __shared__ int32_t lpos[kPosLds];                 // the tile's insertion points, relative to b0
   __shared__ int32_t csum[kRowsPerThread][kThreads / 64];
-  __shared__ int64_t jr[2];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int64_t b0 = (int64_t)blockIdx.x * kMergeTile;
-  if (t < 2) jr[t] = lower_bound_pos(pos, n, b0 + t * kMergeTile);
-  // the tile's rows, coalesced: row b0 + k * 256 + t
+  const int64_t j0 = jbeg[blockIdx.x], j1 = jbeg[blockIdx.x + 1], nj = j1 - j0;
+  // the tile's rows, coalesced: row b0 + k * 256 + t. Every load is issued before the first
+  // remap gather (indices clamped to the last row, no branches: a branch per row made each row's
+  // gather wait for its column load, 16 round trips per tile).
   int32_t r1[kRowsPerThread], r2[kRowsPerThread], rc[kRowsPerThread];
   uint32_t keep = 0;
+  if (R > 0) {
 #pragma unroll
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const int64_t i = b0 + k * kThreads + t;
-    r1[k] = r2[k] = rc[k] = 0;
-    if (i < R) {
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const int64_t i = min(b0 + k * kThreads + t, R - 1);
       r1[k] = m1s[i];
       r2[k] = m2s[i];
-      rc[k] = remap[cols[i]];
-      keep |= (uint32_t)(rc[k] >= 0) << k;
+      rc[k] = cols[i];
+    }
+    if (brk.n >= 0) {  // no removals: the step function of the breakpoints (kernel arguments)
+#pragma unroll
+      for (int k = 0; k < kRowsPerThread; k++) {
+        int32_t d = 0;
+        for (int j = 0; j < brk.n; j++) d += rc[k] >= brk.p[j];
+        rc[k] += d;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kRowsPerThread; k++) rc[k] = remap[rc[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) keep |= (uint32_t)(b0 + k * kThreads + t < R && rc[k] >= 0) << k;
+  }
+  // Nothing removed (base == nullptr, every old row survives): a row's place in the tile is its own
+  // index, and the tile needs no prefix (an enrolment's update: a plain streaming copy).
+  const bool all_kept = base == nullptr;
+  uint32_t lo[kRowsPerThread];
+  if (!all_kept) {
+    // in-tile exclusive prefix of the surviving rows, in row order (chunk k, then wave, then lane)
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const uint64_t m = __ballot((keep >> k) & 1u);
+      lo[k] = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == 0) csum[k][wv] = __popcll(m);
     }
   }
-  // in-tile exclusive prefix of the surviving rows, in row order (chunk k, then wave, then lane)
-  uint32_t lo[kRowsPerThread];
-#pragma unroll
-  for (int k = 0; k < kRowsPerThread; k++) {
-    const uint64_t m = __ballot((keep >> k) & 1u);
-    lo[k] = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == 0) csum[k][wv] = __popcll(m);
-  }
   __syncthreads();
-  if (t == 0) {  // 64 partial sums, in row order
+  if (!all_kept && t == 0) {  // 64 partial sums, in row order
     int32_t run = 0;
     for (int k = 0; k < kRowsPerThread; k++)
       for (int w = 0; w < kThreads / 64; w++) {
@@ -131,13 +157,14 @@ __global__ __launch_bounds__(kThreads) void merge_write_kernel(
     pref[kMergeTile] = run;
   }
   __syncthreads();
-  const int64_t j0 = jr[0], j1 = jr[1], nj = j1 - j0;
   const bool in_lds = nj <= kPosLds;
   if (in_lds)
     for (int64_t j = t; j < nj; j += kThreads) lpos[j] = (int32_t)(pos[j0 + j] - b0);
+  if (!all_kept)
 #pragma unroll
-  for (int k = 0; k < kRowsPerThread; k++) pref[k * kThreads + t] = csum[k][wv] + (int32_t)lo[k];
+    for (int k = 0; k < kRowsPerThread; k++) pref[k * kThreads + t] = csum[k][wv] + (int32_t)lo[k];
   __syncthreads();
+  auto place = [&](int32_t r) -> int32_t { return all_kept ? r : pref[r]; };
   const int64_t bb = base ? (int64_t)base[blockIdx.x] : b0;
 #pragma unroll
   for (int k = 0; k < kRowsPerThread; k++) {
@@ -154,26 +181,75 @@ __global__ __launch_bounds__(kThreads) void merge_write_kernel(
       }
       before += a;
     }
-    const int64_t o = bb + pref[r] + before;
+    const int64_t o = bb + place(r) + before;
     o1[o] = r1[k];
     o2[o] = r2[k];
     oc[o] = rc[k];
   }
   for (int64_t j = t; j < nj; j += kThreads) {
     const int64_t p = in_lds ? (int64_t)lpos[j] : pos[j0 + j] - b0;  // in [0, 4096]
-    const int64_t o = bb + pref[p] + j0 + j;
+    const int64_t o = bb + place((int32_t)p) + j0 + j;
     o1[o] = nm1[j0 + j];
     o2[o] = nm2[j0 + j];
     oc[o] = ncol[j0 + j];
   }
 }
 
+// One word of a key row with a zero bit inserted at column p (words below p's unchanged).
+__global__ void key_bits_insert_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int32_t W, int32_t p) {
+  const int64_t n = (int64_t)kKeyRange * W;
+  const int32_t wp = p >> 5, bp = p & 31;
+  const uint32_t low = (1u << bp) - 1u;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t w = (int32_t)(i % W);
+    const uint32_t x = src[i];
+    uint32_t y;
+    if (w < wp) y = x;
+    else if (w == wp) y = (x & low) | ((x << 1) & ~(low | (1u << bp)));
+    else y = (x << 1) | (src[i - 1] >> 31);
+    dst[i] = y;
+  }
+}
+
+// Per key: the new rows (sorted by m1) whose m1 lies in [m1 of the box's first row, m1 of its last].
+__global__ __launch_bounds__(64) void key_bits_add_kernel(const int64_t* __restrict__ rng_all, const int32_t* __restrict__ m1s,
+                                                          const int32_t* __restrict__ nm1, const int32_t* __restrict__ ncol,
+                                                          int64_t n, int32_t W, uint32_t* __restrict__ bits) {
+  const int key = blockIdx.x;
+  const int64_t lo = rng_all[2 * key], hi = rng_all[2 * key + 1];
+  if (lo >= hi || n <= 0) return;
+  const int32_t vmin = m1s[lo], vmax = m1s[hi - 1];
+  int64_t a = 0, b = n;  // first new row with m1 >= vmin
+  while (a < b) {
+    const int64_t mid = (a + b) >> 1;
+    if (nm1[mid] < vmin) a = mid + 1; else b = mid;
+  }
+  uint32_t* row = bits + (int64_t)key * W;
+  for (int64_t j = a + threadIdx.x; j < n && nm1[j] <= vmax; j += blockDim.x) {
+    const int32_t c = ncol[j];
+    atomicOr(&row[c >> 5], 1u << (c & 31));
+  }
+}
+
 }  // namespace
 
+hipError_t launch_key_bits_insert(const uint32_t* src, uint32_t* dst, int32_t W, int32_t p, hipStream_t s) {
+  const int64_t n = (int64_t)kKeyRange * W;
+  hipLaunchKernelGGL(key_bits_insert_kernel, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, s, src,
+                     dst, W, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_key_bits_add(const int64_t* d_rng_all, const int32_t* m1s, const int32_t* nm1, const int32_t* ncol,
+                               int64_t n, int32_t W, uint32_t* bits, hipStream_t s) {
+  hipLaunchKernelGGL(key_bits_add_kernel, dim3(kKeyRange), dim3(64), 0, s, d_rng_all, m1s, nm1, ncol, n, W, bits);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge_update(const int32_t* m1s, const int32_t* m2s, const int32_t* cols, int64_t R,
-                               const int32_t* d_remap, bool removed, const int32_t* nm1, const int32_t* nm2,
-                               const int32_t* ncol, int64_t n, MergeScratch* ms, int32_t* o1, int32_t* o2, int32_t* oc,
-                               int64_t* kept_old, hipStream_t s) {
+                               const int32_t* d_remap, bool removed, const MergeBreaks& brk, const int32_t* nm1,
+                               const int32_t* nm2, const int32_t* ncol, int64_t n, MergeScratch* ms, int32_t* o1,
+                               int32_t* o2, int32_t* oc, int64_t* kept_old, hipStream_t s) {
   // tiles: floor(R / 4096) + 1, so the insertion points 0..R all fall in some tile
   const int64_t ntiles = R / kMergeTile + 1;
   if (ntiles >= INT32_MAX / 2) return hipErrorInvalidValue;
@@ -184,6 +260,9 @@ hipError_t launch_merge_update(const int32_t* m1s, const int32_t* m2s, const int
     hipLaunchKernelGGL(merge_pos_kernel, dim3(g), dim3(256), 0, s, m1s, R, nm1, n, ms->pos);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  hipLaunchKernelGGL(merge_tiles_kernel, dim3((unsigned)std::min<int64_t>(1024, (ntiles + 256) / 256)), dim3(256), 0, s,
+                     ms->pos, n, (int32_t)ntiles, ms->jbeg);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
   const int32_t* d_base = nullptr;
   *kept_old = R;
   if (removed) {
@@ -199,8 +278,10 @@ hipError_t launch_merge_update(const int32_t* m1s, const int32_t* m2s, const int
     *kept_old = total;
     d_base = ms->base;
   }
-  hipLaunchKernelGGL(merge_write_kernel, dim3((unsigned)ntiles), dim3(kThreads), 0, s, m1s, m2s, cols, R, d_remap,
-                     d_base, nm1, nm2, ncol, ms->pos, n, o1, o2, oc);
+  MergeBreaks kb = brk;
+  if (removed) kb.n = -1;
+  hipLaunchKernelGGL(merge_write_kernel, dim3((unsigned)ntiles), dim3(kThreads), 0, s, m1s, m2s, cols, R, d_remap, kb,
+                     d_base, nm1, nm2, ncol, ms->pos, ms->jbeg, o1, o2, oc);
   return hipGetLastError();
 }
 
@@ -214,15 +295,17 @@ hipError_t MergeScratch::reserve(int64_t n, int32_t ntiles) {
     cap_pos = n + 1;
   }
   if (ntiles + 1 > cap_tiles) {
-    for (void* p : {(void*)kept, (void*)base, tmp})
+    for (void* p : {(void*)kept, (void*)base, (void*)jbeg, tmp})
       if (p) (void)hipFree(p);
     kept = base = nullptr;
+    jbeg = nullptr;
     tmp = nullptr;
     cap_tiles = 0;
     tmp_bytes = 0;
     const int32_t cap = ntiles + 1 + ntiles / 4;  // room to grow
     if ((e = hipMalloc(&kept, sizeof(int32_t) * cap)) != hipSuccess) return e;
     if ((e = hipMalloc(&base, sizeof(int32_t) * cap)) != hipSuccess) return e;
+    if ((e = hipMalloc(&jbeg, sizeof(int64_t) * cap)) != hipSuccess) return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, kept, base, cap, (hipStream_t)0)) != hipSuccess) return e;
     if ((e = hipMalloc(&tmp, tb > 0 ? tb : 1)) != hipSuccess) return e;
@@ -233,10 +316,11 @@ hipError_t MergeScratch::reserve(int64_t n, int32_t ntiles) {
 }
 
 void MergeScratch::release() {
-  for (void* p : {(void*)pos, (void*)kept, (void*)base, tmp})
+  for (void* p : {(void*)pos, (void*)kept, (void*)base, (void*)jbeg, tmp})
     if (p) (void)hipFree(p);
   pos = nullptr;
   kept = base = nullptr;
+  jbeg = nullptr;
   tmp = nullptr;
   cap_pos = 0;
   cap_tiles = 0;
