@@ -215,3 +215,62 @@ def test_compaction_failure_leaves_index_intact(tfp_lib, oracle):
     assert got == exp
     assert sum(x is not None for x in exp) >= 5
     eng.close()
+
+
+def test_key_bits_carried_across_merges(tfp_lib, oracle):
+    """The small path's key bitsets are carried across single-clip merges (a zero column at each
+    breakpoint, then the new rows' bits; tfp_index.hip key_bits_*), and rebuilt where the row width
+    changes (384 -> 385 clips: 12 -> 16 words) or a clip was removed. Every step's batch-1 searches
+    (the small path reads the bitsets) == the oracle; new uuids sort first, last and in between."""
+    rng = np.random.default_rng(77)
+    nrow = 60
+
+    def rows_of():  # each clip's rows in two of 30 keys' boxes: a query's own clip outscores the rest
+        k = rng.choice(rng.choice(np.arange(10, 40), 2, replace=False), nrow)
+        m1 = (k * 1_000_000 + rng.integers(0, 250_000, nrow)).astype(np.int32)
+        m2 = rng.integers(0, 30_000_000, nrow).astype(np.int32)
+        return m1, m2
+
+    uu = _uuids(rng, 400)
+    uu[385] = "00000000-0000-4000-8000-000000000001"  # sorts first
+    uu[386] = "ffffffff-ffff-4fff-bfff-fffffffffffe"  # sorts last
+    data = [rows_of() for _ in range(400)]
+    eng = tfp_lib.Engine(0)
+    mir = Mirror()
+    p = tfp_lib.params(1, 0.3)
+
+    def check(step, sources):
+        q = []
+        for c in sources:
+            m1, m2 = data[c]
+            sel = rng.integers(0, nrow, 40)
+            q.append(np.stack([m1[sel] / 1e6 + 0.001, m2[sel] / 1e6], axis=1))
+        qdb = np.concatenate(q)
+        qoff = np.arange(len(sources) + 1, dtype=np.int64) * 40
+        exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+        fr = _frames(tfp_lib, qdb)
+        for i in range(len(sources)):
+            r, _ = eng.search(fr[qoff[i]:qoff[i + 1]], p)  # batch-1: the small path over the bitsets
+            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
+        return sum(e is not None for e in exp)
+
+    try:
+        for c in range(380):
+            eng.index_add(uu[c], *data[c])
+            mir.rows[uu[c]] = data[c]
+        eng.index_commit()
+        found = check("initial", [0, 5, 100, 379])
+        for c in list(range(380, 393)) + ["remove", 393, 394]:
+            if c == "remove":
+                eng.index_remove(uu[7])
+                del mir.rows[uu[7]]
+            else:
+                eng.index_add(uu[c], *data[c])
+                mir.rows[uu[c]] = data[c]
+            eng.index_commit()
+            found += check(c, [int(x) for x in rng.integers(0, 380, 2)] + ([c] if c != "remove" else [8]))
+        assert found > 20
+        fb, merges = eng.index_build_stats()
+        assert fb == 1 and merges == 16, (fb, merges)
+    finally:
+        eng.close()
