@@ -12,6 +12,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <numeric>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -134,13 +135,14 @@ struct tfp_engine {
   bool force_full = false;   // TFP_INDEX_FULL: every update is a full build (A/B, tests)
   size_t built_clips = 0;
   int64_t built_staged = 0;
+  bool removed_built = false;  // a clip of the last build was removed since (else an update only adds)
+  int64_t live_rows = 0;       // staged rows of live clips (kept per add / remove, not counted per build)
   int64_t n_merges = 0, n_full_builds = 0;
   DevBuf m1s_b, m2s_b, cols_b, remap;
   MergeScratch merge;
   int64_t nrows = 0;       // rows that can match (live clip, non-NULL max1)
   int32_t ncols = 0;       // live clips
   std::vector<int32_t> col_clip;                 // column (uuid rank) -> clip id
-  std::vector<int32_t> tiekey_host;              // column -> tie-break key
   std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> column (with an override)
   bool key_identity = true;                      // no override: key == column
   std::vector<int32_t> tiebreak_override;        // clip id -> key (empty = uuid rank)
@@ -462,6 +464,7 @@ int new_clip(tfp_engine* e, const char* uuid, int64_t nrows, int64_t off, int32_
   *id = (int32_t)e->clips.size();
   e->clips.push_back(c);
   e->by_uuid[uuid] = *id;
+  e->live_rows += nrows;
   e->dirty = true;
   return TFP_OK;
 }
@@ -534,14 +537,25 @@ int compact_staging(tfp_engine* e) {
 // Live clips in uuid order (the columns: the tie-break order of SQLite's result sort) and each
 // clip's rank (-1 when dead). Incremental: the previous build's order with the clips added since
 // merged in (no re-sort of every uuid).
-void live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* live, std::vector<int32_t>* rank) {
+// Returns true for an update that only adds (no clip of the last build removed) with at most
+// kMergeBreaks new uuids placed before an old one: the old columns are then col_clip as it stands
+// (no alive filter), *brk is the merge's column map (old col c -> c + breakpoints <= c) and rank
+// holds the new clips' ranks only (the merge and the device rank table read no other; skipping
+// the scatter over every clip is most of an enrolment's host time at 100k clips).
+bool live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* live, std::vector<int32_t>* rank,
+                MergeBreaks* brk) {
   auto by_uuid = [&](int32_t a, int32_t b) { return e->clips[a].uuid < e->clips[b].uuid; };
   live->clear();
+  brk->n = -1;
   if (incremental) {
-    std::vector<int32_t> old, add;
-    old.reserve(e->col_clip.size());
-    for (int32_t c : e->col_clip)
-      if (e->clips[c].alive) old.push_back(c);
+    const bool add_only = !e->removed_built;
+    std::vector<int32_t> kept, add;
+    if (!add_only) {
+      kept.reserve(e->col_clip.size());
+      for (int32_t c : e->col_clip)
+        if (e->clips[c].alive) kept.push_back(c);
+    }
+    const std::vector<int32_t>& old = add_only ? e->col_clip : kept;
     for (int32_t i = (int32_t)e->built_clips; i < (int32_t)e->clips.size(); i++)
       if (e->clips[i].alive) add.push_back(i);
     std::sort(add.begin(), add.end(), by_uuid);
@@ -549,14 +563,26 @@ void live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* liv
     // string compares per new clip instead of a linear merge (each compare is two uuid strings
     // on the heap, a cache miss apiece: ~10 ms at 100k clips)
     live->reserve(old.size() + add.size());
+    std::vector<int32_t> at_col(add.size());
+    int32_t before_old = 0;  // new uuids placed before some old one
     auto from = old.begin();
-    for (int32_t a : add) {
-      const auto at = std::lower_bound(from, old.end(), a, by_uuid);
+    for (size_t j = 0; j < add.size(); j++) {
+      const auto at = std::lower_bound(from, old.end(), add[j], by_uuid);
       live->insert(live->end(), from, at);
-      live->push_back(a);
+      live->push_back(add[j]);
       from = at;
+      at_col[j] = (int32_t)(at - old.begin());
+      before_old += at != old.end();
     }
     live->insert(live->end(), from, old.end());
+    if (add_only && before_old <= kMergeBreaks) {
+      brk->n = 0;
+      for (int32_t p : at_col)
+        if ((size_t)p < old.size()) brk->p[brk->n++] = p;
+      rank->assign(std::max<size_t>(e->clips.size(), 1), -1);
+      for (size_t j = 0; j < add.size(); j++) (*rank)[add[j]] = at_col[j] + (int32_t)j;
+      return true;
+    }
   } else {
     for (int32_t i = 0; i < (int32_t)e->clips.size(); i++)
       if (e->clips[i].alive) live->push_back(i);
@@ -564,11 +590,15 @@ void live_order(const tfp_engine* e, bool incremental, std::vector<int32_t>* liv
   }
   rank->assign(std::max<size_t>(e->clips.size(), 1), -1);
   for (size_t r = 0; r < live->size(); r++) (*rank)[(*live)[r]] = (int32_t)r;
+  return false;
 }
 
-// Sorted (m1, m2, col) of staging rows [b, b + n) whose clip is live and max1 non-NULL: m1 in
-// keys_b, m2 in vals_a, col in keys_a (the first *valid entries). Synchronous.
-int sort_staged_rows(tfp_engine* e, int64_t b, int64_t n, int64_t* valid) {
+// Staging rows [b, b + n) sorted by m1 with the rows that cannot match (dead clip or NULL max1,
+// key INT32_MAX) last: m1 in keys_b, m2 in vals_a, col in keys_a; the count of the others (the
+// first ones) in e->cnt. Asynchronous: the merge runs over all n rows (those with key INT32_MAX
+// land after every index row, past the new row count) and the count is read with its result,
+// one host wait per update instead of two.
+int sort_staged_rows(tfp_engine* e, int64_t b, int64_t n) {
   HIPCHK(e, e->keys_a.reserve(sizeof(int32_t) * (n + 1)));
   HIPCHK(e, e->keys_b.reserve(sizeof(int32_t) * (n + 1)));
   HIPCHK(e, e->vals_a.reserve(sizeof(int32_t) * (n + 1)));
@@ -582,54 +612,68 @@ int sort_staged_rows(tfp_engine* e, int64_t b, int64_t n, int64_t* valid) {
                              e->vals_a.as<int32_t>(), e->vals_b.as<int32_t>(), n, e->stream));
   HIPCHK(e, e->cnt.reserve(sizeof(int64_t)));
   HIPCHK(e, launch_count_below(e->keys_b.as<int32_t>(), n, INT32_MAX, e->cnt.as<int64_t>(), e->stream));
+  HIPCHK(e, launch_index_gather(e->vals_b.as<int32_t>(), e->st_m2.as<int32_t>() + b, e->st_clip.as<int32_t>() + b,
+                                e->rank_of_clip.as<int32_t>(), n, e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), e->stream));
+  return TFP_OK;
+}
+
+// e->cnt (sort_staged_rows' row count) after the work queued on e->stream. Synchronous.
+int read_sorted_count(tfp_engine* e, int64_t* valid) {
   HIPCHK(e, hipMemcpyAsync(valid, e->cnt.p, sizeof *valid, hipMemcpyDeviceToHost, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  if (*valid)
-    HIPCHK(e, launch_index_gather(e->vals_b.as<int32_t>(), e->st_m2.as<int32_t>() + b, e->st_clip.as<int32_t>() + b,
-                                  e->rank_of_clip.as<int32_t>(), *valid, e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(),
-                                  e->stream));
   return TFP_OK;
 }
 
 // Index update without a full re-sort (tfp_index.hip): the rows staged since the last build are
 // sorted alone and merged into (m1s, m2s, cols) in one pass that also drops removed clips' rows
 // and renumbers the columns around the inserted / removed uuids. Commits nothing on failure.
-int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, int32_t new_cols, bool* carried) {
+// fast_brk: live_order's column map of an update that only adds (rank then holds the new clips'
+// ranks only), else nullptr (the map from rank over every old column).
+int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, const MergeBreaks* fast_brk, int32_t new_cols,
+                bool* carried) {
   *carried = false;
   const int64_t b = e->built_staged, n = e->n_staged - e->built_staged;
-  // old column -> new column (-1: the clip was removed)
-  std::vector<int32_t> remap(std::max<size_t>(e->col_clip.size(), 1), -1);
   bool removed = false;
-  for (size_t c = 0; c < e->col_clip.size(); c++) {
-    remap[c] = rank[e->col_clip[c]];
-    removed |= remap[c] < 0;
-  }
-  if (n == 0 && !removed) return TFP_OK;  // (e.g. new tie-break keys only: the rows are unchanged)
-  // without removals remap[c] - c only steps up (uuid order is kept): its breakpoints, when few
   MergeBreaks brk;
-  brk.n = removed ? -1 : 0;
-  for (size_t c = 0, shift = 0; brk.n >= 0 && c < e->col_clip.size(); c++)
-    while ((size_t)remap[c] - c > shift) {
-      if (brk.n == kMergeBreaks) {
-        brk.n = -1;
-        break;
-      }
-      brk.p[brk.n++] = (int32_t)c;
-      shift++;
+  int rc = TFP_OK;
+  if (fast_brk) {
+    brk = *fast_brk;
+  } else {
+    // old column -> new column (-1: the clip was removed)
+    std::vector<int32_t> remap(std::max<size_t>(e->col_clip.size(), 1), -1);
+    for (size_t c = 0; c < e->col_clip.size(); c++) {
+      remap[c] = rank[e->col_clip[c]];
+      removed |= remap[c] < 0;
     }
-  int rc = brk.n >= 0 ? TFP_OK : upload(e, e->remap, remap.data(), sizeof(int32_t) * remap.size());  // (table: only when gathered)
-  if (rc) return rc;
-  int64_t valid = 0;
-  if (n > 0 && (rc = sort_staged_rows(e, b, n, &valid))) return rc;
+    // without removals remap[c] - c only steps up (uuid order is kept): its breakpoints, when few
+    brk.n = removed ? -1 : 0;
+    for (size_t c = 0, shift = 0; brk.n >= 0 && c < e->col_clip.size(); c++)
+      while ((size_t)remap[c] - c > shift) {
+        if (brk.n == kMergeBreaks) {
+          brk.n = -1;
+          break;
+        }
+        brk.p[brk.n++] = (int32_t)c;
+        shift++;
+      }
+    if (brk.n < 0 && (rc = upload(e, e->remap, remap.data(), sizeof(int32_t) * remap.size())))  // (only when gathered)
+      return rc;
+  }
+  // (e.g. new tie-break keys only: the rows and their columns are unchanged; a clip without rows
+  // placed before an old one still renumbers the columns)
+  if (n == 0 && !removed && brk.n == 0) return TFP_OK;
+  if (n > 0 && (rc = sort_staged_rows(e, b, n))) return rc;
   const int64_t R = e->nrows;
-  HIPCHK(e, e->m1s_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
-  HIPCHK(e, e->m2s_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
-  HIPCHK(e, e->cols_b.reserve_grow(sizeof(int32_t) * (R + valid + 1)));
+  HIPCHK(e, e->m1s_b.reserve_grow(sizeof(int32_t) * (R + n + 1)));
+  HIPCHK(e, e->m2s_b.reserve_grow(sizeof(int32_t) * (R + n + 1)));
+  HIPCHK(e, e->cols_b.reserve_grow(sizeof(int32_t) * (R + n + 1)));
   int64_t kept = R;
   HIPCHK(e, launch_merge_update(e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, e->remap.as<int32_t>(),
-                                removed, brk, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
+                                removed, brk, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), n,
                                 &e->merge, e->m1s_b.as<int32_t>(), e->m2s_b.as<int32_t>(), e->cols_b.as<int32_t>(), &kept,
                                 e->stream));
+  int64_t valid = 0;
+  if (n > 0 && (rc = read_sorted_count(e, &valid))) return rc;
   HIPCHK(e, hipStreamSynchronize(e->stream));
   std::swap(e->m1s.p, e->m1s_b.p); std::swap(e->m1s.bytes, e->m1s_b.bytes);
   std::swap(e->m2s.p, e->m2s_b.p); std::swap(e->m2s.bytes, e->m2s_b.bytes);
@@ -670,9 +714,7 @@ int rebuild(tfp_engine* e) {
   // Incremental (merge) when there is an index to merge into, the new rows are few next to it, and
   // the staging area needs no compaction (the staged rows since the last build are then exactly
   // rows [built_staged, n_staged)); otherwise the full build.
-  int64_t live_rows = 0;
-  for (const auto& c : e->clips)
-    if (c.alive) live_rows += c.nrows;
+  const int64_t live_rows = e->live_rows;
   const int64_t dead = e->n_staged - live_rows, fresh = e->n_staged - e->built_staged;
   const bool incremental = e->built && !e->force_full && fresh <= std::max<int64_t>(e->nrows / 2, 0) &&
                            dead <= std::max<int64_t>(1 << 16, live_rows / 4) && e->n_staged < INT32_MAX;
@@ -684,21 +726,22 @@ int rebuild(tfp_engine* e) {
       return fail(e, TFP_E_CAPACITY, "%lld staged rows (limit 2^31 - 1)", (long long)e->n_staged);
   }
   std::vector<int32_t> live, rank;
-  live_order(e, incremental, &live, &rank);
+  MergeBreaks brk;
+  const bool add_only = live_order(e, incremental, &live, &rank, &brk);
   const double t_order = ms_since(t0);
-  std::vector<int32_t> tiekey(std::max<size_t>(live.size(), 1), 0);
+  const size_t nkeys = std::max<size_t>(live.size(), 1);
+  std::vector<int32_t> tiekey;  // column -> tie-break key: with an override every column, else the identity's new tail
   // key -> column: the identity without an override (the key is the uuid rank), so no map is built
   // (a 100k-entry hash map was most of an enrolment's host time); with one, a map that also
   // rejects a key given twice
   std::unordered_map<int32_t, int32_t> key_col;
   const bool ovr = !e->tiebreak_override.empty();
-  if (ovr) key_col.reserve(live.size());
-  for (size_t r = 0; r < live.size(); r++) {
+  if (ovr) {
+    key_col.reserve(live.size());
+    tiekey.assign(nkeys, 0);
+  }
+  for (size_t r = 0; ovr && r < live.size(); r++) {
     const int32_t clip = live[r];
-    if (!ovr) {
-      tiekey[r] = (int32_t)r;
-      continue;
-    }
     // With an override every live clip needs its own key (a clip added after the override would
     // otherwise take its local rank, which can equal another shard's global key).
     if ((size_t)clip >= e->tiebreak_override.size())
@@ -719,16 +762,21 @@ int rebuild(tfp_engine* e) {
     const void* before = e->tiekey.p;
     const int64_t ident = e->tiekey_ident;
     e->tiekey_ident = -1;
-    HIPCHK(e, e->tiekey.reserve_grow(sizeof(int32_t) * tiekey.size()));
-    const size_t tb = !ovr && e->tiekey.p == before && ident > 0 ? std::min<size_t>((size_t)ident, tiekey.size()) : 0;
-    HIPCHK(e, hipMemcpyAsync(e->tiekey.as<int32_t>() + tb, tiekey.data() + tb, sizeof(int32_t) * (tiekey.size() - tb),
-                             hipMemcpyHostToDevice, e->stream));
-    if (!ovr) e->tiekey_ident = (int64_t)tiekey.size();
+    HIPCHK(e, e->tiekey.reserve_grow(sizeof(int32_t) * nkeys));
+    const size_t tb = !ovr && e->tiekey.p == before && ident > 0 ? std::min<size_t>((size_t)ident, nkeys) : 0;
+    if (!ovr) {
+      tiekey.resize(nkeys - tb);
+      std::iota(tiekey.begin(), tiekey.end(), (int32_t)tb);
+    }
+    if (nkeys > tb)
+      HIPCHK(e, hipMemcpyAsync(e->tiekey.as<int32_t>() + tb, tiekey.data(), sizeof(int32_t) * (nkeys - tb),
+                               hipMemcpyHostToDevice, e->stream));
+    if (!ovr) e->tiekey_ident = (int64_t)nkeys;
   }
   const double t_keys = ms_since(t0);
   bool carried = false;
   if (incremental) {
-    if ((rc = merge_index(e, rank, (int32_t)live.size(), &carried))) return rc;
+    if ((rc = merge_index(e, rank, add_only ? &brk : nullptr, (int32_t)live.size(), &carried))) return rc;
     e->n_merges++;
   } else {
     e->nrows = 0;
@@ -737,12 +785,12 @@ int rebuild(tfp_engine* e) {
   }
   e->ncols = (int32_t)live.size();
   e->col_clip = std::move(live);
-  e->tiekey_host = std::move(tiekey);
   e->key_col = std::move(key_col);
   e->key_identity = !ovr;
   e->built = true;
   e->built_clips = e->clips.size();
   e->built_staged = e->n_staged;
+  e->removed_built = false;
   e->dirty = false;
   e->rng_valid = carried;  // the key-range and clip-set caches follow the index (merge_index may carry the ranges and bitsets)
   e->key_bits_valid = carried && e->key_bits_valid;
@@ -759,9 +807,9 @@ int full_index(tfp_engine* e) {
   const int64_t n = e->n_staged;
   int64_t valid = 0;
   if (n > 0) {
-    int rc = sort_staged_rows(e, 0, n, &valid);
+    int rc = sort_staged_rows(e, 0, n);
+    if (!rc) rc = read_sorted_count(e, &valid);
     if (rc) return rc;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
     std::swap(e->m1s.p, e->keys_b.p); std::swap(e->m1s.bytes, e->keys_b.bytes);
     std::swap(e->m2s.p, e->vals_a.p); std::swap(e->m2s.bytes, e->vals_a.bytes);
     std::swap(e->cols.p, e->keys_a.p); std::swap(e->cols.bytes, e->keys_a.bytes);
@@ -1337,7 +1385,10 @@ int tfp_index_remove(tfp_engine* e, const char* uuid) {
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   auto it = e->by_uuid.find(uuid);
   if (it == e->by_uuid.end()) return fail(e, TFP_E_NOENT, "uuid %s not indexed", uuid);
-  e->clips[it->second].alive = false;
+  Clip& c = e->clips[it->second];
+  c.alive = false;
+  e->live_rows -= c.nrows;
+  e->removed_built |= (size_t)it->second < e->built_clips;
   e->by_uuid.erase(it);
   e->dirty = true;
   return TFP_OK;
@@ -1353,6 +1404,8 @@ int tfp_index_clear(tfp_engine* e) {
   e->built = false;
   e->built_clips = 0;
   e->built_staged = 0;
+  e->removed_built = false;
+  e->live_rows = 0;
   e->col_clip.clear();
   e->dirty = true;
   return TFP_OK;

@@ -274,3 +274,88 @@ def test_key_bits_carried_across_merges(tfp_lib, oracle):
         assert fb == 1 and merges == 16, (fb, merges)
     finally:
         eng.close()
+
+
+def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle):
+    """Updates that only add take the engine's host fast path (no pass over every clip; the
+    column map from the new uuids' insertion points, csrc/tfp_engine.cpp live_order) and merge every
+    staged row with the rows that cannot match (NULL max1: the reference's max1 >= ... never holds
+    for them, fp_handler.c:339-347) sorted past the new row count. Covered: a clip without rows that
+    sorts first (the columns still shift), clips with some and with only NULL max1 rows, a clip
+    added and removed between builds (still add-only), more new uuids before old ones than the
+    column map holds, a removal (the general path) and an add after it. Every step, batch and
+    batch-1 searches == the oracle over the live rows."""
+    rng = np.random.default_rng(123)
+    nrow = 60
+
+    def rows_of():
+        k = rng.choice(rng.choice(np.arange(10, 40), 2, replace=False), nrow)
+        m1 = (k * 1_000_000 + rng.integers(0, 250_000, nrow)).astype(np.int32)
+        m2 = rng.integers(0, 30_000_000, nrow).astype(np.int32)
+        return m1, m2
+
+    uu = _uuids(rng, 260)
+    uu[200] = "00000000-0000-4000-8000-000000000002"  # sorts first
+    for i in range(240, 252):                          # sort before most old uuids
+        uu[i] = "0%07x-0000-4000-8000-000000000000" % (i * 997)
+    data = [rows_of() for _ in range(260)]
+    data[200] = (np.zeros(0, np.int32), np.zeros(0, np.int32))
+    m1 = data[201][0].copy()
+    m1[::2] = tfp_lib.NULL_MICRO
+    data[201] = (m1, data[201][1])
+    data[202] = (np.full(nrow, tfp_lib.NULL_MICRO, np.int32), data[202][1])
+    eng = tfp_lib.Engine(0)
+    mir = Mirror()
+    params = (tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05))
+
+    def check(step, sources):
+        q = []
+        for c in sources:
+            m1, m2 = data[c]
+            sel = rng.integers(0, nrow, 40)
+            q.append(np.stack([m1[sel] / 1e6 + 0.001, m2[sel] / 1e6], axis=1))
+        qdb = np.concatenate(q)
+        qoff = np.arange(len(sources) + 1, dtype=np.int64) * 40
+        fr = _frames(tfp_lib, qdb)
+        found = 0
+        for p in params:
+            exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+            res, _ = eng.search_batch(fr, qoff, p)
+            got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+            assert got == exp, (step, p.coefs)
+            found += sum(e is not None for e in exp)
+        p = params[0]
+        exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+        for i in range(len(sources)):
+            r, _ = eng.search(fr[qoff[i]:qoff[i + 1]], p)  # batch-1: the small path
+            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
+        return found
+
+    def add(cs):
+        for c in cs:
+            eng.index_add(uu[c], *data[c])
+            mir.rows[uu[c]] = data[c]
+
+    try:
+        add(range(200))
+        eng.index_commit()
+        found = check("initial", [0, 50, 199])
+        steps = [("empty clip first", [200], None), ("half NULL", [201], None), ("all NULL", [202], None),
+                 ("batch + transient", [203, 204, 205], 206), ("12 before old uuids", list(range(240, 252)), None),
+                 ("removal", [207], "remove"), ("after removal", [208], None), ("one more", [209], None)]
+        for name, cs, extra in steps:
+            if extra == "remove":
+                eng.index_remove(uu[3])
+                del mir.rows[uu[3]]
+            add(cs)
+            if isinstance(extra, int):  # added and removed before the build
+                eng.index_add(uu[extra], *data[extra])
+                eng.index_remove(uu[extra])
+            eng.index_commit()
+            found += check(name, [int(x) for x in rng.integers(4, 200, 2)] + [c for c in cs if c not in (200, 201, 202)])
+        assert found > 20
+        fb, merges = eng.index_build_stats()
+        assert fb == 1 and merges == len(steps), (fb, merges)
+        assert eng.index_stats() == (sum(len(r[0]) for r in mir.rows.values()), len(mir.rows))
+    finally:
+        eng.close()
