@@ -1114,7 +1114,6 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   e->wide.points_only = getenv("TFP_WIDE_POINTS") != nullptr;
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
-  e->wide.radix_sort = getenv("TFP_WIDE_RADIX") != nullptr;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;

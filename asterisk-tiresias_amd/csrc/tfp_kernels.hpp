@@ -234,7 +234,7 @@ struct WideScratch {
   int64_t* chw = nullptr;                            // [nchunks + 1] first work item of each chunk
   uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
   uint8_t* touch = nullptr;                          // [slab][C] 1 = the chunk scored the clip; zero between calls
-  int32_t* info = nullptr;                           // [4]: frames kept, ineligible frames, wide windows, a segment too large to sort in LDS
+  int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
   int32_t* doff = nullptr;                           // [nchunks * kKeyRange + 1] each window segment's directory offset
   int32_t* dtab = nullptr;                           // [<= 4 nf] segment directories: first frame per L2 / U2 bucket
   void* tmp = nullptr;
@@ -249,13 +249,6 @@ struct WideScratch {
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
   int32_t* nuk = nullptr;                            // [nchunks] their number
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima
-  // the frame sort by (chunk, key) counts and a sort per segment in LDS (tfp_scan.hip wide_seg_*)
-  int32_t* shist = nullptr;                          // [nchunks][kWideSegs][slices] + [nchunks][slices] + 1 counts
-  int32_t* soff = nullptr;                           // ... their exclusive prefix: each slice's first sorted position
-  void* stmp = nullptr;
-  size_t stmp_bytes = 0;
-  int64_t cap_shist = 0;
-  bool radix_sort = false;                           // TFP_WIDE_RADIX (tests, A/B): hipCUB's sort of the composite keys
   hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
   void release();
   WideScratch() = default;

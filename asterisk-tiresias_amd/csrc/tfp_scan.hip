@@ -596,150 +596,6 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
   }
 }
 
-// The same order without the device-wide sort (hipCUB's merge sort of 0.6 M pairs is ~20 launches
-// and 0.15 ms at C3): the frames of a chunk are contiguous (queries in order), so
-//   wide_seg_count: per (chunk, slice of its frames) block, each frame's key without the chunk bits
-//     (ka; ~0 for frames that take no part) and an LDS histogram by segment key, stored as
-//     shist[chunk][segment][slice] (the frames that take no part after every chunk's segments);
-//   an exclusive scan of shist (soff): each (chunk, segment, slice)'s first position;
-//   wide_seg_scatter: each frame's position from its slice's LDS cursor (order within a segment
-//     arbitrary);
-//   wide_seg_sort: per segment, a bitonic sort in LDS by (L2, U2 - L2, frame in chunk).
-// The last key field is the frame, so the result is the stable radix sort's exactly: same keys
-// (kb) and frame order (vb). A segment above kSegSortCap frames sets info[3] and the caller takes
-// the radix sort after its one host wait.
-constexpr int kSegSortCap = 4096, kSegSortThreads = 256, kSegFrameBits = 23;  // frame in chunk < 128 x 65536
-constexpr int64_t kSegSortMaxChunks = 4096;                                  // shist stays <= 32 MB
-inline int32_t seg_slices(int64_t nch) { return (int32_t)std::max<int64_t>(1, std::min<int64_t>(8, 256 / nch)); }
-
-__device__ __forceinline__ void chunk_frames(const int64_t* __restrict__ qoff, int32_t nq, int64_t ch, int64_t* f0,
-                                             int64_t* f1) {
-  *f0 = qoff[ch * kWideCh] - qoff[0];
-  *f1 = qoff[min((ch + 1) * kWideCh, (int64_t)nq)] - qoff[0];
-}
-
-__global__ __launch_bounds__(512) void wide_seg_count_kernel(const FrameBox* __restrict__ boxes,
-                                                             const int64_t* __restrict__ qoff, int32_t nq, int64_t dbase,
-                                                             unsigned long long* __restrict__ ka, int32_t* __restrict__ hist,
-                                                             int32_t* __restrict__ info) {
-  __shared__ int32_t h[kWideSegs + 1];
-  __shared__ int32_t red[512 / 64];
-  const int64_t ch = blockIdx.x, nch = gridDim.x;
-  const int32_t S = gridDim.y, j = blockIdx.y;
-  for (int b = threadIdx.x; b <= kWideSegs; b += blockDim.x) h[b] = 0;
-  __syncthreads();
-  int64_t c0, c1;
-  chunk_frames(qoff, nq, ch, &c0, &c1);
-  const int64_t f0 = c0 + (c1 - c0) * j / S, f1 = c0 + (c1 - c0) * (j + 1) / S;
-  int32_t wide = 0;
-  for (int64_t f = f0 + threadIdx.x; f < f1; f += blockDim.x) {
-    const FrameBox bx = boxes[f];  // (as wide_keys_c_kernel, without the chunk field)
-    unsigned long long key = ~0ull;
-    int32_t bin = kWideSegs;
-    const int64_t kk = (int64_t)bx.k + kKeyOffset;
-    if ((bx.flags & 1) && kk >= 0 && kk < kKeyRange) {
-      const bool w2 = bx.flags & 2;
-      bin = w2 ? (int32_t)kk : (int32_t)kk | kKeyRange;
-      const unsigned long long l2 = w2 ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
-      unsigned long long d = 0;
-      if (w2 && dbase >= 0) {
-        const int64_t dd = bx.U2 - bx.L2 - dbase;
-        if (dd < 0 || dd >= (1 << kWideDeltaBits)) wide++;
-        else d = (unsigned long long)dd;
-      }
-      key = ((unsigned long long)bin << kWideSegShift) | (l2 << kWideDeltaBits) | d;
-    }
-    ka[f] = key;
-    atomicAdd(&h[bin], 1);
-  }
-  for (int o = 32; o > 0; o >>= 1) wide += __shfl_xor(wide, o, 64);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wide;
-  __syncthreads();
-  for (int b = threadIdx.x; b < kWideSegs; b += blockDim.x) hist[(ch * kWideSegs + b) * S + j] = h[b];
-  if (threadIdx.x == 0) {
-    hist[nch * kWideSegs * S + ch * S + j] = h[kWideSegs];
-    int32_t w = 0;
-    for (int i = 0; i < 512 / 64; i++) w += red[i];
-    if (w) atomicAdd(&info[2], w);
-  }
-}
-
-__global__ __launch_bounds__(512) void wide_seg_scatter_kernel(const int64_t* __restrict__ qoff, int32_t nq,
-                                                               const unsigned long long* __restrict__ ka,
-                                                               const int32_t* __restrict__ off, int32_t* __restrict__ va) {
-  __shared__ int32_t cur[kWideSegs];
-  const int64_t ch = blockIdx.x;
-  const int32_t S = gridDim.y, j = blockIdx.y;
-  for (int b = threadIdx.x; b < kWideSegs; b += blockDim.x) cur[b] = off[(ch * kWideSegs + b) * S + j];
-  __syncthreads();
-  int64_t c0, c1;
-  chunk_frames(qoff, nq, ch, &c0, &c1);
-  const int64_t f0 = c0 + (c1 - c0) * j / S, f1 = c0 + (c1 - c0) * (j + 1) / S;
-  for (int64_t f = f0 + threadIdx.x; f < f1; f += blockDim.x) {
-    const unsigned long long key = ka[f];
-    if (key != ~0ull) va[atomicAdd(&cur[(int32_t)(key >> kWideSegShift)], 1)] = (int32_t)f;
-  }
-}
-
-// One segment per iteration of a persistent grid (most (chunk, segment) pairs are empty).
-__global__ __launch_bounds__(kSegSortThreads) void wide_seg_sort_kernel(
-    const int64_t* __restrict__ qoff, int32_t nq, int64_t nch, int32_t S, const unsigned long long* __restrict__ ka,
-    const int32_t* __restrict__ off, const int32_t* __restrict__ va, unsigned long long* __restrict__ kb,
-    int32_t* __restrict__ vb, int32_t* __restrict__ info) {
-  __shared__ unsigned long long sk[kSegSortCap];
-  const int64_t nseg = nch * kWideSegs;
-  if (blockIdx.x == 0 && threadIdx.x == 0) info[0] = off[nseg * S];  // frames kept
-  constexpr unsigned long long kLow = (1ull << kWideSegShift) - 1, kFrame = (1ull << kSegFrameBits) - 1;
-  for (int64_t sid = blockIdx.x; sid < nseg; sid += gridDim.x) {
-    const int32_t b = off[sid * S], n = off[(sid + 1) * S] - b;
-    if (n == 0) continue;
-    if (n > kSegSortCap) {
-      if (threadIdx.x == 0) info[3] = 1;
-      continue;
-    }
-    const int64_t ch = sid / kWideSegs;
-    const unsigned long long hi = ((unsigned long long)ch << kWideChunkShift) | ((unsigned long long)(sid % kWideSegs) << kWideSegShift);
-    const int64_t c0 = qoff[ch * kWideCh] - qoff[0];
-    if (n == 1) {
-      if (threadIdx.x == 0) {
-        const int32_t f = va[b];
-        kb[b] = hi | (ka[f] & kLow);
-        vb[b] = f;
-      }
-      continue;
-    }
-    int32_t P = 2;
-    while (P < n) P <<= 1;
-    for (int32_t i = threadIdx.x; i < P; i += kSegSortThreads) {
-      unsigned long long v = ~0ull;
-      if (i < n) {
-        const int32_t f = va[b + i];
-        v = ((ka[f] & kLow) << kSegFrameBits) | (unsigned long long)(f - c0);
-      }
-      sk[i] = v;
-    }
-    __syncthreads();
-    for (int32_t k = 2; k <= P; k <<= 1)
-      for (int32_t jj = k >> 1; jj > 0; jj >>= 1) {
-        for (int32_t t = threadIdx.x; t < (P >> 1); t += kSegSortThreads) {
-          const int32_t i = ((t & ~(jj - 1)) << 1) | (t & (jj - 1)), l = i | jj;
-          const unsigned long long x = sk[i], y = sk[l];
-          if ((x > y) == ((i & k) == 0)) {
-            sk[i] = y;
-            sk[l] = x;
-          }
-        }
-        __syncthreads();
-      }
-    for (int32_t i = threadIdx.x; i < n; i += kSegSortThreads) {
-      const unsigned long long v = sk[i];
-      kb[b + i] = hi | (v >> kSegFrameBits);
-      vb[b + i] = (int32_t)(c0 + (int64_t)(v & kFrame));
-    }
-    __syncthreads();
-  }
-}
-
 // Sorted frames' windows and queries; the segment table [chunk][segment key] = [begin, end).
 __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    int64_t n, const unsigned long long* __restrict__ ck,
@@ -1502,12 +1358,8 @@ void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, (void*)ptot,
                   (void*)ukeys, (void*)nuk, (void*)part,
-                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)shist, (void*)soff, stmp})
+                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
     if (p) (void)hipFree(p);
-  shist = soff = nullptr;
-  stmp = nullptr;
-  stmp_bytes = 0;
-  cap_shist = 0;
   touch = nullptr;
   ptot = nullptr;
   ukeys = nuk = nullptr;
@@ -1606,23 +1458,6 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_score = ns;
   }
   if (!info && (e = dmalloc(&info, 4))) return e;
-  if (!radix_sort && nch <= kSegSortMaxChunks) {
-    const int64_t nh = nch * (kWideSegs + 1) * seg_slices(nch) + 1;
-    if (nh > cap_shist) {
-      for (void* p : {(void*)shist, (void*)soff, stmp})
-        if (p) (void)hipFree(p);
-      shist = soff = nullptr;
-      stmp = nullptr;
-      stmp_bytes = 0;
-      cap_shist = 0;
-      if ((e = dmalloc(&shist, nh)) || (e = dmalloc(&soff, nh))) return e;
-      size_t tb = 0;
-      if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, shist, soff, (int)nh, s))) return e;
-      if ((e = hipMalloc(&stmp, tb > 0 ? tb : 1))) return e;
-      stmp_bytes = tb;
-      cap_shist = nh;
-    }
-  }
   return hipSuccess;
 }
 
@@ -1638,40 +1473,19 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int end_bit = kWideChunkShift + cb;
   // U2 - L2 lies within a few micro-units of 2 tol (fmt6 rounds both ends): d = U2 - L2 - dbase
   const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
-  if ((e = hipMemsetAsync(ws->info, 0, 4 * sizeof(int32_t), s))) return e;
+  if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(1024, (nq + 255) / 256)), dim3(256), 0, s,
                      d_qoff, nq, ws->fq);
   // the bad-frame check (a key or a window outside what the cache and the int32 windows hold)
   hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
                      ws->info);
-  // one sort by (chunk, key, L2, U2 - L2): per segment in LDS (wide_seg_*), else hipCUB's
-  const bool seg_sort = !ws->radix_sort && nch <= kSegSortMaxChunks && ws->shist;
+  // one sort by (chunk, key, L2, U2 - L2)
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, (const int32_t*)nullptr,
+                     dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
-  int32_t info[4] = {0, 0, 0, 0};
-  if (seg_sort) {
-    const int32_t S = seg_slices(nch);
-    const int64_t nh = nch * (kWideSegs + 1) * S + 1;
-    hipLaunchKernelGGL(wide_seg_count_kernel, dim3((unsigned)nch, (unsigned)S), dim3(512), 0, s, boxes, d_qoff, nq, dbase,
-                       ws->ka, ws->shist, ws->info);
-    size_t sb = ws->stmp_bytes;
-    if ((e = hipcub::DeviceScan::ExclusiveSum(ws->stmp, sb, ws->shist, ws->soff, (int)nh, s))) return e;
-    hipLaunchKernelGGL(wide_seg_scatter_kernel, dim3((unsigned)nch, (unsigned)S), dim3(512), 0, s, d_qoff, nq, ws->ka,
-                       ws->soff, ws->va);
-    hipLaunchKernelGGL(wide_seg_sort_kernel, dim3((unsigned)std::min<int64_t>(nch * kWideSegs, 1024)), dim3(kSegSortThreads),
-                       0, s, d_qoff, nq, nch, S, ws->ka, ws->soff, ws->va, ws->kb, ws->vb, ws->info);
-    if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
-  }
-  if (!seg_sort || (info[3] && !info[1])) {  // (a segment too large for LDS: the whole sort again)
-    if (seg_sort) {
-      if ((e = hipMemsetAsync(ws->info, 0, 4 * sizeof(int32_t), s))) return e;
-      hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr,
-                         (int32_t*)nullptr, ws->info);
-    }
-    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf,
-                       (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
-    if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
-    if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
-  }
+  if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
+  int32_t info[3] = {0, 0, 0};
+  if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
   if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
   const int32_t* order = ws->vb;
   ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase

@@ -8,8 +8,7 @@ placed inside every gap and on both ends of it, with q2 at several sub-micro off
 exact frame count back as match_count), and all clips also share one key, where the groups batch
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
 (src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
-(TFP_WIDE_POINTS) and in the key-major form with score rows (TFP_WIDE_GROUPS); and with the frames
-ordered by hipCUB's radix sort (TFP_WIDE_RADIX) instead of the per-segment sort in LDS.
+(TFP_WIDE_POINTS) and in the key-major form with score rows (TFP_WIDE_GROUPS).
 """
 import math
 import os
@@ -110,8 +109,7 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     got = {}
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
-                      ("radix", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_RADIX": "1"})):
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(len(kinds)):
@@ -125,7 +123,6 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     assert got["clusters"] == expect, tol
     assert got["points"] == expect, tol
     assert got["key-major"] == expect, tol
-    assert got["radix"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
@@ -170,8 +167,7 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     assert sum(e is not None for e in expect) > nq // 2
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
-                      ("radix", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_RADIX": "1"})):
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(nclips):
@@ -180,58 +176,6 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
             res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol, low, high))
             got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
             assert got == expect, (form, tol, [i for i in range(nq) if got[i] != expect[i]][:5])
-            assert list(fcs) == list(np.diff(qoff))
-        finally:
-            eng.close()
-
-
-@pytest.mark.parametrize("case", ["sizes", "at_cap", "over_cap"])
-def test_sweep_segment_sort_sizes(oracle, tfp_lib, case):
-    """The sweep's frame order from per-(chunk, key) segment sorts in LDS (tfp_scan.hip wide_seg_*):
-    segments of 1, 2, 3, 63-65, 255-257 frames in one chunk ("sizes"), one segment of exactly
-    kSegSortCap = 4096 frames ("at_cap") and one of 4097 (the radix sort takes the batch,
-    "over_cap"). max2 windows repeat (equal sort keys: the frame order breaks the tie). Results ==
-    the oracle, and == the radix sort's (TFP_WIDE_RADIX)."""
-    rng = np.random.default_rng({"sizes": 1, "at_cap": 2, "over_cap": 3}[case])
-    tol = 0.01
-    nclips, rows = 24, 160
-    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
-    keys = rng.integers(20, 40, nclips * rows)
-    m1 = (keys * 1_000_000 + rng.integers(0, 900_000, nclips * rows)).astype(np.int32)
-    m2 = rng.integers(10_000_000, 10_400_000, nclips * rows).astype(np.int32)
-    clip = np.repeat(np.arange(nclips), rows).astype(np.int32)
-    q2pool = rng.integers(10_000_000, 10_400_000, 97) / 1e6  # few distinct windows: many equal keys
-    if case == "sizes":
-        seg = [1, 2, 3, 63, 64, 65, 255, 256, 257]
-        per_key = [(20 + i, n) for i, n in enumerate(seg)]
-        nq = 40
-    else:
-        per_key = [(30, 4096 + (case == "over_cap"))]
-        nq = 32
-    f1 = np.concatenate([np.full(n, k + 0.25) for k, n in per_key])
-    f2 = rng.choice(q2pool, len(f1))
-    order = rng.permutation(len(f1))  # spread each key's frames over the chunk's queries
-    f1, f2 = f1[order], f2[order]
-    cuts = np.sort(rng.choice(np.arange(1, len(f1)), nq - 1, replace=False))
-    qoff = np.concatenate([[0], cuts, [len(f1)]]).astype(np.int64)
-    frames = np.zeros(len(f1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
-                                         ("q1", "<f8"), ("q2", "<f8")]))
-    frames["q1"], frames["q2"] = f1, f2
-    expect = []
-    for i in range(nq):
-        s = slice(qoff[i], qoff[i + 1])
-        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, f1[s], f2[s], 2, tol, -1, -1)
-        expect.append((uuids[w], mc) if found else None)
-    assert sum(e is not None for e in expect) > nq // 2
-    for form, env in (("segments", {"TFP_WIDE_MIN_TOL": "0"}), ("radix", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_RADIX": "1"})):
-        eng = _engine_with(tfp_lib, env)
-        try:
-            for c in range(nclips):
-                sel = clip == c
-                eng.index_add(uuids[c], m1[sel], m2[sel])
-            res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol))
-            got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
-            assert got == expect, (form, case, [i for i in range(nq) if got[i] != expect[i]][:5])
             assert list(fcs) == list(np.diff(qoff))
         finally:
             eng.close()
