@@ -6,7 +6,9 @@
  * tfp_search_pcm_batch call, wall time in ms -> out_ms[i]; found[i] = the result's found flag.
  * The queries are first copied (untimed) into one tfp_host_alloc buffer, as the shim reads its
  * WAV files into one: the engine then reads each query's samples where they lie. */
-#define _POSIX_C_SOURCE 199309L
+#define _GNU_SOURCE
+#include <pthread.h>
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -72,5 +74,74 @@ int tfp_latency_stream(tfp_stream* st, const int16_t* pcm, int32_t nchannels, in
   for (c = 0; c < nchannels; c++) *found_last += res[c].found;
   tfp_host_free(res);
   tfp_host_free(blk);
+  return rc;
+}
+
+/* Searches per second from nthreads concurrent callers, as the module's channel threads make them
+ * (application_handler.c:66, :180): each thread runs reps batch-1 tfp_search_pcm_batch calls, thread
+ * t's r-th on query (t * 7 + r) % nqueries, every query in its own tfp_host_alloc buffer (the shim's
+ * per-call WAV read). Wall time from the threads' common start to the last return -> *seconds;
+ * found per call -> found[t * reps + r] (may be NULL). */
+typedef struct {
+  tfp_engine* eng;
+  int16_t** q;
+  int64_t n;
+  int32_t nq, sr, t, reps;
+  const tfp_search_params* p;
+  int32_t* found;
+  pthread_barrier_t* go;
+  int rc;
+} lat_thread;
+
+static void* lat_thread_main(void* v) {
+  lat_thread* a = (lat_thread*)v;
+  int32_t r;
+  pthread_barrier_wait(a->go);
+  for (r = 0; r < a->reps && a->rc == TFP_OK; r++) {
+    const int64_t off[2] = {0, a->n};
+    tfp_result res;
+    a->rc = tfp_search_pcm_batch(a->eng, a->q[(a->t * 7 + r) % a->nq], off, 1, a->sr, a->p, &res);
+    if (a->found) a->found[(int64_t)a->t * a->reps + r] = res.found;
+  }
+  return NULL;
+}
+
+int tfp_latency_threads(tfp_engine* eng, const int16_t* pcm, int64_t n, int32_t nqueries, int32_t sample_rate,
+                        const tfp_search_params* params, int32_t nthreads, int32_t reps, double* seconds,
+                        int32_t* found) {
+  pthread_t* th;
+  lat_thread* args;
+  int16_t** q;
+  pthread_barrier_t go;
+  int32_t i;
+  int rc = TFP_OK;
+  double t0;
+  if (!eng || !pcm || n <= 0 || nqueries <= 0 || nthreads <= 0 || reps < 0 || !params || !seconds) return TFP_E_ARG;
+  q = (int16_t**)calloc((size_t)nqueries, sizeof *q);
+  th = (pthread_t*)calloc((size_t)nthreads, sizeof *th);
+  args = (lat_thread*)calloc((size_t)nthreads, sizeof *args);
+  for (i = 0; i < nqueries && rc == TFP_OK; i++) {
+    rc = tfp_host_alloc(sizeof(int16_t) * (size_t)n, (void**)&q[i]);
+    if (rc == TFP_OK) memcpy(q[i], pcm + (int64_t)i * n, sizeof(int16_t) * (size_t)n);
+  }
+  if (rc == TFP_OK) {
+    pthread_barrier_init(&go, NULL, (unsigned)nthreads + 1);
+    for (i = 0; i < nthreads; i++) {
+      lat_thread a = {eng, q, n, nqueries, sample_rate, i, reps, params, found, &go, TFP_OK};
+      args[i] = a;
+      pthread_create(&th[i], NULL, lat_thread_main, &args[i]);
+    }
+    t0 = now_ms();
+    pthread_barrier_wait(&go);
+    for (i = 0; i < nthreads; i++) pthread_join(th[i], NULL);
+    *seconds = (now_ms() - t0) * 1e-3;
+    pthread_barrier_destroy(&go);
+    for (i = 0; i < nthreads; i++)
+      if (args[i].rc != TFP_OK) rc = args[i].rc;
+  }
+  for (i = 0; i < nqueries; i++) tfp_host_free(q[i]);
+  free(q);
+  free(th);
+  free(args);
   return rc;
 }

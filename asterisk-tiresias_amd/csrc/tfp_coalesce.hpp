@@ -1,0 +1,134 @@
+// tfp_coalesce.hpp — one search launch for many concurrent callers (engines and device groups).
+//
+// The reference runs one fp_search_fingerprint_info per channel thread (application_handler.c:180)
+// on one shared handle (fp_handler.c:1161-1169). Each call is a batch-1 search: ~30 us of mostly
+// fixed cost (launches, a stream sync), while the batch vote does 4,096 queries in 0.36 ms. So
+// concurrent callers are combined: a caller queues its request; if no batch is running it becomes
+// the leader, takes every queued request that can share its search (same sample format, rate and
+// parameters: the same SQL, fp_handler.c:287-374) up to kMaxQueries queries, runs them as one
+// batch, hands every caller its own results and wakes them. Requests that arrive while a batch
+// runs form the next batch, led by one of their callers. No timer: a lone caller runs at once,
+// and the batches grow with the load. Per-call results are unchanged: a query's result depends
+// only on its own frames and the index ("an internal queue/batcher ... as long as
+// per-call results are unchanged").
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <mutex>
+#include <vector>
+
+#include "../../include/tiresias_fp.h"
+
+namespace tfp {
+
+// One caller's search: its queries as (host pointer, samples), and where its results go.
+struct SearchReq {
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> lens;
+  bool f32 = false;
+  int32_t sr = 0;
+  tfp_search_params P{};
+  tfp_result* out = nullptr;
+  int rc = TFP_OK;
+  bool done = false;
+};
+
+// Two requests give the same SQL per query frame: tolerance < 0 is the default 0.001
+// (fp_handler.c:252-256), compared bitwise otherwise (NaN stays its own class).
+inline bool same_search(const SearchReq& a, const SearchReq& b) {
+  if (a.f32 != b.f32 || a.sr != b.sr || a.P.coefs != b.P.coefs || a.P.freq_ignore_low != b.P.freq_ignore_low ||
+      a.P.freq_ignore_high != b.P.freq_ignore_high)
+    return false;
+  const double ta = a.P.tolerance < 0 ? TFP_DEFAULT_TOLERANCE : a.P.tolerance;
+  const double tb = b.P.tolerance < 0 ? TFP_DEFAULT_TOLERANCE : b.P.tolerance;
+  return memcmp(&ta, &tb, sizeof ta) == 0;
+}
+
+class Coalescer {
+ public:
+  static constexpr int32_t kMaxQueries = 512;   // per combined batch
+  static constexpr int32_t kMaxCallQueries = 16;  // larger calls run on their own
+
+  // Runs *r, alone or with other callers' requests, through exec(std::vector<SearchReq*>&), which
+  // sets every request's rc and results. Returns r->rc.
+  template <class Exec>
+  int submit(SearchReq* r, Exec&& exec) {
+    std::unique_lock<std::mutex> lk(m_);
+    calls_++;
+    q_.push_back(r);
+    while (!r->done) {
+      if (busy_) {
+        cv_.wait(lk);
+        continue;
+      }
+      busy_ = true;
+      std::vector<SearchReq*> batch;
+      take(&batch);
+      lk.unlock();
+      exec(batch);
+      lk.lock();
+      for (SearchReq* b : batch) b->done = true;
+      batches_++;
+      busy_ = false;
+      cv_.notify_all();
+    }
+    return r->rc;
+  }
+
+  void stats(int64_t* calls, int64_t* batches) {
+    std::lock_guard<std::mutex> lk(m_);
+    if (calls) *calls = calls_;
+    if (batches) *batches = batches_;
+  }
+
+ private:
+  // FIFO: the oldest request and every later one that shares its search, up to kMaxQueries
+  void take(std::vector<SearchReq*>* batch) {
+    SearchReq* first = q_.front();
+    size_t n = 0;
+    std::vector<SearchReq*> rest;
+    for (SearchReq* r : q_) {
+      if (same_search(*first, *r) && (batch->empty() || n + r->lens.size() <= (size_t)kMaxQueries)) {
+        batch->push_back(r);
+        n += r->lens.size();
+      } else {
+        rest.push_back(r);
+      }
+    }
+    q_.swap(rest);
+  }
+
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::vector<SearchReq*> q_;
+  bool busy_ = false;
+  int64_t calls_ = 0, batches_ = 0;
+};
+
+// A batch's queries end to end, and each request's results back from the combined array.
+struct Combined {
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> lens;
+  std::vector<tfp_result> res;
+  explicit Combined(const std::vector<SearchReq*>& batch) {
+    for (const SearchReq* b : batch) {
+      ptrs.insert(ptrs.end(), b->ptrs.begin(), b->ptrs.end());
+      lens.insert(lens.end(), b->lens.begin(), b->lens.end());
+    }
+    res.resize(std::max<size_t>(lens.size(), 1));
+  }
+  void scatter(const std::vector<SearchReq*>& batch, int rc) {
+    size_t at = 0;
+    for (SearchReq* b : batch) {
+      b->rc = rc;
+      if (rc == TFP_OK) memcpy(b->out, res.data() + at, sizeof(tfp_result) * b->lens.size());
+      at += b->lens.size();
+    }
+  }
+};
+
+}  // namespace tfp

@@ -21,7 +21,9 @@
 #include <vector>
 
 #include "../../include/tiresias_fp.h"
+#include "tfp_coalesce.hpp"
 #include "tfp_index.hpp"
+#include "tfp_internal.hpp"
 #include "tfp_kernels.hpp"
 #include "tfp_math.hpp"
 #include "tfp_synth.hpp"
@@ -196,6 +198,8 @@ struct tfp_engine {
   int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
+  Coalescer coal;          // concurrent small host-sample searches share one batch (tfp_coalesce.hpp)
+  bool coalesce = true;    // TFP_COALESCE=0: every call runs alone (A/B)
   ~tfp_engine() {
     if (qoff_ev) (void)hipEventDestroy(qoff_ev);
   }
@@ -301,40 +305,96 @@ const char* engine_host_ptr(tfp_engine* e, const void* p, size_t n) {
   return slot.second + (reinterpret_cast<uintptr_t>(p) - base);
 }
 
-// Fingerprint host samples (int16 PCM, or with f32 the fp32 values aubio_source produced);
-// leaves micro/db on the device in e->micro / e->db.
+// Fingerprint host samples (int16 PCM, or with f32 the fp32 values aubio_source produced):
+// clip c is the lens[c] samples at ptrs[c] (the clips may lie anywhere: a coalesced batch gathers
+// the queries of several callers); leaves micro/db on the device in e->micro / e->db.
 // exact_q: the frame values (e->db) equal glibc's 10*log10|c| bit for bit (LogFix lookups); a
 // coefs = 1 search needs only their truncation, which is exact either way.
-int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nclips, int32_t sr,
+int fingerprint_host(tfp_engine* e, const void* const* ptrs, const int64_t* lens, bool f32, int32_t nclips, int32_t sr,
                      int64_t* nframes_out, std::vector<int64_t>* foff_out, bool exact_q = true) {
   const size_t ss = f32 ? sizeof(float) : sizeof(int16_t);
-  const char* src = static_cast<const char*>(pcm);
   const DspTables* T;
   bool fx = false;
   int rc = ensure_tables(e, sr, &T, &fx);
   if (rc) return rc;
-  std::vector<int64_t> soff, foff;
-  std::vector<int32_t> toff, tclip;
+  std::vector<int64_t> foff(nclips + 1, 0);
+  std::vector<int32_t> toff(nclips + 1, 0), tclip;
   // small batches at 8 kHz: 4-frame wave tiles (more waves, fewer passes per wave)
   bool small = false;
   if (fx && !f32) {
     int64_t nf16 = 0;
-    for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(offsets[c + 1] - offsets[c]) + 15) / 16;
+    for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(lens[c]) + 15) / 16;
     small = nf16 <= 256;
   }
   const int tile_frames = fp_tile_frames(e->fpcfg, fx, f32, small);
-  layout(offsets, nclips, soff, foff, toff, &tclip, tile_frames);
-  const int64_t ns = soff[nclips], nf = foff[nclips];
+  for (int32_t c = 0; c < nclips; c++) {
+    const int64_t nfc = tfp_frame_count(lens[c]);
+    foff[c + 1] = foff[c] + nfc;
+    toff[c + 1] = toff[c] + (int32_t)((nfc + tile_frames - 1) / tile_frames);
+  }
+  tclip.assign(std::max<int32_t>(toff[nclips], 1), 0);
+  for (int32_t c = 0; c < nclips; c++)
+    for (int32_t t = toff[c]; t < toff[c + 1]; t++) tclip[t] = c;
+  const int64_t nf = foff[nclips];
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (nf + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (nf + 1)));
+  // Where the samples come from:
+  //  - in place: every clip lies in a tfp_host_alloc buffer (the shim's WAV reads): the kernel reads
+  //    them through their device mapping, clip c at sample offset sbeg[c] from the lowest address;
+  //  - else packed (sbeg = prefix sums): into the pinned staging (small calls) or the device buffer.
+  // Throughput batches that are one contiguous buffer keep the DMA copy into HBM.
+  bool contiguous = true;
+  int64_t ns = 0;
+  for (int32_t c = 0; c < nclips; c++) {
+    ns += lens[c];
+    if (c + 1 < nclips && static_cast<const char*>(ptrs[c]) + ss * lens[c] != ptrs[c + 1]) contiguous = false;
+  }
+  std::vector<int64_t> sbeg(nclips + 1, 0), send(nclips + 1, 0);
+  const char* base_dev = nullptr;
+  bool in_place = ns > 0 && (small || !contiguous);
+  if (in_place) {
+    std::vector<const char*> dv(nclips, nullptr);
+    for (int32_t c = 0; c < nclips && in_place; c++) {
+      if (!lens[c]) continue;
+      dv[c] = engine_host_ptr(e, ptrs[c], ss * lens[c]);
+      in_place = dv[c] != nullptr;
+      if (in_place && (!base_dev || dv[c] < base_dev)) base_dev = dv[c];
+    }
+    for (int32_t c = 0; c < nclips && in_place; c++) {
+      const int64_t d = lens[c] ? (int64_t)(dv[c] - base_dev) : 0;
+      in_place = d % (int64_t)ss == 0;
+      sbeg[c] = d / (int64_t)ss;
+      send[c] = sbeg[c] + lens[c];
+    }
+  }
+  if (!in_place) {
+    for (int32_t c = 0; c < nclips; c++) {
+      sbeg[c + 1] = sbeg[c] + lens[c];
+      send[c] = sbeg[c + 1];
+    }
+  }
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t b_pcm = al(ss * ns), b_so = al(sizeof(int64_t) * soff.size()),
+  const size_t b_pcm = in_place ? 0 : al(ss * ns), b_sb = al(sizeof(int64_t) * nclips),
                b_fo = al(sizeof(int64_t) * foff.size()), b_to = al(sizeof(int32_t) * toff.size()),
                b_tc = al(sizeof(int32_t) * tclip.size());
-  const size_t total = b_pcm + b_so + b_fo + b_to + b_tc;
+  const size_t lay = 2 * b_sb + b_fo + b_to + b_tc, total = b_pcm + lay;
+  auto pack_layout = [&](char* h) {
+    memcpy(h, sbeg.data(), sizeof(int64_t) * nclips);
+    memcpy(h + b_sb, send.data(), sizeof(int64_t) * nclips);
+    memcpy(h + 2 * b_sb, foff.data(), sizeof(int64_t) * foff.size());
+    memcpy(h + 2 * b_sb + b_fo, toff.data(), sizeof(int32_t) * toff.size());
+    memcpy(h + 2 * b_sb + b_fo + b_to, tclip.data(), sizeof(int32_t) * tclip.size());
+  };
+  auto pack_samples = [&](char* h) {
+    if (contiguous) {
+      if (ns) memcpy(h, ptrs[0], ss * ns);
+      return;
+    }
+    for (int32_t c = 0; c < nclips; c++)
+      if (lens[c]) memcpy(h + ss * sbeg[c], ptrs[c], ss * lens[c]);
+  };
   const void* d_pcm;
-  const int64_t *d_soff, *d_foff;
-  const int32_t *d_toff, *d_tclip;
+  const char* lay_d;
   if (total <= ((size_t)8 << 20)) {
     // small call: pack every array into pinned staging, one H2D copy. The 4-frame-tile calls
     // (a query, batch-1 latency) skip the copy: the kernel reads the mapped, coherent staging in
@@ -342,7 +402,7 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
     // Every caller waits for e->stream before it returns and then clears stage_pending, so the
     // staging buffer is free here; after an error return the stream is drained first.
     if (e->stage_pending) HIPCHK(e, hipStreamSynchronize(e->stream));
-    const bool zero_copy = small;
+    const bool zero_copy = small || in_place;
     char* h;
     if (zero_copy) {
       HIPCHK(e, e->zstage.reserve(total, hipHostMallocMapped | hipHostMallocCoherent));
@@ -356,23 +416,18 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
       HIPCHK(e, e->dstage.reserve(total));
       h = e->hstage.as<char>();
     }
-    // samples already in a tfp_host_alloc buffer: read in place (no copy into the staging)
-    const char* in_place = zero_copy && ns ? engine_host_ptr(e, src + ss * offsets[0], ss * ns) : nullptr;
-    if (ns && !in_place) memcpy(h, src + ss * offsets[0], ss * ns);
-    memcpy(h + b_pcm, soff.data(), sizeof(int64_t) * soff.size());
-    memcpy(h + b_pcm + b_so, foff.data(), sizeof(int64_t) * foff.size());
-    memcpy(h + b_pcm + b_so + b_fo, toff.data(), sizeof(int32_t) * toff.size());
-    memcpy(h + b_pcm + b_so + b_fo + b_to, tclip.data(), sizeof(int32_t) * tclip.size());
+    if (!in_place) pack_samples(h);
+    pack_layout(h + b_pcm);
     if (!zero_copy) HIPCHK(e, hipMemcpyAsync(e->dstage.p, h, total, hipMemcpyHostToDevice, e->stream));
     e->stage_pending = true;
     char* d = zero_copy ? e->zstage_dev : e->dstage.as<char>();
-    d_pcm = in_place ? in_place : d;
-    const char* lay_d = d + b_pcm;  // the layout arrays' device address
+    d_pcm = in_place ? base_dev : d;
+    lay_d = d + b_pcm;  // the layout arrays' device address
     if (zero_copy) {
       // The tile layout is read first and in a dependent chain (tile -> clip -> its bounds -> the
-      // PCM address): keep it in device memory. It depends only on the query lengths, so it is
-      // uploaded only when it changes (from the pinned staging; the PCM stays in place).
-      const size_t lay = total - b_pcm;
+      // PCM address): keep it in device memory. It depends only on the query lengths (and, in
+      // place, the buffers' relative positions), so it is uploaded only when it changes (from the
+      // pinned staging; the PCM stays in place).
       if (e->zlayout_host.size() != lay || memcmp(e->zlayout_host.data(), h + b_pcm, lay) != 0) {
         HIPCHK(e, e->zlayout.reserve(lay));
         HIPCHK(e, hipMemcpyAsync(e->zlayout.p, h + b_pcm, lay, hipMemcpyHostToDevice, e->stream));
@@ -380,33 +435,54 @@ int fingerprint_host(tfp_engine* e, const void* pcm, bool f32, const int64_t* of
       }
       lay_d = e->zlayout.as<char>();
     }
-    d_soff = reinterpret_cast<const int64_t*>(lay_d);
-    d_foff = reinterpret_cast<const int64_t*>(lay_d + b_so);
-    d_toff = reinterpret_cast<const int32_t*>(lay_d + b_so + b_fo);
-    d_tclip = reinterpret_cast<const int32_t*>(lay_d + b_so + b_fo + b_to);
   } else {
-    if ((rc = upload(e, e->pcm, src + ss * offsets[0], ss * ns))) return rc;
-    if ((rc = upload(e, e->soff, soff.data(), sizeof(int64_t) * soff.size()))) return rc;
-    if ((rc = upload(e, e->foff, foff.data(), sizeof(int64_t) * foff.size()))) return rc;
-    if ((rc = upload(e, e->toff, toff.data(), sizeof(int32_t) * toff.size()))) return rc;
-    if ((rc = upload(e, e->tclip, tclip.data(), sizeof(int32_t) * tclip.size()))) return rc;
-    d_pcm = e->pcm.p;
-    d_soff = e->soff.as<int64_t>();
-    d_foff = e->foff.as<int64_t>();
-    d_toff = e->toff.as<int32_t>();
-    d_tclip = e->tclip.as<int32_t>();
+    std::vector<char> hl(lay);
+    pack_layout(hl.data());
+    if ((rc = upload(e, e->soff, hl.data(), lay))) return rc;
+    if (in_place) {
+      d_pcm = base_dev;
+    } else {
+      HIPCHK(e, e->pcm.reserve(ss * ns));
+      if (contiguous) {
+        if ((rc = upload(e, e->pcm, ptrs[0], ss * ns))) return rc;
+      } else {
+        for (int32_t c = 0; c < nclips; c++)
+          if (lens[c])
+            HIPCHK(e, hipMemcpyAsync(e->pcm.as<char>() + ss * sbeg[c], ptrs[c], ss * lens[c], hipMemcpyHostToDevice,
+                                     e->stream));
+      }
+      d_pcm = e->pcm.p;
+    }
+    lay_d = e->soff.as<char>();
+    HIPCHK(e, hipStreamSynchronize(e->stream));  // (hl is released on return)
   }
+  const int64_t* d_sbeg = reinterpret_cast<const int64_t*>(lay_d);
+  const int64_t* d_send = reinterpret_cast<const int64_t*>(lay_d + b_sb);
+  const int64_t* d_foff = reinterpret_cast<const int64_t*>(lay_d + 2 * b_sb);
+  const int32_t* d_toff = reinterpret_cast<const int32_t*>(lay_d + 2 * b_sb + b_fo);
+  const int32_t* d_tclip = reinterpret_cast<const int32_t*>(lay_d + 2 * b_sb + b_fo + b_to);
   if (f32)
-    HIPCHK(e, launch_fingerprint_f32(e->fpcfg, T, static_cast<const float*>(d_pcm), d_soff, d_soff + 1, d_foff, d_toff, d_tclip,
+    HIPCHK(e, launch_fingerprint_f32(e->fpcfg, T, static_cast<const float*>(d_pcm), d_sbeg, d_send, d_foff, d_toff, d_tclip,
                                      toff[nclips], e->micro.as<int32_t>(), e->db.as<double>(), e->stream,
                                      exact_q ? e->logfix : LogFix{}));
   else
-    HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_soff, d_soff + 1, d_foff,
+    HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, tile_frames, static_cast<const int16_t*>(d_pcm), d_sbeg, d_send, d_foff,
                                  d_toff, d_tclip, toff[nclips], nf, e->micro.as<int32_t>(), e->db.as<double>(),
-                                 e->stream, exact_q ? e->logfix : LogFix{}, nclips == 1 && soff[0] == 0 ? soff[1] : -1));
+                                 e->stream, exact_q ? e->logfix : LogFix{}, nclips == 1 && sbeg[0] == 0 ? send[0] : -1));
   *nframes_out = nf;
   if (foff_out) *foff_out = foff;
   return TFP_OK;
+}
+
+// The clips of one buffer at sample offsets offsets[0..nclips] as (pointer, length) lists.
+void split_offsets(const void* pcm, size_t ss, const int64_t* offsets, int32_t nclips, std::vector<const void*>* ptrs,
+                   std::vector<int64_t>* lens) {
+  ptrs->resize(nclips);
+  lens->resize(nclips);
+  for (int32_t c = 0; c < nclips; c++) {
+    (*ptrs)[c] = static_cast<const char*>(pcm) + ss * offsets[c];
+    (*lens)[c] = offsets[c + 1] - offsets[c];
+  }
 }
 
 int copy_frames_out(tfp_engine* e, int64_t nf, const std::vector<int64_t>& foff, tfp_frame* out) {
@@ -1114,6 +1190,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   e->wide.points_only = getenv("TFP_WIDE_POINTS") != nullptr;
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
+  if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;
@@ -1175,7 +1252,10 @@ int fingerprint_batch_impl(tfp_engine* e, const void* pcm, bool f32, const int64
   HIPCHK(e, hipSetDevice(e->device));
   int64_t nf;
   std::vector<int64_t> foff;
-  int rc = fingerprint_host(e, pcm, f32, offsets, nclips, sr, &nf, &foff);
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> lens;
+  split_offsets(pcm, f32 ? sizeof(float) : sizeof(int16_t), offsets, nclips, &ptrs, &lens);
+  int rc = fingerprint_host(e, ptrs.data(), lens.data(), f32, nclips, sr, &nf, &foff);
   if (rc) return rc;
   return copy_frames_out(e, nf, foff, out);
 }
@@ -1256,17 +1336,19 @@ int tfp_index_add(tfp_engine* e, const char* uuid, const int32_t* m1, const int3
   if (e->by_uuid.count(uuid)) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuid);
   int rc = stage_reserve(e, nframes);
   if (rc) return rc;
-  if ((rc = new_clip(e, uuid, nframes, e->n_staged, &id))) return rc;
+  // the rows go in past the staged ones first; the clip is registered only once they are there
+  // (a failed copy leaves the index as it was)
+  const int64_t o = e->n_staged;
   if (nframes) {
-    std::vector<int32_t> cl(nframes, id);
-    const int64_t o = e->n_staged;
+    std::vector<int32_t> cl(nframes, (int32_t)e->clips.size());
     HIPCHK(e, hipMemcpyAsync(e->st_m1.as<int32_t>() + o, m1, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->st_m2.as<int32_t>() + o, m2, sizeof(int32_t) * nframes, hipMemcpyHostToDevice, e->stream));
     HIPCHK(e, hipMemcpyAsync(e->st_clip.as<int32_t>() + o, cl.data(), sizeof(int32_t) * nframes, hipMemcpyHostToDevice,
                              e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->n_staged += nframes;
   }
+  if ((rc = new_clip(e, uuid, nframes, o, &id))) return rc;
+  e->n_staged += nframes;
   if (clip_id) *clip_id = id;
   return TFP_OK;
 }
@@ -1292,20 +1374,18 @@ int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids
     return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
+  std::unordered_map<std::string, int> seen;
   for (int32_t c = 0; c < nclips; c++) {
     if (!uuids[c] || !*uuids[c] || strlen(uuids[c]) >= 64) return fail(e, TFP_E_ARG, "bad uuid %d", c);
-    if (e->by_uuid.count(uuids[c])) return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
+    if (frame_offsets[c + 1] < frame_offsets[c]) return fail(e, TFP_E_ARG, "frame_offsets not monotone at %d", c);
+    if (e->by_uuid.count(uuids[c]) || !seen.emplace(uuids[c], c).second)
+      return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
   }
   const int64_t nf = frame_offsets[nclips] - frame_offsets[0];
   int rc = stage_reserve(e, nf);
   if (rc) return rc;
   const int32_t clip0 = (int32_t)e->clips.size();
-  for (int32_t c = 0; c < nclips; c++) {
-    int32_t id;
-    if ((rc = new_clip(e, uuids[c], frame_offsets[c + 1] - frame_offsets[c],
-                       e->n_staged + frame_offsets[c] - frame_offsets[0], &id)))
-      return rc;
-  }
+  // rows first, clips registered once they are staged (a failure leaves the index as it was)
   if (nf) {
     std::vector<int64_t> fo(frame_offsets, frame_offsets + nclips + 1);
     for (auto& v : fo) v -= frame_offsets[0];
@@ -1318,9 +1398,31 @@ int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids
                        e->st_clip.as<int32_t>() + o);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(s));
-    e->n_staged += nf;
   }
+  for (int32_t c = 0; c < nclips; c++) {
+    int32_t id;
+    if ((rc = new_clip(e, uuids[c], frame_offsets[c + 1] - frame_offsets[c],
+                       e->n_staged + frame_offsets[c] - frame_offsets[0], &id)))
+      return rc;  // (cannot fail: checked above)
+  }
+  e->n_staged += nf;
   return TFP_OK;
+}
+
+// TFP_TEST_FAIL_ADD_BATCH=n (tests): the n-th tfp_index_add_batch call of the process since the
+// variable took its value fails as a device error would, before it changes anything.
+static bool injected_add_batch_failure() {
+  static std::mutex mu;
+  static std::string val;
+  static int64_t calls = 0;
+  const char* v = getenv("TFP_TEST_FAIL_ADD_BATCH");
+  std::lock_guard<std::mutex> lk(mu);
+  if (!v) return false;
+  if (val != v) {
+    val = v;
+    calls = 0;
+  }
+  return ++calls == atoll(v);
 }
 
 int tfp_index_add_batch(tfp_engine* e, int32_t nclips, const char* const* uuids, const int64_t* frame_offsets,
@@ -1337,17 +1439,17 @@ int tfp_index_add_batch(tfp_engine* e, int32_t nclips, const char* const* uuids,
     if (e->by_uuid.count(uuids[c]) || !seen.emplace(uuids[c], c).second)
       return fail(e, TFP_E_EXISTS, "uuid %s already indexed", uuids[c]);
   }
+  if (injected_add_batch_failure()) return fail(e, TFP_E_HIP, "tfp_index_add_batch: injected device failure");
   int rc = stage_reserve(e, nf);
   if (rc) return rc;
-  std::vector<int32_t> cl(nf);
+  // All-or-nothing: the rows go in past the staged ones, and the clips are registered only once
+  // every copy has succeeded.
   const int32_t clip0 = (int32_t)e->clips.size();
-  for (int32_t c = 0; c < nclips; c++) {
-    int32_t id;
-    const int64_t b = frame_offsets[c] - frame_offsets[0], n = frame_offsets[c + 1] - frame_offsets[c];
-    if ((rc = new_clip(e, uuids[c], n, e->n_staged + b, &id))) return rc;
-    std::fill(cl.begin() + b, cl.begin() + b + n, clip0 + c);
-  }
   if (nf) {
+    std::vector<int32_t> cl(nf);
+    for (int32_t c = 0; c < nclips; c++)
+      std::fill(cl.begin() + (frame_offsets[c] - frame_offsets[0]), cl.begin() + (frame_offsets[c + 1] - frame_offsets[0]),
+                clip0 + c);
     const int64_t o = e->n_staged;
     const int32_t* s1 = m1 + frame_offsets[0];
     const int32_t* s2 = m2 + frame_offsets[0];
@@ -1356,8 +1458,13 @@ int tfp_index_add_batch(tfp_engine* e, int32_t nclips, const char* const* uuids,
     HIPCHK(e, hipMemcpyAsync(e->st_clip.as<int32_t>() + o, cl.data(), sizeof(int32_t) * nf, hipMemcpyHostToDevice,
                              e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->n_staged += nf;
   }
+  for (int32_t c = 0; c < nclips; c++) {
+    int32_t id;
+    const int64_t b = frame_offsets[c] - frame_offsets[0], n = frame_offsets[c + 1] - frame_offsets[c];
+    if ((rc = new_clip(e, uuids[c], n, e->n_staged + b, &id))) return rc;  // (cannot fail: checked above)
+  }
+  e->n_staged += nf;
   return TFP_OK;
 }
 
@@ -1484,24 +1591,65 @@ int tfp_search(tfp_engine* e, const tfp_frame* frames, int32_t nframes, const tf
 }
 
 namespace {
-int search_samples_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
-                        const tfp_search_params* P, tfp_result* out) {
-  if (!e || !offsets || nq < 0 || !out) return TFP_E_ARG;
+// One search over host samples, the queries given as (pointer, samples); no coalescing.
+int search_gather_impl(tfp_engine* e, const void* const* ptrs, const int64_t* lens, int32_t nq, bool f32, int32_t sr,
+                       const tfp_search_params* P, tfp_result* out) {
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
-  std::vector<int64_t> soff, foff;
-  std::vector<int32_t> toff;
-  layout(offsets, nq, soff, foff, toff);
+  std::vector<int64_t> foff(nq + 1, 0);
+  for (int32_t i = 0; i < nq; i++) foff[i + 1] = foff[i] + tfp_frame_count(lens[i]);
   std::vector<unsigned long long> keys(nq, 0ull);
   if (valid_params(P) && nq && foff[nq] > 0) {
     int64_t nf;
-    int rc = fingerprint_host(e, pcm, f32, offsets, nq, sr, &nf, nullptr, P->coefs == 2);
+    int rc = fingerprint_host(e, ptrs, lens, f32, nq, sr, &nf, nullptr, P->coefs == 2);
     if (rc) return rc;
     if ((rc = search_core(e, foff.data(), nq, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
     e->stage_pending = false;  // search_core waited for e->stream (keys on the host)
   }
   fill_results(e, keys, foff.data(), nq, out);
   return TFP_OK;
+}
+
+// Argument checks, then the call alone (large batches, TFP_COALESCE=0) or through the coalescer.
+int search_gather_entry(tfp_engine* e, const void* const* ptrs, const int64_t* lens, int32_t nq, bool f32, int32_t sr,
+                        const tfp_search_params* P, tfp_result* out) {
+  if (!e || nq < 0 || !out || (nq && (!ptrs || !lens))) return TFP_E_ARG;
+  for (int32_t i = 0; i < nq; i++)
+    if (lens[i] < 0 || (lens[i] && !ptrs[i])) return fail(e, TFP_E_ARG, "bad query %d", i);
+  if (!e->coalesce || nq == 0 || nq > Coalescer::kMaxCallQueries)
+    return search_gather_impl(e, ptrs, lens, nq, f32, sr, P, out);
+  SearchReq r;
+  r.ptrs.assign(ptrs, ptrs + nq);
+  r.lens.assign(lens, lens + nq);
+  r.f32 = f32;
+  r.sr = sr;
+  if (P) r.P = *P;
+  else r.P.coefs = 0;  // (invalid: NULL results, fp_handler.c:247-250)
+  r.out = out;
+  return e->coal.submit(&r, [e](std::vector<SearchReq*>& batch) {
+    if (batch.size() == 1) {
+      SearchReq* b = batch[0];
+      b->rc = search_gather_impl(e, b->ptrs.data(), b->lens.data(), (int32_t)b->lens.size(), b->f32, b->sr, &b->P, b->out);
+      return;
+    }
+    Combined c(batch);
+    const SearchReq* b0 = batch[0];
+    const int rc = search_gather_impl(e, c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P,
+                                      c.res.data());
+    c.scatter(batch, rc);
+  });
+}
+
+int search_samples_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
+                        const tfp_search_params* P, tfp_result* out) {
+  if (!e || !offsets || nq < 0 || !out) return TFP_E_ARG;
+  for (int32_t i = 0; i < nq; i++)
+    if (offsets[i + 1] < offsets[i]) return fail(e, TFP_E_ARG, "offsets not monotone");
+  if (!pcm && nq && offsets[nq] > offsets[0]) return fail(e, TFP_E_ARG, "samples are NULL");
+  std::vector<const void*> ptrs;
+  std::vector<int64_t> lens;
+  split_offsets(pcm, f32 ? sizeof(float) : sizeof(int16_t), offsets, nq, &ptrs, &lens);
+  return search_gather_entry(e, ptrs.data(), lens.data(), nq, f32, sr, P, out);
 }
 }  // namespace
 
@@ -1513,6 +1661,24 @@ int tfp_search_pcm_batch(tfp_engine* e, const int16_t* pcm, const int64_t* offse
 int tfp_search_f32_batch(tfp_engine* e, const float* x, const int64_t* offsets, int32_t nq, int32_t sr,
                          const tfp_search_params* P, tfp_result* out) {
   return search_samples_impl(e, x, true, offsets, nq, sr, P, out);
+}
+
+int tfp_search_pcm_gather(tfp_engine* e, const int16_t* const* pcms, const int64_t* nsamples, int32_t nq, int32_t sr,
+                          const tfp_search_params* P, tfp_result* out) {
+  return search_gather_entry(e, reinterpret_cast<const void* const*>(pcms), nsamples, nq, false, sr, P, out);
+}
+
+int tfp_search_coalesce_stats(tfp_engine* e, int64_t* calls, int64_t* batches) {
+  if (!e) return TFP_E_ARG;
+  e->coal.stats(calls, batches);
+  return TFP_OK;
+}
+
+// (internal, tfp_internal.hpp) the device group's per-shard search: already coalesced by the group
+int tfp_internal_search_gather(tfp_engine* e, const void* const* ptrs, const int64_t* lens, int32_t nq, bool f32,
+                               int32_t sr, const tfp_search_params* P, tfp_result* out) {
+  if (!e || nq < 0 || !out || (nq && (!ptrs || !lens))) return TFP_E_ARG;
+  return search_gather_impl(e, ptrs, lens, nq, f32, sr, P, out);
 }
 
 int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, const tfp_search_params* P,

@@ -19,6 +19,7 @@
 // few tens of microseconds of GPU time), each shard matching them against its clips.
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -34,6 +35,8 @@
 #include <vector>
 
 #include "../../include/tiresias_fp.h"
+#include "tfp_coalesce.hpp"
+#include "tfp_internal.hpp"
 
 namespace {
 
@@ -166,6 +169,8 @@ struct tfp_group {
   std::vector<int32_t> member_rank;                    // member -> its global rank (valid when !ranks_dirty)
   bool ranks_dirty = true;
   std::vector<ShardBufs> bufs;
+  tfp::Coalescer coal;   // concurrent channel searches share one batch per shard (tfp_coalesce.hpp)
+  bool coalesce = true;  // TFP_COALESCE=0: every call alone
   ~tfp_group() {
     delete pool;
     for (size_t s = 0; s < bufs.size(); s++) {
@@ -408,6 +413,7 @@ int tfp_group_create(const int32_t* devices, int32_t n, tfp_group** out) {
   g->rows.assign(n, 0);
   g->bufs.resize(n);
   g->pool = new ShardPool(n);
+  if (const char* v = getenv("TFP_COALESCE")) g->coalesce = atoi(v) != 0;
   *out = g;
   return TFP_OK;
 }
@@ -472,7 +478,10 @@ int tfp_group_index_add(tfp_group* g, const char* uuid, const int32_t* m1, const
   int32_t id = -1;
   const int rc = tfp_index_add(g->eng[s], uuid, m1, m2, nframes, &id);
   if (rc) return shard_fail(g, rc, s);
-  if (id != (int32_t)g->id2member[s].size()) return gfail(g, TFP_E_HIP, "shard %d clip id %d out of step", s, id);
+  if (id != (int32_t)g->id2member[s].size()) {  // (never expected) undo the engine's add: no clip without a member
+    (void)tfp_index_remove(g->eng[s], uuid);
+    return gfail(g, TFP_E_HIP, "shard %d clip id %d out of step", s, id);
+  }
   g->rows[s] += nframes;
   return add_members(g, s, 1, &uuid);
 }
@@ -515,14 +524,22 @@ int tfp_group_index_add_batch(tfp_group* g, int32_t nclips, const char* const* u
     return rcs[s] = tfp_index_add_batch(g->eng[s], (int32_t)uu[s].size(), uu[s].data(), fo[s].data(), a1[s].data(),
                                         a2[s].data());
   });
-  // (arguments were checked above, so a shard fails only on a device error; the shards that
-  // succeeded keep their clips, as the engine's own add_batch is all-or-nothing per call)
+  // All-or-nothing over the group, as each engine's add_batch is per call: when a shard failed (a
+  // device error: the arguments were checked above), the shards that succeeded drop the batch's
+  // clips again, so no clip stays on a GPU without a member (or a catalog row: the shim deletes
+  // the batch's rows on failure).
+  if (rc) {
+    for (int s = 0; s < n; s++)
+      if (!uu[s].empty() && rcs[s] == TFP_OK)
+        for (const char* u : uu[s]) (void)tfp_index_remove(g->eng[s], u);
+    return rc;
+  }
   for (int s = 0; s < n; s++)
-    if (!uu[s].empty() && rcs[s] == TFP_OK) {
+    if (!uu[s].empty()) {
       add_members(g, s, (int32_t)uu[s].size(), uu[s].data());
       g->rows[s] += fo[s].back();
     }
-  return rc;
+  return TFP_OK;
 }
 
 int tfp_group_index_remove(tfp_group* g, const char* uuid) {
@@ -547,13 +564,31 @@ int tfp_group_index_remove(tfp_group* g, const char* uuid) {
 int tfp_group_index_clear(tfp_group* g) {
   if (!g) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(g->mu);
-  const int rc = run_all(g, [&](int s) { return tfp_index_clear(g->eng[s]); });
-  g->where.clear();
-  g->members.clear();
-  g->by_uuid.clear();
-  for (auto& v : g->id2member) v.clear();
-  std::fill(g->rows.begin(), g->rows.end(), 0);
+  const int n = (int)g->eng.size();
+  std::vector<int> rcs(n, TFP_OK);
+  const int rc = run_all(g, [&](int s) { return rcs[s] = tfp_index_clear(g->eng[s]); });
   g->ranks_dirty = true;
+  if (rc == TFP_OK) {
+    g->where.clear();
+    g->members.clear();
+    g->by_uuid.clear();
+    for (auto& v : g->id2member) v.clear();
+    std::fill(g->rows.begin(), g->rows.end(), 0);
+    return TFP_OK;
+  }
+  // a shard whose clear failed keeps its clips, and the group keeps them as its members
+  for (int s = 0; s < n; s++) {
+    if (rcs[s] != TFP_OK) continue;
+    for (int32_t mi : g->id2member[s]) {
+      if (mi < 0) continue;
+      Member& m = g->members[mi];
+      erase_live(g, mi);
+      g->where.erase(m.uuid);
+      m.uuid.clear();
+    }
+    g->id2member[s].clear();
+    g->rows[s] = 0;
+  }
   return rc;
 }
 
@@ -608,26 +643,73 @@ int tfp_group_search_batch(tfp_group* g, const tfp_frame* frames, const int64_t*
 }
 
 namespace {
-int group_search_samples(tfp_group* g, const void* x, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
-                         const tfp_search_params* P, tfp_result* out) {
-  if (!g || !offsets || nq < 0 || !out) return TFP_E_ARG;
+// One search over host samples on every shard (each fingerprints the whole batch: no exchange on
+// the latency path), combined by the integer max of the keys.
+int group_search_direct(tfp_group* g, const void* const* ptrs, const int64_t* lens, int32_t nq, bool f32, int32_t sr,
+                        const tfp_search_params* P, tfp_result* out) {
   std::lock_guard<std::recursive_mutex> lk(g->mu);
   int rc = refresh_ranks(g);
   if (rc) return rc;
   const int n = (int)g->eng.size();
-  // throughput batches of equal-length int16 queries: query-sharded (fingerprint once, exchange)
-  bool equal = nq > 0;
-  for (int32_t i = 0; i < nq && equal; i++) equal = offsets[i + 1] - offsets[i] == offsets[1] - offsets[0];
-  if (!f32 && n > 1 && equal && nq >= 64 * n && offsets[1] > offsets[0] && valid_params(P) && x)
-    return search_sharded(g, (const int16_t*)x, offsets, nq, sr, P, out);
   std::vector<std::vector<tfp_result>> res(n, std::vector<tfp_result>(std::max(nq, 1)));
-  rc = run_all(g, [&](int s) {
-    return f32 ? tfp_search_f32_batch(g->eng[s], (const float*)x, offsets, nq, sr, P, res[s].data())
-               : tfp_search_pcm_batch(g->eng[s], (const int16_t*)x, offsets, nq, sr, P, res[s].data());
-  });
+  rc = run_all(g, [&](int s) { return tfp_internal_search_gather(g->eng[s], ptrs, lens, nq, f32, sr, P, res[s].data()); });
   if (rc) return rc;
   combine(g, res, nq, out);
   return TFP_OK;
+}
+
+int group_search_gather(tfp_group* g, const void* const* ptrs, const int64_t* lens, int32_t nq, bool f32, int32_t sr,
+                        const tfp_search_params* P, tfp_result* out) {
+  if (!g || nq < 0 || !out || (nq && (!ptrs || !lens))) return TFP_E_ARG;
+  for (int32_t i = 0; i < nq; i++)
+    if (lens[i] < 0 || (lens[i] && !ptrs[i])) return gfail(g, TFP_E_ARG, "bad query %d", i);
+  if (!g->coalesce || nq == 0 || nq > tfp::Coalescer::kMaxCallQueries)
+    return group_search_direct(g, ptrs, lens, nq, f32, sr, P, out);
+  tfp::SearchReq r;
+  r.ptrs.assign(ptrs, ptrs + nq);
+  r.lens.assign(lens, lens + nq);
+  r.f32 = f32;
+  r.sr = sr;
+  if (P) r.P = *P;
+  else r.P.coefs = 0;  // (invalid: NULL results, fp_handler.c:247-250)
+  r.out = out;
+  return g->coal.submit(&r, [g](std::vector<tfp::SearchReq*>& batch) {
+    if (batch.size() == 1) {
+      tfp::SearchReq* b = batch[0];
+      b->rc = group_search_direct(g, b->ptrs.data(), b->lens.data(), (int32_t)b->lens.size(), b->f32, b->sr, &b->P, b->out);
+      return;
+    }
+    tfp::Combined c(batch);
+    const tfp::SearchReq* b0 = batch[0];
+    const int rc = group_search_direct(g, c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P,
+                                       c.res.data());
+    c.scatter(batch, rc);
+  });
+}
+
+int group_search_samples(tfp_group* g, const void* x, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,
+                         const tfp_search_params* P, tfp_result* out) {
+  if (!g || !offsets || nq < 0 || !out) return TFP_E_ARG;
+  for (int32_t i = 0; i < nq; i++)
+    if (offsets[i + 1] < offsets[i]) return gfail(g, TFP_E_ARG, "offsets not monotone");
+  if (!x && nq && offsets[nq] > offsets[0]) return gfail(g, TFP_E_ARG, "samples are NULL");
+  const int n = (int)g->eng.size();
+  // throughput batches of equal-length int16 queries: query-sharded (fingerprint once, exchange)
+  bool equal = nq > 0;
+  for (int32_t i = 0; i < nq && equal; i++) equal = offsets[i + 1] - offsets[i] == offsets[1] - offsets[0];
+  if (!f32 && n > 1 && equal && nq >= 64 * n && offsets[1] > offsets[0] && valid_params(P)) {
+    std::lock_guard<std::recursive_mutex> lk(g->mu);
+    const int rc = refresh_ranks(g);
+    return rc ? rc : search_sharded(g, (const int16_t*)x, offsets, nq, sr, P, out);
+  }
+  const size_t ss = f32 ? sizeof(float) : sizeof(int16_t);
+  std::vector<const void*> ptrs(nq);
+  std::vector<int64_t> lens(nq);
+  for (int32_t i = 0; i < nq; i++) {
+    ptrs[i] = static_cast<const char*>(x) + ss * offsets[i];
+    lens[i] = offsets[i + 1] - offsets[i];
+  }
+  return group_search_gather(g, ptrs.data(), lens.data(), nq, f32, sr, P, out);
 }
 }  // namespace
 
@@ -639,6 +721,17 @@ int tfp_group_search_pcm_batch(tfp_group* g, const int16_t* pcm, const int64_t* 
 int tfp_group_search_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nq, int32_t sr,
                                const tfp_search_params* P, tfp_result* out) {
   return group_search_samples(g, x, true, offsets, nq, sr, P, out);
+}
+
+int tfp_group_search_pcm_gather(tfp_group* g, const int16_t* const* pcms, const int64_t* nsamples, int32_t nq,
+                                int32_t sr, const tfp_search_params* P, tfp_result* out) {
+  return group_search_gather(g, reinterpret_cast<const void* const*>(pcms), nsamples, nq, false, sr, P, out);
+}
+
+int tfp_group_search_coalesce_stats(tfp_group* g, int64_t* calls, int64_t* batches) {
+  if (!g) return TFP_E_ARG;
+  g->coal.stats(calls, batches);
+  return TFP_OK;
 }
 
 int tfp_group_stream_create(tfp_group* g, int32_t nch, int32_t sr, int64_t W, tfp_group_stream** out) {

@@ -80,6 +80,8 @@ _SIGS = {
     "tfp_search": (C.c_int, [P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_search_pcm_gather": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_search_coalesce_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "tfp_search_device": (C.c_int, [P, P, P, C.POINTER(SearchParams), P, P]),
     "tfp_search_q_device": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P, P]),
     "tfp_index_uuid_of_key": (C.c_int, [P, C.c_int32, C.c_char_p, C.c_int32]),
@@ -107,6 +109,8 @@ _SIGS = {
     "tfp_group_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_group_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_group_search_f32_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_group_search_pcm_gather": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),
+    "tfp_group_search_coalesce_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "tfp_group_stream_create": (C.c_int, [P, C.c_int32, C.c_int32, C.c_int64, C.POINTER(P)]),
     "tfp_group_stream_destroy": (None, [P]),
     "tfp_group_stream_reset": (C.c_int, [P, C.c_int32]),

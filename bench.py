@@ -532,6 +532,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             kdev.item()
         lat.append(max_over_ranks(time.perf_counter() - t0) * 1e3)
     lat_py = list(lat)
+    threads = None
     harness = "python (ctypes) loop, max over ranks + 8-byte all_reduce" if dist else "python (ctypes) loop"
     if not dist:
         # the same calls from C (asterisk-tiresias_amd/bench/tfp_latency.c), as the Asterisk shim's
@@ -549,6 +550,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             lat = out_ms.tolist()
             harness = ("C loop over tfp_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries held in a "
                        "tfp_host_alloc buffer (read in place, as the shim's WAV reads)" % (n_it, len(hq)))
+        threads = concurrent_searches(eng, T, clat, hq, qn, p)
     # SURVEY §8(d)'s match roofline: one pass over the index per batch (12 B per row) plus the
     # query frames (16 B each) against HBM; the vote path reads only the used keys' boxes, so a
     # fraction above 1 means the batch costs less than one index pass
@@ -566,6 +568,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "latency_p50_ms": float(np.percentile(lat, 50)), "latency_p99_ms": float(np.percentile(lat, 99)),
             "latency_samples": len(lat), "latency_harness": harness,
             "latency_p50_ms_python": float(np.percentile(lat_py, 50)),
+            "concurrent_callers": threads if not dist else None,
             "roofline": {"bound": "hbm", "definition": "one index pass per batch: 12 B x index rows + 16 B x query frames "
                                                        "(SURVEY 8d)", "bytes": match_bytes,
                          "achieved": match_bytes / (batch_ms / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -579,38 +582,79 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     return res
 
 
+def concurrent_searches(eng, T, clat, hq, qn, p, counts=(1, 8, 64), calls_per_count=1536):
+    """Batch-1 searches per second from 1, 8 and 64 concurrent calling threads, timed from C
+    (bench/tfp_latency.c: tfp_latency_threads), as the module's channel threads call
+    fp_search_fingerprint_info (application_handler.c:66, :180) on one shared engine
+    (fp_handler.c:1161-1169). Concurrent calls are coalesced into shared batches
+    (csrc/tfp_coalesce.hpp): `batches` counts the GPU batches the calls ran as."""
+    out = []
+    nq = len(hq)
+    for nth in counts:
+        reps = max(1, calls_per_count // nth)
+        sec = ctypes.c_double(0)
+        found = np.zeros(nth * reps, np.int32)
+        c0, b0 = ctypes.c_int64(0), ctypes.c_int64(0)
+        T.lib().tfp_search_coalesce_stats(eng.handle, ctypes.byref(c0), ctypes.byref(b0))
+        rc = clat.tfp_latency_threads(eng.handle, ctypes.c_void_p(hq.ctypes.data), ctypes.c_int64(qn), ctypes.c_int32(nq),
+                                      ctypes.c_int32(8000), ctypes.byref(p), ctypes.c_int32(nth), ctypes.c_int32(reps),
+                                      ctypes.byref(sec), ctypes.c_void_p(found.ctypes.data))
+        c1, b1 = ctypes.c_int64(0), ctypes.c_int64(0)
+        T.lib().tfp_search_coalesce_stats(eng.handle, ctypes.byref(c1), ctypes.byref(b1))
+        if rc != 0:
+            out.append({"threads": nth, "error": rc})
+            continue
+        out.append({"threads": nth, "calls": nth * reps, "seconds": sec.value, "searches_per_s": nth * reps / sec.value,
+                    "mean_call_ms": sec.value * 1e3 * nth / (nth * reps) if nth else None,
+                    "gpu_batches": b1.value - b0.value, "found": int(found.sum())})
+        log(f"concurrent callers {nth}: {out[-1]['searches_per_s']:.0f} searches/s in {out[-1]['gpu_batches']} batches")
+    return {"harness": "C threads over tfp_search_pcm_batch, one query each call, each query in its own tfp_host_alloc "
+                       "buffer (bench/tfp_latency.c tfp_latency_threads)", "legs": out}
+
+
 def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
     """Enrol-then-first-search at configs[2]'s 100k-clip DB: one new 30 s clip's rows added
-    (tfp_index_add, as the shim's fp_craete_audio_list_info does) and a batch-1 search of an excerpt
-    of it right after, timed together: the first search pays the index update. The engine merges
-    the new rows into the sorted index (tfp_index.hip); a second engine built with TFP_INDEX_FULL=1
-    (a full re-sort per update, the round-2 behaviour) gives the figure to compare against. The
-    reference's INSERT updates its B-tree per row (fp_handler.c:559-571, :745-753)."""
+    (tfp_index_add, as the shim's fp_craete_audio_list_info does) and a batch-1 search of a 5 s
+    excerpt of it right after, timed together: the first search pays the index update. The reference's
+    INSERT updates its B-tree per row (fp_handler.c:559-571, :745-753). A second engine built with
+    TFP_INDEX_FULL=1 (a full re-sort per update, the round-2 behaviour) gives the figure to compare
+    against.
+
+    The new clips are full-scale white noise with uuids above every DB uuid, each above the one before
+    (tests/test_gpu_configs.py: noise_clips, new_clip_uuid): their max1 values (16.19-16.25 dB) lie in
+    key 16's box at tolerance 0.45 ([15.55, 16.45] dB), which holds no DB row (those are >= 16.6 dB),
+    so a coefs = 1, tolerance 0.45 search of an excerpt can only be won by a new clip, and the newest
+    has the greatest uuid: `new_clip_won` counts the searches that saw the clip just added. (A DB-like
+    clip would not do: under the reference's trunc rule an excerpt of the synthetic audio is rarely won
+    by its own clip, at any tolerance.)"""
     n_db, qn = 8000 * 30, 8000 * 5
     nf_db = (n_db + HOP - 1) // HOP
-    ids = list(range(args.db_clips, args.db_clips + n_add))
-    pcm = T.synth_pcm(SEED_DB, ids, n_db)
+    pcm = np.random.default_rng(0x7153C3).integers(-32768, 32768, (n_add, n_db)).astype(np.int16)
     fr = eng.fingerprint_batch(pcm.reshape(-1), np.arange(n_add + 1) * n_db)
+    uuids = ["ffffffff-ffff-4fff-bfff-%012x" % i for i in range(n_add)]
+    pq = T.params(1, 0.45)
+    for i in range(min(2, n_add)):  # untimed: this tolerance's key bitsets, built once per index version
+        eng.search_pcm_batch(np.ascontiguousarray(pcm[i, :qn]), [0, qn], pq)
 
     def run(e, tag):
         out = []
         hits[tag] = 0
-        for i, g in enumerate(ids):
+        for i, u in enumerate(uuids):
             q = np.ascontiguousarray(pcm[i, 256 * 100: 256 * 100 + qn])
             t0 = time.perf_counter()
-            e.index_add(uuid_of(g), fr["m1"][i * nf_db:(i + 1) * nf_db], fr["m2"][i * nf_db:(i + 1) * nf_db])
-            res, _ = e.search_pcm_batch(q, [0, qn], p)
+            e.index_add(u, fr["m1"][i * nf_db:(i + 1) * nf_db], fr["m2"][i * nf_db:(i + 1) * nf_db])
+            res, _ = e.search_pcm_batch(q, [0, qn], pq)
             out.append((time.perf_counter() - t0) * 1e3)
-            hits[tag] += res[0] is not None and res[0]["audio_uuid"] == uuid_of(g)
-        for g in ids:
-            e.index_remove(uuid_of(g))
+            hits[tag] += res[0] is not None and res[0]["audio_uuid"] == u
+        for u in uuids:
+            e.index_remove(u)
         e.index_commit()
-        log(f"enrol-then-search ({tag}): p50 {np.percentile(out, 50):.2f} ms")
+        log(f"enrol-then-search ({tag}): p50 {np.percentile(out, 50):.2f} ms, new clip won {hits[tag]}/{len(uuids)}")
         return out
 
     hits = {}
     fb0, mg0 = eng.index_build_stats()
-    inc = run(eng, "merge")
+    inc = run(eng, "engine")
     fb1, mg1 = eng.index_build_stats()
     os.environ["TFP_INDEX_FULL"] = "1"
     try:
@@ -619,14 +663,17 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
         del os.environ["TFP_INDEX_FULL"]
     enroll(full_eng, torch, dev, sh, list(range(args.db_clips)))
     full_eng.index_commit()
+    full_eng.search_pcm_batch(np.ascontiguousarray(pcm[0, :qn]), [0, qn], pq)
     full = run(full_eng, "full re-sort")
     full_eng.close()
     torch.cuda.empty_cache()
-    return {"workload": f"{n_add} x (tfp_index_add of one 30 s clip + batch-1 search of a 5 s excerpt of it) on the "
-                        f"{args.db_clips}-clip DB, host PCM",
+    return {"workload": f"{n_add} x (tfp_index_add of one 30 s clip + batch-1 search of a 5 s excerpt of it, coefs 1, "
+                        f"tolerance 0.45) on the {args.db_clips}-clip DB, host PCM",
             "p50_ms": float(np.percentile(inc, 50)), "max_ms": float(np.max(inc)), "samples_ms": inc,
             "index_updates": {"merges": mg1 - mg0, "full_sorts": fb1 - fb0},
-            "new_clip_won": hits,  # (at the dialplan's tolerance 0.001 a 5 s excerpt often finds nothing: the trunc rule)
+            "new_clip_won": hits,
+            "new_clips": "full-scale white noise, uuids above the DB's: only a new clip's rows lie in the query's "
+                         "key box (see enrol_latency)",
             "full_resort": {"p50_ms": float(np.percentile(full, 50)), "max_ms": float(np.max(full)), "samples_ms": full,
                             "how": "same calls on an engine with TFP_INDEX_FULL=1 (every update a full radix sort of all "
                                    "staged rows + a uuid sort), the round-2 behaviour"}}

@@ -201,6 +201,21 @@ int tfp_search_pcm_batch(tfp_engine* eng, const int16_t* pcm, const int64_t* off
 /* The same over fp32 hop values (tfp_wav_decode_f32). */
 int tfp_search_f32_batch(tfp_engine* eng, const float* x, const int64_t* offsets, int32_t nqueries,
                          int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+/* Queries in separate buffers (new in round 4): query i is the nsamples[i] int16 samples at pcms[i].
+ * The results equal tfp_search_pcm_batch's over the same queries laid end to end. Samples inside
+ * tfp_host_alloc buffers are read in place wherever they lie (one per channel recording, say).
+ *
+ * Concurrent callers (new in round 4). The reference runs one fp_search_fingerprint_info per channel
+ * thread (application_handler.c:180) on one shared handle (fp_handler.c:1161-1169). Calls of
+ * tfp_search_pcm_batch, tfp_search_f32_batch and tfp_search_pcm_gather with at most 16 queries each
+ * are coalesced: a call made while another batch runs on the engine waits for it, then runs together
+ * with every other waiting call of the same sample format, rate and search parameters as one batch
+ * (<= 512 queries). A lone call runs at once. Each call gets exactly its own results.
+ * TFP_COALESCE=0 in the environment at engine creation turns this off. tfp_search_coalesce_stats:
+ * calls taken through the coalescer and the batches they ran as (either pointer may be NULL). */
+int tfp_search_pcm_gather(tfp_engine* eng, const int16_t* const* pcms, const int64_t* nsamples, int32_t nqueries,
+                          int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+int tfp_search_coalesce_stats(tfp_engine* eng, int64_t* calls, int64_t* batches);
 /* Device form for benchmarks / sharded search: per query a 64-bit key
  * (match_count << 32 | tiebreak key), 0 = NOTFOUND, written to d_keys[nqueries] (device).
  * The maximum key over shards is the global winner (RCCL allreduce MAX). */
@@ -271,6 +286,11 @@ int tfp_group_search_pcm_batch(tfp_group* g, const int16_t* pcm, const int64_t* 
                                int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
 int tfp_group_search_f32_batch(tfp_group* g, const float* x, const int64_t* offsets, int32_t nqueries,
                                int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+/* tfp_search_pcm_gather and the coalescing of concurrent calls (as for one engine) on a group: the
+ * channel threads' batch-1 searches through the shim run as shared batches on every GPU. */
+int tfp_group_search_pcm_gather(tfp_group* g, const int16_t* const* pcms, const int64_t* nsamples, int32_t nqueries,
+                                int32_t sample_rate, const tfp_search_params* params, tfp_result* out);
+int tfp_group_search_coalesce_stats(tfp_group* g, int64_t* calls, int64_t* batches);
 /* Live channels on a group: every engine keeps every channel's window and matches it against its
  * clips each tick; out[nchannels] = the combined results (as tfp_stream_push). */
 typedef struct tfp_group_stream tfp_group_stream;

@@ -452,6 +452,11 @@ static int frame_box(double q1v, double q2v, int coefs, double tole, int low, in
   return 1;
 }
 
+int tfo_frame_box(double q1v, double q2v, int coefs, double tole, int low, int high, int64_t* L1, int64_t* U1,
+                  int* has2, int64_t* L2, int64_t* U2) {
+  return frame_box(q1v, q2v, coefs, tole, low, high, L1, U1, has2, L2, U2);
+}
+
 int tfo_search(const int32_t* m1, const int32_t* m2, const int32_t* row_clip, int64_t nrows,
                const char* const* uuids, int32_t nclips, const double* q1, const double* q2,
                int32_t nq, int coefs, double tolerance, int low, int high, int32_t* winner,

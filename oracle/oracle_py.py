@@ -67,6 +67,8 @@ def lib():
                                               + [C.c_int32, C.c_int, C.c_double, C.c_int, C.c_int, C.c_void_p,
                                                  C.c_void_p, C.c_int])
         L.tfo_search_sorted_batch.restype = C.c_int
+        L.tfo_search_boxes_batch.argtypes = L.tfo_search_sorted_batch.argtypes + [C.c_int]
+        L.tfo_search_boxes_batch.restype = C.c_int
         L.tfo_fmt6.argtypes = [C.c_double]
         L.tfo_fmt6.restype = C.c_int64
         _lib = L
@@ -187,18 +189,26 @@ class SortedIndex:
             raise MemoryError("tfo_sort_rows")
         self.tiekey = np.ascontiguousarray(tiekey, np.int32)
 
-    def search_batch(self, q1, q2, qoff, coefs=1, tolerance=0.001, low=-1, high=-1, nthreads=8):
-        """-> (winner clip int32[nq] (-1 = NOTFOUND), match_count int32[nq])."""
+    def search_batch(self, q1, q2, qoff, coefs=1, tolerance=0.001, low=-1, high=-1, nthreads=8, method="scan",
+                     mode=0):
+        """-> (winner clip int32[nq] (-1 = NOTFOUND), match_count int32[nq]). method "scan": one row
+        scan per distinct frame clause (tfo_search_sorted_batch); "boxes": per distinct max1 box, max2
+        runs or per-clip merges (tfo_search_boxes_batch; mode 1/2 forces one form), for wide
+        coefs = 2 windows at configs[2] size."""
         q1 = np.ascontiguousarray(q1, np.float64)
         q2 = np.ascontiguousarray(q2, np.float64)
         qoff = np.ascontiguousarray(qoff, np.int64)
         nq = len(qoff) - 1
         w = np.zeros(nq, np.int32)
         mc = np.zeros(nq, np.int32)
-        lib().tfo_search_sorted_batch(self.m1.ctypes.data, self.m2.ctypes.data, self.clip.ctypes.data, len(self.m1),
-                                      self.tiekey.ctypes.data, len(self.tiekey), q1.ctypes.data, q2.ctypes.data,
-                                      qoff.ctypes.data, nq, coefs, float(tolerance), int(low), int(high),
-                                      w.ctypes.data, mc.ctypes.data, int(nthreads))
+        args = (self.m1.ctypes.data, self.m2.ctypes.data, self.clip.ctypes.data, len(self.m1), self.tiekey.ctypes.data,
+                len(self.tiekey), q1.ctypes.data, q2.ctypes.data, qoff.ctypes.data, nq, coefs, float(tolerance), int(low),
+                int(high), w.ctypes.data, mc.ctypes.data, int(nthreads))
+        if method == "boxes":
+            if lib().tfo_search_boxes_batch(*args, int(mode)) != 0:
+                raise MemoryError("tfo_search_boxes_batch")
+        else:
+            lib().tfo_search_sorted_batch(*args)
         return w, mc
 
 

@@ -88,6 +88,20 @@ int tfo_search_sorted_batch(const int32_t* m1s, const int32_t* m2s, const int32_
                             const int64_t* qoff, int32_t nq, int coefs, double tolerance, int low, int high,
                             int32_t* winner, int32_t* match_count, int nthreads);
 
+/* The same search, organised per distinct max1 box (oracle_boxes.c): for wide coefs = 2 windows at
+ * configs[2] size, where one row scan per frame box would read tens of millions of rows per frame.
+ * Same arguments and results as tfo_search_sorted_batch (rows sorted by max1); mode 0 picks the
+ * cheaper form per (query, box), 1 forces the max2-ordered runs, 2 the per-clip merges (tests). */
+int tfo_search_boxes_batch(const int32_t* m1s, const int32_t* m2s, const int32_t* row_clip, int64_t nrows,
+                           const int32_t* tiekey, int32_t nclips, const double* q1, const double* q2,
+                           const int64_t* qoff, int32_t nq, int coefs, double tolerance, int low, int high,
+                           int32_t* winner, int32_t* match_count, int nthreads, int mode);
+
+/* One query frame's WHERE clause (fp_handler.c:287-351): 0 = the frame runs no SQL; else [L1, U1]
+ * on max1 and, when *has2, [L2, U2] on max2, in micro-units. */
+int tfo_frame_box(double q1v, double q2v, int coefs, double tole, int low, int high, int64_t* L1, int64_t* U1,
+                  int* has2, int64_t* L2, int64_t* U2);
+
 /* printf("%f") micro-units of x, parsed from the printed string. */
 int64_t tfo_fmt6(double x);
 

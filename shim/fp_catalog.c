@@ -319,6 +319,12 @@ char* fp_generate_uuid(void)
 /* create_audio_list_info (fp_handler.c:479-530) */
 int fpc_create_audio_list_info(const char* context, const char* filename, const char* uuid)
 {
+	return fpc_create_audio_list_info_ex(context, filename, uuid, NULL, 0);
+}
+
+int fpc_create_audio_list_info_ex(const char* context, const char* filename, const char* uuid, char* existing,
+		size_t len)
+{
 	char* hash;
 	const char* name;
 	struct ast_json* j;
@@ -340,6 +346,10 @@ int fpc_create_audio_list_info(const char* context, const char* filename, const 
 	j = query_one("select * from audio_list where context = ? and hash = ?;", context, hash);
 	if(j != NULL) {
 		ast_log(LOG_VERBOSE, "The given file is already fingerprinted. context[%s], filename[%s]\n", context, filename);
+		if(existing != NULL && len > 0) {
+			const char* u = ast_json_string_get(ast_json_object_get(j, "uuid"));
+			snprintf(existing, len, "%s", u ? u : "");
+		}
 		ast_json_unref(j);
 		ret = 0;
 	}
@@ -530,8 +540,8 @@ bool fpc_load_fingerprints(fpc_rows* r)
 		if(r->nclips == 0 || strcmp(r->uuids[r->nclips - 1], u) != 0) {
 			if(r->nclips + 1 >= ccap) {
 				int32_t nc = ccap ? 2 * ccap : 1024;
-				char** nu = realloc(r->uuids, sizeof(char*) * (size_t)nc);
-				int64_t* no = nu ? realloc(r->frame_offsets, sizeof(int64_t) * ((size_t)nc + 1)) : NULL;
+				char** nu = ast_realloc(r->uuids, sizeof(char*) * (size_t)nc);
+				int64_t* no = nu ? ast_realloc(r->frame_offsets, sizeof(int64_t) * ((size_t)nc + 1)) : NULL;
 				if(nu) r->uuids = nu;
 				if(no) r->frame_offsets = no;
 				if(nu == NULL || no == NULL) {
@@ -546,8 +556,8 @@ bool fpc_load_fingerprints(fpc_rows* r)
 		}
 		if(n == cap) {
 			int64_t nc = cap ? 2 * cap : 1 << 16;
-			int32_t* a = realloc(r->m1, sizeof(int32_t) * (size_t)nc);
-			int32_t* b = a ? realloc(r->m2, sizeof(int32_t) * (size_t)nc) : NULL;
+			int32_t* a = ast_realloc(r->m1, sizeof(int32_t) * (size_t)nc);
+			int32_t* b = a ? ast_realloc(r->m2, sizeof(int32_t) * (size_t)nc) : NULL;
 			if(a) r->m1 = a;
 			if(b) r->m2 = b;
 			if(a == NULL || b == NULL) {

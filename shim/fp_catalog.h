@@ -43,6 +43,9 @@ void fpc_db_close(void);
 
 /* 1 created, 0 already enrolled (same context and file hash), < 0 error */
 int fpc_create_audio_list_info(const char* context, const char* filename, const char* uuid);
+/* The same; when the file is already enrolled (0), existing[len] receives that row's uuid. */
+int fpc_create_audio_list_info_ex(const char* context, const char* filename, const char* uuid, char* existing,
+		size_t len);
 struct ast_json* fpc_get_audio_list_info(const char* uuid); /* {uuid, name, context, hash} or NULL */
 bool fpc_delete_audio_list_info(const char* uuid);
 /* m1/m2: "%f" micro-units, INT32_MIN for NULL (TFP_NULL_MICRO) */

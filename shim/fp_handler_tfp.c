@@ -79,6 +79,11 @@ static bool create_group(void)
 	return tfp_group_create(dev, n, &g_tfp) == TFP_OK;
 }
 
+bool fp_get_search_stats(int64_t* calls, int64_t* batches)
+{
+	return g_tfp != NULL && tfp_group_search_coalesce_stats(g_tfp, calls, batches) == TFP_OK;
+}
+
 /* fp_init (fp_handler.c:68-90): the catalog (init_database + the backup's tables), the engine, and
  * the GPU index from the restored audio_fingerprint table in one tfp_group_index_add_batch. A failure
  * closes whatever was opened, without writing the backup. */
@@ -461,9 +466,9 @@ static bool group_add(enrol_group* g, int f, const char* filename, char* uuid, i
 	int rc;
 	if(g->n + 1 >= g->cap) {
 		int nc = g->cap ? 2 * g->cap : 64;
-		int* nf = realloc(g->file, sizeof(int) * (size_t)nc);
-		char** nu = nf ? realloc(g->uuid, sizeof(char*) * (size_t)nc) : NULL;
-		int64_t* no = nu ? realloc(g->off, sizeof(int64_t) * ((size_t)nc + 1)) : NULL;
+		int* nf = ast_realloc(g->file, sizeof(int) * (size_t)nc);
+		char** nu = nf ? ast_realloc(g->uuid, sizeof(char*) * (size_t)nc) : NULL;
+		int64_t* no = nu ? ast_realloc(g->off, sizeof(int64_t) * ((size_t)nc + 1)) : NULL;
 		if(nf) g->file = nf;
 		if(nu) g->uuid = nu;
 		if(no) g->off = no;
@@ -478,7 +483,7 @@ static bool group_add(enrol_group* g, int f, const char* filename, char* uuid, i
 		while(nc < at + ns + 1) {
 			nc *= 2;
 		}
-		nx = realloc(g->x, ss * (size_t)nc);
+		nx = ast_realloc(g->x, ss * (size_t)nc);
 		if(nx == NULL) {
 			return false;
 		}
@@ -501,10 +506,27 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 {
 	enrol_group groups[ENROL_GROUPS];
 	int i, k, enrolled = 0;
+	/* a file repeated within the list: its first copy's uuid (created in this call) and index;
+	 * the repeat reports the first copy's final result, known only after the flushes */
+	char** made = NULL;
+	int* dup_of = NULL;
+	bool* res = NULL;
 
 	if((context == NULL) || (filenames == NULL) || (count < 0)) {
 		ast_log(LOG_WARNING, "Wrong input parameter.\n");
 		return -1;
+	}
+	made = ast_calloc(count ? count : 1, sizeof(char*));
+	dup_of = ast_calloc(count ? count : 1, sizeof(int));
+	res = ast_calloc(count ? count : 1, sizeof(bool));
+	if(made == NULL || dup_of == NULL || res == NULL) {
+		ast_free(made);
+		ast_free(dup_of);
+		ast_free(res);
+		return -1;
+	}
+	for(i = 0; i < count; i++) {
+		dup_of[i] = -1;
 	}
 	memset(groups, 0, sizeof(groups));
 	for(i = 0; i < count; i++) {
@@ -516,9 +538,8 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 		bool f32 = false;
 		enrol_group* g = NULL;
 
-		if(ok) {
-			ok[i] = false;
-		}
+		char existing[64] = "";
+
 		if(f == NULL) {
 			continue;
 		}
@@ -526,7 +547,7 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 		if(uuid == NULL) {
 			continue;
 		}
-		ret = fpc_create_audio_list_info(context, f, uuid);
+		ret = fpc_create_audio_list_info_ex(context, f, uuid, existing, sizeof(existing));
 		if(ret < 0) {
 			ast_log(LOG_WARNING, "Could not create audio_list info. context[%s], filename[%s]\n", context, f);
 			ast_free(uuid);
@@ -536,10 +557,18 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 			ast_log(LOG_VERBOSE, "The given audio file is already exist in the list. context[%s], filename[%s]\n",
 					context, f);
 			ast_free(uuid);
-			if(ok) {
-				ok[i] = true;
+			res[i] = true;
+			for(k = 0; k < i; k++) {
+				if(made[k] != NULL && strcmp(made[k], existing) == 0) {
+					dup_of[i] = k;
+					break;
+				}
 			}
 			continue;
+		}
+		made[i] = ast_malloc(strlen(uuid) + 1);
+		if(made[i] != NULL) {
+			memcpy(made[i], uuid, strlen(uuid) + 1);
 		}
 		/* aubio_source at the native rate: int16 PCM, else the fp32 hop values (read_audio) */
 		if(tfp_wav_read(f, NULL, 0, &ns, &sr) != TFP_OK) {
@@ -563,7 +592,7 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 			}
 			if(k == ENROL_GROUPS) { /* many formats in one scan: flush them all */
 				for(k = 0; k < ENROL_GROUPS; k++) {
-					enrolled += group_flush(context, &groups[k], ok);
+					enrolled += group_flush(context, &groups[k], res);
 					group_free(&groups[k]);
 				}
 				k = 0;
@@ -579,7 +608,7 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 			}
 		}
 		if(g->n > 0 && g->off[g->n] + ns > ENROL_BATCH_SAMPLES) {
-			enrolled += group_flush(context, g, ok);
+			enrolled += group_flush(context, g, res);
 		}
 		if(group_add(g, i, f, uuid, ns) == false) {
 			ast_log(LOG_WARNING, "Could not read %s: %s\n", f, tfp_engine_last_error(NULL));
@@ -588,9 +617,21 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 		}
 	}
 	for(k = 0; k < ENROL_GROUPS; k++) {
-		enrolled += group_flush(context, &groups[k], ok);
+		enrolled += group_flush(context, &groups[k], res);
 		group_free(&groups[k]);
 	}
+	for(i = 0; i < count; i++) {
+		if(dup_of[i] >= 0) {
+			res[i] = res[dup_of[i]];
+		}
+		if(ok) {
+			ok[i] = res[i];
+		}
+		ast_free(made[i]);
+	}
+	ast_free(made);
+	ast_free(dup_of);
+	ast_free(res);
 	return enrolled;
 }
 

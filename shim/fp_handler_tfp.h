@@ -5,6 +5,7 @@
 #define FP_HANDLER_TFP_H
 
 #include <stdbool.h>
+#include <stdint.h>
 
 struct ast_json;
 
@@ -34,5 +35,10 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
  * every search on all of them), before fp_init — e.g. from a "devices" option of tiresias.conf:
  * "0-7", "0,2,5", or "" / NULL for every visible GPU (the default). */
 void fp_set_gpu_devices(const char* list);
+
+/* New: how the channel threads' fp_search_fingerprint_info calls ran. Concurrent calls are
+ * coalesced into shared GPU batches (tfp_group_search_pcm_batch, include/tiresias_fp.h): *calls
+ * searches went through the coalescer as *batches batches. false before fp_init. */
+bool fp_get_search_stats(int64_t* calls, int64_t* batches);
 
 #endif

@@ -6,5 +6,6 @@
 #define ast_malloc(n) malloc(n)
 #define ast_calloc(n, m) calloc((n), (m))
 #define ast_free(p) free(p)
+#define ast_realloc(p, n) realloc((p), (n))
 #define ast_strdup(s) strdup(s)
 #endif

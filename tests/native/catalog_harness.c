@@ -24,6 +24,10 @@ struct ast_json* fp_search_fingerprint_info(const char* c, const char* f, const 
 }
 bool fp_delete_audio_list_info(const char* uuid) { return fpc_delete_audio_list_info(uuid); }
 void fp_set_gpu_devices(const char* list) { (void)list; }
+bool fp_get_search_stats(int64_t* calls, int64_t* batches) {
+  (void)calls; (void)batches;
+  return false;
+}
 
 static void print_ints(const int32_t* v, int64_t n) {
   int64_t k;

@@ -6,12 +6,18 @@
  *   shim_driver BACKUP_DB CMD...   with CMD one of
  *     init | term | enroll CONTEXT FILE | enrolldir CONTEXT DIR | enrolldir1 CONTEXT DIR |
  *     delete UUID | search CONTEXT FILE COEFS TOL LOW HIGH | ctx NAME DIR | ctxdel NAME |
- *     lists | hash FILE | devices LIST
+ *     lists | hash FILE | devices LIST |
+ *     psearch NTHREADS REPS CONTEXT COEFS TOL LOW HIGH NFILES FILE...
+ * psearch plays the module's channel threads: NTHREADS threads (application_handler.c:66, one per
+ * call) each run REPS fp_search_fingerprint_info calls at once, thread t's r-th on file
+ * (t * 7 + r) % NFILES, and print every result, the wall time and the coalescer's counts.
  * enrolldir batches the scan through fp_create_audio_list_infos, enrolldir1 calls
  * fp_craete_audio_list_info per file as the reference does. Each command prints one JSON line. */
 #define _GNU_SOURCE
 #include <dirent.h>
 #include <inttypes.h>
+#include <pthread.h>
+#include <time.h>
 #include <stdarg.h>
 #include <stdbool.h>
 #include <stdio.h>
@@ -140,6 +146,78 @@ static void print_search(const char* file, struct ast_json* j) {
   ast_json_unref(j);
 }
 
+/* ---- psearch: concurrent channel threads ---- */
+typedef struct {
+  int found, fc, mc;
+  char uuid[64];
+} psres;
+typedef struct {
+  int t, reps, nfiles, coefs, low, high;
+  double tol;
+  const char* ctx;
+  char** files;
+  psres* out;  /* [reps] */
+  pthread_barrier_t* go;
+} psarg;
+
+static void* psearch_thread(void* p) {
+  psarg* a = p;
+  int r;
+  pthread_barrier_wait(a->go);
+  for (r = 0; r < a->reps; r++) {
+    struct ast_json* j = fp_search_fingerprint_info(a->ctx, a->files[(a->t * 7 + r) % a->nfiles], a->coefs, a->tol,
+                                                    a->low, a->high);
+    psres* o = &a->out[r];
+    memset(o, 0, sizeof *o);
+    if (j) {
+      o->found = 1;
+      o->fc = (int)ast_json_integer_get(ast_json_object_get(j, "frame_count"));
+      o->mc = (int)ast_json_integer_get(ast_json_object_get(j, "match_count"));
+      snprintf(o->uuid, sizeof o->uuid, "%s", ast_json_string_get(ast_json_object_get(j, "uuid")));
+      ast_json_unref(j);
+    }
+  }
+  return NULL;
+}
+
+static void psearch(int nth, int reps, const char* ctx, int coefs, double tol, int low, int high, int nfiles,
+                    char** files) {
+  pthread_t* th = calloc(nth, sizeof *th);
+  psarg* args = calloc(nth, sizeof *args);
+  psres* out = calloc((size_t)nth * reps, sizeof *out);
+  pthread_barrier_t go;
+  struct timespec t0, t1;
+  int64_t c0 = 0, b0 = 0, c1 = 0, b1 = 0;
+  int t, r;
+  pthread_barrier_init(&go, NULL, nth + 1);
+  fp_get_search_stats(&c0, &b0);
+  for (t = 0; t < nth; t++) {
+    psarg a = {t, reps, nfiles, coefs, low, high, tol, ctx, files, out + (size_t)t * reps, &go};
+    args[t] = a;
+    pthread_create(&th[t], NULL, psearch_thread, &args[t]);
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  pthread_barrier_wait(&go);
+  for (t = 0; t < nth; t++) pthread_join(th[t], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  fp_get_search_stats(&c1, &b1);
+  {
+    const double s = (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+    printf("{\"psearch\": %d, \"reps\": %d, \"seconds\": %.6f, \"per_s\": %.1f, \"calls\": %" PRId64
+           ", \"batches\": %" PRId64 ", \"results\": [", nth, reps, s, nth * reps / s, c1 - c0, b1 - b0);
+  }
+  for (t = 0; t < nth; t++)
+    for (r = 0; r < reps; r++) {
+      const psres* o = &out[(size_t)t * reps + r];
+      printf("%s[%d, %d, \"%s\", %d, %d]", t || r ? ", " : "", (t * 7 + r) % nfiles, o->found, o->uuid, o->mc, o->fc);
+    }
+  printf("]}\n");
+  pthread_barrier_destroy(&go);
+  free(th);
+  free(args);
+  free(out);
+}
+
 static int file_select(const struct dirent* e) { return strcmp(e->d_name, ".") && strcmp(e->d_name, ".."); }
 
 /* app_tiresias.c:365-424: the context's directory, alphasort; batched or file by file */
@@ -218,6 +296,12 @@ int main(int argc, char** argv) {
       printf("{\"hash\": \"%s\"}\n", h ? h : "");
       free(h);
       i += 1;
+    } else if (!strcmp(cmd, "psearch") && i + 7 < argc && i + 8 + atoi(argv[i + 7]) <= argc) {
+      const int nf = atoi(argv[i + 7]);
+      const char* ctx = strcmp(argv[i + 2], "NULL") ? argv[i + 2] : NULL;
+      psearch(atoi(argv[i]), atoi(argv[i + 1]), ctx, atoi(argv[i + 3]), atof(argv[i + 4]), atoi(argv[i + 5]),
+              atoi(argv[i + 6]), nf, argv + i + 8);
+      i += 8 + nf;
     } else if (!strcmp(cmd, "devices") && i < argc) {
       fp_set_gpu_devices(argv[i]);
       printf("{\"devices\": \"%s\"}\n", argv[i]);

@@ -267,9 +267,12 @@ def _oracle_q(oracle, qpcm):
 
 
 def _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, p, nthreads=ORACLE_THREADS):
+    """The device path's key per query (search_device on the queries' PCM) == the oracle's over the
+    same rows. coefs = 2 batches take the oracle's per-box form (oracle_boxes.c): at a wide tolerance
+    one row scan per frame clause would read tens of millions of rows per frame."""
     eng, idx, rank = c3db["eng"], c3db["idx"], c3db["rank"]
     w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], qoff, p.coefs, p.tolerance, p.freq_ignore_low, p.freq_ignore_high,
-                             nthreads=nthreads)
+                             nthreads=nthreads, method="boxes" if p.coefs == 2 else "scan")
     keys = torch.zeros(len(qpcm), dtype=torch.int64, device="cuda")
     stream = torch.cuda.current_stream().cuda_stream
     eng.search_device(eng.plan(np.arange(len(qpcm) + 1, dtype=np.int64) * qpcm.shape[1]), d_q.data_ptr(), p,
@@ -301,21 +304,26 @@ def test_configs2_full_db_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
         assert fc[0] == nfq
 
 
-@pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 64), (2, 0.01, -1, -1, 32), (2, 0.1, -1, -1, 16),
-                                                   (1, 0.45, -1, -1, 64), (1, 0.01, 100, 3400, 64),
-                                                   (2, 0.1, 100, 3400, 16), (1, 0.001, 50, 60, 64),
-                                                   (2, 0.01, 50, 60, 32)])
+@pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 128), (2, 0.01, -1, -1, 128), (2, 0.1, -1, -1, 128),
+                                                   (2, 0.45, -1, -1, 128), (1, 0.45, -1, -1, 64),
+                                                   (1, 0.01, 100, 3400, 64), (2, 0.1, 100, 3400, 64),
+                                                   (2, 0.45, 100, 3400, 128), (1, 0.001, 50, 60, 64),
+                                                   (2, 0.01, 50, 60, 64), (2, 0.45, 50, 60, 128)])
 def test_configs2_sweeps_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda, coefs, tol, low, high, nq):
     """SURVEY §8(d)'s configs[2] sweeps at full DB size: coefs = 2 (the general path over the
     m2-ordered key segments, src/fp_handler.c:318-351), wider tolerances and the ignore filter
     (:293-306, :324-337) — every key == the oracle's. 100/3400 Hz drops ~92% of the synthetic
     frames (max1 ~17 dB < 20 dB) and matches nothing; 50/60 Hz (16.99/17.78 dB) keeps about a third
-    and still matches, so the filter's kept/dropped split is exercised on both sides."""
+    and still matches, and drops the max2 condition of the frames whose max2 falls outside it (the
+    case whose 16-bit count pairs once borrowed across the halves: round 3, golden rand_05), so the
+    filter's kept/dropped split is exercised on both sides. 128 queries = one full sweep chunk; at
+    tolerance 0.45 every (key, clip) group of the chunk's keys is one long cluster of the clip-major
+    sweep (bench.py times (2, 0.45) on all 4,096)."""
     torch = torch_cuda
     qpcm, d_q = _c3_batch(c3db, tfp_lib, torch, nq, SEED_Q + coefs)
     qdb, qoff = _oracle_q(oracle, qpcm)
     w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(coefs, tol, low, high))
-    if low == 50:
+    if low == 50 or (low < 0 and tol >= 0.1):
         assert (w >= 0).sum() > 0  # the filter keeps frames that still match
 
 
@@ -379,14 +387,118 @@ def _bench_batch(c3db, torch, nq=4096):
 def test_configs2_timed_batch_all_4096_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
     """The batch bench.py times (4,096 x 5 s queries, coefs = 1, tolerance 0.001, the vote path),
     every one of its keys == the oracle's sorted-index search over the same 93.8 M rows; and the
-    bench's coefs = 2 tolerance 0.001 sweep on its first 256 queries (4 sweep chunks of 64 queries
-    in one slab of the general path, src/fp_handler.c:318-351) at full DB size."""
+    bench's coefs = 2 sweeps of the same batch, all 4,096 queries (32 sweep chunks of 128 queries,
+    src/fp_handler.c:318-351) at tolerance 0.001 and at 0.45 (its widest, the clip-major sweep's
+    longest clusters), at full DB size."""
     torch = torch_cuda
     qpcm, d_q = _bench_batch(c3db, torch)
     qdb, qoff = _oracle_q(oracle, qpcm)
     w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(1, 0.001))
     assert (w >= 0).sum() >= 1000  # (the bench reports ~1,500 found)
-    k = 256
-    w2, _ = _check_keys(c3db, tfp_lib, torch, qpcm[:k], d_q[:k].contiguous(), qdb[:k * int(qoff[1])], qoff[:k + 1],
-                        tfp_lib.params(2, 0.001))
-    assert (w2 >= 0).sum() > 0
+    for tol in (0.001, 0.45):
+        w2, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(2, tol))
+        assert (w2 >= 0).sum() > 0
+
+
+def noise_clips(n, nsamples, seed=0x7153C3):
+    """Full-scale white noise clips (int16): their max1 values sit at 16.19-16.25 dB, below every
+    configs[2] DB row (>= 16.6 dB), so key 16's box at tolerance 0.45 ([15.55, 16.45] dB) holds
+    only these clips' rows. A coefs = 1, tolerance 0.45 query cut from one can only be won by a
+    noise clip (ties between them: the greatest uuid, src/fp_handler.c:367-374)."""
+    rng = np.random.default_rng(seed)
+    return rng.integers(-32768, 32768, (n, nsamples)).astype(np.int16)
+
+
+def new_clip_uuid(i: int) -> str:
+    """uuids above every _uuid_of(): the i-th enrolled noise clip sorts after all clips before it."""
+    return "ffffffff-ffff-4fff-bfff-%012x" % i
+
+
+@pytest.mark.timeout(900)
+def test_updated_index_at_100k_clips_vs_full_build_and_oracle(c3db, oracle, tfp_lib, torch_cuda):
+    """The enrolled index as single-clip enrolments leave it at configs[2] size (the reference's
+    INSERTs into its max1 B-tree, src/fp_handler.c:559-571, :745-753: a clip is searchable at once):
+    8 single-clip tfp_index_add calls and one removal of a clip the queries hit. The new clips are 7
+    noise clips (noise_clips: after each add, a batch-1 search of an excerpt at coefs 1, tolerance
+    0.45 must return the clip just added, which only its own rows can make win) and a copy of a DB
+    clip's audio under a new uuid (a tie across old and new rows, decided by the uuid). Then a
+    query batch (512 configs[2] queries + 32 excerpts of the new clips) at coefs 1 (vote) and 2
+    (sweep): every key == an engine forced to full re-sorts (TFP_INDEX_FULL) over the same
+    operations == the oracle's sorted index over the live rows. Runs last in the module: it changes
+    the shared DB."""
+    torch = torch_cuda
+    eng, idx, db_clips = c3db["eng"], c3db["idx"], c3db["db_clips"]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    n_db, qn = 8000 * 30, 8000 * 5
+    nf_db = (n_db + HOP - 1) // HOP
+    assert int(idx.m1[(idx.m1 != oracle.NULL_MICRO) & (idx.m1 < 16_450_000)].size) == 0  # key 16's box at 0.45 is empty
+    full = _engine_with(tfp_lib, {"TFP_INDEX_FULL": "1"})
+    try:
+        _enroll_db(full, torch, dev, stream, list(range(db_clips)), keep_rows=False)
+        fb0, _ = eng.index_build_stats()
+        spec = _c3_queries(512, db_clips, SEED_Q + 11)
+        victim = spec[0][1]  # a DB clip the first query is an excerpt of
+        copy_of = spec[1][1]
+        new_pcm = np.concatenate([noise_clips(7, n_db), tfp_lib.synth_pcm(SEED_DB, [copy_of], n_db)])
+        new_rows, _ = oracle.fingerprint_batch(new_pcm.reshape(-1), np.arange(9) * n_db, nthreads=ORACLE_THREADS,
+                                               want_db=False)
+        new_uuids = [new_clip_uuid(i) for i in range(7)] + [_uuid_of(10**7 + copy_of)]
+        rows_m1, rows_m2, rows_clip = [idx.m1], [idx.m2], [idx.clip]
+        uuids = list(c3db["uuids"])
+        rng = np.random.default_rng(5)
+        live = np.ones(db_clips + 8, bool)
+        p1, p45 = tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.45)
+        for i in range(8):
+            m = new_rows[i * nf_db:(i + 1) * nf_db]
+            for e in (eng, full):
+                e.index_add(new_uuids[i], m[:, 0], m[:, 1])
+            uuids.append(new_uuids[i])
+            rows_m1.append(m[:, 0].copy())
+            rows_m2.append(m[:, 1].copy())
+            rows_clip.append(np.full(nf_db, db_clips + i, np.int32))
+            if i == 4:
+                for e in (eng, full):
+                    e.index_remove(_uuid_of(victim))
+                live[victim] = False
+            # batch-1 searches of an excerpt of the new clip (the dialplan's call, application_handler.c:180)
+            o = 256 * int(rng.integers(0, (n_db - qn) // HOP))
+            q = np.ascontiguousarray(new_pcm[i, o:o + qn])
+            for p in (p1, p45):
+                got = [e.search_pcm_batch(q, [0, qn], p)[0][0] for e in (eng, full)]
+                assert got[0] == got[1], (i, p.tolerance)
+                if i < 7 and p is p45:
+                    assert got[0] is not None and got[0]["audio_uuid"] == new_uuids[i], (i, got[0])
+        assert eng.index_build_stats()[0] == fb0  # no full re-sort of the 100k-clip index
+        r1, r2, rc = (np.concatenate(a) for a in (rows_m1, rows_m2, rows_clip))
+        keep = live[rc]
+        rank = np.full(len(uuids), -1, np.int32)
+        for r, (_, c) in enumerate(sorted((u, c) for c, u in enumerate(uuids) if live[c])):
+            rank[c] = r
+        oidx = oracle.SortedIndex(r1[keep], r2[keep], rc[keep], rank)
+        del r1, r2, rc, keep
+        qpcm = [tfp_lib.synth_pcm(sd, [c], qn, offsets=[o])[0] for sd, c, o in spec]
+        for i in range(8):
+            for _ in range(4):
+                o = 256 * int(rng.integers(0, (n_db - qn) // HOP))
+                qpcm.append(new_pcm[i, o:o + qn])
+        qpcm = np.stack(qpcm)
+        d_q = torch.from_numpy(qpcm).to("cuda")
+        qdb, qoff = _oracle_q(oracle, qpcm)
+        plan_off = np.arange(len(qpcm) + 1, dtype=np.int64) * qn
+        for p in (p1, p45, tfp_lib.params(2, 0.001), tfp_lib.params(2, 0.1)):
+            w, mc = oidx.search_batch(qdb[:, 0], qdb[:, 1], qoff, p.coefs, p.tolerance, nthreads=ORACLE_THREADS,
+                                      method="boxes" if p.coefs == 2 else "scan")
+            expk = np.where(w >= 0, (mc.astype(np.uint64) << np.uint64(32)) | rank[np.maximum(w, 0)].astype(np.uint64), 0)
+            for e in (eng, full):
+                keys = torch.zeros(len(qpcm), dtype=torch.int64, device="cuda")
+                e.search_device(e.plan(plan_off), d_q.data_ptr(), p, keys.data_ptr(), stream)
+                torch.cuda.synchronize()
+                k = keys.cpu().numpy().view(np.uint64)
+                assert np.array_equal(k, expk.astype(np.uint64)), (e is full, p.coefs, p.tolerance,
+                                                                    np.nonzero(k != expk)[0][:8])
+            if p is p45:  # the noise excerpts: the newest noise clip (greatest uuid), the victim never
+                assert all(w[512 + j] == db_clips + 6 for j in range(28)) and victim not in set(w.tolist())
+        assert full.index_build_stats()[1] == 0  # the reference engine never merged
+    finally:
+        full.close()

@@ -157,3 +157,45 @@ def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
     assert g.index_stats() == (0, 0)
     g.close()
     e.close()
+
+
+def test_group_add_batch_all_or_nothing(tfp_lib, oracle, monkeypatch):
+    """A batch add on a group fails as a whole when one shard's engine fails (a device error,
+    injected by TFP_TEST_FAIL_ADD_BATCH on the 5th engine call: the second group batch's middle
+    shard call): the shards that took their part drop it again, so no clip stays on a GPU without
+    a member (advisor r3: such an orphan could win a search the shim then reports as NOTFOUND and
+    never be deleted). The group's clips, rows and every search stay as before the failed batch, and
+    the next batch enrols normally."""
+    n = 8000 * 4
+    nf = (n + HOP - 1) // HOP
+    pcm = tfp_lib.synth_pcm(SEED_DB, range(60), n)
+    micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(61) * n, nthreads=16, want_db=False)
+    uuids = _uuids(np.random.default_rng(31), 60)
+    q = np.ascontiguousarray(pcm[:6, 256 * 10: 256 * 10 + 16000])
+    p = tfp_lib.params(1, 0.45)
+
+    def batch(g, a, b):
+        fo = np.arange(b - a + 1, dtype=np.int64) * nf
+        g.index_add_batch(uuids[a:b], fo, micro[a * nf:b * nf, 0], micro[a * nf:b * nf, 1])
+
+    monkeypatch.setenv("TFP_TEST_FAIL_ADD_BATCH", "5")
+    g = tfp_lib.Group([0, 0, 0])
+    try:
+        batch(g, 0, 30)  # engine calls 1-3
+        before = (g.index_stats(), _pairs(g.search_pcm_batch(q.reshape(-1), np.arange(7) * 16000, p)[0]))
+        with pytest.raises(tfp_lib.TfpError):
+            batch(g, 30, 45)  # calls 4-6: the 5th fails
+        assert g.index_stats() == before[0]
+        assert sum(c for _, c in g.engine_stats()) == 30  # nothing of the failed batch left on any engine
+        assert _pairs(g.search_pcm_batch(q.reshape(-1), np.arange(7) * 16000, p)[0]) == before[1]
+        for u in uuids[30:45]:  # never members: removal reports them missing
+            with pytest.raises(tfp_lib.TfpError):
+                g.index_remove(u)
+        batch(g, 30, 60)  # calls 7-9
+        assert g.index_stats()[1] == 60
+        live = {uuids[c]: (micro[c * nf:(c + 1) * nf, 0], micro[c * nf:(c + 1) * nf, 1]) for c in range(60)}
+        _, qdb = oracle.fingerprint_batch(q.reshape(-1), np.arange(7) * 16000, nthreads=16)
+        exp = _oracle_search(oracle, live, qdb[:, 0], qdb[:, 1], np.arange(7) * ((16000 + HOP - 1) // HOP), p)
+        assert _pairs(g.search_pcm_batch(q.reshape(-1), np.arange(7) * 16000, p)[0]) == exp
+    finally:
+        g.close()

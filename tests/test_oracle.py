@@ -108,9 +108,10 @@ def test_oracle_batch_equals_single(oracle):
     assert np.array_equal(micro, single)
 
 
-def test_sorted_index_search_matches_sqlite_golden(oracle):
-    """The sorted-index batch search (large tables) gives the SQLite-pinned results too: every
-    golden scenario, every query, ties by uuid rank."""
+@pytest.mark.parametrize("method,mode", [("scan", 0), ("boxes", 0), ("boxes", 1), ("boxes", 2)])
+def test_sorted_index_search_matches_sqlite_golden(oracle, method, mode):
+    """The sorted-index batch searches (large tables) give the SQLite-pinned results too: every
+    golden scenario, every query, ties by uuid rank; the per-box form in both of its forms."""
     g = load_golden()
     n = 0
     for s in g["scenarios"]:
@@ -128,7 +129,8 @@ def test_sorted_index_search_matches_sqlite_golden(oracle):
             q1 = np.concatenate([_q(q["q1"]) for q in qs]) if qs else np.zeros(0)
             q2 = np.concatenate([_q(q["q2"]) for q in qs])
             qoff = np.concatenate([[0], np.cumsum([len(q["q1"]) for q in qs])])
-            w, mc = idx.search_batch(q1, q2, qoff, coefs, tol if tol is not None else float("nan"), low, high, nthreads=3)
+            w, mc = idx.search_batch(q1, q2, qoff, coefs, tol if tol is not None else float("nan"), low, high, nthreads=3,
+                                     method=method, mode=mode)
             for i, q in enumerate(qs):
                 got = {"audio_uuid": s["uuids"][w[i]], "match_count": int(mc[i]), "frame_count": len(q["q1"])} \
                     if w[i] >= 0 else None
@@ -137,8 +139,9 @@ def test_sorted_index_search_matches_sqlite_golden(oracle):
     assert n > 900
 
 
-def test_sorted_index_search_equals_linear_scan(oracle):
-    """Random tables with NULL rows, coefs 1 and 2, ignore filters: sorted search == row scan."""
+@pytest.mark.parametrize("method,mode", [("scan", 0), ("boxes", 0), ("boxes", 1), ("boxes", 2)])
+def test_sorted_index_search_equals_linear_scan(oracle, method, mode):
+    """Random tables with NULL rows, coefs 1 and 2, ignore filters: sorted searches == row scan."""
     rng = np.random.default_rng(17)
     nclips, nrows = 300, 40000
     m1 = rng.integers(-5_000_000, 5_000_000, nrows).astype(np.int32)
@@ -159,7 +162,7 @@ def test_sorted_index_search_equals_linear_scan(oracle):
     q1[rng.random(len(q1)) < 0.05] = np.inf
     for coefs, tol, low, high in [(1, 0.001, -1, -1), (1, 0.4, -1, -1), (2, 0.3, -1, -1), (2, 0.05, 1, 3),
                                   (1, -1.0, 1, -1), (3, 0.1, -1, -1)]:
-        w, mc = idx.search_batch(q1, q2, qoff, coefs, tol, low, high, nthreads=4)
+        w, mc = idx.search_batch(q1, q2, qoff, coefs, tol, low, high, nthreads=4, method=method, mode=mode)
         for i in range(nq):
             a, b = qoff[i], qoff[i + 1]
             found, ww, mm, _ = oracle.search(m1, m2, clip, uuids, q1[a:b], q2[a:b], coefs, tol, low, high)

@@ -31,7 +31,7 @@ def _build(tmp_path, tfp_lib):
         subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-pedantic", *INC, "-c", src, "-o",
                         str(tmp_path / (os.path.basename(src) + ".o"))], check=True)
     subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", *INC, *SHIM_SRC, "-o", exe, "-L" + lib,
-                    "-ltiresias_fp", "-Wl,-rpath," + lib, *LIBS], check=True)
+                    "-ltiresias_fp", "-Wl,-rpath," + lib, *LIBS, "-lpthread"], check=True)
     return exe
 
 
@@ -282,3 +282,47 @@ def test_shim_backup_interchangeable_with_dbio(tmp_path, tfp_lib):
     py_uuids = {o["TIRFILENAME"]: o["TIRFILEUUID"] for o in py_first if o["TIRSTATUS"] == "FOUND"}
     assert searches_c(py_db, []) == py_first         # Python writes, C reads
     assert py_uuids  # (the two enrolments drew different random uuids, so their tie-breaks may differ)
+
+
+@pytest.mark.gpu
+def test_shim_64_channel_threads_equal_serial(tmp_path, tfp_lib):
+    """The module's channel threads (application_handler.c:66 runs tiresias_exec per channel; each
+    calls fp_search_fingerprint_info, :180) on one shared module (fp_handler.c:1161-1169): 64 threads
+    x 6 searches at once through the shim on a 3-engine group ("0,0,0"), over 12 recordings, at the
+    dialplan's coefs 1 and at coefs 2. Every result == the same file's serial search, and the calls
+    ran coalesced (fewer GPU batches than calls: tfp_group_search_pcm_batch's coalescer)."""
+    exe = _build(tmp_path, tfp_lib)
+    db = str(tmp_path / "p.db")
+    n = 8000 * 8
+    pcm = tfp_lib.synth_pcm(0x7153A1, range(16), n)
+    files = []
+    for c in range(16):
+        files.append(str(tmp_path / ("e%02d.wav" % c)))
+        _write_wav(files[-1], pcm[c])
+    qf = []
+    for i in range(12):
+        qf.append(str(tmp_path / ("q%02d.wav" % i)))
+        q = pcm[i % 16, 256 * (3 + 5 * i): 256 * (3 + 5 * i) + 24000] if i % 4 != 3 else \
+            tfp_lib.synth_pcm(0x7153B2, [i], 24000)[0]
+        _write_wav(qf[-1], q)
+    cmd = ["devices", "0,0,0", "init"]
+    for f in files:
+        cmd += ["enroll", "ctx", f]
+    for coefs, tol in ((1, "0.45"), (2, "0.3")):
+        for f in qf:
+            cmd += ["search", "ctx", f, str(coefs), tol, "-1", "-1"]
+        cmd += ["psearch", "64", "6", "ctx", str(coefs), tol, "-1", "-1", str(len(qf)), *qf]
+    out = _run(exe, db, *(cmd + ["term"]))
+    serial = [o for o in out if "TIRSTATUS" in o]
+    par = [o for o in out if "psearch" in o]
+    assert len(serial) == 24 and len(par) == 2
+    for k, ps in enumerate(par):
+        want = {}
+        for i, o in enumerate(serial[12 * k: 12 * k + 12]):
+            want[i] = (o["TIRSTATUS"] == "FOUND", o.get("TIRFILEUUID", ""), o.get("TIRMATCHCOUNT", 0),
+                       o.get("TIRFRAMECOUNT", 0))
+        assert sum(v[0] for v in want.values()) >= 6
+        assert len(ps["results"]) == 64 * 6
+        for fi, found, uuid, mc, fc in ps["results"]:
+            assert (bool(found), uuid, mc, fc) == want[fi], (k, fi)
+        assert ps["calls"] == 64 * 6 and ps["batches"] < ps["calls"], ps  # coalesced
