@@ -635,6 +635,43 @@ int fp_create_audio_list_infos(const char* context, const char* const* filenames
 	return enrolled;
 }
 
+/* fp_handler.c:386-407: the winner's audio_list row + frame_count + match_count; NULL for NOTFOUND */
+static struct ast_json* search_result(const tfp_result* r)
+{
+	struct ast_json* j_res;
+
+	if(r->found == 0) {
+		return NULL; /* no row in the temp table: NOTFOUND (fp_handler.c:367-382) */
+	}
+	j_res = fpc_get_audio_list_info(r->uuid); /* fp_handler.c:394-401 */
+	if(j_res == NULL) {
+		ast_log(LOG_ERROR, "Could not get audio list info. uuid[%s]\n", r->uuid);
+		return NULL;
+	}
+	ast_json_object_set(j_res, "frame_count", ast_json_integer_create(r->frame_count));
+	ast_json_object_set(j_res, "match_count", ast_json_integer_create(r->match_count));
+	return j_res;
+}
+
+static bool search_params(tfp_search_params* p, const char* context, const int coefs, const double tolerance,
+		const int freq_ignore_low, const int freq_ignore_high)
+{
+	if(context == NULL) {
+		ast_log(LOG_WARNING, "Wrong input parameter.\n");
+		return false;
+	}
+	if((coefs < 1) || (coefs > 2)) { /* fp_handler.c:247-250 */
+		ast_log(LOG_WARNING, "Wrong coefs count. coefs[%d]\n", coefs);
+		return false;
+	}
+	memset(p, 0, sizeof(*p));
+	p->coefs = coefs;
+	p->tolerance = tolerance; /* < 0: the default 0.001 (fp_handler.c:252-256) */
+	p->freq_ignore_low = freq_ignore_low;
+	p->freq_ignore_high = freq_ignore_high;
+	return true;
+}
+
 struct ast_json* fp_search_fingerprint_info(const char* context, const char* filename, const int coefs,
 		const double tolerance, const int freq_ignore_low, const int freq_ignore_high)
 {
@@ -645,26 +682,20 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 	int rc;
 	tfp_search_params p;
 	tfp_result r;
-	struct ast_json* j_res;
 
-	if((context == NULL) || (filename == NULL)) {
+	if(filename == NULL) {
 		ast_log(LOG_WARNING, "Wrong input parameter.\n");
 		return NULL;
 	}
-	if((coefs < 1) || (coefs > 2)) { /* fp_handler.c:247-250 */
-		ast_log(LOG_WARNING, "Wrong coefs count. coefs[%d]\n", coefs);
+	if(search_params(&p, context, coefs, tolerance, freq_ignore_low, freq_ignore_high) == false) {
 		return NULL;
 	}
 	if(read_audio(filename, &pcm, &cap, &x, &ns, &sr) != 0) {
 		return NULL;
 	}
-	memset(&p, 0, sizeof(p));
-	p.coefs = coefs;
-	p.tolerance = tolerance; /* < 0: the default 0.001 (fp_handler.c:252-256) */
-	p.freq_ignore_low = freq_ignore_low;
-	p.freq_ignore_high = freq_ignore_high;
 	off[0] = 0;
 	off[1] = ns;
+	/* concurrent channel threads' calls run as shared GPU batches (tfp_group's coalescer) */
 	rc = pcm ? tfp_group_search_pcm_batch(g_tfp, pcm, off, 1, sr, &p, &r)
 	         : tfp_group_search_f32_batch(g_tfp, x, off, 1, sr, &p, &r);
 	pcm_put(pcm, cap);
@@ -673,15 +704,105 @@ struct ast_json* fp_search_fingerprint_info(const char* context, const char* fil
 		ast_log(LOG_ERROR, "Could not search %s: %s\n", filename, tfp_group_last_error(g_tfp));
 		return NULL;
 	}
-	if(r.found == 0) {
-		return NULL; /* no row in the temp table: NOTFOUND (fp_handler.c:367-382) */
-	}
-	j_res = fpc_get_audio_list_info(r.uuid); /* fp_handler.c:394-401 */
-	if(j_res == NULL) {
-		ast_log(LOG_ERROR, "Could not get audio list info. uuid[%s]\n", r.uuid);
+	return search_result(&r);
+}
+
+/* ---- live channels: the dialplan application's recording without the /tmp WAV -------------
+ * application_handler.c:152-185 records `duration` ms of the channel's voice frames
+ * (record_voice, :248-312) into /tmp/tiresias-UUID.wav and searches that file. A channel keeps the
+ * same samples in engine-mapped host memory instead: every voice frame is pushed as it is read,
+ * and the search reads the recording in place (tfp_group_search_pcm_gather, coalesced with the
+ * other channels' searches). The ring keeps the last max_ms of audio (written twice, so the kept
+ * samples are always one contiguous run); with max_ms >= the recording's length it holds exactly
+ * what record_voice would have written. */
+struct fp_channel {
+	int32_t sr;
+	int64_t cap;   /* samples kept */
+	int64_t n;     /* samples pushed since open / reset */
+	int64_t pos;   /* ring position of the next sample */
+	int16_t* ring; /* 2 * cap samples, tfp_host_alloc */
+};
+
+fp_channel* fp_channel_open(int sample_rate, int max_ms)
+{
+	fp_channel* ch;
+	void* p = NULL;
+
+	if(sample_rate <= 0 || max_ms <= 0) {
+		ast_log(LOG_WARNING, "Wrong input parameter.\n");
 		return NULL;
 	}
-	ast_json_object_set(j_res, "frame_count", ast_json_integer_create(r.frame_count));
-	ast_json_object_set(j_res, "match_count", ast_json_integer_create(r.match_count));
-	return j_res;
+	ch = ast_calloc(1, sizeof(*ch));
+	if(ch == NULL) {
+		return NULL;
+	}
+	ch->sr = sample_rate;
+	ch->cap = ((int64_t)sample_rate * max_ms + 999) / 1000;
+	if(tfp_host_alloc(sizeof(int16_t) * 2 * (size_t)ch->cap, &p) != TFP_OK) {
+		ast_free(ch);
+		return NULL;
+	}
+	ch->ring = (int16_t*)p;
+	return ch;
+}
+
+bool fp_channel_push(fp_channel* ch, const int16_t* slin, int nsamples)
+{
+	int64_t i;
+
+	if(ch == NULL || nsamples < 0 || (nsamples > 0 && slin == NULL)) {
+		return false;
+	}
+	for(i = 0; i < nsamples; i++) {
+		ch->ring[ch->pos] = slin[i];
+		ch->ring[ch->pos + ch->cap] = slin[i];
+		if(++ch->pos == ch->cap) {
+			ch->pos = 0;
+		}
+	}
+	ch->n += nsamples;
+	return true;
+}
+
+void fp_channel_reset(fp_channel* ch)
+{
+	if(ch != NULL) {
+		ch->n = 0;
+		ch->pos = 0;
+	}
+}
+
+struct ast_json* fp_channel_search(fp_channel* ch, const char* context, const int coefs, const double tolerance,
+		const int freq_ignore_low, const int freq_ignore_high)
+{
+	tfp_search_params p;
+	tfp_result r;
+	const int16_t* q;
+	int64_t len;
+	int rc;
+
+	if(ch == NULL) {
+		ast_log(LOG_WARNING, "Wrong input parameter.\n");
+		return NULL;
+	}
+	if(search_params(&p, context, coefs, tolerance, freq_ignore_low, freq_ignore_high) == false) {
+		return NULL;
+	}
+	/* the kept samples: [0, n) before the ring wraps, else the cap samples from pos */
+	len = ch->n < ch->cap ? ch->n : ch->cap;
+	q = ch->n < ch->cap ? ch->ring : ch->ring + ch->pos;
+	rc = tfp_group_search_pcm_gather(g_tfp, &q, &len, 1, ch->sr, &p, &r);
+	if(rc != TFP_OK) {
+		ast_log(LOG_ERROR, "Could not search the channel's recording: %s\n", tfp_group_last_error(g_tfp));
+		return NULL;
+	}
+	return search_result(&r);
+}
+
+void fp_channel_close(fp_channel* ch)
+{
+	if(ch != NULL) {
+		tfp_host_free(ch->ring);
+		ast_free(ch);
+	}
 }

@@ -41,4 +41,19 @@ void fp_set_gpu_devices(const char* list);
  * searches went through the coalescer as *batches batches. false before fp_init. */
 bool fp_get_search_stats(int64_t* calls, int64_t* batches);
 
+/* New: a live channel, for the dialplan application's record loop (application_handler.c:152-185,
+ * record_voice :248-312) without the /tmp WAV round trip. Open one per call with max_ms >= the
+ * recording's duration, push every voice frame's SLIN samples as it is read (160 per 20 ms frame
+ * at 8 kHz), then fp_channel_search: the same result as fp_search_fingerprint_info on a WAV of
+ * the samples pushed since open / reset (of the last max_ms of them, if more were pushed). The
+ * samples stay in engine-mapped memory, read by the GPU in place; concurrent channels' searches run
+ * as shared batches. A channel is used by one thread at a time. */
+typedef struct fp_channel fp_channel;
+fp_channel* fp_channel_open(int sample_rate, int max_ms);
+bool fp_channel_push(fp_channel* ch, const int16_t* slin, int nsamples);
+void fp_channel_reset(fp_channel* ch);
+struct ast_json* fp_channel_search(fp_channel* ch, const char* context, const int coefs, const double tolerance,
+		const int freq_ignore_low, const int freq_ignore_high);
+void fp_channel_close(fp_channel* ch);
+
 #endif

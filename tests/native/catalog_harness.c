@@ -3,9 +3,11 @@
  * with its main renamed; fp_delete_audio_list_info (the hot half's) is the catalog's own delete.
  *   catalog_driver BACKUP_DB CMD...   with CMD one of
  *     init | term | close | create CONTEXT FILE UUID | store CONTEXT UUID ROWS_BIN | load |
- *     delete UUID | ctx NAME DIR | ctxdel NAME | lists | hash FILE | uuid
+ *     delete UUID | ctx NAME DIR | ctxdel NAME | lists | hash FILE | uuid |
+ *     cthreads NTHREADS ITERS NFILES FILE...  (the catalog from many threads, shim_harness.c)
  * ROWS_BIN: n int32 m1 values then n int32 m2 values. */
 #define main shim_harness_main
+#define SHIM_HARNESS_NO_ENGINE
 #include "shim_harness.c"
 #undef main
 
@@ -24,6 +26,20 @@ struct ast_json* fp_search_fingerprint_info(const char* c, const char* f, const 
 }
 bool fp_delete_audio_list_info(const char* uuid) { return fpc_delete_audio_list_info(uuid); }
 void fp_set_gpu_devices(const char* list) { (void)list; }
+fp_channel* fp_channel_open(int sr, int ms) {
+  (void)sr; (void)ms;
+  return NULL;
+}
+bool fp_channel_push(fp_channel* ch, const int16_t* s, int n) {
+  (void)ch; (void)s; (void)n;
+  return false;
+}
+void fp_channel_reset(fp_channel* ch) { (void)ch; }
+struct ast_json* fp_channel_search(fp_channel* ch, const char* c, const int co, const double t, const int l, const int h) {
+  (void)ch; (void)c; (void)co; (void)t; (void)l; (void)h;
+  return NULL;
+}
+void fp_channel_close(fp_channel* ch) { (void)ch; }
 bool fp_get_search_stats(int64_t* calls, int64_t* batches) {
   (void)calls; (void)batches;
   return false;
@@ -109,6 +125,10 @@ int main(int argc, char** argv) {
       printf("{\"hash\": \"%s\"}\n", h ? h : "");
       free(h);
       i += 1;
+    } else if (!strcmp(cmd, "cthreads") && i + 2 < argc && i + 3 + atoi(argv[i + 2]) <= argc) {
+      const int nf = atoi(argv[i + 2]);
+      cthreads(atoi(argv[i]), atoi(argv[i + 1]), nf, argv + i + 3);  /* (shim_harness.c) */
+      i += 3 + nf;
     } else if (!strcmp(cmd, "uuid")) {
       char* u = fp_generate_uuid();
       printf("{\"uuid\": \"%s\"}\n", u ? u : "");

@@ -7,7 +7,10 @@
  *     init | term | enroll CONTEXT FILE | enrolldir CONTEXT DIR | enrolldir1 CONTEXT DIR |
  *     delete UUID | search CONTEXT FILE COEFS TOL LOW HIGH | ctx NAME DIR | ctxdel NAME |
  *     lists | hash FILE | devices LIST |
- *     psearch NTHREADS REPS CONTEXT COEFS TOL LOW HIGH NFILES FILE...
+ *     psearch NTHREADS REPS CONTEXT COEFS TOL LOW HIGH NFILES FILE... |
+ *     chan CONTEXT FILE CHUNK MAXMS COEFS TOL LOW HIGH | cthreads NTHREADS ITERS NFILES FILE...
+ * chan plays the record loop (application_handler.c:248-312) on a live channel (fp_channel_*): the
+ * file's samples pushed CHUNK at a time (160 = one 20 ms SLIN frame), then searched.
  * psearch plays the module's channel threads: NTHREADS threads (application_handler.c:66, one per
  * call) each run REPS fp_search_fingerprint_info calls at once, thread t's r-th on file
  * (t * 7 + r) % NFILES, and print every result, the wall time and the coalescer's counts.
@@ -28,6 +31,7 @@
 #include "asterisk/logger.h"
 #include "fp_catalog.h"
 #include "fp_handler_tfp.h"
+#include "tiresias_fp.h"
 
 /* ---- ast_json: object / array / integer / real / string / null ---- */
 enum { J_OBJ, J_INT, J_STR, J_ARR, J_REAL, J_NULL };
@@ -218,6 +222,98 @@ static void psearch(int nth, int reps, const char* ctx, int coefs, double tol, i
   free(out);
 }
 
+/* ---- cthreads: the catalog from many threads (tests/test_sanitizers.py, under TSan / ASan) ----
+ * thread t, iteration i: file (t + i) % NFILES into context "ctx": create (dedup: of threads racing
+ * on one file exactly one creates it), store rows, read the row and the lists back, delete. */
+typedef struct {
+  int t, iters, nfiles;
+  char** files;
+  int created, dup;
+} cthr;
+
+static void* cthread_main(void* v) {
+  cthr* a = v;
+  int i;
+  for (i = 0; i < a->iters; i++) {
+    char* uuid = fp_generate_uuid();
+    int32_t m1[3] = {1000000 + i, INT32_MIN, -5}, m2[3] = {a->t, 7, INT32_MIN};
+    int ret;
+    if (uuid == NULL) continue;
+    ret = fpc_create_audio_list_info("ctx", a->files[(a->t + i) % a->nfiles], uuid);
+    if (ret == 1) {
+      struct ast_json* j;
+      a->created++;
+      fpc_store_fingerprints("ctx", uuid, m1, m2, 3);
+      j = fpc_get_audio_list_info(uuid);
+      ast_json_unref(j);
+      j = fp_get_audio_lists_all();
+      ast_json_unref(j);
+      fpc_delete_audio_list_info(uuid);
+    } else if (ret == 0) {
+      a->dup++;
+    }
+    free(uuid);
+  }
+  return NULL;
+}
+
+static void cthreads(int nth, int iters, int nfiles, char** files) {
+  pthread_t* th = calloc(nth, sizeof *th);
+  cthr* a = calloc(nth, sizeof *a);
+  int t, created = 0, dup = 0;
+  for (t = 0; t < nth; t++) {
+    a[t].t = t;
+    a[t].iters = iters;
+    a[t].nfiles = nfiles;
+    a[t].files = files;
+    pthread_create(&th[t], NULL, cthread_main, &a[t]);
+  }
+  for (t = 0; t < nth; t++) {
+    pthread_join(th[t], NULL);
+    created += a[t].created;
+    dup += a[t].dup;
+  }
+  printf("{\"cthreads\": %d, \"calls\": %d, \"created\": %d, \"dup\": %d}\n", nth, nth * iters, created, dup);
+  free(th);
+  free(a);
+}
+
+/* ---- chan: a live channel fed frame by frame ---- */
+static void chan_search(const char* ctx, const char* file, int chunk, int max_ms, int coefs, double tol, int low,
+                        int high) {
+  int64_t n = 0, i;
+  int32_t sr = 0;
+  int16_t* pcm;
+  fp_channel* ch;
+  char label[600];
+  snprintf(label, sizeof label, "chan:%s", file);
+#ifdef SHIM_HARNESS_NO_ENGINE  /* (catalog_harness.c: no engine library linked) */
+  (void)pcm; (void)ch; (void)i; (void)n; (void)chunk; (void)max_ms; (void)ctx; (void)coefs; (void)tol; (void)low;
+  (void)high; (void)sr;
+  print_search(label, NULL);
+  return;
+#else
+  if (tfp_wav_read(file, NULL, 0, &n, &sr) != TFP_OK || chunk <= 0) {
+    print_search(label, NULL);
+    return;
+  }
+  pcm = malloc(sizeof(int16_t) * (size_t)(n ? n : 1));
+  ch = fp_channel_open(sr, max_ms);
+  if (!pcm || !ch || tfp_wav_read(file, pcm, n, &n, &sr) != TFP_OK) {
+    free(pcm);
+    fp_channel_close(ch);
+    print_search(label, NULL);
+    return;
+  }
+  fp_channel_push(ch, pcm, 7);  /* a previous call's audio, dropped by the reset below */
+  fp_channel_reset(ch);
+  for (i = 0; i < n; i += chunk) fp_channel_push(ch, pcm + i, (int)(n - i < chunk ? n - i : chunk));
+  print_search(label, fp_channel_search(ch, ctx, coefs, tol, low, high));
+  fp_channel_close(ch);
+  free(pcm);
+#endif
+}
+
 static int file_select(const struct dirent* e) { return strcmp(e->d_name, ".") && strcmp(e->d_name, ".."); }
 
 /* app_tiresias.c:365-424: the context's directory, alphasort; batched or file by file */
@@ -302,6 +398,14 @@ int main(int argc, char** argv) {
       psearch(atoi(argv[i]), atoi(argv[i + 1]), ctx, atoi(argv[i + 3]), atof(argv[i + 4]), atoi(argv[i + 5]),
               atoi(argv[i + 6]), nf, argv + i + 8);
       i += 8 + nf;
+    } else if (!strcmp(cmd, "cthreads") && i + 2 < argc && i + 3 + atoi(argv[i + 2]) <= argc) {
+      const int nf = atoi(argv[i + 2]);
+      cthreads(atoi(argv[i]), atoi(argv[i + 1]), nf, argv + i + 3);
+      i += 3 + nf;
+    } else if (!strcmp(cmd, "chan") && i + 7 < argc) {
+      chan_search(argv[i], argv[i + 1], atoi(argv[i + 2]), atoi(argv[i + 3]), atoi(argv[i + 4]), atof(argv[i + 5]),
+                  atoi(argv[i + 6]), atoi(argv[i + 7]));
+      i += 8;
     } else if (!strcmp(cmd, "devices") && i < argc) {
       fp_set_gpu_devices(argv[i]);
       printf("{\"devices\": \"%s\"}\n", argv[i]);

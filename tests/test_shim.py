@@ -326,3 +326,55 @@ def test_shim_64_channel_threads_equal_serial(tmp_path, tfp_lib):
         for fi, found, uuid, mc, fc in ps["results"]:
             assert (bool(found), uuid, mc, fc) == want[fi], (k, fi)
         assert ps["calls"] == 64 * 6 and ps["batches"] < ps["calls"], ps  # coalesced
+
+
+@pytest.mark.gpu
+def test_shim_live_channel_equals_recorded_file_search(tmp_path, tfp_lib, oracle):
+    """fp_channel_* (the dialplan's record loop, application_handler.c:248-312, without the /tmp
+    WAV): a call's audio pushed as 160-sample SLIN frames (plus a 7-sample tail frame), then searched,
+    == fp_search_fingerprint_info on the recorded file (application_handler.c:180) == the oracle
+    over the enrolled rows; a ring kept shorter than the call (max_ms 2000 of a 3.02 s call) == the
+    search of a file holding its last 2 s."""
+    exe = _build(tmp_path, tfp_lib)
+    db = str(tmp_path / "c.db")
+    n = 8000 * 8
+    pcm = tfp_lib.synth_pcm(0x7153A1, range(8), n)
+    files = []
+    for c in range(8):
+        files.append(str(tmp_path / ("e%d.wav" % c)))
+        _write_wav(files[-1], pcm[c])
+    calls, tails = [], []
+    for i in range(5):
+        src = pcm[i % 8, 256 * (4 + 9 * i): 256 * (4 + 9 * i) + 24167] if i != 4 else \
+            tfp_lib.synth_pcm(0x7153B2, [3], 24167)[0]
+        calls.append(str(tmp_path / ("call%d.wav" % i)))
+        _write_wav(calls[-1], src)
+        tails.append(str(tmp_path / ("tail%d.wav" % i)))
+        _write_wav(tails[-1], src[-16000:])
+    cmd = ["init"]
+    for f in files:
+        cmd += ["enroll", "ctx", f]
+    for f, t in zip(calls, tails):
+        for coefs, tol in (("1", "0.45"), ("2", "0.3"), ("1", "-1")):
+            cmd += ["search", "ctx", f, coefs, tol, "-1", "-1", "chan", "ctx", f, "160", "3500", coefs, tol, "-1", "-1"]
+        cmd += ["search", "ctx", t, "1", "0.45", "-1", "-1", "chan", "ctx", f, "160", "2000", "1", "0.45", "-1", "-1"]
+    out = _run(exe, db, *(cmd + ["lists", "term"]))
+    res = [o for o in out if "TIRSTATUS" in o]
+    assert len(res) == 5 * 8
+    for k in range(0, len(res), 2):
+        a, b = dict(res[k]), dict(res[k + 1])
+        assert b.pop("file").startswith("chan:") and a.pop("file")
+        assert a == b, (k, a, b)
+    assert sum(o["TIRSTATUS"] == "FOUND" for o in res) >= 10
+    # the oracle on the first call at coefs 1, tolerance 0.45
+    lists = next(o for o in out if "audio_lists" in o)["audio_lists"]
+    uid = {int(a["name"][1:-4]): a["uuid"] for a in lists}
+    rows = [oracle.fingerprint(pcm[c])[2] for c in range(8)]
+    _, qdb, _ = oracle.fingerprint(pcm[0, 256 * 4: 256 * 4 + 24167])
+    found, w, mc, fc = oracle.search(np.concatenate([r[:, 0] for r in rows]), np.concatenate([r[:, 1] for r in rows]),
+                                     np.repeat(np.arange(8), len(rows[0])), [uid[c] for c in range(8)], qdb[:, 0],
+                                     qdb[:, 1], 1, 0.45, -1, -1)
+    o = res[1]
+    assert (o["TIRSTATUS"] == "FOUND") == found
+    if found:
+        assert (o["TIRFILEUUID"], o["TIRMATCHCOUNT"], o["TIRFRAMECOUNT"]) == (uid[w], mc, fc)
