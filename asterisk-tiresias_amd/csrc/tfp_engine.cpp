@@ -173,6 +173,7 @@ struct tfp_engine {
   int64_t tiekey_ident = -1; // tiekey on the device holds the identity over this many columns (-1: not known)
   bool key_bits_valid = false;
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
+  HostBuf spec_pin;         // pinned copy of the speculative sweep's counts (WideScratch::info)
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
   void* small_res_host = nullptr;  // the allocation small_res_dev was taken for
@@ -1066,59 +1067,76 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     // a count above fp16's exact range or a key outside the vote range: the scan path below
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }
-  if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
-    // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
-    if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
-    if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
-    if (e->cells.valid) {
-      HIPCHK(e, e->wide.reserve(nf, nq, C, s));
-      bool ok = false;
-      HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
-                                         &e->wide, &ok, s));
-      if (ok) {
-        HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
-        done = true;
+  for (int pass = 0;; pass++) {
+    bool spec = false;  // the sweep ran without the host reading its sort's counts (checked below)
+    if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
+      // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
+      if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
+      if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
+      if (e->cells.valid) {
+        HIPCHK(e, e->wide.reserve(nf, nq, C, s));
+        bool ok = false;
+        HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
+                                           &e->wide, &ok, s, pass == 0));
+        if (ok) {
+          HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
+          done = true;
+          spec = e->wide.spec;
+        }
+        if (e->dbg_vote) fprintf(stderr, "[tfp] general path: nq %d nf %lld C %d tol %g -> %s%s\n", nq, (long long)nf, C,
+                                 sc.tole, ok ? "sweep by groups" : "cells / row scan", spec ? " (speculative)" : "");
       }
-      if (e->dbg_vote) fprintf(stderr, "[tfp] general path: nq %d nf %lld C %d tol %g -> %s\n", nq, (long long)nf, C, sc.tole,
-                               ok ? "sweep by groups" : "cells / row scan");
     }
-  }
-  if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
-    // general path (tfp_scan.hip): queries in chunks of <= 256 MB of scratch per array
-    if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
-    int64_t chunk = (int64_t)(256ll << 20) / (4ll * C);
-    chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, nq));
-    const size_t bytes = sizeof(int32_t) * chunk * C;
-    if (bytes > e->scan_zeroed || bytes > e->stamp.bytes || bytes > e->score.bytes || bytes > e->touched.bytes ||
-        sizeof(int32_t) * chunk > e->tcnt.bytes) {
-      HIPCHK(e, e->stamp.reserve(bytes));
-      HIPCHK(e, e->score.reserve(bytes));
-      HIPCHK(e, e->touched.reserve(bytes));
-      HIPCHK(e, e->tcnt.reserve(sizeof(int32_t) * chunk));
-      const size_t z = std::min(std::min(e->stamp.bytes, e->score.bytes), e->touched.bytes);
-      HIPCHK(e, hipMemsetAsync(e->stamp.p, 0, z, s));
-      HIPCHK(e, hipMemsetAsync(e->score.p, 0, z, s));
-      HIPCHK(e, hipMemsetAsync(e->tcnt.p, 0, e->tcnt.bytes, s));
-      e->scan_zeroed = z;  // (touched is written before it is read)
+    if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
+      // general path (tfp_scan.hip): queries in chunks of <= 256 MB of scratch per array
+      if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
+      int64_t chunk = (int64_t)(256ll << 20) / (4ll * C);
+      chunk = std::max<int64_t>(1, std::min<int64_t>(chunk, nq));
+      const size_t bytes = sizeof(int32_t) * chunk * C;
+      if (bytes > e->scan_zeroed || bytes > e->stamp.bytes || bytes > e->score.bytes || bytes > e->touched.bytes ||
+          sizeof(int32_t) * chunk > e->tcnt.bytes) {
+        HIPCHK(e, e->stamp.reserve(bytes));
+        HIPCHK(e, e->score.reserve(bytes));
+        HIPCHK(e, e->touched.reserve(bytes));
+        HIPCHK(e, e->tcnt.reserve(sizeof(int32_t) * chunk));
+        const size_t z = std::min(std::min(e->stamp.bytes, e->score.bytes), e->touched.bytes);
+        HIPCHK(e, hipMemsetAsync(e->stamp.p, 0, z, s));
+        HIPCHK(e, hipMemsetAsync(e->score.p, 0, z, s));
+        HIPCHK(e, hipMemsetAsync(e->tcnt.p, 0, e->tcnt.bytes, s));
+        e->scan_zeroed = z;  // (touched is written before it is read)
+      }
+      for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
+        const int32_t n = (int32_t)std::min<int64_t>(chunk, nq - q0);
+        HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), qo.data(), (int32_t)q0, n,
+                              e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, &e->cells,
+                              e->tiekey.as<int32_t>(), C, e->stamp.as<int32_t>(), e->score.as<int32_t>(),
+                              e->touched.as<int32_t>(), e->tcnt.as<int32_t>(), d_best, s));
+      }
     }
-    for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
-      const int32_t n = (int32_t)std::min<int64_t>(chunk, nq - q0);
-      HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), qo.data(), (int32_t)q0, n,
-                            e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R, &e->cells,
-                            e->tiekey.as<int32_t>(), C, e->stamp.as<int32_t>(), e->score.as<int32_t>(),
-                            e->touched.as<int32_t>(), e->tcnt.as<int32_t>(), d_best, s));
+    // the speculative sweep's counts come back with the results (one host wait per batch)
+    if (spec) {
+      HIPCHK(e, e->spec_pin.reserve(4 * sizeof(int32_t)));
+      HIPCHK(e, hipMemcpyAsync(e->spec_pin.p, e->wide.info, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     }
-  }
-  if (d_keys_out) {
-    HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
-    // the scan kernels read and write engine scratch (boxes, stamp, score, best): the next call,
-    // on any stream or thread, may reuse it only once they are done
+    if (d_keys_out) {
+      HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+    } else if (nq) {
+      HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
+    }
+    // (the scan kernels read and write engine scratch: the next call, on any stream or thread, may
+    // reuse it only once they are done)
     HIPCHK(e, hipStreamSynchronize(s));
+    if (spec) {
+      const int32_t* info = e->spec_pin.as<int32_t>();
+      if (info[1] > 0 || info[2] > 0) {  // a frame for the row scan, or a window the one-sort key cannot order
+        if (e->dbg_vote) fprintf(stderr, "[tfp] speculative sweep redone (info %d %d %d)\n", info[0], info[1], info[2]);
+        done = false;
+        HIPCHK(e, hipMemsetAsync(d_best, 0, sizeof(unsigned long long) * nq, s));
+        continue;
+      }
+    }
     return TFP_OK;
   }
-  if (nq) HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
-  HIPCHK(e, hipStreamSynchronize(s));
-  return TFP_OK;
 }
 
 // The index column of a tie-break key (-1: none).
@@ -1190,6 +1208,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   e->wide.points_only = getenv("TFP_WIDE_POINTS") != nullptr;
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
+  e->wide.no_spec = getenv("TFP_WIDE_SYNC") != nullptr;
   if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;

@@ -244,6 +244,8 @@ struct WideScratch {
   int64_t cap_nf = 0, cap_nch = 0, cap_score = 0, cap_dtab = 0;
   int32_t slab = 0;                                  // chunks per groups launch
   int64_t min_width = -1;                            // prepare: every max2 window is at least this wide (-1: unknown)
+  bool spec = false;                                 // prepare ran without reading info back: the caller checks it with the results
+  bool no_spec = false;                              // TFP_WIDE_SYNC (A/B): read the counts back before the sweep
   bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
   bool groups_form = false;                          // TFP_WIDE_GROUPS (tests, A/B): the key-major sweep with score rows
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
@@ -259,8 +261,14 @@ struct WideScratch {
 // Sorts the batch's frames; *eligible = false (nothing else queued) when a frame needs the row
 // scan (key outside the cache, window outside int32) or a query has 2^16 frames or more (the
 // score rows hold 16-bit counts), the caller then takes launch_scan.
+// speculative: no host wait for the sort's counts (the sweep's kernels read the kept-frame count
+// on the device); ws->spec is then set, and the caller reads ws->info with the results: a batch
+// with info[1] > 0 (a frame for the row scan) or info[2] > 0 (a window width outside the sort key's
+// delta field) is redone with speculative = false. Without speculation (or when the tolerance's
+// window width is unknown) the counts are read back first, as before.
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s);
+                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s,
+                                    bool speculative = false);
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s);

@@ -597,10 +597,12 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
 }
 
 // Sorted frames' windows and queries; the segment table [chunk][segment key] = [begin, end).
+// (n: the kept frames, info[0] of the key pass, read on the device: no host wait for the sort)
 __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
-                                   int64_t n, const unsigned long long* __restrict__ ck,
+                                   const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
                                    const int32_t* __restrict__ fv, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
                                    uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
+  const int64_t n = *pn;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = fv[i];
     const FrameBox bx = boxes[f];
@@ -614,8 +616,9 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
 }
 
 // Chunk boundaries in the sorted frames: cbeg[ch] = first frame of chunk ch (n for ch >= chunks).
-__global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, int64_t n, int64_t nch,
+__global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, const int32_t* __restrict__ pn, int64_t nch,
                                  int32_t* __restrict__ cbeg) {
+  const int64_t n = *pn;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << kWideChunkShift);
 }
@@ -656,10 +659,12 @@ __global__ void wide_dir_count_kernel(const int32_t* __restrict__ seg, int64_t n
 // also fills the buckets after its own with se. Lanes write short runs themselves; a long run (a
 // sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
 // buckets per step, so no lane loops over thousands of buckets alone.
-__global__ void wide_dir_fill_kernel(int64_t n, const unsigned long long* __restrict__ ck, const int32_t* __restrict__ seg,
-                                     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s,
-                                     const int32_t* __restrict__ doff, int32_t* __restrict__ dtab) {
+__global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
+                                     const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
+                                     const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
+                                     int32_t* __restrict__ dtab) {
   constexpr int32_t kShort = 8;
+  const int64_t n = *pn;
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t i0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; i0 < n; i0 += nw * 64) {
@@ -1462,8 +1467,10 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
 }
 
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
-                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s) {
+                                    int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s,
+                                    bool speculative) {
   *eligible = false;
+  ws->spec = false;
   if (nq <= 0 || nf <= 0 || nf >= INT32_MAX / (4 << kDirScale) - 8 || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
     return hipSuccess;
   hipError_t e;
@@ -1473,6 +1480,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int end_bit = kWideChunkShift + cb;
   // U2 - L2 lies within a few micro-units of 2 tol (fmt6 rounds both ends): d = U2 - L2 - dbase
   const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
+  speculative = speculative && dbase >= 0 && !ws->no_spec;
   if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(1024, (nq + 255) / 256)), dim3(256), 0, s,
                      d_qoff, nq, ws->fq);
@@ -1484,39 +1492,43 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
                      dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
   if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
-  int32_t info[3] = {0, 0, 0};
-  if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
-  if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
   const int32_t* order = ws->vb;
-  ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase
-  if (info[2] > 0 || dbase < 0) {
-    // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
-    if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
-    hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
-    tb = ws->tmp_bytes;
-    if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
-    hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
-                       ws->ka, (int32_t*)nullptr, ws->info);
-    tb = ws->tmp_bytes;
-    if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, end_bit, s)))
-      return e;
+  if (speculative) {
+    // every window at least dbase wide and no frame for the row scan, as the caller checks after
+    // the results (info[1], info[2]); the kept-frame count stays on the device
+    ws->min_width = dbase;
+    ws->spec = true;
+  } else {
+    int32_t info[3] = {0, 0, 0};
     if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
-    order = ws->va;
+    if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
+    ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase
+    if (info[2] > 0 || dbase < 0) {
+      // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
+      if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
+      hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
+      tb = ws->tmp_bytes;
+      if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
+      hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
+                         ws->ka, (int32_t*)nullptr, ws->info);
+      tb = ws->tmp_bytes;
+      if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, end_bit, s)))
+        return e;
+      order = ws->va;
+    }
   }
-  const int64_t n = info[0];
+  // (info[0] = the kept frames, read by the kernels below on the device)
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
-  if (n > 0)
-    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(n)), dim3(256), 0, s, boxes, ws->fq, n, ws->kb, order, ws->L2s,
-                       ws->U2s, ws->qis, ws->seg);
-  hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, n, nch, ws->cbeg);
+  hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, ws->L2s,
+                     ws->U2s, ws->qis, ws->seg);
+  hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, ws->info, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
   const int64_t nd = nch * kKeyRange + 1;
   hipLaunchKernelGGL(wide_dir_count_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, ws->seg, nch, ws->dtab);
   size_t db = ws->dtmp_bytes;
   if ((e = hipcub::DeviceScan::ExclusiveSum(ws->dtmp, db, ws->dtab, ws->doff, (int)nd, s))) return e;
-  if (n > 0)
-    hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, n, ws->kb, ws->seg, ws->L2s, ws->U2s,
-                       ws->doff, ws->dtab);
+  hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb, ws->seg, ws->L2s, ws->U2s,
+                     ws->doff, ws->dtab);
   hipLaunchKernelGGL(wide_pcount_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
   hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
   hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot,

@@ -410,6 +410,49 @@ def test_search_small_out_of_range_key_falls_back(engine, tfp_lib):
     engine.index_clear()
 
 
+def test_speculative_sweep_redone_for_out_of_range_key(engine, oracle, tfp_lib):
+    """coefs = 2 batches take the sweep without a host wait for its sort's counts (the sweep runs on
+    the speculation that every frame's key lies in the clip-set cache and every max2 window fits the
+    one-sort key); the counts come back with the results. A batch with a key outside the cache
+    (|k| > 511) must then be redone on the row scan: its results == the oracle's, and == a batch
+    without that query."""
+    engine.index_clear()
+    rng = np.random.default_rng(4)
+    m1s, m2s, clip, uu = [], [], [], []
+    for c in range(40):
+        n = 30
+        m1 = (rng.integers(22, 26, n) * 1000000 + rng.integers(-300000, 300000, n)).astype(np.int32)
+        m2 = rng.integers(-3000000, 3000000, n).astype(np.int32)
+        if c == 7:
+            m1[:3] = 1000000000 + np.arange(3)  # rows at 1000 dB
+        u = "00000000-0000-4000-8000-%012d" % c
+        engine.index_add(u, m1, m2)
+        m1s.append(m1), m2s.append(m2), clip.append(np.full(n, c, np.int32)), uu.append(u)
+    m1, m2, cl = np.concatenate(m1s), np.concatenate(m2s), np.concatenate(clip)
+    qs = []
+    for i in range(6):
+        q1 = rng.uniform(21.5, 26.5, 50)
+        q2 = rng.uniform(-3.2, 3.2, 50)
+        if i == 2:
+            q1[:2] = 1000.0005  # key 1000: outside the cache, only the row scan can serve it
+            q2[:2] = m2s[7][0] / 1e6
+        qs.append((q1, q2))
+    fr = _frames_from_q(np.concatenate([q[0] for q in qs]), np.concatenate([q[1] for q in qs]))
+    qoff = np.arange(7) * 50
+    for tol in (0.3, 0.05):
+        p = tfp_lib.params(2, tol)
+        res, fcs = engine.search_batch(fr, qoff, p)
+        for i, (q1, q2) in enumerate(qs):
+            found, w, mc, fc = oracle.search(m1, m2, cl, uu, q1, q2, 2, tol, -1, -1)
+            got = None if res[i] is None else (res[i]["audio_uuid"], res[i]["match_count"])
+            assert got == ((uu[w], mc) if found else None), (tol, i)
+        keep = [0, 1, 3, 4, 5]
+        fr2 = _frames_from_q(np.concatenate([qs[i][0] for i in keep]), np.concatenate([qs[i][1] for i in keep]))
+        res2, _ = engine.search_batch(fr2, np.arange(6) * 50, p)
+        assert [res[i] for i in keep] == list(res2)
+    engine.index_clear()
+
+
 def _many_key_index(engine, nclips, spread, seed):
     """Rows whose max1 sit within +-0.002 of integers in [-spread, spread] (half inside the
     tol=0.001 boxes), so queries with keys over that range use up to 2*spread+1 vote keys."""
