@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 }
 
 #ifndef TFP_CLIP_OCC
-#define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spills 12 VGPRs)
+#define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 #endif
 __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
@@ -1152,7 +1152,9 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
     const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
     unsigned long long* __restrict__ part) {
   __shared__ uint32_t accs[kClipWaves][kWin * 64];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wv through readfirstlane: the wave's chunk, window range and per-chunk pointers are then scalar
+  // (as per-lane values they took 64-bit VGPR pairs, and 12 VGPRs spilled at 8 waves per SIMD)
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t gw = (int64_t)blockIdx.x * kClipWaves + wv;
   const int ch = (int)(gw / xw), x = (int)(gw % xw);
   uint32_t* acc = accs[wv];
