@@ -199,6 +199,21 @@ struct tfp_engine {
   int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
+  // index delta (round 4, tfp_index.hpp): the live clips added since the last build, searched by the
+  // coefs = 1 vote paths beside the main index instead of merged into it per enrolment
+  static constexpr int32_t kDeltaMaxClips = 512;        // columns reserved for them
+  static constexpr int64_t kDeltaMaxRows = 1ll << 20;  // beyond either limit the next update merges
+  bool use_delta = true;          // TFP_INDEX_DELTA=0: every update merges (A/B, tests)
+  bool force_merge = false;       // consolidate(): the next rebuild merges the delta
+  std::vector<int32_t> delta_clip;  // delta column delta_col0 + j -> clip id (uuid order)
+  std::vector<int32_t> delta_at;    // delta j's insertion point among the main columns' uuids
+  int32_t delta_col0 = 0;           // first delta column (a multiple of 1024)
+  int64_t delta_rows = 0;           // staged rows of the delta's clips
+  int64_t n_delta_updates = 0;
+  DevBuf d_delta, d_delta_at, kbox;
+  double kbox_tol = 0.0;
+  bool kbox_valid = false;
+  int32_t key_bits_cols = -1;       // the column count key_bits was laid out for (its row width)
   Coalescer coal;          // concurrent small host-sample searches share one batch (tfp_coalesce.hpp)
   bool coalesce = true;    // TFP_COALESCE=0: every call runs alone (A/B)
   ~tfp_engine() {
@@ -761,7 +776,8 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, const MergeBrea
   // bitsets get zero columns at the breakpoints (highest first) and the new rows' bits. Only
   // without removals, with few breakpoints and the same row width; best effort (else rebuilt).
   const int32_t W = key_bits_words(new_cols);
-  if (brk.n >= 0 && e->rng_valid && e->key_bits_valid && key_bits_words((int32_t)e->col_clip.size()) == W &&
+  if (brk.n >= 0 && e->rng_valid && e->key_bits_valid && e->key_bits_cols == (int32_t)e->col_clip.size() &&
+      key_bits_words((int32_t)e->col_clip.size()) == W &&
       e->key_bits.bytes >= sizeof(uint32_t) * (size_t)kKeyRange * W) {
     hipStream_t s = e->stream;
     bool ok = launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, e->rng_tol, e->rng_all.as<int64_t>(), s) == hipSuccess &&
@@ -782,8 +798,12 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, const MergeBrea
 
 int full_index(tfp_engine* e);
 
+int delta_update(tfp_engine* e);
+bool delta_eligible(const tfp_engine* e);
+
 int rebuild(tfp_engine* e) {
   if (!e->dirty) return TFP_OK;
+  if (delta_eligible(e)) return delta_update(e);
   int rc;
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
@@ -862,6 +882,10 @@ int rebuild(tfp_engine* e) {
   }
   e->ncols = (int32_t)live.size();
   e->col_clip = std::move(live);
+  e->delta_clip.clear();  // (every clip is in the main index now)
+  e->delta_at.clear();
+  e->delta_col0 = e->ncols;
+  e->delta_rows = 0;
   e->key_col = std::move(key_col);
   e->key_identity = !ovr;
   e->built = true;
@@ -871,6 +895,7 @@ int rebuild(tfp_engine* e) {
   e->dirty = false;
   e->rng_valid = carried;  // the key-range and clip-set caches follow the index (merge_index may carry the ranges and bitsets)
   e->key_bits_valid = carried && e->key_bits_valid;
+  if (e->key_bits_valid) e->key_bits_cols = e->ncols;
   e->cell_fresh = false;
   if (e->dbg_index)
     fprintf(stderr, "[tfp] index %s: %lld rows, %d clips; order %.3f keys %.3f total %.3f ms\n",
@@ -911,12 +936,142 @@ int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
 }
 
 // The small path's key-presence bitsets, from the cached row ranges (after ensure_ranges).
+int delta_bits(tfp_engine* e, hipStream_t s);
+
 int ensure_key_bits(tfp_engine* e, hipStream_t s) {
   if (e->key_bits_valid) return TFP_OK;
   HIPCHK(e, e->key_bits.reserve(sizeof(uint32_t) * (size_t)kKeyRange * key_bits_words(e->ncols)));
   HIPCHK(e, launch_key_bits(e->rng_all.as<int64_t>(), e->cols.as<int32_t>(), e->ncols, e->key_bits.as<uint32_t>(), s));
+  int rc = delta_bits(e, s);  // (the delta's columns, from its staged rows)
+  if (rc) return rc;
   e->key_bits_valid = true;
+  e->key_bits_cols = e->ncols;
   return TFP_OK;
+}
+
+// ---- index delta ---------------------------------------------------------------------------
+
+// The delta's key bits at the bitsets' tolerance (rng_tol), into columns that hold no bit.
+int delta_bits(tfp_engine* e, hipStream_t s) {
+  if (e->delta_clip.empty()) return TFP_OK;
+  if (!e->kbox_valid || memcmp(&e->kbox_tol, &e->rng_tol, sizeof e->rng_tol) != 0) {
+    HIPCHK(e, e->kbox.reserve(sizeof(int64_t) * 2 * kKeyRange));
+    HIPCHK(e, launch_key_boxes(e->rng_tol, e->kbox.as<int64_t>(), s));
+    e->kbox_tol = e->rng_tol;
+    e->kbox_valid = true;
+  }
+  const int32_t kspan = (int32_t)ceil(e->rng_tol) + 1;  // (delta_tol_ok: tol <= 8)
+  HIPCHK(e, launch_delta_bits(e->d_delta.as<DeltaClip>(), (int32_t)e->delta_clip.size(), e->st_m1.as<int32_t>(),
+                              e->kbox.as<int64_t>(), kspan, key_bits_words(e->ncols), e->key_bits.as<uint32_t>(), s));
+  return TFP_OK;
+}
+
+// Tolerances the delta's bits are set for: finite, 0 <= tol <= 8 (a row is in at most 2 ceil(tol) + 3
+// keys' boxes); other searches merge the delta first.
+bool delta_tol_ok(double tol) { return std::isfinite(tol) && tol >= 0.0 && tol <= 8.0; }
+
+bool delta_eligible(const tfp_engine* e) {
+  if (!e->use_delta || !e->built || e->force_full || e->force_merge || e->removed_built || e->n_staged >= INT32_MAX)
+    return false;
+  int64_t n = 0, rows = 0;
+  for (size_t i = e->built_clips; i < e->clips.size(); i++)
+    if (e->clips[i].alive) {
+      n++;
+      rows += e->clips[i].nrows;
+    }
+  return n <= tfp_engine::kDeltaMaxClips && rows <= tfp_engine::kDeltaMaxRows;
+}
+
+// An update that only adds (or removes clips added since the last build): the new clips become the
+// delta, in uuid order after the main columns; the tie keys are re-derived (global uuid ranks, or
+// the override's keys), and the key bits get the delta's columns. The main index, its row ranges
+// and its columns' bits stay as they are: the cost is the new clips' rows, not a pass over the DB.
+int delta_update(tfp_engine* e) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  hipStream_t s = e->stream;
+  auto by_uuid = [&](int32_t a, int32_t b) { return e->clips[a].uuid < e->clips[b].uuid; };
+  std::vector<int32_t> add;
+  int64_t rows = 0;
+  for (int32_t i = (int32_t)e->built_clips; i < (int32_t)e->clips.size(); i++)
+    if (e->clips[i].alive) {
+      add.push_back(i);
+      rows += e->clips[i].nrows;
+    }
+  std::sort(add.begin(), add.end(), by_uuid);
+  const int32_t Cm = (int32_t)e->col_clip.size(), D = (int32_t)add.size();
+  std::vector<int32_t> at(std::max(D, 1));
+  for (int32_t j = 0; j < D; j++)
+    at[j] = (int32_t)(std::lower_bound(e->col_clip.begin(), e->col_clip.end(), add[j], by_uuid) - e->col_clip.begin());
+  const int32_t col0 = D ? (Cm + 1023) / 1024 * 1024 : Cm;
+  const int32_t ncols = D ? col0 + tfp_engine::kDeltaMaxClips : Cm;
+  // tie keys (and the key -> column map with an override)
+  const bool ovr = !e->tiebreak_override.empty();
+  std::unordered_map<int32_t, int32_t> key_col;
+  HIPCHK(e, e->tiekey.reserve_grow(sizeof(int32_t) * std::max(ncols, 1)));
+  if (ovr) {
+    std::vector<int32_t> tk(std::max(ncols, 1), 0);
+    key_col.reserve(Cm + D);
+    for (int32_t c = 0; c < Cm + D; c++) {
+      const int32_t col = c < Cm ? c : col0 + (c - Cm);
+      const int32_t clip = c < Cm ? e->col_clip[c] : add[c - Cm];
+      if ((size_t)clip >= e->tiebreak_override.size())
+        return fail(e, TFP_E_ARG, "clip %s was added after tfp_index_set_tiebreak: set the tie-break keys again",
+                    e->clips[clip].uuid.c_str());
+      tk[col] = e->tiebreak_override[clip];
+      if (!key_col.emplace(tk[col], col).second) return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", tk[col]);
+    }
+    HIPCHK(e, hipMemcpyAsync(e->tiekey.p, tk.data(), sizeof(int32_t) * ncols, hipMemcpyHostToDevice, s));
+    e->tiekey_ident = -1;
+  } else {
+    HIPCHK(e, e->d_delta_at.reserve(sizeof(int32_t) * std::max(D, 1)));
+    if (D) HIPCHK(e, hipMemcpyAsync(e->d_delta_at.p, at.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
+    HIPCHK(e, launch_delta_tiekey(e->d_delta_at.as<int32_t>(), D, Cm, col0, ncols, e->tiekey.as<int32_t>(), s));
+    e->tiekey_ident = D ? -1 : Cm;
+  }
+  // the delta's clips for the bits kernel
+  std::vector<DeltaClip> dc(std::max(D, 1));
+  for (int32_t j = 0; j < D; j++) {
+    const Clip& c = e->clips[add[j]];
+    dc[j] = DeltaClip{c.off, (int32_t)c.nrows, col0 + j};
+  }
+  HIPCHK(e, e->d_delta.reserve(sizeof(DeltaClip) * std::max(D, 1)));
+  if (D) HIPCHK(e, hipMemcpyAsync(e->d_delta.p, dc.data(), sizeof(DeltaClip) * D, hipMemcpyHostToDevice, s));
+  e->delta_clip = std::move(add);
+  e->delta_at.assign(at.begin(), at.begin() + D);
+  e->delta_col0 = col0;
+  e->delta_rows = rows;
+  e->ncols = ncols;
+  e->key_col = std::move(key_col);
+  e->key_identity = !ovr;
+  // key bits: the delta columns cleared and set again when the layout stands, else rebuilt later
+  if (e->key_bits_valid && e->key_bits_cols == ncols && D > 0) {
+    const int32_t W = key_bits_words(ncols);
+    HIPCHK(e, hipMemset2DAsync(e->key_bits.as<uint32_t>() + col0 / 32, sizeof(uint32_t) * W, 0,
+                               sizeof(uint32_t) * (tfp_engine::kDeltaMaxClips / 32), kKeyRange, s));
+    int rc = delta_bits(e, s);
+    if (rc) return rc;
+  } else {
+    e->key_bits_valid = false;
+  }
+  HIPCHK(e, hipStreamSynchronize(s));  // (dc and at are released on return)
+  e->dirty = false;
+  e->n_delta_updates++;
+  if (e->dbg_index)
+    fprintf(stderr, "[tfp] index delta: %d clips (%lld rows) beside %d main columns; %.3f ms\n", D, (long long)rows, Cm,
+            std::chrono::duration<double, std::milli>(clk::now() - t0).count());
+  return TFP_OK;
+}
+
+// The delta merged into the main index now (coefs = 2, a fallback to the row scan, a tolerance the
+// delta's bits do not cover).
+int consolidate(tfp_engine* e) {
+  if (e->delta_clip.empty() && !e->dirty) return TFP_OK;
+  e->force_merge = true;
+  e->dirty = true;
+  const int rc = rebuild(e);
+  e->force_merge = false;
+  return rc;
 }
 
 // The general path's clip-set cache at tolerance tole (after ensure_ranges at tole).
@@ -957,10 +1112,15 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   sc.has_high = P->freq_ignore_high > 0;
   if (sc.has_low) sc.thr_low = 10 * log10((double)P->freq_ignore_low);
   if (sc.has_high) sc.thr_high = 10 * log10((double)P->freq_ignore_high);
+  // the index delta serves the coefs = 1 vote paths at the tolerances its bits cover; any other
+  // search reads the sorted rows, so the delta is merged into them first
+  if (!e->delta_clip.empty() && (sc.coefs != 1 || !delta_tol_ok(sc.tole)) && (rc = consolidate(e))) return rc;
+  const bool has_delta = !e->delta_clip.empty();
+  const int64_t R_all = e->nrows + e->delta_rows;  // rows that may match (main index + delta)
 
   std::vector<int64_t> qo(h_qoff, h_qoff + nq + 1);
   for (auto& v : qo) v -= h_qoff[0];
-  if (!d_keys_out && sc.coefs == 1 && nq >= 1 && nq <= kSmallQ && e->ncols > 0 && e->nrows > 0) {
+  if (!d_keys_out && sc.coefs == 1 && nq >= 1 && nq <= kSmallQ && e->ncols > 0 && R_all > 0) {
     // small batch (batch-1 latency): one vote launch over the cached key bitsets, results into
     // host-mapped memory
     bool fits = true;
@@ -996,7 +1156,12 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         }
         return TFP_OK;
       }
-      // a key outside the vote range: redo the batch on the general path below
+      // a key outside the vote range: redo the batch on the general path below (the index's rows:
+      // the delta merged first)
+      if (has_delta) {
+        if ((rc = consolidate(e))) return rc;
+        return search_core(e, h_qoff, nq, d_q, P, keys, d_keys_out, s);
+      }
     }
   }
   // Query offsets are the same on every call of one plan or stream: copy them only when they
@@ -1030,7 +1195,11 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   const int64_t R = e->nrows;
   int64_t max_frames = 0;
   for (int32_t i = 0; i < nq; i++) max_frames = std::max<int64_t>(max_frames, qo[i + 1] - qo[i]);
-  const bool vote = sc.coefs == 1 && C > 0 && R > 0 && max_frames < 16384;  // packed scores exact below 16384 frames
+  const bool vote = sc.coefs == 1 && C > 0 && R_all > 0 && max_frames < 16384;  // packed scores exact below 16384 frames
+  if (!vote && has_delta) {  // (the general path reads the sorted rows)
+    if ((rc = consolidate(e))) return rc;
+    return search_core(e, h_qoff, nq, d_q, P, keys, d_keys_out, s);
+  }
   // the vote path needs only the zeroing; the scan path the frames' boxes too
   HIPCHK(e, launch_prep_boxes(d_q, vote ? 0 : nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
 
@@ -1064,7 +1233,12 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       memcpy(keys.data(), e->vres_pin.as<char>() + sizeof(VoteMeta), sizeof(unsigned long long) * nq);
     if (e->dbg_vote) fprintf(stderr, "[tfp] vote: nq %d Qp %d C %d ku %d kp %d ok %d\n", nq, Qp, C, hm.ku, hm.kp, hm.ok);
     if (hm.ok) return TFP_OK;
-    // a count above fp16's exact range or a key outside the vote range: the scan path below
+    // a count above fp16's exact range or a key outside the vote range: the scan path below (over
+    // the sorted rows: the delta merged into them first)
+    if (has_delta) {
+      if ((rc = consolidate(e))) return rc;
+      return search_core(e, h_qoff, nq, d_q, P, keys, d_keys_out, s);
+    }
     HIPCHK(e, launch_prep_boxes(d_q, nf, sc, e->boxes.as<FrameBox>(), d_mask, nzero, s));
   }
   for (int pass = 0;; pass++) {
@@ -1139,11 +1313,30 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   }
 }
 
-// The index column of a tie-break key (-1: none).
+// The index column of a tie-break key (-1: none). Without an override the key is the clip's rank
+// among all live uuids: a main column's, or with a delta (ranks at[j] + j, ascending) either a delta
+// column's or main column k - #{delta ranks below k}.
 int32_t col_of_key(const tfp_engine* e, int32_t k) {
-  if (e->key_identity) return k >= 0 && (size_t)k < e->col_clip.size() ? k : -1;
+  if (e->key_identity) {
+    const int32_t Cm = (int32_t)e->col_clip.size(), D = (int32_t)e->delta_clip.size();
+    if (k < 0 || k >= Cm + D) return -1;
+    int32_t lo = 0, hi = D;  // first delta j with rank >= k
+    while (lo < hi) {
+      const int32_t mid = (lo + hi) >> 1;
+      if (e->delta_at[mid] + mid < k) lo = mid + 1; else hi = mid;
+    }
+    if (lo < D && e->delta_at[lo] + lo == k) return e->delta_col0 + lo;
+    return k - lo;
+  }
   auto it = e->key_col.find(k);
   return it == e->key_col.end() ? -1 : it->second;
+}
+
+// The clip of an index column (-1: none): a main column or a delta column.
+int32_t clip_of_col(const tfp_engine* e, int32_t col) {
+  if (col >= 0 && (size_t)col < e->col_clip.size()) return e->col_clip[col];
+  const int32_t j = col - e->delta_col0;
+  return j >= 0 && (size_t)j < e->delta_clip.size() ? e->delta_clip[j] : -1;
 }
 
 void fill_results(tfp_engine* e, const std::vector<unsigned long long>& keys, const int64_t* qoff, int32_t nq,
@@ -1155,9 +1348,8 @@ void fill_results(tfp_engine* e, const std::vector<unsigned long long>& keys, co
     r.clip_id = -1;
     const unsigned long long k = keys[i];
     if (!k) continue;
-    const int32_t col = col_of_key(e, (int32_t)(uint32_t)(k & 0xffffffffu));
-    if (col < 0) continue;
-    const int32_t clip = e->col_clip[col];
+    const int32_t clip = clip_of_col(e, col_of_key(e, (int32_t)(uint32_t)(k & 0xffffffffu)));
+    if (clip < 0) continue;
     r.found = 1;
     r.match_count = (int32_t)(k >> 32);
     r.clip_id = clip;
@@ -1210,6 +1402,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
   e->wide.no_spec = getenv("TFP_WIDE_SYNC") != nullptr;
   if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
+  if (const char* v = getenv("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;
@@ -1533,6 +1726,10 @@ int tfp_index_clear(tfp_engine* e) {
   e->removed_built = false;
   e->live_rows = 0;
   e->col_clip.clear();
+  e->delta_clip.clear();
+  e->delta_at.clear();
+  e->delta_col0 = 0;
+  e->delta_rows = 0;
   e->dirty = true;
   return TFP_OK;
 }
@@ -1564,6 +1761,14 @@ int tfp_index_build_stats(tfp_engine* e, int64_t* full_builds, int64_t* merges) 
   return TFP_OK;
 }
 
+int tfp_index_delta_stats(tfp_engine* e, int64_t* delta_updates, int32_t* delta_clips) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (delta_updates) *delta_updates = e->n_delta_updates;
+  if (delta_clips) *delta_clips = (int32_t)e->delta_clip.size();
+  return TFP_OK;
+}
+
 int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {
   if (!e || n < 0 || (n && !keys)) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
@@ -1575,9 +1780,9 @@ int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {
 int tfp_index_uuid_of_key(tfp_engine* e, int32_t key, char* uuid, int32_t len) {
   if (!e || !uuid || len <= 0) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
-  const int32_t col = col_of_key(e, key);
-  if (col < 0) return fail(e, TFP_E_NOENT, "no clip with key %d", key);
-  snprintf(uuid, len, "%s", e->clips[e->col_clip[col]].uuid.c_str());
+  const int32_t clip = clip_of_col(e, col_of_key(e, key));
+  if (clip < 0) return fail(e, TFP_E_NOENT, "no clip with key %d", key);
+  snprintf(uuid, len, "%s", e->clips[clip].uuid.c_str());
   return TFP_OK;
 }
 

@@ -26,6 +26,7 @@
 
 #include "tfp_index.hpp"
 #include "tfp_kernels.hpp"
+#include "tfp_math.hpp"
 
 namespace tfp {
 namespace {
@@ -325,6 +326,81 @@ void MergeScratch::release() {
   cap_pos = 0;
   cap_tiles = 0;
   tmp_bytes = 0;
+}
+
+// ---- index delta --------------------------------------------------------------------------
+
+namespace {
+
+__global__ void key_boxes_kernel(double tole, int64_t* __restrict__ kbox) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= kKeyRange) return;
+  const double freq = (double)(t - kKeyOffset);
+  kbox[2 * t] = fmt6_bound(freq - tole);
+  kbox[2 * t + 1] = fmt6_bound(freq + tole);
+}
+
+// One block per delta clip: its rows' keys as LDS flags, then one atomicOr per (key, clip).
+__global__ __launch_bounds__(256) void delta_bits_kernel(const DeltaClip* __restrict__ dc, const int32_t* __restrict__ st_m1,
+                                                         const int64_t* __restrict__ kbox, int32_t kspan, int32_t W,
+                                                         uint32_t* __restrict__ bits) {
+  __shared__ uint32_t flags[kKeyRange / 32];
+  const DeltaClip d = dc[blockIdx.x];
+  for (int i = threadIdx.x; i < kKeyRange / 32; i += blockDim.x) flags[i] = 0u;
+  __syncthreads();
+  for (int32_t r = threadIdx.x; r < d.n; r += blockDim.x) {
+    const int32_t m1 = st_m1[d.off + r];
+    if (m1 == INT32_MIN) continue;  // NULL max1: never in a box
+    const int64_t kc = (m1 >= 0 ? (int64_t)m1 : (int64_t)m1 - 999999) / 1000000;  // floor(m1 / 10^6)
+    for (int64_t k = kc - kspan; k <= kc + kspan; k++) {
+      const int64_t t = k + kKeyOffset;
+      if (t < 0 || t >= kKeyRange) continue;
+      if ((int64_t)m1 >= kbox[2 * t] && (int64_t)m1 <= kbox[2 * t + 1]) atomicOr(&flags[t >> 5], 1u << (t & 31));
+    }
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < kKeyRange; t += blockDim.x)
+    if ((flags[t >> 5] >> (t & 31)) & 1u) atomicOr(&bits[(int64_t)t * W + (d.col >> 5)], 1u << (d.col & 31));
+}
+
+__global__ void delta_tiekey_kernel(const int32_t* __restrict__ at, int32_t nd, int32_t main_cols, int32_t col0, int32_t ncols,
+                                    int32_t* __restrict__ tiekey) {
+  for (int32_t c = blockIdx.x * blockDim.x + threadIdx.x; c < ncols; c += gridDim.x * blockDim.x) {
+    int32_t v = 0;
+    if (c < main_cols) {
+      int32_t lo = 0, hi = nd;  // #{j : at[j] <= c} (at ascending)
+      while (lo < hi) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (at[mid] <= c) lo = mid + 1; else hi = mid;
+      }
+      v = c + lo;
+    } else if (c >= col0 && c - col0 < nd) {
+      v = at[c - col0] + (c - col0);
+    }
+    tiekey[c] = v;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_key_boxes(double tole, int64_t* d_kbox, hipStream_t s) {
+  hipLaunchKernelGGL(key_boxes_kernel, dim3(kKeyRange / 64), dim3(64), 0, s, tole, d_kbox);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_bits(const DeltaClip* d_dc, int32_t nd, const int32_t* st_m1, const int64_t* d_kbox, int32_t kspan,
+                             int32_t W, uint32_t* bits, hipStream_t s) {
+  if (nd <= 0) return hipSuccess;
+  hipLaunchKernelGGL(delta_bits_kernel, dim3((unsigned)nd), dim3(256), 0, s, d_dc, st_m1, d_kbox, kspan, W, bits);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_tiekey(const int32_t* d_at, int32_t nd, int32_t main_cols, int32_t col0, int32_t ncols,
+                               int32_t* tiekey, hipStream_t s) {
+  if (ncols <= 0) return hipSuccess;
+  hipLaunchKernelGGL(delta_tiekey_kernel, dim3((unsigned)std::min<int64_t>(1024, (ncols + 255) / 256)), dim3(256), 0, s, d_at,
+                     nd, main_cols, col0, ncols, tiekey);
+  return hipGetLastError();
 }
 
 }  // namespace tfp

@@ -53,4 +53,28 @@ hipError_t launch_key_bits_insert(const uint32_t* src, uint32_t* dst, int32_t W,
 hipError_t launch_key_bits_add(const int64_t* d_rng_all, const int32_t* m1s, const int32_t* nm1, const int32_t* ncol,
                                int64_t n, int32_t W, uint32_t* bits, hipStream_t s);
 
+// ---- index delta (round 4) ---------------------------------------------------------------
+// The clips enrolled since the last build, searched beside the main index by the coefs = 1 vote
+// paths without merging their rows into it (an enrolment then costs its own rows, not a pass over
+// the DB). Their columns follow the main index's, from the next multiple of 1024 (the vote GEMM
+// breaks ties inside a 1024-column chunk by position, so a chunk must hold main or delta columns
+// only, each in uuid order); their key-presence bits are set from their staged rows directly.
+struct DeltaClip {
+  int64_t off;  // first staged row
+  int32_t n;    // staged rows
+  int32_t col;  // its column
+};
+// kbox[2 t], kbox[2 t + 1] = the "%f" box of key t - kKeyOffset at tolerance tole, in micro-units
+// (the bounds key_ranges_all_kernel searches the sorted index with).
+hipError_t launch_key_boxes(double tole, int64_t* d_kbox, hipStream_t s);
+// Sets bit (key, column) for every delta clip and every key whose box (d_kbox) holds one of its
+// staged rows' max1 (NULL max1 never does); kspan >= ceil(tole) + 1 bounds the keys a row can be in.
+// The delta's columns must be clear (their words hold no main column).
+hipError_t launch_delta_bits(const DeltaClip* d_dc, int32_t nd, const int32_t* st_m1, const int64_t* d_kbox, int32_t kspan,
+                             int32_t W, uint32_t* bits, hipStream_t s);
+// Tie keys without an override: main column c -> c + #{j : at[j] <= c} (its rank among all live
+// uuids), delta column col0 + j -> at[j] + j, the columns between -> 0 (they never score).
+hipError_t launch_delta_tiekey(const int32_t* d_at, int32_t nd, int32_t main_cols, int32_t col0, int32_t ncols,
+                               int32_t* tiekey, hipStream_t s);
+
 }  // namespace tfp

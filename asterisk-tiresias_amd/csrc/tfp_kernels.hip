@@ -1653,15 +1653,16 @@ __global__ __launch_bounds__(256) void build_B_kernel(const uint32_t* __restrict
   }
 }
 
-// Pattern-class path: every clip's pattern from its flags, the greatest column per pattern
+// Pattern-class path: every clip's pattern from its flags, the greatest tie key per pattern (the
+// columns need not be in uuid order: an index delta's clips sit in columns after the main index's)
 // reduced in LDS per block first (many clips share a pattern; same-address global atomics
 // serialise, so only the first kClassMaxBlocks blocks take part), then merged with one global
 // atomicMax per pattern present in the block. Run by vote_gemm_regs_kernel's blocks when
 // meta->cls (its GEMM is not needed then): a launch of its own cost ~4.5 us per batch.
 constexpr int kClassMaxBlocks = 64;
 __device__ void class_max_block(int blk, int nblk, int32_t Ku, const uint32_t* __restrict__ mask,
-                                const uint32_t* __restrict__ bits, int32_t C, _Float16* __restrict__ Bt, int32_t* best,
-                                int32_t* kk) {
+                                const uint32_t* __restrict__ bits, int32_t C, const int32_t* __restrict__ tiekey,
+                                _Float16* __restrict__ Bt, int32_t* best, int32_t* kk) {
   for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x) best[i] = 0;
   if (threadIdx.x == 0) {  // the used keys, ascending (= columns kc)
     int n = 0;
@@ -1674,7 +1675,7 @@ __device__ void class_max_block(int blk, int nblk, int32_t Ku, const uint32_t* _
   for (int64_t c = (int64_t)blk * blockDim.x + threadIdx.x; c < C; c += (int64_t)nblk * blockDim.x) {
     uint32_t pat = 0;
     for (int k = 0; k < Ku; k++) pat |= ((bits[(int64_t)kk[k] * W + (c >> 5)] >> (c & 31)) & 1u) << k;
-    if (pat) atomicMax(&best[pat], (int32_t)c + 1);
+    if (pat) atomicMax(&best[pat], tiekey[c] + 1);  // the pattern's greatest tie key (uuid order), + 1
   }
   __syncthreads();
   for (int i = threadIdx.x; i < (1 << kClassKuMax); i += blockDim.x)
@@ -1688,8 +1689,8 @@ hipError_t launch_build_B(const uint32_t* d_mask, const uint32_t* d_bits, int32_
 }
 
 // Pattern-class path: one wave per query, lanes over the patterns present; score = the query's
-// counts (A, exact in fp16) summed over the pattern's keys; key = score << 32 | tiekey of the
-// pattern's greatest column, max over patterns with a non-zero score.
+// counts (A, exact in fp16) summed over the pattern's keys; key = score << 32 | the pattern's
+// greatest tie key, max over patterns with a non-zero score.
 // The vote's last step, one wave per query: the pattern-class vote (meta->cls), or for the GEMM
 // path the max of the query's per-chunk keys (one launch for both: the path is known only on the
 // device).
@@ -1730,7 +1731,7 @@ __global__ __launch_bounds__(256) void class_vote_kernel(const _Float16* __restr
 #pragma unroll
     for (int k = 0; k < kClassKuMax; k++) score += (P >> k) & 1 ? (uint32_t)cnt[k] : 0u;
     if (!score) continue;
-    const unsigned long long key = ((unsigned long long)score << 32) | (unsigned)tiekey[c1 - 1];
+    const unsigned long long key = ((unsigned long long)score << 32) | (unsigned)(c1 - 1);  // (c1 = tie key + 1)
     mine = key > mine ? key : mine;
   }
 #pragma unroll
@@ -1979,7 +1980,7 @@ __global__ __launch_bounds__(256) void vote_gemm_regs_kernel(const _Float16* __r
     __shared__ int32_t ckk[kClassKuMax];
     const int blk = blockIdx.y * gridDim.x + blockIdx.x;
     const int nblk = min((int)(gridDim.x * gridDim.y), min(kClassMaxBlocks, (C + 255) / 256));
-    if (blk < nblk) class_max_block(blk, nblk, meta->ku, mask, bits, C, Bt, cbest, ckk);
+    if (blk < nblk) class_max_block(blk, nblk, meta->ku, mask, bits, C, tiekey, Bt, cbest, ckk);
     return;
   }
   if (!meta->ok || (Kp > 32 && Kp <= 128)) return;

@@ -77,6 +77,7 @@ _SIGS = {
     "tfp_index_commit": (C.c_int, [P]),
     "tfp_index_build_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "tfp_index_set_tiebreak": (C.c_int, [P, P, C.c_int32]),
+    "tfp_index_delta_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_search": (C.c_int, [P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_pcm_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, C.POINTER(SearchParams), P]),

@@ -196,6 +196,12 @@ class Engine:
         self._chk(lib().tfp_index_build_stats(self._h, C.byref(f), C.byref(m)))
         return f.value, m.value
 
+    def index_delta_stats(self):
+        """(delta updates so far, clips in the index delta now)."""
+        u, c = C.c_int64(), C.c_int32()
+        self._chk(lib().tfp_index_delta_stats(self._h, C.byref(u), C.byref(c)))
+        return u.value, c.value
+
     def set_tiebreak(self, keys):
         keys = np.ascontiguousarray(keys, np.int32)
         self._chk(lib().tfp_index_set_tiebreak(self._h, keys.ctypes.data, len(keys)))

@@ -181,6 +181,14 @@ int tfp_index_commit(tfp_engine* eng);
 /* How the index was brought up to date so far: full sorts and incremental merges (new in round 3;
  * either pointer may be NULL). */
 int tfp_index_build_stats(tfp_engine* eng, int64_t* full_builds, int64_t* merges);
+/* Index delta (new in round 4): up to 512 clips enrolled since the last merge are searched beside
+ * the sorted index by the coefs = 1 paths (the dialplan's, application_handler.c:180) without a
+ * merge: an enrolment then costs its own rows, as the reference's INSERT into its B-tree does
+ * (fp_handler.c:559-571, :745-753). The delta is merged when it outgrows that, when a clip of the
+ * sorted index is removed, or before a search that reads the sorted rows (coefs = 2, a tolerance
+ * above 8, a row-scan fallback); results are unchanged either way. TFP_INDEX_DELTA=0 at engine
+ * creation turns it off. Stats: delta updates so far and the clips in the delta now. */
+int tfp_index_delta_stats(tfp_engine* eng, int64_t* delta_updates, int32_t* delta_clips);
 /* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
  * this engine's uuids). keys[clip_id] must order like the uuids across all shards and be
  * distinct over live clips. A clip added after this call has no key: the next search (or

@@ -9,6 +9,10 @@ batch-1 small path, coefs = 2 general path) and must equal the oracle over the l
 (count(*) DESC, ties to the greatest audio_uuid, :367-374) and an engine that rebuilds fully
 (TFP_INDEX_FULL=1); the merge count proves no full sort ran.
 
+Each test runs twice: with the index delta (round 4, the default: clips enrolled since the last
+merge searched beside the sorted index by the coefs = 1 paths, merged before a coefs = 2 search or a
+removal of an indexed clip) and with TFP_INDEX_DELTA=0 (every update a merge).
+
 Also the staging compaction's failure path (advisor finding, round 2): an allocation failure
 inside compact_staging must leave every clip's rows readable and the next build correct."""
 import os
@@ -69,7 +73,8 @@ def _frames(tfp_lib, qdb):
     return fr
 
 
-def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
+@pytest.mark.parametrize("delta", ["1", "0"])
+def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle, delta):
     rng = np.random.default_rng(31)
     n, nclips = 8000 * 10, 420
     nf = (n + HOP - 1) // HOP
@@ -90,7 +95,7 @@ def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
     qoff = np.arange(len(qpcm) + 1, dtype=np.int64) * nfq
     frames = _frames(tfp_lib, qdb)
 
-    inc = tfp_lib.Engine(0)
+    inc = _engine_with(tfp_lib, {"TFP_INDEX_DELTA": delta})
     full = _engine_with(tfp_lib, {"TFP_INDEX_FULL": "1"})
     mir = Mirror()
     engines = (inc, full)
@@ -113,6 +118,13 @@ def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
         del mir.rows[u]
 
     def check(step):
+        # batch-1 (small path) on the first queries, first: with the delta, before the coefs = 2
+        # search below merges it
+        p = tfp_lib.params(1, 0.001)
+        exp = mir.search(oracle, qdb[:6 * nfq, 0], qdb[:6 * nfq, 1], qoff[:7], p)
+        for i in range(6):
+            r, _ = inc.search(frames[qoff[i]:qoff[i + 1]], p)
+            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
         found = 0
         for p in (tfp_lib.params(1, 0.001), tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05)):
             exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
@@ -122,12 +134,6 @@ def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
                 got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
                 assert got == exp, (step, p.coefs, p.tolerance, [i for i in range(len(exp)) if got[i] != exp[i]][:5])
                 assert all(f == nfq for f in fcs)
-        # batch-1 (small path) on the first queries
-        p = tfp_lib.params(1, 0.001)
-        exp = mir.search(oracle, qdb[:6 * nfq, 0], qdb[:6 * nfq, 1], qoff[:7], p)
-        for i in range(6):
-            r, _ = inc.search(frames[qoff[i]:qoff[i + 1]], p)
-            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
         return found
 
     add(list(range(300)))
@@ -163,7 +169,11 @@ def test_incremental_updates_equal_oracle_and_full_build(tfp_lib, oracle):
             check("stream of adds %d" % c)
     assert check("final") > 10
     fb, merges = inc.index_build_stats()
-    assert fb == 1 and merges == steps, (fb, merges, steps)   # no full sort after the first build
+    if delta == "0":
+        assert fb == 1 and merges == steps, (fb, merges, steps)   # no full sort after the first build
+    else:  # updates went to the delta, merged by the coefs = 2 searches and the removals
+        nd, _ = inc.index_delta_stats()
+        assert fb == 1 and nd >= 10 and 1 <= merges <= steps, (fb, merges, nd, steps)
     assert full.index_build_stats()[1] == 0
     for e in engines:
         assert e.index_stats() == (sum(len(r[0]) for r in mir.rows.values()), len(mir.rows))
@@ -217,7 +227,8 @@ def test_compaction_failure_leaves_index_intact(tfp_lib, oracle):
     eng.close()
 
 
-def test_key_bits_carried_across_merges(tfp_lib, oracle):
+@pytest.mark.parametrize("delta", ["0", "1"])
+def test_key_bits_carried_across_merges(tfp_lib, oracle, delta):
     """The small path's key bitsets are carried across single-clip merges (a zero column at each
     breakpoint, then the new rows' bits; tfp_index.hip key_bits_*), and rebuilt where the row width
     changes (384 -> 385 clips: 12 -> 16 words) or a clip was removed. Every step's batch-1 searches
@@ -235,7 +246,7 @@ def test_key_bits_carried_across_merges(tfp_lib, oracle):
     uu[385] = "00000000-0000-4000-8000-000000000001"  # sorts first
     uu[386] = "ffffffff-ffff-4fff-bfff-fffffffffffe"  # sorts last
     data = [rows_of() for _ in range(400)]
-    eng = tfp_lib.Engine(0)
+    eng = _engine_with(tfp_lib, {"TFP_INDEX_DELTA": delta})
     mir = Mirror()
     p = tfp_lib.params(1, 0.3)
 
@@ -271,12 +282,17 @@ def test_key_bits_carried_across_merges(tfp_lib, oracle):
             found += check(c, [int(x) for x in rng.integers(0, 380, 2)] + ([c] if c != "remove" else [8]))
         assert found > 20
         fb, merges = eng.index_build_stats()
-        assert fb == 1 and merges == 16, (fb, merges)
+        if delta == "0":
+            assert fb == 1 and merges == 16, (fb, merges)
+        else:  # every add a delta update; the removal of an indexed clip merged the delta once
+            nd, _ = eng.index_delta_stats()
+            assert fb == 1 and merges == 1 and nd == 15, (fb, merges, nd)
     finally:
         eng.close()
 
 
-def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle):
+@pytest.mark.parametrize("delta", ["0", "1"])
+def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle, delta):
     """Updates that only add take the engine's host fast path (no pass over every clip; the
     column map from the new uuids' insertion points, csrc/tfp_engine.cpp live_order) and merge every
     staged row with the rows that cannot match (NULL max1: the reference's max1 >= ... never holds
@@ -304,7 +320,7 @@ def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle):
     m1[::2] = tfp_lib.NULL_MICRO
     data[201] = (m1, data[201][1])
     data[202] = (np.full(nrow, tfp_lib.NULL_MICRO, np.int32), data[202][1])
-    eng = tfp_lib.Engine(0)
+    eng = _engine_with(tfp_lib, {"TFP_INDEX_DELTA": delta})
     mir = Mirror()
     params = (tfp_lib.params(1, 0.3), tfp_lib.params(2, 0.05))
 
@@ -331,6 +347,23 @@ def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle):
             assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
         return found
 
+    def check_delta(step, sources):  # coefs = 1 only (batch and batch-1): served with the delta
+        q = []
+        for c in sources:
+            m1, m2 = data[c]
+            sel = rng.integers(0, nrow, 40)
+            q.append(np.stack([m1[sel] / 1e6 + 0.001, m2[sel] / 1e6], axis=1))
+        qdb = np.concatenate(q)
+        qoff = np.arange(len(sources) + 1, dtype=np.int64) * 40
+        fr = _frames(tfp_lib, qdb)
+        p = params[0]
+        exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+        for i in range(len(sources)):
+            r, _ = eng.search(fr[qoff[i]:qoff[i + 1]], p)
+            assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, i)
+        res, _ = eng.search_batch(fr, qoff, p)
+        assert [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res] == exp, step
+
     def add(cs):
         for c in cs:
             eng.index_add(uu[c], *data[c])
@@ -352,10 +385,18 @@ def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle):
                 eng.index_add(uu[extra], *data[extra])
                 eng.index_remove(uu[extra])
             eng.index_commit()
-            found += check(name, [int(x) for x in rng.integers(4, 200, 2)] + [c for c in cs if c not in (200, 201, 202)])
+            srcs = [int(x) for x in rng.integers(4, 200, 2)] + [c for c in cs if c not in (200, 201, 202)]
+            if delta == "1":
+                check_delta(name, srcs)
+            found += check(name, srcs)
         assert found > 20
         fb, merges = eng.index_build_stats()
-        assert fb == 1 and merges == len(steps), (fb, merges)
+        if delta == "0":
+            assert fb == 1 and merges == len(steps), (fb, merges)
+        else:  # each step's adds a delta update, merged by that step's coefs = 2 search; the removal
+            # of an indexed clip (uu[3]) merges at once
+            nd, _ = eng.index_delta_stats()
+            assert fb == 1 and merges == len(steps) and nd == len(steps) - 1, (fb, merges, nd)
         assert eng.index_stats() == (sum(len(r[0]) for r in mir.rows.values()), len(mir.rows))
     finally:
         eng.close()
