@@ -7,7 +7,7 @@
 // the leader, takes every queued request that can share its search (same sample format, rate and
 // parameters: the same SQL, fp_handler.c:287-374) up to kMaxQueries queries, runs them as one
 // batch, hands every caller its own results and wakes them. Requests that arrive while a batch
-// runs form the next batch, led by one of their callers. No timer: a lone caller runs at once,
+// runs form the next batch, led by the oldest of their callers. No timer: a lone caller runs at once,
 // and the batches grow with the load. Per-call results are unchanged: a query's result depends
 // only on its own frames and the index ("an internal queue/batcher ... as long as
 // per-call results are unchanged").
@@ -25,7 +25,9 @@
 
 namespace tfp {
 
-// One caller's search: its queries as (host pointer, samples), and where its results go.
+// One caller's search: its queries as (host pointer, samples), and where its results go. The
+// caller sleeps on its own condition variable (state: 0 queued, 1 done, 2 lead the next batch), so
+// finishing a batch wakes exactly its callers and one next leader, not every waiting thread.
 struct SearchReq {
   std::vector<const void*> ptrs;
   std::vector<int64_t> lens;
@@ -34,7 +36,9 @@ struct SearchReq {
   tfp_search_params P{};
   tfp_result* out = nullptr;
   int rc = TFP_OK;
-  bool done = false;
+  std::mutex m;
+  std::condition_variable cv;
+  int state = 0;
 };
 
 // Two requests give the same SQL per query frame: tolerance < 0 is the default 0.001
@@ -57,26 +61,41 @@ class Coalescer {
   // sets every request's rc and results. Returns r->rc.
   template <class Exec>
   int submit(SearchReq* r, Exec&& exec) {
-    std::unique_lock<std::mutex> lk(m_);
-    calls_++;
-    q_.push_back(r);
-    while (!r->done) {
-      if (busy_) {
-        cv_.wait(lk);
-        continue;
-      }
-      busy_ = true;
-      std::vector<SearchReq*> batch;
-      take(&batch);
-      lk.unlock();
-      exec(batch);
-      lk.lock();
-      for (SearchReq* b : batch) b->done = true;
-      batches_++;
-      busy_ = false;
-      cv_.notify_all();
+    bool lead = false;
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      calls_++;
+      q_.push_back(r);
+      if (!busy_) busy_ = lead = true;
     }
-    return r->rc;
+    if (!lead && wait(r) == 1) return r->rc;
+    // the leader: batches until its own request is done, then hands the lead to the oldest waiter
+    for (;;) {
+      std::vector<SearchReq*> batch;
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        take(&batch);
+      }
+      exec(batch);
+      bool mine = false;
+      for (SearchReq* b : batch) {
+        if (b == r) {
+          mine = true;
+          continue;
+        }
+        set_state(b, 1);
+      }
+      SearchReq* next = nullptr;
+      {
+        std::lock_guard<std::mutex> lk(m_);
+        batches_++;
+        if (q_.empty()) busy_ = false;
+        else if (mine) next = q_.front();
+      }
+      if (!mine) continue;  // (its own request was not in this batch: the queue still holds it)
+      if (next) set_state(next, 2);
+      return r->rc;
+    }
   }
 
   void stats(int64_t* calls, int64_t* batches) {
@@ -102,8 +121,18 @@ class Coalescer {
     q_.swap(rest);
   }
 
+  static int wait(SearchReq* r) {
+    std::unique_lock<std::mutex> lk(r->m);
+    r->cv.wait(lk, [r] { return r->state != 0; });
+    return r->state;
+  }
+  static void set_state(SearchReq* r, int st) {
+    std::lock_guard<std::mutex> lk(r->m);
+    r->state = st;
+    r->cv.notify_one();
+  }
+
   std::mutex m_;
-  std::condition_variable cv_;
   std::vector<SearchReq*> q_;
   bool busy_ = false;
   int64_t calls_ = 0, batches_ = 0;

@@ -1234,6 +1234,12 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
     fprintf(stderr, "[tfp] fingerprint8k_kernel<%d>: %d blocks/CU (occupancy query %d), grid cap %d\n", kTile8k / 4,
             cfg->grid_cap_8k / cus, per, cfg->grid_cap_8k);
   }
+  // TFP_FP_BLOCKS_PER_CU (experiments): fewer resident workgroups per CU for the 8 kHz throughput
+  // kernel (1 = one wave per SIMD), to measure how its time scales with the waves per SIMD
+  if (const char* b = getenv("TFP_FP_BLOCKS_PER_CU")) {
+    const int n = atoi(b);
+    if (n > 0 && cus * n < cfg->grid_cap_8k) cfg->grid_cap_8k = cus * n;
+  }
   const char* g = getenv("TFP_GENERIC");
   cfg->force_generic = g && atoi(g);
   const char* rt = getenv("TFP_RARE_THR_LOG2");

@@ -654,8 +654,10 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
 
     hits = {}
     fb0, mg0 = eng.index_build_stats()
+    nd0, _ = eng.index_delta_stats()
     inc = run(eng, "engine")
     fb1, mg1 = eng.index_build_stats()
+    nd1, _ = eng.index_delta_stats()
     os.environ["TFP_INDEX_FULL"] = "1"
     try:
         full_eng = T.Engine(eng.device)
@@ -670,7 +672,9 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
     return {"workload": f"{n_add} x (tfp_index_add of one 30 s clip + batch-1 search of a 5 s excerpt of it, coefs 1, "
                         f"tolerance 0.45) on the {args.db_clips}-clip DB, host PCM",
             "p50_ms": float(np.percentile(inc, 50)), "max_ms": float(np.max(inc)), "samples_ms": inc,
-            "index_updates": {"merges": mg1 - mg0, "full_sorts": fb1 - fb0},
+            "index_updates": {"delta_updates": nd1 - nd0, "merges": mg1 - mg0, "full_sorts": fb1 - fb0,
+                              "how": "each add a delta update (the clip's rows beside the sorted index, tfp_index_delta_stats); "
+                                     "the closing removals merge the delta once"},
             "new_clip_won": hits,
             "new_clips": "full-scale white noise, uuids above the DB's: only a new clip's rows lie in the query's "
                          "key box (see enrol_latency)",
