@@ -182,9 +182,25 @@ static struct ast_json* record(sqlite3_stmt* st)
 		case SQLITE_FLOAT:
 			v = ast_json_real_create(sqlite3_column_double(st, i));
 			break;
-		case SQLITE_TEXT:
-			v = ast_json_string_create((const char*)sqlite3_column_text(st, i));
+		case SQLITE_TEXT: {
+			/* db_ctx_handler.c:311-333: text that loads as JSON keeps the loaded array / object /
+			 * string, anything else is the text as a string */
+			const char* t = (const char*)sqlite3_column_text(st, i);
+			if(t == NULL) {
+				v = ast_json_null();
+				break;
+			}
+			v = ast_json_load_string(t, NULL);
+			if(v != NULL && ast_json_typeof(v) != AST_JSON_ARRAY && ast_json_typeof(v) != AST_JSON_OBJECT &&
+					ast_json_typeof(v) != AST_JSON_STRING) {
+				ast_json_unref(v);
+				v = NULL;
+			}
+			if(v == NULL) {
+				v = ast_json_string_create(t);
+			}
 			break;
+		}
 		default:
 			v = ast_json_null();
 			break;

@@ -5,6 +5,12 @@
 #include <stddef.h>
 #include <stdint.h>
 struct ast_json;
+enum ast_json_type { AST_JSON_OBJECT, AST_JSON_ARRAY, AST_JSON_STRING, AST_JSON_INTEGER, AST_JSON_REAL, AST_JSON_TRUE,
+                     AST_JSON_FALSE, AST_JSON_NULL };
+struct ast_json_error;
+/* jansson's json_loads(input, 0, ...) as Asterisk calls it: an array or object at the top, else NULL */
+struct ast_json* ast_json_load_string(const char* input, struct ast_json_error* error);
+enum ast_json_type ast_json_typeof(const struct ast_json* value);
 struct ast_json* ast_json_object_create(void);
 struct ast_json* ast_json_array_create(void);
 struct ast_json* ast_json_null(void);

@@ -108,13 +108,120 @@ void ast_json_unref(struct ast_json* v) {
   free(v->s);
   free(v);
 }
+/* ast_json_load_string: a small JSON reader (objects, arrays, strings with the common escapes,
+ * numbers, true / false / null); as jansson with flags 0, only an array or object at the top. */
+static const char* jws(const char* p) {
+  while (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r') p++;
+  return p;
+}
+static struct ast_json* jparse(const char** pp);
+static char* jstr(const char** pp) {
+  const char* p = *pp + 1;
+  char* out = malloc(strlen(p) + 1);
+  size_t n = 0;
+  while (*p && *p != '"') {
+    if (*p == '\\') {
+      p++;
+      switch (*p) {
+        case 'n': out[n++] = '\n'; break;
+        case 't': out[n++] = '\t'; break;
+        case '"': case '\\': case '/': out[n++] = *p; break;
+        default: free(out); return NULL;
+      }
+      p++;
+    } else {
+      out[n++] = *p++;
+    }
+  }
+  if (*p != '"') { free(out); return NULL; }
+  out[n] = 0;
+  *pp = p + 1;
+  return out;
+}
+static struct ast_json* jparse(const char** pp) {
+  const char* p = jws(*pp);
+  struct ast_json* j = NULL;
+  if (*p == '{' || *p == '[') {
+    const int obj = *p == '{';
+    j = jnew(obj ? J_OBJ : J_ARR);
+    p = jws(p + 1);
+    if (*p == (obj ? '}' : ']')) { *pp = p + 1; return j; }
+    for (;;) {
+      char* k = NULL;
+      struct ast_json* v;
+      if (obj) {
+        if (*p != '"' || !(k = jstr(&p))) break;
+        p = jws(p);
+        if (*p != ':') { free(k); break; }
+        p++;
+      }
+      if (!(v = jparse(&p))) { free(k); break; }
+      jpush(j, k, v);
+      p = jws(p);
+      if (*p == ',') { p = jws(p + 1); continue; }
+      if (*p == (obj ? '}' : ']')) { *pp = p + 1; return j; }
+      break;
+    }
+    ast_json_unref(j);
+    return NULL;
+  }
+  if (*p == '"') {
+    char* s = jstr(&p);
+    if (!s) return NULL;
+    j = jnew(J_STR);
+    j->s = s;
+  } else if (!strncmp(p, "true", 4) || !strncmp(p, "false", 5) || !strncmp(p, "null", 4)) {
+    j = *p == 'n' ? jnew(J_NULL) : ast_json_integer_create(*p == 't');
+    p += *p == 'f' ? 5 : 4;
+  } else {
+    char* e;
+    const double d = strtod(p, &e);
+    if (e == p) return NULL;
+    j = ast_json_real_create(d);
+    p = e;
+  }
+  *pp = p;
+  return j;
+}
+struct ast_json* ast_json_load_string(const char* input, struct ast_json_error* error) {
+  const char* p;
+  struct ast_json* j;
+  (void)error;
+  if (!input) return NULL;
+  p = jws(input);
+  if (*p != '{' && *p != '[') return NULL;
+  j = jparse(&p);
+  if (j && *jws(p) != 0) { ast_json_unref(j); return NULL; }
+  return j;
+}
+enum ast_json_type ast_json_typeof(const struct ast_json* v) {
+  switch (v->type) {
+    case J_OBJ: return AST_JSON_OBJECT;
+    case J_ARR: return AST_JSON_ARRAY;
+    case J_STR: return AST_JSON_STRING;
+    case J_INT: return AST_JSON_INTEGER;
+    case J_REAL: return AST_JSON_REAL;
+    default: return AST_JSON_NULL;
+  }
+}
+
 static void jprint(const struct ast_json* j) {
   int i;
   if (!j) { printf("null"); return; }
   switch (j->type) {
     case J_INT: printf("%jd", j->i); break;
     case J_REAL: printf("%.17g", j->d); break;
-    case J_STR: printf("\"%s\"", j->s); break;
+    case J_STR: {
+      const char* c;
+      putchar('"');
+      for (c = j->s; *c; c++) {
+        if (*c == '"' || *c == '\\') putchar('\\');
+        if (*c == '\n') { printf("\\n"); continue; }
+        putchar(*c);
+      }
+      putchar('"');
+      break;
+    }
     case J_NULL: printf("null"); break;
     case J_ARR:
       printf("[");

@@ -182,3 +182,20 @@ def test_hash_and_uuid(driver, tmp_path):
     us = [uuid.UUID(o["uuid"]) for o in out[2:]]
     assert all(u.version == 4 and u.variant == uuid.RFC_4122 for u in us) and us[0] != us[1]
     assert all(str(u) == o["uuid"] for u, o in zip(us, out[2:]))
+
+
+def test_json_shaped_text_reads_back_as_the_reference_does(driver, tmp_path):
+    """db_ctx_get_record (db_ctx_handler.c:311-333) loads every TEXT column with
+    ast_json_load_string (jansson json_loads, flags 0: an array or object at the top) and keeps an
+    array / object / string result, else the text as a string. A context whose name and directory
+    are JSON text come back in the listings as the parsed values; other text, a JSON string literal
+    included, comes back as the text itself."""
+    db = str(tmp_path / "j.db")
+    out = run(driver, db, "init", "ctx", '{"a": [1, "x"]}', '["d1", "d2"]', "ctx", '"quoted"', "plain dir",
+              "ctx", "[1, 2", "{}", "lists", "term")
+    ctx = [o for o in out if "context_lists" in o][0]["context_lists"]
+    byname = {json.dumps(c["name"], sort_keys=True): c for c in ctx}
+    assert set(byname) == {json.dumps({"a": [1, "x"]}, sort_keys=True), json.dumps('"quoted"'), json.dumps("[1, 2")}
+    assert byname[json.dumps({"a": [1, "x"]}, sort_keys=True)]["directory"] == ["d1", "d2"]
+    assert byname[json.dumps('"quoted"')]["directory"] == "plain dir"
+    assert byname[json.dumps("[1, 2")]["directory"] == {}
