@@ -99,6 +99,11 @@ struct LdsTables {
   LogfEntry logf[16];
   LogfEntry logf2[kLogf2Entries];  // (invc, y0) for aubio_log10_frexp (tfp_log.hpp)
   int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
+  // frame-pair filterbank jobs per pattern and segment (12-wave workgroups read them per double
+  // pass): bin offset in a pair row, band-sum index, 0 where the segment starts a job (else 1)
+  alignas(16) int32_t fb_boff[16][4];
+  alignas(16) int32_t fb_sidx[16][4];
+  alignas(16) float fb_k[16][4];
   union {
     alignas(16) float ms_w[kMsLds];                  // slot schedule (fingerprint_kernel, fingerprint8k_kernel<1>)
     alignas(16) float fbw[kFbSteps * kFbPatterns];  // frame-pair schedule (fingerprint8k_kernel<4>)
@@ -153,6 +158,32 @@ static_assert(2 * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride8 && 48 + 260 <
 static_assert(2 * kFbRow <= 2 * 4 * kFrameStride8 && 2 * kFbRowBins <= kFbRow && kWaveFrames * kFbNf <= kWaveFrames * kLogStride,
               "frame-pair rows");
 static_assert(kFbSegs == 4, "fb_seg");
+// The throughput kernel's workgroup: TFP_FP8_BLOCK_WAVES waves (4, or 12 = one workgroup of three
+// waves per SIMD). At 12 waves a wave's LDS is cut to fit 160 KiB: its transposes run in two
+// rounds of two frames through two padded squares (WaveLds8P; the same LDS reads and writes,
+// issued per half wave), and the band sums are kept compact (kFbNf per row).
+#ifndef TFP_FP8_BLOCK_WAVES
+#define TFP_FP8_BLOCK_WAVES 4
+#endif
+#ifndef TFP_FP8_WAVES
+#define TFP_FP8_WAVES TFP_FP_WAVES
+#endif
+constexpr int kBW8 = TFP_FP8_BLOCK_WAVES;
+constexpr bool kHalfSq = kBW8 > 4;
+static_assert(kBW8 == 4 || kBW8 == 8 || kBW8 == 12, "8 kHz workgroup");
+struct WaveLds8P {
+  union {
+    cf scratch[2][kFrameStride8];
+    alignas(16) int16_t pcm[5 * kHopStride];
+  };
+  alignas(16) float xeven[2 * kFbRow];
+  float logs[kWaveFrames * kFbNf];
+};
+static_assert(2 * 5 * kHopStride <= sizeof(cf) * 2 * kFrameStride8 && 2 * kFbRow <= 2 * 2 * kFrameStride8 &&
+                  2 * kFbNf * 7 + 68 <= 2 * kFrameStride8,
+              "half-square scratch: PCM, the odd pass's |X| rows, the tail's products");
+template <int kPasses>
+constexpr int fp8_block_waves() { return kPasses >= 2 ? kBW8 : kBlockWaves; }
 constexpr int fb_seg(int s) { return s < kFbSegStart[1] ? 0 : s < kFbSegStart[2] ? 1 : s < kFbSegStart[3] ? 2 : 3; }
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
@@ -722,7 +753,7 @@ __device__ __forceinline__ void load_w(const float* __restrict__ w, float4 (&wv)
 // kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
 // small batches: 4x the waves on a short query, a quarter of the per-wave latency).
 template <int kPasses>
-__global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_kernel(
+__global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP_FP8_WAVES : TFP_FP_WAVES) void fingerprint8k_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
@@ -735,8 +766,13 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const uint64_t t_entry = __builtin_amdgcn_s_memtime();
 #endif
   const uint32_t rare_m1 = __builtin_bit_cast(uint32_t, rare_thr) - 1u;  // 2^-98 (tests may raise it)
+  // filterbank weights: the frame-pair schedule (throughput) or the slot schedule (small tiles)
+  constexpr bool kPairFb = kPasses >= 2;
+  constexpr int kBW = fp8_block_waves<kPasses>();
+  constexpr bool kHalf = kPairFb && kHalfSq;
+  using WaveT = std::conditional_t<kHalf, WaveLds8P, WaveLds8>;
   __shared__ __attribute__((aligned(16))) LdsTables S;
-  __shared__ __attribute__((aligned(16))) WaveLds8 WL[kBlockWaves];
+  __shared__ __attribute__((aligned(16))) WaveT WL[kBW];
   const int tid = threadIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lane = tid & 63, grp = lane >> 4, L = lane & 15;
@@ -802,7 +838,7 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   // (a two-pass distance measured no faster: the pass is bound by instruction issue, not by the
   // PCM loads).
   int4 pf[kChunkRounds];
-  int b = blockIdx.x * kBlockWaves + wave;
+  int b = blockIdx.x * kBW + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
   // n1 (k2) = 2i, 2i+1 are one conflict-free ds_read_b128 (16 lanes read 256 consecutive bytes)
@@ -811,42 +847,45 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   // Table staging: every global load below is issued before any LDS write (indices clamped,
   // writes predicated), so a block waits for one round trip instead of one per table: a small
   // launch is latency-bound.
-  static_assert(kBlockThreads == 256, "one entry per thread per table");
-  // filterbank weights: the frame-pair schedule (throughput) or the slot schedule (small tiles)
-  constexpr bool kPairFb = kPasses >= 2;
+  // The first 256 threads stage (one entry per thread per table); a 12-wave workgroup's others
+  // read clamped copies of the same entries and write nothing.
+  constexpr int kStage = 256;
+  const int ts = tid < kStage ? tid : kStage - 1;
+  const bool stager = tid < kStage;
   constexpr int kMsW = kPairFb ? kFbSteps * kFbPatterns : 16 * (LA + LB + LC);  // DspTables_fixed8k
   const float* const wsrc = kPairFb ? &T->fb_w[0][0][0] : T->ms_w;
-  const int wL = (tid >> 1) & 15, wn1 = 2 * (tid >> 5) + (tid & 1);
+  const int wL = (ts >> 1) & 15, wn1 = 2 * (ts >> 5) + (ts & 1);
   const int wj = (32 * wn1 + 2 * wL + 256) & 511;
   const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
   // [k2][L] = (re w512^k, re w512^k', im w512^k, im w512^k'), k = L + 16 k2, k' = 256 - k (k2 < 8;
   // lane 0 at k2 = 0: k = 128): the pair layout of split_pair_sq
   const int tk2 = tid >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
-  const float* tws = (tid & 1) ? T->tw512_im : T->tw512_re;
+  const float* tws = (ts & 1) ? T->tw512_im : T->tw512_re;
   const float twk = tws[tkk], twk2 = tws[256 - tkk];
-  const int li = tid < 240 ? tid : 239, lk1 = 1 + li / 16, lL = li % 16;
+  const int li = ts < 240 ? ts : 239, lk1 = 1 + li / 16, lL = li % 16;
   const float ltre = T->lane_tw_re[lk1][lL], ltim = T->lane_tw_im[lk1][lL];
-  const int i10 = tid < 10 ? tid : 9;
+  const int i10 = ts < 10 ? ts : 9;
   const float w16re = T->tw256_re[16 * i10], w16im = T->tw256_im[16 * i10];
-  const int i80 = tid < kCoefs * kFilters ? tid : kCoefs * kFilters - 1;
+  const int i80 = ts < kCoefs * kFilters ? ts : kCoefs * kFilters - 1;
   const float dctv = (&T->dct[0][0])[i80];
-  const int i48 = tid < 48 ? tid : 47;
+  const int i48 = ts < 48 ? ts : 47;
   const int msf = (&T->ms_filter[0][0])[i48], mss = (&T->ms_start[0][0])[i48];
-  const int i3 = tid < 3 ? tid : 2;
+  const int i3 = ts < 3 ? ts : 2;
   const int msl = T->ms_len[i3], mso = T->ms_woff[i3];
-  const LogfEntry lge = logf_table()[tid & 15];
-  float mw[(kMsW + kBlockThreads - 1) / kBlockThreads];
+  const LogfEntry lge = logf_table()[ts & 15];
+  float mw[(kMsW + kStage - 1) / kStage];
 #pragma unroll
-  for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
-    const int idx = tid + kBlockThreads * r;
+  for (int r = 0; r < (kMsW + kStage - 1) / kStage; r++) {
+    const int idx = ts + kStage * r;
     mw[r] = wsrc[idx < kMsW ? idx : kMsW - 1];
   }
   const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
   // the first pass's PCM after the table loads (loads complete in order, so the tables' waits
   // would otherwise include the PCM's: a batch-1 query's is read across PCIe)
   fetch(cur, 0, b < ntiles, pf);
-  winr[tid] = cf{win0, win1};
-  twr[tid] = cf{twk, twk2};
+  if (stager) {
+    winr[tid] = cf{win0, win1};
+    twr[tid] = cf{twk, twk2};
   if (tid < 240) S.lane_tw[lk1 - 1][lL] = cf{ltre, ltim};
   if (tid < 10) S.w16[tid] = cf{w16re, w16im};
   if (tid < kCoefs * kFilters) (&S.dct[0][0])[tid] = dctv;
@@ -857,11 +896,18 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   if (tid < 3) { S.ms_len[tid] = msl; S.ms_woff[tid] = mso; }
   if (tid < 16) S.logf[tid] = lge;
   if (kPairFb && tid < kLogf2Entries) S.logf2[tid] = logf2_entry(tid, logf_table());
+    if (kPairFb && tid < 64) {
+      const int pl = tid >> 2, pk = tid & 3;
+      S.fb_boff[pl][pk] = 2 * (T->fb_bin[pl][pk] - kFbSegStart[pk]);
+      S.fb_sidx[pl][pk] = T->fb_filter[pl][pk];
+      S.fb_k[pl][pk] = T->fb_new[pl][pk] ? 0.f : 1.f;
+    }
   if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
 #pragma unroll
-  for (int r = 0; r < (kMsW + kBlockThreads - 1) / kBlockThreads; r++) {
-    const int idx = tid + kBlockThreads * r;
-    if (idx < kMsW) S.ms_w[idx] = 0.5f * mw[r];  // exact: w/2
+    for (int r = 0; r < (kMsW + kStage - 1) / kStage; r++) {
+      const int idx = tid + kStage * r;
+      if (idx < kMsW) S.ms_w[idx] = 0.5f * mw[r];  // exact: w/2
+    }
   }
   const unsigned long long empty_filters = __ballot(lane < kFilters && mlen == 0);  // (log of 0 + 2e-42)
   __syncthreads();
@@ -869,10 +915,10 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   const uint64_t t_staged = __builtin_amdgcn_s_memtime();
 #endif
 
-  WaveLds8& M = WL[wave];
-  cf* W = M.scratch[grp];
+  WaveT& M = WL[wave];
+  cf* W = M.scratch[kHalf ? (grp & 1) : grp];
   float* N = reinterpret_cast<float*>(W) + 48 * (grp & 1);  // |X| row (WaveLds8)
-  const int nwaves = gridDim.x * kBlockWaves;
+  const int nwaves = gridDim.x * kBW;
   const int maxbin = T->ms_maxbin;
   const int fA = S.ms_filter[0][L], fB = S.ms_filter[1][L], fC = S.ms_filter[2][L];
   const bool c_real = fC >= 0 && (fC == S.c_real[0] || fC == S.c_real[1]);
@@ -883,9 +929,12 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   for (int e = 0; e < 10; e++)
     w16r[e] = cf{T->tw256_re[16 * e], T->tw256_im[16 * e]};
   // inter-stage lane twiddles w256^(L k1) held in registers (30 VGPRs) instead of read per pass
-  cf ltw[15];
+  // (at 12-wave workgroups read per pass from LDS instead: the register budget is 168)
+  cf ltw[kHalf ? 1 : 15];
+  if constexpr (!kHalf) {
 #pragma unroll
-  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+    for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
+  }
   const float lempty = aubio_log10_fast(0.f, S.logf);  // log of an empty filter's clamped 0
   if constexpr (!kPairFb) {
     for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
@@ -898,20 +947,24 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
   // s reads the bins at fbb[k] + 2 s), where the job's raw sums go (frames 2 grp, 2 grp + 1 of
   // double pass 0: rows 4 grp, 4 grp + 2; double pass 1 one row on), and 0 where the segment
   // starts a job (acc = fma(acc, 0, p) = p; 1: acc + p).
-  const float* fbb[kFbSegs];
-  float* fbc[kFbSegs];
-  float fbk[kFbSegs];
+  constexpr int kFbS = kHalf ? 1 : kFbSegs;  // (12-wave workgroups: read per double pass)
+  const float* fbb[kFbS];
+  float* fbc[kFbS];
+  float fbk[kFbS];
   cf dctl, dct9;  // the DCT weights (rows 0, 1) of this lane's filter in the tail's log rounds
+  const float* const fbrow = (grp < 2 ? M.xeven : reinterpret_cast<const float*>(M.scratch)) + (grp & 1) * kFbRow;
+  float* const fblog = M.logs + 4 * grp * kFbNf;
   if constexpr (kPairFb) {
     const int lf = lane < kFbNf ? lane : lane - kFbNf, l9 = kFbNf - 4 + (lane & 3);
     dctl = cf{S.dct[0][lf], S.dct[1][lf]};
     dct9 = cf{S.dct[0][l9], S.dct[1][l9]};
-    const float* row = (grp < 2 ? M.xeven : reinterpret_cast<const float*>(M.scratch)) + (grp & 1) * kFbRow;
+    if constexpr (!kHalf) {
 #pragma unroll
-    for (int k = 0; k < kFbSegs; k++) {
-      fbb[k] = row + 2 * (T->fb_bin[L][k] - kFbSegStart[k]);
-      fbc[k] = M.logs + 4 * grp * kFbNf + T->fb_filter[L][k];
-      fbk[k] = T->fb_new[L][k] ? 0.f : 1.f;
+      for (int k = 0; k < kFbSegs; k++) {
+        fbb[k % kFbS] = fbrow + 2 * (T->fb_bin[L][k] - kFbSegStart[k]);
+        fbc[k % kFbS] = fblog + T->fb_filter[L][k];
+        fbk[k % kFbS] = T->fb_new[L][k] ? 0.f : 1.f;
+      }
     }
   }
 
@@ -964,17 +1017,37 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
       }
       dft16q(w16r, z, Y);
 #pragma unroll
-      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], kHalf ? S.lane_tw[k1 - 1][L + oz] : ltw[(k1 - 1) % (kHalf ? 1 : 15)]);
       wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
       TFP_STAMP(2);
+      if constexpr (kHalf) {  // frames 0, 1 then 2, 3 through the two squares
 #pragma unroll
-      for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
-      wave_sync();
+        for (int h = 0; h < 2; h++) {
+          if (h) wave_sync();  // the first round's reads are done before the second's writes
+          if ((grp >> 1) == h) {
 #pragma unroll
-      for (int n2 = 0; n2 < 16; n2 += 2) {
-        const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
-        z[n2] = cf{v.x, v.y};
-        z[n2 + 1] = cf{v.z, v.w};
+            for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
+          }
+          wave_sync();
+          if ((grp >> 1) == h) {
+#pragma unroll
+            for (int n2 = 0; n2 < 16; n2 += 2) {
+              const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
+              z[n2] = cf{v.x, v.y};
+              z[n2 + 1] = cf{v.z, v.w};
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
+        wave_sync();
+#pragma unroll
+        for (int n2 = 0; n2 < 16; n2 += 2) {
+          const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
+          z[n2] = cf{v.x, v.y};
+          z[n2 + 1] = cf{v.z, v.w};
+        }
       }
       dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       wave_sync();         // every lane has read its column of the square: W is free for |X|
@@ -1070,6 +1143,24 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
         auto pair_fb = [&](auto dp) {
           constexpr int doff = decltype(dp)::value * kFbNf;
           cf acc;
+          const float* jb[kFbSegs];
+          float* jc[kFbSegs];
+          float jk[kFbSegs];
+          if constexpr (kHalf) {
+            const int4 bo = *reinterpret_cast<const int4*>(&S.fb_boff[L][0] + oz);
+            const int4 si = *reinterpret_cast<const int4*>(&S.fb_sidx[L][0] + oz);
+            const float4 kk = *reinterpret_cast<const float4*>(&S.fb_k[L][0] + oz);
+            jb[0] = fbrow + bo.x; jb[1] = fbrow + bo.y; jb[2] = fbrow + bo.z; jb[3] = fbrow + bo.w;
+            jc[0] = fblog + si.x; jc[1] = fblog + si.y; jc[2] = fblog + si.z; jc[3] = fblog + si.w;
+            jk[0] = kk.x; jk[1] = kk.y; jk[2] = kk.z; jk[3] = kk.w;
+          } else {
+#pragma unroll
+            for (int k = 0; k < kFbSegs; k++) {
+              jb[k] = fbb[k % kFbS];
+              jc[k] = fbc[k % kFbS];
+              jk[k] = fbk[k % kFbS];
+            }
+          }
           // a step pair's weights: one ds_read_b64 each, whose halves the packed multiplies
           // broadcast with op_sel (a b128 of 4 steps made the compiler move the halves apart)
           const cf* const wfb = reinterpret_cast<const cf*>(S.fbw) + L + oz;
@@ -1077,16 +1168,16 @@ __global__ __launch_bounds__(kBlockThreads, TFP_FP_WAVES) void fingerprint8k_ker
           for (int st = 0; st < kFbSteps; st += 2) {
             const int k = fb_seg(st);
             const cf wv = wfb[(st >> 1) * kFbPatterns];
-            const f4v nv = *reinterpret_cast<const f4v*>(fbb[k] + 2 * st);
+            const f4v nv = *reinterpret_cast<const f4v*>(jb[k] + 2 * st);
             const cf p0 = cf{nv.x, nv.y} * cf{wv.x, wv.x};
             const cf p1 = cf{nv.z, nv.w} * cf{wv.y, wv.y};
             if (st == 0) acc = p0;
-            else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{fbk[k], fbk[k]}, p0);
+            else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{jk[k], jk[k]}, p0);
             else acc = acc + p0;
             acc = acc + p1;
             if (st + 2 == kFbSegStart[k + 1]) {
-              fbc[k][doff] = acc.x;
-              fbc[k][doff + 2 * kFbNf] = acc.y;
+              jc[k][doff] = acc.x;
+              jc[k][doff + 2 * kFbNf] = acc.y;
             }
           }
         };
@@ -1203,14 +1294,15 @@ bool DspTables_fixed8k(const DspTables& t) {
 // a block per SIMD; 160 KiB of LDS per CU). The query alone over-counted once the LDS shrank
 // below a third of the CU while the VGPRs still admitted two waves: a grid of 3 blocks per CU
 // ran its last third as a tail (0.71 vs 0.54 ms per C2 launch).
-static int resident_blocks(const void* k) {
+static int resident_blocks(const void* k, int waves = kBlockWaves) {
   int per = 0;
-  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, kBlockThreads, 0);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 64 * waves, 0);
   hipFuncAttributes a;
   if (hipFuncGetAttributes(&a, k) == hipSuccess) {
     const int vg = ((a.numRegs > 0 ? a.numRegs : 1) + 7) / 8 * 8;
-    int by_vgpr = 512 / vg;
+    int by_vgpr = 512 / vg;  // waves per SIMD
     if (by_vgpr > 8) by_vgpr = 8;
+    by_vgpr = by_vgpr * 4 / waves;  // workgroups per CU (a workgroup's waves spread over the 4 SIMDs)
     const int by_lds = a.sharedSizeBytes ? (int)((160 * 1024) / a.sharedSizeBytes) : 8;
     const int own = by_vgpr < by_lds ? by_vgpr : by_lds;
     if (per <= 0 || own < per) per = own;
@@ -1222,15 +1314,15 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
   int cus = 0;
   hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return e;
-  auto cap = [&](const void* k) { return cus * resident_blocks(k); };
-  cfg->grid_cap_8k = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>));
+  auto cap = [&](const void* k, int waves = kBlockWaves) { return cus * resident_blocks(k, waves); };
+  cfg->grid_cap_8k = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>), kBW8);
   cfg->grid_cap_8k_small = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<1>));
   cfg->grid_cap_generic = cap(reinterpret_cast<const void*>(fingerprint_kernel<int16_t>));
   cfg->grid_cap_f32 = cap(reinterpret_cast<const void*>(fingerprint_kernel<float>));
   if (getenv("TFP_DEBUG_OCC")) {
     int per = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>),
-                                                       kBlockThreads, 0);
+                                                       64 * kBW8, 0);
     fprintf(stderr, "[tfp] fingerprint8k_kernel<%d>: %d blocks/CU (occupancy query %d), grid cap %d\n", kTile8k / 4,
             cfg->grid_cap_8k / cus, per, cfg->grid_cap_8k);
   }
@@ -1258,14 +1350,15 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
   if (ntiles <= 0) return hipSuccess;
   const int cap = v8 ? (tile_frames == 4 ? cfg.grid_cap_8k_small : cfg.grid_cap_8k) : cfg.grid_cap_generic;
   if (cap <= 0) return hipErrorInvalidValue;
-  const int want = (ntiles + kBlockWaves - 1) / kBlockWaves;  // one tile per wave per step
+  const int bw = (v8 && tile_frames != 4) ? kBW8 : kBlockWaves;
+  const int want = (ntiles + bw - 1) / bw;  // one tile per wave per step
   const int grid = want < cap ? want : cap;
   if (v8) {
     if (tile_frames == 4) {  // fingerprint8k_kernel<1> finishes its own tail
       hipLaunchKernelGGL(fingerprint8k_kernel<1>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg, d_send,
                          d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx, single_ns);
     } else {
-      hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(kBlockThreads), 0, s, d_tables, d_pcm, d_sbeg,
+      hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(64 * kBW8), 0, s, d_tables, d_pcm, d_sbeg,
                          d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx, single_ns);
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
