@@ -2009,21 +2009,26 @@ int tfp_stream_reset(tfp_stream* st, int32_t ch) {
   return TFP_OK;
 }
 
-int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, tfp_result* out) {
-  if (!st || !pcm || T <= 0 || T > st->W || (P && !out)) return TFP_E_ARG;
+// One tick into a stream: the samples into the ring, then (match) the windows that are full after
+// it fingerprinted into d_db (frame values, 2 doubles per frame; nullptr: the engine's buffer) at
+// window i's frames [i F, (i + 1) F). act = their channels, in channel order. Caller holds e->mu.
+static int stream_tick(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, double* d_db,
+                       int64_t cap_frames, std::vector<int32_t>& act, int64_t* F_out, std::vector<int64_t>& fov) {
+  const bool match = P && valid_params(P);
   tfp_engine* e = st->eng;
-  std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
   int rc;
   // Windows to match after this tick: the channels whose history is full once it is in.
   const int64_t wpos = (st->wpos + T) % st->W;
-  std::vector<int32_t> act;
-  const bool match = P && valid_params(P);  // fp_handler.c:247-250: bad params -> NULL results
+  act.clear();
   if (match)
     for (int32_t c = 0; c < st->nch; c++)
       if (std::min<int64_t>(st->W, st->filled[c] + T) >= st->W) act.push_back(c);
   const int32_t na = (int32_t)act.size();
   const int64_t F = tfp_frame_count(st->W);
+  *F_out = F;
+  if (d_db && (int64_t)na * F > cap_frames) return fail(e, TFP_E_ARG, "stream tick: %d windows of %lld frames past %lld", na,
+                                                        (long long)F, (long long)cap_frames);
   const DspTables* Tb;
   bool fx = false;
   if ((rc = ensure_tables(e, st->sr, &Tb, &fx))) return rc;
@@ -2066,29 +2071,61 @@ int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_sea
   HIPCHK(e, hipGetLastError());
   st->wpos = wpos;
   for (auto& f : st->filled) f = std::min<int64_t>(st->W, f + T);
-  if (!P) return TFP_OK;
-  for (int32_t c = 0; c < st->nch; c++) {
-    memset(&out[c], 0, sizeof out[c]);
-    out[c].clip_id = -1;
-  }
-  if (!match || !na) return TFP_OK;  // full windows only
+  fov.assign(fo, fo + na + 1);  // (the pinned buffer is rewritten next tick)
+  if (!na) return TFP_OK;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (fo[na] + 1)));
-  HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
+  if (!d_db) HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (fo[na] + 1)));
   const int64_t* d_sb = reinterpret_cast<const int64_t*>(d + b_pcm);
   HIPCHK(e, launch_fingerprint(e->fpcfg, Tb, fx, tile, st->ring.as<int16_t>(), d_sb,
                                reinterpret_cast<const int64_t*>(d + b_pcm + b_sb),
                                reinterpret_cast<const int64_t*>(d + b_pcm + 2 * b_sb),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo),
                                reinterpret_cast<const int32_t*>(d + b_pcm + 2 * b_sb + b_fo + b_to), to[na], fo[na],
-                               e->micro.as<int32_t>(), e->db.as<double>(), e->stream,
+                               e->micro.as<int32_t>(), d_db ? d_db : e->db.as<double>(), e->stream,
                                P->coefs == 2 ? e->logfix : LogFix{}));
-  const std::vector<int64_t> fov(fo, fo + na + 1);  // (the pinned buffer is rewritten next tick)
+  return TFP_OK;
+}
+
+int tfp_stream_push(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, tfp_result* out) {
+  if (!st || !pcm || T <= 0 || T > st->W || (P && !out)) return TFP_E_ARG;
+  tfp_engine* e = st->eng;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  const bool match = P && valid_params(P);  // fp_handler.c:247-250: bad params -> NULL results
+  std::vector<int32_t> act;
+  std::vector<int64_t> fov;
+  int64_t F = 0;
+  int rc = stream_tick(st, pcm, T, P, nullptr, 0, act, &F, fov);
+  if (rc) return rc;
+  if (!P) return TFP_OK;
+  for (int32_t c = 0; c < st->nch; c++) {
+    memset(&out[c], 0, sizeof out[c]);
+    out[c].clip_id = -1;
+  }
+  const int32_t na = (int32_t)act.size();
+  if (!match || !na) return TFP_OK;  // full windows only
   std::vector<unsigned long long> keys;
   if ((rc = search_core(e, fov.data(), na, e->db.as<double>(), P, keys, nullptr, e->stream))) return rc;
   st->stage_pending = false;  // search_core waited for e->stream
   std::vector<tfp_result> res(na);
   fill_results(e, keys, fov.data(), na, res.data());
   for (int32_t i = 0; i < na; i++) out[act[i]] = res[i];
+  return TFP_OK;
+}
+
+int tfp_internal_stream_fp(tfp_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, double* d_db,
+                           int64_t cap_frames, int32_t* act, int32_t* nact, int64_t* frames_per_window) {
+  const bool match = P && valid_params(P);
+  if (!st || !pcm || T <= 0 || T > st->W || !nact || !frames_per_window || (match && (!d_db || !act))) return TFP_E_ARG;
+  tfp_engine* e = st->eng;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  std::vector<int32_t> a;
+  std::vector<int64_t> fov;
+  int rc = stream_tick(st, pcm, T, P, d_db, cap_frames, a, frames_per_window, fov);
+  if (rc) return rc;
+  HIPCHK(e, hipStreamSynchronize(e->stream));  // the values are read by other devices' streams next
+  st->stage_pending = false;
+  *nact = (int32_t)a.size();
+  if (match) std::copy(a.begin(), a.end(), act);
   return TFP_OK;
 }
 

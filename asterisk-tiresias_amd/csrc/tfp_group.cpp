@@ -14,9 +14,11 @@
 // queries [s·nq/N, (s+1)·nq/N) on its GPU, the frame values are exchanged device to device
 // (hipMemcpyPeerAsync over xGMI; a plain device copy when a device repeats), and every shard
 // searches the whole batch against its clips (tfp_search_q_device). Smaller batches (batch-1
-// latency) and stream ticks are fingerprinted by every shard itself: no exchange on the latency
-// path. Stream channels run on every shard's engine (the windows are fingerprinted per shard, a
-// few tens of microseconds of GPU time), each shard matching them against its clips.
+// latency) are fingerprinted by every shard itself: no exchange on the latency path. Stream
+// channels are split over the shards (channel c on shard c mod N): each shard keeps its channels'
+// rings and fingerprints their full windows, the windows' frame values are exchanged as for a
+// query-sharded batch, and every shard matches all of them against its clips. (TFP_GROUP_STREAM=
+// replicate: every shard runs every channel, no exchange; the round-3 form.)
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdlib.h>
@@ -53,7 +55,8 @@ struct ShardBufs {
   void* micro = nullptr;    // their stored values (unused by the search, written by the kernel)
   void* q = nullptr;        // the whole batch's frame values (2 doubles per frame)
   void* keys = nullptr;     // per-query keys
-  size_t b_pcm = 0, b_micro = 0, b_q = 0, b_keys = 0;
+  void* sfp = nullptr;      // split streams: this shard's channels' window values of the tick
+  size_t b_pcm = 0, b_micro = 0, b_q = 0, b_keys = 0, b_sfp = 0;
   hipStream_t stream = nullptr;
   hipEvent_t fp_done = nullptr;
   tfp_plan* plan = nullptr;  // this shard's share of the last batch shape (k queries of qn samples)
@@ -93,7 +96,7 @@ struct tfp_group {
     delete pool;
     for (size_t s = 0; s < bufs.size(); s++) {
       (void)hipSetDevice(dev[s]);
-      for (void* p : {bufs[s].pcm, bufs[s].micro, bufs[s].q, bufs[s].keys})
+      for (void* p : {bufs[s].pcm, bufs[s].micro, bufs[s].q, bufs[s].keys, bufs[s].sfp})
         if (p) (void)hipFree(p);
       if (bufs[s].fp_done) (void)hipEventDestroy(bufs[s].fp_done);
       tfp_plan_destroy(bufs[s].plan);
@@ -105,8 +108,15 @@ struct tfp_group {
 
 struct tfp_group_stream {
   tfp_group* g = nullptr;
-  std::vector<tfp_stream*> st;  // one per shard, every channel
+  std::vector<tfp_stream*> st;  // one per shard: every channel (replicated) or its own (split; null if none)
   int32_t nch = 0;
+  int64_t W = 0;
+  bool split = false;
+  std::vector<std::vector<int32_t>> chans;  // split: shard -> its channels (c mod N == s), ascending
+  std::vector<std::vector<int16_t>> tick;   // split: the shard's rows of the tick
+  std::vector<std::vector<int32_t>> act;    // split: the shard's windows of the tick (local channel indices)
+  std::vector<int32_t> nact;
+  std::vector<std::vector<unsigned long long>> keys;
   std::vector<std::vector<tfp_result>> res;
 };
 
@@ -661,10 +671,26 @@ int tfp_group_stream_create(tfp_group* g, int32_t nch, int32_t sr, int64_t W, tf
   std::lock_guard<std::recursive_mutex> lk(g->mu);
   *out = nullptr;
   tfp_group_stream* st = new tfp_group_stream();
+  const int n = (int)g->eng.size();
   st->g = g;
   st->nch = nch;
-  st->st.assign(g->eng.size(), nullptr);
-  const int rc = run_all(g, [&](int s) { return tfp_stream_create(g->eng[s], nch, sr, W, &st->st[s]); });
+  st->W = W;
+  const char* mode = getenv("TFP_GROUP_STREAM");
+  st->split = n > 1 && !(mode && !strcmp(mode, "replicate"));
+  st->st.assign(n, nullptr);
+  if (st->split) {
+    st->chans.assign(n, {});
+    for (int32_t c = 0; c < nch; c++) st->chans[c % n].push_back(c);
+    st->tick.assign(n, {});
+    st->act.assign(n, {});
+    st->nact.assign(n, 0);
+    st->keys.assign(n, {});
+    for (int s = 0; s < n; s++) st->act[s].assign(st->chans[s].size(), 0);
+  }
+  const int rc = run_all(g, [&](int s) {
+    if (!st->split) return tfp_stream_create(g->eng[s], nch, sr, W, &st->st[s]);
+    return st->chans[s].empty() ? TFP_OK : tfp_stream_create(g->eng[s], (int32_t)st->chans[s].size(), sr, W, &st->st[s]);
+  });
   if (rc) {
     for (auto* p : st->st) tfp_stream_destroy(p);
     delete st;
@@ -684,8 +710,87 @@ void tfp_group_stream_destroy(tfp_group_stream* st) {
 int tfp_group_stream_reset(tfp_group_stream* st, int32_t ch) {
   if (!st || ch >= st->nch) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(st->g->mu);
+  if (st->split) {
+    const int n = (int)st->g->eng.size();
+    if (ch >= 0) return tfp_stream_reset(st->st[ch % n], ch / n);  // channel c is local channel c / N of shard c mod N
+    return run_all(st->g, [&](int s) { return st->st[s] ? tfp_stream_reset(st->st[s], -1) : TFP_OK; });
+  }
   return run_all(st->g, [&](int s) { return tfp_stream_reset(st->st[s], ch); });
 }
+
+namespace {
+
+// A tick of a split-channel stream: (1) every shard pushes its channels' rows and fingerprints its
+// full windows into its sfp buffer; (2) every shard gathers all shards' window values in shard
+// order (hipMemcpyPeerAsync; a device copy when a device repeats) and matches them against its
+// clips; (3) per window, the greatest key over the shards.
+int split_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t T, const tfp_search_params* P, tfp_result* out) {
+  tfp_group* g = st->g;
+  const int n = (int)g->eng.size();
+  for (int s = 0; s < n; s++) {
+    const auto& ch = st->chans[s];
+    st->tick[s].resize(ch.size() * (size_t)T);
+    for (size_t j = 0; j < ch.size(); j++)
+      memcpy(st->tick[s].data() + j * T, pcm + (size_t)ch[j] * T, sizeof(int16_t) * (size_t)T);
+  }
+  const bool match = valid_params(P);
+  const int64_t F = tfp_frame_count(st->W);
+  int rc = run_all(g, [&](int s) -> int {
+    st->nact[s] = 0;
+    if (!st->st[s]) return TFP_OK;
+    ShardBufs& b = g->bufs[s];
+    if (hipSetDevice(g->dev[s]) != hipSuccess) return TFP_E_HIP;
+    const int64_t cap = (int64_t)st->chans[s].size() * F;
+    if (match && grow(&b.sfp, &b.b_sfp, sizeof(double) * 2 * (size_t)(cap + 1)) != hipSuccess) return TFP_E_NOMEM;
+    int64_t fw = 0;
+    return tfp_internal_stream_fp(st->st[s], st->tick[s].data(), T, match ? P : nullptr, (double*)b.sfp, cap,
+                                  st->act[s].data(), &st->nact[s], &fw);
+  });
+  if (rc || !P) return rc;
+  for (int32_t c = 0; c < st->nch; c++) {
+    memset(&out[c], 0, sizeof out[c]);
+    out[c].clip_id = -1;
+  }
+  std::vector<int32_t> base(n + 1, 0);
+  for (int s = 0; s < n; s++) base[s + 1] = base[s] + st->nact[s];
+  const int32_t na = base[n];
+  if (!match || !na) return TFP_OK;
+  std::vector<int64_t> qoff(na + 1);
+  for (int32_t i = 0; i <= na; i++) qoff[i] = F * i;
+  rc = run_all(g, [&](int s) -> int {
+    ShardBufs& b = g->bufs[s];
+    if (hipSetDevice(g->dev[s]) != hipSuccess) return TFP_E_HIP;
+    if (!b.stream && hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking) != hipSuccess) return TFP_E_HIP;
+    if (grow(&b.q, &b.b_q, sizeof(double) * 2 * (size_t)(na * F + 1)) != hipSuccess ||
+        grow(&b.keys, &b.b_keys, sizeof(unsigned long long) * (size_t)(na + 1)) != hipSuccess)
+      return TFP_E_NOMEM;
+    for (int o = 0; o < n; o++) {
+      if (!st->nact[o]) continue;
+      const size_t off = sizeof(double) * 2 * (size_t)(F * base[o]), bytes = sizeof(double) * 2 * (size_t)(F * st->nact[o]);
+      if (hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], g->bufs[o].sfp, g->dev[o], bytes, b.stream) != hipSuccess)
+        return TFP_E_HIP;
+    }
+    st->keys[s].resize(na);
+    int r = tfp_search_q_device(g->eng[s], (const double*)b.q, qoff.data(), na, P, (uint64_t*)b.keys, b.stream);
+    if (r) return r;
+    if (hipMemcpyAsync(st->keys[s].data(), b.keys, sizeof(unsigned long long) * na, hipMemcpyDeviceToHost, b.stream) !=
+            hipSuccess ||
+        hipStreamSynchronize(b.stream) != hipSuccess)
+      return TFP_E_HIP;
+    return TFP_OK;
+  });
+  if (rc) return rc;
+  for (int o = 0; o < n; o++)
+    for (int32_t j = 0; j < st->nact[o]; j++) {
+      const int32_t i = base[o] + j;
+      unsigned long long k = 0ull;
+      for (int s = 0; s < n; s++) k = std::max(k, st->keys[s][i]);
+      fill_from_key(g, k, (int32_t)F, &out[st->chans[o][st->act[o][j]]]);
+    }
+  return TFP_OK;
+}
+
+}  // namespace
 
 int tfp_group_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t tick, const tfp_search_params* P,
                           tfp_result* out) {
@@ -694,6 +799,7 @@ int tfp_group_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t tick
   std::lock_guard<std::recursive_mutex> lk(g->mu);
   int rc = P ? refresh_ranks(g) : TFP_OK;
   if (rc) return rc;
+  if (st->split) return split_stream_push(st, pcm, tick, P, out);
   rc = run_all(g, [&](int s) { return tfp_stream_push(st->st[s], pcm, tick, P, P ? st->res[s].data() : nullptr); });
   if (rc || !P) return rc;
   combine(g, st->res, st->nch, out);

@@ -31,5 +31,5 @@ for _ in range(reps):
     b.record(s)
     b.synchronize()
     ts.append(a.elapsed_time(b))
-print("fp C2 [%s]: median %.4f ms (min %.4f)" % (os.environ.get("TFP_FP_BLOCKS_PER_CU", "default"), float(np.median(ts)),
+print("fp C2 [%s %s]: median %.4f ms (min %.4f)" % (os.environ.get("TFP_FP_BLOCKS_PER_CU", "default"), os.path.basename(os.path.dirname(T.LIB_PATH)), float(np.median(ts)),
                                                 float(np.min(ts))), flush=True)

@@ -4,10 +4,12 @@ in one process, searched on all of them in parallel and combined on the host.
 On this one-GPU box the group is three engines on device 0 (the same code path as three GPUs,
 with device-to-device copies in place of xGMI peer copies). Every search — batch-1 (each shard
 fingerprints the queries), a batch (each shard's vote), a query-sharded batch of >= 64 queries per
-shard (fingerprint shares exchanged between shards) and coefs = 2 — and every stream tick must
-equal the single engine over the same clips and the oracle (count(*) DESC, ties to the greatest
+shard (fingerprint shares exchanged between shards) and coefs = 2 — and every stream tick (channels
+split over the shards, or replicated) must equal the single engine over the same clips and the oracle (count(*) DESC, ties to the greatest
 audio_uuid: src/fp_handler.c:367-374; clip-aligned shards: :353), including ties whose clips sit on
 different shards."""
+import os
+
 import numpy as np
 import pytest
 
@@ -128,31 +130,53 @@ def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
             assert r2[0] == r[0]
     t.close()
 
-    # live channels: every tick == the single engine's stream == the oracle on the window
-    nch, W, tick = 12, 24000, 160
-    span = W + 3 * tick
+    # live channels: every tick == the single engine's stream == the oracle on the window, with the
+    # channels split over the shards (13 channels: 5 / 4 / 4, the windows exchanged between shards)
+    # and replicated on every shard (TFP_GROUP_STREAM=replicate); a channel reset mid-way (its
+    # window not full again: no result, the others still matched), coefs = 2, invalid params
+    nch, W, tick = 13, 24000, 160
+    span = W + 4 * tick
     chs = [int(rng.integers(nsrc)) for _ in range(nch)]
     spcm = tfp_lib.synth_pcm(SEED_DB, chs, span, offsets=[256 * int(rng.integers(0, 100)) for _ in range(nch)])
     spcm[3] = tfp_lib.synth_pcm(SEED_Q + 5, [3], span)[0]
-    gs = tfp_lib.GroupStream(g, nch, W)
-    es = tfp_lib.Stream(e, nch, W)
-    for t in range(W // tick):
-        blk = np.ascontiguousarray(spcm[:, t * tick:(t + 1) * tick])
-        gs.push(blk)
-        es.push(blk)
-    p = tfp_lib.params(1, 0.001)
     nfw = (W + HOP - 1) // HOP
-    for t in range(3):
-        s0 = W + t * tick
-        blk = np.ascontiguousarray(spcm[:, s0:s0 + tick])
-        rg = gs.push(blk, p)
-        assert rg == es.push(blk, p)
-        _, wdb = oracle.fingerprint_batch(np.ascontiguousarray(spcm[:, s0 + tick - W:s0 + tick]).reshape(-1),
-                                          np.arange(nch + 1) * W, nthreads=16)
-        exp = _oracle_search(oracle, live, wdb[:, 0], wdb[:, 1], np.arange(nch + 1) * nfw, p)
-        assert [None if r is None else (r["audio_uuid"], r["match_count"]) for r in rg] == exp
-    gs.close()
-    es.close()
+    for mode in ("split", "replicate"):
+        os.environ["TFP_GROUP_STREAM"] = mode
+        try:
+            gs = tfp_lib.GroupStream(g, nch, W)
+        finally:
+            del os.environ["TFP_GROUP_STREAM"]
+        es = tfp_lib.Stream(e, nch, W)
+        for t in range(W // tick):
+            blk = np.ascontiguousarray(spcm[:, t * tick:(t + 1) * tick])
+            gs.push(blk)
+            es.push(blk)
+        for t, p in enumerate((tfp_lib.params(1, 0.001), tfp_lib.params(2, 0.05), tfp_lib.params(1, 0.45),
+                               tfp_lib.params(3, 0.001))):
+            s0 = W + t * tick
+            if t == 2:  # channel 7 (shard 1 of 3 when split) starts over
+                gs.reset(7)
+                es.reset(7)
+            blk = np.ascontiguousarray(spcm[:, s0:s0 + tick])
+            rg = gs.push(blk, p)
+            assert rg == es.push(blk, p), (mode, t)
+            if p.coefs == 3:  # invalid: every channel NULL (fp_handler.c:247-250)
+                assert rg == [None] * nch
+                continue
+            _, wdb = oracle.fingerprint_batch(np.ascontiguousarray(spcm[:, s0 + tick - W:s0 + tick]).reshape(-1),
+                                              np.arange(nch + 1) * W, nthreads=16)
+            exp = _oracle_search(oracle, live, wdb[:, 0], wdb[:, 1], np.arange(nch + 1) * nfw, p)
+            if t >= 2:
+                exp[7] = None
+            assert _pairs(rg) == exp, (mode, t)
+            assert all(r is None or r["frame_count"] == nfw for r in rg)
+            assert sum(x is not None for x in exp) >= 6
+        gs.reset()
+        es.reset()
+        blk = np.ascontiguousarray(spcm[:, :tick])
+        assert gs.push(blk, tfp_lib.params(1, 0.45)) == [None] * nch  # every window empty again
+        gs.close()
+        es.close()
     g.index_clear()
     assert g.index_stats() == (0, 0)
     g.close()
