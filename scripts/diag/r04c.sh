@@ -1,6 +1,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 W12=$GRAFT_REPO_ROOT/asterisk-tiresias_amd/abv/w12/libtiresias_fp.so
+(ldconfig -p | grep -i -E "aubio|fftw" ; ls /usr/lib/x86_64-linux-gnu | grep -i -E "aubio|fftw"; true) > gpurun_out/r04c_aubio_probe.txt 2>&1
 timeout -k 10 120 ./scripts/microbench/valu_issue > gpurun_out/r04c_valu.txt 2>&1 || exit 3
 for r in 1 2; do
   timeout -k 10 120 python scripts/diag/fp_c2.py >> gpurun_out/r04c_fpc2.txt 2>&1 || exit 4
