@@ -177,6 +177,15 @@ def test_group_of_three_equals_engine_and_oracle(tfp_lib, oracle):
         assert gs.push(blk, tfp_lib.params(1, 0.45)) == [None] * nch  # every window empty again
         gs.close()
         es.close()
+    # fewer channels than shards: shard 2 holds none (split)
+    gs, es = tfp_lib.GroupStream(g, 2, W), tfp_lib.Stream(e, 2, W)
+    for t in range(W // tick + 2):
+        blk = np.ascontiguousarray(spcm[:2, t * tick:(t + 1) * tick])
+        rg = gs.push(blk, tfp_lib.params(1, 0.45))
+        assert rg == es.push(blk, tfp_lib.params(1, 0.45))
+    assert rg[0] is not None
+    gs.close()
+    es.close()
     g.index_clear()
     assert g.index_stats() == (0, 0)
     g.close()
