@@ -77,14 +77,7 @@ class Coalescer {
         take(&batch);
       }
       exec(batch);
-      bool mine = false;
-      for (SearchReq* b : batch) {
-        if (b == r) {
-          mine = true;
-          continue;
-        }
-        set_state(b, 1);
-      }
+      const bool mine = std::find(batch.begin(), batch.end(), r) != batch.end();
       SearchReq* next = nullptr;
       {
         std::lock_guard<std::mutex> lk(m_);
@@ -92,8 +85,12 @@ class Coalescer {
         if (q_.empty()) busy_ = false;
         else if (mine) next = q_.front();
       }
-      if (!mine) continue;  // (its own request was not in this batch: the queue still holds it)
+      // the next batch starts first, then this batch's callers wake (a wake-up is a few us; 25 of
+      // them before the hand-off would idle the GPU for a whole batch-1 search)
       if (next) set_state(next, 2);
+      for (SearchReq* b : batch)
+        if (b != r) set_state(b, 1);
+      if (!mine) continue;  // (its own request was not in this batch: the queue still holds it)
       return r->rc;
     }
   }
