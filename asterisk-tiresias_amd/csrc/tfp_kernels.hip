@@ -859,7 +859,7 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   const float win0 = T->window_s[wj], win1 = T->window_s[wj + 1];
   // [k2][L] = (re w512^k, re w512^k', im w512^k, im w512^k'), k = L + 16 k2, k' = 256 - k (k2 < 8;
   // lane 0 at k2 = 0: k = 128): the pair layout of split_pair_sq
-  const int tk2 = tid >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
+  const int tk2 = ts >> 5, tkk = (wL == 0 && tk2 == 0) ? 128 : wL + 16 * tk2;
   const float* tws = (ts & 1) ? T->tw512_im : T->tw512_re;
   const float twk = tws[tkk], twk2 = tws[256 - tkk];
   const int li = ts < 240 ? ts : 239, lk1 = 1 + li / 16, lL = li % 16;
@@ -1325,6 +1325,14 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
                                                        64 * kBW8, 0);
     fprintf(stderr, "[tfp] fingerprint8k_kernel<%d>: %d blocks/CU (occupancy query %d), grid cap %d\n", kTile8k / 4,
             cfg->grid_cap_8k / cus, per, cfg->grid_cap_8k);
+    hipFuncAttributes fa;
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>)) == hipSuccess)
+      fprintf(stderr, "[tfp]   %d threads/block (max %d), %d VGPRs, %zu B LDS, %zu B scratch\n", 64 * kBW8,
+              fa.maxThreadsPerBlock, fa.numRegs, fa.sharedSizeBytes, fa.localSizeBytes);
+    int smem = 0, smem_optin = 0;
+    (void)hipDeviceGetAttribute(&smem, hipDeviceAttributeMaxSharedMemoryPerBlock, device);
+    (void)hipDeviceGetAttribute(&smem_optin, hipDeviceAttributeSharedMemPerBlockOptin, device);
+    fprintf(stderr, "[tfp]   device: %d B LDS per block (opt-in %d)\n", smem, smem_optin);
   }
   // TFP_FP_BLOCKS_PER_CU (experiments): fewer resident workgroups per CU for the 8 kHz throughput
   // kernel (1 = one wave per SIMD), to measure how its time scales with the waves per SIMD
@@ -1360,6 +1368,8 @@ hipError_t launch_fingerprint(const FpLaunchCfg& cfg, const DspTables* d_tables,
     } else {
       hipLaunchKernelGGL(fingerprint8k_kernel<kTile8k / 4>, dim3(grid), dim3(64 * kBW8), 0, s, d_tables, d_pcm, d_sbeg,
                          d_send, d_foff, d_toff, d_tclip, ntiles, d_micro, d_db, cfg.rare_thr, fx, single_ns);
+      // (each HIP call overwrites the last error: a failed launch must be caught before the next one)
+      if (const hipError_t le = hipGetLastError(); le != hipSuccess) return le;
       const int64_t nv = 2 * nframes;
       int64_t g = (nv + 255) / 256;
       if (g > 8192) g = 8192;

@@ -13,7 +13,7 @@ import tiresias_amd as T  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 dev = torch.device("cuda", 0)
-s = torch.cuda.current_stream()
+s = torch.cuda.Stream()  # a real stream: the null stream's handle (0) would send the launches to the engine's own
 eng = T.Engine(0)
 nclips, n = 1024, 8000 * 30
 pcm = torch.empty((nclips, n), dtype=torch.int16, device=dev)
