@@ -168,8 +168,11 @@ static_assert(kFbSegs == 4, "fb_seg");
 #ifndef TFP_FP8_WAVES
 #define TFP_FP8_WAVES TFP_FP_WAVES
 #endif
+#ifndef TFP_FP8_HALF_SQ
+#define TFP_FP8_HALF_SQ (TFP_FP8_BLOCK_WAVES > 4)
+#endif
 constexpr int kBW8 = TFP_FP8_BLOCK_WAVES;
-constexpr bool kHalfSq = kBW8 > 4;
+constexpr bool kHalfSq = TFP_FP8_HALF_SQ;
 static_assert(kBW8 == 4 || kBW8 == 8 || kBW8 == 12, "8 kHz workgroup");
 struct WaveLds8P {
   union {
