@@ -38,7 +38,10 @@ __device__ __forceinline__ cf2 split_pair_sq(cf2 y, cf2 p, cf2 WX, cf2 WY) {
 // Both bins: n = m + med3(bits(rp), 0, 1) + med3(bits(rm), 0, 1) on the bit patterns (med3 = 1 iff
 // the float is > 0, not a negative NaN). One asm block: the compiler's own form of the clamps is a
 // compare, a select and an add-with-carry per bin, and every separate asm block gets a hazard
-// s_nop before its VALU consumer; here the only consumers are the caller's ds_writes.
+// s_nop before its VALU consumer; here the only consumers are the caller's ds_writes. a0 is
+// early-clobber too: it is written before the last instruction reads m1 (sharing a register
+// with m1, which the allocator chose under the 12-wave build's 168-VGPR budget, it gave bin
+// 256 - k the bits of bin k).
 __device__ __forceinline__ void step_tuckerman(uint32_t m0, uint32_t m1, cf2 rp, cf2 rm, float& n0, float& n1) {
   uint32_t a0, a1, t0, t1, u0, u1;
   asm("v_med3_i32 %2, %6, 0, 1\n\t"
@@ -47,7 +50,7 @@ __device__ __forceinline__ void step_tuckerman(uint32_t m0, uint32_t m1, cf2 rp,
       "v_med3_i32 %5, %9, 0, 1\n\t"
       "v_add3_u32 %0, %10, %2, %3\n\t"
       "v_add3_u32 %1, %11, %4, %5"
-      : "=v"(a0), "=v"(a1), "=&v"(t0), "=&v"(t1), "=&v"(u0), "=&v"(u1)
+      : "=&v"(a0), "=v"(a1), "=&v"(t0), "=&v"(t1), "=&v"(u0), "=&v"(u1)
       : "v"(rp.x), "v"(rp.y), "v"(rm.x), "v"(rm.y), "v"(m0), "v"(m1));
   n0 = __builtin_bit_cast(float, a0);
   n1 = __builtin_bit_cast(float, a1);
