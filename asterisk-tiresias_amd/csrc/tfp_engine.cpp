@@ -1044,7 +1044,23 @@ int delta_update(tfp_engine* e) {
   e->ncols = ncols;
   e->key_col = std::move(key_col);
   e->key_identity = !ovr;
-  // key bits: the delta columns cleared and set again when the layout stands, else rebuilt later
+  // key bits: the first delta after a build widens the rows (the delta's columns start at a
+  // multiple of 1024): the main columns' words move to the wider rows in one 2-D device copy
+  // (~13 MB at 100k clips) instead of a rebuild from the index rows (46 ms at 100k clips)
+  if (e->key_bits_valid && D > 0 && e->key_bits_cols != ncols && e->key_bits_cols <= col0) {
+    const int32_t Wo = key_bits_words(e->key_bits_cols), Wn = key_bits_words(ncols);
+    if (Wn > Wo) {
+      const size_t nb = sizeof(uint32_t) * (size_t)kKeyRange * Wn;
+      HIPCHK(e, e->key_bits_b.reserve(nb));
+      HIPCHK(e, hipMemsetAsync(e->key_bits_b.p, 0, nb, s));
+      HIPCHK(e, hipMemcpy2DAsync(e->key_bits_b.p, sizeof(uint32_t) * Wn, e->key_bits.p, sizeof(uint32_t) * Wo,
+                                 sizeof(uint32_t) * Wo, kKeyRange, hipMemcpyDeviceToDevice, s));
+      std::swap(e->key_bits.p, e->key_bits_b.p);
+      std::swap(e->key_bits.bytes, e->key_bits_b.bytes);
+    }
+    e->key_bits_cols = ncols;
+  }
+  // the delta columns cleared and set again when the layout stands, else rebuilt later
   if (e->key_bits_valid && e->key_bits_cols == ncols && D > 0) {
     const int32_t W = key_bits_words(ncols);
     HIPCHK(e, hipMemset2DAsync(e->key_bits.as<uint32_t>() + col0 / 32, sizeof(uint32_t) * W, 0,
