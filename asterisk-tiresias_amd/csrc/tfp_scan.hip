@@ -1142,6 +1142,10 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
   }
 }
 
+#ifndef TFP_CLIP_KEYPRE
+#define TFP_CLIP_KEYPRE 1  // the used keys' segment constants once per wave (wide_clips_kernel)
+#endif
+constexpr bool kClipKeyPre = TFP_CLIP_KEYPRE;
 #ifndef TFP_CLIP_OCC
 #define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 #endif
@@ -1190,6 +1194,26 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
   auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
     cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
   };
+  // The chunk's used keys' segment constants, one key per lane, loaded once per wave instead of
+  // once per window and key (three dependent loads ahead of every key's groups): the window loop
+  // reads them with readlane. More than 64 used keys: loaded per window and key as below.
+  const bool kpre = kClipKeyPre && nu <= 64;
+  int32_t ksb = 0, kse = 0, kfb = 0, kfe = 0, knbk = 1, kshf = 0, kl2 = 0, ku2 = 0, ktoff = 0;
+  if (kpre && lane < nu) {
+    const int kq = uk[lane];
+    ksb = sg[2 * kq];
+    kse = sg[2 * kq + 1];
+    kfb = sg[2 * (kq | kKeyRange)];
+    kfe = sg[2 * (kq | kKeyRange) + 1];
+    if (kse > ksb) {
+      const int lg = dir_log2(kse - ksb);
+      knbk = 1 << lg;
+      kl2 = L2s[ksb];
+      ku2 = U2s[ksb];
+      kshf = dir_shift(max((int64_t)L2s[kse - 1] - kl2, (int64_t)U2s[kse - 1] - ku2), lg);
+      ktoff = doff[(int64_t)ch * kKeyRange + kq];
+    }
+  }
   for (int32_t w = w0; w < w1; w++) {
     const int32_t c0 = kWin * w;
 #pragma unroll
@@ -1211,16 +1235,31 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
         const int32_t g1 = __builtin_amdgcn_readlane(gb, sl);
         int32_t g = __builtin_amdgcn_readlane(ga, sl);
         // the key's window segment and its frames without a max2 window (as in wide_groups)
-        sb = sg[2 * k];
-        se = sg[2 * k + 1];
-        const int32_t fb = sg[2 * (k | kKeyRange)], fe = sg[2 * (k | kKeyRange) + 1];
+        int32_t fb, fe;
+        if (kpre) {  // (u0 == 0: the key's slot is lane sl)
+          sb = __builtin_amdgcn_readlane(ksb, sl);
+          se = __builtin_amdgcn_readlane(kse, sl);
+          fb = __builtin_amdgcn_readlane(kfb, sl);
+          fe = __builtin_amdgcn_readlane(kfe, sl);
+        } else {
+          sb = sg[2 * k];
+          se = sg[2 * k + 1];
+          fb = sg[2 * (k | kKeyRange)];
+          fe = sg[2 * (k | kKeyRange) + 1];
+        }
         base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
         fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
         if (se <= sb) {  // no frame of the key has a max2 window: every group scores the rest
           for (; g < g1; g++) add((int32_t)(cv.g_key[g] & kColMask), fcnt);
           continue;
         }
-        {
+        if (kpre) {
+          nbk = __builtin_amdgcn_readlane(knbk, sl);
+          l2min = __builtin_amdgcn_readlane(kl2, sl);
+          u2min = __builtin_amdgcn_readlane(ku2, sl);
+          shf = __builtin_amdgcn_readlane(kshf, sl);
+          TL = dtab + __builtin_amdgcn_readlane(ktoff, sl);
+        } else {
           const int lg = dir_log2(se - sb);
           nbk = 1 << lg;
           l2min = L2s[sb];

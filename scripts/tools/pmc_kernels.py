@@ -15,7 +15,7 @@ per = collections.defaultdict(lambda: collections.defaultdict(lambda: collection
 for d in sys.argv[1:]:
     for path in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(path)):
-            k = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "")).replace("tfp::", "")
+            k = re.sub(r"\(.*", "", r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")).replace("tfp::", "")
             per[k][r["Counter_Name"]][(path, r["Dispatch_Id"])] += float(r["Counter_Value"])
 out = {}
 for k, cs in per.items():
