@@ -1146,6 +1146,10 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 #define TFP_CLIP_KEYPRE 1  // the used keys' segment constants once per wave (wide_clips_kernel)
 #endif
 constexpr bool kClipKeyPre = TFP_CLIP_KEYPRE;
+#ifndef TFP_CLIP_WINPRE
+#define TFP_CLIP_WINPRE 0  // each key's next-window group range requested a window ahead
+#endif
+constexpr bool kClipWinPre = TFP_CLIP_WINPRE;
 #ifndef TFP_CLIP_OCC
 #define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 #endif
@@ -1198,16 +1202,21 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
   // once per window and key (three dependent loads ahead of every key's groups): the window loop
   // reads them with readlane. More than 64 used keys: loaded per window and key as below.
   const bool kpre = kClipKeyPre && nu <= 64;
-  int32_t ksb = 0, kse = 0, kfb = 0, kfe = 0, knbk = 1, kshf = 0, kl2 = 0, ku2 = 0, ktoff = 0;
+  const bool wpre = kpre && kClipWinPre;
+  int32_t ksb = 0, kse = 0, kfb = 0, kfe = 0, kshf = 0, kl2 = 0, ku2 = 0, ktoff = 0;
+  int32_t kga = 0, kgb = 0, kgbn = 0;  // each key's group range in the current / next window
   if (kpre && lane < nu) {
     const int kq = uk[lane];
+    if (kClipWinPre && w0 < w1) {
+      kga = kdir[(int64_t)kq * (nwin + 1) + w0];
+      kgb = kdir[(int64_t)kq * (nwin + 1) + w0 + 1];
+    }
     ksb = sg[2 * kq];
     kse = sg[2 * kq + 1];
     kfb = sg[2 * (kq | kKeyRange)];
     kfe = sg[2 * (kq | kKeyRange) + 1];
     if (kse > ksb) {
       const int lg = dir_log2(kse - ksb);
-      knbk = 1 << lg;
       kl2 = L2s[ksb];
       ku2 = U2s[ksb];
       kshf = dir_shift(max((int64_t)L2s[kse - 1] - kl2, (int64_t)U2s[kse - 1] - ku2), lg);
@@ -1222,7 +1231,12 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
     for (int32_t u0 = 0; u0 < nu; u0 += 64) {
       // the used keys with groups in this window, 64 keys a step
       int32_t kk = 0, ga = 0, gb = 0;
-      if (u0 + lane < nu) {
+      if (wpre) {  // this window's group ranges came with the previous one; the next one's is requested now
+        kk = lane < nu ? uk[lane] : 0;
+        ga = kga;
+        gb = kgb;
+        if (lane < nu && w + 1 < w1) kgbn = kdir[(int64_t)kk * (nwin + 1) + w + 2];
+      } else if (u0 + lane < nu) {
         kk = uk[u0 + lane];
         ga = kdir[(int64_t)kk * (nwin + 1) + w];
         gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
@@ -1254,7 +1268,7 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
           continue;
         }
         if (kpre) {
-          nbk = __builtin_amdgcn_readlane(knbk, sl);
+          nbk = 1 << dir_log2(se - sb);
           l2min = __builtin_amdgcn_readlane(kl2, sl);
           u2min = __builtin_amdgcn_readlane(ku2, sl);
           shf = __builtin_amdgcn_readlane(kshf, sl);
@@ -1354,6 +1368,10 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
           g += nG;
         }
       }
+    }
+    if (wpre) {
+      kga = kgb;
+      kgb = kgbn;
     }
     // the window's clips: each query's best (count << 32 | tie key)
     const int32_t tk = c0 + lane < C && lane < kWin ? tiekey[c0 + lane] : 0;
