@@ -1150,6 +1150,10 @@ constexpr bool kClipKeyPre = TFP_CLIP_KEYPRE;
 #define TFP_CLIP_WINPRE 0  // each key's next-window group range requested a window ahead
 #endif
 constexpr bool kClipWinPre = TFP_CLIP_WINPRE;
+#ifndef TFP_CLIP_GRPPRE
+#define TFP_CLIP_GRPPRE 0  // the next batch of groups' records requested before this batch's searches
+#endif
+constexpr bool kClipGrpPre = TFP_CLIP_GRPPRE;
 #ifndef TFP_CLIP_OCC
 #define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 #endif
@@ -1281,16 +1285,40 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
           shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
           TL = dtab + doff[(int64_t)ch * kKeyRange + k];
         }
+        // (kClipGrpPre: the next batch's group records are requested before this batch's searches;
+        // raw values, so nothing waits for them until the next iteration)
+        bool have = false;
+        int32_t npb0 = 0, nr0 = 0, nr1 = 0, nkey = 0;
         while (g < g1) {
           const int32_t left = g1 - g;
-          const int32_t pb0 = cv.g_beg[g];
-          int32_t pj0 = 0, pj1 = INT32_MAX, colj = 0;
-          if (lane < left) {
-            pj0 = cv.g_beg[g + lane] - pb0;
-            pj1 = cv.g_beg[g + lane + 1] - pb0;
-            colj = (int32_t)(cv.g_key[g + lane] & kColMask);
+          int32_t pb0, pj0 = 0, pj1 = INT32_MAX, colj = 0;
+          if (have) {
+            pb0 = npb0;
+            if (lane < left) {
+              pj0 = nr0 - pb0;
+              pj1 = nr1 - pb0;
+              colj = nkey;
+            }
+            have = false;
+          } else {
+            pb0 = cv.g_beg[g];
+            if (lane < left) {
+              pj0 = cv.g_beg[g + lane] - pb0;
+              pj1 = cv.g_beg[g + lane + 1] - pb0;
+              colj = (int32_t)(cv.g_key[g + lane] & kColMask);
+            }
           }
           const int nG = __popcll(__ballot(lane < left && pj1 <= 64));
+          if (kClipGrpPre && nG > 0 && g + nG < g1) {
+            const int32_t gn = g + nG;
+            npb0 = cv.g_beg[gn];
+            if (lane < g1 - gn) {
+              nr0 = cv.g_beg[gn + lane];
+              nr1 = cv.g_beg[gn + lane + 1];
+              nkey = (int32_t)(cv.g_key[gn + lane] & kColMask);
+            }
+            have = true;
+          }
           if (nG == 0) {  // one group with more than 64 items: 64 at a time, runs merged across the steps
             const int32_t pn = __shfl(pj1, 0, 64);
             uint32_t cnt = fcnt;
