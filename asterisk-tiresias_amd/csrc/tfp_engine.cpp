@@ -1265,6 +1265,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
       if (e->cells.valid) {
         HIPCHK(e, e->wide.reserve(nf, nq, C, s));
+        e->wide.clip_major = e->cells.kdir != nullptr && !e->wide.groups_form;
         bool ok = false;
         HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
                                            &e->wide, &ok, s, pass == 0));
@@ -1417,6 +1418,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.points_only = getenv("TFP_WIDE_POINTS") != nullptr;
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
   e->wide.no_spec = getenv("TFP_WIDE_SYNC") != nullptr;
+  e->wide.ch128 = getenv("TFP_WIDE_CH128") != nullptr;
   if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = getenv("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {

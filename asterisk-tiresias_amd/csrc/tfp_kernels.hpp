@@ -248,6 +248,9 @@ struct WideScratch {
   bool no_spec = false;                              // TFP_WIDE_SYNC (A/B): read the counts back before the sweep
   bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
   bool groups_form = false;                          // TFP_WIDE_GROUPS (tests, A/B): the key-major sweep with score rows
+  bool ch128 = false;                                // TFP_WIDE_CH128 (tests, A/B): 128-query chunks only
+  bool clip_major = true;                            // set by the caller before prepare: the clip-major sweep will run
+  int32_t qch = kChunk;                              // prepare: queries per chunk of this batch (128, or 256 with 8-bit counts)
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
   int32_t* nuk = nullptr;                            // [nchunks] their number
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima

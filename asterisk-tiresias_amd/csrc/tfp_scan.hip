@@ -550,7 +550,7 @@ __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_
 // (d = 0: that stable pre-sort orders equal L2 by U2 instead).
 constexpr int kWideDeltaBits = 3, kWideSegShift = 32 + kWideDeltaBits, kWideChunkShift = kWideSegShift + 11;
 __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
-                                   int64_t nf, const int32_t* __restrict__ fv, int64_t dbase,
+                                   int64_t nf, int32_t qch, const int32_t* __restrict__ fv, int64_t dbase,
                                    unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
                                    int32_t* __restrict__ info) {
   int32_t kept = 0, wide = 0;
@@ -560,7 +560,7 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
     unsigned long long key = ~0ull;
     const int64_t kk = (int64_t)bx.k + kKeyOffset;
     if ((bx.flags & 1) && kk >= 0 && kk < kKeyRange) {
-      const unsigned long long ch = (unsigned long long)(fq[f] / kWideCh);
+      const unsigned long long ch = (unsigned long long)(fq[f] / qch);
       const bool w2 = bx.flags & 2;
       const unsigned long long sk = w2 ? (unsigned long long)kk : (unsigned long long)kk | kKeyRange;
       const unsigned long long l2 = w2 ? (unsigned long long)((uint32_t)(int32_t)bx.L2 ^ 0x80000000u) : 0ull;
@@ -600,15 +600,15 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
 // (n: the kept frames, info[0] of the key pass, read on the device: no host wait for the sort)
 __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
-                                   const int32_t* __restrict__ fv, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
-                                   uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
+                                   const int32_t* __restrict__ fv, int32_t qch, int32_t* __restrict__ L2s,
+                                   int32_t* __restrict__ U2s, uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
   const int64_t n = *pn;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = fv[i];
     const FrameBox bx = boxes[f];
     L2s[i] = (int32_t)bx.L2;
     U2s[i] = (int32_t)bx.U2;
-    qis[i] = (uint8_t)(fq[f] % kWideCh);
+    qis[i] = (uint8_t)(fq[f] % qch);
     const unsigned long long sg = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
     if (i == 0 || (ck[i - 1] >> kWideSegShift) != sg) seg[2 * sg] = (int32_t)i;
     if (i == n - 1 || (ck[i + 1] >> kWideSegShift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
@@ -725,10 +725,16 @@ __device__ __forceinline__ void portion_range(const int32_t* cbeg, int ch, int p
   r0 = min(n, p * per);
   r1 = min(n, r0 + per);
 }
-// frame x's increment for lane l: 1 (query 2l), 1 << 16 (query 2l + 1) or 0; 255 pads
+// frame x's increment for lane l. QPL = 2 (128-query chunks, 16-bit counts): 1 (query 2l), 1 << 16
+// (query 2l + 1) or 0. QPL = 4 (256-query chunks, 8-bit counts, queries under 256 frames): 1 << 8j
+// for query 4l + j. kPadQ pads (no lane's).
+constexpr int32_t kPadQ = 4096;
+template <int QPL>
 __device__ __forceinline__ uint32_t prefix_inc(int32_t x, int lane) {
-  return (x >> 1) == lane ? (x & 1 ? 0x10000u : 1u) : 0u;
+  if constexpr (QPL == 2) return (x >> 1) == lane ? (x & 1 ? 0x10000u : 1u) : 0u;
+  else return (x >> 2) == lane ? (1u << (8 * (x & 3))) : 0u;
 }
+template <int QPL>
 __global__ __launch_bounds__(1024) void wide_pcount_kernel(const int32_t* __restrict__ cbeg,
                                                            const uint8_t* __restrict__ qis, uint32_t* __restrict__ ptot) {
   const int lane = threadIdx.x & 63, p = blockIdx.y * 16 + (threadIdx.x >> 6);
@@ -736,9 +742,9 @@ __global__ __launch_bounds__(1024) void wide_pcount_kernel(const int32_t* __rest
   portion_range(cbeg, blockIdx.x, p, b, r0, r1);
   uint32_t cnt = 0;
   for (int32_t i = r0; i < r1; i += 64) {
-    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
+    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : kPadQ;
 #pragma unroll
-    for (int j = 0; j < 64; j++) cnt += prefix_inc(__builtin_amdgcn_readlane(x, j), lane);
+    for (int j = 0; j < 64; j++) cnt += prefix_inc<QPL>(__builtin_amdgcn_readlane(x, j), lane);
   }
   ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane] = cnt;
 }
@@ -763,6 +769,7 @@ __global__ __launch_bounds__(1024) void wide_pscan_kernel(uint32_t* __restrict__
 #pragma unroll
   for (int j = 0; j < 16; j++) t[64 * j] = base + v[j];
 }
+template <int QPL>
 __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg, const uint8_t* __restrict__ qis,
                                                            const uint32_t* __restrict__ ptot, uint32_t* __restrict__ P) {
   const int lane = threadIdx.x & 63, p = blockIdx.y * 16 + (threadIdx.x >> 6);
@@ -770,12 +777,12 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   portion_range(cbeg, blockIdx.x, p, b, r0, r1);
   uint32_t run = ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane];
   for (int32_t i = r0; i < r1; i += 64) {
-    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : 255;
+    const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : kPadQ;
     uint32_t* row = P + ((int64_t)b + i) * kWideW + lane;
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
-      run += prefix_inc(__builtin_amdgcn_readlane(x, j), lane);
+      run += prefix_inc<QPL>(__builtin_amdgcn_readlane(x, j), lane);
       if (j < m) row[(int64_t)j * kWideW] = run;
     }
   }
@@ -1157,13 +1164,14 @@ constexpr bool kClipGrpPre = TFP_CLIP_GRPPRE;
 #ifndef TFP_CLIP_OCC
 #define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 #endif
+template <int QPL>
 __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
     const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
     unsigned long long* __restrict__ part) {
-  __shared__ uint32_t accs[kClipWaves][kWin * 64];
+  __shared__ __attribute__((aligned(16))) uint32_t accs[kClipWaves][kWin * 64];
   // wv through readfirstlane: the wave's chunk, window range and per-chunk pointers are then scalar
   // (as per-lane values they took 64-bit VGPR pairs, and 12 VGPRs spilled at 8 waves per SIMD)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1176,7 +1184,9 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
   const int32_t* uk = ukeys + (int64_t)ch * kKeyRange;
   const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
   const int32_t cb = cbeg[ch];
-  unsigned long long rlo = 0, rhi = 0;  // queries 128 ch + 2 lane, + 1
+  unsigned long long r[QPL];  // queries 64 QPL ch + QPL lane + j: best (count << 32 | tie key)
+#pragma unroll
+  for (int j = 0; j < QPL; j++) r[j] = 0;
   int32_t sb = 0, se = 0;
   uint32_t base = 0, fcnt = 0;
   int32_t nbk = 1, shf = 0, l2min = 0, u2min = 0;
@@ -1407,39 +1417,49 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
     for (int j = 0; j < kWin; j++) {
       const uint32_t v = acc[j * 64 + lane];
       const unsigned long long t = (uint32_t)__builtin_amdgcn_readlane(tk, j);
-      const unsigned long long klo = ((unsigned long long)(v & 0xffffu) << 32) | t;
-      const unsigned long long khi = ((unsigned long long)(v >> 16) << 32) | t;
-      if (v & 0xffffu) rlo = klo > rlo ? klo : rlo;
-      if (v >> 16) rhi = khi > rhi ? khi : rhi;
+#pragma unroll
+      for (int b = 0; b < QPL; b++) {
+        const uint32_t c = QPL == 2 ? (b ? v >> 16 : v & 0xffffu) : (v >> (8 * b)) & 0xffu;
+        const unsigned long long k = ((unsigned long long)c << 32) | t;
+        if (c) r[b] = k > r[b] ? k : r[b];
+      }
     }
   }
-  // the workgroup's maxima (its waves share the chunk: xw is a multiple of kClipWaves)
-  __shared__ unsigned long long red[kClipWaves][kWideCh];
-  red[wv][2 * lane] = rlo;
-  red[wv][2 * lane + 1] = rhi;
+  // the workgroup's maxima (its waves share the chunk: xw is a multiple of kClipWaves), through
+  // each wave's own count rows (free after its last window: 4 KB, the chunk's 64 QPL keys fit)
+  constexpr int Q = 64 * QPL;
+  static_assert(Q * sizeof(unsigned long long) <= kWin * 64 * sizeof(uint32_t), "maxima in the count rows");
+  unsigned long long* redw = reinterpret_cast<unsigned long long*>(accs[wv]);
+#pragma unroll
+  for (int b = 0; b < QPL; b++) redw[QPL * lane + b] = r[b];
   __syncthreads();
-  if (threadIdx.x < kWideCh) {
-    unsigned long long m = red[0][threadIdx.x];
-    for (int w2 = 1; w2 < kClipWaves; w2++) m = red[w2][threadIdx.x] > m ? red[w2][threadIdx.x] : m;
-    part[((int64_t)ch * (xw / kClipWaves) + x / kClipWaves) * kWideCh + threadIdx.x] = m;
+  for (int t = threadIdx.x; t < Q; t += 64 * kClipWaves) {
+    unsigned long long m = reinterpret_cast<const unsigned long long*>(accs[0])[t];
+    for (int w2 = 1; w2 < kClipWaves; w2++) {
+      const unsigned long long y = reinterpret_cast<const unsigned long long*>(accs[w2])[t];
+      m = y > m ? y : m;
+    }
+    part[((int64_t)ch * (xw / kClipWaves) + x / kClipWaves) * Q + t] = m;
   }
 }
 
 // best[q] = max over the chunk's nb per-workgroup maxima (one workgroup per chunk: query t & 127,
 // every 8th maximum from t >> 7, then the 8 slices in LDS).
+template <int QPL>
 __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long long* __restrict__ part, int32_t nb,
                                                              int32_t nq, unsigned long long* __restrict__ best) {
-  __shared__ unsigned long long red[8][kWideCh];
-  const int ch = blockIdx.x, t = threadIdx.x & (kWideCh - 1), sl = threadIdx.x >> 7;
-  const unsigned long long* pp = part + (int64_t)ch * nb * kWideCh + t;
+  constexpr int Q = 64 * QPL, S = 1024 / Q;  // queries per chunk, slices
+  __shared__ unsigned long long red[S][Q];
+  const int ch = blockIdx.x, t = threadIdx.x & (Q - 1), sl = threadIdx.x / Q;
+  const unsigned long long* pp = part + (int64_t)ch * nb * Q + t;
   unsigned long long m = 0;
 #pragma unroll 4
-  for (int32_t x = sl; x < nb; x += 8) m = pp[(int64_t)x * kWideCh] > m ? pp[(int64_t)x * kWideCh] : m;
+  for (int32_t x = sl; x < nb; x += S) m = pp[(int64_t)x * Q] > m ? pp[(int64_t)x * Q] : m;
   red[sl][t] = m;
   __syncthreads();
   if (sl == 0) {
-    for (int j = 1; j < 8; j++) m = red[j][t] > m ? red[j][t] : m;
-    const int32_t q = ch * kWideCh + t;
+    for (int j = 1; j < S; j++) m = red[j][t] > m ? red[j][t] : m;
+    const int32_t q = ch * Q + t;
     if (m && q < nq) best[q] = m > best[q] ? m : best[q];
   }
 }
@@ -1561,7 +1581,11 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   if (nq <= 0 || nf <= 0 || nf >= INT32_MAX / (4 << kDirScale) - 8 || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
     return hipSuccess;
   hipError_t e;
-  const int64_t nch = (nq + kWideCh - 1) / kWideCh;
+  // 256-query chunks (four 8-bit counts per lane word) when every query has under 256 frames and the
+  // clip-major sweep will run: half the chunks, so half the (clip, key, chunk) searches
+  ws->qch = (ws->clip_major && !ws->ch128 && max_qframes < 256) ? 256 : kWideCh;
+  const int32_t qch = ws->qch;
+  const int64_t nch = (nq + qch - 1) / qch;
   int cb = 1;  // chunk bits: every chunk number below 2^cb - 1, so no key reaches the ~0 of unused frames
   while (((int64_t)1 << cb) - 1 <= nch) cb++;
   const int end_bit = kWideChunkShift + cb;
@@ -1575,8 +1599,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
                      ws->info);
   // one sort by (chunk, key, L2, U2 - L2)
-  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, (const int32_t*)nullptr,
-                     dbase, ws->ka, ws->va, ws->info);
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
+                     (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
   if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
   const int32_t* order = ws->vb;
@@ -1596,8 +1620,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
       tb = ws->tmp_bytes;
       if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
-      hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, ws->vb, (int64_t)-1,
-                         ws->ka, (int32_t*)nullptr, ws->info);
+      hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
+                         ws->vb, (int64_t)-1, ws->ka, (int32_t*)nullptr, ws->info);
       tb = ws->tmp_bytes;
       if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, end_bit, s)))
         return e;
@@ -1606,8 +1630,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   }
   // (info[0] = the kept frames, read by the kernels below on the device)
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
-  hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, ws->L2s,
-                     ws->U2s, ws->qis, ws->seg);
+  hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
+                     ws->L2s, ws->U2s, ws->qis, ws->seg);
   hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, ws->info, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
   const int64_t nd = nch * kKeyRange + 1;
@@ -1616,10 +1640,17 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   if ((e = hipcub::DeviceScan::ExclusiveSum(ws->dtmp, db, ws->dtab, ws->doff, (int)nd, s))) return e;
   hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb, ws->seg, ws->L2s, ws->U2s,
                      ws->doff, ws->dtab);
-  hipLaunchKernelGGL(wide_pcount_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
-  hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
-  hipLaunchKernelGGL(wide_prefix_kernel, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot,
-                     ws->P);
+  if (qch == 256) {
+    hipLaunchKernelGGL(wide_pcount_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
+    hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
+    hipLaunchKernelGGL(wide_prefix_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot,
+                       ws->P);
+  } else {
+    hipLaunchKernelGGL(wide_pcount_kernel<2>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
+    hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
+    hipLaunchKernelGGL(wide_prefix_kernel<2>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot,
+                       ws->P);
+  }
   if ((e = hipGetLastError())) return e;
   *eligible = true;
   return hipSuccess;
@@ -1629,7 +1660,9 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s) {
   if (nq <= 0 || !cells || !cells->valid || !cells->k_gbeg) return hipErrorInvalidValue;
   (void)nf;
-  const int64_t nch = (nq + kWideCh - 1) / kWideCh;
+  const int64_t nch = (nq + ws->qch - 1) / ws->qch;
+  const bool clip_major = cells->kdir && !ws->groups_form;
+  if (ws->qch != kWideCh && !clip_major) return hipErrorInvalidValue;  // (prepare chose the chunks for the clip-major sweep)
   CellView cv;
   memset(&cv, 0, sizeof cv);
   cv.g_key = cells->g_key;
@@ -1644,17 +1677,25 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
     cv.g_beg = cells->g_beg;
   }
   cv.valid = 1;
-  if (cells->kdir && !ws->groups_form) {
+  if (clip_major) {
     // clip-major: xw waves per chunk (a multiple of the workgroup's), ~32 k waves in all
     int64_t xw = std::max<int64_t>(1, 32768 / nch);
     xw = std::min<int64_t>(xw, std::min<int64_t>(kPartWaves, cells->nwin));
     xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
     hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
-    hipLaunchKernelGGL(wide_clips_kernel, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                       C, ws->doff, ws->dtab, ws->part);
-    hipLaunchKernelGGL(wide_part_max_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves), nq,
-                       d_best);
+    if (ws->qch == 256) {
+      hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
+                         ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                         C, ws->doff, ws->dtab, ws->part);
+      hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+                         nq, d_best);
+    } else {
+      hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
+                         ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                         C, ws->doff, ws->dtab, ws->part);
+      hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+                         nq, d_best);
+    }
     return hipGetLastError();
   }
   hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);

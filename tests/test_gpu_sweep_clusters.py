@@ -8,7 +8,8 @@ placed inside every gap and on both ends of it, with q2 at several sub-micro off
 exact frame count back as match_count), and all clips also share one key, where the groups batch
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
 (src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
-(TFP_WIDE_POINTS) and in the key-major form with score rows (TFP_WIDE_GROUPS).
+(TFP_WIDE_POINTS), in the key-major form with score rows (TFP_WIDE_GROUPS), and with 128-query
+chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks).
 """
 import math
 import os
@@ -109,7 +110,8 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     got = {}
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
+                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(len(kinds)):
@@ -123,6 +125,7 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     assert got["clusters"] == expect, tol
     assert got["points"] == expect, tol
     assert got["key-major"] == expect, tol
+    assert got["clusters-128"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
@@ -132,8 +135,10 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
 @pytest.mark.parametrize("tol", [0.001, 0.05, 0.3])
 def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
     """Chunks that use more than 64 keys (the clip-major sweep takes them 64 per step), frames
-    with and without max2 windows (a 3400 Hz ignore filter drops max2 conditions), two 128-query
-    chunks, a last clip window only partly filled, and NULL max2 rows: every form == the oracle."""
+    with and without max2 windows (a 3400 Hz ignore filter drops max2 conditions), 300 queries (two
+    256-query chunks with 8-bit counts, or three 128-query chunks with TFP_WIDE_CH128), a last clip
+    window only partly filled, and NULL max2 rows: every form == the oracle. Then the same batch with
+    one query of 300 frames (over 8-bit counts: 128-query chunks)."""
     rng = np.random.default_rng(int(tol * 1e4) + 5)
     nclips, rows = 70, 260
     uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
@@ -142,7 +147,7 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
     m2 = rng.integers(0, 40_000_000, nclips * rows).astype(np.int32)
     m2[rng.random(nclips * rows) < 0.02] = np.iinfo(np.int32).min  # NULL max2 (never matches a max2 window)
     clip = np.repeat(np.arange(nclips), rows).astype(np.int32)
-    nq = 150
+    nq = 300
     q1s, q2s, qoff = [], [], [0]
     for i in range(nq):
         c = int(rng.integers(nclips))
@@ -167,7 +172,8 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     assert sum(e is not None for e in expect) > nq // 2
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"})):
+                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
+                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(nclips):
@@ -179,3 +185,24 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
             assert list(fcs) == list(np.diff(qoff))
         finally:
             eng.close()
+    # query 0 repeated to 300 frames: the batch no longer fits 8-bit counts
+    n0 = qoff[1] - qoff[0]
+    rep = np.arange(300) % n0
+    lq1 = np.concatenate([q1[rep], q1[qoff[1]:]])
+    lq2 = np.concatenate([q2[rep], q2[qoff[1]:]])
+    lqoff = np.concatenate([[0], qoff[1:] - n0 + 300]).astype(np.int64)
+    found, w, mc, fc = oracle.search(m1, m2, clip, uuids, lq1[:300], lq2[:300], 2, tol, low, high)
+    lexp = [(uuids[w], mc) if found else None] + expect[1:]
+    lframes = np.zeros(len(lq1), frames.dtype)
+    lframes["q1"], lframes["q2"] = lq1, lq2
+    eng = _engine_with(tfp_lib, {"TFP_WIDE_MIN_TOL": "0"})
+    try:
+        for c in range(nclips):
+            sel = clip == c
+            eng.index_add(uuids[c], m1[sel], m2[sel])
+        res, fcs = eng.search_batch(lframes, lqoff, tfp_lib.params(2, tol, low, high))
+        got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+        assert got == lexp, (tol, [i for i in range(nq) if got[i] != lexp[i]][:5])
+        assert fcs[0] == 300
+    finally:
+        eng.close()
