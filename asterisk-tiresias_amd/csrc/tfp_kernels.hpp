@@ -251,6 +251,7 @@ struct WideScratch {
   bool ch128 = false;                                // TFP_WIDE_CH128 (tests, A/B): 128-query chunks only
   bool clip_major = true;                            // set by the caller before prepare: the clip-major sweep will run
   int32_t qch = kChunk;                              // prepare: queries per chunk of this batch (128, or 256 with 8-bit counts)
+  int32_t xw_cap = 0;                                // TFP_CLIP_XW (A/B): clip-major waves per chunk (0: 1024 per 128 queries)
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
   int32_t* nuk = nullptr;                            // [nchunks] their number
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima

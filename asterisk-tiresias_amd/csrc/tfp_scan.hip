@@ -1534,7 +1534,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
         (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
         (e = dmalloc(&ptot, nch * kPortions * 64)) || (e = dmalloc(&ukeys, nch * kKeyRange)) || (e = dmalloc(&nuk, nch)) ||
-        (e = dmalloc(&part, nch * kPartWaves * kWideCh)))
+        (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)))  // up to 2 kPartWaves waves per chunk, either chunk size
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1680,7 +1680,9 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (clip_major) {
     // clip-major: xw waves per chunk (a multiple of the workgroup's), ~32 k waves in all
     int64_t xw = std::max<int64_t>(1, 32768 / nch);
-    xw = std::min<int64_t>(xw, std::min<int64_t>(kPartWaves, cells->nwin));
+    // (256-query chunks: half the chunks, so up to twice the waves per chunk, ~32 k in all)
+    const int64_t xcap = std::min<int64_t>(2 * kPartWaves, ws->xw_cap > 0 ? ws->xw_cap : (int64_t)kPartWaves * (ws->qch / kWideCh));
+    xw = std::min<int64_t>(xw, std::min<int64_t>(xcap, cells->nwin));
     xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
     hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
     if (ws->qch == 256) {
