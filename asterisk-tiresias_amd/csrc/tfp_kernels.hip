@@ -172,6 +172,10 @@ static_assert(kFbSegs == 4, "fb_seg");
 #define TFP_FP8_HALF_SQ (TFP_FP8_BLOCK_WAVES > 4)
 #endif
 constexpr int kBW8 = TFP_FP8_BLOCK_WAVES;
+#ifndef TFP_FP8_INLINE_EDGE
+#define TFP_FP8_INLINE_EDGE 0
+#endif
+constexpr bool kInlineEdge8 = TFP_FP8_INLINE_EDGE;
 constexpr bool kHalfSq = TFP_FP8_HALF_SQ;
 static_assert(kBW8 == 4 || kBW8 == 8 || kBW8 == 12, "8 kHz workgroup");
 struct WaveLds8P {
@@ -207,6 +211,9 @@ struct SmpLayout {
   static constexpr int kHopChunks = kHop / kPer;              // chunks per staged hop
 };
 
+#ifndef TFP_FP_CHECKED_FAST
+#define TFP_FP_CHECKED_FAST 1
+#endif
 // Slow path of one 16-byte chunk: clip edges (zeros outside [0, ns): aubio_source pads the last
 // hop, the phase vocoder's first history hop is zeros) and unaligned clips.
 __device__ __noinline__ int4 fetch_chunk_checked(const float* clip, int64_t ns, int64_t s) {
@@ -216,6 +223,9 @@ __device__ __noinline__ int4 fetch_chunk_checked(const float* clip, int64_t ns, 
                    __builtin_bit_cast(int, v[3]));
 }
 __device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns, int64_t s) {
+  // an aligned chunk wholly inside the clip (most of an edge pass's): one 16-byte load
+  if (TFP_FP_CHECKED_FAST && s >= 0 && s + 8 <= ns && (reinterpret_cast<uintptr_t>(clip + s) & 15) == 0)
+    return *reinterpret_cast<const int4*>(clip + s);
   uint32_t w[4];
   for (int e = 0; e < 4; e++) {
     const int64_t a = s + 2 * e;
@@ -811,9 +821,11 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
         const int chunk = lane + 64 * r;
         pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
       }
-    } else if constexpr (kPasses == 1) {
-      // clip edges of a small launch (its PCM may be across PCIe): chunks wholly inside are one
-      // 16-byte load, wholly outside zeros, no call (a call waits for every outstanding load)
+    } else if constexpr (kPasses == 1 || kInlineEdge8) {
+      // clip edges of a small launch (its PCM may be across PCIe), or of any launch with
+      // TFP_FP8_INLINE_EDGE (short clips, such as the 5 s queries of a search batch, spend a
+      // twentieth of their passes on edges): chunks wholly inside are one 16-byte load, wholly
+      // outside zeros, no call (a call waits for every outstanding load)
       const bool aligned = (reinterpret_cast<uintptr_t>(clip) & 15) == 0;
 #pragma unroll
       for (int r = 0; r < kChunkRounds; r++) {

@@ -1450,17 +1450,19 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
                                                              int32_t nq, unsigned long long* __restrict__ best) {
   constexpr int Q = 64 * QPL, S = 1024 / Q;  // queries per chunk, slices
   __shared__ unsigned long long red[S][Q];
+  // (gridDim.y workgroups per chunk, each over every gridDim.y-th slice of the maxima: a chunk's
+  // 8-17 MB of maxima read by more than one CU; their results meet in an atomic max)
   const int ch = blockIdx.x, t = threadIdx.x & (Q - 1), sl = threadIdx.x / Q;
   const unsigned long long* pp = part + (int64_t)ch * nb * Q + t;
   unsigned long long m = 0;
 #pragma unroll 4
-  for (int32_t x = sl; x < nb; x += S) m = pp[(int64_t)x * Q] > m ? pp[(int64_t)x * Q] : m;
+  for (int32_t x = blockIdx.y * S + sl; x < nb; x += S * gridDim.y) m = pp[(int64_t)x * Q] > m ? pp[(int64_t)x * Q] : m;
   red[sl][t] = m;
   __syncthreads();
   if (sl == 0) {
     for (int j = 1; j < S; j++) m = red[j][t] > m ? red[j][t] : m;
     const int32_t q = ch * Q + t;
-    if (m && q < nq) best[q] = m > best[q] ? m : best[q];
+    if (m && q < nq) atomicMax(&best[q], m);
   }
 }
 
@@ -1689,13 +1691,13 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
       hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                          ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
                          C, ws->doff, ws->dtab, ws->part);
-      hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+      hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                          nq, d_best);
     } else {
       hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                          ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
                          C, ws->doff, ws->dtab, ws->part);
-      hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+      hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                          nq, d_best);
     }
     return hipGetLastError();
