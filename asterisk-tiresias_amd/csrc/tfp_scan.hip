@@ -533,12 +533,14 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
   if ((threadIdx.x & 63) == 0 && nbad) atomicAdd(&info[1], nbad);
 }
 
-// fq[f] = the query of frame f (one thread per query writes its frames' entries): the key and
-// gather passes read it instead of searching qoff per frame.
+// fq[f] = the query of frame f (one wave per query writes its frames' entries, coalesced): the key
+// and gather passes read it instead of searching qoff per frame.
 __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq) {
-  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += (int64_t)gridDim.x * blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; q < nq; q += nw) {
     const int64_t b = qoff[q] - qoff[0], e = qoff[q + 1] - qoff[0];
-    for (int64_t f = b; f < e; f++) fq[f] = (int32_t)q;
+    for (int64_t f = b + lane; f < e; f += 64) fq[f] = (int32_t)q;
   }
 }
 
@@ -553,12 +555,18 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
                                    int64_t nf, int32_t qch, const int32_t* __restrict__ fv, int64_t dbase,
                                    unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
                                    int32_t* __restrict__ info) {
-  int32_t kept = 0, wide = 0;
+  int32_t kept = 0, wide = 0, nbad = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = fv ? fv[i] : (int32_t)i;
     const FrameBox bx = boxes[f];
     unsigned long long key = ~0ull;
     const int64_t kk = (int64_t)bx.k + kKeyOffset;
+    // the bad-frame check of wide_keys_u (a key or a window outside what the cache and the int32
+    // windows hold: the batch takes the row scan)
+    if (bx.flags & 1)
+      nbad += kk < 0 || kk >= kKeyRange ||
+              ((bx.flags & 2) && (bx.L2 <= (int64_t)INT32_MIN || bx.L2 > (int64_t)INT32_MAX ||
+                                  bx.U2 < (int64_t)INT32_MIN || bx.U2 > (int64_t)INT32_MAX));
     if ((bx.flags & 1) && kk >= 0 && kk < kKeyRange) {
       const unsigned long long ch = (unsigned long long)(fq[f] / qch);
       const bool w2 = bx.flags & 2;
@@ -578,21 +586,24 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
   }
   // one atomic per block, on a grid of at most kKeysBlocks blocks: same-address atomics serialise in
   // L2 (one per frame cost ~0.13 ms at C3, and one per wave still ~0.1 ms: 10k waves)
-  __shared__ int32_t red[2][256 / 64];
+  __shared__ int32_t red[3][256 / 64];
   for (int o = 32; o > 0; o >>= 1) {
     kept += __shfl_xor(kept, o, 64);
     wide += __shfl_xor(wide, o, 64);
+    nbad += __shfl_xor(nbad, o, 64);
   }
   if ((threadIdx.x & 63) == 0) {
     red[0][threadIdx.x >> 6] = kept;
     red[1][threadIdx.x >> 6] = wide;
+    red[2][threadIdx.x >> 6] = nbad;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    int32_t k = 0, w = 0;
-    for (int i = 0; i < 256 / 64; i++) k += red[0][i], w += red[1][i];
+    int32_t k = 0, w = 0, b = 0;
+    for (int i = 0; i < 256 / 64; i++) k += red[0][i], w += red[1][i], b += red[2][i];
     if (k) atomicAdd(&info[0], k);
     if (w) atomicAdd(&info[2], w);
+    if (b) atomicAdd(&info[1], b);
   }
 }
 
@@ -601,8 +612,11 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
 __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
                                    const int32_t* __restrict__ fv, int32_t qch, int32_t* __restrict__ L2s,
-                                   int32_t* __restrict__ U2s, uint8_t* __restrict__ qis, int32_t* __restrict__ seg) {
+                                   int32_t* __restrict__ U2s, uint8_t* __restrict__ qis, int32_t* __restrict__ seg,
+                                   int64_t nch, int32_t* __restrict__ cbeg) {
   const int64_t n = *pn;
+  if (n == 0 && blockIdx.x == 0)  // no kept frame: every chunk empty
+    for (int64_t x = threadIdx.x; x <= nch; x += blockDim.x) cbeg[x] = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t f = fv[i];
     const FrameBox bx = boxes[f];
@@ -612,16 +626,16 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
     const unsigned long long sg = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
     if (i == 0 || (ck[i - 1] >> kWideSegShift) != sg) seg[2 * sg] = (int32_t)i;
     if (i == n - 1 || (ck[i + 1] >> kWideSegShift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
+    // chunk boundaries: cbeg[c] = the first sorted frame of chunk c (n for chunks past the last
+    // frame's; chunks without kept frames take the next chunk's first frame; zeroed when n = 0)
+    const int64_t c = (int64_t)(ck[i] >> kWideChunkShift);
+    const int64_t cp = i == 0 ? -1 : (int64_t)(ck[i - 1] >> kWideChunkShift);
+    for (int64_t x = cp + 1; x <= c; x++) cbeg[x] = (int32_t)i;
+    if (i == n - 1)
+      for (int64_t x = c + 1; x <= nch; x++) cbeg[x] = (int32_t)n;
   }
 }
 
-// Chunk boundaries in the sorted frames: cbeg[ch] = first frame of chunk ch (n for ch >= chunks).
-__global__ void wide_cbeg_kernel(const unsigned long long* __restrict__ ck, const int32_t* __restrict__ pn, int64_t nch,
-                                 int32_t* __restrict__ cbeg) {
-  const int64_t n = *pn;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t <= nch) cbeg[t] = (int32_t)lower_bound_t<unsigned long long>(ck, n, (unsigned long long)t << kWideChunkShift);
-}
 
 // Segment directories. A window segment's S frames are sorted by L2 (and U2); its directory has
 // NB = 2^ceil(log2 S) buckets over each bound's range: TL[b] = the first frame whose L2 >=
@@ -1595,12 +1609,9 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
   speculative = speculative && dbase >= 0 && !ws->no_spec;
   if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
-  hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(1024, (nq + 255) / 256)), dim3(256), 0, s,
-                     d_qoff, nq, ws->fq);
-  // the bad-frame check (a key or a window outside what the cache and the int32 windows hold)
-  hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, (uint32_t*)nullptr, (int32_t*)nullptr,
-                     ws->info);
-  // one sort by (chunk, key, L2, U2 - L2)
+  hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
+                     0, s, d_qoff, nq, ws->fq);
+  // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
   hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
                      (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
@@ -1633,8 +1644,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   // (info[0] = the kept frames, read by the kernels below on the device)
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
   hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
-                     ws->L2s, ws->U2s, ws->qis, ws->seg);
-  hipLaunchKernelGGL(wide_cbeg_kernel, dim3((unsigned)((nch + 256) / 256)), dim3(256), 0, s, ws->kb, ws->info, nch, ws->cbeg);
+                     ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
   const int64_t nd = nch * kKeyRange + 1;
   hipLaunchKernelGGL(wide_dir_count_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, ws->seg, nch, ws->dtab);
