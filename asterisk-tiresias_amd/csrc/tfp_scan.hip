@@ -653,19 +653,40 @@ __device__ __forceinline__ int dir_shift(int64_t range, int lg) {
   return bits > lg ? bits - lg : 0;
 }
 
-// Directory sizes: nb[ch * kKeyRange + k] = 2 NB of chunk ch's window segment of key k (0: empty);
-// nb[nch * kKeyRange] = 0 (the scan's total).
-__global__ void wide_dir_count_kernel(const int32_t* __restrict__ seg, int64_t nch, int32_t* __restrict__ nb) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t > nch * kKeyRange) return;
-  int32_t v = 0;
-  if (t < nch * kKeyRange) {
+  nb[t] = v;
+}
+
+// Directory offsets in one workgroup: doff[t] = the exclusive prefix of the directory sizes
+// (2 NB per window segment of S frames, 0 when empty) over the nch * kKeyRange window segments, doff[nd - 1] their total; each
+// thread sums a contiguous run of segments, one LDS scan over the threads' sums (one launch instead
+// of a size pass and a device-wide scan).
+__global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* __restrict__ seg, int64_t nch,
+                                                                int32_t* __restrict__ doff) {
+  __shared__ int32_t tsum[1024];
+  const int64_t nseg = nch * kKeyRange, per = (nseg + 1023) / 1024;
+  const int64_t a = (int64_t)threadIdx.x * per, b = min(nseg, a + per);
+  auto size_of = [&](int64_t t) {
     const int64_t ch = t / kKeyRange, k = t % kKeyRange;
     const int32_t* sg = seg + ch * kWideSegs * 2 + 2 * k;
     const int32_t S = sg[1] - sg[0];
-    v = S > 0 ? 2 << dir_log2(S) : 0;
+    return S > 0 ? 2 << dir_log2(S) : 0;
+  };
+  int32_t sum = 0;
+  for (int64_t t = a; t < b; t++) sum += size_of(t);
+  tsum[threadIdx.x] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
+    const int32_t y = threadIdx.x >= o ? tsum[threadIdx.x - o] : 0;
+    __syncthreads();
+    tsum[threadIdx.x] += y;
+    __syncthreads();
   }
-  nb[t] = v;
+  int32_t run = tsum[threadIdx.x] - sum;
+  for (int64_t t = a; t < b; t++) {
+    doff[t] = run;
+    run += size_of(t);
+  }
+  if (threadIdx.x == 1023) doff[nseg] = tsum[1023];
 }
 
 // The directories, from the sorted frames: frame i of a window segment is the first frame of the
@@ -1647,9 +1668,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
                      ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
   const int64_t nd = nch * kKeyRange + 1;
-  hipLaunchKernelGGL(wide_dir_count_kernel, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, ws->seg, nch, ws->dtab);
-  size_t db = ws->dtmp_bytes;
-  if ((e = hipcub::DeviceScan::ExclusiveSum(ws->dtmp, db, ws->dtab, ws->doff, (int)nd, s))) return e;
+  (void)nd;
+  hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
   hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb, ws->seg, ws->L2s, ws->U2s,
                      ws->doff, ws->dtab);
   if (qch == 256) {
