@@ -653,13 +653,11 @@ __device__ __forceinline__ int dir_shift(int64_t range, int lg) {
   return bits > lg ? bits - lg : 0;
 }
 
-  nb[t] = v;
-}
 
 // Directory offsets in one workgroup: doff[t] = the exclusive prefix of the directory sizes
-// (2 NB per window segment of S frames, 0 when empty) over the nch * kKeyRange window segments, doff[nd - 1] their total; each
-// thread sums a contiguous run of segments, one LDS scan over the threads' sums (one launch instead
-// of a size pass and a device-wide scan).
+// (2 NB per window segment of S frames, 0 when empty) over the nch * kKeyRange window segments,
+// doff[nch * kKeyRange] their total; each thread sums a contiguous run of segments, one LDS scan
+// over the threads' sums (one launch instead of a size pass and a device-wide scan).
 __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* __restrict__ seg, int64_t nch,
                                                                 int32_t* __restrict__ doff) {
   __shared__ int32_t tsum[1024];
