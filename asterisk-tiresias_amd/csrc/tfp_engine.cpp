@@ -1419,6 +1419,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
   e->wide.no_spec = getenv("TFP_WIDE_SYNC") != nullptr;
   e->wide.ch128 = getenv("TFP_WIDE_CH128") != nullptr;
+  e->wide.unpacked = getenv("TFP_WIDE_UNPACKED") != nullptr;
   if (const char* x = getenv("TFP_CLIP_XW")) e->wide.xw_cap = atoi(x);
   if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = getenv("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;

@@ -249,6 +249,7 @@ struct WideScratch {
   bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
   bool groups_form = false;                          // TFP_WIDE_GROUPS (tests, A/B): the key-major sweep with score rows
   bool ch128 = false;                                // TFP_WIDE_CH128 (tests, A/B): 128-query chunks only
+  bool unpacked = false;                             // TFP_WIDE_UNPACKED (tests, A/B): sort (key, frame) pairs, no packed key
   bool clip_major = true;                            // set by the caller before prepare: the clip-major sweep will run
   int32_t qch = kChunk;                              // prepare: queries per chunk of this batch (128, or 256 with 8-bit counts)
   int32_t xw_cap = 0;                                // TFP_CLIP_XW (A/B): clip-major waves per chunk (0: 1024 per 128 queries)

@@ -156,6 +156,10 @@ __global__ void cluster_kdir_kernel(const uint32_t* __restrict__ g_key, const in
 // 0.17 ms at C3). rocPRIM's onesweep forced instead measured slower there (6 digit passes of
 // 23 us: 0.18 ms).
 template <class K>
+hipError_t sweep_sort_keys(void* tmp, size_t& bytes, const K* kin, K* kout, int64_t n, unsigned end_bit, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortKeys(tmp, bytes, kin, kout, (int)n, 0, (int)end_bit, s);
+}
+template <class K>
 hipError_t sweep_sort_pairs(void* tmp, size_t& bytes, const K* kin, K* kout, const int32_t* vin, int32_t* vout, int64_t n,
                             unsigned end_bit, hipStream_t s) {
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, (int)end_bit, s);
@@ -551,8 +555,13 @@ __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_
 // [dbase, dbase + 8) counts in info[2]; the caller then sorts by U2 first and passes dbase = -1
 // (d = 0: that stable pre-sort orders equal L2 by U2 instead).
 constexpr int kWideDeltaBits = 3, kWideSegShift = 32 + kWideDeltaBits, kWideChunkShift = kWideSegShift + 11;
+// The packed layout (every window's U2 - L2 in [dbase, dbase + 8), at most 10 chunk bits): the
+// frame's query within its chunk in the low byte, chunk << 54 | segment key << 43 | L2 << 11 |
+// d << 8 | query; the keys alone are sorted (no frame index to carry), and the gather reads L2,
+// U2 = L2 + dbase + d and the query back from the sorted key.
+constexpr int kPackSegShift = 43, kPackChunkShift = kPackSegShift + 11;
 __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
-                                   int64_t nf, int32_t qch, const int32_t* __restrict__ fv, int64_t dbase,
+                                   int64_t nf, int32_t qch, bool packed, const int32_t* __restrict__ fv, int64_t dbase,
                                    unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
                                    int32_t* __restrict__ info) {
   int32_t kept = 0, wide = 0, nbad = 0;
@@ -578,7 +587,9 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
         if (dd < 0 || dd >= (1 << kWideDeltaBits)) wide++;
         else d = (unsigned long long)dd;
       }
-      key = (ch << kWideChunkShift) | (sk << kWideSegShift) | (l2 << kWideDeltaBits) | d;
+      key = packed ? (ch << kPackChunkShift) | (sk << kPackSegShift) | (l2 << 11) | (d << 8) |
+                         (unsigned long long)(fq[f] % qch)
+                   : (ch << kWideChunkShift) | (sk << kWideSegShift) | (l2 << kWideDeltaBits) | d;
       kept++;
     }
     ck[i] = key;
@@ -611,25 +622,34 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
 // (n: the kept frames, info[0] of the key pass, read on the device: no host wait for the sort)
 __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
-                                   const int32_t* __restrict__ fv, int32_t qch, int32_t* __restrict__ L2s,
-                                   int32_t* __restrict__ U2s, uint8_t* __restrict__ qis, int32_t* __restrict__ seg,
-                                   int64_t nch, int32_t* __restrict__ cbeg) {
+                                   const int32_t* __restrict__ fv, int32_t qch, bool packed, int64_t dbase,
+                                   int32_t* __restrict__ L2s, int32_t* __restrict__ U2s, uint8_t* __restrict__ qis,
+                                   int32_t* __restrict__ seg, int64_t nch, int32_t* __restrict__ cbeg) {
+  const int segshift = packed ? kPackSegShift : kWideSegShift, chshift = segshift + 11;
   const int64_t n = *pn;
   if (n == 0 && blockIdx.x == 0)  // no kept frame: every chunk empty
     for (int64_t x = threadIdx.x; x <= nch; x += blockDim.x) cbeg[x] = 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t f = fv[i];
-    const FrameBox bx = boxes[f];
-    L2s[i] = (int32_t)bx.L2;
-    U2s[i] = (int32_t)bx.U2;
-    qis[i] = (uint8_t)(fq[f] % qch);
-    const unsigned long long sg = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
-    if (i == 0 || (ck[i - 1] >> kWideSegShift) != sg) seg[2 * sg] = (int32_t)i;
-    if (i == n - 1 || (ck[i + 1] >> kWideSegShift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
+    const unsigned long long k = ck[i];
+    if (packed) {
+      const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u);
+      L2s[i] = l2;
+      U2s[i] = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));  // (frames without a window: never read)
+      qis[i] = (uint8_t)(k & 255);
+    } else {
+      const int32_t f = fv[i];
+      const FrameBox bx = boxes[f];
+      L2s[i] = (int32_t)bx.L2;
+      U2s[i] = (int32_t)bx.U2;
+      qis[i] = (uint8_t)(fq[f] % qch);
+    }
+    const unsigned long long sg = k >> segshift;  // chunk << 11 | segment key
+    if (i == 0 || (ck[i - 1] >> segshift) != sg) seg[2 * sg] = (int32_t)i;
+    if (i == n - 1 || (ck[i + 1] >> segshift) != sg) seg[2 * sg + 1] = (int32_t)(i + 1);
     // chunk boundaries: cbeg[c] = the first sorted frame of chunk c (n for chunks past the last
     // frame's; chunks without kept frames take the next chunk's first frame; zeroed when n = 0)
-    const int64_t c = (int64_t)(ck[i] >> kWideChunkShift);
-    const int64_t cp = i == 0 ? -1 : (int64_t)(ck[i - 1] >> kWideChunkShift);
+    const int64_t c = (int64_t)(k >> chshift);
+    const int64_t cp = i == 0 ? -1 : (int64_t)(ck[i - 1] >> chshift);
     for (int64_t x = cp + 1; x <= c; x++) cbeg[x] = (int32_t)i;
     if (i == n - 1)
       for (int64_t x = c + 1; x <= nch; x++) cbeg[x] = (int32_t)n;
@@ -693,7 +713,7 @@ __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* _
 // sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
 // buckets per step, so no lane loops over thousands of buckets alone.
 __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
-                                     const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
+                                     int segshift, const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
                                      const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
                                      int32_t* __restrict__ dtab) {
   constexpr int32_t kShort = 8;
@@ -705,7 +725,7 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
     // this lane's runs: [lo, hi] of table entries at base + (lo..hi), value v (up to 4: L2, U2, tails)
     int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
     if (i < n) {
-      const unsigned long long sgk = ck[i] >> kWideSegShift;  // chunk << 11 | segment key
+      const unsigned long long sgk = ck[i] >> segshift;  // chunk << 11 | segment key
       const int32_t skey = (int32_t)(sgk & (kWideSegs - 1));
       if (skey < kKeyRange) {  // (no max2 window: no searches, no directory)
         const int64_t ch = (int64_t)(sgk >> 11);
@@ -1548,10 +1568,12 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
         (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideW)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
+    size_t t3 = 0;
     if ((e = sweep_sort_pairs<uint32_t>(nullptr, t1, ua, ub, va, vb, nf, 32, s)) ||
-        (e = sweep_sort_pairs<unsigned long long>(nullptr, t2, ka, kb, va, vb, nf, 64, s)))
+        (e = sweep_sort_pairs<unsigned long long>(nullptr, t2, ka, kb, va, vb, nf, 64, s)) ||
+        (e = sweep_sort_keys<unsigned long long>(nullptr, t3, ka, kb, nf, 64, s)))
       return e;
-    tmp_bytes = t1 > t2 ? t1 : t2;
+    tmp_bytes = std::max(t1, std::max(t2, t3));
     if ((e = hipMalloc(&tmp, tmp_bytes > 0 ? tmp_bytes : 1))) return e;
     cap_nf = nf;
   }
@@ -1623,18 +1645,25 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int64_t nch = (nq + qch - 1) / qch;
   int cb = 1;  // chunk bits: every chunk number below 2^cb - 1, so no key reaches the ~0 of unused frames
   while (((int64_t)1 << cb) - 1 <= nch) cb++;
-  const int end_bit = kWideChunkShift + cb;
   // U2 - L2 lies within a few micro-units of 2 tol (fmt6 rounds both ends): d = U2 - L2 - dbase
   const int64_t dbase = (tole >= 0.0 && tole < 1e6) ? (int64_t)floor(2.0 * tole * 1e6) - 3 : -1;
+  // the packed key (keys-only sort) whenever the delta field can hold every width (checked with
+  // the results: info[2]) and the chunk number fits its 10 bits
+  bool packed = dbase >= 0 && cb <= 10 && !ws->unpacked;
+  const int end_bit = (packed ? kPackChunkShift : kWideChunkShift) + cb;
   speculative = speculative && dbase >= 0 && !ws->no_spec;
   if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
                      0, s, d_qoff, nq, ws->fq);
   // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
   hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
-                     (const int32_t*)nullptr, dbase, ws->ka, ws->va, ws->info);
+                     packed, (const int32_t*)nullptr, dbase, ws->ka, packed ? (int32_t*)nullptr : ws->va, ws->info);
   size_t tb = ws->tmp_bytes;
-  if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
+  if (packed) {
+    if ((e = sweep_sort_keys<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, nf, end_bit, s))) return e;
+  } else {
+    if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
+  }
   const int32_t* order = ws->vb;
   if (speculative) {
     // every window at least dbase wide and no frame for the row scan, as the caller checks after
@@ -1652,10 +1681,11 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
       tb = ws->tmp_bytes;
       if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
+      packed = false;  // (the U2 pre-sort's order: frame indices carried)
       hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
-                         ws->vb, (int64_t)-1, ws->ka, (int32_t*)nullptr, ws->info);
+                         false, ws->vb, (int64_t)-1, ws->ka, (int32_t*)nullptr, ws->info);
       tb = ws->tmp_bytes;
-      if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, end_bit, s)))
+      if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, kWideChunkShift + cb, s)))
         return e;
       order = ws->va;
     }
@@ -1663,13 +1693,13 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   // (info[0] = the kept frames, read by the kernels below on the device)
   if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
   hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
-                     ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
+                     packed, dbase, ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
   const int64_t nd = nch * kKeyRange + 1;
   (void)nd;
   hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
-  hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb, ws->seg, ws->L2s, ws->U2s,
-                     ws->doff, ws->dtab);
+  hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb,
+                     packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab);
   if (qch == 256) {
     hipLaunchKernelGGL(wide_pcount_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
     hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);

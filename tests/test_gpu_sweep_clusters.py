@@ -9,7 +9,8 @@ exact frame count back as match_count), and all clips also share one key, where 
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
 (src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
 (TFP_WIDE_POINTS), in the key-major form with score rows (TFP_WIDE_GROUPS), and with 128-query
-chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks).
+chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks),
+and with the (key, frame) pair sort instead of the packed keys-only sort (TFP_WIDE_UNPACKED).
 """
 import math
 import os
@@ -111,7 +112,8 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     got = {}
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
                       ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
-                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"})):
+                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
+                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(len(kinds)):
@@ -126,6 +128,7 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     assert got["points"] == expect, tol
     assert got["key-major"] == expect, tol
     assert got["clusters-128"] == expect, tol
+    assert got["unpacked"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
@@ -173,7 +176,8 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
     assert sum(e is not None for e in expect) > nq // 2
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
                       ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
-                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"})):
+                      ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
+                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(nclips):
