@@ -539,7 +539,13 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
 
 // fq[f] = the query of frame f (one wave per query writes its frames' entries, coalesced): the key
 // and gather passes read it instead of searching qoff per frame.
-__global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq) {
+// It also zeroes the counts (info) and the segment table, which the key pass and the gather fill
+// (two fill launches fewer on the timeline).
+__global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq,
+                                        int32_t* __restrict__ info, int32_t* __restrict__ seg, int64_t nseg) {
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
+  if (tid < 3) info[tid] = 0;
+  for (int64_t i = tid; i < nseg; i += nt) seg[i] = 0;
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; q < nq; q += nw) {
@@ -1652,9 +1658,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   bool packed = dbase >= 0 && cb <= 10 && !ws->unpacked;
   const int end_bit = (packed ? kPackChunkShift : kWideChunkShift) + cb;
   speculative = speculative && dbase >= 0 && !ws->no_spec;
-  if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
-                     0, s, d_qoff, nq, ws->fq);
+                     0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2);
   // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
   hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
                      packed, (const int32_t*)nullptr, dbase, ws->ka, packed ? (int32_t*)nullptr : ws->va, ws->info);
@@ -1690,8 +1695,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       order = ws->va;
     }
   }
-  // (info[0] = the kept frames, read by the kernels below on the device)
-  if ((e = hipMemsetAsync(ws->seg, 0, sizeof(int32_t) * (size_t)nch * kWideSegs * 2, s))) return e;
+  // (info[0] = the kept frames, read by the kernels below on the device; seg zeroed with the
+  // frame -> query map)
   hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
                      packed, dbase, ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
   // the window segments' directories (sizes, offsets, then filled from the sorted frames)
