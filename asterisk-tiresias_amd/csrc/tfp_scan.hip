@@ -682,35 +682,56 @@ __device__ __forceinline__ int dir_shift(int64_t range, int lg) {
 
 // Directory offsets in one workgroup: doff[t] = the exclusive prefix of the directory sizes
 // (2 NB per window segment of S frames, 0 when empty) over the nch * kKeyRange window segments,
-// doff[nch * kKeyRange] their total; each thread sums a contiguous run of segments, one LDS scan
-// over the threads' sums (one launch instead of a size pass and a device-wide scan).
+// doff[nch * kKeyRange] their total (one launch instead of a size pass and a device-wide scan). In
+// rounds of 16,384 segments: the sizes loaded coalesced into LDS, each thread scans 16 consecutive
+// ones, one LDS scan over the threads' sums, the offsets written coalesced.
 __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* __restrict__ seg, int64_t nch,
                                                                 int32_t* __restrict__ doff) {
+  constexpr int kPer = 16, kRound = 1024 * kPer;
+  __shared__ int32_t sz[kRound];
   __shared__ int32_t tsum[1024];
-  const int64_t nseg = nch * kKeyRange, per = (nseg + 1023) / 1024;
-  const int64_t a = (int64_t)threadIdx.x * per, b = min(nseg, a + per);
-  auto size_of = [&](int64_t t) {
-    const int64_t ch = t / kKeyRange, k = t % kKeyRange;
-    const int32_t* sg = seg + ch * kWideSegs * 2 + 2 * k;
-    const int32_t S = sg[1] - sg[0];
-    return S > 0 ? 2 << dir_log2(S) : 0;
-  };
-  int32_t sum = 0;
-  for (int64_t t = a; t < b; t++) sum += size_of(t);
-  tsum[threadIdx.x] = sum;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
-    const int32_t y = threadIdx.x >= o ? tsum[threadIdx.x - o] : 0;
+  const int t = threadIdx.x;
+  const int64_t nseg = nch * kKeyRange;
+  int32_t carry = 0;
+  for (int64_t base = 0; base < nseg; base += kRound) {
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {  // coalesced: consecutive threads, consecutive segments
+      const int64_t g = base + j * 1024 + t;
+      int32_t v = 0;
+      if (g < nseg) {
+        const int32_t* sg = seg + (g / kKeyRange) * kWideSegs * 2 + 2 * (g % kKeyRange);
+        const int32_t S = sg[1] - sg[0];
+        v = S > 0 ? 2 << dir_log2(S) : 0;
+      }
+      sz[j * 1024 + t] = v;
+    }
     __syncthreads();
-    tsum[threadIdx.x] += y;
+    int32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {  // this thread's 16 consecutive sizes -> exclusive prefix
+      const int32_t v = sz[t * kPer + j];
+      sz[t * kPer + j] = sum;
+      sum += v;
+    }
+    tsum[t] = sum;
     __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the thread sums
+      const int32_t y = t >= o ? tsum[t - o] : 0;
+      __syncthreads();
+      tsum[t] += y;
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < kPer; j++) {
+      const int i = j * 1024 + t;
+      const int64_t g = base + i;
+      const int owner = i / kPer;
+      if (g < nseg) doff[g] = carry + (owner ? tsum[owner - 1] : 0) + sz[i];
+    }
+    carry += tsum[1023];
+    __syncthreads();  // (the next round rewrites sz and tsum)
   }
-  int32_t run = tsum[threadIdx.x] - sum;
-  for (int64_t t = a; t < b; t++) {
-    doff[t] = run;
-    run += size_of(t);
-  }
-  if (threadIdx.x == 1023) doff[nseg] = tsum[1023];
+  if (t == 0) doff[nseg] = carry;
 }
 
 // The directories, from the sorted frames: frame i of a window segment is the first frame of the
