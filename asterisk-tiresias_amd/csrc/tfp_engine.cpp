@@ -173,7 +173,9 @@ struct tfp_engine {
   int64_t tiekey_ident = -1; // tiekey on the device holds the identity over this many columns (-1: not known)
   bool key_bits_valid = false;
   HostBuf vres_pin;         // pinned (VoteMeta, best[]) of the vote path
-  HostBuf spec_pin;         // pinned copy of the speculative sweep's counts (WideScratch::info)
+  HostBuf spec_pin;         // pinned copy of the speculative sweep's counts (WideScratch::info), host-mapped
+  void* spec_pin_host = nullptr;   // the allocation spec_pin_dev was taken for
+  int32_t* spec_pin_dev = nullptr; // its device address (the sweep's last kernel writes it)
   HostBuf small_res;        // host-mapped SmallResult, written by small_vote_kernel (no copy back)
   SmallResult* small_res_dev = nullptr;
   void* small_res_host = nullptr;  // the allocation small_res_dev was taken for
@@ -1259,6 +1261,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   }
   for (int pass = 0;; pass++) {
     bool spec = false;  // the sweep ran without the host reading its sort's counts (checked below)
+    bool spec_mapped = false;  // its counts were written to spec_pin by its last kernel
     if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
       // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
@@ -1270,7 +1273,17 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
                                            &e->wide, &ok, s, pass == 0));
         if (ok) {
-          HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s));
+          // a speculative sweep's counts come back through host-mapped memory, written by its last kernel
+          int32_t* d_info = nullptr;
+          if (e->wide.spec) {
+            HIPCHK(e, e->spec_pin.reserve(4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
+            if (e->spec_pin.p != e->spec_pin_host) {
+              HIPCHK(e, hipHostGetDevicePointer(reinterpret_cast<void**>(&e->spec_pin_dev), e->spec_pin.p, 0));
+              e->spec_pin_host = e->spec_pin.p;
+            }
+            d_info = e->spec_pin_dev;
+          }
+          HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s, d_info, &spec_mapped));
           done = true;
           spec = e->wide.spec;
         }
@@ -1305,8 +1318,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       }
     }
     // the speculative sweep's counts come back with the results (one host wait per batch)
-    if (spec) {
-      HIPCHK(e, e->spec_pin.reserve(4 * sizeof(int32_t)));
+    if (spec && !spec_mapped) {
+      HIPCHK(e, e->spec_pin.reserve(4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
       HIPCHK(e, hipMemcpyAsync(e->spec_pin.p, e->wide.info, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     }
     if (d_keys_out) {

@@ -275,7 +275,10 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
                                     int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s,
                                     bool speculative = false);
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
+// d_info_out (optional, device address of host-mapped memory): the clip-major sweep's last kernel
+// copies ws->info (3 ints) there; *info_written says whether it did.
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
-                            WideScratch* ws, unsigned long long* d_best, hipStream_t s);
+                            WideScratch* ws, unsigned long long* d_best, hipStream_t s, int32_t* d_info_out = nullptr,
+                            bool* info_written = nullptr);
 
 }  // namespace tfp

@@ -752,6 +752,8 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
     // this lane's runs: [lo, hi] of table entries at base + (lo..hi), value v (up to 4: L2, U2, tails)
     int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
     if (i < n) {
+      // this frame's and its predecessor's bounds requested with the key (they depend on i only)
+      const int32_t xl = L2s[i], xu = U2s[i], xlp = i > 0 ? L2s[i - 1] : 0, xup = i > 0 ? U2s[i - 1] : 0;
       const unsigned long long sgk = ck[i] >> segshift;  // chunk << 11 | segment key
       const int32_t skey = (int32_t)(sgk & (kWideSegs - 1));
       if (skey < kKeyRange) {  // (no max2 window: no searches, no directory)
@@ -764,10 +766,9 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
         const int32_t t0 = doff[ch * kKeyRange + skey];
 #pragma unroll
         for (int h = 0; h < 2; h++) {
-          const int32_t* X = h ? U2s : L2s;
           const int64_t mn = h ? u2min : l2min;
-          const int32_t bi = (int32_t)(((int64_t)X[i] - mn) >> shf);
-          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)X[i - 1] - mn) >> shf);
+          const int32_t bi = (int32_t)(((int64_t)(h ? xu : xl) - mn) >> shf);
+          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)(h ? xup : xlp) - mn) >> shf);
           base[h] = base[2 + h] = t0 + h * nbk;
           lo[h] = bp + 1, hi[h] = bi, val[h] = (int32_t)i;
           if (i == se - 1) lo[2 + h] = bi + 1, hi[2 + h] = nbk - 1, val[2 + h] = se;
@@ -1527,7 +1528,10 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
 // every 8th maximum from t >> 7, then the 8 slices in LDS).
 template <int QPL>
 __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long long* __restrict__ part, int32_t nb,
-                                                             int32_t nq, unsigned long long* __restrict__ best) {
+                                                             int32_t nq, unsigned long long* __restrict__ best,
+                                                             const int32_t* __restrict__ info, int32_t* __restrict__ info_out) {
+  // (the sweep's counts into the caller's host-mapped memory, read with the results: no copy launch)
+  if (info_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 3) info_out[threadIdx.x] = info[threadIdx.x];
   constexpr int Q = 64 * QPL, S = 1024 / Q;  // queries per chunk, slices
   __shared__ unsigned long long red[S][Q];
   // (gridDim.y workgroups per chunk, each over every gridDim.y-th slice of the maxima: a chunk's
@@ -1743,7 +1747,9 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
 }
 
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
-                            WideScratch* ws, unsigned long long* d_best, hipStream_t s) {
+                            WideScratch* ws, unsigned long long* d_best, hipStream_t s, int32_t* d_info_out,
+                            bool* info_written) {
+  if (info_written) *info_written = false;
   if (nq <= 0 || !cells || !cells->valid || !cells->k_gbeg) return hipErrorInvalidValue;
   (void)nf;
   const int64_t nch = (nq + ws->qch - 1) / ws->qch;
@@ -1776,14 +1782,15 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
                          ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
                          C, ws->doff, ws->dtab, ws->part);
       hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
-                         nq, d_best);
+                         nq, d_best, ws->info, d_info_out);
     } else {
       hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                          ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
                          C, ws->doff, ws->dtab, ws->part);
       hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
-                         nq, d_best);
+                         nq, d_best, ws->info, d_info_out);
     }
+    if (info_written) *info_written = d_info_out != nullptr;
     return hipGetLastError();
   }
   hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
