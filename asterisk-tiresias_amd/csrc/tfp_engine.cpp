@@ -1262,6 +1262,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   for (int pass = 0;; pass++) {
     bool spec = false;  // the sweep ran without the host reading its sort's counts (checked below)
     bool spec_mapped = false;  // its counts were written to spec_pin by its last kernel
+    bool out_written = false;  // the sweep wrote its keys straight into d_keys_out
     if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
       // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
@@ -1270,8 +1271,10 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         HIPCHK(e, e->wide.reserve(nf, nq, C, s));
         e->wide.clip_major = e->cells.kdir != nullptr && !e->wide.groups_form;
         bool ok = false;
+        // (a device caller's output buffer takes the sweep's keys directly: zeroed by the prepare)
+        unsigned long long* wbest = d_keys_out ? reinterpret_cast<unsigned long long*>(d_keys_out) : d_best;
         HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
-                                           &e->wide, &ok, s, pass == 0));
+                                           &e->wide, &ok, s, pass == 0, d_keys_out ? wbest : nullptr));
         if (ok) {
           // a speculative sweep's counts come back through host-mapped memory, written by its last kernel
           int32_t* d_info = nullptr;
@@ -1283,8 +1286,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
             }
             d_info = e->spec_pin_dev;
           }
-          HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, d_best, s, d_info, &spec_mapped));
+          HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, wbest, s, d_info, &spec_mapped));
           done = true;
+          out_written = d_keys_out != nullptr;
           spec = e->wide.spec;
         }
         if (e->dbg_vote) fprintf(stderr, "[tfp] general path: nq %d nf %lld C %d tol %g -> %s%s\n", nq, (long long)nf, C,
@@ -1323,7 +1327,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       HIPCHK(e, hipMemcpyAsync(e->spec_pin.p, e->wide.info, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     }
     if (d_keys_out) {
-      HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
+      if (!out_written)
+        HIPCHK(e, hipMemcpyAsync(d_keys_out, d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToDevice, s));
     } else if (nq) {
       HIPCHK(e, hipMemcpyAsync(keys.data(), d_best, sizeof(unsigned long long) * nq, hipMemcpyDeviceToHost, s));
     }

@@ -273,7 +273,7 @@ struct WideScratch {
 // window width is unknown) the counts are read back first, as before.
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
                                     int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s,
-                                    bool speculative = false);
+                                    bool speculative = false, unsigned long long* d_best_zero = nullptr);
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
 // d_info_out (optional, device address of host-mapped memory): the clip-major sweep's last kernel
 // copies ws->info (3 ints) there; *info_written says whether it did.

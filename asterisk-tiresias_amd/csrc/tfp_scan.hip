@@ -542,10 +542,13 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
 // It also zeroes the counts (info) and the segment table, which the key pass and the gather fill
 // (two fill launches fewer on the timeline).
 __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq,
-                                        int32_t* __restrict__ info, int32_t* __restrict__ seg, int64_t nseg) {
+                                        int32_t* __restrict__ info, int32_t* __restrict__ seg, int64_t nseg,
+                                        unsigned long long* __restrict__ best) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
   if (tid < 3) info[tid] = 0;
   for (int64_t i = tid; i < nseg; i += nt) seg[i] = 0;
+  if (best)  // the sweep's result keys (the caller's output buffer), maxed into from zero
+    for (int64_t i = tid; i < nq; i += nt) best[i] = 0ull;
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t q = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; q < nq; q += nw) {
@@ -1663,7 +1666,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
 
 hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff, int32_t nq, int64_t nf,
                                     int64_t max_qframes, double tole, WideScratch* ws, bool* eligible, hipStream_t s,
-                                    bool speculative) {
+                                    bool speculative, unsigned long long* d_best_zero) {
   *eligible = false;
   ws->spec = false;
   if (nq <= 0 || nf <= 0 || nf >= INT32_MAX / (4 << kDirScale) - 8 || (int64_t)nq / kWideCh >= (1 << 17) || max_qframes >= 65536)
@@ -1684,7 +1687,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   const int end_bit = (packed ? kPackChunkShift : kWideChunkShift) + cb;
   speculative = speculative && dbase >= 0 && !ws->no_spec;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
-                     0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2);
+                     0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2, d_best_zero);
   // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
   hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
                      packed, (const int32_t*)nullptr, dbase, ws->ka, packed ? (int32_t*)nullptr : ws->va, ws->info);
