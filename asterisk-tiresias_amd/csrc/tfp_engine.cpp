@@ -1268,8 +1268,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
       if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
       if (e->cells.valid) {
-        HIPCHK(e, e->wide.reserve(nf, nq, C, s));
-        e->wide.clip_major = e->cells.kdir != nullptr && !e->wide.groups_form;
+        HIPCHK(e, e->wide.reserve(nf, nq, s));
         bool ok = false;
         // (a device caller's output buffer takes the sweep's keys directly: zeroed by the prepare)
         unsigned long long* wbest = d_keys_out ? reinterpret_cast<unsigned long long*>(d_keys_out) : d_best;
@@ -1427,20 +1426,18 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
     delete e;
     return TFP_E_HIP;
   }
-  if (const char* v = getenv("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
-  e->dbg_vote = getenv("TFP_DEBUG_VOTE") != nullptr;
-  e->dbg_index = getenv("TFP_DEBUG_INDEX") != nullptr;
-  if (const char* v = getenv("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
-  e->force_full = getenv("TFP_INDEX_FULL") != nullptr;
-  if (const char* v = getenv("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
-  e->wide.points_only = getenv("TFP_WIDE_POINTS") != nullptr;
-  e->wide.groups_form = getenv("TFP_WIDE_GROUPS") != nullptr;
-  e->wide.no_spec = getenv("TFP_WIDE_SYNC") != nullptr;
-  e->wide.ch128 = getenv("TFP_WIDE_CH128") != nullptr;
-  e->wide.unpacked = getenv("TFP_WIDE_UNPACKED") != nullptr;
-  if (const char* x = getenv("TFP_CLIP_XW")) e->wide.xw_cap = atoi(x);
-  if (const char* v = getenv("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
-  if (const char* v = getenv("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
+  // test knobs (tfp::knob: only under TFP_TEST_KNOBS)
+  if (const char* v = tfp::knob("TFP_VOTE_CLASS_MAX")) e->class_ku_max = (int32_t)atoi(v);
+  e->dbg_vote = tfp::knob("TFP_DEBUG_VOTE") != nullptr;
+  e->dbg_index = tfp::knob("TFP_DEBUG_INDEX") != nullptr;
+  if (const char* v = tfp::knob("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
+  e->force_full = tfp::knob("TFP_INDEX_FULL") != nullptr;
+  if (const char* v = tfp::knob("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
+  e->wide.points_only = tfp::knob("TFP_WIDE_POINTS") != nullptr;
+  e->wide.ch128 = tfp::knob("TFP_WIDE_CH128") != nullptr;
+  e->wide.unpacked = tfp::knob("TFP_WIDE_UNPACKED") != nullptr;
+  if (const char* v = tfp::knob("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
+  if (const char* v = tfp::knob("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;
@@ -1665,7 +1662,7 @@ static bool injected_add_batch_failure() {
   static std::mutex mu;
   static std::string val;
   static int64_t calls = 0;
-  const char* v = getenv("TFP_TEST_FAIL_ADD_BATCH");
+  const char* v = tfp::knob("TFP_TEST_FAIL_ADD_BATCH");
   std::lock_guard<std::mutex> lk(mu);
   if (!v) return false;
   if (val != v) {

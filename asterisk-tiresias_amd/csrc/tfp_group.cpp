@@ -39,6 +39,7 @@
 #include "../../include/tiresias_fp.h"
 #include "tfp_coalesce.hpp"
 #include "tfp_internal.hpp"
+#include "tfp_kernels.hpp"
 #include "tfp_shardpool.hpp"
 
 namespace {
@@ -341,7 +342,7 @@ int tfp_group_create(const int32_t* devices, int32_t n, tfp_group** out) {
   g->rows.assign(n, 0);
   g->bufs.resize(n);
   g->pool = new tfp::ShardPool(n);
-  if (const char* v = getenv("TFP_COALESCE")) g->coalesce = atoi(v) != 0;
+  if (const char* v = tfp::knob("TFP_COALESCE")) g->coalesce = atoi(v) != 0;
   *out = g;
   return TFP_OK;
 }
@@ -675,7 +676,7 @@ int tfp_group_stream_create(tfp_group* g, int32_t nch, int32_t sr, int64_t W, tf
   st->g = g;
   st->nch = nch;
   st->W = W;
-  const char* mode = getenv("TFP_GROUP_STREAM");
+  const char* mode = tfp::knob("TFP_GROUP_STREAM");
   st->split = n > 1 && !(mode && !strcmp(mode, "replicate"));
   st->st.assign(n, nullptr);
   if (st->split) {

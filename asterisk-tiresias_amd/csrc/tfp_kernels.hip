@@ -99,11 +99,6 @@ struct LdsTables {
   LogfEntry logf[16];
   LogfEntry logf2[kLogf2Entries];  // (invc, y0) for aubio_log10_frexp (tfp_log.hpp)
   int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
-  // frame-pair filterbank jobs per pattern and segment (12-wave workgroups read them per double
-  // pass): bin offset in a pair row, band-sum index, 0 where the segment starts a job (else 1)
-  alignas(16) int32_t fb_boff[16][4];
-  alignas(16) int32_t fb_sidx[16][4];
-  alignas(16) float fb_k[16][4];
   union {
     alignas(16) float ms_w[kMsLds];                  // slot schedule (fingerprint_kernel, fingerprint8k_kernel<1>)
     alignas(16) float fbw[kFbSteps * kFbPatterns];  // frame-pair schedule (fingerprint8k_kernel<4>)
@@ -158,39 +153,13 @@ static_assert(2 * 5 * kHopStride <= sizeof(cf) * 4 * kFrameStride8 && 48 + 260 <
 static_assert(2 * kFbRow <= 2 * 4 * kFrameStride8 && 2 * kFbRowBins <= kFbRow && kWaveFrames * kFbNf <= kWaveFrames * kLogStride,
               "frame-pair rows");
 static_assert(kFbSegs == 4, "fb_seg");
-// The throughput kernel's workgroup: TFP_FP8_BLOCK_WAVES waves (4, or 12 = one workgroup of three
-// waves per SIMD). At 12 waves a wave's LDS is cut to fit 160 KiB: its transposes run in two
-// rounds of two frames through two padded squares (WaveLds8P; the same LDS reads and writes,
-// issued per half wave), and the band sums are kept compact (kFbNf per row).
-#ifndef TFP_FP8_BLOCK_WAVES
-#define TFP_FP8_BLOCK_WAVES 4
-#endif
-#ifndef TFP_FP8_WAVES
-#define TFP_FP8_WAVES TFP_FP_WAVES
-#endif
-#ifndef TFP_FP8_HALF_SQ
-#define TFP_FP8_HALF_SQ (TFP_FP8_BLOCK_WAVES > 4)
-#endif
-constexpr int kBW8 = TFP_FP8_BLOCK_WAVES;
-#ifndef TFP_FP8_INLINE_EDGE
-#define TFP_FP8_INLINE_EDGE 0
-#endif
-constexpr bool kInlineEdge8 = TFP_FP8_INLINE_EDGE;
-constexpr bool kHalfSq = TFP_FP8_HALF_SQ;
-static_assert(kBW8 == 4 || kBW8 == 8 || kBW8 == 12, "8 kHz workgroup");
-struct WaveLds8P {
-  union {
-    cf scratch[2][kFrameStride8];
-    alignas(16) int16_t pcm[5 * kHopStride];
-  };
-  alignas(16) float xeven[2 * kFbRow];
-  float logs[kWaveFrames * kFbNf];
-};
-static_assert(2 * 5 * kHopStride <= sizeof(cf) * 2 * kFrameStride8 && 2 * kFbRow <= 2 * 2 * kFrameStride8 &&
-                  2 * kFbNf * 7 + 68 <= 2 * kFrameStride8,
-              "half-square scratch: PCM, the odd pass's |X| rows, the tail's products");
+// The throughput kernel's workgroup: 4 waves (two workgroups per CU, two waves per SIMD). A
+// bit-exact 12-wave form (three waves per SIMD, transposes through half squares to fit the LDS)
+// measured 0.469 vs 0.442 ms per C2 launch in round 4 and was removed in round 5.
+constexpr int kBW8 = 4;
 template <int kPasses>
 constexpr int fp8_block_waves() { return kPasses >= 2 ? kBW8 : kBlockWaves; }
+static_assert(kBW8 == kBlockWaves, "one workgroup shape");
 constexpr int fb_seg(int s) { return s < kFbSegStart[1] ? 0 : s < kFbSegStart[2] ? 1 : s < kFbSegStart[3] ? 2 : 3; }
 
 // Where a pass of 4 frames reads: the clip's samples [(f_first - 1) * 256, (f_first + 4) * 256).
@@ -211,9 +180,6 @@ struct SmpLayout {
   static constexpr int kHopChunks = kHop / kPer;              // chunks per staged hop
 };
 
-#ifndef TFP_FP_CHECKED_FAST
-#define TFP_FP_CHECKED_FAST 1
-#endif
 // Slow path of one 16-byte chunk: clip edges (zeros outside [0, ns): aubio_source pads the last
 // hop, the phase vocoder's first history hop is zeros) and unaligned clips.
 __device__ __noinline__ int4 fetch_chunk_checked(const float* clip, int64_t ns, int64_t s) {
@@ -224,7 +190,7 @@ __device__ __noinline__ int4 fetch_chunk_checked(const float* clip, int64_t ns, 
 }
 __device__ __noinline__ int4 fetch_chunk_checked(const int16_t* clip, int64_t ns, int64_t s) {
   // an aligned chunk wholly inside the clip (most of an edge pass's): one 16-byte load
-  if (TFP_FP_CHECKED_FAST && s >= 0 && s + 8 <= ns && (reinterpret_cast<uintptr_t>(clip + s) & 15) == 0)
+  if (s >= 0 && s + 8 <= ns && (reinterpret_cast<uintptr_t>(clip + s) & 15) == 0)
     return *reinterpret_cast<const int4*>(clip + s);
   uint32_t w[4];
   for (int e = 0; e < 4; e++) {
@@ -766,7 +732,7 @@ __device__ __forceinline__ void load_w(const float* __restrict__ w, float4 (&wv)
 // kPasses = passes of 4 frames per tile: 4 (16-frame tiles, throughput) or 1 (4-frame tiles, for
 // small batches: 4x the waves on a short query, a quarter of the per-wave latency).
 template <int kPasses>
-__global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP_FP8_WAVES : TFP_FP_WAVES) void fingerprint8k_kernel(
+__global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void fingerprint8k_kernel(
     const DspTables* __restrict__ T, const int16_t* __restrict__ pcm, const int64_t* __restrict__ sbeg,
     const int64_t* __restrict__ send, const int64_t* __restrict__ foff, const int32_t* __restrict__ toff,
     const int32_t* __restrict__ tclip, int32_t ntiles, int32_t* __restrict__ micro, double* __restrict__ db,
@@ -782,8 +748,7 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   // filterbank weights: the frame-pair schedule (throughput) or the slot schedule (small tiles)
   constexpr bool kPairFb = kPasses >= 2;
   constexpr int kBW = fp8_block_waves<kPasses>();
-  constexpr bool kHalf = kPairFb && kHalfSq;
-  using WaveT = std::conditional_t<kHalf, WaveLds8P, WaveLds8>;
+  using WaveT = WaveLds8;
   __shared__ __attribute__((aligned(16))) LdsTables S;
   __shared__ __attribute__((aligned(16))) WaveT WL[kBW];
   const int tid = threadIdx.x;
@@ -821,11 +786,10 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
         const int chunk = lane + 64 * r;
         pf[r] = (64 * r + 63 < kPassChunks || chunk < kPassChunks) ? src[chunk] : make_int4(0, 0, 0, 0);
       }
-    } else if constexpr (kPasses == 1 || kInlineEdge8) {
-      // clip edges of a small launch (its PCM may be across PCIe), or of any launch with
-      // TFP_FP8_INLINE_EDGE (short clips, such as the 5 s queries of a search batch, spend a
-      // twentieth of their passes on edges): chunks wholly inside are one 16-byte load, wholly
-      // outside zeros, no call (a call waits for every outstanding load)
+    } else if constexpr (kPasses == 1) {
+      // clip edges of a small launch (its PCM may be across PCIe): chunks wholly inside are one
+      // 16-byte load, wholly outside zeros, no call (a call waits for every outstanding load).
+      // (Throughput launches inline too measured within noise: profiles/r04/edge_fetch_ab_r04m.txt.)
       const bool aligned = (reinterpret_cast<uintptr_t>(clip) & 15) == 0;
 #pragma unroll
       for (int r = 0; r < kChunkRounds; r++) {
@@ -862,8 +826,7 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   // Table staging: every global load below is issued before any LDS write (indices clamped,
   // writes predicated), so a block waits for one round trip instead of one per table: a small
   // launch is latency-bound.
-  // The first 256 threads stage (one entry per thread per table); a 12-wave workgroup's others
-  // read clamped copies of the same entries and write nothing.
+  // The first 256 threads stage (one entry per thread per table).
   constexpr int kStage = 256;
   const int ts = tid < kStage ? tid : kStage - 1;
   const bool stager = tid < kStage;
@@ -911,12 +874,6 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   if (tid < 3) { S.ms_len[tid] = msl; S.ms_woff[tid] = mso; }
   if (tid < 16) S.logf[tid] = lge;
   if (kPairFb && tid < kLogf2Entries) S.logf2[tid] = logf2_entry(tid, logf_table());
-    if (kPairFb && tid < 64) {
-      const int pl = tid >> 2, pk = tid & 3;
-      S.fb_boff[pl][pk] = 2 * (T->fb_bin[pl][pk] - kFbSegStart[pk]);
-      S.fb_sidx[pl][pk] = T->fb_filter[pl][pk];
-      S.fb_k[pl][pk] = T->fb_new[pl][pk] ? 0.f : 1.f;
-    }
   if (tid == 0) { S.c_defer = T->ms_c_defer; S.c_real[0] = T->ms_c_real[0]; S.c_real[1] = T->ms_c_real[1]; }
 #pragma unroll
     for (int r = 0; r < (kMsW + kStage - 1) / kStage; r++) {
@@ -931,7 +888,7 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
 #endif
 
   WaveT& M = WL[wave];
-  cf* W = M.scratch[kHalf ? (grp & 1) : grp];
+  cf* W = M.scratch[grp];
   float* N = reinterpret_cast<float*>(W) + 48 * (grp & 1);  // |X| row (WaveLds8)
   const int nwaves = gridDim.x * kBW;
   const int maxbin = T->ms_maxbin;
@@ -944,12 +901,9 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   for (int e = 0; e < 10; e++)
     w16r[e] = cf{T->tw256_re[16 * e], T->tw256_im[16 * e]};
   // inter-stage lane twiddles w256^(L k1) held in registers (30 VGPRs) instead of read per pass
-  // (at 12-wave workgroups read per pass from LDS instead: the register budget is 168)
-  cf ltw[kHalf ? 1 : 15];
-  if constexpr (!kHalf) {
+  cf ltw[15];
 #pragma unroll
-    for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
-  }
+  for (int k1 = 1; k1 < 16; k1++) ltw[k1 - 1] = S.lane_tw[k1 - 1][L];
   const float lempty = aubio_log10_fast(0.f, S.logf);  // log of an empty filter's clamped 0
   if constexpr (!kPairFb) {
     for (int i = lane; i < 4 * kPasses * kFilters; i += 64) {
@@ -962,10 +916,9 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
   // s reads the bins at fbb[k] + 2 s), where the job's raw sums go (frames 2 grp, 2 grp + 1 of
   // double pass 0: rows 4 grp, 4 grp + 2; double pass 1 one row on), and 0 where the segment
   // starts a job (acc = fma(acc, 0, p) = p; 1: acc + p).
-  constexpr int kFbS = kHalf ? 1 : kFbSegs;  // (12-wave workgroups: read per double pass)
-  const float* fbb[kFbS];
-  float* fbc[kFbS];
-  float fbk[kFbS];
+  const float* fbb[kFbSegs];
+  float* fbc[kFbSegs];
+  float fbk[kFbSegs];
   cf dctl, dct9;  // the DCT weights (rows 0, 1) of this lane's filter in the tail's log rounds
   const float* const fbrow = (grp < 2 ? M.xeven : reinterpret_cast<const float*>(M.scratch)) + (grp & 1) * kFbRow;
   float* const fblog = M.logs + 4 * grp * kFbNf;
@@ -973,13 +926,11 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
     const int lf = lane < kFbNf ? lane : lane - kFbNf, l9 = kFbNf - 4 + (lane & 3);
     dctl = cf{S.dct[0][lf], S.dct[1][lf]};
     dct9 = cf{S.dct[0][l9], S.dct[1][l9]};
-    if constexpr (!kHalf) {
 #pragma unroll
-      for (int k = 0; k < kFbSegs; k++) {
-        fbb[k % kFbS] = fbrow + 2 * (T->fb_bin[L][k] - kFbSegStart[k]);
-        fbc[k % kFbS] = fblog + T->fb_filter[L][k];
-        fbk[k % kFbS] = T->fb_new[L][k] ? 0.f : 1.f;
-      }
+    for (int k = 0; k < kFbSegs; k++) {
+      fbb[k] = fbrow + 2 * (T->fb_bin[L][k] - kFbSegStart[k]);
+      fbc[k] = fblog + T->fb_filter[L][k];
+      fbk[k] = T->fb_new[L][k] ? 0.f : 1.f;
     }
   }
 
@@ -1032,37 +983,17 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
       }
       dft16q(w16r, z, Y);
 #pragma unroll
-      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], kHalf ? S.lane_tw[k1 - 1][L + oz] : ltw[(k1 - 1) % (kHalf ? 1 : 15)]);
+      for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
       wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
       TFP_STAMP(2);
-      if constexpr (kHalf) {  // frames 0, 1 then 2, 3 through the two squares
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-          if (h) wave_sync();  // the first round's reads are done before the second's writes
-          if ((grp >> 1) == h) {
+      for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
+      wave_sync();
 #pragma unroll
-            for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
-          }
-          wave_sync();
-          if ((grp >> 1) == h) {
-#pragma unroll
-            for (int n2 = 0; n2 < 16; n2 += 2) {
-              const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
-              z[n2] = cf{v.x, v.y};
-              z[n2 + 1] = cf{v.z, v.w};
-            }
-          }
-        }
-      } else {
-#pragma unroll
-        for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
-        wave_sync();
-#pragma unroll
-        for (int n2 = 0; n2 < 16; n2 += 2) {
-          const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
-          z[n2] = cf{v.x, v.y};
-          z[n2 + 1] = cf{v.z, v.w};
-        }
+      for (int n2 = 0; n2 < 16; n2 += 2) {
+        const float4 v = *reinterpret_cast<const float4*>(W + L * kSq8 + n2);
+        z[n2] = cf{v.x, v.y};
+        z[n2 + 1] = cf{v.z, v.w};
       }
       dft16q(w16r, z, Y);  // Y[k2] = Z[L + 16 k2]
       wave_sync();         // every lane has read its column of the square: W is free for |X|
@@ -1161,20 +1092,11 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), kPasses >= 2 ? TFP
           const float* jb[kFbSegs];
           float* jc[kFbSegs];
           float jk[kFbSegs];
-          if constexpr (kHalf) {
-            const int4 bo = *reinterpret_cast<const int4*>(&S.fb_boff[L][0] + oz);
-            const int4 si = *reinterpret_cast<const int4*>(&S.fb_sidx[L][0] + oz);
-            const float4 kk = *reinterpret_cast<const float4*>(&S.fb_k[L][0] + oz);
-            jb[0] = fbrow + bo.x; jb[1] = fbrow + bo.y; jb[2] = fbrow + bo.z; jb[3] = fbrow + bo.w;
-            jc[0] = fblog + si.x; jc[1] = fblog + si.y; jc[2] = fblog + si.z; jc[3] = fblog + si.w;
-            jk[0] = kk.x; jk[1] = kk.y; jk[2] = kk.z; jk[3] = kk.w;
-          } else {
 #pragma unroll
-            for (int k = 0; k < kFbSegs; k++) {
-              jb[k] = fbb[k % kFbS];
-              jc[k] = fbc[k % kFbS];
-              jk[k] = fbk[k % kFbS];
-            }
+          for (int k = 0; k < kFbSegs; k++) {
+            jb[k] = fbb[k];
+            jc[k] = fbc[k];
+            jk[k] = fbk[k];
           }
           // a step pair's weights: one ds_read_b64 each, whose halves the packed multiplies
           // broadcast with op_sel (a b128 of 4 steps made the compiler move the halves apart)
@@ -1334,7 +1256,7 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
   cfg->grid_cap_8k_small = cap(reinterpret_cast<const void*>(fingerprint8k_kernel<1>));
   cfg->grid_cap_generic = cap(reinterpret_cast<const void*>(fingerprint_kernel<int16_t>));
   cfg->grid_cap_f32 = cap(reinterpret_cast<const void*>(fingerprint_kernel<float>));
-  if (getenv("TFP_DEBUG_OCC")) {
+  if (knob("TFP_DEBUG_OCC")) {
     int per = 0;
     (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(fingerprint8k_kernel<kTile8k / 4>),
                                                        64 * kBW8, 0);
@@ -1351,13 +1273,13 @@ hipError_t fp_launch_config(int device, FpLaunchCfg* cfg) {
   }
   // TFP_FP_BLOCKS_PER_CU (experiments): fewer resident workgroups per CU for the 8 kHz throughput
   // kernel (1 = one wave per SIMD), to measure how its time scales with the waves per SIMD
-  if (const char* b = getenv("TFP_FP_BLOCKS_PER_CU")) {
+  if (const char* b = knob("TFP_FP_BLOCKS_PER_CU")) {
     const int n = atoi(b);
     if (n > 0 && cus * n < cfg->grid_cap_8k) cfg->grid_cap_8k = cus * n;
   }
-  const char* g = getenv("TFP_GENERIC");
+  const char* g = knob("TFP_GENERIC");
   cfg->force_generic = g && atoi(g);
-  const char* rt = getenv("TFP_RARE_THR_LOG2");
+  const char* rt = knob("TFP_RARE_THR_LOG2");
   int rl = rt ? atoi(rt) : -98;
   rl = rl < -98 ? -98 : (rl > 100 ? 100 : rl);  // any threshold >= 2^-98 gives the same, exact, result
   cfg->rare_thr = ldexpf(1.f, rl);

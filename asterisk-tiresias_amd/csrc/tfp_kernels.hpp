@@ -2,11 +2,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 
 #include "tfp_math.hpp"
 #include "tfp_tables.hpp"
 
 namespace tfp {
+
+// Test and diagnostic knobs (TFP_GENERIC, TFP_WIDE_POINTS, TFP_INDEX_FULL, ...): each forces a
+// form that some input reaches on its own, or injects a failure, so the -m gpu suite can run every
+// form against the oracle. They are read only when TFP_TEST_KNOBS is set (tests/conftest.py sets
+// it), so the environment of a production process cannot change which kernel a search runs.
+inline const char* knob(const char* name) {
+  const char* on = getenv("TFP_TEST_KNOBS");
+  return on && *on && strcmp(on, "0") != 0 ? getenv(name) : nullptr;
+}
 
 constexpr int kFramesPerBlock = 16;   // frames per wave tile of the generic kernel (16 lanes per frame)
 // Frames per wave tile of fingerprint8k_kernel's throughput launches. 16: the tile tail (deferred
@@ -188,10 +199,7 @@ struct CellCache {
   int32_t* c_hi = nullptr;                 // [nc] last point of each cluster
   int32_t* c_beg = nullptr;                // [n1 + 1] first cluster of each group
   // the clip-major sweep's directory: kdir[k][w] = first group of key k with column >= kWin w
-#ifndef TFP_CLIP_WIN
-#define TFP_CLIP_WIN 16
-#endif
-  static constexpr int32_t kWin = TFP_CLIP_WIN;
+  static constexpr int32_t kWin = 16;
   int32_t* kdir = nullptr;                 // [kKeyRange][nwin + 1]
   int32_t nwin = 0;                        // ceil(columns / kWin)
   int64_t S = 0, n1 = 0, n2 = 0, w = 0, nc = 0, dgap = 0;
@@ -212,14 +220,14 @@ hipError_t launch_scan(const FrameBox* boxes, const int64_t* d_qoff, const int64
                        const int32_t* d_tiekey, int32_t C, int32_t* d_stamp, int32_t* d_score, int32_t* d_touched,
                        int32_t* d_tcnt, unsigned long long* d_best, hipStream_t s);
 
-// The general path's sweep by groups (tfp_scan.hip): every query frame of
-// the batch sorted by (128-query chunk, key, max2 window); per chunk, one wave per clip group of
-// each key the chunk uses counts, for the chunk's 128 queries at once, the frames whose window
-// holds one of the group's points (prefix counts over the sorted frames), so its work follows
-// the groups, not the hits. Needs every frame's key inside the clip-set cache.
+// The general path's sweep by groups (tfp_scan.hip): every query frame of the batch sorted by
+// (query chunk, key, max2 window); per chunk and window of 16 clip columns, one wave counts, for
+// the chunk's 128 or 256 queries at once, the frames whose window holds one of each clip group's
+// points (prefix counts over the sorted frames), so its work follows the groups, not the hits.
+// Needs every frame's key inside the clip-set cache.
 struct WideScratch {
   static constexpr int32_t kChunk = 128;  // queries per chunk: two per lane (a word of two 16-bit counts)
-  // all sized by wide_reserve for nf frames, nq queries, C clips
+  // all sized by reserve for nf frames and nq queries
   unsigned long long *ka = nullptr, *kb = nullptr;  // sort keys
   uint32_t *ua = nullptr, *ub = nullptr;
   int32_t *va = nullptr, *vb = nullptr;             // frame indices
@@ -229,11 +237,7 @@ struct WideScratch {
   uint32_t* P = nullptr;                             // [nf][kChunk / 2] in-chunk prefix counts, 16-bit pairs (< 2^16: every query < 65536 frames)
   uint32_t* ptot = nullptr;                          // [nchunks][256][kChunk / 2] the prefix counts' per-share totals, then their prefix
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
-  int32_t* wpre = nullptr;                           // [nchunks][kKeyRange + 1] work prefix
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk
-  int64_t* chw = nullptr;                            // [nchunks + 1] first work item of each chunk
-  uint32_t* score = nullptr;                         // [slab][C][kChunk / 2] 16-bit pairs, zero between calls
-  uint8_t* touch = nullptr;                          // [slab][C] 1 = the chunk scored the clip; zero between calls
   int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
   int32_t* doff = nullptr;                           // [nchunks * kKeyRange + 1] each window segment's directory offset
   int32_t* dtab = nullptr;                           // [<= 4 nf] segment directories: first frame per L2 / U2 bucket
@@ -241,22 +245,18 @@ struct WideScratch {
   size_t tmp_bytes = 0;
   void* dtmp = nullptr;                              // the directory offsets' scan
   size_t dtmp_bytes = 0;
-  int64_t cap_nf = 0, cap_nch = 0, cap_score = 0, cap_dtab = 0;
-  int32_t slab = 0;                                  // chunks per groups launch
+  int64_t cap_nf = 0, cap_nch = 0, cap_dtab = 0;
   int64_t min_width = -1;                            // prepare: every max2 window is at least this wide (-1: unknown)
   bool spec = false;                                 // prepare ran without reading info back: the caller checks it with the results
-  bool no_spec = false;                              // TFP_WIDE_SYNC (A/B): read the counts back before the sweep
-  bool points_only = false;                          // TFP_WIDE_POINTS (tests, A/B): search points, not clusters
-  bool groups_form = false;                          // TFP_WIDE_GROUPS (tests, A/B): the key-major sweep with score rows
-  bool ch128 = false;                                // TFP_WIDE_CH128 (tests, A/B): 128-query chunks only
-  bool unpacked = false;                             // TFP_WIDE_UNPACKED (tests, A/B): sort (key, frame) pairs, no packed key
-  bool clip_major = true;                            // set by the caller before prepare: the clip-major sweep will run
+  // test knobs (TFP_TEST_KNOBS; each forces a form that other batches reach on their own):
+  bool points_only = false;                          // TFP_WIDE_POINTS: search points, not clusters
+  bool ch128 = false;                                // TFP_WIDE_CH128: 128-query chunks only
+  bool unpacked = false;                             // TFP_WIDE_UNPACKED: sort (key, frame) pairs, no packed key
   int32_t qch = kChunk;                              // prepare: queries per chunk of this batch (128, or 256 with 8-bit counts)
-  int32_t xw_cap = 0;                                // TFP_CLIP_XW (A/B): clip-major waves per chunk (0: 1024 per 128 queries)
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
   int32_t* nuk = nullptr;                            // [nchunks] their number
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima
-  hipError_t reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s);
+  hipError_t reserve(int64_t nf, int32_t nq, hipStream_t s);
   void release();
   WideScratch() = default;
   WideScratch(const WideScratch&) = delete;
@@ -265,7 +265,7 @@ struct WideScratch {
 };
 // Sorts the batch's frames; *eligible = false (nothing else queued) when a frame needs the row
 // scan (key outside the cache, window outside int32) or a query has 2^16 frames or more (the
-// score rows hold 16-bit counts), the caller then takes launch_scan.
+// counts are 16-bit), the caller then takes launch_scan.
 // speculative: no host wait for the sort's counts (the sweep's kernels read the kept-frame count
 // on the device); ws->spec is then set, and the caller reads ws->info with the results: a batch
 // with info[1] > 0 (a frame for the row scan) or info[2] > 0 (a window width outside the sort key's

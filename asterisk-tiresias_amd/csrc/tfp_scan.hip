@@ -872,63 +872,6 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   }
 }
 
-// Per chunk: the work list over the groups of every key the chunk's frames use (exclusive prefix
-// of the keys' group counts), one block per chunk.
-__global__ __launch_bounds__(256) void wide_work_kernel(const int32_t* __restrict__ seg, const int32_t* __restrict__ k_gbeg,
-                                                        int32_t* __restrict__ wpre) {
-  __shared__ int32_t part[256];
-  const int ch = blockIdx.x, t = threadIdx.x;
-  const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
-  int32_t n[kKeyRange / 256], sum = 0;
-#pragma unroll
-  for (int j = 0; j < kKeyRange / 256; j++) {
-    const int kk = t * (kKeyRange / 256) + j;
-    const bool used = sg[2 * kk + 1] > sg[2 * kk] || sg[2 * (kk | kKeyRange) + 1] > sg[2 * (kk | kKeyRange)];
-    n[j] = used ? k_gbeg[kk + 1] - k_gbeg[kk] : 0;
-    sum += n[j];
-  }
-  part[t] = sum;
-  __syncthreads();
-  for (int o = 1; o < 256; o <<= 1) {  // inclusive scan of the per-thread sums
-    const int32_t y = t >= o ? part[t - o] : 0;
-    __syncthreads();
-    part[t] += y;
-    __syncthreads();
-  }
-  int32_t run = part[t] - sum;
-  int32_t* wp = wpre + (int64_t)ch * (kKeyRange + 1);
-#pragma unroll
-  for (int j = 0; j < kKeyRange / 256; j++) {
-    wp[t * (kKeyRange / 256) + j] = run;
-    run += n[j];
-  }
-  if (t == 255) wp[kKeyRange] = part[255];
-}
-
-// Exclusive prefix of the chunks' work counts (wpre[ch][kKeyRange]): chw[0..nch], one block.
-__global__ __launch_bounds__(1024) void wide_chw_kernel(const int32_t* __restrict__ wpre, int64_t nch,
-                                                        int64_t* __restrict__ chw) {
-  __shared__ int64_t part[1024];
-  const int t = threadIdx.x;
-  int64_t carry = 0;
-  for (int64_t c0 = 0; c0 < nch; c0 += 1024) {
-    const int64_t c = c0 + t;
-    const int64_t v = c < nch ? (int64_t)wpre[c * (kKeyRange + 1) + kKeyRange] : 0;
-    part[t] = v;
-    __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
-      const int64_t y = t >= o ? part[t - o] : 0;
-      __syncthreads();
-      part[t] += y;
-      __syncthreads();
-    }
-    if (c < nch) chw[c] = carry + part[t] - v;
-    carry += part[1023];
-    __syncthreads();
-  }
-  if (t == 0) chw[nch] = carry;
-}
-
 __device__ __forceinline__ int32_t lb32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] >= v
   int32_t lo = 0, hi = n;
   while (lo < hi) {
@@ -946,270 +889,14 @@ __device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) 
   return lo;
 }
 
-// The work items (chunk, key, clip group) of chunks [ch0, ch1), in chunk and key order; each wave
-// takes a contiguous share, so it locates its first item by binary search and then steps through
-// keys and chunks. Lane l = queries 128 ch + 2l, 128 ch + 2l + 1 (a word of two 16-bit counts). A
-// group's counts go to the slab's score rows as those words.
-__global__ __launch_bounds__(256) void wide_groups_kernel(int32_t ch0, int32_t ch1, const int64_t* __restrict__ chw,
-                                                          const int32_t* __restrict__ wpre, const int32_t* __restrict__ seg,
-                                                          const int32_t* __restrict__ cbeg, CellView cv,
-                                                          const int32_t* __restrict__ k_gbeg, const int32_t* __restrict__ L2s,
-                                                          const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
-                                                          int32_t C, uint32_t* __restrict__ score, uint8_t* __restrict__ touch,
-                                                          const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab) {
-  const int lane = threadIdx.x & 63;
-  const int64_t W0 = chw[ch0], W1 = chw[ch1];
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t per = (W1 - W0 + nw - 1) / nw;
-  int64_t t = W0 + (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * per;
-  const int64_t tend = min(W1, t + per);
-  if (t >= tend) return;
-  int ch = ch0;
-  {
-    int hi = ch1;  // the last chunk with chw[ch] <= t
-    while (hi - ch > 1) {
-      const int mid = (ch + hi) >> 1;
-      if (chw[mid] <= t) ch = mid; else hi = mid;
-    }
-  }
-  const int32_t* wp = wpre + (int64_t)ch * (kKeyRange + 1);
-  int32_t tt = (int32_t)(t - chw[ch]);
-  int kk = 0;
-  {
-    int hi = kKeyRange;  // the last key with wp[kk] <= tt
-    while (hi - kk > 1) {
-      const int mid = (kk + hi) >> 1;
-      if (wp[mid] <= tt) kk = mid; else hi = mid;
-    }
-  }
-  int32_t kend = wp[kk + 1];
-  bool fresh = true;
-  int32_t sb = 0, se = 0, gk0 = 0;
-  uint32_t base = 0, fcnt = 0;
-  int32_t nbk = 1, shf = 0, l2min = 0, u2min = 0;  // the segment's directory
-  const int32_t* TL = dtab;
-  auto add_score = [&](int32_t col, uint32_t cnt) {
-#ifdef TFP_EXP_NO_SCORE  // timing experiment only (wrong results): the groups' work without its score writes
-    if (cnt == 12345u) score[0] = col;
-    return;
-#endif
-    if (cnt) atomicAdd(&score[((int64_t)(ch - ch0) * C + col) * kWideW + lane], cnt);
-    // the chunk's touched-clip bytes (plain stores, idempotent): wide_final reads only those rows
-    if (__ballot(cnt != 0) && lane == 0) touch[(int64_t)(ch - ch0) * C + col] = 1;
-  };
-  // an item's run in the segment: A = first frame with U2 >= va, B = last frame with L2 <= vb (an
-  // item is a point, va = vb, or a cluster, va its first and vb its last point)
-  auto find_ab = [&](int32_t va, int32_t vb, int32_t& A, int32_t& B) {
-    const int32_t v = vb;
-    const int64_t dv = (int64_t)v - l2min;
-    if (dv < 0) {
-      B = sb - 1;
-    } else {
-      const int32_t b = (int32_t)min<int64_t>(dv >> shf, nbk - 1);
-      const int32_t lo = TL[b], hi = b + 1 < nbk ? TL[b + 1] : se;
-      B = lo + ub32(L2s + lo, hi - lo, v) - 1;
-    }
-    const int64_t du = (int64_t)va - u2min;
-    if (du <= 0) {
-      A = sb;
-    } else {
-      const int32_t b = (int32_t)min<int64_t>(du >> shf, nbk - 1);
-      const int32_t lo = TL[nbk + b], hi = b + 1 < nbk ? TL[nbk + b + 1] : se;
-      A = lo + lb32(U2s + lo, hi - lo, va);
-    }
-  };
-  auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
-    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
-  };
-  while (t < tend) {
-    while (tt >= kend) {  // past this key's items: the next key with items, or the next chunk
-      if (++kk == kKeyRange) {
-        ++ch;
-        wp += kKeyRange + 1;
-        tt = (int32_t)(t - chw[ch]);
-        kk = 0;
-      }
-      kend = wp[kk + 1];
-      fresh = true;
-    }
-    if (fresh) {
-      fresh = false;
-      const int32_t* sg = seg + (int64_t)ch * kWideSegs * 2;
-      const int32_t cb = cbeg[ch];
-      sb = sg[2 * kk];
-      se = sg[2 * kk + 1];
-      const int32_t fb = sg[2 * (kk | kKeyRange)], fe = sg[2 * (kk | kKeyRange) + 1];
-      base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
-      fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
-      gk0 = k_gbeg[kk] - wp[kk];
-      if (se > sb) {
-        const int lg = dir_log2(se - sb);
-        nbk = 1 << lg;
-        l2min = L2s[sb];
-        u2min = U2s[sb];
-        shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
-        TL = dtab + doff[(int64_t)ch * kKeyRange + kk];
-      }
-    }
-    const int32_t g0 = gk0 + tt;
-    if (se <= sb) {  // no frame of the segment has a max2 window: every group scores the rest
-      add_score((int32_t)(cv.g_key[g0] & kColMask), fcnt);
-      t++, tt++;
-      continue;
-    }
-    // A batch of consecutive groups of this segment whose points fit the 64 lanes: lane j holds
-    // group j's point range [pj0, pj1) relative to the first point pb0.
-    const int64_t left = min(tend - t, (int64_t)(kend - tt));
-    const int32_t pb0 = cv.g_beg[g0];
-    int32_t pj0 = 0, pj1 = INT32_MAX, colj = 0;
-    if (lane < left) {
-      pj0 = cv.g_beg[g0 + lane] - pb0;
-      pj1 = cv.g_beg[g0 + lane + 1] - pb0;
-      colj = (int32_t)(cv.g_key[g0 + lane] & kColMask);
-    }
-    const int nG = __popcll(__ballot(lane < left && pj1 <= 64));  // (pj1 grows with j: a prefix)
-    if (nG == 0) {
-      // one group with more than 64 points: its points 64 at a time, runs merged across the steps
-      const int32_t pn = __shfl(pj1, 0, 64);
-      uint32_t cnt = fcnt;
-      int32_t carry = -2, aopen = 0;
-      bool open = false;
-      for (int32_t pbase = 0; pbase < pn; pbase += 64) {
-        const int32_t i = pbase + lane;
-        int32_t A = INT32_MAX, B = -2;
-        if (i < pn) find_ab(cv.p_m2[pb0 + i], cv.p_hi[pb0 + i], A, B);
-        const bool ok = A <= B;
-        int32_t bm = ok ? B : -2;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {  // inclusive running max of B over the valid runs
-          const int32_t y = __shfl_up(bm, o, 64);
-          if (lane >= o) bm = max(bm, y);
-        }
-        int32_t pe = __shfl_up(bm, 1, 64);
-        if (lane == 0) pe = -2;
-        pe = max(pe, carry);  // the largest B before this lane's run
-        unsigned long long starts = __ballot(ok && A > pe + 1);  // a gap before it: a new merged run
-        while (starts) {
-          const int sl = __ffsll((long long)starts) - 1;
-          starts &= starts - 1;
-          const int32_t as = __shfl(A, sl, 64), ps = __shfl(pe, sl, 64);
-          if (open) close_run(cnt, aopen, ps);
-          open = true;
-          aopen = as;
-        }
-        carry = max(carry, __shfl(bm, 63, 64));
-      }
-      if (open) close_run(cnt, aopen, carry);
-      add_score(__shfl(colj, 0, 64), cnt);
-      t++, tt++;
-      continue;
-    }
-    // every point of the batch on its own lane: its group (the last j < nG with pj0 <= lane, by
-    // binary lifting over the lanes' starts) and its run [A, B] of the segment's frames
-    const int32_t npts = __shfl(pj1, nG - 1, 64);
-    int gi = 0;
-#pragma unroll
-    for (int bit = 32; bit >= 1; bit >>= 1) {
-      const int cand = gi + bit;
-      const int32_t x = __shfl(pj0, min(cand, 63), 64);
-      if (cand < nG && x <= lane) gi = cand;
-    }
-    const int32_t gst = __shfl(pj0, gi, 64);  // the first point lane of this lane's group
-    int32_t A = INT32_MAX, B = -2;
-    if (lane < npts) find_ab(cv.p_m2[pb0 + lane], cv.p_hi[pb0 + lane], A, B);
-    const bool ok = lane < npts && A <= B;
-    int32_t bm = ok ? B : -2;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {  // running max of B within each group (segmented by gst)
-      const int32_t y = __shfl_up(bm, o, 64);
-      if (lane - o >= gst) bm = max(bm, y);
-    }
-    int32_t pe = __shfl_up(bm, 1, 64);
-    if (lane == gst) pe = -2;
-    const unsigned long long starts = __ballot(ok && A > pe + 1);
-    for (int j = 0; j < nG; j++) {  // per group: its merged runs, counted per query lane
-      const int32_t a0 = __shfl(pj0, j, 64), a1 = __shfl(pj1, j, 64);
-      const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
-      unsigned long long m = starts & rng;
-      uint32_t cnt = fcnt;
-      int32_t aopen = 0;
-      bool open = false;
-      while (m) {
-        const int sl = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int32_t as = __shfl(A, sl, 64), ps = __shfl(pe, sl, 64);
-        if (open) close_run(cnt, aopen, ps);
-        open = true;
-        aopen = as;
-      }
-      if (open) close_run(cnt, aopen, __shfl(bm, a1 - 1, 64));
-      add_score(__shfl(colj, j, 64), cnt);
-    }
-    t += nG;
-    tt += nG;
-  }
-}
-
-// Per chunk of the slab (blockIdx.y): each query's max over the chunk's touched clips of
-// (count << 32 | tie key), and those score rows and touch bytes back to zero. A wave reads the
-// touch bytes of 64 clips per step (64 B) and only the touched clips' rows (256 B each, one per
-// load, the loads of 32 clips issued before the first use): the row traffic follows the hits, not C.
-__global__ __launch_bounds__(256) void wide_final_kernel(int32_t ch0, int32_t nq, int32_t C,
-                                                         const int32_t* __restrict__ tiekey, uint32_t* __restrict__ score,
-                                                         uint8_t* __restrict__ touch, unsigned long long* __restrict__ best) {
-  __shared__ unsigned long long red[4][kWideCh];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* rows = score + (int64_t)blockIdx.y * C * kWideW;
-  uint8_t* tch = touch + (int64_t)blockIdx.y * C;
-  unsigned long long rlo = 0, rhi = 0;  // queries 2 lane, 2 lane + 1
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t c0 = 64 * (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); c0 < C; c0 += 64 * nw) {
-    const bool t = c0 + lane < C && tch[c0 + lane];
-    const unsigned long long m = __ballot(t);
-    if (!m) continue;
-    if (t) tch[c0 + lane] = 0;
-    const int32_t tkl = t ? tiekey[c0 + lane] : 0;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      if (!((m >> (32 * h)) & 0xffffffffull)) continue;
-      uint32_t w[32];
-#pragma unroll
-      for (int j = 0; j < 32; j++) {
-        const int b = 32 * h + j;
-        w[j] = (m >> b) & 1 ? rows[(c0 + b) * kWideW + lane] : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < 32; j++) {
-        const int b = 32 * h + j;
-        if ((m >> b) & 1) {
-          const unsigned long long tk = (uint32_t)__builtin_amdgcn_readlane(tkl, b);
-          const unsigned long long klo = ((unsigned long long)(w[j] & 0xffffu) << 32) | tk;
-          const unsigned long long khi = ((unsigned long long)(w[j] >> 16) << 32) | tk;
-          if (w[j] & 0xffffu) rlo = klo > rlo ? klo : rlo;
-          if (w[j] >> 16) rhi = khi > rhi ? khi : rhi;
-          if (w[j]) rows[(c0 + b) * kWideW + lane] = 0u;
-        }
-      }
-    }
-  }
-  red[wave][2 * lane] = rlo;
-  red[wave][2 * lane + 1] = rhi;
-  __syncthreads();
-  if (threadIdx.x < kWideCh) {
-    unsigned long long mm = red[0][threadIdx.x];
-    for (int w2 = 1; w2 < 4; w2++) mm = red[w2][threadIdx.x] > mm ? red[w2][threadIdx.x] : mm;
-    const int32_t q = (ch0 + (int32_t)blockIdx.y) * kWideCh + (int32_t)threadIdx.x;
-    if (mm && q < nq) atomicMax(&best[q], mm);
-  }
-}
-
 // ---- clip-major sweep ------------------------------------------------------------------------
-// The same per-group work as wide_groups, ordered by clip instead of by key: a wave takes windows of
-// kWin consecutive clip columns of one chunk and, for each key the chunk uses, the groups of those
-// clips (two kdir loads per key, no search), so every count a clip gets in the chunk lands in the
-// wave's own LDS row for it. After a window's keys the wave takes each query's best (count << 32 |
-// tie key) over the window's clips in registers: no score rows in memory, no atomics, no
-// wide_final pass. Per-wave maxima go to part[ch][x][query], reduced by wide_part_max.
+// Work items are (chunk, key, clip group). A wave takes windows of kWin consecutive clip columns of
+// one chunk and, for each key the chunk uses, the groups of those clips (two kdir loads per key, no
+// search), so every count a clip gets in the chunk lands in the wave's own LDS row for it. After a
+// window's keys the wave takes each query's best (count << 32 | tie key) over the window's clips in
+// registers: no score rows in memory, no atomics, no final pass over the clips. Per-wave maxima go to
+// part[ch][x][query], reduced by wide_part_max. (Round 3 also had a key-major form with score rows in
+// memory; it lost its A/B and was removed in round 5.)
 constexpr int kWin = CellCache::kWin;
 constexpr int kClipWaves = 4;  // waves per workgroup
 
@@ -1233,23 +920,11 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
   }
 }
 
-#ifndef TFP_CLIP_KEYPRE
-#define TFP_CLIP_KEYPRE 1  // the used keys' segment constants once per wave (wide_clips_kernel)
-#endif
-constexpr bool kClipKeyPre = TFP_CLIP_KEYPRE;
-#ifndef TFP_CLIP_WINPRE
-#define TFP_CLIP_WINPRE 0  // each key's next-window group range requested a window ahead
-#endif
-constexpr bool kClipWinPre = TFP_CLIP_WINPRE;
-#ifndef TFP_CLIP_GRPPRE
-#define TFP_CLIP_GRPPRE 0  // the next batch of groups' records requested before this batch's searches
-#endif
-constexpr bool kClipGrpPre = TFP_CLIP_GRPPRE;
-#ifndef TFP_CLIP_OCC
-#define TFP_CLIP_OCC 8  // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001; 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
-#endif
+// waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001;
+// 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
+constexpr int kClipOcc = 8;
 template <int QPL>
-__global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kernel(
+__global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
@@ -1299,16 +974,10 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
   // The chunk's used keys' segment constants, one key per lane, loaded once per wave instead of
   // once per window and key (three dependent loads ahead of every key's groups): the window loop
   // reads them with readlane. More than 64 used keys: loaded per window and key as below.
-  const bool kpre = kClipKeyPre && nu <= 64;
-  const bool wpre = kpre && kClipWinPre;
+  const bool kpre = nu <= 64;
   int32_t ksb = 0, kse = 0, kfb = 0, kfe = 0, kshf = 0, kl2 = 0, ku2 = 0, ktoff = 0;
-  int32_t kga = 0, kgb = 0, kgbn = 0;  // each key's group range in the current / next window
   if (kpre && lane < nu) {
     const int kq = uk[lane];
-    if (kClipWinPre && w0 < w1) {
-      kga = kdir[(int64_t)kq * (nwin + 1) + w0];
-      kgb = kdir[(int64_t)kq * (nwin + 1) + w0 + 1];
-    }
     ksb = sg[2 * kq];
     kse = sg[2 * kq + 1];
     kfb = sg[2 * (kq | kKeyRange)];
@@ -1329,12 +998,7 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
     for (int32_t u0 = 0; u0 < nu; u0 += 64) {
       // the used keys with groups in this window, 64 keys a step
       int32_t kk = 0, ga = 0, gb = 0;
-      if (wpre) {  // this window's group ranges came with the previous one; the next one's is requested now
-        kk = lane < nu ? uk[lane] : 0;
-        ga = kga;
-        gb = kgb;
-        if (lane < nu && w + 1 < w1) kgbn = kdir[(int64_t)kk * (nwin + 1) + w + 2];
-      } else if (u0 + lane < nu) {
+      if (u0 + lane < nu) {
         kk = uk[u0 + lane];
         ga = kdir[(int64_t)kk * (nwin + 1) + w];
         gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
@@ -1346,7 +1010,7 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
         const int k = __builtin_amdgcn_readlane(kk, sl);
         const int32_t g1 = __builtin_amdgcn_readlane(gb, sl);
         int32_t g = __builtin_amdgcn_readlane(ga, sl);
-        // the key's window segment and its frames without a max2 window (as in wide_groups)
+        // the key's window segment and its frames without a max2 window
         int32_t fb, fe;
         if (kpre) {  // (u0 == 0: the key's slot is lane sl)
           sb = __builtin_amdgcn_readlane(ksb, sl);
@@ -1379,40 +1043,18 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
           shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
           TL = dtab + doff[(int64_t)ch * kKeyRange + k];
         }
-        // (kClipGrpPre: the next batch's group records are requested before this batch's searches;
-        // raw values, so nothing waits for them until the next iteration)
-        bool have = false;
-        int32_t npb0 = 0, nr0 = 0, nr1 = 0, nkey = 0;
+        // A batch of consecutive groups whose items fit the 64 lanes: lane j holds group j's item
+        // range [pj0, pj1) relative to the first item pb0.
         while (g < g1) {
           const int32_t left = g1 - g;
-          int32_t pb0, pj0 = 0, pj1 = INT32_MAX, colj = 0;
-          if (have) {
-            pb0 = npb0;
-            if (lane < left) {
-              pj0 = nr0 - pb0;
-              pj1 = nr1 - pb0;
-              colj = nkey;
-            }
-            have = false;
-          } else {
-            pb0 = cv.g_beg[g];
-            if (lane < left) {
-              pj0 = cv.g_beg[g + lane] - pb0;
-              pj1 = cv.g_beg[g + lane + 1] - pb0;
-              colj = (int32_t)(cv.g_key[g + lane] & kColMask);
-            }
+          int32_t pj0 = 0, pj1 = INT32_MAX, colj = 0;
+          const int32_t pb0 = cv.g_beg[g];
+          if (lane < left) {
+            pj0 = cv.g_beg[g + lane] - pb0;
+            pj1 = cv.g_beg[g + lane + 1] - pb0;
+            colj = (int32_t)(cv.g_key[g + lane] & kColMask);
           }
-          const int nG = __popcll(__ballot(lane < left && pj1 <= 64));
-          if (kClipGrpPre && nG > 0 && g + nG < g1) {
-            const int32_t gn = g + nG;
-            npb0 = cv.g_beg[gn];
-            if (lane < g1 - gn) {
-              nr0 = cv.g_beg[gn + lane];
-              nr1 = cv.g_beg[gn + lane + 1];
-              nkey = (int32_t)(cv.g_key[gn + lane] & kColMask);
-            }
-            have = true;
-          }
+          const int nG = __popcll(__ballot(lane < left && pj1 <= 64));  // (pj1 grows with j: a prefix)
           if (nG == 0) {  // one group with more than 64 items: 64 at a time, runs merged across the steps
             const int32_t pn = __shfl(pj1, 0, 64);
             uint32_t cnt = fcnt;
@@ -1448,6 +1090,8 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
             g++;
             continue;
           }
+          // every item of the batch on its own lane: its group (the last j < nG with pj0 <= lane, by
+          // binary lifting over the lanes' starts) and its run [A, B] of the segment's frames
           const int32_t npts = __shfl(pj1, nG - 1, 64);
           int gi = 0;
 #pragma unroll
@@ -1490,10 +1134,6 @@ __global__ __launch_bounds__(64 * kClipWaves, TFP_CLIP_OCC) void wide_clips_kern
           g += nG;
         }
       }
-    }
-    if (wpre) {
-      kga = kgb;
-      kgb = kgbn;
     }
     // the window's clips: each query's best (count << 32 | tie key)
     const int32_t tk = c0 + lane < C && lane < kWin ? tiekey[c0 + lane] : 0;
@@ -1557,11 +1197,9 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
 
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
-                  (void*)P, (void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)score, (void*)info, (void*)touch, (void*)ptot,
-                  (void*)ukeys, (void*)nuk, (void*)part,
+                  (void*)P, (void*)seg, (void*)cbeg, (void*)info, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part,
                   (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
     if (p) (void)hipFree(p);
-  touch = nullptr;
   ptot = nullptr;
   ukeys = nuk = nullptr;
   part = nullptr;
@@ -1572,18 +1210,15 @@ void WideScratch::release() {
   cap_dtab = 0;
   ka = kb = nullptr;
   ua = ub = nullptr;
-  va = vb = L2s = U2s = seg = wpre = cbeg = info = nullptr;
+  va = vb = L2s = U2s = seg = cbeg = info = nullptr;
   P = nullptr;
-  chw = nullptr;
-  score = nullptr;
   qis = nullptr;
   tmp = nullptr;
   tmp_bytes = 0;
-  cap_nf = cap_nch = cap_score = 0;
-  slab = 0;
+  cap_nf = cap_nch = 0;
 }
 
-hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s) {
+hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
   const int64_t nch = (nq + kWideCh - 1) / kWideCh;
   hipError_t e = hipSuccess;
   if (nf > cap_nf) {
@@ -1612,18 +1247,15 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    for (void* p : {(void*)seg, (void*)wpre, (void*)cbeg, (void*)chw, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk,
-                    (void*)part, dtmp})
+    for (void* p : {(void*)seg, (void*)cbeg, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part, dtmp})
       if (p) (void)hipFree(p);
-    seg = wpre = cbeg = doff = ukeys = nuk = nullptr;
+    seg = cbeg = doff = ukeys = nuk = nullptr;
     ptot = nullptr;
     part = nullptr;
-    chw = nullptr;
     dtmp = nullptr;
     dtmp_bytes = 0;
     cap_nch = 0;
-    if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&wpre, nch * (kKeyRange + 1))) ||
-        (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&chw, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
+    if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
         (e = dmalloc(&ptot, nch * kPortions * 64)) || (e = dmalloc(&ukeys, nch * kKeyRange)) || (e = dmalloc(&nuk, nch)) ||
         (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)))  // up to 2 kPartWaves waves per chunk, either chunk size
       return e;
@@ -1643,23 +1275,6 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, int32_t C, hipStream_t s
     if ((e = dmalloc(&dtab, need_d))) return e;
     cap_dtab = need_d;
   }
-  // score rows for a slab of chunks at once: [slab][C][kChunk / 2] 16-bit pairs, at most ~1 GiB
-  const int64_t row = (int64_t)(C > 0 ? C : 1) * kWideW * (int64_t)sizeof(uint32_t);
-  slab = (int32_t)std::max<int64_t>(1, std::min<int64_t>(nch, (int64_t)(1ll << 30) / row));
-  const int64_t ns = (int64_t)slab * (C > 0 ? C : 1) * kWideW;
-  if (groups_form && ns > cap_score) {  // (the clip-major sweep keeps its counts in LDS)
-    for (void* p : {(void*)score, (void*)touch})
-      if (p) (void)hipFree(p);
-    score = nullptr;
-    touch = nullptr;
-    cap_score = 0;
-    if ((e = dmalloc(&score, ns)) || (e = dmalloc(&touch, (int64_t)slab * (C > 0 ? C : 1)))) return e;
-    // kept zero by wide_final (score rows and touch bytes)
-    if ((e = hipMemsetAsync(score, 0, sizeof(uint32_t) * (size_t)ns, s)) ||
-        (e = hipMemsetAsync(touch, 0, (size_t)slab * (C > 0 ? C : 1), s)))
-      return e;
-    cap_score = ns;
-  }
   if (!info && (e = dmalloc(&info, 4))) return e;
   return hipSuccess;
 }
@@ -1674,7 +1289,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   hipError_t e;
   // 256-query chunks (four 8-bit counts per lane word) when every query has under 256 frames and the
   // clip-major sweep will run: half the chunks, so half the (clip, key, chunk) searches
-  ws->qch = (ws->clip_major && !ws->ch128 && max_qframes < 256) ? 256 : kWideCh;
+  ws->qch = (!ws->ch128 && max_qframes < 256) ? 256 : kWideCh;
   const int32_t qch = ws->qch;
   const int64_t nch = (nq + qch - 1) / qch;
   int cb = 1;  // chunk bits: every chunk number below 2^cb - 1, so no key reaches the ~0 of unused frames
@@ -1685,7 +1300,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   // the results: info[2]) and the chunk number fits its 10 bits
   bool packed = dbase >= 0 && cb <= 10 && !ws->unpacked;
   const int end_bit = (packed ? kPackChunkShift : kWideChunkShift) + cb;
-  speculative = speculative && dbase >= 0 && !ws->no_spec;
+  speculative = speculative && dbase >= 0;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
                      0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2, d_best_zero);
   // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
@@ -1756,8 +1371,7 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (nq <= 0 || !cells || !cells->valid || !cells->k_gbeg) return hipErrorInvalidValue;
   (void)nf;
   const int64_t nch = (nq + ws->qch - 1) / ws->qch;
-  const bool clip_major = cells->kdir && !ws->groups_form;
-  if (ws->qch != kWideCh && !clip_major) return hipErrorInvalidValue;  // (prepare chose the chunks for the clip-major sweep)
+  if (!cells->kdir) return hipErrorInvalidValue;
   CellView cv;
   memset(&cv, 0, sizeof cv);
   cv.g_key = cells->g_key;
@@ -1772,41 +1386,27 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
     cv.g_beg = cells->g_beg;
   }
   cv.valid = 1;
-  if (clip_major) {
-    // clip-major: xw waves per chunk (a multiple of the workgroup's), ~32 k waves in all
-    int64_t xw = std::max<int64_t>(1, 32768 / nch);
-    // (256-query chunks: half the chunks, so up to twice the waves per chunk, ~32 k in all)
-    const int64_t xcap = std::min<int64_t>(2 * kPartWaves, ws->xw_cap > 0 ? ws->xw_cap : (int64_t)kPartWaves * (ws->qch / kWideCh));
-    xw = std::min<int64_t>(xw, std::min<int64_t>(xcap, cells->nwin));
-    xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
-    hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
-    if (ws->qch == 256) {
-      hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                         ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                         C, ws->doff, ws->dtab, ws->part);
-      hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
-                         nq, d_best, ws->info, d_info_out);
-    } else {
-      hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                         ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                         C, ws->doff, ws->dtab, ws->part);
-      hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
-                         nq, d_best, ws->info, d_info_out);
-    }
-    if (info_written) *info_written = d_info_out != nullptr;
-    return hipGetLastError();
+  // xw waves per chunk (a multiple of the workgroup's), ~32 k waves in all
+  int64_t xw = std::max<int64_t>(1, 32768 / nch);
+  // (256-query chunks: half the chunks, so up to twice the waves per chunk, ~32 k in all)
+  const int64_t xcap = std::min<int64_t>(2 * kPartWaves, (int64_t)kPartWaves * (ws->qch / kWideCh));
+  xw = std::min<int64_t>(xw, std::min<int64_t>(xcap, cells->nwin));
+  xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
+  hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
+  if (ws->qch == 256) {
+    hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       C, ws->doff, ws->dtab, ws->part);
+    hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+                       nq, d_best, ws->info, d_info_out);
+  } else {
+    hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       C, ws->doff, ws->dtab, ws->part);
+    hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
+                       nq, d_best, ws->info, d_info_out);
   }
-  hipLaunchKernelGGL(wide_work_kernel, dim3((unsigned)nch), dim3(256), 0, s, ws->seg, cells->k_gbeg, ws->wpre);
-  hipLaunchKernelGGL(wide_chw_kernel, dim3(1), dim3(1024), 0, s, ws->wpre, nch, ws->chw);
-  const int32_t slab = ws->slab > 0 ? ws->slab : 1;
-  const unsigned fx = (unsigned)std::max<int64_t>(1, std::min<int64_t>(256, (C + 2047) / 2048));
-  for (int64_t c0 = 0; c0 < nch; c0 += slab) {
-    const int32_t c1 = (int32_t)std::min<int64_t>(nch, c0 + slab);
-    hipLaunchKernelGGL(wide_groups_kernel, dim3(8192), dim3(256), 0, s, (int32_t)c0, c1, ws->chw, ws->wpre, ws->seg, ws->cbeg,
-                       cv, cells->k_gbeg, ws->L2s, ws->U2s, ws->P, C, ws->score, ws->touch, ws->doff, ws->dtab);
-    hipLaunchKernelGGL(wide_final_kernel, dim3(fx, (unsigned)(c1 - c0)), dim3(256), 0, s, (int32_t)c0, nq, C, d_tiekey,
-                       ws->score, ws->touch, d_best);
-  }
+  if (info_written) *info_written = d_info_out != nullptr;
   return hipGetLastError();
 }
 

@@ -662,10 +662,12 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
     fb1, mg1 = eng.index_build_stats()
     nd1, _ = eng.index_delta_stats()
     os.environ["TFP_INDEX_FULL"] = "1"
+    os.environ["TFP_TEST_KNOBS"] = "1"  # (the library reads its knobs only under this switch)
     try:
         full_eng = T.Engine(eng.device)
     finally:
         del os.environ["TFP_INDEX_FULL"]
+        del os.environ["TFP_TEST_KNOBS"]
     enroll(full_eng, torch, dev, sh, list(range(args.db_clips)))
     full_eng.index_commit()
     full_eng.search_pcm_batch(np.ascontiguousarray(pcm[0, :qn]), [0, qn], pq)

@@ -10,6 +10,11 @@ try:  # torch first: it and libtiresias_fp.so must share one HIP runtime (same S
 except Exception:  # pragma: no cover - torch is plumbing for the device-path tests only
     torch = None
 
+# The library reads its test knobs (TFP_GENERIC, TFP_WIDE_POINTS, TFP_INDEX_FULL, ...; tfp::knob)
+# only under TFP_TEST_KNOBS: set for the whole session, so a test's monkeypatched knob reaches the
+# engines it creates, while a production process's environment never selects a kernel.
+os.environ["TFP_TEST_KNOBS"] = "1"
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(REPO, "asterisk-tiresias_amd")
 for p in (PKG, os.path.join(REPO, "oracle")):

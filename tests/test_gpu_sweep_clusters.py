@@ -8,8 +8,7 @@ placed inside every gap and on both ends of it, with q2 at several sub-micro off
 exact frame count back as match_count), and all clips also share one key, where the groups batch
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
 (src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
-(TFP_WIDE_POINTS), in the key-major form with score rows (TFP_WIDE_GROUPS), and with 128-query
-chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks),
+(TFP_WIDE_POINTS), with 128-query chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks),
 and with the (key, frame) pair sort instead of the packed keys-only sort (TFP_WIDE_UNPACKED).
 """
 import math
@@ -111,7 +110,6 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     got = {}
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
                       ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
                       ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
         eng = _engine_with(tfp_lib, env)
@@ -126,7 +124,6 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
             eng.close()
     assert got["clusters"] == expect, tol
     assert got["points"] == expect, tol
-    assert got["key-major"] == expect, tol
     assert got["clusters-128"] == expect, tol
     assert got["unpacked"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
@@ -175,7 +172,6 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
         expect.append((uuids[w], mc) if found else None)
     assert sum(e is not None for e in expect) > nq // 2
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
-                      ("key-major", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_GROUPS": "1"}),
                       ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
                       ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
         eng = _engine_with(tfp_lib, env)
