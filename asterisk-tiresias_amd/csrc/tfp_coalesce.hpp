@@ -19,6 +19,8 @@
 #include <algorithm>
 #include <condition_variable>
 #include <mutex>
+#include <new>
+#include <string>
 #include <vector>
 
 #include "../../include/tiresias_fp.h"
@@ -36,6 +38,7 @@ struct SearchReq {
   tfp_search_params P{};
   tfp_result* out = nullptr;
   int rc = TFP_OK;
+  std::string err;  // the failure's message (set on the leader's thread, noted on the caller's)
   std::mutex m;
   std::condition_variable cv;
   int state = 0;
@@ -58,25 +61,50 @@ class Coalescer {
   static constexpr int32_t kMaxCallQueries = 16;  // larger calls run on their own
 
   // Runs *r, alone or with other callers' requests, through exec(std::vector<SearchReq*>&), which
-  // sets every request's rc and results. Returns r->rc.
+  // sets every request's rc, results and (on failure) err; see exec_batch. Returns r->rc. An
+  // exception out of exec (host allocations) fails that batch's requests; the lead always moves on.
   template <class Exec>
   int submit(SearchReq* r, Exec&& exec) {
     bool lead = false;
-    {
+    try {
       std::lock_guard<std::mutex> lk(m_);
       calls_++;
       q_.push_back(r);
       if (!busy_) busy_ = lead = true;
+    } catch (const std::bad_alloc&) {
+      r->err = "out of host memory";
+      return r->rc = TFP_E_NOMEM;
     }
     if (!lead && wait(r) == 1) return r->rc;
     // the leader: batches until its own request is done, then hands the lead to the oldest waiter
     for (;;) {
       std::vector<SearchReq*> batch;
-      {
+      bool took = false;
+      try {
         std::lock_guard<std::mutex> lk(m_);
-        take(&batch);
+        take(&batch);  // (q_ is only changed by its final swap)
+        took = true;
+      } catch (const std::bad_alloc&) {
       }
-      exec(batch);
+      if (!took) {  // no batch could be formed: this request fails alone, the lead passes on
+        SearchReq* next = nullptr;
+        {
+          std::lock_guard<std::mutex> lk(m_);
+          q_.erase(std::remove(q_.begin(), q_.end(), r), q_.end());
+          if (q_.empty()) busy_ = false;
+          else next = q_.front();
+        }
+        if (next) set_state(next, 2);
+        r->err = "out of host memory";
+        return r->rc = TFP_E_NOMEM;
+      }
+      try {
+        exec(batch);
+      } catch (const std::bad_alloc&) {
+        for (SearchReq* b : batch) b->err = "out of host memory", b->rc = TFP_E_NOMEM;
+      } catch (...) {
+        for (SearchReq* b : batch) b->err = "internal error", b->rc = TFP_E_HIP;
+      }
       const bool mine = std::find(batch.begin(), batch.end(), r) != batch.end();
       SearchReq* next = nullptr;
       {
@@ -147,14 +175,38 @@ struct Combined {
     }
     res.resize(std::max<size_t>(lens.size(), 1));
   }
-  void scatter(const std::vector<SearchReq*>& batch, int rc) {
+  void scatter(const std::vector<SearchReq*>& batch) {
     size_t at = 0;
     for (SearchReq* b : batch) {
-      b->rc = rc;
-      if (rc == TFP_OK) memcpy(b->out, res.data() + at, sizeof(tfp_result) * b->lens.size());
+      b->rc = TFP_OK;
+      memcpy(b->out, res.data() + at, sizeof(tfp_result) * b->lens.size());
       at += b->lens.size();
     }
   }
 };
+
+// A coalesced batch through run(ptrs, lens, nq, f32, sr, P, out) -> rc (the handle's uncoalesced
+// search); last_error() reads the message of run's failure on this (the leader's) thread. When the
+// combined batch fails (a device allocation sized for all of it, or one caller's query that fails
+// on its own), every request is run again alone, so only a request that fails by itself reports an
+// error, with its own message, and the others get their results.
+template <class Run, class LastError>
+void exec_batch(std::vector<SearchReq*>& batch, Run&& run, LastError&& last_error) {
+  auto alone = [&](SearchReq* b) {
+    b->rc = run(b->ptrs.data(), b->lens.data(), (int32_t)b->lens.size(), b->f32, b->sr, &b->P, b->out);
+    if (b->rc) b->err = last_error();
+  };
+  if (batch.size() == 1) {
+    alone(batch[0]);
+    return;
+  }
+  Combined c(batch);
+  const SearchReq* b0 = batch[0];
+  if (run(c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P, c.res.data()) == TFP_OK) {
+    c.scatter(batch);
+    return;
+  }
+  for (SearchReq* b : batch) alone(b);
+}
 
 }  // namespace tfp

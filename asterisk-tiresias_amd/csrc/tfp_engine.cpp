@@ -118,7 +118,7 @@ struct tfp_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   std::recursive_mutex mu;
-  std::string err;
+  tfp::ErrorSlot err;  // last-error messages (tfp_internal.hpp)
   std::map<int, DevBuf> tables;  // sample rate -> device DspTables
   std::map<int, bool> tables_fixed8k;  // sample rate -> DspTables_fixed8k (kernel variant)
 
@@ -199,6 +199,7 @@ struct tfp_engine {
   bool dbg_vote = false;      // TFP_DEBUG_VOTE: log the vote path's shape per batch
   bool dbg_index = false;     // TFP_DEBUG_INDEX: log each index update's phases (host ms)
   int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
+  int64_t fail_query_len = -1;  // TFP_TEST_FAIL_QUERY_SAMPLES=n: a search with a query of n samples fails (tests)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
   // index delta (round 4, tfp_index.hpp): the live clips added since the last build, searched by the
@@ -232,7 +233,7 @@ int fail(tfp_engine* e, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (e) e->err = buf;
+  if (e) e->err.note(e, buf);
   return code;
 }
 
@@ -1431,6 +1432,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->dbg_vote = tfp::knob("TFP_DEBUG_VOTE") != nullptr;
   e->dbg_index = tfp::knob("TFP_DEBUG_INDEX") != nullptr;
   if (const char* v = tfp::knob("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
+  if (const char* v = tfp::knob("TFP_TEST_FAIL_QUERY_SAMPLES")) e->fail_query_len = atoll(v);
   e->force_full = tfp::knob("TFP_INDEX_FULL") != nullptr;
   if (const char* v = tfp::knob("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   e->wide.points_only = tfp::knob("TFP_WIDE_POINTS") != nullptr;
@@ -1456,7 +1458,9 @@ void tfp_engine_destroy(tfp_engine* e) {
 }
 
 __attribute__((visibility("hidden"))) const char* tfp_ingest_last_error();  // tfp_wav.cpp: engine-less errors of this thread
-const char* tfp_engine_last_error(const tfp_engine* e) { return e ? e->err.c_str() : tfp_ingest_last_error(); }
+const char* tfp_engine_last_error(const tfp_engine* e) {
+  return e ? const_cast<tfp_engine*>(e)->err.read(e) : tfp_ingest_last_error();
+}
 
 int tfp_host_alloc(size_t bytes, void** out) {
   if (!bytes || !out) return TFP_E_ARG;
@@ -1857,6 +1861,10 @@ int search_gather_impl(tfp_engine* e, const void* const* ptrs, const int64_t* le
   HIPCHK(e, hipSetDevice(e->device));
   std::vector<int64_t> foff(nq + 1, 0);
   for (int32_t i = 0; i < nq; i++) foff[i + 1] = foff[i] + tfp_frame_count(lens[i]);
+  for (int32_t i = 0; e->fail_query_len >= 0 && i < nq; i++)  // (test knob: a query that fails on the device)
+    if (lens[i] == e->fail_query_len)
+      return fail(e, TFP_E_HIP, "hipMalloc for query %d of %d (%lld samples): out of memory (TFP_TEST_FAIL_QUERY_SAMPLES)", i,
+                  nq, (long long)lens[i]);
   std::vector<unsigned long long> keys(nq, 0ull);
   if (valid_params(P) && nq && foff[nq] > 0) {
     int64_t nf;
@@ -1885,18 +1893,15 @@ int search_gather_entry(tfp_engine* e, const void* const* ptrs, const int64_t* l
   if (P) r.P = *P;
   else r.P.coefs = 0;  // (invalid: NULL results, fp_handler.c:247-250)
   r.out = out;
-  return e->coal.submit(&r, [e](std::vector<SearchReq*>& batch) {
-    if (batch.size() == 1) {
-      SearchReq* b = batch[0];
-      b->rc = search_gather_impl(e, b->ptrs.data(), b->lens.data(), (int32_t)b->lens.size(), b->f32, b->sr, &b->P, b->out);
-      return;
-    }
-    Combined c(batch);
-    const SearchReq* b0 = batch[0];
-    const int rc = search_gather_impl(e, c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P,
-                                      c.res.data());
-    c.scatter(batch, rc);
+  const int rc = e->coal.submit(&r, [e](std::vector<SearchReq*>& batch) {
+    exec_batch(
+        batch,
+        [e](const void* const* p, const int64_t* l, int32_t n, bool f, int32_t rate, const tfp_search_params* q,
+            tfp_result* o) { return search_gather_impl(e, p, l, n, f, rate, q, o); },
+        [e] { return std::string(tfp_engine_last_error(e)); });
   });
+  if (rc) e->err.note(e, r.err.c_str());  // (the leader ran it: the message into this caller's slot)
+  return rc;
 }
 
 int search_samples_impl(tfp_engine* e, const void* pcm, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,

@@ -82,7 +82,7 @@ struct tfp_group {
   std::vector<int32_t> dev;
   tfp::ShardPool* pool = nullptr;
   std::recursive_mutex mu;
-  std::string err;
+  tfp::ErrorSlot err;  // last-error messages (tfp_internal.hpp)
   std::unordered_map<std::string, int32_t> where;     // uuid -> index in members
   std::vector<Member> members;                         // every clip ever added (uuid "" once removed)
   std::vector<std::vector<int32_t>> id2member;         // [shard][engine clip id] -> member index (-1 removed)
@@ -130,19 +130,29 @@ int gfail(tfp_group* g, int code, const char* fmt, ...) {
   va_start(ap, fmt);
   vsnprintf(buf, sizeof buf, fmt, ap);
   va_end(ap);
-  if (g) g->err = buf;
+  if (g) g->err.note(g, buf);
   return code;
 }
 
-// The error of shard s's failed call, into the group's message.
+// The error of shard s's failed call made on this thread, into the group's message.
 int shard_fail(tfp_group* g, int rc, int s) {
   return gfail(g, rc, "shard %d (device %d): %s", s, g->dev[s], tfp_engine_last_error(g->eng[s]));
 }
 
+// f(s) on every shard in parallel; a failure becomes the group's error with the failing shard's
+// message, read on the thread that ran that shard's call (the engine's per-thread slot).
 int run_all(tfp_group* g, const std::function<int(int)>& f) {
+  const int n = (int)g->eng.size();
+  std::vector<std::string> why(n);
   int bad = 0;
-  const int rc = g->pool->run(f, &bad);
-  return rc ? shard_fail(g, rc, bad) : TFP_OK;
+  const int rc = g->pool->run(
+      [&](int s) {
+        const int r = f(s);
+        if (r) why[s] = r == TFP_E_NOMEM ? "out of host memory" : tfp_engine_last_error(g->eng[s]);
+        return r;
+      },
+      &bad);
+  return rc ? gfail(g, rc, "shard %d (device %d): %s", bad, g->dev[bad], why[bad].c_str()) : TFP_OK;
 }
 
 // Group-wide uuid ranks as every engine's tie-break keys (before any search after a change).
@@ -351,7 +361,7 @@ void tfp_group_destroy(tfp_group* g) { delete g; }
 
 int32_t tfp_group_size(const tfp_group* g) { return g ? (int32_t)g->eng.size() : 0; }
 
-const char* tfp_group_last_error(const tfp_group* g) { return g ? g->err.c_str() : ""; }
+const char* tfp_group_last_error(const tfp_group* g) { return g ? const_cast<tfp_group*>(g)->err.read(g) : ""; }
 
 tfp_engine* tfp_group_engine(tfp_group* g, int32_t shard) {
   return g && shard >= 0 && shard < (int32_t)g->eng.size() ? g->eng[shard] : nullptr;
@@ -606,18 +616,15 @@ int group_search_gather(tfp_group* g, const void* const* ptrs, const int64_t* le
   if (P) r.P = *P;
   else r.P.coefs = 0;  // (invalid: NULL results, fp_handler.c:247-250)
   r.out = out;
-  return g->coal.submit(&r, [g](std::vector<tfp::SearchReq*>& batch) {
-    if (batch.size() == 1) {
-      tfp::SearchReq* b = batch[0];
-      b->rc = group_search_direct(g, b->ptrs.data(), b->lens.data(), (int32_t)b->lens.size(), b->f32, b->sr, &b->P, b->out);
-      return;
-    }
-    tfp::Combined c(batch);
-    const tfp::SearchReq* b0 = batch[0];
-    const int rc = group_search_direct(g, c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P,
-                                       c.res.data());
-    c.scatter(batch, rc);
+  const int rc = g->coal.submit(&r, [g](std::vector<tfp::SearchReq*>& batch) {
+    tfp::exec_batch(
+        batch,
+        [g](const void* const* p, const int64_t* l, int32_t n, bool f, int32_t rate, const tfp_search_params* q,
+            tfp_result* o) { return group_search_direct(g, p, l, n, f, rate, q, o); },
+        [g] { return std::string(tfp_group_last_error(g)); });
   });
+  if (rc) g->err.note(g, r.err.c_str());  // (the leader ran it: the message into this caller's slot)
+  return rc;
 }
 
 int group_search_samples(tfp_group* g, const void* x, bool f32, const int64_t* offsets, int32_t nq, int32_t sr,

@@ -3,7 +3,50 @@
 
 #include <stdint.h>
 
+#include <mutex>
+#include <string>
+
 #include "../../include/tiresias_fp.h"
+
+namespace tfp {
+// Last-error messages of a shared handle (engine or device group). The Asterisk module's channel
+// threads all call one handle (application_handler.c:180, fp_handler.c:1161-1169), so a message is
+// kept per calling thread: a failing call records it in the thread's own slot (with the handle it
+// failed on) and, under the handle's lock, in the handle's slot. tfp_*_last_error(h) returns the
+// calling thread's message when its last failure was on h (valid until that thread's next failing
+// call), else a thread-local copy of the handle's latest message taken under the lock (a device
+// group reads its shards' engines' messages from its own threads). Never a pointer into a string
+// another thread may rewrite.
+struct ErrorSlot {
+  std::mutex mu;
+  std::string msg;
+  void note(const void* h, const char* m);
+  const char* read(const void* h);
+};
+struct ThreadError {
+  const void* h = nullptr;
+  std::string msg;
+};
+inline ThreadError& thread_error() {
+  thread_local ThreadError te;
+  return te;
+}
+inline void ErrorSlot::note(const void* h, const char* m) {
+  ThreadError& te = thread_error();
+  te.h = h;
+  te.msg = m;
+  std::lock_guard<std::mutex> lk(mu);
+  msg = m;
+}
+inline const char* ErrorSlot::read(const void* h) {
+  ThreadError& te = thread_error();
+  if (te.h == h) return te.msg.c_str();
+  thread_local std::string copy;
+  std::lock_guard<std::mutex> lk(mu);
+  copy = msg;
+  return copy.c_str();
+}
+}  // namespace tfp
 
 extern "C" {
 // The search over host samples (query i = lens[i] samples at ptrs[i]), without the engine's

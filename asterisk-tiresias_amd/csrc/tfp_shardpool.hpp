@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <new>
 #include <thread>
 #include <vector>
 
@@ -45,7 +46,7 @@ class ShardPool {
       gen_.fetch_add(1, std::memory_order_release);
     }
     cv_.notify_all();
-    rc_[0] = f(0);
+    rc_[0] = call(f, 0);
     if (!spin_until([&] { return pending_.load(std::memory_order_acquire) == 0; })) {
       std::unique_lock<std::mutex> lk(m_);
       done_.wait(lk, [this] { return pending_.load(std::memory_order_acquire) == 0; });
@@ -61,6 +62,18 @@ class ShardPool {
 
  private:
   static constexpr int64_t kSpinNs = 50000;
+  // f(s), with an exception (an allocation inside a shard's call) as that shard's error code: a
+  // throw on a worker thread would otherwise end the process, and one on the caller would leave
+  // the workers running f after run() unwound
+  static int call(const std::function<int(int)>& f, int s) {
+    try {
+      return f(s);
+    } catch (const std::bad_alloc&) {
+      return TFP_E_NOMEM;
+    } catch (...) {
+      return TFP_E_HIP;
+    }
+  }
   template <class P>
   static bool spin_until(P ready) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -82,7 +95,7 @@ class ShardPool {
       }
       if (stop_.load(std::memory_order_acquire)) return;
       seen = gen_.load(std::memory_order_acquire);
-      rc_[s] = (*f_)(s);
+      rc_[s] = call(*f_, s);
       if (pending_.fetch_sub(1, std::memory_order_acq_rel) == 1) {
         std::lock_guard<std::mutex> lk(m_);
         done_.notify_one();

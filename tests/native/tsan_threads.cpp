@@ -4,7 +4,11 @@
 //     time as tfp_group does under its mutex, with short and long (blocking) shard functions, so
 //     both the spin and the condition-variable hand-offs are taken;
 //   - tfp::Coalescer (csrc/tfp_coalesce.hpp): many threads submitting searches at once, the leader
-//     running a combined batch and handing each caller its own results.
+//     running a combined batch (tfp::exec_batch) and handing each caller its own results; some
+//     callers' requests fail, so failed combined batches are re-run request by request and each
+//     failing caller gets its own message through the real per-thread error slots
+//     (csrc/tfp_internal.hpp: tfp::ErrorSlot), read concurrently by every caller;
+//   - a shard function that throws (std::bad_alloc) becomes that shard's TFP_E_NOMEM.
 // Every result is checked; TSan (halt_on_error=1) turns any data race into a failing exit code.
 #include <stdio.h>
 #include <stdlib.h>
@@ -17,6 +21,7 @@
 #include <vector>
 
 #include "../../asterisk-tiresias_amd/csrc/tfp_coalesce.hpp"
+#include "../../asterisk-tiresias_amd/csrc/tfp_internal.hpp"
 #include "../../asterisk-tiresias_amd/csrc/tfp_shardpool.hpp"
 
 static int fails = 0;
@@ -42,10 +47,12 @@ static void pool_test(int shards, int rounds) {
           [&](int s) {
             if (slow) std::this_thread::sleep_for(std::chrono::microseconds(200));
             acc[s] += add;
+            if (r % 31 == 7 && s == 0) throw std::bad_alloc();  // (after its add: counted below)
             return (r % 29 == 5 && s == shards - 1) ? -2 : 0;
           },
           &bad);
-      if (r % 29 == 5) CHECK(rc == -2 && bad == shards - 1);
+      if (r % 31 == 7) CHECK(rc == TFP_E_NOMEM && bad == 0);
+      else if (r % 29 == 5) CHECK(rc == -2 && bad == shards - 1);
       else CHECK(rc == 0);
     }
   };
@@ -68,20 +75,33 @@ static void coalesce_test(int nthreads, int reps) {
     data[t].resize(64 + t);
     for (size_t i = 0; i < data[t].size(); i++) data[t][i] = (int16_t)(t * 31 + i);
   }
-  auto exec = [&](std::vector<tfp::SearchReq*>& batch) {
-    tfp::Combined c(batch);
-    for (size_t q = 0; q < c.lens.size(); q++) {
-      const int16_t* x = static_cast<const int16_t*>(c.ptrs[q]);
+  // the handle's uncoalesced search: fails (a message naming the query's length) when any query
+  // has a poisoned length, as a device allocation for it would
+  tfp::ErrorSlot slot;
+  auto run = [&](const void* const* ptrs, const int64_t* lens, int32_t nq, bool, int32_t, const tfp_search_params*,
+                 tfp_result* out) {
+    for (int32_t q = 0; q < nq; q++)
+      if (lens[q] % 7 == 3) {
+        char m[64];
+        snprintf(m, sizeof m, "poisoned query of %lld samples", (long long)lens[q]);
+        slot.note(&slot, m);
+        return TFP_E_HIP;
+      }
+    for (int32_t q = 0; q < nq; q++) {
+      const int16_t* x = static_cast<const int16_t*>(ptrs[q]);
       int64_t sum = 0;
-      for (int64_t i = 0; i < c.lens[q]; i++) sum += x[i];
-      memset(&c.res[q], 0, sizeof c.res[q]);
-      c.res[q].found = 1;
-      c.res[q].match_count = (int32_t)sum;
-      c.res[q].frame_count = (int32_t)c.lens[q];
+      for (int64_t i = 0; i < lens[q]; i++) sum += x[i];
+      memset(&out[q], 0, sizeof out[q]);
+      out[q].found = 1;
+      out[q].match_count = (int32_t)sum;
+      out[q].frame_count = (int32_t)lens[q];
     }
-    exec_queries += (int64_t)c.lens.size();
-    if (batch.size() > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
-    c.scatter(batch, 0);
+    exec_queries += nq;
+    if (nq > 1) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    return TFP_OK;
+  };
+  auto exec = [&](std::vector<tfp::SearchReq*>& batch) {
+    tfp::exec_batch(batch, run, [&] { return std::string(slot.read(&slot)); });
   };
   auto caller = [&](int t) {
     for (int r = 0; r < reps; r++) {
@@ -97,6 +117,21 @@ static void coalesce_test(int nthreads, int reps) {
       std::vector<tfp_result> out(nq);
       req.out = out.data();
       const int rc = coal.submit(&req, exec);
+      bool poisoned = false;
+      for (int q = 0; q < nq; q++) poisoned = poisoned || req.lens[q] % 7 == 3;
+      if (poisoned) {  // this caller alone fails, with the message of its own request
+        CHECK(rc == TFP_E_HIP);
+        if (rc) slot.note(&slot, req.err.c_str());
+        const char* m = slot.read(&slot);
+        bool mine = false;
+        for (int q = 0; q < nq; q++) {
+          char want[64];
+          snprintf(want, sizeof want, "poisoned query of %lld samples", (long long)req.lens[q]);
+          mine = mine || strcmp(m, want) == 0;
+        }
+        CHECK(mine);
+        continue;
+      }
       CHECK(rc == 0);
       for (int q = 0; q < nq; q++) {
         const auto& d = data[(t + q) % nthreads];
@@ -112,9 +147,13 @@ static void coalesce_test(int nthreads, int reps) {
   int64_t calls = 0, batches = 0, want = 0;
   coal.stats(&calls, &batches);
   for (int t = 0; t < nthreads; t++)
-    for (int r = 0; r < reps; r++) want += 1 + (t + r) % 3;
+    for (int r = 0; r < reps; r++) {
+      bool poisoned = false;
+      for (int q = 0; q < 1 + (t + r) % 3; q++) poisoned = poisoned || (64 + (t + q) % nthreads) % 7 == 3;
+      if (!poisoned) want += 1 + (t + r) % 3;
+    }
   CHECK(calls == (int64_t)nthreads * reps);
-  CHECK(exec_queries.load() == want);
+  CHECK(exec_queries.load() >= want);  // (the good requests, some more than once after a failed batch)
   CHECK(batches >= 1 && batches <= calls);
   printf("coalescer: %lld calls in %lld batches\n", (long long)calls, (long long)batches);
 }

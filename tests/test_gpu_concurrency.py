@@ -147,3 +147,79 @@ def test_group_concurrent_searches_during_enrolment(oracle, tfp_lib):
         r, f = g.search_pcm_batch(qpcm.reshape(-1), np.arange(25) * n, p)
         assert [(_key(r[q]), f[q]) for q in range(24)] == [want[pi, q] for q in range(24)]
     g.close()
+
+
+def _stats(fn, h):
+    import ctypes as C
+    a, b = C.c_int64(), C.c_int64()
+    assert fn(h, C.byref(a), C.byref(b)) == 0
+    return a.value, b.value
+
+
+@pytest.mark.parametrize("kind", ["engine", "group"])
+def test_failing_caller_in_coalesced_batch_is_isolated(oracle, tfp_lib, kind, monkeypatch):
+    """32 channel threads search at once on one shared handle (application_handler.c:180 over
+    fp_handler.c:1161-1169) while one of them submits a query that fails on the device (test knob
+    TFP_TEST_FAIL_QUERY_SAMPLES: a forced allocation failure for a query of that length). Concurrent
+    calls are coalesced into shared batches (tfp_coalesce.hpp); a batch holding the failing query
+    fails as a whole and is re-run request by request, so the 31 others get their serial results and
+    only the failing caller sees an error, with its own message read on its own thread."""
+    from tiresias_amd._lib import TfpError, lib
+    bad_len = 8000 * 2 + 77
+    monkeypatch.setenv("TFP_TEST_FAIL_QUERY_SAMPLES", str(bad_len))
+    h = tfp_lib.Engine(0) if kind == "engine" else tfp_lib.Group([0, 0])
+    try:
+        n = 8000 * 12
+        pcm = tfp_lib.synth_pcm(7, range(60), n)
+        micro, _ = oracle.fingerprint_batch(pcm.reshape(-1), np.arange(61) * n, nthreads=8, want_db=False)
+        nf = (n + 255) // 256
+        for c in range(60):
+            h.index_add("%032x" % (c + 1), micro[c * nf:(c + 1) * nf, 0], micro[c * nf:(c + 1) * nf, 1])
+        # 31 three-second excerpts of enrolled clips (the 31 good callers' queries)
+        qpcm = np.stack([tfp_lib.synth_pcm(7, [2 * c], 8000 * 3, offsets=[256 * (7 * c + 3)])[0] for c in range(31)])
+        nq = qpcm.shape[1]
+        p = tfp_lib.params(1, 0.001)
+        want = [_key(h.search_pcm_batch(qpcm[t], [0, nq], p)[0][0]) for t in range(31)]
+        assert sum(w is not None for w in want) > 20
+        bad = tfp_lib.synth_pcm(99, [0], bad_len)[0]
+        with pytest.raises(TfpError) as ei:  # alone, first: the knob is live
+            h.search_pcm_batch(bad, [0, bad_len], p)
+        assert "TFP_TEST_FAIL_QUERY_SAMPLES" in str(ei.value)
+        statfn = lib().tfp_search_coalesce_stats if kind == "engine" else lib().tfp_group_search_coalesce_stats
+        c0, b0 = _stats(statfn, h.handle)
+        iters = 25
+        bar = threading.Barrier(32)
+        errors, bad_seen = [], []
+
+        def worker(t):
+            try:
+                for it in range(iters):
+                    bar.wait(timeout=60)
+                    if t == 31:
+                        try:
+                            h.search_pcm_batch(bad, [0, bad_len], p)
+                            errors.append((t, it, "no error"))
+                        except TfpError as ex:
+                            bad_seen.append(str(ex))
+                    else:
+                        r, f = h.search_pcm_batch(qpcm[t], [0, nq], p)
+                        if _key(r[0]) != want[t] or f[0] != tfp_lib.frame_count(nq):
+                            errors.append((t, it, _key(r[0]), want[t]))
+            except Exception as ex:  # pragma: no cover - reported below
+                errors.append((t, repr(ex)))
+                bar.abort()
+
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(32)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join(timeout=200)
+        assert not any(th.is_alive() for th in threads), "a caller thread did not finish"
+        assert not errors, errors[:5]
+        assert len(bad_seen) == iters
+        # the failing caller's own message (its query alone: "query 0 of 1"), never a neighbour's
+        assert all("TFP_TEST_FAIL_QUERY_SAMPLES" in m and "query 0 of 1" in m for m in bad_seen), bad_seen[:3]
+        c1, b1 = _stats(statfn, h.handle)
+        assert c1 - c0 == 32 * iters and b1 - b0 < c1 - c0  # calls were coalesced (some batches held the bad query)
+    finally:
+        h.close()
