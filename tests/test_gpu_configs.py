@@ -304,11 +304,11 @@ def test_configs2_full_db_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
         assert fc[0] == nfq
 
 
-@pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 128), (2, 0.01, -1, -1, 128), (2, 0.1, -1, -1, 128),
-                                                   (2, 0.45, -1, -1, 128), (1, 0.45, -1, -1, 64),
-                                                   (1, 0.01, 100, 3400, 64), (2, 0.1, 100, 3400, 64),
-                                                   (2, 0.45, 100, 3400, 128), (1, 0.001, 50, 60, 64),
-                                                   (2, 0.01, 50, 60, 64), (2, 0.45, 50, 60, 128)])
+@pytest.mark.parametrize("coefs,tol,low,high,nq", [(2, 0.001, -1, -1, 512), (2, 0.01, -1, -1, 512), (2, 0.1, -1, -1, 512),
+                                                   (2, 0.45, -1, -1, 512), (1, 0.45, -1, -1, 64),
+                                                   (1, 0.01, 100, 3400, 64), (2, 0.1, 100, 3400, 512),
+                                                   (2, 0.45, 100, 3400, 512), (1, 0.001, 50, 60, 64),
+                                                   (2, 0.01, 50, 60, 512), (2, 0.45, 50, 60, 512)])
 def test_configs2_sweeps_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda, coefs, tol, low, high, nq):
     """SURVEY §8(d)'s configs[2] sweeps at full DB size: coefs = 2 (the general path over the
     m2-ordered key segments, src/fp_handler.c:318-351), wider tolerances and the ignore filter
@@ -316,9 +316,11 @@ def test_configs2_sweeps_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda, coe
     frames (max1 ~17 dB < 20 dB) and matches nothing; 50/60 Hz (16.99/17.78 dB) keeps about a third
     and still matches, and drops the max2 condition of the frames whose max2 falls outside it (the
     case whose 16-bit count pairs once borrowed across the halves: round 3, golden rand_05), so the
-    filter's kept/dropped split is exercised on both sides. 128 queries = one full sweep chunk; at
-    tolerance 0.45 every (key, clip) group of the chunk's keys is one long cluster of the clip-major
-    sweep (bench.py times (2, 0.45) on all 4,096)."""
+    filter's kept/dropped split is exercised on both sides. Every coefs = 2 setting runs 512 queries:
+    the 5 s queries have 157 frames (< 256), so the sweep takes 256-query chunks with four 8-bit
+    counts per lane word, and 512 queries are two full chunks. At tolerance 0.45 every (key, clip)
+    group of a chunk's keys is one long cluster of the clip-major sweep (bench.py times the coefs = 2
+    settings on all 4,096)."""
     torch = torch_cuda
     qpcm, d_q = _c3_batch(c3db, tfp_lib, torch, nq, SEED_Q + coefs)
     qdb, qoff = _oracle_q(oracle, qpcm)
@@ -387,9 +389,9 @@ def _bench_batch(c3db, torch, nq=4096):
 def test_configs2_timed_batch_all_4096_vs_sorted_oracle(c3db, oracle, tfp_lib, torch_cuda):
     """The batch bench.py times (4,096 x 5 s queries, coefs = 1, tolerance 0.001, the vote path),
     every one of its keys == the oracle's sorted-index search over the same 93.8 M rows; and the
-    bench's coefs = 2 sweeps of the same batch, all 4,096 queries (32 sweep chunks of 128 queries,
-    src/fp_handler.c:318-351) at tolerance 0.001 and at 0.45 (its widest, the clip-major sweep's
-    longest clusters), at full DB size."""
+    bench's coefs = 2 sweeps of the same batch, all 4,096 queries (16 sweep chunks of 256 queries
+    with 8-bit counts, src/fp_handler.c:318-351) at tolerance 0.001 and at 0.45 (its widest, the
+    clip-major sweep's longest clusters), at full DB size."""
     torch = torch_cuda
     qpcm, d_q = _bench_batch(c3db, torch)
     qdb, qoff = _oracle_q(oracle, qpcm)

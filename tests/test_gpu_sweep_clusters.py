@@ -206,3 +206,70 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
         assert fcs[0] == 300
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("tol", [0.001, 0.45])
+def test_sweep_8bit_count_field_edge(oracle, tfp_lib, tol):
+    """The 256-query sweep chunks pack four 8-bit counts per lane word when every query has fewer
+    than 256 frames (tfp_scan.hip: wide_prefix / wide_clips_kernel<4>): a query's count per clip
+    and its prefix counts never exceed its frame count. This fills one chunk exactly (256 queries of
+    255 frames, the field's maximum) with queries whose every frame hits one clip X (match_count 255,
+    the four queries of a lane word all at 255 together), queries whose frames hit nothing (count 0
+    beside them), and queries at 254 for another clip Y. Keys == the oracle (src/fp_handler.c:318-374).
+    The same batch with one more non-hitting frame per query (256 frames: over the 8-bit field, so
+    128-query chunks with 16-bit counts) gives identical results."""
+    rng = np.random.default_rng(255)
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(4)]
+    # every row in trunc key 20's max1 box ([20 - tol, 20 + tol] contains 20.000000); clip c's
+    # max2 points around 30 + 10 c dB, far apart at either tolerance
+    rows = 300
+    m1 = np.full(4 * rows, 20_000_000, np.int32)
+    m2 = np.concatenate([30_000_000 + 10_000_000 * c + rng.integers(-20, 20, rows) * 5 for c in range(4)]).astype(np.int32)
+    clip = np.repeat(np.arange(4), rows).astype(np.int32)
+    X, Y = 1, 2
+    vx, vy, vnone = 30.0 + 10 * X, 30.0 + 10 * Y, -100.0
+
+    def batch(nframes):
+        q2 = []
+        for q in range(256):
+            kind = q % 4 if q < 128 else (q // 4) % 4  # lane words of one kind, and of mixed kinds
+            if kind in (0, 2):
+                v = np.full(255, vx)        # all 255 frames hit X
+            elif kind == 1:
+                v = np.full(255, vnone)     # no frame hits anything
+            else:
+                v = np.full(255, vy)        # 254 hit Y, one misses
+                v[q % 255] = vnone
+            q2.append(np.concatenate([v, np.full(nframes - 255, vnone)]))
+        q2 = np.concatenate(q2)
+        q1 = np.full(len(q2), 20.5)
+        qoff = np.arange(257, dtype=np.int64) * nframes
+        frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                             ("q1", "<f8"), ("q2", "<f8")]))
+        frames["q1"], frames["q2"] = q1, q2
+        return frames, q1, q2, qoff
+
+    frames, q1, q2, qoff = batch(255)
+    expect = []
+    for i in range(256):
+        s = slice(qoff[i], qoff[i + 1])
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, -1, -1)
+        expect.append((uuids[w], mc) if found else None)
+    assert sum(e == (uuids[X], 255) for e in expect) == 128
+    assert sum(e == (uuids[Y], 254) for e in expect) == 64 and sum(e is None for e in expect) == 64
+    eng = tfp_lib.Engine(0)
+    try:
+        for c in range(4):
+            sel = clip == c
+            eng.index_add(uuids[c], m1[sel], m2[sel])
+        res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol))
+        got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+        assert got == expect, [i for i in range(256) if got[i] != expect[i]][:8]
+        assert list(fcs) == [255] * 256
+        frames2, _, _, qoff2 = batch(256)
+        res2, fcs2 = eng.search_batch(frames2, qoff2, tfp_lib.params(2, tol))
+        got2 = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res2]
+        assert got2 == expect
+        assert list(fcs2) == [256] * 256
+    finally:
+        eng.close()
