@@ -145,3 +145,58 @@ int tfp_latency_threads(tfp_engine* eng, const int16_t* pcm, int64_t n, int32_t 
   free(args);
   return rc;
 }
+
+/* The same two loops through a device group (tfp_group_*: the shim's handle, one engine per GPU of
+ * the node): batch-1 host-PCM searches, and stream ticks of a group stream. */
+int tfp_latency_group_search_pcm(tfp_group* g, const int16_t* pcm, int64_t n, int32_t nqueries, int32_t sample_rate,
+                                 const tfp_search_params* params, int32_t iters, double* out_ms, int32_t* found) {
+  int32_t i;
+  int rc = TFP_OK;
+  int16_t* hq = NULL;
+  if (!g || !pcm || n <= 0 || nqueries <= 0 || iters < 0 || !params || (iters && (!out_ms || !found)))
+    return TFP_E_ARG;
+  if (tfp_host_alloc(sizeof(int16_t) * (size_t)n * (size_t)nqueries, (void**)&hq) != TFP_OK) return TFP_E_NOMEM;
+  memcpy(hq, pcm, sizeof(int16_t) * (size_t)n * (size_t)nqueries);
+  for (i = 0; i < iters && rc == TFP_OK; i++) {
+    const int64_t off[2] = {0, n};
+    tfp_result r;
+    double t0 = now_ms(), t1;
+    rc = tfp_group_search_pcm_batch(g, hq + (int64_t)(i % nqueries) * n, off, 1, sample_rate, params, &r);
+    t1 = now_ms();
+    out_ms[i] = t1 - t0;
+    found[i] = r.found;
+  }
+  tfp_host_free(hq);
+  return rc;
+}
+
+int tfp_latency_group_stream(tfp_group_stream* st, const int16_t* pcm, int32_t nchannels, int64_t total, int64_t first,
+                             int32_t tick, int32_t nticks, const tfp_search_params* params, double* out_ms,
+                             int32_t* found_last) {
+  int32_t t, c;
+  int rc = TFP_OK;
+  int16_t* blk;
+  tfp_result* res;
+  if (!st || !pcm || nchannels <= 0 || tick <= 0 || nticks < 0 || !params || !out_ms || !found_last ||
+      first < 0 || first + (int64_t)tick * nticks > total)
+    return TFP_E_ARG;
+  if (tfp_host_alloc(sizeof(int16_t) * (size_t)nchannels * (size_t)tick, (void**)&blk) != TFP_OK) return TFP_E_NOMEM;
+  if (tfp_host_alloc(sizeof(tfp_result) * (size_t)nchannels, (void**)&res) != TFP_OK) {
+    tfp_host_free(blk);
+    return TFP_E_NOMEM;
+  }
+  *found_last = 0;
+  for (t = 0; t < nticks && rc == TFP_OK; t++) {
+    double t0, t1;
+    for (c = 0; c < nchannels; c++)
+      memcpy(blk + (int64_t)c * tick, pcm + (int64_t)c * total + first + (int64_t)t * tick, sizeof(int16_t) * (size_t)tick);
+    t0 = now_ms();
+    rc = tfp_group_stream_push(st, blk, tick, params, res);
+    t1 = now_ms();
+    out_ms[t] = t1 - t0;
+  }
+  for (c = 0; c < nchannels; c++) *found_last += res[c].found;
+  tfp_host_free(res);
+  tfp_host_free(blk);
+  return rc;
+}

@@ -21,6 +21,15 @@ Also reported (same JSON line):
                 combined by one RCCL all_reduce(MAX) (configs[3]).
   stream        configs[4]: 512 live channels, 160-sample ticks, 3 s window, matched every tick;
                 with N GPUs the channels are split over the ranks against a replicated DB.
+  group         the in-process device group (tfp_group_*): the path the Asterisk shim serves its
+                channel threads with (one process, one handle, fp_handler.c:1161-1169), over every
+                GPU the process sees: the configs[3] batch from host PCM, batch-1 latency and the
+                512-channel stream through the same entry points the shim calls.
+
+--gpus N: under a launcher (torchrun / torch.distributed.run: WORLD_SIZE set) WORLD_SIZE must equal
+N, or bench.py exits non-zero; without one, bench.py starts the N rank processes itself (a child
+torch.distributed.run, before any GPU call) and exits with its code. It never runs fewer ranks than
+asked.
 """
 from __future__ import annotations
 
@@ -29,6 +38,8 @@ import ctypes
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -58,6 +69,45 @@ def uuid_of(global_clip: int) -> str:
     return "%s-%s-%s-%s-%s" % (s[:8], s[8:12], s[12:16], s[16:20], s[20:32])
 
 
+def launch_plan(gpus: int, env, argv):
+    """How this process runs `--gpus gpus`: ("run", None) when it is one rank of a launcher's job
+    (WORLD_SIZE == gpus) or gpus == 1 without one; ("spawn", cmd) without a launcher for gpus > 1:
+    cmd starts the gpus rank processes (torch.distributed.run, rendezvous on 127.0.0.1) with the
+    same arguments; ("refuse", why) when a launcher's WORLD_SIZE disagrees with --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: need at least 1"
+    if ws is not None:
+        if int(ws) != gpus:
+            return "refuse", f"--gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks"
+        return "run", None
+    if gpus == 1:
+        return "run", None
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    return "spawn", [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+                     "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def launch_check(args):
+    """--launch-check (tests/test_bench_launch.py): the ranks meet over gloo and rank 0 prints the
+    world size it sees, with no GPU call at all."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    n = world
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        n = int(t.item())
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "gpus": args.gpus, "world_size": world, "ranks_met": n}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,7 +133,21 @@ def main():
     ap.add_argument("--stream-channels", type=int, default=512)
     ap.add_argument("--stream-ticks", type=int, default=200)
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL) on MI355X; gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--no-group", action="store_true", help="skip the in-process device-group leg")
+    ap.add_argument("--launch-check", action="store_true", help="start the ranks, meet over gloo, print, exit (no GPU)")
     args = ap.parse_args()
+
+    # --gpus N: every rank process exists before any GPU call (a child launcher, never an exec)
+    how, what = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if how == "refuse":
+        log(f"bench.py: {what}")
+        sys.exit(2)
+    if how == "spawn":
+        log(f"bench.py: starting {args.gpus} ranks: {' '.join(what)}")
+        sys.exit(subprocess.call(what))
+    if args.launch_check:
+        launch_check(args)
+        return
 
     import torch
     import tiresias_amd as T
@@ -228,6 +292,8 @@ def main():
         out["match"] = run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ranks, T)
         if args.stream_channels > 0:
             out["stream"] = run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier)
+        if not args.no_group:
+            out["group"] = run_group(args, eng, T, torch, dev, sh, rank, world, dist)
 
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -873,6 +939,135 @@ def run_stream(args, eng, T, torch, dev, sh, rank, world, dist, barrier):
             "tick_harness": "C loop over tfp_stream_push (bench/tfp_latency.c), the tick's samples in a tfp_host_alloc buffer",
             "tick_latency_p50_ms_python": float(np.percentile(plat, 50)),
             "fingerprints_per_tick": nch * ((W + HOP - 1) // HOP), "channels_found_last_tick": found}
+
+
+def run_group(args, eng, T, torch, dev, sh, rank, world, dist):
+    """The in-process device group (tfp_group_*, csrc/tfp_group.cpp) over every GPU this process
+    sees (tfp_device_count): the Asterisk module is one process whose channel threads all call one
+    handle (application_handler.c:180, fp_handler.c:1161-1169), and the shim (shim/fp_handler_tfp.c)
+    serves them through a group. Measured through the entry points the shim calls:
+      enrolment   the 100k-clip DB (configs[2]) added with tfp_group_index_add_batch (the clips'
+                  rows fingerprinted on this rank's engine first), each clip on the lightest shard;
+      batch       configs[3]'s 4,096 x 5 s queries from host PCM (tfp_group_search_pcm_batch: the
+                  queries fingerprinted 1/N per shard, frame values exchanged peer to peer, every
+                  shard searching its clips, keys max-combined), median of 5 calls;
+      latency     batch-1 host-PCM searches from C (bench/tfp_latency.c), p50 / p99;
+      stream      configs[4]: 512 channels through tfp_group_stream_push ticks, from C.
+    Rank 0 runs it; the other ranks wait on the rendezvous store (no GPU work meanwhile)."""
+    store = None
+    if dist:
+        store = dist.distributed_c10d._get_default_store()
+        if rank != 0:
+            store.wait(["tfp_group_leg_done"], __import__("datetime").timedelta(seconds=900))
+            return None
+    try:
+        return _group_leg(args, eng, T, torch, dev, sh, world)
+    except Exception as ex:  # reported in the line; the fingerprint and match legs stand
+        log(f"group leg failed: {ex!r}")
+        return {"error": repr(ex)}
+    finally:
+        if store is not None:
+            store.set("tfp_group_leg_done", "1")
+
+
+def _group_leg(args, eng, T, torch, dev, sh, world):
+    from tiresias_amd import Group, GroupStream
+    ndev = T.device_count()
+    g = Group(list(range(ndev)))
+    n_db = 8000 * 30
+    nf_db = (n_db + HOP - 1) // HOP
+    chunk = 2048
+    t0 = time.perf_counter()
+    buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
+    micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
+    for s0 in range(0, args.db_clips, chunk):
+        ids = list(range(s0, min(args.db_clips, s0 + chunk)))
+        k = len(ids)
+        plan = eng.plan(np.arange(k + 1, dtype=np.int64) * n_db)
+        eng.synth_device(SEED_DB, ids, n_db, buf.data_ptr(), stream=sh)
+        eng.fingerprint_device(plan, buf.data_ptr(), micro.data_ptr(), 0, sh)
+        torch.cuda.synchronize(dev)
+        rows = micro[:k * nf_db].cpu().numpy()
+        g.index_add_batch([uuid_of(i) for i in ids], np.arange(k + 1, dtype=np.int64) * nf_db, rows[:, 0], rows[:, 1])
+    del buf, micro
+    torch.cuda.empty_cache()
+    g.index_commit()
+    t_enrol = time.perf_counter() - t0
+    shards = g.engine_stats()
+    log(f"group: {ndev} device(s), enrolled {args.db_clips} clips in {t_enrol:.1f} s, shards {shards}")
+
+    nq, qn = args.queries, 8000 * 5
+    hq = np.ascontiguousarray(c3_queries(eng, torch, dev, sh, nq, args.db_clips).cpu().numpy())
+    off = np.arange(nq + 1, dtype=np.int64) * qn
+    p = T.params(1, 0.001)
+    res = None
+    for _ in range(2):  # untimed: first-call allocations, caches
+        res = g.search_pcm_batch(hq, off, p)
+    times = []
+    for _ in range(5):
+        t1 = time.perf_counter()
+        res = g.search_pcm_batch(hq, off, p)
+        times.append(time.perf_counter() - t1)
+    batch_ms = float(np.median(times)) * 1e3
+    found = sum(r is not None for r in res)
+    same = None
+    if world == 1:  # this rank's engine holds the same 100k clips: the group must answer as it does
+        ref = eng.search_pcm_batch(hq, off, p)[0]
+        same = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in ref] == \
+               [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+    log(f"group batch: {nq} queries {batch_ms:.2f} ms (host PCM in), found {found}, equal to the engine: {same}")
+
+    clat = ctypes.CDLL(os.path.join(os.path.dirname(T.LIB_PATH), "libtfp_latency.so"))
+    nl = min(args.latency_queries, nq)
+    lq = np.ascontiguousarray(hq[:nl])
+    for i in range(3):
+        g.search_pcm_batch(lq[i], [0, qn], p)
+    n_it = max(200, 10 * nl)
+    out_ms = np.zeros(n_it, np.float64)
+    fnd = np.zeros(n_it, np.int32)
+    rc = clat.tfp_latency_group_search_pcm(g.handle, ctypes.c_void_p(lq.ctypes.data), ctypes.c_int64(qn), ctypes.c_int32(nl),
+                                           ctypes.c_int32(8000), ctypes.byref(p), ctypes.c_int32(n_it),
+                                           ctypes.c_void_p(out_ms.ctypes.data), ctypes.c_void_p(fnd.ctypes.data))
+    assert rc == 0, rc
+    out = {"workload": f"configs[3] through the shim's handle: a tfp_group over {ndev} GPU(s) in one process, "
+                       f"{args.db_clips} x 30 s clips sharded by clip, {nq} x 5 s queries from host PCM",
+           "n_devices": ndev, "shards_rows_clips": shards, "enrol_s": t_enrol,
+           "batch_queries": nq, "batch_ms": batch_ms, "queries_per_s": nq / (batch_ms / 1e3), "found": found,
+           "equal_to_engine": same,
+           "latency_p50_ms": float(np.percentile(out_ms, 50)), "latency_p99_ms": float(np.percentile(out_ms, 99)),
+           "latency_harness": "C loop over tfp_group_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries"
+                              % (n_it, nl)}
+    del hq
+    if args.stream_channels > 0:
+        nch, W, tick, nt = args.stream_channels, 24000, 160, args.stream_ticks
+        rng = np.random.default_rng(SEED_Q + 1)
+        span = W + nt * tick
+        clips = [int(rng.integers(args.db_clips)) for _ in range(nch)]
+        offs = [256 * int(rng.integers(0, (n_db - span) // HOP)) for _ in range(nch)]
+        pcm = T.synth_pcm(SEED_DB, clips, span, offsets=offs)
+        for c in range(3, nch, 4):
+            pcm[c] = T.synth_pcm(SEED_Q + 7, [c // 4], span)[0]
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        st = GroupStream(g, nch, W)
+        for t in range(W // tick):
+            st.push(pcm[:, t * tick:(t + 1) * tick])
+        cms = np.zeros(nt, np.float64)
+        cfound = ctypes.c_int32()
+        rc = clat.tfp_latency_group_stream(st._h, ctypes.c_void_p(pcm.ctypes.data), ctypes.c_int32(nch), ctypes.c_int64(span),
+                                           ctypes.c_int64(W), ctypes.c_int32(tick), ctypes.c_int32(nt), ctypes.byref(p),
+                                           ctypes.c_void_p(cms.ctypes.data), ctypes.byref(cfound))
+        assert rc == 0, rc
+        st.close()
+        out["stream"] = {"workload": f"configs[4]: {nch} channels, {tick}-sample ticks, {W}-sample window, channels split "
+                                     f"over the group's {ndev} shard(s) (channel c on shard c mod N), window frame values "
+                                     f"copied to the other shards, every shard matching its clips",
+                         "ticks_timed": nt, "tick_latency_p50_ms": float(np.percentile(cms, 50)),
+                         "tick_latency_p99_ms": float(np.percentile(cms, 99)), "channels_found_last_tick": cfound.value,
+                         "tick_harness": "C loop over tfp_group_stream_push (bench/tfp_latency.c)"}
+        log(f"group stream: p50 {out['stream']['tick_latency_p50_ms']:.2f} ms")
+    g.close()
+    torch.cuda.empty_cache()
+    return out
 
 
 if __name__ == "__main__":

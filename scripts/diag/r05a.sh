@@ -12,3 +12,4 @@ for r in 1 2; do
   done
 done
 grep "fp C2" gpurun_out/${R}_abl.txt
+timeout -k 10 600 python bench.py > gpurun_out/${R}_bench.json 2> gpurun_out/${R}_bench.err; rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/${R}_bench.err; exit $rc
