@@ -50,6 +50,21 @@ struct DevBuf {
   // enrolments does not free and reallocate hundreds of MB each time
   hipError_t reserve_grow(size_t n) { return n <= bytes ? hipSuccess : reserve(n + n / 8); }
   template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+  void swap_with(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(bytes, o.bytes);
+  }
+};
+
+// A tolerance's key row ranges and key bitsets kept beside the active ones (tfp_engine::tol_lru):
+// the dialplan passes the tolerance per call (application_handler.c:114-122), so extensions at
+// different tolerances alternate on one engine. Valid while the index is at `version`.
+struct TolSlot {
+  double tol = 0.0;
+  DevBuf rng_all, key_bits;
+  bool rng_valid = false, bits_valid = false;
+  int32_t bits_cols = -1;
+  uint64_t version = 0, used = 0;
 };
 
 // Pinned host staging (one H2D copy per small call instead of one per array).
@@ -182,6 +197,12 @@ struct tfp_engine {
   DevBuf rng_all;            // row ranges of all keys' boxes at tolerance rng_tol (valid for this index)
   double rng_tol = 0.0;
   bool rng_valid = false;
+  // other tolerances' ranges and bitsets (least recently used first out), valid at index_version;
+  // index_version changes with every index update (rebuild, delta update), which carries only the
+  // active tolerance's
+  static constexpr int kTolSlots = 3;
+  TolSlot tol_lru[kTolSlots];
+  uint64_t index_version = 1, tol_clock = 0;
   // general path: clip-set cache at tolerance cell_tol (tfp_scan.hip), built on first use per
   // index version and tolerance
   CellCache cells;
@@ -200,6 +221,8 @@ struct tfp_engine {
   bool dbg_index = false;     // TFP_DEBUG_INDEX: log each index update's phases (host ms)
   int32_t fail_compact = 0;   // TFP_TEST_FAIL_COMPACT=n: the next n staging compactions fail (tests)
   int64_t fail_query_len = -1;  // TFP_TEST_FAIL_QUERY_SAMPLES=n: a search with a query of n samples fails (tests)
+  int32_t kb_win = 0;           // TFP_KEYBITS_WIN: LDS words per column window of launch_key_bits (tests; 0 = default)
+  int64_t kb_direct = -1;       // TFP_KEYBITS_DIRECT: pieces below this many rows use global atomics (tests; -1 = default)
   DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
   // index delta (round 4, tfp_index.hpp): the live clips added since the last build, searched by the
@@ -207,6 +230,11 @@ struct tfp_engine {
   static constexpr int32_t kDeltaMaxClips = 512;        // columns reserved for them
   static constexpr int64_t kDeltaMaxRows = 1ll << 20;  // beyond either limit the next update merges
   bool use_delta = true;          // TFP_INDEX_DELTA=0: every update merges (A/B, tests)
+  // The delta pads the main columns to a multiple of 1024 and reserves kDeltaMaxClips columns
+  // after them, which a small DB's vote passes would pay for on every search (300 clips -> 1,536
+  // columns); below this many main columns an update merges instead (cheap at that size).
+  // TFP_INDEX_DELTA=1 (tests) takes the delta at any size.
+  int64_t delta_min_cols = 4096;
   bool force_merge = false;       // consolidate(): the next rebuild merges the delta
   std::vector<int32_t> delta_clip;  // delta column delta_col0 + j -> clip id (uuid order)
   std::vector<int32_t> delta_at;    // delta j's insertion point among the main columns' uuids
@@ -775,18 +803,21 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, const MergeBrea
   std::swap(e->cols.p, e->cols_b.p); std::swap(e->cols.bytes, e->cols_b.bytes);
   e->nrows = kept + valid;
   // The small path's key ranges and bitsets, carried to the merged index at their tolerance
-  // instead of rebuilt from every box row (tfp_index.hpp): the ranges are searched again, the
-  // bitsets get zero columns at the breakpoints (highest first) and the new rows' bits. Only
-  // without removals, with few breakpoints and the same row width; best effort (else rebuilt).
+  // instead of rebuilt from every box row (tfp_index.hpp): the ranges are searched again, every
+  // surviving column's bits move to its new column (removed clips' and an index delta's columns
+  // dropped: the delta's clips are among the new rows), then the new rows' bits are set. Best
+  // effort: on any failure the bitsets are rebuilt when next needed.
   const int32_t W = key_bits_words(new_cols);
-  if (brk.n >= 0 && e->rng_valid && e->key_bits_valid && e->key_bits_cols == (int32_t)e->col_clip.size() &&
-      key_bits_words((int32_t)e->col_clip.size()) == W &&
-      e->key_bits.bytes >= sizeof(uint32_t) * (size_t)kKeyRange * W) {
+  const int32_t Cm = (int32_t)e->col_clip.size();
+  if (e->rng_valid && e->key_bits_valid && e->key_bits_cols >= Cm &&
+      e->key_bits.bytes >= sizeof(uint32_t) * (size_t)kKeyRange * key_bits_words(e->key_bits_cols)) {
     hipStream_t s = e->stream;
     bool ok = launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, e->rng_tol, e->rng_all.as<int64_t>(), s) == hipSuccess &&
-              e->key_bits_b.reserve(e->key_bits.bytes) == hipSuccess;
-    for (int j = brk.n - 1; ok && j >= 0; j--) {
-      ok = launch_key_bits_insert(e->key_bits.as<uint32_t>(), e->key_bits_b.as<uint32_t>(), W, brk.p[j], s) == hipSuccess;
+              e->key_bits_b.reserve(sizeof(uint32_t) * (size_t)kKeyRange * W) == hipSuccess &&
+              launch_key_bits_remap(e->key_bits.as<uint32_t>(), key_bits_words(e->key_bits_cols), Cm,
+                                    brk.n >= 0 ? nullptr : e->remap.as<int32_t>(), brk, e->key_bits_b.as<uint32_t>(), W,
+                                    s) == hipSuccess;
+    if (ok) {
       std::swap(e->key_bits.p, e->key_bits_b.p);
       std::swap(e->key_bits.bytes, e->key_bits_b.bytes);
     }
@@ -896,6 +927,7 @@ int rebuild(tfp_engine* e) {
   e->built_staged = e->n_staged;
   e->removed_built = false;
   e->dirty = false;
+  e->index_version++;  // (other tolerances' cached ranges and bitsets are for the previous index)
   e->rng_valid = carried;  // the key-range and clip-set caches follow the index (merge_index may carry the ranges and bitsets)
   e->key_bits_valid = carried && e->key_bits_valid;
   if (e->key_bits_valid) e->key_bits_cols = e->ncols;
@@ -927,9 +959,40 @@ int full_index(tfp_engine* e) {
   return TFP_OK;
 }
 
-// Row ranges of every key's box at tolerance tole, cached per index version and tolerance.
+// The active tolerance's ranges and bitsets exchanged with slot t's.
+void swap_active(tfp_engine* e, TolSlot& t) {
+  e->rng_all.swap_with(t.rng_all);
+  e->key_bits.swap_with(t.key_bits);
+  std::swap(e->rng_tol, t.tol);
+  std::swap(e->rng_valid, t.rng_valid);
+  std::swap(e->key_bits_valid, t.bits_valid);
+  std::swap(e->key_bits_cols, t.bits_cols);
+}
+
+// Row ranges of every key's box at tolerance tole, cached per index version and tolerance: the
+// active tolerance's, and up to kTolSlots others (a search at another tolerance moves the active
+// ones into the least recently used slot, and takes its tolerance's from a slot when it is there).
 int ensure_ranges(tfp_engine* e, double tole, hipStream_t s) {
   if (e->rng_valid && memcmp(&e->rng_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  TolSlot* hit = nullptr;
+  TolSlot* victim = &e->tol_lru[0];
+  for (TolSlot& t : e->tol_lru) {
+    if (t.version != e->index_version) t.rng_valid = t.bits_valid = false;
+    if (t.rng_valid && memcmp(&t.tol, &tole, sizeof tole) == 0) hit = &t;
+    // the victim: a slot holding nothing valid, else the least recently used
+    if (t.rng_valid != victim->rng_valid ? !t.rng_valid : t.used < victim->used) victim = &t;
+  }
+  if (hit) {
+    swap_active(e, *hit);  // (the previous active ones, valid or not, into the slot)
+    hit->version = e->index_version;
+    hit->used = ++e->tol_clock;
+    return TFP_OK;
+  }
+  if (e->rng_valid) {
+    swap_active(e, *victim);  // the active ones kept; their buffers' old contents reused below
+    victim->version = e->index_version;
+    victim->used = ++e->tol_clock;
+  }
   HIPCHK(e, e->rng_all.reserve(sizeof(int64_t) * 2 * kKeyRange));
   HIPCHK(e, launch_key_ranges_all(e->m1s.as<int32_t>(), e->nrows, tole, e->rng_all.as<int64_t>(), s));
   e->rng_tol = tole;
@@ -944,7 +1007,11 @@ int delta_bits(tfp_engine* e, hipStream_t s);
 int ensure_key_bits(tfp_engine* e, hipStream_t s) {
   if (e->key_bits_valid) return TFP_OK;
   HIPCHK(e, e->key_bits.reserve(sizeof(uint32_t) * (size_t)kKeyRange * key_bits_words(e->ncols)));
-  HIPCHK(e, launch_key_bits(e->rng_all.as<int64_t>(), e->cols.as<int32_t>(), e->ncols, e->key_bits.as<uint32_t>(), s));
+  // the boxes' rows in all: a row is in the boxes of the keys within tol of its m1
+  const double tl = e->rng_tol;
+  const int64_t per_row = std::isfinite(tl) && tl >= 0 && tl < kKeyRange ? 2 * (int64_t)ceil(tl) + 2 : kKeyRange;
+  HIPCHK(e, launch_key_bits(e->rng_all.as<int64_t>(), e->cols.as<int32_t>(), e->ncols, e->nrows * std::min<int64_t>(per_row, kKeyRange),
+                            e->kb_win, e->kb_direct, e->key_bits.as<uint32_t>(), s));
   int rc = delta_bits(e, s);  // (the delta's columns, from its staged rows)
   if (rc) return rc;
   e->key_bits_valid = true;
@@ -974,7 +1041,8 @@ int delta_bits(tfp_engine* e, hipStream_t s) {
 bool delta_tol_ok(double tol) { return std::isfinite(tol) && tol >= 0.0 && tol <= 8.0; }
 
 bool delta_eligible(const tfp_engine* e) {
-  if (!e->use_delta || !e->built || e->force_full || e->force_merge || e->removed_built || e->n_staged >= INT32_MAX)
+  if (!e->use_delta || !e->built || e->force_full || e->force_merge || e->removed_built || e->n_staged >= INT32_MAX ||
+      (int64_t)e->col_clip.size() < e->delta_min_cols)
     return false;
   int64_t n = 0, rows = 0;
   for (size_t i = e->built_clips; i < e->clips.size(); i++)
@@ -1075,6 +1143,7 @@ int delta_update(tfp_engine* e) {
   }
   HIPCHK(e, hipStreamSynchronize(s));  // (dc and at are released on return)
   e->dirty = false;
+  e->index_version++;  // (other tolerances' cached ranges and bitsets are for the previous index)
   e->n_delta_updates++;
   if (e->dbg_index)
     fprintf(stderr, "[tfp] index delta: %d clips (%lld rows) beside %d main columns; %.3f ms\n", D, (long long)rows, Cm,
@@ -1433,13 +1502,18 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->dbg_index = tfp::knob("TFP_DEBUG_INDEX") != nullptr;
   if (const char* v = tfp::knob("TFP_TEST_FAIL_COMPACT")) e->fail_compact = (int32_t)atoi(v);
   if (const char* v = tfp::knob("TFP_TEST_FAIL_QUERY_SAMPLES")) e->fail_query_len = atoll(v);
+  if (const char* v = tfp::knob("TFP_KEYBITS_WIN")) e->kb_win = atoi(v);
+  if (const char* v = tfp::knob("TFP_KEYBITS_DIRECT")) e->kb_direct = atoll(v);
   e->force_full = tfp::knob("TFP_INDEX_FULL") != nullptr;
   if (const char* v = tfp::knob("TFP_WIDE_MIN_TOL")) e->wide_min_tol = atof(v);
   e->wide.points_only = tfp::knob("TFP_WIDE_POINTS") != nullptr;
   e->wide.ch128 = tfp::knob("TFP_WIDE_CH128") != nullptr;
   e->wide.unpacked = tfp::knob("TFP_WIDE_UNPACKED") != nullptr;
   if (const char* v = tfp::knob("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
-  if (const char* v = tfp::knob("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
+  if (const char* v = tfp::knob("TFP_INDEX_DELTA")) {
+    e->use_delta = atoi(v) != 0;
+    if (e->use_delta) e->delta_min_cols = 0;
+  }
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;

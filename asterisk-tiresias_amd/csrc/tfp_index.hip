@@ -197,18 +197,40 @@ __global__ __launch_bounds__(kThreads) void merge_write_kernel(
 }
 
 // One word of a key row with a zero bit inserted at column p (words below p's unchanged).
-__global__ void key_bits_insert_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, int32_t W, int32_t p) {
-  const int64_t n = (int64_t)kKeyRange * W;
-  const int32_t wp = p >> 5, bp = p & 31;
-  const uint32_t low = (1u << bp) - 1u;
+// The bitsets through a column renumbering (one thread per old row word): old column c < Cm moves to
+// remap[c] (-1: removed) or, without a table, to c plus the breakpoints <= c; columns >= Cm (an index
+// delta's, whose clips are among the merge's new rows) are dropped. The columns keep their order, so
+// a word's bits land in a few new words, each ORed in once; dst (Wn words per row) is zero on entry.
+__global__ void key_bits_remap_kernel(const uint32_t* __restrict__ src, int32_t Wo, int32_t Cm, const int32_t* __restrict__ remap,
+                                      MergeBreaks brk, uint32_t* __restrict__ dst, int32_t Wn) {
+  const int64_t n = (int64_t)kKeyRange * Wo;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t w = (int32_t)(i % W);
-    const uint32_t x = src[i];
-    uint32_t y;
-    if (w < wp) y = x;
-    else if (w == wp) y = (x & low) | ((x << 1) & ~(low | (1u << bp)));
-    else y = (x << 1) | (src[i - 1] >> 31);
-    dst[i] = y;
+    const int32_t w = (int32_t)(i % Wo);
+    const int64_t k = i / Wo;
+    if (32 * w >= Cm) continue;
+    uint32_t x = src[i];
+    if (32 * w + 32 > Cm) x &= (1u << (Cm - 32 * w)) - 1u;
+    uint32_t acc = 0;
+    int32_t aw = -1;
+    while (x) {
+      const int b = __ffs(x) - 1;
+      x &= x - 1;
+      const int32_t c = 32 * w + b;
+      int32_t nc = c;
+      if (remap) {
+        nc = remap[c];
+      } else {
+        for (int j = 0; j < brk.n; j++) nc += c >= brk.p[j];
+      }
+      if (nc < 0) continue;
+      if ((nc >> 5) != aw) {
+        if (aw >= 0) atomicOr(&dst[k * Wn + aw], acc);
+        aw = nc >> 5;
+        acc = 0;
+      }
+      acc |= 1u << (nc & 31);
+    }
+    if (aw >= 0) atomicOr(&dst[k * Wn + aw], acc);
   }
 }
 
@@ -234,10 +256,13 @@ __global__ __launch_bounds__(64) void key_bits_add_kernel(const int64_t* __restr
 
 }  // namespace
 
-hipError_t launch_key_bits_insert(const uint32_t* src, uint32_t* dst, int32_t W, int32_t p, hipStream_t s) {
-  const int64_t n = (int64_t)kKeyRange * W;
-  hipLaunchKernelGGL(key_bits_insert_kernel, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, s, src,
-                     dst, W, p);
+hipError_t launch_key_bits_remap(const uint32_t* src, int32_t Wo, int32_t Cm, const int32_t* d_remap, const MergeBreaks& brk,
+                                 uint32_t* dst, int32_t Wn, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(dst, 0, sizeof(uint32_t) * (size_t)kKeyRange * Wn, s);
+  if (e) return e;
+  const int64_t n = (int64_t)kKeyRange * Wo;
+  hipLaunchKernelGGL(key_bits_remap_kernel, dim3((unsigned)std::min<int64_t>(8192, (n + 255) / 256)), dim3(256), 0, s, src,
+                     Wo, Cm, d_remap, brk, dst, Wn);
   return hipGetLastError();
 }
 

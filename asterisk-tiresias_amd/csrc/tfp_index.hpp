@@ -45,11 +45,14 @@ hipError_t launch_merge_update(const int32_t* m1s, const int32_t* m2s, const int
 
 // The key-presence bitsets (launch_key_bits: W words per key row, bit c = column c has a row in
 // the key's box) carried across such an update instead of rebuilt from every box row:
-// key_bits_insert copies src to dst with a zero bit inserted at column p of every row (the
-// breakpoints, highest first), key_bits_add then sets the new rows' bits. A new row is in key k's
-// box iff its m1 lies between the first and the last m1 of the box's rows in the merged index
-// (d_rng_all at the bitsets' tolerance, recomputed for it): the box is an interval and holds the row.
-hipError_t launch_key_bits_insert(const uint32_t* src, uint32_t* dst, int32_t W, int32_t p, hipStream_t s);
+// key_bits_remap moves every surviving old column's bits (columns < Cm of rows Wo words wide) to
+// its new column (d_remap, or the breakpoints when d_remap is null) in dst (rows Wn words wide;
+// removed clips' and an index delta's columns dropped), key_bits_add then sets the new rows' bits.
+// A new row is in key k's box iff its m1 lies between the first and the last m1 of the box's rows
+// in the merged index (d_rng_all at the bitsets' tolerance, recomputed for it): the box is an
+// interval and holds the row.
+hipError_t launch_key_bits_remap(const uint32_t* src, int32_t Wo, int32_t Cm, const int32_t* d_remap, const MergeBreaks& brk,
+                                 uint32_t* dst, int32_t Wn, hipStream_t s);
 hipError_t launch_key_bits_add(const int64_t* d_rng_all, const int32_t* m1s, const int32_t* nm1, const int32_t* ncol,
                                int64_t n, int32_t W, uint32_t* bits, hipStream_t s);
 

@@ -2137,26 +2137,95 @@ __device__ __forceinline__ int small_kc(const SmallKeySet& K, int key) {
   return K.pre[w] + __popc(K.mask[w] & ((1u << (key & 31)) - 1u));
 }
 
-// Key-presence bitsets: one block row-range share per (key, slice); rows of a box spread over
-// kKeyBitsSlices blocks (a box can hold most of the index at wide tolerances).
-constexpr int kKeyBitsSlices = 16;
-__global__ __launch_bounds__(256) void key_bits_kernel(const int64_t* __restrict__ rng_all, const int32_t* __restrict__ cols,
-                                                       int32_t W, uint32_t* __restrict__ bits) {
-  const int key = blockIdx.x;
-  const int64_t lo = rng_all[2 * key], hi = rng_all[2 * key + 1];
-  uint32_t* row = bits + (int64_t)key * W;
-  const int64_t stride = (int64_t)kKeyBitsSlices * blockDim.x;
-  for (int64_t r = lo + (int64_t)blockIdx.y * blockDim.x + threadIdx.x; r < hi; r += stride) {
-    const int32_t c = cols[r];
-    atomicOr(&row[c >> 5], 1u << (c & 31));
+// Key-presence bitsets without a global atomic per box row (round 5; the round-2 kernel's
+// atomicOr per row serialised in L2 on the few dense keys: 42-50 ms at tolerance 0.45 on 100k
+// clips, where one key's box holds ~84 M rows). A key's box rows are a contiguous range of the
+// m1-sorted index, so the grid walks the concatenation of all keys' ranges in chunks of kKbChunk
+// rows (every block scans the 1,024 range sizes into an LDS prefix first). Per piece of a key in its
+// chunk, the block sets the piece's bits in an LDS copy of the key's row (one LDS OR per row) and
+// then ORs its nonzero words into the row in memory (one atomic per word: the key's other chunks
+// share the row). Pieces under `direct` rows (small boxes) set their bits with global atomics
+// directly. A row wider than the LDS window (win words) is done window by window.
+constexpr int kKbChunk = 1 << 16;
+constexpr int kKbThreads = 256;
+__global__ __launch_bounds__(kKbThreads) void key_bits_kernel(const int64_t* __restrict__ rng_all, const int32_t* __restrict__ cols,
+                                                              int32_t W, int32_t win, int64_t direct, uint32_t* __restrict__ bits) {
+  extern __shared__ uint32_t lrow[];  // win words
+  __shared__ int64_t pre[kKeyRange + 1];
+  __shared__ int64_t part[kKbThreads];
+  const int t = threadIdx.x;
+  constexpr int kPer = kKeyRange / kKbThreads;
+  int64_t sz[kPer], sum = 0;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    const int k = t * kPer + j;
+    sz[j] = max((int64_t)0, rng_all[2 * k + 1] - rng_all[2 * k]);
+    sum += sz[j];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < kKbThreads; o <<= 1) {  // inclusive scan of the per-thread sums
+    const int64_t y = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += y;
+    __syncthreads();
+  }
+  int64_t run = part[t] - sum;
+#pragma unroll
+  for (int j = 0; j < kPer; j++) {
+    pre[t * kPer + j] = run;
+    run += sz[j];
+  }
+  if (t == kKbThreads - 1) pre[kKeyRange] = part[t];
+  __syncthreads();
+  const int64_t total = pre[kKeyRange];
+  for (int64_t v0 = (int64_t)blockIdx.x * kKbChunk; v0 < total; v0 += (int64_t)gridDim.x * kKbChunk) {
+    const int64_t v1 = min(total, v0 + kKbChunk);
+    int k = 0, hi = kKeyRange;  // the key whose range holds v0: the last k with pre[k] <= v0
+    while (hi - k > 1) {
+      const int mid = (k + hi) >> 1;
+      if (pre[mid] <= v0) k = mid; else hi = mid;
+    }
+    for (; k < kKeyRange && pre[k] < v1; k++) {
+      const int64_t a = max(v0, pre[k]), b = min(v1, pre[k + 1]);
+      if (a >= b) continue;
+      const int32_t* c = cols + rng_all[2 * k] + (a - pre[k]);
+      const int64_t n = b - a;
+      uint32_t* row = bits + (int64_t)k * W;
+      if (n < direct) {  // (block-uniform)
+        for (int64_t i = t; i < n; i += kKbThreads) atomicOr(&row[c[i] >> 5], 1u << (c[i] & 31));
+        continue;
+      }
+      for (int32_t w0 = 0; w0 < W; w0 += win) {
+        const int32_t wn = min(win, W - w0);
+        const int32_t c0 = 32 * w0, c1 = 32 * (w0 + wn);
+        for (int32_t j = t; j < wn; j += kKbThreads) lrow[j] = 0u;
+        __syncthreads();
+        for (int64_t i = t; i < n; i += kKbThreads) {
+          const int32_t x = c[i];
+          if (x >= c0 && x < c1) atomicOr(&lrow[(x - c0) >> 5], 1u << (x & 31));
+        }
+        __syncthreads();
+        for (int32_t j = t; j < wn; j += kKbThreads)
+          if (lrow[j]) atomicOr(&row[w0 + j], lrow[j]);
+        __syncthreads();
+      }
+    }
   }
 }
 
-hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, uint32_t* d_bits, hipStream_t s) {
+hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, int64_t rows_bound, int32_t win,
+                           int64_t direct, uint32_t* d_bits, hipStream_t s) {
   const int32_t W = key_bits_words(C);
   hipError_t e = hipMemsetAsync(d_bits, 0, sizeof(uint32_t) * (size_t)kKeyRange * W, s);
   if (e) return e;
-  hipLaunchKernelGGL(key_bits_kernel, dim3(kKeyRange, kKeyBitsSlices), dim3(256), 0, s, d_rng_all, cols, W, d_bits);
+  // LDS window: the whole row up to 16 K words (64 KB: 524,288 columns), else windows of it
+  win = win > 0 ? std::min(win, W) : std::min<int32_t>(W, 16384);
+  win = std::max(win, 1);
+  if (direct < 0) direct = std::max<int64_t>(2048, W / 2);  // a piece below a few row-clears of work
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(4096, (rows_bound + kKbChunk - 1) / kKbChunk));
+  hipLaunchKernelGGL(key_bits_kernel, dim3(grid), dim3(kKbThreads), sizeof(uint32_t) * (size_t)win, s, d_rng_all, cols, W,
+                     win, direct, d_bits);
   return hipGetLastError();
 }
 

@@ -169,9 +169,12 @@ inline size_t small_result_bytes(int32_t C) {
 TFP_HD unsigned long long* small_result_parts(SmallResult* r) { return reinterpret_cast<unsigned long long*>(r + 1); }
 // Key-presence bitsets: d_bits[k][w] (kKeyRange rows of W = key_bits_words(C) words), bit c of row
 // k set iff column c has an index row in key k's box (d_rng_all, the cached row ranges). Cleared
-// and rebuilt on the stream.
+// and rebuilt on the stream. rows_bound: at least the sum of the boxes' row counts (sizes the
+// grid; more is harmless). win (LDS words per column window) and direct (pieces below it use
+// global atomics): <= 0 / < 0 for the defaults; tests force small windows and either path.
 TFP_HD int32_t key_bits_words(int32_t C) { return (C + 127) / 128 * 4; }  // rows 16-byte aligned
-hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, uint32_t* d_bits, hipStream_t s);
+hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_t C, int64_t rows_bound, int32_t win,
+                           int64_t direct, uint32_t* d_bits, hipStream_t s);
 // h_out: host-mapped memory of small_result_bytes(C) the device writes.
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, const uint32_t* d_bits,
                                int32_t C, const int32_t* d_tiekey, SmallResult* h_out, hipStream_t s);

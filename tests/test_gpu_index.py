@@ -400,3 +400,98 @@ def test_add_only_updates_empty_and_null_rows(tfp_lib, oracle, delta):
         assert eng.index_stats() == (sum(len(r[0]) for r in mir.rows.values()), len(mir.rows))
     finally:
         eng.close()
+
+
+def _dense_db(rng, nclips, nrow):
+    """Clips whose rows crowd into keys 16-18 (fractions across the whole key, so the 0.45 boxes
+    hold thousands of rows each and the 0.001 boxes a few): every key-bits path gets big pieces."""
+    data = []
+    for _ in range(nclips):
+        k = rng.choice([16, 17, 17, 18], nrow)
+        m1 = (k * 1_000_000 + rng.integers(-499_000, 499_000, nrow)).astype(np.int32)
+        m1[: nrow // 10] = (k[: nrow // 10] * 1_000_000 + rng.integers(-900, 900, nrow // 10)).astype(np.int32)
+        m2 = rng.integers(0, 30_000_000, nrow).astype(np.int32)
+        data.append((m1, m2))
+    return data
+
+
+def _check_batch1(eng, oracle, tfp_lib, mir, data, sources, p, rng, step):
+    q = []
+    for c in sources:
+        m1, m2 = data[c]
+        sel = rng.integers(0, len(m1), 30)
+        q.append(np.stack([m1[sel] / 1e6 + 0.0004, m2[sel] / 1e6], axis=1))
+    qdb = np.concatenate(q)
+    qoff = np.arange(len(sources) + 1, dtype=np.int64) * 30
+    exp = mir.search(oracle, qdb[:, 0], qdb[:, 1], qoff, p)
+    fr = _frames(tfp_lib, qdb)
+    for i in range(len(sources)):
+        r, _ = eng.search(fr[qoff[i]:qoff[i + 1]], p)  # batch-1: the small path over the key bitsets
+        assert (None if r is None else (r["audio_uuid"], r["match_count"])) == exp[i], (step, p.tolerance, i)
+    return sum(e is not None for e in exp)
+
+
+@pytest.mark.parametrize("knobs", [{}, {"TFP_KEYBITS_WIN": "4"}, {"TFP_KEYBITS_DIRECT": "0"},
+                                   {"TFP_KEYBITS_DIRECT": "1000000000"}, {"TFP_KEYBITS_WIN": "8", "TFP_KEYBITS_DIRECT": "0"}])
+def test_key_bits_build_forms(tfp_lib, oracle, knobs):
+    """launch_key_bits (round 5): the boxes' rows walked in chunks, each piece's bits set in an LDS
+    copy of the key's row and ORed into memory once per word, small pieces with global atomics,
+    rows wider than the LDS window window by window. Forced forms (windows of 4 / 8 words = 128 /
+    256 columns over 700 clips; every piece through LDS; every piece direct) == the default ==
+    the oracle, on boxes of thousands of rows (tol 0.45) and of a few (tol 0.001)."""
+    rng = np.random.default_rng(5150)
+    data = _dense_db(rng, 700, 50)
+    uu = _uuids(rng, 700)
+    eng = _engine_with(tfp_lib, knobs)
+    mir = Mirror()
+    try:
+        for c in range(700):
+            eng.index_add(uu[c], *data[c])
+            mir.rows[uu[c]] = data[c]
+        eng.index_commit()
+        found = 0
+        for tol in (0.45, 0.001, 0.2, 1.5):
+            found += _check_batch1(eng, oracle, tfp_lib, mir, data, [int(x) for x in rng.integers(0, 700, 6)],
+                                   tfp_lib.params(1, tol), rng, "build")
+        assert found > 10
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("delta", ["0", "1"])
+def test_tolerance_alternation_and_removals(tfp_lib, oracle, delta):
+    """The dialplan passes the tolerance per call (application_handler.c:114-122): batch-1 searches
+    alternating between tolerances (0.001 and 0.45, and two more, so the engine's cache of other
+    tolerances' key ranges and bitsets evicts its least recently used entry) between adds and
+    removals of indexed clips (the bitsets carried through the column renumbering, removed columns
+    dropped, src/fp_handler.c:115-159): every search == the oracle over the live rows."""
+    rng = np.random.default_rng(4242)
+    data = _dense_db(rng, 460, 40)
+    uu = _uuids(rng, 460)
+    uu[450] = "00000000-0000-4000-8000-000000000002"  # sorts first
+    eng = _engine_with(tfp_lib, {"TFP_INDEX_DELTA": delta})
+    mir = Mirror()
+    tols = [0.001, 0.45, 0.001, 0.45, 0.1, 0.3, 0.45, 0.001, 0.7, 0.45]
+    try:
+        for c in range(420):
+            eng.index_add(uu[c], *data[c])
+            mir.rows[uu[c]] = data[c]
+        eng.index_commit()
+        found = 0
+        live = list(range(420))
+        for step, op in enumerate(["-", "remove", "add", "-", "remove", "remove", "add", "add", "-", "remove"]):
+            if op == "remove":
+                c = live.pop(int(rng.integers(len(live))))
+                eng.index_remove(uu[c])
+                del mir.rows[uu[c]]
+            elif op == "add":
+                c = 420 + step if step != 6 else 450
+                eng.index_add(uu[c], *data[c])
+                mir.rows[uu[c]] = data[c]
+                live.append(c)
+            for tol in tols[step:] + tols[:step]:
+                src = [int(live[int(x)]) for x in rng.integers(0, len(live), 2)]
+                found += _check_batch1(eng, oracle, tfp_lib, mir, data, src, tfp_lib.params(1, tol), rng, (step, op))
+        assert found > 50
+    finally:
+        eng.close()
