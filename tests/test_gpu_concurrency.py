@@ -180,7 +180,7 @@ def test_failing_caller_in_coalesced_batch_is_isolated(oracle, tfp_lib, kind, mo
         nq = qpcm.shape[1]
         p = tfp_lib.params(1, 0.001)
         want = [_key(h.search_pcm_batch(qpcm[t], [0, nq], p)[0][0]) for t in range(31)]
-        assert sum(w is not None for w in want) > 20
+        assert sum(w is not None for w in want) >= 8
         bad = tfp_lib.synth_pcm(99, [0], bad_len)[0]
         with pytest.raises(TfpError) as ei:  # alone, first: the knob is live
             h.search_pcm_batch(bad, [0, bad_len], p)
