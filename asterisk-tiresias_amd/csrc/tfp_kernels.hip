@@ -947,6 +947,19 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
 
     for (int sub = 0; sub < kPasses; sub++) {
       const int row = sub * 4 + grp;
+      // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
+      // them into registers for the whole kernel (occupancy).
+      int oz = 0;
+      asm volatile("" : "+v"(oz));
+      // the pass's window values (a table no one writes) requested before the syncs of the PCM
+      // staging, so their latency overlaps it
+      cf wreg[16];
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const float4 w4 = *reinterpret_cast<const float4*>(winr + (i * 16 + L) * 2 + oz);
+        wreg[2 * i] = cf{w4.x, w4.y};
+        wreg[2 * i + 1] = cf{w4.z, w4.w};
+      }
       wave_sync();  // the previous pass's readers of the scratch are done
       TFP_STAMP(0);
 #pragma unroll
@@ -959,17 +972,6 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
       wave_sync();
       TFP_STAMP(1);
       const int16_t* hop0 = M.pcm + grp * kHopStride;
-      // Opaque zero: keeps the per-lane table reads in LDS instead of letting the compiler hoist
-      // them into registers for the whole kernel (occupancy).
-      int oz = 0;
-      asm volatile("" : "+v"(oz));
-      cf wreg[16];
-#pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const float4 w4 = *reinterpret_cast<const float4*>(winr + (i * 16 + L) * 2 + oz);
-        wreg[2 * i] = cf{w4.x, w4.y};
-        wreg[2 * i + 1] = cf{w4.z, w4.w};
-      }
       // z[m] = x[2m] + i x[2m+1], x = fftshift(hanningz * [hop f-1 | hop f]); lane L holds
       // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
       // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
@@ -984,6 +986,11 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
       dft16q(w16r, z, Y);
 #pragma unroll
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
+      // the split's twiddles (a table no one writes) requested now: in flight during the transpose
+      const float4* tw4 = reinterpret_cast<const float4*>(twr + 2 * L + oz);  // + 16 k2: one base, immediate offsets
+      float4 t4s[8];
+#pragma unroll
+      for (int k2 = 0; k2 < 8; k2++) t4s[k2] = tw4[16 * k2];
       wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
       TFP_STAMP(2);
 #pragma unroll
@@ -1014,14 +1021,13 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
       // v_sqrt_f32: that returns 0 for denormal inputs; tests/native/check_fast_sqrt.hip.)
       uint32_t umin = 0xffffffffu;
       float nk[8], nk2[8];
-      const float4* tw4 = reinterpret_cast<const float4*>(twr + 2 * L + oz);  // + 16 k2: one base, immediate offsets
 #pragma unroll
       for (int k2 = 0; k2 < 8; k2++) {
         const cf own = Y[k2 == 0 ? 8 : 16 - k2];
         cf y = Y[k2];
         if (k2 == 0) y = cf{L == 0 ? own.x : y.x, L == 0 ? own.y : y.y};
         const cf p = cf{L == 0 ? own.x : Pq[k2].x, L == 0 ? own.y : Pq[k2].y};
-        const float4 t4 = tw4[16 * k2];
+        const float4 t4 = t4s[k2];
         const cf sq = split_pair_sq(y, p, cf{t4.x, t4.y}, cf{t4.z, t4.w});
         sqrt_pair_cr(sq, nk[k2], nk2[k2]);
         umin = min(umin, rare_key_pair(sq));
@@ -1099,23 +1105,58 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
             jk[k] = fbk[k];
           }
           // a step pair's weights: one ds_read_b64 each, whose halves the packed multiplies
-          // broadcast with op_sel (a b128 of 4 steps made the compiler move the halves apart)
+          // broadcast with op_sel (a b128 of 4 steps made the compiler move the halves apart).
+          // The segments' sums are stored after the last step: a store to the log rows between
+          // them kept the compiler from hoisting the later reads above it (it cannot tell the two
+          // LDS arrays apart), so the phase waited out the LDS latency once per segment.
           const cf* const wfb = reinterpret_cast<const cf*>(S.fbw) + L + oz;
+          // Each segment's reads are issued one segment ahead of its sums (all of them at once
+          // needed 108 VGPRs and spilled); the compiler barriers keep them in those groups.
+          cf seg[kFbSegs];
+          cf wv[kFbSteps / 2];
+          f4v nv[kFbSteps / 2];
+          auto load_seg = [&](auto kk) {
+            constexpr int k = decltype(kk)::value;
 #pragma unroll
-          for (int st = 0; st < kFbSteps; st += 2) {
-            const int k = fb_seg(st);
-            const cf wv = wfb[(st >> 1) * kFbPatterns];
-            const f4v nv = *reinterpret_cast<const f4v*>(jb[k] + 2 * st);
-            const cf p0 = cf{nv.x, nv.y} * cf{wv.x, wv.x};
-            const cf p1 = cf{nv.z, nv.w} * cf{wv.y, wv.y};
-            if (st == 0) acc = p0;
-            else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{jk[k], jk[k]}, p0);
-            else acc = acc + p0;
-            acc = acc + p1;
-            if (st + 2 == kFbSegStart[k + 1]) {
-              jc[k][doff] = acc.x;
-              jc[k][doff + 2 * kFbNf] = acc.y;
+            for (int st = kFbSegStart[k]; st < kFbSegStart[k + 1]; st += 2) {
+              wv[st >> 1] = wfb[(st >> 1) * kFbPatterns];
+              nv[st >> 1] = *reinterpret_cast<const f4v*>(jb[k] + 2 * st);
             }
+          };
+          auto sum_seg = [&](auto kk) {
+            constexpr int k = decltype(kk)::value;
+#pragma unroll
+            for (int st = kFbSegStart[k]; st < kFbSegStart[k + 1]; st += 2) {
+              const int i = st >> 1;
+              const cf p0 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].x};
+              const cf p1 = cf{nv[i].z, nv[i].w} * cf{wv[i].y, wv[i].y};
+              if (st == 0) acc = p0;
+              else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{jk[k], jk[k]}, p0);
+              else acc = acc + p0;
+              acc = acc + p1;
+            }
+            seg[k] = acc;
+          };
+          using I0 = std::integral_constant<int, 0>;
+          using I1 = std::integral_constant<int, 1>;
+          using I2 = std::integral_constant<int, 2>;
+          using I3 = std::integral_constant<int, 3>;
+          static_assert(kFbSegs == 4, "four segments");
+          load_seg(I0{});
+          load_seg(I1{});
+          asm volatile("" ::: "memory");
+          sum_seg(I0{});
+          load_seg(I2{});
+          asm volatile("" ::: "memory");
+          sum_seg(I1{});
+          load_seg(I3{});
+          asm volatile("" ::: "memory");
+          sum_seg(I2{});
+          sum_seg(I3{});
+#pragma unroll
+          for (int k = 0; k < kFbSegs; k++) {
+            jc[k][doff] = seg[k].x;
+            jc[k][doff + 2 * kFbNf] = seg[k].y;
           }
         };
         if (sub == 1) pair_fb(std::integral_constant<int, 0>{});
