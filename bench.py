@@ -645,6 +645,8 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             "sweeps": sweeps}
     if world == 1 and not args.no_enrol:
         res["enrol_then_search"] = enrol_latency(args, eng, T, torch, dev, sh, p)
+    if world == 1:
+        res["tolerance_alternation"] = tol_alternation(args, eng, T, host_q, qn)
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = match_cpu_baseline(args, T, eng, torch, dev, sh)
         res["cpu_baseline_full_db"] = match_cpu_full_db(args, eng, torch, dev, sh, qpcm[:256].cpu().numpy())
@@ -715,13 +717,16 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
             res, _ = e.search_pcm_batch(q, [0, qn], pq)
             out.append((time.perf_counter() - t0) * 1e3)
             hits[tag] += res[0] is not None and res[0]["audio_uuid"] == u
+        t0 = time.perf_counter()  # the closing removals and the update they trigger (a deferred delta merges here)
         for u in uuids:
             e.index_remove(u)
         e.index_commit()
-        log(f"enrol-then-search ({tag}): p50 {np.percentile(out, 50):.2f} ms, new clip won {hits[tag]}/{len(uuids)}")
+        closing[tag] = (time.perf_counter() - t0) * 1e3
+        log(f"enrol-then-search ({tag}): p50 {np.percentile(out, 50):.2f} ms, new clip won {hits[tag]}/{len(uuids)}, "
+            f"closing removals {closing[tag]:.2f} ms")
         return out
 
-    hits = {}
+    hits, closing = {}, {}
     fb0, mg0 = eng.index_build_stats()
     nd0, _ = eng.index_delta_stats()
     inc = run(eng, "engine")
@@ -740,18 +745,83 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
     full = run(full_eng, "full re-sort")
     full_eng.close()
     torch.cuda.empty_cache()
+    # the same workload with a merge per update (TFP_INDEX_DELTA=0, the round-3 path): like for like
+    os.environ["TFP_INDEX_DELTA"] = "0"
+    os.environ["TFP_TEST_KNOBS"] = "1"
+    try:
+        merge_eng = T.Engine(eng.device)
+    finally:
+        del os.environ["TFP_INDEX_DELTA"]
+        del os.environ["TFP_TEST_KNOBS"]
+    enroll(merge_eng, torch, dev, sh, list(range(args.db_clips)))
+    merge_eng.index_commit()
+    merge_eng.search_pcm_batch(np.ascontiguousarray(pcm[0, :qn]), [0, qn], pq)
+    merged = run(merge_eng, "merge per update")
+    merge_eng.close()
+    torch.cuda.empty_cache()
     return {"workload": f"{n_add} x (tfp_index_add of one 30 s clip + batch-1 search of a 5 s excerpt of it, coefs 1, "
                         f"tolerance 0.45) on the {args.db_clips}-clip DB, host PCM",
             "p50_ms": float(np.percentile(inc, 50)), "max_ms": float(np.max(inc)), "samples_ms": inc,
             "index_updates": {"delta_updates": nd1 - nd0, "merges": mg1 - mg0, "full_sorts": fb1 - fb0,
                               "how": "each add a delta update (the clip's rows beside the sorted index, tfp_index_delta_stats); "
                                      "the closing removals merge the delta once"},
+            "closing_removals_ms": closing,
+            "merge_per_update": {"p50_ms": float(np.percentile(merged, 50)), "max_ms": float(np.max(merged)),
+                                 "samples_ms": merged,
+                                 "how": "same workload on an engine with TFP_INDEX_DELTA=0 (each update merged into the "
+                                        "sorted index at once, the round-3 path): the like-for-like comparison for the delta"},
             "new_clip_won": hits,
             "new_clips": "full-scale white noise, uuids above the DB's: only a new clip's rows lie in the query's "
                          "key box (see enrol_latency)",
             "full_resort": {"p50_ms": float(np.percentile(full, 50)), "max_ms": float(np.max(full)), "samples_ms": full,
                             "how": "same calls on an engine with TFP_INDEX_FULL=1 (every update a full radix sort of all "
                                    "staged rows + a uuid sort), the round-2 behaviour"}}
+
+
+def tol_alternation(args, eng, T, hq, qn, n_calls=200):
+    """The dialplan passes the tolerance per call (application_handler.c:114-122), so two extensions
+    at different tolerances alternate on the one engine: batch-1 searches (host PCM in -> result
+    out) alternating tolerance 0.001 and 0.45 on the 100k-clip DB, p50 / p99. The engine keeps other
+    tolerances' key ranges and bitsets beside the active ones (tfp_engine::tol_lru), and a new
+    tolerance's bitsets are built without per-row atomics (launch_key_bits, round 5; the round-4
+    build took 42-50 ms at 0.45). Also: the first search at a tolerance not used before (its ranges
+    and bitsets built inside the call), and the first searches after the removal of an indexed clip
+    (fp_handler.c:115-159: the removal merges the index; the active bitsets are carried through the
+    column renumbering, the other tolerance's rebuilt). The removed clip is added back afterwards."""
+    p_lo, p_hi = T.params(1, 0.001), T.params(1, 0.45)
+    for i in range(4):  # untimed: both tolerances' caches
+        eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
+    lat = []
+    for i in range(n_calls):
+        t0 = time.perf_counter()
+        eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    cold = []
+    for tol in (0.44, 0.3):  # tolerances no search used before: ranges + bitsets built in the call
+        t0 = time.perf_counter()
+        eng.search_pcm_batch(hq[0], [0, qn], T.params(1, tol))
+        cold.append((time.perf_counter() - t0) * 1e3)
+    u = uuid_of(17)
+    m1, m2 = eng.index_rows(u)
+    eng.index_remove(u)
+    after = []
+    for i, pp in enumerate((p_hi, p_lo, p_hi, p_lo)):
+        t0 = time.perf_counter()
+        eng.search_pcm_batch(hq[i + 1], [0, qn], pp)
+        after.append((time.perf_counter() - t0) * 1e3)
+    eng.index_add(u, m1, m2)
+    eng.index_commit()
+    out = {"workload": f"{n_calls} batch-1 searches of 5 s host-PCM queries on the {args.db_clips}-clip DB, coefs 1, "
+                       "tolerance alternating 0.001 / 0.45 per call",
+           "p50_ms": float(np.percentile(lat, 50)), "p99_ms": float(np.percentile(lat, 99)), "max_ms": float(np.max(lat)),
+           "first_search_at_new_tolerance_ms": {"0.44": cold[0], "0.3": cold[1]},
+           "after_removal_ms": {"first (0.45: the index merge + carried bitsets)": after[0],
+                                "second (0.001: its ranges and bitsets rebuilt)": after[1],
+                                "third (0.45)": after[2], "fourth (0.001)": after[3]},
+           "harness": "python (ctypes) loop over tfp_search_pcm_batch"}
+    log(f"tolerance alternation: p50 {out['p50_ms']:.3f} ms p99 {out['p99_ms']:.3f} ms; new tolerance {cold[0]:.2f} ms; "
+        f"after a removal {after[0]:.2f} / {after[1]:.2f} ms")
+    return out
 
 
 def match_cpu_baseline(args, T, eng, torch, dev, sh):
