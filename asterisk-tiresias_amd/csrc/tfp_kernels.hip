@@ -101,7 +101,7 @@ struct LdsTables {
   int32_t c_defer, c_real[2];  // slot-2 log deferral (DspTables::ms_c_defer)
   union {
     alignas(16) float ms_w[kMsLds];                  // slot schedule (fingerprint_kernel, fingerprint8k_kernel<1>)
-    alignas(16) float fbw[kFbSteps * kFbPatterns];  // frame-pair schedule (fingerprint8k_kernel<4>)
+    alignas(16) float fbw[kFbSteps * kFbPatterns];  // frame-pair schedule (fingerprint8k_kernel<4>): [step / 4][pattern][step % 4]
   };
 };
 
@@ -758,6 +758,15 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
   struct Tile {
     int c;
     int64_t f0, s0, ns;
+    __amdgpu_buffer_rsrc_t rs;  // (throughput launches) the clip's whole 4-byte words, fetchd
+    bool odd;                   // ... and whether it starts on an odd sample
+  };
+  // The clip's bytes as a buffer: its whole 4-byte words (an odd start: from one sample before).
+  auto clip_rsrc = [&](int64_t s0, int64_t ns) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(pcm + s0);
+    const int16_t* base = reinterpret_cast<const int16_t*>(a & ~(uintptr_t)3);
+    const int64_t bytes = (2 * ns + (int64_t)(a & 3) + 3) & ~(int64_t)3;
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(base), (short)0, (int)bytes, 0x00020000);
   };
   auto tile_of = [&](int b) {
     Tile t;
@@ -772,6 +781,10 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
     t.f0 = (int64_t)(b - toff[t.c]) * (4 * kPasses);
     t.s0 = sbeg[t.c];
     t.ns = send[t.c] - t.s0;
+    if constexpr (kPairFb) {
+      t.rs = clip_rsrc(t.s0, t.ns);
+      t.odd = (reinterpret_cast<uintptr_t>(pcm + t.s0) & 3) != 0;
+    }
     return t;
   };
   // 16-byte PCM chunks of pass `sub` of tile t (samples [(f0 + 4 sub - 1) 256, + 1280)) into registers.
@@ -811,12 +824,34 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
     }
   };
 
+  // Direct PCM (throughput launches, round 5): lane (grp, L) loads its own frame's 16 sample
+  // pairs straight into registers, one pass ahead: for n1 < 8 the pair 32 n1 + 2L of hop f, for
+  // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f - 1 (z's fftshifted layout), as buffer loads over
+  // the clip's bytes, one offset register and immediate offsets. No LDS staging of the pass's PCM
+  // (3 16-byte stores and 8 paired reads per lane before). Samples outside the clip (the zero hop
+  // before frame 0, the zero-padded tail) are masked where the pass uses them (pcm_pair); the
+  // buffer's range only keeps every load inside the clip's 4-byte words (0 beyond). A clip that
+  // starts on an odd sample (a stream window after odd-sized ticks) has no 4-byte-aligned pairs:
+  // its passes read each pair from two aligned words, synchronously (pcm_pair_odd).
+  // (a launch's last tiles fetch their "next" pass from their own clip: loaded, never used)
+  auto fetchd = [&](const Tile& t, int sub, uint32_t (&pw)[16]) {
+    if (t.odd) return;  // (odd start: read when used)
+    const __amdgpu_buffer_rsrc_t rs = t.rs;
+    const int32_t fs = (int32_t)((t.f0 + 4 * sub - 1 + grp) * kHop) + 2 * L;  // this frame's first sample + 2L
+#pragma unroll
+    for (int n1 = 0; n1 < 16; n1++) {
+      const int32_t j = n1 < 8 ? 256 + 32 * n1 : 32 * (n1 - 8);
+      pw[n1] = __builtin_amdgcn_raw_buffer_load_b32(rs, 2 * (fs + j), 0, 0);
+    }
+  };
+
   // The first tile's bounds are known before the tables are staged (a one-clip launch passes
   // them as an argument), and its PCM is requested right after the table loads, so its latency
   // overlaps the staging (most of a small launch's time). The PCM is prefetched one pass ahead
   // (a two-pass distance measured no faster: the pass is bound by instruction issue, not by the
   // PCM loads).
   int4 pf[kChunkRounds];
+  uint32_t pw[16];  // (throughput launches: the next pass's sample pairs, fetchd)
   int b = blockIdx.x * kBW + wave;
   Tile cur = tile_of(b < ntiles ? b : 0);
   // window and split twiddles in lane-interleaved pair layouts, [i][L][2] cf: lane L's values for
@@ -854,13 +889,21 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
   float mw[(kMsW + kStage - 1) / kStage];
 #pragma unroll
   for (int r = 0; r < (kMsW + kStage - 1) / kStage; r++) {
-    const int idx = ts + kStage * r;
-    mw[r] = wsrc[idx < kMsW ? idx : kMsW - 1];
+    int idx = ts + kStage * r;
+    idx = idx < kMsW ? idx : kMsW - 1;
+    if constexpr (kPairFb) {
+      // LDS layout [step / 4][pattern][step % 4] (a lane's weights of two step pairs are one
+      // ds_read_b128: 4 LDS cycles, where two 8-byte reads took 8) from the table's [step / 2][pattern][step % 2]
+      const int q = idx & 3, pat = (idx >> 2) & 15, s4 = idx >> 6;
+      idx = ((2 * s4 + (q >> 1)) * kFbPatterns + pat) * 2 + (q & 1);
+    }
+    mw[r] = wsrc[idx];
   }
   const int mlen = T->mel_len[lane < kFilters ? lane : kFilters - 1];
   // the first pass's PCM after the table loads (loads complete in order, so the tables' waits
   // would otherwise include the PCM's: a batch-1 query's is read across PCIe)
-  fetch(cur, 0, b < ntiles, pf);
+  if constexpr (kPairFb) fetchd(cur, 0, pw);
+  else fetch(cur, 0, b < ntiles, pf);
   if (stager) {
     winr[tid] = cf{win0, win1};
     twr[tid] = cf{twk, twk2};
@@ -951,8 +994,10 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
       // them into registers for the whole kernel (occupancy).
       int oz = 0;
       asm volatile("" : "+v"(oz));
-      // the pass's window values (a table no one writes) requested before the syncs of the PCM
-      // staging, so their latency overlaps it
+      wave_sync();  // the previous pass's readers of the scratch are done
+      TFP_STAMP(0);
+      // the pass's window values (a table no one writes) requested with the PCM staging, so the
+      // staging's sync waits for both at once
       cf wreg[16];
 #pragma unroll
       for (int i = 0; i < 8; i++) {
@@ -960,15 +1005,15 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
         wreg[2 * i] = cf{w4.x, w4.y};
         wreg[2 * i + 1] = cf{w4.z, w4.w};
       }
-      wave_sync();  // the previous pass's readers of the scratch are done
-      TFP_STAMP(0);
+      if constexpr (!kPairFb) {
 #pragma unroll
-      for (int r = 0; r < kChunkRounds; r++) {
-        const int chunk = lane + 64 * r;
-        if (chunk < kPassChunks) *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+        for (int r = 0; r < kChunkRounds; r++) {
+          const int chunk = lane + 64 * r;
+          if (chunk < kPassChunks) *reinterpret_cast<int4*>(M.pcm + (chunk >> 5) * kHopStride + (chunk & 31) * 8) = pf[r];
+        }
+        if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
+        else fetch(nxt, 0, bn < ntiles, pf);
       }
-      if (sub < kPasses - 1) fetch(cur, sub + 1, true, pf);
-      else fetch(nxt, 0, bn < ntiles, pf);
       wave_sync();
       TFP_STAMP(1);
       const int16_t* hop0 = M.pcm + grp * kHopStride;
@@ -976,23 +1021,56 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
       // m = 16 n1 + L: for n1 < 8 the sample pair 32 n1 + 2L of hop f (window half 2), for
       // n1 >= 8 the pair 32 (n1 - 8) + 2L of hop f-1. Frame grp's hops are staged hops grp, grp+1.
       cf z[16], Y[16];
+      if constexpr (kPairFb) {
+        const int64_t pb = (cur.f0 + 4 * sub - 1) * kHop;  // the pass's first sample
+        const int32_t fs = (int32_t)(pb + grp * kHop) + 2 * L;
+        if (cur.odd) {  // odd start: two aligned words per pair
+          const __amdgpu_buffer_rsrc_t rs = cur.rs;
+#pragma unroll
+          for (int n1 = 0; n1 < 16; n1++) {
+            const int32_t j = n1 < 8 ? 256 + 32 * n1 : 32 * (n1 - 8);
+            const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rs, 2 * (fs + j), 0, 0);  // (samples s - 1, s)
+            const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rs, 2 * (fs + j) + 4, 0, 0);
+            pw[n1] = (lo >> 16) | (hi << 16);
+          }
+        }
+        if (pb < 0 || pb + kPassSamples > cur.ns) {  // an edge pass: samples outside [0, ns) are 0 (aubio's padding)
+#pragma unroll
+          for (int n1 = 0; n1 < 16; n1++) {
+            const int32_t s0 = fs + (n1 < 8 ? 256 + 32 * n1 : 32 * (n1 - 8));
+            const uint32_t lo = (s0 >= 0 && s0 < cur.ns) ? 0xffffu : 0u;
+            const uint32_t hi = (s0 + 1 >= 0 && s0 + 1 < cur.ns) ? 0xffff0000u : 0u;
+            pw[n1] &= lo | hi;
+          }
+        }
+      }
 #pragma unroll
       for (int n1 = 0; n1 < 16; n1++) {
-        const int j = (32 * n1 + 2 * L + 256) & 511;
-        const int hsel = n1 < 8 ? 1 : 0;
-        const int32_t v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
+        int32_t v;
+        if constexpr (kPairFb) {
+          v = (int32_t)pw[n1];
+        } else {
+          const int j = (32 * n1 + 2 * L + 256) & 511;
+          const int hsel = n1 < 8 ? 1 : 0;
+          v = *reinterpret_cast<const int32_t*>(hop0 + hsel * kHopStride + (j & 255));
+        }
         z[n1] = cf{(float)(int16_t)(v & 0xffff), (float)(int16_t)(v >> 16)} * wreg[n1];
+      }
+      if constexpr (kPairFb) {  // the next pass's samples, into the registers just read
+        if (sub < kPasses - 1) fetchd(cur, sub + 1, pw);
+        else fetchd(nxt, 0, pw);
       }
       dft16q(w16r, z, Y);
 #pragma unroll
       for (int k1 = 1; k1 < 16; k1++) Y[k1] = cmul(Y[k1], ltw[k1 - 1]);
-      // the split's twiddles (a table no one writes) requested now: in flight during the transpose
+      wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
+      TFP_STAMP(2);
+      // the split's twiddles (a table no one writes) requested with the square's writes, so the
+      // square's sync waits for both at once
       const float4* tw4 = reinterpret_cast<const float4*>(twr + 2 * L + oz);  // + 16 k2: one base, immediate offsets
       float4 t4s[8];
 #pragma unroll
       for (int k2 = 0; k2 < 8; k2++) t4s[k2] = tw4[16 * k2];
-      wave_sync();  // every lane has read its PCM: the scratch becomes the transpose square
-      TFP_STAMP(2);
 #pragma unroll
       for (int k1 = 0; k1 < 16; k1++) W[k1 * kSq8 + L] = Y[k1];
       wave_sync();
@@ -1109,17 +1187,19 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
           // The segments' sums are stored after the last step: a store to the log rows between
           // them kept the compiler from hoisting the later reads above it (it cannot tell the two
           // LDS arrays apart), so the phase waited out the LDS latency once per segment.
-          const cf* const wfb = reinterpret_cast<const cf*>(S.fbw) + L + oz;
+          const f4v* const wfb = reinterpret_cast<const f4v*>(S.fbw) + L + oz;
           // Each segment's reads are issued one segment ahead of its sums (all of them at once
           // needed 108 VGPRs and spilled); the compiler barriers keep them in those groups.
+          // (the weights of step pairs 2g, 2g + 1 are one read, with pair 2g's segment's)
           cf seg[kFbSegs];
-          cf wv[kFbSteps / 2];
+          f4v wv4[kFbSteps / 4];
           f4v nv[kFbSteps / 2];
+          static_assert(kFbSteps % 4 == 0, "weights in groups of 4 steps");
           auto load_seg = [&](auto kk) {
             constexpr int k = decltype(kk)::value;
 #pragma unroll
             for (int st = kFbSegStart[k]; st < kFbSegStart[k + 1]; st += 2) {
-              wv[st >> 1] = wfb[(st >> 1) * kFbPatterns];
+              if ((st & 3) == 0) wv4[st >> 2] = wfb[(st >> 2) * kFbPatterns];
               nv[st >> 1] = *reinterpret_cast<const f4v*>(jb[k] + 2 * st);
             }
           };
@@ -1128,8 +1208,10 @@ __global__ __launch_bounds__(64 * fp8_block_waves<kPasses>(), TFP_FP_WAVES) void
 #pragma unroll
             for (int st = kFbSegStart[k]; st < kFbSegStart[k + 1]; st += 2) {
               const int i = st >> 1;
-              const cf p0 = cf{nv[i].x, nv[i].y} * cf{wv[i].x, wv[i].x};
-              const cf p1 = cf{nv[i].z, nv[i].w} * cf{wv[i].y, wv[i].y};
+              const f4v w = wv4[st >> 2];
+              const float w0 = (st & 3) ? w.z : w.x, w1 = (st & 3) ? w.w : w.y;
+              const cf p0 = cf{nv[i].x, nv[i].y} * cf{w0, w0};
+              const cf p1 = cf{nv[i].z, nv[i].w} * cf{w1, w1};
               if (st == 0) acc = p0;
               else if (st == kFbSegStart[k]) acc = __builtin_elementwise_fma(acc, cf{jk[k], jk[k]}, p0);
               else acc = acc + p0;

@@ -1,6 +1,7 @@
 """Diagnostic (not a test): one 1,024-clip x 2 s fingerprint launch (16-frame tiles) of the library
 TFP_LIB_PATH points at, against the oracle: prints the count of differing rows and the first few
-(got vs expected micro-units)."""
+(got vs expected micro-units). Then 400 clips of random lengths (odd and even, 1 to 9,000 samples)
+back to back in one buffer, so clips start on odd samples too."""
 import os
 import sys
 
@@ -30,3 +31,19 @@ print("%s: %d of %d rows differ" % (os.path.basename(os.path.dirname(T.LIB_PATH)
 for i in bad[:6]:
     print("  row %d (clip %d frame %d): got %s exp %s" % (i, i // plan.nframes * nclips, i % (plan.nframes // nclips),
                                                          got[i].tolist(), exp[i].tolist()))
+
+# ragged: random lengths back to back (odd starts, odd lengths, clips shorter than a tile)
+rng = np.random.default_rng(7)
+lens = rng.integers(1, 9000, 400)
+lens[:8] = [1, 2, 255, 256, 257, 511, 512, 513]
+off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+host = rng.integers(-32768, 32768, int(off[-1])).astype(np.int16)
+d_pcm = torch.from_numpy(host).to(dev)
+plan = eng.plan(off)
+micro = torch.zeros((max(plan.nframes, 1), 2), dtype=torch.int32, device=dev)
+eng.fingerprint_device(plan, d_pcm.data_ptr(), micro.data_ptr(), 0, s.cuda_stream)
+s.synchronize()
+got = micro.cpu().numpy()[:plan.nframes]
+exp, _ = oracle_py.fingerprint_batch(host, off, nthreads=16, want_db=False)
+bad = np.nonzero((got != exp).any(axis=1))[0]
+print("%s ragged: %d of %d rows differ" % (os.path.basename(os.path.dirname(T.LIB_PATH)), len(bad), len(got)))
