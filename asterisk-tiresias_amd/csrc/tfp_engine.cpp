@@ -277,14 +277,15 @@ int ensure_logfix(tfp_engine* e) {
   const uint32_t* k;
   const double* v;
   int32_t n;
-  log_fix_table(&k, &v, &n);
+  log_fix_hash(&k, &v, &n);  // (the hashed form: one or two key loads per lookup on the device)
   if (n <= 0) return TFP_OK;
-  HIPCHK(e, e->logfix_key.reserve(sizeof(uint32_t) * n));
-  HIPCHK(e, e->logfix_val.reserve(sizeof(double) * n));
-  HIPCHK(e, hipMemcpyAsync(e->logfix_key.p, k, sizeof(uint32_t) * n, hipMemcpyHostToDevice, e->stream));
-  HIPCHK(e, hipMemcpyAsync(e->logfix_val.p, v, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+  const size_t slots = (size_t)1 << kLogFixHashBits;
+  HIPCHK(e, e->logfix_key.reserve(sizeof(uint32_t) * slots));
+  HIPCHK(e, e->logfix_val.reserve(sizeof(double) * slots));
+  HIPCHK(e, hipMemcpyAsync(e->logfix_key.p, k, sizeof(uint32_t) * slots, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(e, hipMemcpyAsync(e->logfix_val.p, v, sizeof(double) * slots, hipMemcpyHostToDevice, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  e->logfix = LogFix{e->logfix_key.as<uint32_t>(), e->logfix_val.as<double>(), n};
+  e->logfix = LogFix{e->logfix_key.as<uint32_t>(), e->logfix_val.as<double>(), n, 1};
   return TFP_OK;
 }
 

@@ -185,15 +185,29 @@ TFP_HD double log_acc(double x) {
 // reduced argument is its mantissa in [1, 2) or [0.5, 1)). LogFix lists them, keyed
 // i << 23 | mantissa23 (i = 1 for [0.5, 1)), with glibc's value: built on the host from glibc
 // itself (tfp_tables.cpp build_log_fix), ascending keys. n = 0: no table (log_acc everywhere).
+// hashed: key/val are instead the 2^kLogFixHashBits slots of tfp_tables.cpp log_fix_hash (the
+// device copy: at load 0.44 a lookup, hit or miss, reads one or two adjacent keys).
+constexpr int kLogFixHashBits = 17;
+constexpr uint32_t kLogFixEmpty = 0xffffffffu;
+TFP_HD uint32_t log_fix_slot(uint32_t k) { return (k * 0x9E3779B1u) >> (32 - kLogFixHashBits); }
 struct LogFix {
   const uint32_t* key;
   const double* val;
   int32_t n;
+  int32_t hashed = 0;
 };
 
 TFP_HD double log_fixed(double x, int32_t i, const LogFix& fx) {
   if (fx.n > 0 && (d2u(x) & 0x1fffffffull) == 0) {  // (a float's double: the table's domain)
     const uint32_t k = ((uint32_t)i << 23) | (uint32_t)((d2u(x) >> 29) & 0x7fffffu);
+    if (fx.hashed) {
+      for (uint32_t h = log_fix_slot(k);; h = (h + 1) & ((1u << kLogFixHashBits) - 1)) {
+        const uint32_t s = fx.key[h];
+        if (s == k) return fx.val[h];
+        if (s == kLogFixEmpty) break;
+      }
+      return log_acc(x);
+    }
     int32_t lo = 0, hi = fx.n;
     while (lo < hi) {
       const int32_t mid = (lo + hi) >> 1;

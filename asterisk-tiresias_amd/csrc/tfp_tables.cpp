@@ -398,4 +398,28 @@ void log_fix_table(const uint32_t** keys, const double** vals, int32_t* n) {
   *n = (int32_t)K.size();
 }
 
+void log_fix_hash(const uint32_t** keys, const double** vals, int32_t* n) {
+  static std::vector<uint32_t> K;
+  static std::vector<double> V;
+  static int32_t N = 0;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const uint32_t* k;
+    const double* v;
+    log_fix_table(&k, &v, &N);
+    const uint32_t mask = (1u << kLogFixHashBits) - 1;
+    K.assign(mask + 1, kLogFixEmpty);
+    V.assign(mask + 1, 0.0);
+    for (int32_t j = 0; j < N; j++) {
+      uint32_t h = log_fix_slot(k[j]);
+      while (K[h] != kLogFixEmpty) h = (h + 1) & mask;
+      K[h] = k[j];
+      V[h] = v[j];
+    }
+  });
+  *keys = K.data();
+  *vals = V.data();
+  *n = N;
+}
+
 }  // namespace tfp

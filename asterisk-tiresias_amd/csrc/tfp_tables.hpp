@@ -75,5 +75,9 @@ bool build_tables(int sample_rate, DspTables* t);
 // The reduced arguments where log_acc differs from this host's glibc log, with glibc's value
 // (tfp_math.hpp LogFix), ascending keys; computed once per process (~0.3 s).
 void log_fix_table(const uint32_t** keys, const double** vals, int32_t* n);
+// The same entries as an open-addressing hash of 2^kLogFixHashBits slots (tfp_math.hpp
+// log_fix_slot: multiplicative hash, linear probing, empty slots keyed kLogFixEmpty): the device
+// lookup is one or two loads from a 512 KiB key array instead of a 16-step binary search.
+void log_fix_hash(const uint32_t** keys, const double** vals, int32_t* n);
 
 }  // namespace tfp

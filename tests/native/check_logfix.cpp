@@ -18,6 +18,20 @@ int main(int argc, char** argv) {
   int32_t n;
   log_fix_table(&k, &v, &n);
   const LogFix fx{k, v, n};
+  // the hashed form the engine uploads (tfp_tables.cpp log_fix_hash): the same value as the sorted
+  // table's binary search for every key of the 2^24 reduced-argument domain, present or not
+  const uint32_t* hk;
+  const double* hv;
+  int32_t hn;
+  log_fix_hash(&hk, &hv, &hn);
+  const LogFix hx{hk, hv, hn, 1};
+  uint64_t bad_hash = hn != n;
+#pragma omp parallel for reduction(+ : bad_hash) schedule(static)
+  for (int64_t key = 0; key < (1 << 24); key++) {
+    const int32_t i = (int32_t)(key >> 23);
+    const double x = u2d(((uint64_t)(0x3ff - i) << 52) | ((uint64_t)(key & 0x7fffff) << 29));
+    bad_hash += d2u(log_fixed(x, i, hx)) != d2u(log_fixed(x, i, fx));
+  }
   uint64_t tot = 0, bad = 0, bad_nofix = 0;
 #pragma omp parallel for reduction(+ : tot, bad, bad_nofix) schedule(static)
   for (int64_t u = 1; u < 0x7f800000LL; u += (int64_t)stride) {
@@ -25,11 +39,14 @@ int main(int argc, char** argv) {
     const double want = 10.0 * log10(fabs((double)c));
     tot++;
     bad += d2u(db_of_coef(c, fx)) != d2u(want);
+    bad += d2u(db_of_coef(c, hx)) != d2u(want);
     bad_nofix += d2u(db_of_coef(c)) != d2u(want);
   }
   printf("LogFix entries: %d\n", n);
+  printf("hashed LogFix vs sorted over the 2^24 key domain: %lu mismatches\n", (unsigned long)bad_hash);
   printf("10*log10|c| with LogFix vs glibc : %lu / %lu mismatches (without the table: %lu)\n", (unsigned long)bad,
          (unsigned long)tot, (unsigned long)bad_nofix);
+  bad += bad_hash;
   printf("%s\n", bad ? "FAIL" : "OK");
   return bad ? 1 : 0;
 }

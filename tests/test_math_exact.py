@@ -40,6 +40,7 @@ def test_logfix_sampled(tmp_path):
     out = subprocess.run([exe, "997"], capture_output=True, text=True, timeout=300)
     print(out.stdout)
     assert out.returncode == 0 and out.stdout.strip().endswith("OK"), out.stdout
+    assert "hashed LogFix vs sorted over the 2^24 key domain: 0 mismatches" in out.stdout
 
 
 def test_logfix_exhaustive_log_committed():
