@@ -1510,6 +1510,8 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.points_only = tfp::knob("TFP_WIDE_POINTS") != nullptr;
   e->wide.ch128 = tfp::knob("TFP_WIDE_CH128") != nullptr;
   e->wide.unpacked = tfp::knob("TFP_WIDE_UNPACKED") != nullptr;
+  e->wide.libsort = tfp::knob("TFP_WIDE_LIBSORT") != nullptr;
+  e->wide.debug_bins = tfp::knob("TFP_DEBUG_BINS") != nullptr;
   if (const char* v = tfp::knob("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = tfp::knob("TFP_INDEX_DELTA")) {
     e->use_delta = atoi(v) != 0;

@@ -258,6 +258,16 @@ struct WideScratch {
   int32_t qch = kChunk;                              // prepare: queries per chunk of this batch (128, or 256 with 8-bit counts)
   int32_t* ukeys = nullptr;                          // [nchunks][kKeyRange] each chunk's used keys, ascending
   int32_t* nuk = nullptr;                            // [nchunks] their number
+  bool ukeys_ready = false;                          // prepare wrote ukeys / nuk (the bin sort)
+  bool libsort = false;                              // TFP_WIDE_LIBSORT: the library sort on the speculative pass too
+  bool debug_bins = false;                           // TFP_DEBUG_BINS: the bin sort's counts on stderr
+  // the bin sort (tfp_scan.hip wide_bin_hist ...): per (chunk, segment) frame count and L2 range,
+  // per chunk and bin the frame count and first sorted frame, each window segment's first / last
+  // L2 and U2
+  uint32_t* segstat = nullptr;
+  int32_t *ghist = nullptr, *bstart = nullptr, *segc = nullptr;
+  int32_t *gs = nullptr, *gb = nullptr, *hb = nullptr;  // sort groups per chunk: first frame, first bin, bin of frame 64 g
+  int64_t cap_groups = 0;
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima
   hipError_t reserve(int64_t nf, int32_t nq, hipStream_t s);
   void release();

@@ -25,6 +25,8 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdio>
+#include <vector>
 
 #include "tfp_kernels.hpp"
 #include "tfp_math.hpp"
@@ -541,12 +543,19 @@ __global__ void wide_keys_u_kernel(const FrameBox* __restrict__ boxes, int64_t n
 // and gather passes read it instead of searching qoff per frame.
 // It also zeroes the counts (info) and the segment table, which the key pass and the gather fill
 // (two fill launches fewer on the timeline).
+// With segstat (the bin sort's): each (chunk, segment)'s frame count, least and greatest L2 start
+// at 0, ~0, 0, and ghist (each chunk's fine-bin counts, nghist words) at 0.
 __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t* __restrict__ fq,
                                         int32_t* __restrict__ info, int32_t* __restrict__ seg, int64_t nseg,
-                                        unsigned long long* __restrict__ best) {
+                                        unsigned long long* __restrict__ best, uint32_t* __restrict__ segstat,
+                                        int32_t* __restrict__ ghist, int64_t nghist) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
   if (tid < 3) info[tid] = 0;
   for (int64_t i = tid; i < nseg; i += nt) seg[i] = 0;
+  if (segstat) {  // (nseg / 2 segments of 3 words)
+    for (int64_t i = tid; i < 3 * (nseg / 2); i += nt) segstat[i] = i % 3 == 1 ? 0xffffffffu : 0u;
+    for (int64_t i = tid; i < nghist; i += nt) ghist[i] = 0;
+  }
   if (best)  // the sweep's result keys (the caller's output buffer), maxed into from zero
     for (int64_t i = tid; i < nq; i += nt) best[i] = 0ull;
   const int lane = threadIdx.x & 63;
@@ -572,11 +581,26 @@ constexpr int kPackSegShift = 43, kPackChunkShift = kPackSegShift + 11;
 __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int32_t* __restrict__ fq,
                                    int64_t nf, int32_t qch, bool packed, const int32_t* __restrict__ fv, int64_t dbase,
                                    unsigned long long* __restrict__ ck, int32_t* __restrict__ fo,
-                                   int32_t* __restrict__ info) {
+                                   int32_t* __restrict__ info, uint32_t* __restrict__ segstat) {
+  // segstat (the bin sort's): per (chunk, segment) of this workgroup's frames, in a small LDS table
+  // (a workgroup takes a contiguous range: one or two chunks, a few segments), flushed with one set
+  // of global atomics per entry (same-address atomics from every wave of the grid serialise: ~80 us)
+  constexpr int kSlots = 128;
+  __shared__ int32_t hk[kSlots];
+  __shared__ uint32_t hc[kSlots], hmn[kSlots], hmx[kSlots];
+  const int lane = threadIdx.x & 63;
+  if (segstat) {
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) hk[j] = -1, hc[j] = 0u, hmn[j] = 0xffffffffu, hmx[j] = 0u;
+    __syncthreads();
+  }
+  const int64_t per = (nf + gridDim.x - 1) / gridDim.x, r1 = min(nf, per * (blockIdx.x + 1));
   int32_t kept = 0, wide = 0, nbad = 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t f = fv ? fv[i] : (int32_t)i;
-    const FrameBox bx = boxes[f];
+  // (whole waves in every step: the segment stats' shuffles read every lane)
+  for (int64_t i0 = per * blockIdx.x; i0 < r1; i0 += blockDim.x) {
+    const int64_t i = i0 + threadIdx.x;
+    const bool in = i < r1;
+    const int32_t f = !in ? 0 : fv ? fv[i] : (int32_t)i;
+    FrameBox bx = in ? boxes[f] : FrameBox{};
     unsigned long long key = ~0ull;
     const int64_t kk = (int64_t)bx.k + kKeyOffset;
     // the bad-frame check of wide_keys_u (a key or a window outside what the cache and the int32
@@ -601,8 +625,63 @@ __global__ void wide_keys_c_kernel(const FrameBox* __restrict__ boxes, const int
                    : (ch << kWideChunkShift) | (sk << kWideSegShift) | (l2 << kWideDeltaBits) | d;
       kept++;
     }
-    ck[i] = key;
-    if (fo) fo[i] = f;
+    if (in) {
+      ck[i] = key;
+      if (fo) fo[i] = f;
+    }
+    if (segstat) {
+      // (the bin sort's) this frame's (chunk, segment): its count and L2 range, one set of atomics per
+      // distinct (chunk, segment) of the wave (a wave's consecutive frames share a few)
+      int32_t id = key != ~0ull ? (int32_t)(key >> kPackSegShift) : -1;  // chunk << 11 | segment
+      const uint32_t l2 = (uint32_t)(key >> 11);
+      while (true) {
+        const unsigned long long m = __ballot(id >= 0);
+        if (!m) break;
+        const int l = __ffsll((long long)m) - 1;
+        const int32_t v = __builtin_amdgcn_readlane(id, l);
+        const bool me = id == v;
+        const uint32_t cnt = (uint32_t)__popcll(__ballot(me));
+        uint32_t mn = me ? l2 : 0xffffffffu, mx = me ? l2 : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+          mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+        }
+        if (lane == l) {
+          int32_t h = (int32_t)(((uint32_t)v * 2654435761u) >> 25), probes = 0;
+          for (; probes < kSlots; probes++, h = (h + 1) & (kSlots - 1)) {
+            const int32_t o = atomicCAS(&hk[h], -1, v);
+            if (o == -1 || o == v) break;
+          }
+          uint32_t *c, *a, *z;
+          if (probes < kSlots) {
+            c = &hc[h], a = &hmn[h], z = &hmx[h];
+          } else {  // (table full: straight to the global entry)
+            uint32_t* st = segstat + 3 * (int64_t)v;
+            c = &st[0], a = &st[1], z = &st[2];
+          }
+          atomicAdd(c, cnt);
+          if ((v & kKeyRange) == 0) {
+            atomicMin(a, mn);
+            atomicMax(z, mx);
+          }
+        }
+        if (me) id = -1;
+      }
+    }
+  }
+  if (segstat) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < kSlots; j += blockDim.x) {
+      const int32_t v = hk[j];
+      if (v < 0) continue;
+      uint32_t* st = segstat + 3 * (int64_t)v;
+      atomicAdd(&st[0], hc[j]);
+      if ((v & kKeyRange) == 0) {
+        atomicMin(&st[1], hmn[j]);
+        atomicMax(&st[2], hmx[j]);
+      }
+    }
   }
   // one atomic per block, on a grid of at most kKeysBlocks blocks: same-address atomics serialise in
   // L2 (one per frame cost ~0.13 ms at C3, and one per wave still ~0.1 ms: 10k waves)
@@ -673,9 +752,12 @@ __global__ void wide_gather_kernel(const FrameBox* __restrict__ boxes, const int
 // [T[b], T[b + 1]] (b = v's bucket): one table load and a search over the bucket's few frames,
 // instead of a search over the whole segment.
 #ifndef TFP_DIR_SCALE
-#define TFP_DIR_SCALE 2
+#define TFP_DIR_SCALE 0
 #endif
-constexpr int kDirScale = TFP_DIR_SCALE;  // NB = 2^(ceil(log2 S) + kDirScale)
+// NB = 2^(ceil(log2 S) + kDirScale): 0 since round 5 (C3 coefs=2 at tol 0.001 / 0.45: 0.804 / 0.926
+// ms against 0.810 / 0.936 with 1 and 0.827 / 0.955 with 2, profiles/r05/c3_dirscale_r05h.txt;
+// the fill's scattered writes shrink 4x, the sweep's bucket searches grow by about one step)
+constexpr int kDirScale = TFP_DIR_SCALE;
 __device__ __forceinline__ int dir_log2(int32_t S) { return (S <= 1 ? 0 : 32 - __clz(S - 1)) + kDirScale; }
 __device__ __forceinline__ int dir_shift(int64_t range, int lg) {
   const int bits = range > 0 ? 64 - __clzll((unsigned long long)range) : 0;
@@ -775,6 +857,488 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
           base[h] = base[2 + h] = t0 + h * nbk;
           lo[h] = bp + 1, hi[h] = bi, val[h] = (int32_t)i;
           if (i == se - 1) lo[2 + h] = bi + 1, hi[2 + h] = nbk - 1, val[2 + h] = se;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int32_t len = hi[r] - lo[r] + 1;
+      if (len > 0 && len <= kShort)
+        for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
+      unsigned long long m = __ballot(len > kShort);
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64),
+                      o = __shfl(base[r], l, 64);
+        for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
+      }
+    }
+  }
+}
+
+// ---- the sweep's frame order, sorted by bins (round 5) ---------------------------------------
+// The packed keys of a chunk (seg << 43 | L2 << 11 | d << 8 | query) are ordered without a
+// device-wide sort. A chunk's frames are contiguous in the input, and the key pass counts each
+// (chunk, segment)'s frames and L2 range (segstat). Each segment then gets nb = 2^ceil(log2(S / 8))
+// bins (one without a max2 window) cut evenly over its L2 range: a bin index is monotone in the
+// key, and bins hold ~8 frames where the values spread evenly. wide_bin_hist counts the bins of
+// each chunk (workgroups over slices of the chunk: per-workgroup counts in LDS, one global atomic
+// per bin, which also hands the workgroup its offset in the bin) and records each frame's bin and
+// place in it; wide_bin_scan (a workgroup per chunk) scans the counts into each bin's first frame
+// and writes the segment table, the directory offsets, the used keys and the non-empty bins;
+// wide_bin_scatter moves the keys to their places; one wave sorts each bin in registers or LDS
+// and writes the sorted windows, queries and segment of each frame (wide_bin_sort); the
+// directories are filled from those with a per-segment constants table (wide_dir_fill_bins).
+// Chunk ch's kept frames occupy [cbeg[ch], cbeg[ch] + kept) of the sorted arrays; the rest of its
+// input range holds no frame of a segment (query 0, segment -1), so the prefix counts run over the
+// whole range. A bin whose frames all share (segment, L2, d), or whose segment has no max2 window,
+// is not sorted (any order counts the same). Any other bin above kBinCap frames sets info[2],
+// which sends the speculative batch to the library sort (as a window width outside the key's delta
+// field does).
+constexpr int kNFine = 16384;        // bins per chunk at most (the per-segment counts halve until they fit)
+constexpr int kBinCap = 1024;        // frames one wave sorts in LDS
+constexpr int kBinSortWaves = 4;     // waves per wide_bin_sort workgroup
+constexpr int kGroup = 64;           // a sort group: the bins whose first frame lies in [64 g, 64 g + 64)
+constexpr int kHistPer = 2;          // frames per thread of wide_bin_hist (1024 threads)
+constexpr int kPlaceBits = 18;       // place of a frame in its bin (chunks of at most 2^18 frames)
+
+// exclusive prefix of v over the workgroup (NT threads), and the total
+template <int NT>
+__device__ __forceinline__ int32_t block_excl(int32_t v, int32_t* ws, int32_t& total) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) ws[w] = x;
+  __syncthreads();
+  int32_t off = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; i++) {
+    const int32_t y = ws[i];
+    off += i < w ? y : 0;
+    tot += y;
+  }
+  __syncthreads();  // (ws is reused by the next call)
+  total = tot;
+  return off + x - v;
+}
+
+// The chunk's bin layout from segstat, in LDS (one workgroup of NT threads, 2 segments a thread):
+// base[s], nb[s] (0: unused), shift[s], l2min[s]; returns the chunk's bins. Synchronises.
+template <int NT>
+__device__ int32_t bin_layout(const uint32_t* __restrict__ st, int32_t* base, int32_t* nbs, int32_t* shf, uint32_t* lmn,
+                              int32_t* ws) {
+  static_assert(NT * 2 == kWideSegs, "two segments a thread");
+  const int t = threadIdx.x;
+  uint32_t cnt[2], lo[2], hi[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int sk = 2 * t + j;
+    cnt[j] = st[3 * sk];
+    lo[j] = st[3 * sk + 1];
+    hi[j] = st[3 * sk + 2];
+  }
+  int32_t total = 0, off = 0;
+  for (int extra = 3;; extra++) {  // ~2^extra frames a bin, coarser until the chunk's bins fit
+    int32_t n[2];
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      const int sk = 2 * t + j;
+      const uint32_t per = (cnt[j] + (1u << extra) - 1) >> extra;
+      n[j] = cnt[j] == 0 ? 0 : (sk >= kKeyRange || per <= 1) ? 1 : 1 << (32 - __clz(per - 1));
+    }
+    off = block_excl<NT>(n[0] + n[1], ws, total);
+    if (total <= kNFine) {
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const int sk = 2 * t + j;
+        const uint32_t range = hi[j] >= lo[j] ? hi[j] - lo[j] : 0u;
+        const int32_t rb = range ? 32 - __clz(range) : 0, lg = n[j] ? 31 - __clz(n[j]) : 0;
+        base[sk] = off;
+        nbs[sk] = n[j];
+        shf[sk] = rb > lg ? rb - lg : 0;
+        lmn[sk] = sk < kKeyRange ? lo[j] : 0u;
+        off += n[j];
+      }
+      break;
+    }
+  }
+  __syncthreads();
+  return total;
+}
+__device__ __forceinline__ int32_t bin_of(unsigned long long key, const int32_t* base, const int32_t* shf, const uint32_t* lmn) {
+  const int sk = (int)(key >> kPackSegShift) & (kWideSegs - 1);
+  return base[sk] + (sk < kKeyRange ? (int32_t)(((uint32_t)(key >> 11) - lmn[sk]) >> shf[sk]) : 0);
+}
+
+// Workgroup (ch, j): frames [cb + 2048 j, cb + 2048 (j + 1)) of chunk ch. Per bin in LDS: the
+// workgroup's count (the count before a frame's add is its place among them), then one global
+// atomic per non-empty bin (the workgroup's offset in the bin); each frame's bin << 18 | place in
+// pos (~0: not kept; chunks under 2^18 frames, so no kept frame's word is ~0).
+__global__ __launch_bounds__(1024) void wide_bin_hist_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t qch,
+                                                             const unsigned long long* __restrict__ ka,
+                                                             const uint32_t* __restrict__ segstat, int32_t* __restrict__ ghist,
+                                                             uint32_t* __restrict__ pos) {
+  constexpr int NT = 1024;
+  __shared__ int32_t base[kWideSegs], nbs[kWideSegs], shf[kWideSegs], ws[NT / 64];
+  __shared__ uint32_t lmn[kWideSegs];
+  __shared__ int32_t h[kNFine];
+  const int t = threadIdx.x, ch = blockIdx.x;
+  const int32_t q0 = ch * qch, q1 = min(nq, q0 + qch);
+  const int64_t cb = qoff[q0] - qoff[0], ce = qoff[q1] - qoff[0];
+  const int64_t b0 = cb + (int64_t)blockIdx.y * (NT * kHistPer);
+  if (b0 >= ce) return;  // (uniform in the workgroup)
+  for (int b = t; b < kNFine; b += NT) h[b] = 0;
+  (void)bin_layout<NT>(segstat + (int64_t)ch * kWideSegs * 3, base, nbs, shf, lmn, ws);  // (synchronises)
+  unsigned long long k[kHistPer];
+  int32_t bin[kHistPer], rk[kHistPer];
+#pragma unroll
+  for (int j = 0; j < kHistPer; j++) {
+    const int64_t i = b0 + j * NT + t;
+    k[j] = i < ce ? ka[i] : ~0ull;
+  }
+#pragma unroll
+  for (int j = 0; j < kHistPer; j++) {
+    bin[j] = k[j] != ~0ull ? bin_of(k[j], base, shf, lmn) : -1;
+    rk[j] = bin[j] >= 0 ? atomicAdd(&h[bin[j]], 1) : 0;
+  }
+  __syncthreads();
+  for (int b = t; b < kNFine; b += NT) {
+    const int32_t n = h[b];
+    if (n) h[b] = atomicAdd(&ghist[(int64_t)ch * kNFine + b], n);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kHistPer; j++) {
+    const int64_t i = b0 + j * NT + t;
+    if (i < ce) pos[i] = bin[j] >= 0 ? ((uint32_t)bin[j] << kPlaceBits) | (uint32_t)(h[bin[j]] + rk[j]) : ~0u;
+  }
+}
+
+// One workgroup per chunk: the bin counts scanned into each bin's first frame (bstart, relative to
+// cbeg[ch]), the sort groups (gs, gb: wide_bin_sort), the segment table, the directory offsets
+// (chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
+// the table's size per frame), the used keys, the chunk's
+// tail of non-frames, and cbeg.
+__global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t qch,
+                                                             int32_t nch, const uint32_t* __restrict__ segstat,
+                                                             const int32_t* __restrict__ ghist, int32_t* __restrict__ bstart,
+                                                             int32_t* __restrict__ seg, int32_t* __restrict__ doff,
+                                                             int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
+                                                             int32_t* __restrict__ cbeg, uint8_t* __restrict__ qis,
+                                                             int32_t* __restrict__ fseg, int32_t* __restrict__ gs,
+                                                             int32_t* __restrict__ gb, int32_t* __restrict__ hb, int32_t gcap) {
+  constexpr int NT = 1024, FPER = kNFine / NT;
+  __shared__ int32_t base[kWideSegs], nbs[kWideSegs], shf[kWideSegs], ws[NT / 64];
+  __shared__ uint32_t lmn[kWideSegs];
+  __shared__ int32_t start[kNFine + 1];
+  __shared__ int32_t used[kKeyRange];
+  const int t = threadIdx.x, ch = blockIdx.x;
+  const int32_t q0 = ch * qch, q1 = min(nq, q0 + qch);
+  const int64_t cb = qoff[q0] - qoff[0], ce = qoff[q1] - qoff[0];
+  used[t] = 0;
+  (void)bin_layout<NT>(segstat + (int64_t)ch * kWideSegs * 3, base, nbs, shf, lmn, ws);  // (synchronises)
+  int32_t g[FPER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < FPER; j++) {
+    g[j] = ghist[(int64_t)ch * kNFine + FPER * t + j];
+    sum += g[j];
+  }
+  int32_t T;
+  int32_t st = block_excl<NT>(sum, ws, T);
+  int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
+#pragma unroll
+  for (int j = 0; j < FPER; j++) {
+    const int f = FPER * t + j;
+    bs[f] = st;
+    start[f] = st;
+    st += g[j];
+  }
+  if (t == 0) {
+    bs[kNFine] = T;
+    start[kNFine] = T;
+    cbeg[ch] = (int32_t)cb;
+    if (ch == nch - 1) cbeg[nch] = (int32_t)ce;
+  }
+  __syncthreads();
+  // segments: segment sk's bins [base, base + nb)
+  int32_t dv[2] = {0, 0};
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const int sk = 2 * t + j;
+    if (nbs[sk]) {
+      const int32_t b = start[base[sk]], e = start[base[sk] + nbs[sk]];
+      if (e > b) {
+        int32_t* sg = seg + ((int64_t)ch * kWideSegs + sk) * 2;
+        sg[0] = (int32_t)cb + b;
+        sg[1] = (int32_t)cb + e;
+        used[sk & (kKeyRange - 1)] = 1;
+        if (sk < kKeyRange) dv[j] = 2 << dir_log2(e - b);  // (the directory's entries)
+      }
+    }
+  }
+  int32_t DT;
+  int32_t dof = block_excl<NT>(dv[0] + dv[1], ws, DT);  // (synchronises: used is complete)
+  (void)DT;
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    if (dv[j]) doff[(int64_t)ch * kKeyRange + 2 * t + j] = (4 << kDirScale) * (int32_t)cb + dof;
+    dof += dv[j];
+  }
+  // the used keys, ascending
+  int32_t NU;
+  const int32_t uo = block_excl<NT>(used[t], ws, NU);
+  if (used[t]) ukeys[(int64_t)ch * kKeyRange + uo] = t;
+  if (t == 0) nuk[ch] = NU;
+  // sort groups (wide_bin_sort): group g starts at the first bin whose first frame is >= 64 g (the
+  // bin holding frame 64 g: hb[g], or the next one); g = ceil(T / 64) closes the last
+  for (int32_t gi = t; (int64_t)gi * kGroup < (int64_t)T + kGroup; gi += NT) {
+    const int32_t p = gi * kGroup;
+    int32_t a = T, f = kNFine, lo = kNFine;
+    if (p < T) {  // the last bin starting at or before p (non-empty: start[kNFine] = T > p)
+      int32_t hi = kNFine;
+      lo = 0;
+      while (hi - lo > 1) {
+        const int32_t mid = (lo + hi) >> 1;
+        if (start[mid] <= p) lo = mid; else hi = mid;
+      }
+      f = start[lo] == p ? lo : lo + 1;
+      a = start[f];
+    }
+    gs[(int64_t)ch * gcap + gi] = a;
+    gb[(int64_t)ch * gcap + gi] = f;
+    hb[(int64_t)ch * gcap + gi] = lo;
+  }
+  // the range's tail (no kept frame): query 0, no segment
+  for (int64_t i = cb + T + t; i < ce; i += NT) {
+    qis[i] = 0;
+    fseg[i] = -1;
+  }
+}
+
+// Each kept frame's key to its bin's place: kb[cbeg[ch] + bstart[ch][bin] + place].
+__global__ void wide_bin_scatter_kernel(int64_t nf, int32_t qch, const int32_t* __restrict__ fq,
+                                        const unsigned long long* __restrict__ ka, const uint32_t* __restrict__ pos,
+                                        const int32_t* __restrict__ cbeg, const int32_t* __restrict__ bstart,
+                                        unsigned long long* __restrict__ kb) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint32_t p = pos[i];
+    if (p == ~0u) continue;
+    const int ch = fq[i] / qch;
+    kb[(int64_t)cbeg[ch] + bstart[(int64_t)ch * (kNFine + 1) + (p >> kPlaceBits)] + (p & ((1u << kPlaceBits) - 1))] = ka[i];
+  }
+}
+
+__device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+// ascending bitonic sort of one key per lane
+__device__ __forceinline__ unsigned long long bitonic_wave(unsigned long long v, int lane) {
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const unsigned long long o = shfl_xor_u64(v, j);
+      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
+      v = lower == up ? (o < v ? o : v) : (o > v ? o : v);
+    }
+  return v;
+}
+// ascending bitonic sort of S[0, N) (N a power of two, 128 .. kBinCap) by one wave in LDS (a
+// wave's LDS operations complete in order: no barrier between the stages)
+__device__ void bitonic_lds(unsigned long long* S, int N, int lane) {
+  for (int k = 2; k <= N; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1)
+      for (int t = lane; t < N / 2; t += 64) {
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1)), ip = i | j;
+        const unsigned long long a = S[i], b = S[ip];
+        if ((a > b) == ((i & k) == 0)) {
+          S[i] = b;
+          S[ip] = a;
+        }
+      }
+}
+
+// Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
+// (bins are monotone in the key, so sorting a run of whole bins sorts each of them): frames
+// [gs[g], gs[g + 1]) of the chunk, bins [gb[g], gb[g + 1]). One wave per group sorts it in registers
+// (up to 128 frames) or LDS, and writes each sorted frame's L2, U2 (= L2 + dbase + d), query and
+// segment (ch << 11 | segment key); a frame that starts or ends a window segment writes the
+// segment's first or last L2 / U2 (segc) for the directory fill. A group above kBinCap frames (a
+// crowded bin) goes bin by bin: a bin whose frames all share (segment, L2, d), or whose segment
+// has no max2 window, needs no order; any other bin above kBinCap frames sets info[2].
+__global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
+    const int32_t* __restrict__ bstart, const int32_t* __restrict__ gs, const int32_t* __restrict__ gb,
+    const int32_t* __restrict__ hb, int32_t gcap,
+    const int32_t* __restrict__ cbeg, const unsigned long long* __restrict__ kb, int64_t dbase,
+    const int32_t* __restrict__ seg, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s, uint8_t* __restrict__ qis,
+    int32_t* __restrict__ fseg, int32_t* __restrict__ segc, int32_t* __restrict__ info) {
+  __shared__ unsigned long long sk[kBinSortWaves][kBinCap];
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int ch = blockIdx.x;
+  const int32_t g = blockIdx.y * kBinSortWaves + wv;
+  const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
+  const int32_t* gsc = gs + (int64_t)ch * gcap;
+  if ((int64_t)g * kGroup >= bs[kNFine]) return;  // (no frame of the chunk starts here; wave-uniform)
+  const int32_t S0 = gsc[g], S1 = gsc[g + 1];
+  const int64_t cb = cbeg[ch];
+  unsigned long long* S = sk[wv];
+  auto sk_of = [](unsigned long long k) { return (int32_t)((k >> kPackSegShift) & (kWideSegs - 1)); };
+  // sorted frame p (chunk-relative) of key k; first / last: p may start / end its segment
+  auto put = [&](int32_t p, unsigned long long k, bool first, bool last) {
+    const int64_t pos = cb + p;
+    const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
+    const int32_t u2 = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
+    L2s[pos] = l2;
+    U2s[pos] = u2;
+    qis[pos] = (uint8_t)(k & 255);
+    fseg[pos] = (ch << 11) | sgk;
+    if ((first || last) && sgk < kKeyRange) {
+      const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
+      int32_t* c4 = segc + ((int64_t)ch * kKeyRange + sgk) * 4;
+      if (first && sg[0] == pos) c4[0] = l2, c4[1] = u2;
+      if (last && sg[1] == pos + 1) c4[2] = l2, c4[3] = u2;
+    }
+  };
+  // frames [b, b + n) sorted in LDS, written
+  auto sort_lds = [&](int32_t b, int32_t n) {
+    const int N = n <= 1 ? 1 : 1 << (32 - __clz(n - 1));
+    for (int p = lane; p < N; p += 64) S[p] = p < n ? kb[cb + b + p] : ~0ull;
+    bitonic_lds(S, N, lane);
+    for (int p = lane; p < n; p += 64) {
+      const unsigned long long k = S[p];
+      put(b + p, k, p == 0 || sk_of(S[p - 1]) != sk_of(k), p == n - 1 || sk_of(S[p + 1]) != sk_of(k));
+    }
+  };
+  // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
+  // batch is redone: the wave of the bin's group checks, and copies the bin's frames before 64 g)
+  {
+    const int32_t h = hb[(int64_t)ch * gcap + g], b = bs[h], nb = bs[h + 1] - b;
+    if (nb > kBinCap) {
+      const int32_t p = max(g * kGroup, b) + lane;
+      if (p < min(g * kGroup + kGroup, b + nb)) put(p, kb[cb + p], p == b, p == b + nb - 1);
+    }
+  }
+  const int32_t n = S1 - S0;
+  if (n <= 0) return;
+  if (n <= 64) {
+    const unsigned long long v = bitonic_wave(lane < n ? kb[cb + S0 + lane] : ~0ull, lane);
+    const int32_t s = sk_of(v), sp = __shfl_up(s, 1, 64), sn = __shfl_down(s, 1, 64);
+    if (lane < n) put(S0 + lane, v, lane == 0 || sp != s, lane == n - 1 || sn != s);
+    return;
+  }
+  if (n <= 128) {
+    unsigned long long v0 = kb[cb + S0 + lane], v1 = 64 + lane < n ? kb[cb + S0 + 64 + lane] : ~0ull;
+    // bitonic over 128 = 2 x 64: element i = lane + 64 r (r = 0: v0, 1: v1)
+#pragma unroll
+    for (int k = 2; k <= 128; k <<= 1)
+#pragma unroll
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        if (j == 64) {  // (k = 128: ascending) the pair (lane, 64 + lane) in this lane
+          const unsigned long long lo = v0 < v1 ? v0 : v1, hi = v0 < v1 ? v1 : v0;
+          v0 = lo, v1 = hi;
+        } else {
+          const unsigned long long o0 = shfl_xor_u64(v0, j), o1 = shfl_xor_u64(v1, j);
+          const bool lower = (lane & j) == 0;
+          const bool up0 = (lane & k) == 0, up1 = ((64 + lane) & k) == 0;
+          v0 = lower == up0 ? (o0 < v0 ? o0 : v0) : (o0 > v0 ? o0 : v0);
+          v1 = lower == up1 ? (o1 < v1 ? o1 : v1) : (o1 > v1 ? o1 : v1);
+        }
+      }
+    const int32_t s0 = sk_of(v0), s1 = sk_of(v1);
+    const int32_t p0 = __shfl_up(s0, 1, 64), n0 = __shfl_down(s0, 1, 64), p1 = __shfl_up(s1, 1, 64), n1 = __shfl_down(s1, 1, 64);
+    const int32_t l0 = __shfl(s0, 63, 64), f1 = __shfl(s1, 0, 64);  // (the neighbours across the halves)
+    put(S0 + lane, v0, lane == 0 || p0 != s0, (lane == 63 ? f1 : n0) != s0 || lane == n - 1);
+    if (64 + lane < n) put(S0 + 64 + lane, v1, (lane == 0 ? l0 : p1) != s1, 64 + lane == n - 1 || n1 != s1);
+    return;
+  }
+  if (n <= kBinCap) {
+    sort_lds(S0, n);
+    return;
+  }
+  // a crowded group: bin by bin (the bins' bounds 64 at a time)
+  const int32_t fa = gb[(int64_t)ch * gcap + g], fz = gb[(int64_t)ch * gcap + g + 1];
+  for (int32_t f0 = fa; f0 < fz; f0 += 64) {
+    const int32_t bl = f0 + lane < fz ? bs[f0 + lane] : 0, nl = f0 + lane < fz ? bs[f0 + lane + 1] - bl : 0;
+    for (unsigned long long mb = __ballot(nl > 0); mb; mb &= mb - 1) {
+      const int sl = __ffsll((long long)mb) - 1;
+      const int32_t b = __builtin_amdgcn_readlane(bl, sl), nb = __builtin_amdgcn_readlane(nl, sl);
+      if (nb <= kBinCap) {
+        sort_lds(b, nb);
+        continue;
+      }
+      // frames that all share (segment, L2, d) need no order (a crowd of equal values: the silence
+      // floor), nor do those of a segment without a max2 window (the waves of the bin's frames copy
+      // them); any other bin this large goes to the library sort with the batch
+      unsigned long long lo = ~0ull, hi = 0;
+      for (int32_t p0 = 0; p0 < nb; p0 += 256) {
+        unsigned long long k4[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int32_t p = p0 + 64 * u + lane;
+          k4[u] = p < nb ? kb[cb + b + p] >> 8 : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          if (p0 + 64 * u + lane < nb) {
+            lo = k4[u] < lo ? k4[u] : lo;
+            hi = k4[u] > hi ? k4[u] : hi;
+          }
+        }
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long a = shfl_xor_u64(lo, o), z = shfl_xor_u64(hi, o);
+        lo = a < lo ? a : lo;
+        hi = z > hi ? z : hi;
+      }
+      if (lo != hi && (lo >> (kPackSegShift - 8) & kKeyRange) == 0 && lane == 0) atomicAdd(&info[2], 1);
+      // (the frames before the bin's first multiple of 64: no window wave starts inside the bin there)
+      const int32_t p = b + lane;
+      if (p < min(b + nb, (b + kGroup - 1) / kGroup * kGroup)) put(p, kb[cb + p], p == b, p == b + nb - 1);
+    }
+  }
+}
+
+// wide_dir_fill over the bin-sorted frames: the segment of frame i from fseg, its constants from
+// the segment table, segc and doff (loads that depend on fseg only). Nothing after an overflow
+// (info[2] > 0: a bin was left unsorted, its frames without fseg; the batch is redone).
+__global__ void wide_dir_fill_bins_kernel(int64_t n, const int32_t* __restrict__ fseg, const int32_t* __restrict__ seg,
+                                          const int32_t* __restrict__ segc, const int32_t* __restrict__ L2s,
+                                          const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
+                                          int32_t* __restrict__ dtab, const int32_t* __restrict__ info) {
+  constexpr int32_t kShort = 8;
+  if (info[2] > 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; i0 < n; i0 += nw * 64) {
+    const int64_t i = i0 + lane;
+    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
+    if (i < n) {
+      const int32_t fs = fseg[i];
+      const int32_t xl = L2s[i], xu = U2s[i], xlp = i > 0 ? L2s[i - 1] : 0, xup = i > 0 ? U2s[i - 1] : 0;
+      if (fs >= 0 && (fs & kKeyRange) == 0) {
+        const int64_t ch = fs >> 11, key = fs & (kKeyRange - 1);
+        const int32_t* sg = seg + (ch * kWideSegs + key) * 2;
+        const int32_t* c4 = segc + (ch * kKeyRange + key) * 4;
+        const int32_t sb = sg[0], se = sg[1], t0 = doff[ch * kKeyRange + key];
+        const int32_t l2min = c4[0], u2min = c4[1];
+        const int lg = dir_log2(se - sb);
+        const int32_t nbk = 1 << lg;
+        const int shf = dir_shift(max((int64_t)c4[2] - l2min, (int64_t)c4[3] - u2min), lg);
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+          const int64_t mn = hh ? u2min : l2min;
+          const int32_t bi = (int32_t)(((int64_t)(hh ? xu : xl) - mn) >> shf);
+          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)(hh ? xup : xlp) - mn) >> shf);
+          base[hh] = base[2 + hh] = t0 + hh * nbk;
+          lo[hh] = bp + 1, hi[hh] = bi, val[hh] = (int32_t)i;
+          if (i == se - 1) lo[2 + hh] = bi + 1, hi[2 + hh] = nbk - 1, val[2 + hh] = se;
         }
       }
     }
@@ -929,7 +1493,10 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
     const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
-    unsigned long long* __restrict__ part) {
+    unsigned long long* __restrict__ part, const int32_t* __restrict__ stop) {
+  // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
+  // so the sweep reads nothing (the batch is redone; its maxima are not used)
+  if (stop && stop[2] > 0) return;
   __shared__ __attribute__((aligned(16))) uint32_t accs[kClipWaves][kWin * 64];
   // wv through readfirstlane: the wave's chunk, window range and per-chunk pointers are then scalar
   // (as per-lane values they took 64-bit VGPR pairs, and 12 VGPRs spilled at 8 waves per SIMD)
@@ -1198,8 +1765,15 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)cbeg, (void*)info, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part,
-                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp})
+                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)bstart, (void*)segc, (void*)segstat,
+                  (void*)ghist})
     if (p) (void)hipFree(p);
+  bstart = segc = ghist = nullptr;
+  segstat = nullptr;
+  for (void* q : {(void*)gs, (void*)gb, (void*)hb})
+    if (q) (void)hipFree(q);
+  gs = gb = hb = nullptr;
+  cap_groups = 0;
   ptot = nullptr;
   ukeys = nuk = nullptr;
   part = nullptr;
@@ -1247,9 +1821,12 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
     cap_nf = nf;
   }
   if (nch > cap_nch) {
-    for (void* p : {(void*)seg, (void*)cbeg, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part, dtmp})
+    for (void* p : {(void*)seg, (void*)cbeg, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part, dtmp,
+                    (void*)bstart, (void*)segc, (void*)segstat, (void*)ghist})
       if (p) (void)hipFree(p);
     seg = cbeg = doff = ukeys = nuk = nullptr;
+    bstart = segc = ghist = nullptr;
+    segstat = nullptr;
     ptot = nullptr;
     part = nullptr;
     dtmp = nullptr;
@@ -1257,7 +1834,10 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
     cap_nch = 0;
     if ((e = dmalloc(&seg, nch * kWideSegs * 2)) || (e = dmalloc(&cbeg, nch + 1)) || (e = dmalloc(&doff, nch * kKeyRange + 1)) ||
         (e = dmalloc(&ptot, nch * kPortions * 64)) || (e = dmalloc(&ukeys, nch * kKeyRange)) || (e = dmalloc(&nuk, nch)) ||
-        (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)))  // up to 2 kPartWaves waves per chunk, either chunk size
+        (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)) ||  // up to 2 kPartWaves waves per chunk, either chunk size
+        (e = dmalloc(&bstart, nch * (kNFine + 1))) ||
+        (e = dmalloc(&segstat, nch * kWideSegs * 3)) || (e = dmalloc(&ghist, nch * kNFine)) ||
+        (e = dmalloc(&segc, nch * kKeyRange * 4)))
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1301,53 +1881,115 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
   bool packed = dbase >= 0 && cb <= 10 && !ws->unpacked;
   const int end_bit = (packed ? kPackChunkShift : kWideChunkShift) + cb;
   speculative = speculative && dbase >= 0;
+  // the bin sort on the speculative pass of a packed batch (its overflow, like a window width outside
+  // the delta field, sends the batch to the non-speculative pass); the library sort otherwise
+  // (and chunks of at most 2^18 frames: a frame's place in its bin takes kPlaceBits bits)
+  const bool bins = packed && speculative && !ws->libsort && (int64_t)qch * max_qframes < (1 << kPlaceBits);
+  ws->ukeys_ready = bins;
   hipLaunchKernelGGL(wide_frame_query_kernel, dim3((unsigned)std::min<int64_t>(2048, ((int64_t)nq * 64 + 255) / 256)), dim3(256),
-                     0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2, d_best_zero);
+                     0, s, d_qoff, nq, ws->fq, ws->info, ws->seg, nch * kWideSegs * 2, d_best_zero, bins ? ws->segstat : nullptr,
+                     ws->ghist, nch * kNFine);
   // one sort by (chunk, key, L2, U2 - L2); the key pass also counts the bad frames (info[1])
-  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
-                     packed, (const int32_t*)nullptr, dbase, ws->ka, packed ? (int32_t*)nullptr : ws->va, ws->info);
-  size_t tb = ws->tmp_bytes;
-  if (packed) {
-    if ((e = sweep_sort_keys<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, nf, end_bit, s))) return e;
-  } else {
-    if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
-  }
-  const int32_t* order = ws->vb;
-  if (speculative) {
-    // every window at least dbase wide and no frame for the row scan, as the caller checks after
-    // the results (info[1], info[2]); the kept-frame count stays on the device
+  const unsigned kgrid = std::min(grid_for(nf), kKeysBlocks);
+  hipLaunchKernelGGL(wide_keys_c_kernel, dim3(kgrid), dim3(256), 0, s, boxes, ws->fq, nf, qch, packed, (const int32_t*)nullptr,
+                     dbase, ws->ka, packed ? (int32_t*)nullptr : ws->va, ws->info, bins ? ws->segstat : nullptr);
+  if (bins) {
     ws->min_width = dbase;
     ws->spec = true;
-  } else {
-    int32_t info[3] = {0, 0, 0};
-    if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
-    if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
-    ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase
-    if (info[2] > 0 || dbase < 0) {
-      // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
-      if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
-      hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
-      tb = ws->tmp_bytes;
-      if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
-      packed = false;  // (the U2 pre-sort's order: frame indices carried)
-      hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
-                         false, ws->vb, (int64_t)-1, ws->ka, (int32_t*)nullptr, ws->info);
-      tb = ws->tmp_bytes;
-      if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, kWideChunkShift + cb, s)))
+    const int64_t maxc = std::min<int64_t>(nf, (int64_t)qch * max_qframes);
+    const int64_t spc = std::max<int64_t>(1, (maxc + 1024 * kHistPer - 1) / (1024 * kHistPer));
+    hipLaunchKernelGGL(wide_bin_hist_kernel, dim3((unsigned)nch, (unsigned)spc), dim3(1024), 0, s, d_qoff, nq, qch, ws->ka,
+                       ws->segstat, ws->ghist, reinterpret_cast<uint32_t*>(ws->vb));
+    const int64_t gcap = (maxc + kGroup - 1) / kGroup + 2;  // sort groups per chunk, and the closing entry
+    if (nch * gcap > ws->cap_groups) {
+      for (void* q : {(void*)ws->gs, (void*)ws->gb, (void*)ws->hb})
+        if (q) (void)hipFree(q);
+      ws->gs = ws->gb = ws->hb = nullptr;
+      ws->cap_groups = 0;
+      if ((e = dmalloc(&ws->gs, nch * gcap)) || (e = dmalloc(&ws->gb, nch * gcap)) || (e = dmalloc(&ws->hb, nch * gcap)))
         return e;
-      order = ws->va;
+      ws->cap_groups = nch * gcap;
     }
+    hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
+                       ws->ghist, ws->bstart, ws->seg, ws->doff, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->va, ws->gs, ws->gb,
+                       ws->hb, (int32_t)gcap);
+    hipLaunchKernelGGL(wide_bin_scatter_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, qch, ws->fq, ws->ka,
+                       reinterpret_cast<const uint32_t*>(ws->vb), ws->cbeg,
+                       ws->bstart, ws->kb);
+    hipLaunchKernelGGL(wide_bin_sort_kernel, dim3((unsigned)nch, (unsigned)((gcap + kBinSortWaves - 1) / kBinSortWaves)),
+                       dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gs, ws->gb, ws->hb, (int32_t)gcap, ws->cbeg, ws->kb, dbase,
+                       ws->seg,
+                       ws->L2s, ws->U2s, ws->qis, ws->va, ws->segc, ws->info);
+    if (ws->debug_bins) {  // (TFP_DEBUG_BINS: the bin sort's counts of the first chunk, on stderr)
+      std::vector<int32_t> bs(kNFine + 1), g(gcap), gbv(gcap);
+      int32_t inf[3];
+      if ((e = hipMemcpyAsync(bs.data(), ws->bstart, sizeof(int32_t) * (kNFine + 1), hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(g.data(), ws->gs, sizeof(int32_t) * gcap, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(gbv.data(), ws->gb, sizeof(int32_t) * gcap, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(inf, ws->info, sizeof inf, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+        return e;
+      int32_t nb = 0, big = 0, mx = 0, gbig = 0, gmx = 0, ng = 0;
+      for (int f = 0; f < kNFine; f++) {
+        const int32_t c = bs[f + 1] - bs[f];
+        nb += c > 0, big += c > kBinCap, mx = std::max(mx, c);
+      }
+      for (int64_t i = 0; i + 1 < gcap && (int64_t)i * kGroup < bs[kNFine]; i++) {
+        const int32_t c = g[i + 1] - g[i];
+        ng++, gbig += c > kBinCap, gmx = std::max(gmx, c);
+      }
+      fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
+              bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
+      std::vector<uint32_t> st(3 * kWideSegs);
+      if ((e = hipMemcpy(st.data(), ws->segstat, sizeof(uint32_t) * 3 * kWideSegs, hipMemcpyDeviceToHost))) return e;
+      for (int k = 0; k < kWideSegs; k++)
+        if (st[3 * k]) fprintf(stderr, "[tfp]   segment %d: %u frames, L2 %08x .. %08x\n", k, st[3 * k], st[3 * k + 1], st[3 * k + 2]);
+    }
+    hipLaunchKernelGGL(wide_dir_fill_bins_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, ws->va, ws->seg, ws->segc, ws->L2s,
+                       ws->U2s, ws->doff, ws->dtab, ws->info);
+  } else {
+    size_t tb = ws->tmp_bytes;
+    if (packed) {
+      if ((e = sweep_sort_keys<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, nf, end_bit, s))) return e;
+    } else {
+      if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->va, ws->vb, nf, end_bit, s))) return e;
+    }
+    const int32_t* order = ws->vb;
+    if (speculative) {
+      // every window at least dbase wide and no frame for the row scan, as the caller checks after
+      // the results (info[1], info[2]); the kept-frame count stays on the device
+      ws->min_width = dbase;
+      ws->spec = true;
+    } else {
+      int32_t info[3] = {0, 0, 0};
+      if ((e = hipMemcpyAsync(info, ws->info, sizeof info, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s))) return e;
+      if (info[1] > 0) return hipSuccess;  // a frame for the row scan: the caller takes launch_scan
+      ws->min_width = info[2] == 0 && dbase >= 0 ? dbase : -1;  // every window's U2 - L2 >= dbase
+      if (info[2] > 0 || dbase < 0) {
+        // a window width outside the delta field: sort by U2 first, then stably by (chunk, key, L2)
+        if ((e = hipMemsetAsync(ws->info, 0, 3 * sizeof(int32_t), s))) return e;
+        hipLaunchKernelGGL(wide_keys_u_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, nf, ws->ua, ws->va, ws->info);
+        tb = ws->tmp_bytes;
+        if ((e = sweep_sort_pairs<uint32_t>(ws->tmp, tb, ws->ua, ws->ub, ws->va, ws->vb, nf, 32, s))) return e;
+        packed = false;  // (the U2 pre-sort's order: frame indices carried)
+        hipLaunchKernelGGL(wide_keys_c_kernel, dim3(std::min(grid_for(nf), kKeysBlocks)), dim3(256), 0, s, boxes, ws->fq, nf, qch,
+                           false, ws->vb, (int64_t)-1, ws->ka, (int32_t*)nullptr, ws->info, (uint32_t*)nullptr);
+        tb = ws->tmp_bytes;
+        if ((e = sweep_sort_pairs<unsigned long long>(ws->tmp, tb, ws->ka, ws->kb, ws->vb, ws->va, nf, kWideChunkShift + cb, s)))
+          return e;
+        order = ws->va;
+      }
+    }
+    // (info[0] = the kept frames, read by the kernels below on the device; seg zeroed with the
+    // frame -> query map)
+    hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
+                       packed, dbase, ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
+    // the window segments' directories (sizes, offsets, then filled from the sorted frames)
+    const int64_t nd = nch * kKeyRange + 1;
+    (void)nd;
+    hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
+    hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb,
+                       packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab);
   }
-  // (info[0] = the kept frames, read by the kernels below on the device; seg zeroed with the
-  // frame -> query map)
-  hipLaunchKernelGGL(wide_gather_kernel, dim3(grid_for(nf)), dim3(256), 0, s, boxes, ws->fq, ws->info, ws->kb, order, qch,
-                     packed, dbase, ws->L2s, ws->U2s, ws->qis, ws->seg, nch, ws->cbeg);
-  // the window segments' directories (sizes, offsets, then filled from the sorted frames)
-  const int64_t nd = nch * kKeyRange + 1;
-  (void)nd;
-  hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
-  hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb,
-                     packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab);
   if (qch == 256) {
     hipLaunchKernelGGL(wide_pcount_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
     hipLaunchKernelGGL(wide_pscan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->ptot);
@@ -1392,17 +2034,17 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   const int64_t xcap = std::min<int64_t>(2 * kPartWaves, (int64_t)kPartWaves * (ws->qch / kWideCh));
   xw = std::min<int64_t>(xw, std::min<int64_t>(xcap, cells->nwin));
   xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
-  hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
+  if (!ws->ukeys_ready) hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                       C, ws->doff, ws->dtab, ws->part);
+                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                       C, ws->doff, ws->dtab, ws->part);
+                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   }

@@ -9,7 +9,8 @@ exact frame count back as match_count), and all clips also share one key, where 
 per wave and one clip has > 64 clusters. Bar: == the oracle's fp_search_fingerprint_info
 (src/fp_handler.c:308-374), in the default (clip-major, clusters) form, over points
 (TFP_WIDE_POINTS), with 128-query chunks only (TFP_WIDE_CH128; by default batches of queries under 256 frames take 256-query chunks),
-and with the (key, frame) pair sort instead of the packed keys-only sort (TFP_WIDE_UNPACKED).
+with the (key, frame) pair sort instead of the packed keys-only sort (TFP_WIDE_UNPACKED), and with the
+library sort instead of the bin sort on the speculative pass (TFP_WIDE_LIBSORT).
 """
 import math
 import os
@@ -111,7 +112,8 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     got = {}
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
                       ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
-                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
+                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"}),
+                      ("libsort", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_LIBSORT": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(len(kinds)):
@@ -126,6 +128,7 @@ def test_sweep_clusters_gap_boundaries(oracle, tfp_lib, tol):
     assert got["points"] == expect, tol
     assert got["clusters-128"] == expect, tol
     assert got["unpacked"] == expect, tol
+    assert got["libsort"] == expect, tol
     # every query found its own clip with a partial count: windows in the gaps missed, others hit
     for i, e in enumerate(expect):
         assert e is not None and e[0] == uuids[i // 2]
@@ -173,7 +176,8 @@ def test_sweep_many_keys_per_chunk(oracle, tfp_lib, tol):
     assert sum(e is not None for e in expect) > nq // 2
     for form, env in (("clusters", {"TFP_WIDE_MIN_TOL": "0"}), ("points", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_POINTS": "1"}),
                       ("clusters-128", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_CH128": "1"}),
-                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"})):
+                      ("unpacked", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_UNPACKED": "1"}),
+                      ("libsort", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_LIBSORT": "1"})):
         eng = _engine_with(tfp_lib, env)
         try:
             for c in range(nclips):
@@ -273,3 +277,67 @@ def test_sweep_8bit_count_field_edge(oracle, tfp_lib, tol):
         assert list(fcs2) == [256] * 256
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("tol", [0.001, 0.1])
+def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
+    """The sweep's bin sort (tfp_scan.hip wide_bins .. wide_dir_fill_bins) on bins of every size
+    class: 600 queries (three 256-query chunks, the last partly filled) whose max2 values mix a wide
+    spread (bins of a few frames: the in-register sort), a 4 dB cluster (bins of hundreds: the LDS
+    sort), repeated values (equal keys), frames whose max2 condition an ignore filter drops (their
+    segment is not sorted), NULL values and keys over the ignore filter (not kept: the chunk's tail); then the same queries with a
+    0.02 dB cluster (a bin above the per-wave cap: the batch goes to the library sort). Keys == the
+    oracle (src/fp_handler.c:318-374) and == the library sort (TFP_WIDE_LIBSORT)."""
+    rng = np.random.default_rng(int(tol * 1e4) + 11)
+    nclips, rows = 40, 300
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
+    keys = rng.integers(20, 26, nclips * rows)
+    m1 = (keys * 1_000_000 + rng.integers(0, 999_999, nclips * rows)).astype(np.int32)
+    m2 = np.where(rng.random(nclips * rows) < 0.5, rng.normal(40e6, 2e6, nclips * rows),
+                  rng.uniform(-60e6, 30e6, nclips * rows)).astype(np.int32)
+    clip = np.repeat(np.arange(nclips), rows).astype(np.int32)
+    nq = 600
+
+    def batch(cluster_db):
+        q1s, q2s, qoff = [], [], [0]
+        for i in range(nq):
+            c = int(rng.integers(nclips))
+            n = int(rng.integers(150, 250))
+            src = rng.integers(c * rows, (c + 1) * rows, n)
+            q1 = m1[src] / 1e6 + rng.normal(0, 0.01, n)
+            u = rng.random(n)
+            q2 = np.where(u < 0.4, 40.0 + rng.uniform(-cluster_db / 2, cluster_db / 2, n), m2[src] / 1e6 + rng.normal(0, 0.01, n))
+            q2 = np.where((u > 0.9) & (u < 0.95), 12.5, q2)             # repeated values
+            q2 = np.where(u >= 0.97, 36.0, q2)                           # over the 3400 ignore: max1 box only
+            q1 = np.where((u > 0.95) & (u < 0.955), -np.inf, q1)         # NULL value: key 0 (ast_json_real_get)
+            q1 = np.where((u >= 0.955) & (u < 0.96), 50.0, q1)           # key over the ignore: not kept
+            q1s.append(q1)
+            q2s.append(q2)
+            qoff.append(qoff[-1] + n)
+        q1 = np.concatenate(q1s)
+        q2 = np.concatenate(q2s)
+        frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                             ("q1", "<f8"), ("q2", "<f8")]))
+        frames["q1"], frames["q2"] = q1, q2
+        return frames, q1, q2, np.asarray(qoff, np.int64)
+
+    low, high = -1, 3400
+    for cluster_db in (4.0, 0.02):
+        frames, q1, q2, qoff = batch(cluster_db)
+        expect = []
+        for i in range(nq):
+            s = slice(qoff[i], qoff[i + 1])
+            found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, low, high)
+            expect.append((uuids[w], mc) if found else None)
+        assert sum(e is not None for e in expect) > nq // 2
+        for form, env in (("bins", {"TFP_WIDE_MIN_TOL": "0"}), ("libsort", {"TFP_WIDE_MIN_TOL": "0", "TFP_WIDE_LIBSORT": "1"})):
+            eng = _engine_with(tfp_lib, env)
+            try:
+                for c in range(nclips):
+                    sel = clip == c
+                    eng.index_add(uuids[c], m1[sel], m2[sel])
+                res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol, low, high))
+                got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+                assert got == expect, (form, cluster_db, tol, [i for i in range(nq) if got[i] != expect[i]][:5])
+            finally:
+                eng.close()
