@@ -897,7 +897,7 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
 // which sends the speculative batch to the library sort (as a window width outside the key's delta
 // field does).
 constexpr int kNFine = 16384;        // bins per chunk at most (the per-segment counts halve until they fit)
-constexpr int kBinCap = 1024;        // frames one wave sorts in LDS
+constexpr int kBinCap = 512;         // frames one wave sorts in LDS (16 KB a workgroup: 8 workgroups a CU)
 constexpr int kBinSortWaves = 4;     // waves per wide_bin_sort workgroup
 constexpr int kGroup = 64;           // a sort group: the bins whose first frame lies in [64 g, 64 g + 64)
 constexpr int kHistPer = 2;          // frames per thread of wide_bin_hist (1024 threads)
@@ -1217,12 +1217,22 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   };
   // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
   // batch is redone: the wave of the bin's group checks, and copies the bin's frames before 64 g)
+  auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1) {
+    // frames [p0, p1) of big bin [b, b + nb), unsorted: a frame whose (segment, L2, d) differs from
+    // the bin's first in a window segment sends the batch to the library sort
+    const unsigned long long k0 = kb[cb + b];
+    const int32_t p = p0 + lane;
+    bool odd = false;
+    if (p < p1) {
+      const unsigned long long k = kb[cb + p];
+      put(p, k, p == b, p == b + nb - 1);
+      odd = (k >> 8) != (k0 >> 8) && sk_of(k0) < kKeyRange;
+    }
+    if (__ballot(odd) && lane == 0) atomicAdd(&info[2], 1);
+  };
   {
     const int32_t h = hb[(int64_t)ch * gcap + g], b = bs[h], nb = bs[h + 1] - b;
-    if (nb > kBinCap) {
-      const int32_t p = max(g * kGroup, b) + lane;
-      if (p < min(g * kGroup + kGroup, b + nb)) put(p, kb[cb + p], p == b, p == b + nb - 1);
-    }
+    if (nb > kBinCap) copy_big(b, nb, max(g * kGroup, b), min(g * kGroup + kGroup, b + nb));
   }
   const int32_t n = S1 - S0;
   if (n <= 0) return;
@@ -1273,34 +1283,9 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
         continue;
       }
       // frames that all share (segment, L2, d) need no order (a crowd of equal values: the silence
-      // floor), nor do those of a segment without a max2 window (the waves of the bin's frames copy
-      // them); any other bin this large goes to the library sort with the batch
-      unsigned long long lo = ~0ull, hi = 0;
-      for (int32_t p0 = 0; p0 < nb; p0 += 256) {
-        unsigned long long k4[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const int32_t p = p0 + 64 * u + lane;
-          k4[u] = p < nb ? kb[cb + b + p] >> 8 : 0ull;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          if (p0 + 64 * u + lane < nb) {
-            lo = k4[u] < lo ? k4[u] : lo;
-            hi = k4[u] > hi ? k4[u] : hi;
-          }
-        }
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long a = shfl_xor_u64(lo, o), z = shfl_xor_u64(hi, o);
-        lo = a < lo ? a : lo;
-        hi = z > hi ? z : hi;
-      }
-      if (lo != hi && (lo >> (kPackSegShift - 8) & kKeyRange) == 0 && lane == 0) atomicAdd(&info[2], 1);
-      // (the frames before the bin's first multiple of 64: no window wave starts inside the bin there)
-      const int32_t p = b + lane;
-      if (p < min(b + nb, (b + kGroup - 1) / kGroup * kGroup)) put(p, kb[cb + p], p == b, p == b + nb - 1);
+      // floor), nor do those of a segment without a max2 window: the waves of the bin's 64-frame
+      // windows copy and check them, this one the frames before the bin's first multiple of 64
+      copy_big(b, nb, b, min(b + nb, (b + kGroup - 1) / kGroup * kGroup));
     }
   }
 }
