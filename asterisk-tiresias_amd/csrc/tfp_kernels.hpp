@@ -266,7 +266,8 @@ struct WideScratch {
   // L2 and U2
   uint32_t* segstat = nullptr;
   int32_t *ghist = nullptr, *bstart = nullptr, *segc = nullptr;
-  int32_t *gs = nullptr, *gb = nullptr, *hb = nullptr;  // sort groups per chunk: first frame, first bin, bin of frame 64 g
+  int4* gi4 = nullptr;                               // sort groups per chunk (tfp_scan.hip wide_bin_scan)
+  int32_t* gb = nullptr;
   int64_t cap_groups = 0;
   unsigned long long* part = nullptr;                // [nchunks][<= 1024 waves][kChunk] the clip-major sweep's per-wave maxima
   hipError_t reserve(int64_t nf, int32_t nq, hipStream_t s);

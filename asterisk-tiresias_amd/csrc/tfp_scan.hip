@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(1024) void wide_bin_hist_kernel(const int64_t* __re
 }
 
 // One workgroup per chunk: the bin counts scanned into each bin's first frame (bstart, relative to
-// cbeg[ch]), the sort groups (gs, gb: wide_bin_sort), the segment table, the directory offsets
+// cbeg[ch]), the sort groups (gi4, gb: wide_bin_sort), the segment table, the directory offsets
 // (chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
 // the table's size per frame), the used keys, the chunk's
 // tail of non-frames, and cbeg.
@@ -1030,8 +1030,8 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
                                                              int32_t* __restrict__ seg, int32_t* __restrict__ doff,
                                                              int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
                                                              int32_t* __restrict__ cbeg, uint8_t* __restrict__ qis,
-                                                             int32_t* __restrict__ fseg, int32_t* __restrict__ gs,
-                                                             int32_t* __restrict__ gb, int32_t* __restrict__ hb, int32_t gcap) {
+                                                             int32_t* __restrict__ fseg, int4* __restrict__ gi4,
+                                                             int32_t* __restrict__ gb, int32_t gcap) {
   constexpr int NT = 1024, FPER = kNFine / NT;
   __shared__ int32_t base[kWideSegs], nbs[kWideSegs], shf[kWideSegs], ws[NT / 64];
   __shared__ uint32_t lmn[kWideSegs];
@@ -1094,24 +1094,34 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
   const int32_t uo = block_excl<NT>(used[t], ws, NU);
   if (used[t]) ukeys[(int64_t)ch * kKeyRange + uo] = t;
   if (t == 0) nuk[ch] = NU;
-  // sort groups (wide_bin_sort): group g starts at the first bin whose first frame is >= 64 g (the
-  // bin holding frame 64 g: hb[g], or the next one); g = ceil(T / 64) closes the last
-  for (int32_t gi = t; (int64_t)gi * kGroup < (int64_t)T + kGroup; gi += NT) {
-    const int32_t p = gi * kGroup;
-    int32_t a = T, f = kNFine, lo = kNFine;
-    if (p < T) {  // the last bin starting at or before p (non-empty: start[kNFine] = T > p)
-      int32_t hi = kNFine;
-      lo = 0;
+  // sort groups (wide_bin_sort): group g starts at the first bin whose first frame is >= kGroup g
+  // (the bin holding frame kGroup g, or the next one). gi4[g] = {its first frame, the next group's,
+  // the first frame and size of the bin holding frame kGroup g}; gb[g] = its first bin. Groups from
+  // ceil(T / kGroup) on hold nothing ({T, T, 0, 0}).
+  for (int32_t gi = t; gi < gcap; gi += NT) {
+    const int32_t p = gi * kGroup, q = p + kGroup;
+    int32_t a = T, z = T, f = kNFine, hs = 0, hn = 0;
+    auto last_at = [&](int32_t x) {  // the last bin starting at or before x < T (non-empty: start[kNFine] = T > x)
+      int32_t lo = 0, hi = kNFine;
       while (hi - lo > 1) {
         const int32_t mid = (lo + hi) >> 1;
-        if (start[mid] <= p) lo = mid; else hi = mid;
+        if (start[mid] <= x) lo = mid; else hi = mid;
       }
+      return lo;
+    };
+    if (p < T) {
+      const int32_t lo = last_at(p);
       f = start[lo] == p ? lo : lo + 1;
       a = start[f];
+      hs = start[lo];
+      hn = start[lo + 1] - hs;
+      if (q < T) {
+        const int32_t l2 = last_at(q);
+        z = start[start[l2] == q ? l2 : l2 + 1];
+      }
     }
-    gs[(int64_t)ch * gcap + gi] = a;
+    gi4[(int64_t)ch * gcap + gi] = make_int4(a, z, hs, hn);
     gb[(int64_t)ch * gcap + gi] = f;
-    hb[(int64_t)ch * gcap + gi] = lo;
   }
   // the range's tail (no kept frame): query 0, no segment
   for (int64_t i = cb + T + t; i < ce; i += NT) {
@@ -1137,17 +1147,35 @@ __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v,
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((unsigned long long)hi << 32) | lo;
 }
-// ascending bitonic sort of one key per lane
-__device__ __forceinline__ unsigned long long bitonic_wave(unsigned long long v, int lane) {
+// ascending bitonic sort of R keys per lane in registers (element i = lane + 64 r is v[r]): the
+// stages with j >= 64 pair registers of one lane, the others lanes (shuffles)
+template <int R>
+__device__ __forceinline__ void bitonic_regs(unsigned long long (&v)[R], int lane) {
 #pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
+  for (int k = 2; k <= 64 * R; k <<= 1)
 #pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      const unsigned long long o = shfl_xor_u64(v, j);
-      const bool up = (lane & k) == 0, lower = (lane & j) == 0;
-      v = lower == up ? (o < v ? o : v) : (o > v ? o : v);
+      if (j >= 64) {
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const int q = r ^ (j / 64);
+          if (q > r) {  // (i = lane + 64 r, partner lane + 64 q: ascending when (i & k) == 0)
+            const bool up = ((64 * r) & k) == 0;
+            const unsigned long long a = v[r], b = v[q];
+            v[r] = (a < b) == up ? a : b;
+            v[q] = (a < b) == up ? b : a;
+          }
+        }
+      } else {
+        const bool lower = (lane & j) == 0;
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+          const unsigned long long o = shfl_xor_u64(v[r], j);
+          const bool up = ((lane + 64 * r) & k) == 0;
+          v[r] = lower == up ? (o < v[r] ? o : v[r]) : (o > v[r] ? o : v[r]);
+        }
+      }
     }
-  return v;
 }
 // ascending bitonic sort of S[0, N) (N a power of two, 128 .. kBinCap) by one wave in LDS (a
 // wave's LDS operations complete in order: no barrier between the stages)
@@ -1166,15 +1194,15 @@ __device__ void bitonic_lds(unsigned long long* S, int N, int lane) {
 
 // Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
 // (bins are monotone in the key, so sorting a run of whole bins sorts each of them): frames
-// [gs[g], gs[g + 1]) of the chunk, bins [gb[g], gb[g + 1]). One wave per group sorts it in registers
-// (up to 128 frames) or LDS, and writes each sorted frame's L2, U2 (= L2 + dbase + d), query and
-// segment (ch << 11 | segment key); a frame that starts or ends a window segment writes the
-// segment's first or last L2 / U2 (segc) for the directory fill. A group above kBinCap frames (a
-// crowded bin) goes bin by bin: a bin whose frames all share (segment, L2, d), or whose segment
-// has no max2 window, needs no order; any other bin above kBinCap frames sets info[2].
+// [gi4[g].x, gi4[g].y) of the chunk, bins [gb[g], gb[g + 1]). One wave per group sorts it in
+// registers (up to 256 frames, 4 a lane) or LDS, and writes each sorted frame's L2, U2 (= L2 +
+// dbase + d), query and segment (ch << 11 | segment key); a frame that starts or ends a window
+// segment writes the segment's first or last L2 / U2 (segc) for the directory fill. A group above
+// kBinCap frames (a crowded bin) goes bin by bin: a bin whose frames all share (segment, L2, d), or
+// whose segment has no max2 window, needs no order; any other bin above kBinCap frames sets
+// info[2].
 __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
-    const int32_t* __restrict__ bstart, const int32_t* __restrict__ gs, const int32_t* __restrict__ gb,
-    const int32_t* __restrict__ hb, int32_t gcap,
+    const int32_t* __restrict__ bstart, const int4* __restrict__ gi4, const int32_t* __restrict__ gb, int32_t gcap,
     const int32_t* __restrict__ cbeg, const unsigned long long* __restrict__ kb, int64_t dbase,
     const int32_t* __restrict__ seg, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s, uint8_t* __restrict__ qis,
     int32_t* __restrict__ fseg, int32_t* __restrict__ segc, int32_t* __restrict__ info) {
@@ -1183,14 +1211,15 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   const int ch = blockIdx.x;
   const int32_t g = blockIdx.y * kBinSortWaves + wv;
   const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
-  const int32_t* gsc = gs + (int64_t)ch * gcap;
-  if ((int64_t)g * kGroup >= bs[kNFine]) return;  // (no frame of the chunk starts here; wave-uniform)
-  const int32_t S0 = gsc[g], S1 = gsc[g + 1];
+  if (g + 1 >= gcap) return;  // (wave-uniform)
+  const int4 gq = gi4[(int64_t)ch * gcap + g];
+  const int32_t S0 = gq.x, S1 = gq.y;
   const int64_t cb = cbeg[ch];
   unsigned long long* S = sk[wv];
   auto sk_of = [](unsigned long long k) { return (int32_t)((k >> kPackSegShift) & (kWideSegs - 1)); };
-  // sorted frame p (chunk-relative) of key k; first / last: p may start / end its segment
-  auto put = [&](int32_t p, unsigned long long k, bool first, bool last) {
+  // sorted frame p (chunk-relative) of key k; first / last: 1 when p starts / ends its segment, 2
+  // when it may (a neighbour outside the group: the segment table decides)
+  auto put = [&](int32_t p, unsigned long long k, int first, int last) {
     const int64_t pos = cb + p;
     const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
     const int32_t u2 = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
@@ -1201,8 +1230,8 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     if ((first || last) && sgk < kKeyRange) {
       const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
       int32_t* c4 = segc + ((int64_t)ch * kKeyRange + sgk) * 4;
-      if (first && sg[0] == pos) c4[0] = l2, c4[1] = u2;
-      if (last && sg[1] == pos + 1) c4[2] = l2, c4[3] = u2;
+      if (first == 1 || (first == 2 && sg[0] == pos)) c4[0] = l2, c4[1] = u2;
+      if (last == 1 || (last == 2 && sg[1] == pos + 1)) c4[2] = l2, c4[3] = u2;
     }
   };
   // frames [b, b + n) sorted in LDS, written
@@ -1212,59 +1241,60 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     bitonic_lds(S, N, lane);
     for (int p = lane; p < n; p += 64) {
       const unsigned long long k = S[p];
-      put(b + p, k, p == 0 || sk_of(S[p - 1]) != sk_of(k), p == n - 1 || sk_of(S[p + 1]) != sk_of(k));
+      put(b + p, k, p == 0 ? 2 : sk_of(S[p - 1]) != sk_of(k), p == n - 1 ? 2 : sk_of(S[p + 1]) != sk_of(k));
     }
   };
   // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
-  // batch is redone: the wave of the bin's group checks, and copies the bin's frames before 64 g)
+  // batch is redone): each wave copies and checks its own, the wave of the bin's group those before
+  // the bin's first multiple of 64
   auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1) {
     // frames [p0, p1) of big bin [b, b + nb), unsorted: a frame whose (segment, L2, d) differs from
     // the bin's first in a window segment sends the batch to the library sort
     const unsigned long long k0 = kb[cb + b];
-    const int32_t p = p0 + lane;
     bool odd = false;
-    if (p < p1) {
+    for (int32_t p = p0 + lane; p < p1; p += 64) {
       const unsigned long long k = kb[cb + p];
-      put(p, k, p == b, p == b + nb - 1);
-      odd = (k >> 8) != (k0 >> 8) && sk_of(k0) < kKeyRange;
+      put(p, k, p == b ? 2 : 0, p == b + nb - 1 ? 2 : 0);
+      odd = odd || ((k >> 8) != (k0 >> 8) && sk_of(k0) < kKeyRange);
     }
     if (__ballot(odd) && lane == 0) atomicAdd(&info[2], 1);
   };
-  {
-    const int32_t h = hb[(int64_t)ch * gcap + g], b = bs[h], nb = bs[h + 1] - b;
-    if (nb > kBinCap) copy_big(b, nb, max(g * kGroup, b), min(g * kGroup + kGroup, b + nb));
-  }
+  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w));
   const int32_t n = S1 - S0;
   if (n <= 0) return;
+  // n <= 64 R: R keys a lane, sorted in registers; each frame's neighbours through the lanes
+  auto sort_regs = [&](auto rr) {
+    constexpr int R = decltype(rr)::value;
+    unsigned long long v[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) v[r] = 64 * r + lane < n ? kb[cb + S0 + 64 * r + lane] : ~0ull;
+    bitonic_regs<R>(v, lane);
+    int32_t sg[R], prev[R], next[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) sg[r] = sk_of(v[r]);
+#pragma unroll
+    for (int r = 0; r < R; r++) {  // (every lane: the shuffles read whole rows)
+      const int32_t up = __shfl_up(sg[r], 1, 64), dn = __shfl_down(sg[r], 1, 64);
+      const int32_t pl = __shfl(sg[r > 0 ? r - 1 : 0], 63, 64), nf = __shfl(sg[r + 1 < R ? r + 1 : r], 0, 64);
+      prev[r] = lane ? up : r ? pl : -1;
+      next[r] = lane < 63 ? dn : r + 1 < R ? nf : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+      const int32_t i = 64 * r + lane;
+      if (i < n) put(S0 + i, v[r], i == 0 ? 2 : prev[r] != sg[r], i == n - 1 ? 2 : next[r] != sg[r]);
+    }
+  };
   if (n <= 64) {
-    const unsigned long long v = bitonic_wave(lane < n ? kb[cb + S0 + lane] : ~0ull, lane);
-    const int32_t s = sk_of(v), sp = __shfl_up(s, 1, 64), sn = __shfl_down(s, 1, 64);
-    if (lane < n) put(S0 + lane, v, lane == 0 || sp != s, lane == n - 1 || sn != s);
+    sort_regs(std::integral_constant<int, 1>{});
     return;
   }
   if (n <= 128) {
-    unsigned long long v0 = kb[cb + S0 + lane], v1 = 64 + lane < n ? kb[cb + S0 + 64 + lane] : ~0ull;
-    // bitonic over 128 = 2 x 64: element i = lane + 64 r (r = 0: v0, 1: v1)
-#pragma unroll
-    for (int k = 2; k <= 128; k <<= 1)
-#pragma unroll
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        if (j == 64) {  // (k = 128: ascending) the pair (lane, 64 + lane) in this lane
-          const unsigned long long lo = v0 < v1 ? v0 : v1, hi = v0 < v1 ? v1 : v0;
-          v0 = lo, v1 = hi;
-        } else {
-          const unsigned long long o0 = shfl_xor_u64(v0, j), o1 = shfl_xor_u64(v1, j);
-          const bool lower = (lane & j) == 0;
-          const bool up0 = (lane & k) == 0, up1 = ((64 + lane) & k) == 0;
-          v0 = lower == up0 ? (o0 < v0 ? o0 : v0) : (o0 > v0 ? o0 : v0);
-          v1 = lower == up1 ? (o1 < v1 ? o1 : v1) : (o1 > v1 ? o1 : v1);
-        }
-      }
-    const int32_t s0 = sk_of(v0), s1 = sk_of(v1);
-    const int32_t p0 = __shfl_up(s0, 1, 64), n0 = __shfl_down(s0, 1, 64), p1 = __shfl_up(s1, 1, 64), n1 = __shfl_down(s1, 1, 64);
-    const int32_t l0 = __shfl(s0, 63, 64), f1 = __shfl(s1, 0, 64);  // (the neighbours across the halves)
-    put(S0 + lane, v0, lane == 0 || p0 != s0, (lane == 63 ? f1 : n0) != s0 || lane == n - 1);
-    if (64 + lane < n) put(S0 + 64 + lane, v1, (lane == 0 ? l0 : p1) != s1, 64 + lane == n - 1 || n1 != s1);
+    sort_regs(std::integral_constant<int, 2>{});
+    return;
+  }
+  if (n <= 256) {
+    sort_regs(std::integral_constant<int, 4>{});
     return;
   }
   if (n <= kBinCap) {
@@ -1755,9 +1785,10 @@ void WideScratch::release() {
     if (p) (void)hipFree(p);
   bstart = segc = ghist = nullptr;
   segstat = nullptr;
-  for (void* q : {(void*)gs, (void*)gb, (void*)hb})
+  for (void* q : {(void*)gi4, (void*)gb})
     if (q) (void)hipFree(q);
-  gs = gb = hb = nullptr;
+  gi4 = nullptr;
+  gb = nullptr;
   cap_groups = 0;
   ptot = nullptr;
   ukeys = nuk = nullptr;
@@ -1887,30 +1918,29 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
                        ws->segstat, ws->ghist, reinterpret_cast<uint32_t*>(ws->vb));
     const int64_t gcap = (maxc + kGroup - 1) / kGroup + 2;  // sort groups per chunk, and the closing entry
     if (nch * gcap > ws->cap_groups) {
-      for (void* q : {(void*)ws->gs, (void*)ws->gb, (void*)ws->hb})
+      for (void* q : {(void*)ws->gi4, (void*)ws->gb})
         if (q) (void)hipFree(q);
-      ws->gs = ws->gb = ws->hb = nullptr;
+      ws->gi4 = nullptr;
+      ws->gb = nullptr;
       ws->cap_groups = 0;
-      if ((e = dmalloc(&ws->gs, nch * gcap)) || (e = dmalloc(&ws->gb, nch * gcap)) || (e = dmalloc(&ws->hb, nch * gcap)))
-        return e;
+      if ((e = dmalloc(&ws->gi4, nch * gcap)) || (e = dmalloc(&ws->gb, nch * gcap))) return e;
       ws->cap_groups = nch * gcap;
     }
     hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
-                       ws->ghist, ws->bstart, ws->seg, ws->doff, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->va, ws->gs, ws->gb,
-                       ws->hb, (int32_t)gcap);
+                       ws->ghist, ws->bstart, ws->seg, ws->doff, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->va, ws->gi4, ws->gb,
+                       (int32_t)gcap);
     hipLaunchKernelGGL(wide_bin_scatter_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, qch, ws->fq, ws->ka,
                        reinterpret_cast<const uint32_t*>(ws->vb), ws->cbeg,
                        ws->bstart, ws->kb);
     hipLaunchKernelGGL(wide_bin_sort_kernel, dim3((unsigned)nch, (unsigned)((gcap + kBinSortWaves - 1) / kBinSortWaves)),
-                       dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gs, ws->gb, ws->hb, (int32_t)gcap, ws->cbeg, ws->kb, dbase,
-                       ws->seg,
+                       dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gi4, ws->gb, (int32_t)gcap, ws->cbeg, ws->kb, dbase, ws->seg,
                        ws->L2s, ws->U2s, ws->qis, ws->va, ws->segc, ws->info);
     if (ws->debug_bins) {  // (TFP_DEBUG_BINS: the bin sort's counts of the first chunk, on stderr)
-      std::vector<int32_t> bs(kNFine + 1), g(gcap), gbv(gcap);
+      std::vector<int32_t> bs(kNFine + 1);
+      std::vector<int4> g(gcap);
       int32_t inf[3];
       if ((e = hipMemcpyAsync(bs.data(), ws->bstart, sizeof(int32_t) * (kNFine + 1), hipMemcpyDeviceToHost, s)) ||
-          (e = hipMemcpyAsync(g.data(), ws->gs, sizeof(int32_t) * gcap, hipMemcpyDeviceToHost, s)) ||
-          (e = hipMemcpyAsync(gbv.data(), ws->gb, sizeof(int32_t) * gcap, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(g.data(), ws->gi4, sizeof(int4) * gcap, hipMemcpyDeviceToHost, s)) ||
           (e = hipMemcpyAsync(inf, ws->info, sizeof inf, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
         return e;
       int32_t nb = 0, big = 0, mx = 0, gbig = 0, gmx = 0, ng = 0;
@@ -1918,16 +1948,12 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
         const int32_t c = bs[f + 1] - bs[f];
         nb += c > 0, big += c > kBinCap, mx = std::max(mx, c);
       }
-      for (int64_t i = 0; i + 1 < gcap && (int64_t)i * kGroup < bs[kNFine]; i++) {
-        const int32_t c = g[i + 1] - g[i];
-        ng++, gbig += c > kBinCap, gmx = std::max(gmx, c);
+      for (int64_t i = 0; i + 1 < gcap; i++) {
+        const int32_t c = g[i].y - g[i].x;
+        ng += c > 0, gbig += c > kBinCap, gmx = std::max(gmx, c);
       }
       fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
               bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
-      std::vector<uint32_t> st(3 * kWideSegs);
-      if ((e = hipMemcpy(st.data(), ws->segstat, sizeof(uint32_t) * 3 * kWideSegs, hipMemcpyDeviceToHost))) return e;
-      for (int k = 0; k < kWideSegs; k++)
-        if (st[3 * k]) fprintf(stderr, "[tfp]   segment %d: %u frames, L2 %08x .. %08x\n", k, st[3 * k], st[3 * k + 1], st[3 * k + 2]);
     }
     hipLaunchKernelGGL(wide_dir_fill_bins_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, ws->va, ws->seg, ws->segc, ws->L2s,
                        ws->U2s, ws->doff, ws->dtab, ws->info);
