@@ -223,7 +223,7 @@ struct tfp_engine {
   int64_t fail_query_len = -1;  // TFP_TEST_FAIL_QUERY_SAMPLES=n: a search with a query of n samples fails (tests)
   int32_t kb_win = 0;           // TFP_KEYBITS_WIN: LDS words per column window of launch_key_bits (tests; 0 = default)
   int64_t kb_direct = -1;       // TFP_KEYBITS_DIRECT: pieces below this many rows use global atomics (tests; -1 = default)
-  DevBuf logfix_key, logfix_val;  // device copy of the glibc log correction table (LogFix)
+  DevBuf logfix_key, logfix_val, logfix_bits;  // device copy of the glibc log correction table (LogFix)
   LogFix logfix{nullptr, nullptr, 0};
   // index delta (round 4, tfp_index.hpp): the live clips added since the last build, searched by the
   // coefs = 1 vote paths beside the main index instead of merged into it per enrolment
@@ -284,8 +284,14 @@ int ensure_logfix(tfp_engine* e) {
   HIPCHK(e, e->logfix_val.reserve(sizeof(double) * slots));
   HIPCHK(e, hipMemcpyAsync(e->logfix_key.p, k, sizeof(uint32_t) * slots, hipMemcpyHostToDevice, e->stream));
   HIPCHK(e, hipMemcpyAsync(e->logfix_val.p, v, sizeof(double) * slots, hipMemcpyHostToDevice, e->stream));
+  // the keys present as a bitmap over the 2^24 reduced arguments (2 MiB)
+  std::vector<uint32_t> bits(1u << 19, 0u);
+  for (size_t j = 0; j < slots; j++)
+    if (k[j] != kLogFixEmpty) bits[k[j] >> 5] |= 1u << (k[j] & 31);
+  HIPCHK(e, e->logfix_bits.reserve(sizeof(uint32_t) * bits.size()));
+  HIPCHK(e, hipMemcpyAsync(e->logfix_bits.p, bits.data(), sizeof(uint32_t) * bits.size(), hipMemcpyHostToDevice, e->stream));
   HIPCHK(e, hipStreamSynchronize(e->stream));
-  e->logfix = LogFix{e->logfix_key.as<uint32_t>(), e->logfix_val.as<double>(), n, 1};
+  e->logfix = LogFix{e->logfix_key.as<uint32_t>(), e->logfix_val.as<double>(), n, 1, e->logfix_bits.as<uint32_t>()};
   return TFP_OK;
 }
 

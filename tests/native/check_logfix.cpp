@@ -6,6 +6,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include "../../asterisk-tiresias_amd/csrc/tfp_math.hpp"
 #include "../../asterisk-tiresias_amd/csrc/tfp_tables.hpp"
 
@@ -24,7 +25,10 @@ int main(int argc, char** argv) {
   const double* hv;
   int32_t hn;
   log_fix_hash(&hk, &hv, &hn);
-  const LogFix hx{hk, hv, hn, 1};
+  std::vector<uint32_t> bits(1u << 19, 0u);  // (the engine's bitmap of the keys present)
+  for (int32_t j = 0; j < (1 << kLogFixHashBits); j++)
+    if (hk[j] != kLogFixEmpty) bits[hk[j] >> 5] |= 1u << (hk[j] & 31);
+  const LogFix hx{hk, hv, hn, 1, bits.data()};
   uint64_t bad_hash = hn != n;
 #pragma omp parallel for reduction(+ : bad_hash) schedule(static)
   for (int64_t key = 0; key < (1 << 24); key++) {
