@@ -18,7 +18,7 @@ for r in rows:
         cur = []
     if cur is None:
         continue
-    cur.append((name.split("(")[0].replace("tfp::(anonymous namespace)::", "").replace("tfp::", ""),
+    cur.append((name.replace("tfp::(anonymous namespace)::", "").replace("tfp::", "").split("(")[0],
                 int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
     if "wide_part_max" in name:
         batches.append(cur)
