@@ -3,7 +3,9 @@
 Usage: python scripts/tools/pmc_summary.py DIR [DIR ...]  (each DIR a gpurun_out/<tag>/pN with
 run_counter_collection.csv). Picks the fingerprint kernel dispatches of the largest grid (the C2
 launch), averages each counter over them (summed over the counter's instances per dispatch), and
-prints per-launch totals, per-frame instruction counts and the SQ cycle split."""
+prints per-launch totals, per-frame instruction counts and the SQ cycle split.
+FRAMES (default 960512, the C2 launch) and LAST (only the last LAST such dispatches of each pass,
+e.g. the C3 query launches after a DB enrolment of the same grid) from the environment."""
 import collections
 import csv
 import glob
@@ -12,15 +14,18 @@ import os
 import re
 import sys
 
-FRAMES = 960512
+FRAMES = int(os.environ.get("FRAMES", "960512"))
+LAST = int(os.environ.get("LAST", "0"))
 vals = collections.defaultdict(list)
 for d in sys.argv[1:]:
     for path in glob.glob(os.path.join(d, "**", "run_counter_collection.csv"), recursive=True):
         rows = [r for r in csv.DictReader(open(path)) if re.search(r"fingerprint(8k)?_kernel", r["Kernel_Name"])]
         grid = max(int(r["Grid_Size"]) for r in rows)
+        keep = sorted({int(r["Dispatch_Id"]) for r in rows if int(r["Grid_Size"]) == grid})
+        keep = set(keep[-LAST:] if LAST else keep)
         per = collections.defaultdict(lambda: collections.defaultdict(float))
         for r in rows:
-            if int(r["Grid_Size"]) == grid:
+            if int(r["Dispatch_Id"]) in keep:
                 per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
         for c, dd in per.items():
             vals[c].append(sum(dd.values()) / len(dd))

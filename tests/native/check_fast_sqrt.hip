@@ -30,11 +30,11 @@ constexpr uint32_t kHalf = kInf / 2;       // lane 0 takes b, lane 1 takes b + k
 constexpr uint32_t kSampleStride = 1021;   // host pin of the device reference
 
 struct Counts {
-  unsigned long long fast_mismatch, rare_missed, rare_spurious, zero_bad, sqrt_flushed, checked;
+  unsigned long long fast_mismatch, rare_missed, rare_spurious, zero_bad, sqrt_flushed, checked, up, down;
 };
 
 __global__ void check_kernel(Counts* c, uint32_t rare_m1, float* sample) {
-  unsigned long long bad = 0, missed = 0, spur = 0, zbad = 0, flushed = 0, n = 0;
+  unsigned long long bad = 0, missed = 0, spur = 0, zbad = 0, flushed = 0, n = 0, up = 0, down = 0;
   for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < kHalf; b += gridDim.x * blockDim.x) {
     const uint32_t bx[2] = {b, b + kHalf};
     const tfp::cf2 x = {__builtin_bit_cast(float, bx[0]), __builtin_bit_cast(float, bx[1])};
@@ -48,6 +48,11 @@ __global__ void check_kernel(Counts* c, uint32_t rare_m1, float* sample) {
       if (fast && __builtin_bit_cast(uint32_t, r[i]) != __builtin_bit_cast(uint32_t, ref)) bad++;
       if (xi == 0.f && __builtin_bit_cast(uint32_t, r[i]) != 0u) zbad++;
       if (xi > 0.f && __builtin_amdgcn_sqrtf(xi) == 0.f) flushed++;
+      if (fast && xi > 0.f) {  // which neighbour of v_sqrt_f32's result the correct rounding takes
+        const uint32_t y = __builtin_bit_cast(uint32_t, __builtin_amdgcn_sqrtf(xi)), c = __builtin_bit_cast(uint32_t, ref);
+        up += c == y + 1u;
+        down += c == y - 1u;
+      }
       n++;
     }
     // fingerprint8k_kernel's rare test on the pair, with x.x (the low half's candidate; x.y is
@@ -62,6 +67,8 @@ __global__ void check_kernel(Counts* c, uint32_t rare_m1, float* sample) {
   if (zbad) atomicAdd(&c->zero_bad, zbad);
   if (spur) atomicAdd(&c->rare_spurious, spur);
   if (flushed) atomicAdd(&c->sqrt_flushed, flushed);
+  if (up) atomicAdd(&c->up, up);
+  if (down) atomicAdd(&c->down, down);
   atomicAdd(&c->checked, n);
 }
 
@@ -96,8 +103,10 @@ int main() {
   delete[] hs;
   printf("checked %llu floats [0, inf): fast_mismatch %llu, zero_bad %llu, rare_missed %llu, "
          "rare_spurious %llu; v_sqrt_f32 returns 0 for %llu positive inputs; "
-         "device sqrtf vs host sqrtf on %llu samples: %llu differ\n",
-         c.checked, c.fast_mismatch, c.zero_bad, c.rare_missed, c.rare_spurious, c.sqrt_flushed, nsample, ref_bad);
+         "device sqrtf vs host sqrtf on %llu samples: %llu differ; v_sqrt_f32 one below the correctly rounded "
+         "result on %llu fast-range inputs, one above on %llu\n",
+         c.checked, c.fast_mismatch, c.zero_bad, c.rare_missed, c.rare_spurious, c.sqrt_flushed, nsample, ref_bad, c.up,
+         c.down);
   (void)hipFree(d_c);
   (void)hipFree(d_s);
   const bool ok = c.checked == 2ull * kHalf && !c.fast_mismatch && !c.zero_bad && !c.rare_missed && !c.rare_spurious &&
