@@ -17,6 +17,7 @@ PKG = os.path.join(REPO, "asterisk-tiresias_amd")
 
 K = "csrc/tfp_kernels.hip"
 SP = "csrc/tfp_split.hpp"
+SC = "csrc/tfp_scan.hip"
 ABL = {
     "base": [],
     # raw v_sqrt_f32, no Tuckerman correction
@@ -47,6 +48,15 @@ ABL = {
         for (int n2 = 0; n2 < 16; n2++) z[n2] = Y[n2];""")],
     # partner exchange without ds_bpermute
     "nobperm": [(K, "Pq[k2] = cf{partner16(Y[15 - k2].x), partner16(Y[15 - k2].y)};", "Pq[k2] = Y[15 - k2];")],
+    # coefs=2 bin sort (tfp_scan.hip wide_bin_sort) without its sorts: the groups written unsorted,
+    # and info[2] set so the directory fill and the sweep skip the batch (it is redone with the
+    # library sort): only the kernel's own duration in a trace means anything
+    "binsort_nosort": [(SC, "    bitonic_regs<R>(v, lane);\n", "\n"),
+                       (SC, "    bitonic_lds(S, N, lane);\n", "\n"),
+                       (SC, "  const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);\n  if (g + 1 >= gcap) return;",
+                        "  const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);\n"
+                        "  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) atomicAdd(&info[2], 1);\n"
+                        "  if (g + 1 >= gcap) return;")],
 }
 
 
