@@ -542,7 +542,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
     # 100 / 3400 Hz ignore filter — which drops ~92% of the synthetic frames (their max1 sits at
     # 16.8-17.2 dB, under 10*log10(100) = 20 dB) and so finds nothing — plus 50 / 60 Hz
     # (16.99 / 17.78 dB), which keeps about a third of them. First call untimed (it builds the tolerance's caches), then
-    # the median of up to 3 timed calls (1 when a call takes over 2 s).
+    # the median of up to 5 timed calls (1 when a call takes over 2 s).
     sweeps = []
     if not args.no_sweeps:
         for coefs, tol, low, high in [(1, 0.01, -1, -1), (1, 0.1, -1, -1), (1, 0.45, -1, -1), (1, 0.001, 100, 3400),
@@ -560,7 +560,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
             sweep_batch()
             torch.cuda.synchronize(dev)
             ts = []
-            for _ in range(3):
+            for _ in range(5):
                 barrier()
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
