@@ -1409,6 +1409,11 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
 // of two 16-bit counts) among 64 frames by reading their queries out of the lanes (no per-frame
 // memory dependency).
 constexpr int kPortions = 256;
+#ifndef TFP_PSTEP
+#define TFP_PSTEP 4
+#endif
+constexpr int kPStep = TFP_PSTEP;  // frames per prefix-count row (1 or 4)
+static_assert(kPStep == 1 || kPStep == 4, "one row a frame, or a 4-byte word of queries a row");
 __device__ __forceinline__ void portion_range(const int32_t* cbeg, int ch, int p, int32_t& b, int32_t& r0, int32_t& r1) {
   b = cbeg[ch];
   const int32_t n = cbeg[ch + 1] - b;
@@ -1460,6 +1465,9 @@ __global__ __launch_bounds__(1024) void wide_pscan_kernel(uint32_t* __restrict__
 #pragma unroll
   for (int j = 0; j < 16; j++) t[64 * j] = base + v[j];
 }
+// The rows are checkpoints: frame i's row only when i % kPStep == kPStep - 1, at P[i / kPStep] (a
+// fourth of the bytes written; wide_clips adds the up to kPStep - 1 frames after the checkpoint
+// before a position from their queries, prefix_at).
 template <int QPL>
 __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg, const uint8_t* __restrict__ qis,
                                                            const uint32_t* __restrict__ ptot, uint32_t* __restrict__ P) {
@@ -1469,13 +1477,35 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   uint32_t run = ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane];
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : kPadQ;
-    uint32_t* row = P + ((int64_t)b + i) * kWideW + lane;
+    const int32_t bi = b + i;  // (global frame of j = 0)
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
       run += prefix_inc<QPL>(__builtin_amdgcn_readlane(x, j), lane);
-      if (j < m) row[(int64_t)j * kWideW] = run;
+      if (j < m && ((bi + j) & (kPStep - 1)) == kPStep - 1) P[(int64_t)((bi + j) / kPStep) * kWideW + lane] = run;
     }
+  }
+}
+// In-chunk prefix count at frame e (>= cb, the chunk's first frame) from the checkpoint rows: the
+// row at e itself, or the last checkpoint before e in the chunk (none: 0) plus the increments of
+// the frames after it up to e, read from their queries (one aligned 4-byte load; qis is padded).
+// e is wave-uniform (every caller's is a shuffled or read-lane value): as a scalar, the queries'
+// word is a scalar load and only the per-lane compare and add take vector registers.
+template <int QPL>
+__device__ __forceinline__ uint32_t prefix_at(const uint32_t* __restrict__ P, const uint8_t* __restrict__ qis, int32_t cb,
+                                              int32_t e, int lane) {
+  if constexpr (kPStep == 1) {
+    return P[(int64_t)e * kWideW + lane];
+  } else {
+    e = __builtin_amdgcn_readfirstlane(e);
+    const int32_t g = e / kPStep, f0 = g * kPStep;
+    if (e == f0 + kPStep - 1) return P[(int64_t)g * kWideW + lane];
+    uint32_t v = f0 - 1 >= cb ? P[(int64_t)(g - 1) * kWideW + lane] : 0u;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(qis + f0);
+#pragma unroll
+    for (int j = 0; j < kPStep - 1; j++)
+      if (f0 + j <= e && f0 + j >= cb) v += prefix_inc<QPL>((int32_t)((w >> (8 * j)) & 255u), lane);
+    return v;
   }
 }
 
@@ -1520,7 +1550,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
-    const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
+    const uint8_t* __restrict__ qis, const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
     unsigned long long* __restrict__ part, const int32_t* __restrict__ stop) {
   // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
   // so the sweep reads nothing (the batch is redone; its maxima are not used)
@@ -1564,7 +1594,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
   };
   auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
-    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
+    cnt += prefix_at<QPL>(P, qis, cb, b, lane) - (a > sb ? prefix_at<QPL>(P, qis, cb, a - 1, lane) : base);
   };
   // The chunk's used keys' segment constants, one key per lane, loaded once per wave instead of
   // once per window and key (three dependent loads ahead of every key's groups): the window loop
@@ -1618,8 +1648,8 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           fb = sg[2 * (k | kKeyRange)];
           fe = sg[2 * (k | kKeyRange) + 1];
         }
-        base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
-        fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
+        base = se > sb && sb > cb ? prefix_at<QPL>(P, qis, cb, sb - 1, lane) : 0u;
+        fcnt = fe > fb ? prefix_at<QPL>(P, qis, cb, fe - 1, lane) - (fb > cb ? prefix_at<QPL>(P, qis, cb, fb - 1, lane) : 0u) : 0u;
         if (se <= sb) {  // no frame of the key has a max2 window: every group scores the rest
           for (; g < g1; g++) add((int32_t)(cv.g_key[g] & kColMask), fcnt);
           continue;
@@ -1838,7 +1868,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
     cap_nf = 0;
     if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
         (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
-        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideW)) || (e = dmalloc(&fq, nf)))
+        (e = dmalloc(&qis, nf + 16)) || (e = dmalloc(&P, (nf / kPStep + 2) * kWideW)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
     size_t t3 = 0;
@@ -2061,13 +2091,13 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (!ws->ukeys_ready) hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
                        C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
                        C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
