@@ -265,8 +265,7 @@ struct WideScratch {
   // per chunk and bin the frame count and first sorted frame, each window segment's first / last
   // L2 and U2
   uint32_t* segstat = nullptr;
-  int32_t *ghist = nullptr, *bstart = nullptr;
-  int4* segk = nullptr;  // per (chunk, window segment): {min L2, min U2, bucket shift, directory offset}
+  int32_t *ghist = nullptr, *bstart = nullptr, *segc = nullptr;
   int4* gi4 = nullptr;                               // sort groups per chunk (tfp_scan.hip wide_bin_scan)
   int32_t* gb = nullptr;
   int64_t cap_groups = 0;

@@ -29,7 +29,6 @@
 #include <vector>
 
 #include "tfp_kernels.hpp"
-#include "tfp_bsearch.hpp"
 #include "tfp_math.hpp"
 
 namespace tfp {
@@ -822,13 +821,13 @@ __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* _
 
 // The directories, from the sorted frames: frame i of a window segment is the first frame of the
 // buckets after its predecessor's bucket up to its own (each bucket written once), the last frame
-// also fills the buckets after its own with se; the first writes the segment's constants (segk). Lanes write short runs themselves; a long run (a
+// also fills the buckets after its own with se. Lanes write short runs themselves; a long run (a
 // sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
 // buckets per step, so no lane loops over thousands of buckets alone.
 __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
                                      int segshift, const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
                                      const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
-                                     int32_t* __restrict__ dtab, int4* __restrict__ segk) {
+                                     int32_t* __restrict__ dtab) {
   constexpr int32_t kShort = 8;
   const int64_t n = *pn;
   const int lane = threadIdx.x & 63;
@@ -850,7 +849,6 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
         const int32_t l2min = L2s[sb], u2min = U2s[sb];
         const int shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
         const int32_t t0 = doff[ch * kKeyRange + skey];
-        if (i == sb) segk[ch * kKeyRange + skey] = make_int4(l2min, u2min, shf, t0);  // (wide_clips' constants)
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           const int64_t mn = h ? u2min : l2min;
@@ -890,10 +888,10 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
 // place in it; wide_bin_scan (a workgroup per chunk) scans the counts into each bin's first frame
 // and writes the segment table, the directory offsets, the used keys and the non-empty bins;
 // wide_bin_scatter moves the keys to their places; one wave sorts each bin in registers or LDS
-// and writes the sorted windows, queries and segment of each frame and the directory runs of its
-// window segment (wide_bin_sort, with wide_bin_scan's per-segment constants, segk).
+// and writes the sorted windows, queries and segment of each frame (wide_bin_sort); the
+// directories are filled from those with a per-segment constants table (wide_dir_fill_bins).
 // Chunk ch's kept frames occupy [cbeg[ch], cbeg[ch] + kept) of the sorted arrays; the rest of its
-// input range holds no frame of a segment (query 0), so the prefix counts run over the
+// input range holds no frame of a segment (query 0, segment -1), so the prefix counts run over the
 // whole range. A bin whose frames all share (segment, L2, d), or whose segment has no max2 window,
 // is not sorted (any order counts the same). Any other bin above kBinCap frames sets info[2],
 // which sends the speculative batch to the library sort (as a window width outside the key's delta
@@ -1023,18 +1021,17 @@ __global__ __launch_bounds__(1024) void wide_bin_hist_kernel(const int64_t* __re
 
 // One workgroup per chunk: the bin counts scanned into each bin's first frame (bstart, relative to
 // cbeg[ch]), the sort groups (gi4, gb: wide_bin_sort), the segment table, the directory offsets
-// (in segk; chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
-// the table's size per frame), each window segment's directory constants (segk: {min L2, min U2 =
-// min L2 + dbase, bucket shift over the L2 range + 7, directory offset}), the used keys, the
-// chunk's tail of non-frames, and cbeg.
+// (chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
+// the table's size per frame), the used keys, the chunk's
+// tail of non-frames, and cbeg.
 __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t qch,
                                                              int32_t nch, const uint32_t* __restrict__ segstat,
                                                              const int32_t* __restrict__ ghist, int32_t* __restrict__ bstart,
-                                                             int32_t* __restrict__ seg, int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
+                                                             int32_t* __restrict__ seg, int32_t* __restrict__ doff,
+                                                             int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
                                                              int32_t* __restrict__ cbeg, uint8_t* __restrict__ qis,
-                                                             int4* __restrict__ gi4,
-                                                             int32_t* __restrict__ gb, int32_t gcap, int64_t dbase,
-                                                             int4* __restrict__ segk) {
+                                                             int32_t* __restrict__ fseg, int4* __restrict__ gi4,
+                                                             int32_t* __restrict__ gb, int32_t gcap) {
   constexpr int NT = 1024, FPER = kNFine / NT;
   __shared__ int32_t base[kWideSegs], nbs[kWideSegs], shf[kWideSegs], ws[NT / 64];
   __shared__ uint32_t lmn[kWideSegs];
@@ -1069,7 +1066,7 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
   }
   __syncthreads();
   // segments: segment sk's bins [base, base + nb)
-  int32_t dv[2] = {0, 0}, ns[2] = {0, 0};
+  int32_t dv[2] = {0, 0};
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const int sk = 2 * t + j;
@@ -1080,7 +1077,7 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
         sg[0] = (int32_t)cb + b;
         sg[1] = (int32_t)cb + e;
         used[sk & (kKeyRange - 1)] = 1;
-        if (sk < kKeyRange) dv[j] = 2 << dir_log2(e - b), ns[j] = e - b;  // (the directory's entries)
+        if (sk < kKeyRange) dv[j] = 2 << dir_log2(e - b);  // (the directory's entries)
       }
     }
   }
@@ -1089,16 +1086,7 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
   (void)DT;
 #pragma unroll
   for (int j = 0; j < 2; j++) {
-    if (dv[j]) {
-      const int sk = 2 * t + j;
-      const int32_t o = (4 << kDirScale) * (int32_t)cb + dof;
-      const uint32_t* sst = segstat + ((int64_t)ch * kWideSegs + sk) * 3;
-      const uint32_t lo = sst[1], hi = sst[2];
-      const int32_t l2min = (int32_t)(lo ^ 0x80000000u);
-      // (U2 min beyond int32: such frames are out of range, info[1], and the batch is redone)
-      const int64_t u2min = min((int64_t)l2min + dbase, (int64_t)INT32_MAX);
-      segk[(int64_t)ch * kKeyRange + sk] = make_int4(l2min, (int32_t)u2min, dir_shift((int64_t)(hi - lo) + 7, dir_log2(ns[j])), o);
-    }
+    if (dv[j]) doff[(int64_t)ch * kKeyRange + 2 * t + j] = (4 << kDirScale) * (int32_t)cb + dof;
     dof += dv[j];
   }
   // the used keys, ascending
@@ -1135,8 +1123,11 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
     gi4[(int64_t)ch * gcap + gi] = make_int4(a, z, hs, hn);
     gb[(int64_t)ch * gcap + gi] = f;
   }
-  // the range's tail (no kept frame): query 0
-  for (int64_t i = cb + T + t; i < ce; i += NT) qis[i] = 0;
+  // the range's tail (no kept frame): query 0, no segment
+  for (int64_t i = cb + T + t; i < ce; i += NT) {
+    qis[i] = 0;
+    fseg[i] = -1;
+  }
 }
 
 // Each kept frame's key to its bin's place: kb[cbeg[ch] + bstart[ch][bin] + place].
@@ -1152,14 +1143,6 @@ __global__ void wide_bin_scatter_kernel(int64_t nf, int32_t qch, const int32_t* 
   }
 }
 
-__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int d) {
-  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
-  return ((unsigned long long)hi << 32) | lo;
-}
-__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int l) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
-  return ((unsigned long long)hi << 32) | lo;
-}
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((unsigned long long)hi << 32) | lo;
@@ -1209,66 +1192,20 @@ __device__ void bitonic_lds(unsigned long long* S, int N, int lane) {
       }
 }
 
-// A window segment's directory runs for one sorted frame (wide_dir_fill's rule): frame i at
-// absolute position pos writes the L2 and U2 buckets after its predecessor's (key kp; none at the
-// segment's first frame) up to its own, and the segment's last frame also the buckets after its
-// own (value se). sk4 = {l2min, u2min, shift, directory offset} of the segment (segk), sb / se its
-// bounds. A U2 bucket is (U2 - u2min) >> shift with u2min = l2min + dbase, i.e. (L2 - l2min + d)
-// >> shift: formed without dbase, it stays inside the directory even for a batch whose U2 leaves
-// int32 (info[1]: redone). Returns the runs in lo / hi / val / base (empty: lo > hi).
-__device__ __forceinline__ void dir_runs(int64_t pos, unsigned long long k, unsigned long long kp, int4 sk4, int32_t sb,
-                                         int32_t se, int32_t (&lo)[4], int32_t (&hi)[4], int32_t (&val)[4],
-                                         int32_t (&base)[4]) {
-  const int64_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), lp = (int32_t)((uint32_t)(kp >> 11) ^ 0x80000000u);
-  const int64_t dl = l2 - sk4.x, dp = lp - sk4.x;
-  const int lg = dir_log2(se - sb);
-  const int32_t nbk = 1 << lg;
-  const int32_t bi = (int32_t)(dl >> sk4.z), bu = (int32_t)((dl + (int64_t)((k >> 8) & 7)) >> sk4.z);
-  const bool first = pos == sb;
-  const int32_t bp = first ? -1 : (int32_t)(dp >> sk4.z), bq = first ? -1 : (int32_t)((dp + (int64_t)((kp >> 8) & 7)) >> sk4.z);
-  base[0] = base[2] = sk4.w;
-  base[1] = base[3] = sk4.w + nbk;
-  lo[0] = bp + 1, hi[0] = bi, val[0] = (int32_t)pos;
-  lo[1] = bq + 1, hi[1] = bu, val[1] = (int32_t)pos;
-  if (pos == se - 1) {
-    lo[2] = bi + 1, hi[2] = nbk - 1, val[2] = se;
-    lo[3] = bu + 1, hi[3] = nbk - 1, val[3] = se;
-  }
-}
-// Every lane's runs written: short ones by their lane, long ones (a sparse stretch of the value
-// range) by the whole wave, 64 buckets a step. (Call with every lane of the wave.)
-__device__ __forceinline__ void dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
-                                          const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
-  constexpr int32_t kShort = 8;
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int32_t len = hi[r] - lo[r] + 1;
-    if (len > 0 && len <= kShort)
-      for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
-    unsigned long long m = __ballot(len > kShort);
-    while (m) {
-      const int l = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64), o = __shfl(base[r], l, 64);
-      for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
-    }
-  }
-}
-
 // Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
 // (bins are monotone in the key, so sorting a run of whole bins sorts each of them): frames
 // [gi4[g].x, gi4[g].y) of the chunk, bins [gb[g], gb[g + 1]). One wave per group sorts it in
 // registers (up to 256 frames, 4 a lane) or LDS, and writes each sorted frame's L2, U2 (= L2 +
-// dbase + d) and query, and its window segment's directory runs (the frame before the
-// group: the greatest key of the group before it). A group above kBinCap frames (a crowded bin)
-// goes bin by bin: a bin whose frames all share (segment, L2, d), or whose segment has no max2
-// window, needs no order, and the waves of its 64-frame windows copy it; any other bin above
-// kBinCap frames sets info[2] (the batch is redone with the library sort).
+// dbase + d), query and segment (ch << 11 | segment key); a frame that starts or ends a window
+// segment writes the segment's first or last L2 / U2 (segc) for the directory fill. A group above
+// kBinCap frames (a crowded bin) goes bin by bin: a bin whose frames all share (segment, L2, d), or
+// whose segment has no max2 window, needs no order; any other bin above kBinCap frames sets
+// info[2].
 __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     const int32_t* __restrict__ bstart, const int4* __restrict__ gi4, const int32_t* __restrict__ gb, int32_t gcap,
     const int32_t* __restrict__ cbeg, const unsigned long long* __restrict__ kb, int64_t dbase,
-    const int32_t* __restrict__ seg, const int4* __restrict__ segk, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
-    uint8_t* __restrict__ qis, int32_t* __restrict__ dtab, int32_t* __restrict__ info) {
+    const int32_t* __restrict__ seg, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s, uint8_t* __restrict__ qis,
+    int32_t* __restrict__ fseg, int32_t* __restrict__ segc, int32_t* __restrict__ info) {
   __shared__ unsigned long long sk[kBinSortWaves][kBinCap];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ch = blockIdx.x;
@@ -1280,90 +1217,73 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   const int64_t cb = cbeg[ch];
   unsigned long long* S = sk[wv];
   auto sk_of = [](unsigned long long k) { return (int32_t)((k >> kPackSegShift) & (kWideSegs - 1)); };
-  // the key before the group in sorted order: the greatest of the bin before S0 (kb is unsorted:
-  // its greatest over a range holding that whole bin, whose keys exceed those of the bins before
-  // it). That bin is the previous group's last (at most kBinCap frames from S0 on) or, when that
-  // group is empty, the one holding frame 64 (g - 1); a bin above kBinCap frames is a crowd of one
-  // value or has no max2 window (no directory), so any of its keys will do. None at the chunk start
-  // (S0 > 0 has g > 0: group 0 starts at frame 0).
-  unsigned long long kprev = 0;
-  if (S0 > 0 && S0 < S1) {
-    const int4 gr = gi4[(int64_t)ch * gcap + g - 1];
-    const int32_t lo = gr.x < S0 ? max(gr.x, S0 - kBinCap) : gr.w > kBinCap ? S0 - 1 : gr.z;
-    for (int32_t p = lo + lane; p < S0; p += 64) {
-      const unsigned long long k = kb[cb + p];
-      kprev = k > kprev ? k : kprev;
+  // sorted frame p (chunk-relative) of key k; first / last: 1 when p starts / ends its segment, 2
+  // when it may (a neighbour outside the group: the segment table decides)
+  auto put = [&](int32_t p, unsigned long long k, int first, int last) {
+    const int64_t pos = cb + p;
+    const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
+    const int32_t u2 = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
+    L2s[pos] = l2;
+    U2s[pos] = u2;
+    qis[pos] = (uint8_t)(k & 255);
+    fseg[pos] = (ch << 11) | sgk;
+    if ((first || last) && sgk < kKeyRange) {
+      const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
+      int32_t* c4 = segc + ((int64_t)ch * kKeyRange + sgk) * 4;
+      if (first == 1 || (first == 2 && sg[0] == pos)) c4[0] = l2, c4[1] = u2;
+      if (last == 1 || (last == 2 && sg[1] == pos + 1)) c4[2] = l2, c4[3] = u2;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long y = shfl_xor_u64(kprev, o);
-      kprev = y > kprev ? y : kprev;
-    }
-  }
-  // sorted frame p (chunk-relative) of key k after key kp: its outputs and directory runs (valid:
-  // this lane has a frame; every lane calls)
-  auto put = [&](int32_t p, unsigned long long k, unsigned long long kp, bool valid) {
-    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
-    if (valid) {
-      const int64_t pos = cb + p;
-      const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
-      L2s[pos] = l2;
-      U2s[pos] = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
-      qis[pos] = (uint8_t)(k & 255);
-      if (sgk < kKeyRange) {
-        const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
-        dir_runs(pos, k, kp, segk[(int64_t)ch * kKeyRange + sgk], sg[0], sg[1], lo, hi, val, base);
-      }
-    }
-    dir_write(dtab, lo, hi, val, base, lane);
   };
-  // frames [b, b + n) sorted in LDS, written (kp: the key before them); returns their last key
-  auto sort_lds = [&](int32_t b, int32_t n, unsigned long long kp) {
+  // frames [b, b + n) sorted in LDS, written
+  auto sort_lds = [&](int32_t b, int32_t n) {
     const int N = n <= 1 ? 1 : 1 << (32 - __clz(n - 1));
     for (int p = lane; p < N; p += 64) S[p] = p < n ? kb[cb + b + p] : ~0ull;
     bitonic_lds(S, N, lane);
-    for (int p0 = 0; p0 < n; p0 += 64) {
-      const int p = p0 + lane;
-      put(b + p, p < n ? S[p] : 0ull, p == 0 ? kp : S[p > 0 ? p - 1 : 0], p < n);
+    for (int p = lane; p < n; p += 64) {
+      const unsigned long long k = S[p];
+      put(b + p, k, p == 0 ? 2 : sk_of(S[p - 1]) != sk_of(k), p == n - 1 ? 2 : sk_of(S[p + 1]) != sk_of(k));
     }
-    return S[n - 1];
   };
-  // frames [p0, p1) of big bin [b, b + nb), unsorted (kp: the key before the bin): a frame whose
-  // (segment, L2, d) differs from the bin's first in a window segment sends the batch to the
-  // library sort
-  auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1, unsigned long long kp) {
+  // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
+  // batch is redone): each wave copies and checks its own, the wave of the bin's group those before
+  // the bin's first multiple of 64
+  auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1) {
+    // frames [p0, p1) of big bin [b, b + nb), unsorted: a frame whose (segment, L2, d) differs from
+    // the bin's first in a window segment sends the batch to the library sort
     const unsigned long long k0 = kb[cb + b];
     bool odd = false;
-    for (int32_t q0 = p0; q0 < p1; q0 += 64) {
-      const int32_t p = q0 + lane;
-      const unsigned long long k = p < p1 ? kb[cb + p] : k0;
-      put(p, k, p == b ? kp : k0, p < p1);
+    for (int32_t p = p0 + lane; p < p1; p += 64) {
+      const unsigned long long k = kb[cb + p];
+      put(p, k, p == b ? 2 : 0, p == b + nb - 1 ? 2 : 0);
       odd = odd || ((k >> 8) != (k0 >> 8) && sk_of(k0) < kKeyRange);
     }
     if (__ballot(odd) && lane == 0) atomicAdd(&info[2], 1);
   };
-  // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
-  // batch is redone): each wave copies and checks its own (a bin starting at 64 g is this group's
-  // first: its predecessor is kprev), the wave of the bin's group those before the bin's first
-  // multiple of 64
-  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w), kprev);
+  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w));
   const int32_t n = S1 - S0;
   if (n <= 0) return;
-  // n <= 64 R: R keys a lane, sorted in registers; each frame's predecessor through the lanes
+  // n <= 64 R: R keys a lane, sorted in registers; each frame's neighbours through the lanes
   auto sort_regs = [&](auto rr) {
     constexpr int R = decltype(rr)::value;
     unsigned long long v[R];
 #pragma unroll
     for (int r = 0; r < R; r++) v[r] = 64 * r + lane < n ? kb[cb + S0 + 64 * r + lane] : ~0ull;
     bitonic_regs<R>(v, lane);
-    unsigned long long pv[R];
+    int32_t sg[R], prev[R], next[R];
+#pragma unroll
+    for (int r = 0; r < R; r++) sg[r] = sk_of(v[r]);
 #pragma unroll
     for (int r = 0; r < R; r++) {  // (every lane: the shuffles read whole rows)
-      const unsigned long long up = shfl_up_u64(v[r], 1), last = shfl_u64(v[r > 0 ? r - 1 : 0], 63);
-      pv[r] = lane ? up : r ? last : kprev;
+      const int32_t up = __shfl_up(sg[r], 1, 64), dn = __shfl_down(sg[r], 1, 64);
+      const int32_t pl = __shfl(sg[r > 0 ? r - 1 : 0], 63, 64), nf = __shfl(sg[r + 1 < R ? r + 1 : r], 0, 64);
+      prev[r] = lane ? up : r ? pl : -1;
+      next[r] = lane < 63 ? dn : r + 1 < R ? nf : -1;
     }
 #pragma unroll
-    for (int r = 0; r < R; r++) put(S0 + 64 * r + lane, v[r], pv[r], 64 * r + lane < n);
+    for (int r = 0; r < R; r++) {
+      const int32_t i = 64 * r + lane;
+      if (i < n) put(S0 + i, v[r], i == 0 ? 2 : prev[r] != sg[r], i == n - 1 ? 2 : next[r] != sg[r]);
+    }
   };
   if (n <= 64) {
     sort_regs(std::integral_constant<int, 1>{});
@@ -1378,11 +1298,10 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     return;
   }
   if (n <= kBinCap) {
-    (void)sort_lds(S0, n, kprev);
+    sort_lds(S0, n);
     return;
   }
   // a crowded group: bin by bin (the bins' bounds 64 at a time)
-  unsigned long long klast = kprev;
   const int32_t fa = gb[(int64_t)ch * gcap + g], fz = gb[(int64_t)ch * gcap + g + 1];
   for (int32_t f0 = fa; f0 < fz; f0 += 64) {
     const int32_t bl = f0 + lane < fz ? bs[f0 + lane] : 0, nl = f0 + lane < fz ? bs[f0 + lane + 1] - bl : 0;
@@ -1390,14 +1309,67 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
       const int sl = __ffsll((long long)mb) - 1;
       const int32_t b = __builtin_amdgcn_readlane(bl, sl), nb = __builtin_amdgcn_readlane(nl, sl);
       if (nb <= kBinCap) {
-        klast = sort_lds(b, nb, klast);
+        sort_lds(b, nb);
         continue;
       }
       // frames that all share (segment, L2, d) need no order (a crowd of equal values: the silence
       // floor), nor do those of a segment without a max2 window: the waves of the bin's 64-frame
       // windows copy and check them, this one the frames before the bin's first multiple of 64
-      copy_big(b, nb, b, min(b + nb, (b + kGroup - 1) / kGroup * kGroup), klast);
-      klast = kb[cb + b + nb - 1];  // (a crowd of one value: any of its keys)
+      copy_big(b, nb, b, min(b + nb, (b + kGroup - 1) / kGroup * kGroup));
+    }
+  }
+}
+
+// wide_dir_fill over the bin-sorted frames: the segment of frame i from fseg, its constants from
+// the segment table, segc and doff (loads that depend on fseg only). Nothing after an overflow
+// (info[2] > 0: a bin was left unsorted, its frames without fseg; the batch is redone).
+__global__ void wide_dir_fill_bins_kernel(int64_t n, const int32_t* __restrict__ fseg, const int32_t* __restrict__ seg,
+                                          const int32_t* __restrict__ segc, const int32_t* __restrict__ L2s,
+                                          const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
+                                          int32_t* __restrict__ dtab, const int32_t* __restrict__ info) {
+  constexpr int32_t kShort = 8;
+  if (info[2] > 0) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t i0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; i0 < n; i0 += nw * 64) {
+    const int64_t i = i0 + lane;
+    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
+    if (i < n) {
+      const int32_t fs = fseg[i];
+      const int32_t xl = L2s[i], xu = U2s[i], xlp = i > 0 ? L2s[i - 1] : 0, xup = i > 0 ? U2s[i - 1] : 0;
+      if (fs >= 0 && (fs & kKeyRange) == 0) {
+        const int64_t ch = fs >> 11, key = fs & (kKeyRange - 1);
+        const int32_t* sg = seg + (ch * kWideSegs + key) * 2;
+        const int32_t* c4 = segc + (ch * kKeyRange + key) * 4;
+        const int32_t sb = sg[0], se = sg[1], t0 = doff[ch * kKeyRange + key];
+        const int32_t l2min = c4[0], u2min = c4[1];
+        const int lg = dir_log2(se - sb);
+        const int32_t nbk = 1 << lg;
+        const int shf = dir_shift(max((int64_t)c4[2] - l2min, (int64_t)c4[3] - u2min), lg);
+#pragma unroll
+        for (int hh = 0; hh < 2; hh++) {
+          const int64_t mn = hh ? u2min : l2min;
+          const int32_t bi = (int32_t)(((int64_t)(hh ? xu : xl) - mn) >> shf);
+          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)(hh ? xup : xlp) - mn) >> shf);
+          base[hh] = base[2 + hh] = t0 + hh * nbk;
+          lo[hh] = bp + 1, hi[hh] = bi, val[hh] = (int32_t)i;
+          if (i == se - 1) lo[2 + hh] = bi + 1, hi[2 + hh] = nbk - 1, val[2 + hh] = se;
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int32_t len = hi[r] - lo[r] + 1;
+      if (len > 0 && len <= kShort)
+        for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
+      unsigned long long m = __ballot(len > kShort);
+      while (m) {
+        const int l = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64),
+                      o = __shfl(base[r], l, 64);
+        for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
+      }
     }
   }
 }
@@ -1409,11 +1381,6 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
 // of two 16-bit counts) among 64 frames by reading their queries out of the lanes (no per-frame
 // memory dependency).
 constexpr int kPortions = 256;
-#ifndef TFP_PSTEP
-#define TFP_PSTEP 4
-#endif
-constexpr int kPStep = TFP_PSTEP;  // frames per prefix-count row (1 or 4)
-static_assert(kPStep == 1 || kPStep == 4, "one row a frame, or a 4-byte word of queries a row");
 __device__ __forceinline__ void portion_range(const int32_t* cbeg, int ch, int p, int32_t& b, int32_t& r0, int32_t& r1) {
   b = cbeg[ch];
   const int32_t n = cbeg[ch + 1] - b;
@@ -1465,9 +1432,6 @@ __global__ __launch_bounds__(1024) void wide_pscan_kernel(uint32_t* __restrict__
 #pragma unroll
   for (int j = 0; j < 16; j++) t[64 * j] = base + v[j];
 }
-// The rows are checkpoints: frame i's row only when i % kPStep == kPStep - 1, at P[i / kPStep] (a
-// fourth of the bytes written; wide_clips adds the up to kPStep - 1 frames after the checkpoint
-// before a position from their queries, prefix_at).
 template <int QPL>
 __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg, const uint8_t* __restrict__ qis,
                                                            const uint32_t* __restrict__ ptot, uint32_t* __restrict__ P) {
@@ -1477,39 +1441,32 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   uint32_t run = ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane];
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : kPadQ;
-    const int32_t bi = b + i;  // (global frame of j = 0)
+    uint32_t* row = P + ((int64_t)b + i) * kWideW + lane;
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
       run += prefix_inc<QPL>(__builtin_amdgcn_readlane(x, j), lane);
-      if (j < m && ((bi + j) & (kPStep - 1)) == kPStep - 1) P[(int64_t)((bi + j) / kPStep) * kWideW + lane] = run;
+      if (j < m) row[(int64_t)j * kWideW] = run;
     }
   }
 }
-// In-chunk prefix count at frame e (>= cb, the chunk's first frame) from the checkpoint rows: the
-// row at e itself, or the last checkpoint before e in the chunk (none: 0) plus the increments of
-// the frames after it up to e, read from their queries (one aligned 4-byte load; qis is padded).
-// e is wave-uniform (every caller's is a shuffled or read-lane value): as a scalar, the queries'
-// word is a scalar load and only the per-lane compare and add take vector registers.
-template <int QPL>
-__device__ __forceinline__ uint32_t prefix_at(const uint32_t* __restrict__ P, const uint8_t* __restrict__ qis, int32_t cb,
-                                              int32_t e, int lane) {
-  if constexpr (kPStep == 1) {
-    return P[(int64_t)e * kWideW + lane];
-  } else {
-    e = __builtin_amdgcn_readfirstlane(e);
-    const int32_t g = e / kPStep, f0 = g * kPStep;
-    if (e == f0 + kPStep - 1) return P[(int64_t)g * kWideW + lane];
-    uint32_t v = f0 - 1 >= cb ? P[(int64_t)(g - 1) * kWideW + lane] : 0u;
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(qis + f0);
-#pragma unroll
-    for (int j = 0; j < kPStep - 1; j++)
-      if (f0 + j <= e && f0 + j >= cb) v += prefix_inc<QPL>((int32_t)((w >> (8 * j)) & 255u), lane);
-    return v;
-  }
-}
 
-// lb32 / ub32: tfp_bsearch.hpp (both ends read with the first probe)
+__device__ __forceinline__ int32_t lb32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] >= v
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] > v
+  int32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
 
 // ---- clip-major sweep ------------------------------------------------------------------------
 // Work items are (chunk, key, clip group). A wave takes windows of kWin consecutive clip columns of
@@ -1550,7 +1507,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
-    const uint8_t* __restrict__ qis, const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
+    const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
     unsigned long long* __restrict__ part, const int32_t* __restrict__ stop) {
   // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
   // so the sweep reads nothing (the batch is redone; its maxima are not used)
@@ -1594,7 +1551,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
   };
   auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
-    cnt += prefix_at<QPL>(P, qis, cb, b, lane) - (a > sb ? prefix_at<QPL>(P, qis, cb, a - 1, lane) : base);
+    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
   };
   // The chunk's used keys' segment constants, one key per lane, loaded once per wave instead of
   // once per window and key (three dependent loads ahead of every key's groups): the window loop
@@ -1608,11 +1565,11 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     kfb = sg[2 * (kq | kKeyRange)];
     kfe = sg[2 * (kq | kKeyRange) + 1];
     if (kse > ksb) {
-      const int4 c4 = segk[(int64_t)ch * kKeyRange + kq];
-      kl2 = c4.x;
-      ku2 = c4.y;
-      kshf = c4.z;
-      ktoff = c4.w;
+      const int lg = dir_log2(kse - ksb);
+      kl2 = L2s[ksb];
+      ku2 = U2s[ksb];
+      kshf = dir_shift(max((int64_t)L2s[kse - 1] - kl2, (int64_t)U2s[kse - 1] - ku2), lg);
+      ktoff = doff[(int64_t)ch * kKeyRange + kq];
     }
   }
   for (int32_t w = w0; w < w1; w++) {
@@ -1648,8 +1605,8 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           fb = sg[2 * (k | kKeyRange)];
           fe = sg[2 * (k | kKeyRange) + 1];
         }
-        base = se > sb && sb > cb ? prefix_at<QPL>(P, qis, cb, sb - 1, lane) : 0u;
-        fcnt = fe > fb ? prefix_at<QPL>(P, qis, cb, fe - 1, lane) - (fb > cb ? prefix_at<QPL>(P, qis, cb, fb - 1, lane) : 0u) : 0u;
+        base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
+        fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
         if (se <= sb) {  // no frame of the key has a max2 window: every group scores the rest
           for (; g < g1; g++) add((int32_t)(cv.g_key[g] & kColMask), fcnt);
           continue;
@@ -1661,12 +1618,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           shf = __builtin_amdgcn_readlane(kshf, sl);
           TL = dtab + __builtin_amdgcn_readlane(ktoff, sl);
         } else {
-          nbk = 1 << dir_log2(se - sb);
-          const int4 c4 = segk[(int64_t)ch * kKeyRange + k];
-          l2min = c4.x;
-          u2min = c4.y;
-          shf = c4.z;
-          TL = dtab + c4.w;
+          const int lg = dir_log2(se - sb);
+          nbk = 1 << lg;
+          l2min = L2s[sb];
+          u2min = U2s[sb];
+          shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
+          TL = dtab + doff[(int64_t)ch * kKeyRange + k];
         }
         // A batch of consecutive groups whose items fit the 64 lanes: lane j holds group j's item
         // range [pj0, pj1) relative to the first item pb0.
@@ -1823,11 +1780,10 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)cbeg, (void*)info, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part,
-                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)bstart, (void*)segk, (void*)segstat,
+                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)bstart, (void*)segc, (void*)segstat,
                   (void*)ghist})
     if (p) (void)hipFree(p);
-  bstart = ghist = nullptr;
-  segk = nullptr;
+  bstart = segc = ghist = nullptr;
   segstat = nullptr;
   for (void* q : {(void*)gi4, (void*)gb})
     if (q) (void)hipFree(q);
@@ -1868,7 +1824,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
     cap_nf = 0;
     if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
         (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
-        (e = dmalloc(&qis, nf + 16)) || (e = dmalloc(&P, (nf / kPStep + 2) * kWideW)) || (e = dmalloc(&fq, nf)))
+        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideW)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
     size_t t3 = 0;
@@ -1882,11 +1838,10 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
   }
   if (nch > cap_nch) {
     for (void* p : {(void*)seg, (void*)cbeg, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part, dtmp,
-                    (void*)bstart, (void*)segk, (void*)segstat, (void*)ghist})
+                    (void*)bstart, (void*)segc, (void*)segstat, (void*)ghist})
       if (p) (void)hipFree(p);
     seg = cbeg = doff = ukeys = nuk = nullptr;
-    bstart = ghist = nullptr;
-    segk = nullptr;
+    bstart = segc = ghist = nullptr;
     segstat = nullptr;
     ptot = nullptr;
     part = nullptr;
@@ -1898,7 +1853,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
         (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)) ||  // up to 2 kPartWaves waves per chunk, either chunk size
         (e = dmalloc(&bstart, nch * (kNFine + 1))) ||
         (e = dmalloc(&segstat, nch * kWideSegs * 3)) || (e = dmalloc(&ghist, nch * kNFine)) ||
-        (e = dmalloc(&segk, nch * kKeyRange)))
+        (e = dmalloc(&segc, nch * kKeyRange * 4)))
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1972,14 +1927,14 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       ws->cap_groups = nch * gcap;
     }
     hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
-                       ws->ghist, ws->bstart, ws->seg, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->gi4, ws->gb,
-                       (int32_t)gcap, dbase, ws->segk);
+                       ws->ghist, ws->bstart, ws->seg, ws->doff, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->va, ws->gi4, ws->gb,
+                       (int32_t)gcap);
     hipLaunchKernelGGL(wide_bin_scatter_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, qch, ws->fq, ws->ka,
                        reinterpret_cast<const uint32_t*>(ws->vb), ws->cbeg,
                        ws->bstart, ws->kb);
     hipLaunchKernelGGL(wide_bin_sort_kernel, dim3((unsigned)nch, (unsigned)((gcap + kBinSortWaves - 1) / kBinSortWaves)),
                        dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gi4, ws->gb, (int32_t)gcap, ws->cbeg, ws->kb, dbase, ws->seg,
-                       ws->segk, ws->L2s, ws->U2s, ws->qis, ws->dtab, ws->info);
+                       ws->L2s, ws->U2s, ws->qis, ws->va, ws->segc, ws->info);
     if (ws->debug_bins) {  // (TFP_DEBUG_BINS: the bin sort's counts of the first chunk, on stderr)
       std::vector<int32_t> bs(kNFine + 1);
       std::vector<int4> g(gcap);
@@ -2000,6 +1955,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
               bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
     }
+    hipLaunchKernelGGL(wide_dir_fill_bins_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, ws->va, ws->seg, ws->segc, ws->L2s,
+                       ws->U2s, ws->doff, ws->dtab, ws->info);
   } else {
     size_t tb = ws->tmp_bytes;
     if (packed) {
@@ -2042,7 +1999,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
     (void)nd;
     hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
     hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb,
-                       packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab, ws->segk);
+                       packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab);
   }
   if (qch == 256) {
     hipLaunchKernelGGL(wide_pcount_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
@@ -2091,14 +2048,14 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (!ws->ukeys_ready) hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
+                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   }

@@ -281,8 +281,8 @@ def test_sweep_8bit_count_field_edge(oracle, tfp_lib, tol):
 
 @pytest.mark.parametrize("tol", [0.001, 0.1])
 def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
-    """The sweep's bin sort (tfp_scan.hip wide_bin_hist .. wide_bin_sort, which also fills the
-    directories) on bins of every size class: 600 queries (three 256-query chunks, the last partly filled) whose max2 values mix a wide
+    """The sweep's bin sort (tfp_scan.hip wide_bins .. wide_dir_fill_bins) on bins of every size
+    class: 600 queries (three 256-query chunks, the last partly filled) whose max2 values mix a wide
     spread (bins of a few frames: the in-register sort), a 4 dB cluster (bins of hundreds: the LDS
     sort), repeated values (equal keys), frames whose max2 condition an ignore filter drops (their
     segment is not sorted), NULL values and keys over the ignore filter (not kept: the chunk's tail); then the same queries with a
