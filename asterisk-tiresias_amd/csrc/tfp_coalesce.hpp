@@ -187,9 +187,11 @@ struct Combined {
 
 // A coalesced batch through run(ptrs, lens, nq, f32, sr, P, out) -> rc (the handle's uncoalesced
 // search); last_error() reads the message of run's failure on this (the leader's) thread. When the
-// combined batch fails (a device allocation sized for all of it, or one caller's query that fails
-// on its own), every request is run again alone, so only a request that fails by itself reports an
-// error, with its own message, and the others get their results.
+// combined batch fails for want of memory (TFP_E_NOMEM: a device or host allocation sized for all
+// of it, or one caller's query whose own allocation fails), every request is run again alone, so
+// only a request that fails by itself reports an error, with its own message, and the others get
+// their results. Any other failure (a kernel fault, a launch error: a device that is now broken) is
+// not re-run N more times: every request of the batch gets the leader's code and message.
 template <class Run, class LastError>
 void exec_batch(std::vector<SearchReq*>& batch, Run&& run, LastError&& last_error) {
   auto alone = [&](SearchReq* b) {
@@ -202,11 +204,20 @@ void exec_batch(std::vector<SearchReq*>& batch, Run&& run, LastError&& last_erro
   }
   Combined c(batch);
   const SearchReq* b0 = batch[0];
-  if (run(c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P, c.res.data()) == TFP_OK) {
+  const int rc = run(c.ptrs.data(), c.lens.data(), (int32_t)c.lens.size(), b0->f32, b0->sr, &b0->P, c.res.data());
+  if (rc == TFP_OK) {
     c.scatter(batch);
     return;
   }
-  for (SearchReq* b : batch) alone(b);
+  if (rc == TFP_E_NOMEM) {
+    for (SearchReq* b : batch) alone(b);
+    return;
+  }
+  const std::string msg = last_error();
+  for (SearchReq* b : batch) {
+    b->rc = rc;
+    b->err = msg;
+  }
 }
 
 }  // namespace tfp

@@ -67,6 +67,15 @@ struct TolSlot {
   uint64_t version = 0, used = 0;
 };
 
+// A tolerance's clip-set cache kept beside the active one (tfp_engine::cell_lru, round 6): callers
+// alternating coefs = 2 tolerances do not rebuild it per call. Valid while the index is at `version`.
+struct CellSlot {
+  CellCache c;
+  double tol = 0.0;
+  bool has = false;
+  uint64_t version = 0, used = 0;
+};
+
 // Pinned host staging (one H2D copy per small call instead of one per array).
 struct HostBuf {
   void* p = nullptr;
@@ -120,6 +129,7 @@ HostAllocs& host_allocs() {
 
 struct tfp_plan {
   int32_t nclips = 0, ntiles = 0, sample_rate = 0, tile_frames = 0;
+  bool long_clip = false;  // a clip of >= kDirectMaxSamples: the generic kernel
   int64_t nsamples = 0, nframes = 0;
   std::vector<int64_t> soff, foff;
   std::vector<int32_t> toff, tclip;
@@ -160,9 +170,15 @@ struct tfp_engine {
   int64_t nrows = 0;       // rows that can match (live clip, non-NULL max1)
   int32_t ncols = 0;       // live clips
   std::vector<int32_t> col_clip;                 // column (uuid rank) -> clip id
-  std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> column (with an override)
+  std::unordered_map<int32_t, int32_t> key_col;  // tie-break key -> main column (with an override)
+  std::unordered_map<int32_t, int32_t> key_col_delta;  // ... -> the index delta's columns
   bool key_identity = true;                      // no override: key == column
   std::vector<int32_t> tiebreak_override;        // clip id -> key (empty = uuid rank)
+  // with an override: key_col / the device tie keys of the main columns no longer match it (a full
+  // tfp_index_set_tiebreak, or new keys for clips of the last build); tfp_index_update_tiebreak of
+  // clips added since leaves them standing, so a delta update costs the delta's clips only
+  bool ovr_main_stale = true;
+  int64_t n_delta_main_keys = 0;  // delta updates that re-sent every main column's key (tests)
 
   // scratch
   DevBuf sort_tmp, keys_a, keys_b, vals_a, vals_b, cnt;
@@ -209,7 +225,23 @@ struct tfp_engine {
   WideScratch wide;         // the general path's sweep by groups
   double wide_min_tol = 0;  // TFP_WIDE_MIN_TOL: general-path batches below it take the clip-set cells (tests)
   double cell_tol = 0.0;
-  bool cell_fresh = false;
+  bool cell_fresh = false;  // cells holds the cache of cell_tol at index version cell_version
+  uint64_t cell_version = 0;
+  // other tolerances' clip-set caches (round 6), least recently used out, valid at their version
+  static constexpr int kCellSlots = 3;
+  CellSlot cell_lru[kCellSlots];
+  int64_t n_cell_builds = 0, n_cell_hits = 0, n_cell_from_order = 0;
+  // the coefs = 2 sweep's sort path per batch (tfp_sweep_stats): the bin sort's speculative pass
+  // stood, the library sort ran, a speculative pass was redone; crowd bins the bin sort copied
+  int64_t n_sweep_bins = 0, n_sweep_lib = 0, n_sweep_redo = 0, n_sweep_crowd = 0;
+  // the index rows in clip order (tfp_kernels.hpp), the source of the caches at tolerances up to
+  // kOrderMaxTol: built on the first search that needs it, then carried through every merge
+  DevBuf o_key, o_m1, o_key_b, o_m1_b, o_newcol;
+  int64_t o_rows = 0;
+  bool o_valid = false;
+  int64_t n_order_builds = 0, n_order_merges = 0;
+  CacheBuf o_sort_tmp;
+  OrderScratch o_merge;
   // scan scratch: stamp / score / touched nq x ncols int32 each, tcnt nq int32; kept all-zero
   // by the scan kernels themselves
   DevBuf touched, tcnt;
@@ -268,7 +300,9 @@ int fail(tfp_engine* e, int code, const char* fmt, ...) {
 #define HIPCHK(e, expr)                                                                          \
   do {                                                                                           \
     hipError_t _st = (expr);                                                                     \
-    if (_st != hipSuccess) return fail((e), TFP_E_HIP, "%s: %s", #expr, hipGetErrorString(_st)); \
+    if (_st != hipSuccess)                                                                       \
+      return fail((e), _st == hipErrorOutOfMemory ? TFP_E_NOMEM : TFP_E_HIP, "%s: %s", #expr,   \
+                  hipGetErrorString(_st));                                                       \
   } while (0)
 
 // The device copy of the glibc log correction table (frame values == glibc's 10*log10|c|).
@@ -375,6 +409,8 @@ int fingerprint_host(tfp_engine* e, const void* const* ptrs, const int64_t* lens
   std::vector<int32_t> toff(nclips + 1, 0), tclip;
   // small batches at 8 kHz: 4-frame wave tiles (more waves, fewer passes per wave)
   bool small = false;
+  for (int32_t c = 0; c < nclips; c++)
+    if (lens[c] >= kDirectMaxSamples) fx = false;  // (the 8 kHz kernel's 32-bit buffer offsets)
   if (fx && !f32) {
     int64_t nf16 = 0;
     for (int32_t c = 0; c < nclips; c++) nf16 += (tfp_frame_count(lens[c]) + 15) / 16;
@@ -809,6 +845,41 @@ int merge_index(tfp_engine* e, const std::vector<int32_t>& rank, const MergeBrea
   std::swap(e->m2s.p, e->m2s_b.p); std::swap(e->m2s.bytes, e->m2s_b.bytes);
   std::swap(e->cols.p, e->cols_b.p); std::swap(e->cols.bytes, e->cols_b.bytes);
   e->nrows = kept + valid;
+  // The clip order (when built) through the same update: its old rows renumbered, the new rows
+  // inserted (tfp_index.hpp). Best effort: on failure it is rebuilt when next needed.
+  if (e->o_valid) {
+    e->o_valid = false;
+    auto by_uuid = [&](int32_t a, int32_t c) { return e->clips[a].uuid < e->clips[c].uuid; };
+    std::vector<int32_t> add;
+    for (int32_t i = (int32_t)e->built_clips; i < (int32_t)e->clips.size(); i++)
+      if (e->clips[i].alive) add.push_back(i);
+    std::sort(add.begin(), add.end(), by_uuid);
+    const int32_t D = (int32_t)add.size();
+    std::vector<int32_t> nca(2 * (size_t)std::max(D, 1));  // new columns, then their insertion points among the old columns
+    for (int32_t j = 0; j < D; j++) {
+      nca[j] = rank[add[j]];
+      nca[D + j] = fast_brk ? rank[add[j]] - j
+                            : (int32_t)(std::lower_bound(e->col_clip.begin(), e->col_clip.end(), add[j], by_uuid) - e->col_clip.begin());
+    }
+    int64_t orows = 0;
+    const size_t on = (size_t)std::max<int64_t>(e->o_rows + valid, 1);
+    if ((!D || upload(e, e->o_newcol, nca.data(), sizeof(int32_t) * nca.size()) == TFP_OK) &&
+        e->o_key_b.reserve_grow(sizeof(unsigned long long) * on) == hipSuccess &&
+        e->o_m1_b.reserve_grow(sizeof(int32_t) * on) == hipSuccess &&
+        launch_order_merge(e->o_key.as<unsigned long long>(), e->o_m1.as<int32_t>(), e->o_rows, e->remap.as<int32_t>(), removed,
+                           brk, e->keys_b.as<int32_t>(), e->vals_a.as<int32_t>(), e->keys_a.as<int32_t>(), valid,
+                           e->o_newcol.as<int32_t>(), e->o_newcol.as<int32_t>() + D, D, &e->merge, &e->o_merge,
+                           e->o_key_b.as<unsigned long long>(), e->o_m1_b.as<int32_t>(), &orows, e->stream) == hipSuccess &&
+        hipStreamSynchronize(e->stream) == hipSuccess && orows == e->nrows) {  // (nca is read by then)
+      e->o_key.swap_with(e->o_key_b);
+      e->o_m1.swap_with(e->o_m1_b);
+      e->o_rows = orows;
+      e->o_valid = true;
+      e->n_order_merges++;
+    } else {
+      (void)hipGetLastError();
+    }
+  }
   // The small path's key ranges and bitsets, carried to the merged index at their tolerance
   // instead of rebuilt from every box row (tfp_index.hpp): the ranges are searched again, every
   // surviving column's bits move to its new column (removed clips' and an index delta's columns
@@ -918,6 +989,7 @@ int rebuild(tfp_engine* e) {
     e->n_merges++;
   } else {
     e->nrows = 0;
+    e->o_valid = false;  // (the clip order is rebuilt from the new index when next needed)
     if ((rc = full_index(e))) return rc;
     e->n_full_builds++;
   }
@@ -928,6 +1000,8 @@ int rebuild(tfp_engine* e) {
   e->delta_col0 = e->ncols;
   e->delta_rows = 0;
   e->key_col = std::move(key_col);
+  e->key_col_delta.clear();
+  e->ovr_main_stale = !ovr;  // (with an override: its keys for these columns are on the device now)
   e->key_identity = !ovr;
   e->built = true;
   e->built_clips = e->clips.size();
@@ -1083,23 +1157,50 @@ int delta_update(tfp_engine* e) {
     at[j] = (int32_t)(std::lower_bound(e->col_clip.begin(), e->col_clip.end(), add[j], by_uuid) - e->col_clip.begin());
   const int32_t col0 = D ? (Cm + 1023) / 1024 * 1024 : Cm;
   const int32_t ncols = D ? col0 + tfp_engine::kDeltaMaxClips : Cm;
-  // tie keys (and the key -> column map with an override)
+  // tie keys (and the key -> column maps with an override)
   const bool ovr = !e->tiebreak_override.empty();
-  std::unordered_map<int32_t, int32_t> key_col;
+  const void* tk_before = e->tiekey.p;
   HIPCHK(e, e->tiekey.reserve_grow(sizeof(int32_t) * std::max(ncols, 1)));
+  std::unordered_map<int32_t, int32_t> key_col_delta;
+  std::vector<int32_t> tk;  // host staging of the keys uploaded (kept until the sync below)
   if (ovr) {
-    std::vector<int32_t> tk(std::max(ncols, 1), 0);
-    key_col.reserve(Cm + D);
-    for (int32_t c = 0; c < Cm + D; c++) {
-      const int32_t col = c < Cm ? c : col0 + (c - Cm);
-      const int32_t clip = c < Cm ? e->col_clip[c] : add[c - Cm];
+    auto key_of_clip = [&](int32_t clip, int32_t* k) -> int {
       if ((size_t)clip >= e->tiebreak_override.size())
         return fail(e, TFP_E_ARG, "clip %s was added after tfp_index_set_tiebreak: set the tie-break keys again",
                     e->clips[clip].uuid.c_str());
-      tk[col] = e->tiebreak_override[clip];
-      if (!key_col.emplace(tk[col], col).second) return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", tk[col]);
+      *k = e->tiebreak_override[clip];
+      return TFP_OK;
+    };
+    // the main columns' keys: only when the override changed for them (or their device copy was
+    // lost to a larger buffer); otherwise the delta's clips alone (O(new clips), round 6)
+    const bool main_up = e->ovr_main_stale || e->tiekey.p != tk_before;
+    e->n_delta_main_keys += main_up;
+    if (e->ovr_main_stale) {
+      std::unordered_map<int32_t, int32_t> key_col;
+      key_col.reserve(Cm);
+      for (int32_t c = 0; c < Cm; c++) {
+        int32_t k;
+        if (int rc = key_of_clip(e->col_clip[c], &k)) return rc;
+        if (!key_col.emplace(k, c).second) return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
+      }
+      e->key_col = std::move(key_col);
     }
-    HIPCHK(e, hipMemcpyAsync(e->tiekey.p, tk.data(), sizeof(int32_t) * ncols, hipMemcpyHostToDevice, s));
+    tk.assign(main_up ? std::max(ncols, 1) : std::max(D, 1), 0);
+    key_col_delta.reserve(D);
+    for (int32_t j = 0; j < D; j++) {
+      int32_t k;
+      if (int rc = key_of_clip(add[j], &k)) return rc;
+      if (e->key_col.count(k) || !key_col_delta.emplace(k, col0 + j).second)
+        return fail(e, TFP_E_ARG, "tie-break key %d given to two live clips", k);
+      tk[main_up ? col0 + j : j] = k;
+    }
+    if (main_up) {
+      for (int32_t c = 0; c < Cm; c++) tk[c] = e->tiebreak_override[e->col_clip[c]];
+      HIPCHK(e, hipMemcpyAsync(e->tiekey.p, tk.data(), sizeof(int32_t) * ncols, hipMemcpyHostToDevice, s));
+    } else if (D) {
+      HIPCHK(e, hipMemcpyAsync(e->tiekey.as<int32_t>() + col0, tk.data(), sizeof(int32_t) * D, hipMemcpyHostToDevice, s));
+    }
+    e->ovr_main_stale = false;
     e->tiekey_ident = -1;
   } else {
     HIPCHK(e, e->d_delta_at.reserve(sizeof(int32_t) * std::max(D, 1)));
@@ -1120,7 +1221,7 @@ int delta_update(tfp_engine* e) {
   e->delta_col0 = col0;
   e->delta_rows = rows;
   e->ncols = ncols;
-  e->key_col = std::move(key_col);
+  e->key_col_delta = std::move(key_col_delta);
   e->key_identity = !ovr;
   // key bits: the first delta after a build widens the rows (the delta's columns start at a
   // multiple of 1024): the main columns' words move to the wider rows in one 2-D device copy
@@ -1169,25 +1270,88 @@ int consolidate(tfp_engine* e) {
   return rc;
 }
 
-// The general path's clip-set cache at tolerance tole (after ensure_ranges at tole).
+// The clip order of the current index (tfp_kernels.hpp), built when first needed: the index rows'
+// keys (nearest-integer key, column, m2) radix-sorted once; merge_index carries it afterwards.
+int ensure_order(tfp_engine* e, hipStream_t s) {
+  if (e->o_valid) return TFP_OK;
+  const int64_t R = e->nrows;
+  if (R >= INT32_MAX) return fail(e, TFP_E_CAPACITY, "clip order: %lld rows", (long long)R);
+  const size_t n = (size_t)std::max<int64_t>(R, 1);
+  HIPCHK(e, e->o_key.reserve_grow(sizeof(unsigned long long) * n));
+  HIPCHK(e, e->o_m1.reserve_grow(sizeof(int32_t) * n));
+  HIPCHK(e, e->o_key_b.reserve_grow(sizeof(unsigned long long) * n));
+  HIPCHK(e, e->o_m1_b.reserve_grow(sizeof(int32_t) * n));
+  HIPCHK(e, launch_order_fill(e->m1s.as<int32_t>(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), R,
+                              e->o_key_b.as<unsigned long long>(), e->o_m1_b.as<int32_t>(), s));
+  HIPCHK(e, order_sort(e->o_key_b.as<unsigned long long>(), e->o_key.as<unsigned long long>(), e->o_m1_b.as<int32_t>(),
+                       e->o_m1.as<int32_t>(), R, &e->o_sort_tmp, s));
+  e->o_rows = R;
+  e->o_valid = true;
+  e->n_order_builds++;
+  return TFP_OK;
+}
+
+// The general path's clip-set cache at tolerance tole (after ensure_ranges at tole): the active one,
+// or one of kCellSlots others (least recently used out), per index version. Built from the clip
+// order for tolerances up to kOrderMaxTol (no sort), else from the boxes' rows.
 int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
-  if (e->cell_fresh && memcmp(&e->cell_tol, &tole, sizeof tole) == 0) return TFP_OK;
-  std::vector<int64_t> rng(2 * kKeyRange), off(kKeyRange + 1, 0);
-  HIPCHK(e, hipMemcpyAsync(rng.data(), e->rng_all.p, sizeof(int64_t) * rng.size(), hipMemcpyDeviceToHost, s));
-  HIPCHK(e, hipStreamSynchronize(s));
-  for (int k = 0; k < kKeyRange; k++) off[k + 1] = off[k] + std::max<int64_t>(0, rng[2 * k + 1] - rng[2 * k]);
-  // The cache is optional: if building it fails (an allocation or a hipcub call), the batch takes
-  // the row scan, which needs none of it (tfp_scan.hip). The failed build has released its buffers.
-  const hipError_t st = e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(),
-                                       e->ncols, e->nrows, tole, s);
+  if (e->cell_fresh && e->cell_version == e->index_version && memcmp(&e->cell_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  CellSlot* hit = nullptr;
+  CellSlot* victim = &e->cell_lru[0];
+  for (CellSlot& t : e->cell_lru) {
+    if (t.version != e->index_version) t.has = false;
+    if (t.has && memcmp(&t.tol, &tole, sizeof tole) == 0) hit = &t;
+    if (t.has != victim->has ? !t.has : t.used < victim->used) victim = &t;
+  }
+  const bool active = e->cell_fresh && e->cell_version == e->index_version;
+  CellSlot* into = hit ? hit : victim;
+  // the active cache (when current) goes into the slot the wanted one comes from (or the victim's,
+  // whose buffers the build below then reuses)
+  e->cells.swap(into->c);
+  std::swap(e->cell_tol, into->tol);
+  into->has = active;
+  into->version = e->index_version;
+  into->used = ++e->tol_clock;
+  if (hit) {
+    e->cell_tol = tole;
+    e->cell_fresh = true;
+    e->cell_version = e->index_version;
+    e->n_cell_hits++;
+    return TFP_OK;
+  }
+  e->n_cell_builds++;
+  // The cache is optional: if building it fails (an allocation or a library call), the batch takes
+  // the row scan, which needs none of it (tfp_scan.hip).
+  hipError_t st = hipSuccess;
+  if (tole >= 0.0 && tole <= kOrderMaxTol && e->nrows > 0 && e->nrows < INT32_MAX) {
+    int rc = ensure_order(e, s);
+    if (rc) return rc;
+    if (!e->kbox_valid || memcmp(&e->kbox_tol, &tole, sizeof tole) != 0) {
+      HIPCHK(e, e->kbox.reserve(sizeof(int64_t) * 2 * kKeyRange));
+      HIPCHK(e, launch_key_boxes(tole, e->kbox.as<int64_t>(), s));
+      e->kbox_tol = tole;
+      e->kbox_valid = true;
+    }
+    st = e->cells.build_from_order(e->o_key.as<unsigned long long>(), e->o_m1.as<int32_t>(), e->o_rows, e->kbox.as<int64_t>(),
+                                   e->ncols, tole, s);
+    if (st == hipSuccess && e->cells.valid) e->n_cell_from_order++;
+  } else {
+    std::vector<int64_t> rng(2 * kKeyRange), off(kKeyRange + 1, 0);
+    HIPCHK(e, hipMemcpyAsync(rng.data(), e->rng_all.p, sizeof(int64_t) * rng.size(), hipMemcpyDeviceToHost, s));
+    HIPCHK(e, hipStreamSynchronize(s));
+    for (int k = 0; k < kKeyRange; k++) off[k + 1] = off[k] + std::max<int64_t>(0, rng[2 * k + 1] - rng[2 * k]);
+    st = e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), e->ncols, e->nrows,
+                        tole, s);
+  }
   if (st != hipSuccess) {
     (void)hipGetLastError();
     if (e->dbg_vote) fprintf(stderr, "[tfp] clip-set cache not built (%s): row scan\n", hipGetErrorString(st));
-    e->cells.release();
+    e->cells.invalidate();
     HIPCHK(e, hipStreamSynchronize(s));
   }
   e->cell_tol = tole;
   e->cell_fresh = true;
+  e->cell_version = e->index_version;
   return TFP_OK;
 }
 
@@ -1340,6 +1504,8 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     bool spec = false;  // the sweep ran without the host reading its sort's counts (checked below)
     bool spec_mapped = false;  // its counts were written to spec_pin by its last kernel
     bool out_written = false;  // the sweep wrote its keys straight into d_keys_out
+    bool swept = false;        // the sweep by groups ran (not the cells form / row scan)
+    bool bins_used = false;
     if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2) && sc.tole >= e->wide_min_tol) {
       // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
@@ -1351,6 +1517,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         unsigned long long* wbest = d_keys_out ? reinterpret_cast<unsigned long long*>(d_keys_out) : d_best;
         HIPCHK(e, launch_scan_wide_prepare(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), nq, nf, max_frames, sc.tole,
                                            &e->wide, &ok, s, pass == 0, d_keys_out ? wbest : nullptr));
+        bins_used = e->wide.ukeys_ready;  // (the bin sort ran on this pass)
         if (ok) {
           // a speculative sweep's counts come back through host-mapped memory, written by its last kernel
           int32_t* d_info = nullptr;
@@ -1364,6 +1531,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
           }
           HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, wbest, s, d_info, &spec_mapped));
           done = true;
+          swept = true;
           out_written = d_keys_out != nullptr;
           spec = e->wide.spec;
         }
@@ -1389,6 +1557,10 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         HIPCHK(e, hipMemsetAsync(e->tcnt.p, 0, e->tcnt.bytes, s));
         e->scan_zeroed = z;  // (touched is written before it is read)
       }
+      if (e->cells.valid && e->cells.ensure_entries(s) != hipSuccess) {  // (the cells form's candidates)
+        (void)hipGetLastError();
+        e->cells.invalidate();  // every frame takes the row scan
+      }
       for (int64_t q0 = 0; q0 < nq; q0 += chunk) {
         const int32_t n = (int32_t)std::min<int64_t>(chunk, nq - q0);
         HIPCHK(e, launch_scan(e->boxes.as<FrameBox>(), e->qoff.as<int64_t>(), qo.data(), (int32_t)q0, n,
@@ -1400,7 +1572,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
     // the speculative sweep's counts come back with the results (one host wait per batch)
     if (spec && !spec_mapped) {
       HIPCHK(e, e->spec_pin.reserve(4 * sizeof(int32_t), hipHostMallocMapped | hipHostMallocCoherent));
-      HIPCHK(e, hipMemcpyAsync(e->spec_pin.p, e->wide.info, 3 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+      HIPCHK(e, hipMemcpyAsync(e->spec_pin.p, e->wide.info, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     }
     if (d_keys_out) {
       if (!out_written)
@@ -1415,11 +1587,14 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       const int32_t* info = e->spec_pin.as<int32_t>();
       if (info[1] > 0 || info[2] > 0) {  // a frame for the row scan, or a window the one-sort key cannot order
         if (e->dbg_vote) fprintf(stderr, "[tfp] speculative sweep redone (info %d %d %d)\n", info[0], info[1], info[2]);
+        e->n_sweep_redo++;
         done = false;
         HIPCHK(e, hipMemsetAsync(d_best, 0, sizeof(unsigned long long) * nq, s));
         continue;
       }
+      if (bins_used) e->n_sweep_crowd += info[3];
     }
+    if (swept) (bins_used ? e->n_sweep_bins : e->n_sweep_lib)++;
     return TFP_OK;
   }
 }
@@ -1440,7 +1615,9 @@ int32_t col_of_key(const tfp_engine* e, int32_t k) {
     return k - lo;
   }
   auto it = e->key_col.find(k);
-  return it == e->key_col.end() ? -1 : it->second;
+  if (it != e->key_col.end()) return it->second;
+  auto jt = e->key_col_delta.find(k);
+  return jt == e->key_col_delta.end() ? -1 : jt->second;
 }
 
 // The clip of an index column (-1: none): a main column or a delta column.
@@ -1518,11 +1695,12 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.unpacked = tfp::knob("TFP_WIDE_UNPACKED") != nullptr;
   e->wide.libsort = tfp::knob("TFP_WIDE_LIBSORT") != nullptr;
   e->wide.debug_bins = tfp::knob("TFP_DEBUG_BINS") != nullptr;
-  if (const char* v = tfp::knob("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
-  if (const char* v = tfp::knob("TFP_INDEX_DELTA")) {
-    e->use_delta = atoi(v) != 0;
-    if (e->use_delta) e->delta_min_cols = 0;
-  }
+  // operational switches (documented: tiresias_fp.h), read as plain environment variables
+  if (const char* v = tfp::op_env("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
+  if (const char* v = tfp::op_env("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
+  // test form: the delta even below delta_min_cols main columns (small test DBs)
+  if (const char* v = tfp::knob("TFP_INDEX_DELTA"))
+    if (atoi(v) != 0) e->delta_min_cols = 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
     delete e;
     return TFP_E_HIP;
@@ -1624,7 +1802,9 @@ int tfp_plan_create(tfp_engine* e, const int64_t* offsets, int32_t nclips, int32
   p->eng = e;
   p->nclips = nclips;
   p->sample_rate = sr;
-  p->tile_frames = fp_tile_frames(e->fpcfg, fx, false, false);
+  for (int32_t c = 0; c < nclips; c++)
+    if (offsets[c + 1] - offsets[c] >= kDirectMaxSamples) p->long_clip = true;
+  p->tile_frames = fp_tile_frames(e->fpcfg, fx && !p->long_clip, false, false);
   layout(offsets, nclips, p->soff, p->foff, p->toff, &p->tclip, p->tile_frames);
   p->nsamples = p->soff[nclips];
   p->nframes = p->foff[nclips];
@@ -1654,7 +1834,7 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
   int rc = ensure_tables(e, p->sample_rate, &T, &fx);
   if (rc) return rc;
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
-  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx && !p->long_clip, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, d_micro, d_db, s, e->logfix));
   return TFP_OK;
@@ -1895,6 +2075,21 @@ int tfp_index_set_tiebreak(tfp_engine* e, const int32_t* keys, int32_t n) {
   if (!e || n < 0 || (n && !keys)) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   e->tiebreak_override.assign(keys, keys + n);
+  e->ovr_main_stale = true;
+  e->dirty = true;
+  return TFP_OK;
+}
+
+int tfp_index_update_tiebreak(tfp_engine* e, int32_t first_clip_id, const int32_t* keys, int32_t n) {
+  if (!e || first_clip_id < 0 || n < 0 || (n && !keys)) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if ((size_t)first_clip_id > e->tiebreak_override.size() || (e->tiebreak_override.empty() && first_clip_id > 0))
+    return fail(e, TFP_E_ARG, "tie-break keys from clip id %d: the keys before it were never set", first_clip_id);
+  if ((size_t)first_clip_id + (size_t)n > e->tiebreak_override.size()) e->tiebreak_override.resize((size_t)first_clip_id + n);
+  std::copy(keys, keys + n, e->tiebreak_override.begin() + first_clip_id);
+  // new keys for clips of the last build change the main columns' keys (a full refresh at the next
+  // update); keys of clips added since concern the delta or the next merge only
+  if ((size_t)first_clip_id < e->built_clips && n > 0) e->ovr_main_stale = true;
   e->dirty = true;
   return TFP_OK;
 }
@@ -1946,7 +2141,7 @@ int search_gather_impl(tfp_engine* e, const void* const* ptrs, const int64_t* le
   for (int32_t i = 0; i < nq; i++) foff[i + 1] = foff[i] + tfp_frame_count(lens[i]);
   for (int32_t i = 0; e->fail_query_len >= 0 && i < nq; i++)  // (test knob: a query that fails on the device)
     if (lens[i] == e->fail_query_len)
-      return fail(e, TFP_E_HIP, "hipMalloc for query %d of %d (%lld samples): out of memory (TFP_TEST_FAIL_QUERY_SAMPLES)", i,
+      return fail(e, TFP_E_NOMEM, "hipMalloc for query %d of %d (%lld samples): out of memory (TFP_TEST_FAIL_QUERY_SAMPLES)", i,
                   nq, (long long)lens[i]);
   std::vector<unsigned long long> keys(nq, 0ull);
   if (valid_params(P) && nq && foff[nq] > 0) {
@@ -2015,6 +2210,34 @@ int tfp_search_pcm_gather(tfp_engine* e, const int16_t* const* pcms, const int64
   return search_gather_entry(e, reinterpret_cast<const void* const*>(pcms), nsamples, nq, false, sr, P, out);
 }
 
+int tfp_sweep_stats(tfp_engine* e, int64_t* bins, int64_t* library, int64_t* redone, int64_t* crowd_bins) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (bins) *bins = e->n_sweep_bins;
+  if (library) *library = e->n_sweep_lib;
+  if (redone) *redone = e->n_sweep_redo;
+  if (crowd_bins) *crowd_bins = e->n_sweep_crowd;
+  return TFP_OK;
+}
+
+int tfp_index_cache_stats(tfp_engine* e, int64_t* cache_builds, int64_t* cache_hits, int64_t* from_order,
+                          int64_t* order_builds, int64_t* order_merges) {
+  if (!e) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(e->mu);
+  if (cache_builds) *cache_builds = e->n_cell_builds;
+  if (cache_hits) *cache_hits = e->n_cell_hits;
+  if (from_order) *from_order = e->n_cell_from_order;
+  if (order_builds) *order_builds = e->n_order_builds;
+  if (order_merges) *order_merges = e->n_order_merges;
+  return TFP_OK;
+}
+
+int64_t tfp_internal_delta_main_keys(tfp_engine* e) { return e ? e->n_delta_main_keys : 0; }
+const char* tfp_internal_engine_own_error(tfp_engine* e) { return e ? e->err.own() : nullptr; }
+void tfp_internal_engine_clear_error(tfp_engine* e) {
+  if (e) e->err.clear_own();
+}
+
 int tfp_search_coalesce_stats(tfp_engine* e, int64_t* calls, int64_t* batches) {
   if (!e) return TFP_E_ARG;
   e->coal.stats(calls, batches);
@@ -2040,7 +2263,7 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (rc) return rc;
   HIPCHK(e, e->micro.reserve(sizeof(int32_t) * 2 * (p->nframes + 1)));
   HIPCHK(e, e->db.reserve(sizeof(double) * 2 * (p->nframes + 1)));
-  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
+  HIPCHK(e, launch_fingerprint(e->fpcfg, T, fx && !p->long_clip, p->tile_frames, d_pcm, p->d_soff.as<int64_t>(), p->d_soff.as<int64_t>() + 1,
                                p->d_foff.as<int64_t>(), p->d_toff.as<int32_t>(),
                                p->d_tclip.as<int32_t>(), p->ntiles, p->nframes, e->micro.as<int32_t>(),
                                e->db.as<double>(), s, P->coefs == 2 ? e->logfix : LogFix{}));

@@ -47,7 +47,8 @@ namespace {
 struct Member {
   std::string uuid;
   int32_t shard;
-  int32_t id;  // the engine's clip id
+  int32_t id;        // the engine's clip id
+  int32_t key = -1;  // its tie-break key (ordered like the uuids, sparse; -1 until assigned)
 };
 
 // Device buffers of the query-sharded batch path, one set per shard.
@@ -88,11 +89,21 @@ struct tfp_group {
   std::vector<std::vector<int32_t>> id2member;         // [shard][engine clip id] -> member index (-1 removed)
   std::vector<int64_t> rows;                           // live rows per shard (placement)
   std::vector<int32_t> by_uuid;                        // live members in uuid order (global ranks)
-  std::vector<int32_t> member_rank;                    // member -> its global rank (valid when !ranks_dirty)
-  bool ranks_dirty = true;
+  // Tie-break keys (round 6): every live member's key orders like its uuid with gaps between
+  // neighbours, so a new clip takes the middle of its neighbours' gap and no other key changes; the
+  // shards then get the new clips' keys only (tfp_index_update_tiebreak), an enrolment stays
+  // O(new clips). A gap of 1 (or a large batch) respaces every key evenly over [0, 2^31) instead.
+  std::unordered_map<int32_t, int32_t> key2member;     // key -> member
+  std::vector<size_t> pushed;                          // per shard: engine clip ids whose keys it has
+  bool keys_full = true;                               // respace every key and send every shard all its keys
+  bool ranks_dirty = true;                             // some shard lacks keys (keys_full or new clip ids)
+  int64_t n_respaces = 0, n_partial_pushes = 0;        // full key refreshes / new-clip-only pushes
   std::vector<ShardBufs> bufs;
   tfp::Coalescer coal;   // concurrent channel searches share one batch per shard (tfp_coalesce.hpp)
   bool coalesce = true;  // TFP_COALESCE=0: every call alone
+  // ordered pairs of distinct devices; of them, peer-accessible; of those, peer access enabled
+  // (tfp_group_peer_stats: the 8-GPU bench line reports them)
+  int32_t peer_pairs = 0, peer_can = 0, peer_enabled = 0;
   ~tfp_group() {
     delete pool;
     for (size_t s = 0; s < bufs.size(); s++) {
@@ -147,48 +158,96 @@ int run_all(tfp_group* g, const std::function<int(int)>& f) {
   int bad = 0;
   const int rc = g->pool->run(
       [&](int s) {
+        tfp_internal_engine_clear_error(g->eng[s]);
+        g->err.clear_own();  // (this pool thread's: f may note a group-level failure, a peer copy's)
         const int r = f(s);
-        if (r) why[s] = r == TFP_E_NOMEM ? "out of host memory" : tfp_engine_last_error(g->eng[s]);
+        if (r) {  // the message this call recorded on this thread: the shard engine's, else the group's
+          const char* m = tfp_internal_engine_own_error(g->eng[s]);
+          if (!m) m = g->err.own();
+          why[s] = m ? m : r == TFP_E_NOMEM ? "out of memory" : "device call failed";
+        }
         return r;
       },
       &bad);
   return rc ? gfail(g, rc, "shard %d (device %d): %s", bad, g->dev[bad], why[bad].c_str()) : TFP_OK;
 }
 
-// Group-wide uuid ranks as every engine's tie-break keys (before any search after a change).
+constexpr int64_t kKeySpan = int64_t(1) << 31;  // tie-break keys lie in [0, 2^31)
+
+// Every shard's tie-break keys (before any search after a change): after a respace, all of each
+// shard's clips' keys; otherwise only the clip ids enrolled since (tfp_index_update_tiebreak).
 int refresh_ranks(tfp_group* g) {
   if (!g->ranks_dirty) return TFP_OK;
   const int n = (int)g->eng.size();
-  std::vector<std::vector<int32_t>> keys(n);
-  for (int s = 0; s < n; s++) keys[s].assign(std::max<size_t>(g->id2member[s].size(), 1), -1);
-  g->member_rank.assign(g->members.size(), -1);
-  for (size_t r = 0; r < g->by_uuid.size(); r++) {
-    const Member& m = g->members[g->by_uuid[r]];
-    keys[m.shard][m.id] = (int32_t)r;
-    g->member_rank[g->by_uuid[r]] = (int32_t)r;
+  const bool full = g->keys_full;
+  if (full) {  // even spacing over [0, 2^31) in uuid order
+    const int64_t N = (int64_t)g->by_uuid.size(), step = kKeySpan / (N + 1);
+    g->key2member.clear();
+    g->key2member.reserve(N);
+    for (int64_t r = 0; r < N; r++) {
+      Member& m = g->members[g->by_uuid[r]];
+      m.key = (int32_t)((r + 1) * step);
+      g->key2member[m.key] = g->by_uuid[r];
+    }
   }
-  const int rc = run_all(g, [&](int s) {
-    return tfp_index_set_tiebreak(g->eng[s], keys[s].data(), (int32_t)g->id2member[s].size());
+  g->pushed.resize(n, 0);
+  auto key_of_id = [&](int s, size_t id) {
+    const int32_t mi = g->id2member[s][id];
+    return mi < 0 ? -1 : g->members[mi].key;
+  };
+  const int rc = run_all(g, [&](int s) -> int {
+    const size_t have = g->id2member[s].size(), from = full ? 0 : std::min(g->pushed[s], have);
+    if (!full && from == have) return TFP_OK;
+    std::vector<int32_t> keys(std::max<size_t>(have - from, 1));
+    for (size_t id = from; id < have; id++) keys[id - from] = key_of_id(s, id);
+    const int r = full ? tfp_index_set_tiebreak(g->eng[s], keys.data(), (int32_t)have)
+                       : tfp_index_update_tiebreak(g->eng[s], (int32_t)from, keys.data(), (int32_t)(have - from));
+    if (!r) g->pushed[s] = have;
+    return r;
   });
-  if (rc) return rc;
+  if (rc) {
+    g->keys_full = true;  // (the next refresh sends everything again)
+    return rc;
+  }
+  (full ? g->n_respaces : g->n_partial_pushes)++;
+  g->keys_full = false;
   g->ranks_dirty = false;
   return TFP_OK;
 }
 
 bool uuid_less(const tfp_group* g, int32_t a, int32_t b) { return g->members[a].uuid < g->members[b].uuid; }
 
+// A member into the uuid order; its key: the middle of its neighbours' gap (keys_full: the next
+// refresh respaces every key instead).
 void insert_live(tfp_group* g, int32_t mi) {
   auto it = std::lower_bound(g->by_uuid.begin(), g->by_uuid.end(), mi,
                              [&](int32_t a, int32_t b) { return uuid_less(g, a, b); });
+  const size_t pos = (size_t)(it - g->by_uuid.begin());
   g->by_uuid.insert(it, mi);
   g->ranks_dirty = true;
+  if (g->keys_full) return;
+  const int64_t lo = pos > 0 ? g->members[g->by_uuid[pos - 1]].key : -1;
+  const int64_t hi = pos + 1 < g->by_uuid.size() ? g->members[g->by_uuid[pos + 1]].key : kKeySpan;
+  if (hi - lo < 2) {
+    g->keys_full = true;
+    return;
+  }
+  Member& m = g->members[mi];
+  m.key = (int32_t)(lo + (hi - lo) / 2);
+  g->key2member[m.key] = mi;
 }
 
 void erase_live(tfp_group* g, int32_t mi) {
   auto it = std::lower_bound(g->by_uuid.begin(), g->by_uuid.end(), mi,
                              [&](int32_t a, int32_t b) { return uuid_less(g, a, b); });
   if (it != g->by_uuid.end() && *it == mi) g->by_uuid.erase(it);
-  g->ranks_dirty = true;
+  Member& m = g->members[mi];
+  if (m.key >= 0) {
+    auto k = g->key2member.find(m.key);
+    if (k != g->key2member.end() && k->second == mi) g->key2member.erase(k);
+    m.key = -1;
+  }
+  // (no other key changes: the shards' keys stay valid, the removed clip's is never read again)
 }
 
 int32_t lightest(const tfp_group* g) {
@@ -199,8 +258,8 @@ int32_t lightest(const tfp_group* g) {
 unsigned long long key_of(const tfp_group* g, int s, const tfp_result& r) {
   if (!r.found || r.clip_id < 0 || (size_t)r.clip_id >= g->id2member[s].size()) return 0ull;
   const int32_t mi = g->id2member[s][r.clip_id];
-  if (mi < 0 || g->member_rank[mi] < 0) return 0ull;
-  return ((unsigned long long)(uint32_t)r.match_count << 32) | (uint32_t)g->member_rank[mi];
+  if (mi < 0 || g->members[mi].key < 0) return 0ull;
+  return ((unsigned long long)(uint32_t)r.match_count << 32) | (uint32_t)g->members[mi].key;
 }
 
 // Per query, the greatest key over the shards' results -> the group's result.
@@ -223,9 +282,10 @@ void fill_from_key(const tfp_group* g, unsigned long long k, int32_t frame_count
   memset(r, 0, sizeof *r);
   r->frame_count = frame_count;
   r->clip_id = -1;
-  const uint32_t rank = (uint32_t)(k & 0xffffffffu);
-  if (!k || rank >= g->by_uuid.size()) return;
-  const Member& m = g->members[g->by_uuid[rank]];
+  if (!k) return;
+  const auto it = g->key2member.find((int32_t)(uint32_t)(k & 0xffffffffu));
+  if (it == g->key2member.end()) return;
+  const Member& m = g->members[it->second];
   r->found = 1;
   r->match_count = (int32_t)(k >> 32);
   r->clip_id = m.shard;
@@ -235,6 +295,8 @@ void fill_from_key(const tfp_group* g, unsigned long long k, int32_t frame_count
 bool valid_params(const tfp_search_params* P) { return P && P->coefs >= 1 && P->coefs <= 2; }
 
 int add_members(tfp_group* g, int32_t s, int32_t n, const char* const* uuids) {
+  // (a large batch: one even respace at the next refresh instead of many halved gaps)
+  if (n > 64) g->keys_full = true;
   // the engine assigns clip ids in order of addition (tfp_index_add / _add_batch)
   for (int32_t c = 0; c < n; c++) {
     const int32_t mi = (int32_t)g->members.size();
@@ -299,9 +361,11 @@ int search_sharded(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int
       const int32_t k = share[o + 1] - share[o];
       if (o == s || !k) continue;
       const size_t off = sizeof(double) * 2 * (size_t)(nfq * share[o]), bytes = sizeof(double) * 2 * (size_t)(nfq * k);
-      if (hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], (const char*)g->bufs[o].q + off, g->dev[o], bytes, b.stream) !=
-          hipSuccess)
-        return TFP_E_HIP;
+      if (const hipError_t pe = hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], (const char*)g->bufs[o].q + off, g->dev[o],
+                                                   bytes, b.stream);
+          pe != hipSuccess)
+        return gfail(g, TFP_E_HIP, "frame values of shard %d (device %d) to shard %d (device %d): hipMemcpyPeerAsync: %s", o,
+                     g->dev[o], s, g->dev[s], hipGetErrorString(pe));
     }
     int r = tfp_search_q_device(g->eng[s], (const double*)b.q, qoff.data(), nq, P, (uint64_t*)b.keys, b.stream);
     if (r) return r;
@@ -338,26 +402,57 @@ int tfp_group_create(const int32_t* devices, int32_t n, tfp_group** out) {
     g->eng.push_back(e);
     g->dev.push_back(devices[s]);
   }
-  // peer access between the distinct devices (xGMI), for the query-sharded batches
+  // peer access between the distinct devices (xGMI), for the query-sharded batches and split
+  // streams. Counted per ordered pair (tfp_group_peer_stats); a pair without it still copies
+  // (hipMemcpyPeerAsync stages through the host), and a failed copy fails the call loudly.
   for (int32_t a = 0; a < n; a++)
     for (int32_t b = 0; b < n; b++) {
+      if (devices[a] == devices[b]) continue;
+      bool seen = false;  // (a repeated pair of devices counts once)
+      for (int32_t a2 = 0; a2 < n && !seen; a2++)
+        for (int32_t b2 = 0; b2 < n && !seen; b2++)
+          seen = (a2 < a || (a2 == a && b2 < b)) && devices[a2] == devices[a] && devices[b2] == devices[b];
+      if (seen) continue;
+      g->peer_pairs++;
       int can = 0;
-      if (devices[a] != devices[b] && hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can &&
-          hipSetDevice(devices[a]) == hipSuccess) {
+      if (hipDeviceCanAccessPeer(&can, devices[a], devices[b]) == hipSuccess && can && hipSetDevice(devices[a]) == hipSuccess) {
+        g->peer_can++;
         const hipError_t e = hipDeviceEnablePeerAccess(devices[b], 0);
-        if (e != hipSuccess) (void)hipGetLastError();  // (already enabled: fine; else copies stage through the host)
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) g->peer_enabled++;
+        if (e != hipSuccess) (void)hipGetLastError();
       }
     }
   g->id2member.assign(n, {});
   g->rows.assign(n, 0);
   g->bufs.resize(n);
   g->pool = new tfp::ShardPool(n);
-  if (const char* v = tfp::knob("TFP_COALESCE")) g->coalesce = atoi(v) != 0;
+  if (const char* v = tfp::op_env("TFP_COALESCE")) g->coalesce = atoi(v) != 0;
   *out = g;
   return TFP_OK;
 }
 
 void tfp_group_destroy(tfp_group* g) { delete g; }
+
+int tfp_group_peer_stats(const tfp_group* g, int32_t* pairs, int32_t* can_access, int32_t* enabled) {
+  if (!g) return TFP_E_ARG;
+  if (pairs) *pairs = g->peer_pairs;
+  if (can_access) *can_access = g->peer_can;
+  if (enabled) *enabled = g->peer_enabled;
+  return TFP_OK;
+}
+
+int tfp_group_tiebreak_stats(tfp_group* g, int64_t* respaces, int64_t* partial_pushes, int64_t* shard_full_key_updates) {
+  if (!g) return TFP_E_ARG;
+  std::lock_guard<std::recursive_mutex> lk(g->mu);
+  if (respaces) *respaces = g->n_respaces;
+  if (partial_pushes) *partial_pushes = g->n_partial_pushes;
+  if (shard_full_key_updates) {
+    int64_t t = 0;
+    for (tfp_engine* e : g->eng) t += tfp_internal_delta_main_keys(e);
+    *shard_full_key_updates = t;
+  }
+  return TFP_OK;
+}
 
 int32_t tfp_group_size(const tfp_group* g) { return g ? (int32_t)g->eng.size() : 0; }
 
@@ -511,6 +606,7 @@ int tfp_group_index_clear(tfp_group* g) {
   std::vector<int> rcs(n, TFP_OK);
   const int rc = run_all(g, [&](int s) { return rcs[s] = tfp_index_clear(g->eng[s]); });
   g->ranks_dirty = true;
+  g->keys_full = true;
   if (rc == TFP_OK) {
     g->where.clear();
     g->members.clear();
@@ -683,7 +779,7 @@ int tfp_group_stream_create(tfp_group* g, int32_t nch, int32_t sr, int64_t W, tf
   st->g = g;
   st->nch = nch;
   st->W = W;
-  const char* mode = tfp::knob("TFP_GROUP_STREAM");
+  const char* mode = tfp::op_env("TFP_GROUP_STREAM");  // operational switch
   st->split = n > 1 && !(mode && !strcmp(mode, "replicate"));
   st->st.assign(n, nullptr);
   if (st->split) {
@@ -775,8 +871,10 @@ int split_stream_push(tfp_group_stream* st, const int16_t* pcm, int32_t T, const
     for (int o = 0; o < n; o++) {
       if (!st->nact[o]) continue;
       const size_t off = sizeof(double) * 2 * (size_t)(F * base[o]), bytes = sizeof(double) * 2 * (size_t)(F * st->nact[o]);
-      if (hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], g->bufs[o].sfp, g->dev[o], bytes, b.stream) != hipSuccess)
-        return TFP_E_HIP;
+      if (const hipError_t pe = hipMemcpyPeerAsync((char*)b.q + off, g->dev[s], g->bufs[o].sfp, g->dev[o], bytes, b.stream);
+          pe != hipSuccess)
+        return gfail(g, TFP_E_HIP, "stream windows of shard %d (device %d) to shard %d (device %d): hipMemcpyPeerAsync: %s", o,
+                     g->dev[o], s, g->dev[s], hipGetErrorString(pe));
     }
     st->keys[s].resize(na);
     int r = tfp_search_q_device(g->eng[s], (const double*)b.q, qoff.data(), na, P, (uint64_t*)b.keys, b.stream);

@@ -254,6 +254,169 @@ __global__ __launch_bounds__(64) void key_bits_add_kernel(const int64_t* __restr
   }
 }
 
+
+// ---- the clip order through an update (round 6) ----------------------------------------------
+
+constexpr uint32_t kOColMask = (1u << 21) - 1u;
+
+__device__ __forceinline__ int32_t new_at(const int32_t* __restrict__ newcol, const int32_t* __restrict__ newat, int32_t D,
+                                          int32_t col) {
+  int32_t lo = 0, hi = D;  // the new clip with this column
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (newcol[mid] < col) lo = mid + 1; else hi = mid;
+  }
+  return newat[lo < D ? lo : D - 1];
+}
+
+// The new rows' clip-order keys (t << 53 | new column << 32 | m2 bits) and m1 (the nearest-integer
+// key index as tfp_scan.hip's order_key_index).
+__global__ void order_new_keys_kernel(const int32_t* __restrict__ nm1, const int32_t* __restrict__ nm2,
+                                      const int32_t* __restrict__ ncol, int64_t n, unsigned long long* __restrict__ nk,
+                                      int32_t* __restrict__ nv) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t m1 = nm1[i];
+    const int64_t v = (int64_t)m1 + 500000;
+    int64_t t = (v >= 0 ? v : v - 999999) / 1000000 + kKeyOffset;
+    t = t < 0 ? 0 : t >= kKeyRange ? kKeyRange - 1 : t;
+    nk[i] = ((unsigned long long)t << 53) | ((unsigned long long)(uint32_t)ncol[i] << 32) | (uint32_t)(nm2[i] ^ INT32_MIN);
+    nv[i] = m1;
+  }
+}
+
+// pos[j] = old rows before new row j: those of a smaller key index, or of the same one and an old
+// column below the new clip's insertion point (no old row shares a new row's column).
+__global__ void order_pos_kernel(const unsigned long long* __restrict__ okey, int64_t R, const unsigned long long* __restrict__ nk,
+                                 int64_t n, const int32_t* __restrict__ newcol, const int32_t* __restrict__ newat, int32_t D,
+                                 int64_t* __restrict__ pos) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const unsigned long long k = nk[j];
+    const int32_t at = new_at(newcol, newat, D, (int32_t)((k >> 32) & kOColMask));
+    const unsigned long long v = ((k >> 53) << 53) | ((unsigned long long)(uint32_t)at << 32);
+    int64_t lo = 0, hi = R;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (okey[mid] < v) lo = mid + 1; else hi = mid;
+    }
+    pos[j] = lo;
+  }
+}
+
+// kept[t] = old order rows of tile t whose clip survives.
+__global__ __launch_bounds__(kThreads) void order_count_kept_kernel(const unsigned long long* __restrict__ okey, int64_t R,
+                                                                    const int32_t* __restrict__ remap, int32_t ntiles,
+                                                                    int32_t* __restrict__ kept) {
+  __shared__ int32_t wsum[kThreads / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kMergeTile;
+  int32_t c = 0;
+  if (blockIdx.x < (unsigned)ntiles) {
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const int64_t i = b0 + k * kThreads + threadIdx.x;
+      if (i < R) c += remap[(okey[i] >> 32) & kOColMask] >= 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = 0;
+    for (int w = 0; w < kThreads / 64; w++) t += wsum[w];
+    kept[blockIdx.x] = t;
+  }
+}
+
+// merge_write_kernel's tile, for the clip order's (key, m1) rows.
+__global__ __launch_bounds__(kThreads) void order_write_kernel(
+    const unsigned long long* __restrict__ okey, const int32_t* __restrict__ om1, int64_t R, const int32_t* __restrict__ remap,
+    MergeBreaks brk, const int32_t* __restrict__ base, const unsigned long long* __restrict__ nk,
+    const int32_t* __restrict__ nv, const int64_t* __restrict__ pos, const int64_t* __restrict__ jbeg,
+    unsigned long long* __restrict__ ok2, int32_t* __restrict__ om2) {
+  __shared__ int32_t pref[kMergeTile + 1];
+  __shared__ int32_t lpos[kPosLds];
+  __shared__ int32_t csum[kRowsPerThread][kThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int64_t b0 = (int64_t)blockIdx.x * kMergeTile;
+  const int64_t j0 = jbeg[blockIdx.x], j1 = jbeg[blockIdx.x + 1], nj = j1 - j0;
+  unsigned long long rk[kRowsPerThread];
+  int32_t r1[kRowsPerThread];
+  uint32_t keep = 0;
+  if (R > 0) {
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const int64_t i = min(b0 + k * kThreads + t, R - 1);
+      rk[k] = okey[i];
+      r1[k] = om1[i];
+    }
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const int32_t c = (int32_t)((rk[k] >> 32) & kOColMask);
+      int32_t nc = c;
+      if (brk.n >= 0) {
+        for (int j = 0; j < brk.n; j++) nc += c >= brk.p[j];
+      } else {
+        nc = remap[c];
+      }
+      keep |= (uint32_t)(b0 + k * kThreads + t < R && nc >= 0) << k;
+      rk[k] = (rk[k] & ~((unsigned long long)kOColMask << 32)) | ((unsigned long long)(uint32_t)(nc < 0 ? 0 : nc) << 32);
+    }
+  }
+  const bool all_kept = base == nullptr;
+  uint32_t lo[kRowsPerThread];
+  if (!all_kept) {
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) {
+      const uint64_t m = __ballot((keep >> k) & 1u);
+      lo[k] = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (lane == 0) csum[k][wv] = __popcll(m);
+    }
+  }
+  __syncthreads();
+  if (!all_kept && t == 0) {
+    int32_t run = 0;
+    for (int k = 0; k < kRowsPerThread; k++)
+      for (int w = 0; w < kThreads / 64; w++) {
+        const int32_t v = csum[k][w];
+        csum[k][w] = run;
+        run += v;
+      }
+    pref[kMergeTile] = run;
+  }
+  __syncthreads();
+  const bool in_lds = nj <= kPosLds;
+  if (in_lds)
+    for (int64_t j = t; j < nj; j += kThreads) lpos[j] = (int32_t)(pos[j0 + j] - b0);
+  if (!all_kept)
+#pragma unroll
+    for (int k = 0; k < kRowsPerThread; k++) pref[k * kThreads + t] = csum[k][wv] + (int32_t)lo[k];
+  __syncthreads();
+  auto place = [&](int32_t r) -> int32_t { return all_kept ? r : pref[r]; };
+  const int64_t bb = base ? (int64_t)base[blockIdx.x] : b0;
+#pragma unroll
+  for (int k = 0; k < kRowsPerThread; k++) {
+    if (!((keep >> k) & 1u)) continue;
+    const int32_t r = k * kThreads + t;
+    int64_t before = j0;  // new rows placed before old row b0 + r: insertion point <= b0 + r
+    if (nj) {
+      int64_t a = 0, h = nj;
+      while (a < h) {
+        const int64_t mid = (a + h) >> 1;
+        const int64_t p = in_lds ? (int64_t)lpos[mid] : pos[j0 + mid] - b0;
+        if (p <= r) a = mid + 1; else h = mid;
+      }
+      before += a;
+    }
+    const int64_t o = bb + place(r) + before;
+    ok2[o] = rk[k];
+    om2[o] = r1[k];
+  }
+  for (int64_t j = t; j < nj; j += kThreads) {
+    const int64_t p = in_lds ? (int64_t)lpos[j] : pos[j0 + j] - b0;
+    const int64_t o = bb + place((int32_t)p) + j0 + j;
+    ok2[o] = nk[j0 + j];
+    om2[o] = nv[j0 + j];
+  }
+}
+
 }  // namespace
 
 hipError_t launch_key_bits_remap(const uint32_t* src, int32_t Wo, int32_t Cm, const int32_t* d_remap, const MergeBreaks& brk,
@@ -308,6 +471,65 @@ hipError_t launch_merge_update(const int32_t* m1s, const int32_t* m2s, const int
   if (removed) kb.n = -1;
   hipLaunchKernelGGL(merge_write_kernel, dim3((unsigned)ntiles), dim3(kThreads), 0, s, m1s, m2s, cols, R, d_remap, kb,
                      d_base, nm1, nm2, ncol, ms->pos, ms->jbeg, o1, o2, oc);
+  return hipGetLastError();
+}
+
+hipError_t launch_order_merge(const unsigned long long* okey, const int32_t* om1, int64_t R, const int32_t* d_remap,
+                              bool removed, const MergeBreaks& brk, const int32_t* nm1, const int32_t* nm2,
+                              const int32_t* ncol, int64_t n, const int32_t* d_newcol, const int32_t* d_newat, int32_t D,
+                              MergeScratch* ms, OrderScratch* os, unsigned long long* ok2, int32_t* om2, int64_t* out_rows,
+                              hipStream_t s) {
+  const int64_t ntiles = R / kMergeTile + 1;
+  if (ntiles >= INT32_MAX / 2 || n >= INT32_MAX || (n > 0 && D <= 0)) return hipErrorInvalidValue;
+  hipError_t e;
+  if ((e = ms->reserve(n, (int32_t)ntiles)) != hipSuccess) return e;
+  const unsigned long long* nk = nullptr;
+  const int32_t* nv = nullptr;
+  if (n > 0) {
+    // the new rows in clip order: keys, then a radix sort of those rows alone (their count, not the DB's)
+    if ((e = os->nk.reserve(sizeof(unsigned long long) * n)) != hipSuccess || (e = os->nk2.reserve(sizeof(unsigned long long) * n)) != hipSuccess ||
+        (e = os->nv.reserve(sizeof(int32_t) * n)) != hipSuccess || (e = os->nv2.reserve(sizeof(int32_t) * n)) != hipSuccess)
+      return e;
+    const unsigned g = (unsigned)std::min<int64_t>(2048, (n + 255) / 256);
+    hipLaunchKernelGGL(order_new_keys_kernel, dim3(g), dim3(256), 0, s, nm1, nm2, ncol, n, os->nk.as<unsigned long long>(),
+                       os->nv.as<int32_t>());
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tb = 0;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, os->nk.as<unsigned long long>(), os->nk2.as<unsigned long long>(),
+                                                os->nv.as<int32_t>(), os->nv2.as<int32_t>(), (int)n, 0, 63, s)) != hipSuccess ||
+        (e = os->tmp.reserve(tb)) != hipSuccess)
+      return e;
+    tb = os->tmp.bytes;
+    if ((e = hipcub::DeviceRadixSort::SortPairs(os->tmp.p, tb, os->nk.as<unsigned long long>(), os->nk2.as<unsigned long long>(),
+                                                os->nv.as<int32_t>(), os->nv2.as<int32_t>(), (int)n, 0, 63, s)) != hipSuccess)
+      return e;
+    nk = os->nk2.as<unsigned long long>();
+    nv = os->nv2.as<int32_t>();
+    hipLaunchKernelGGL(order_pos_kernel, dim3(g), dim3(256), 0, s, okey, R, nk, n, d_newcol, d_newat, D, ms->pos);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(merge_tiles_kernel, dim3((unsigned)std::min<int64_t>(1024, (ntiles + 256) / 256)), dim3(256), 0, s,
+                     ms->pos, n, (int32_t)ntiles, ms->jbeg);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const int32_t* d_base = nullptr;
+  int64_t kept = R;
+  if (removed) {
+    hipLaunchKernelGGL(order_count_kept_kernel, dim3((unsigned)ntiles + 1), dim3(kThreads), 0, s, okey, R, d_remap,
+                       (int32_t)ntiles, ms->kept);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tb = ms->tmp_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ms->tmp, tb, ms->kept, ms->base, (int)ntiles + 1, s)) != hipSuccess) return e;
+    int32_t total = 0;
+    if ((e = hipMemcpyAsync(&total, ms->base + ntiles, sizeof total, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    kept = total;
+    d_base = ms->base;
+  }
+  MergeBreaks kb = brk;
+  if (removed) kb.n = -1;
+  hipLaunchKernelGGL(order_write_kernel, dim3((unsigned)ntiles), dim3(kThreads), 0, s, okey, om1, R, d_remap, kb, d_base, nk,
+                     nv, ms->pos, ms->jbeg, ok2, om2);
+  *out_rows = kept + n;
   return hipGetLastError();
 }
 

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "tfp_kernels.hpp"
+
 namespace tfp {
 
 constexpr int kMergeTile = 4096;  // old index rows per merge_write block
@@ -55,6 +57,23 @@ hipError_t launch_key_bits_remap(const uint32_t* src, int32_t Wo, int32_t Cm, co
                                  uint32_t* dst, int32_t Wn, hipStream_t s);
 hipError_t launch_key_bits_add(const int64_t* d_rng_all, const int32_t* m1s, const int32_t* nm1, const int32_t* ncol,
                                int64_t n, int32_t W, uint32_t* bits, hipStream_t s);
+
+// The clip order (tfp_kernels.hpp: okey / om1, R rows) carried through the same update (round 6): the
+// old rows' columns renumbered as the index's (remap or brk; removed clips' rows dropped), the
+// merge's n new rows (nm1, nm2, ncol, sorted by m1, ncol in the new numbering) sorted into clip
+// order alone and inserted. The D new clips: d_newcol (their new columns, ascending) and d_newat
+// (each one's insertion point among the old columns: the old columns with a smaller uuid), which
+// places a new clip's rows before the old columns at or after it within each key. ms: the index
+// merge's scratch, free again once that merge is queued. Output into ok2 / om2, *out_rows rows;
+// synchronous on s only when removed.
+struct OrderScratch {
+  CacheBuf nk, nk2, nv, nv2, tmp;
+};
+hipError_t launch_order_merge(const unsigned long long* okey, const int32_t* om1, int64_t R, const int32_t* d_remap,
+                              bool removed, const MergeBreaks& brk, const int32_t* nm1, const int32_t* nm2,
+                              const int32_t* ncol, int64_t n, const int32_t* d_newcol, const int32_t* d_newat, int32_t D,
+                              MergeScratch* ms, OrderScratch* os, unsigned long long* ok2, int32_t* om2, int64_t* out_rows,
+                              hipStream_t s);
 
 // ---- index delta (round 4) ---------------------------------------------------------------
 // The clips enrolled since the last build, searched beside the main index by the coefs = 1 vote

@@ -18,6 +18,13 @@ inline const char* knob(const char* name) {
   const char* on = getenv("TFP_TEST_KNOBS");
   return on && *on && strcmp(on, "0") != 0 ? getenv(name) : nullptr;
 }
+// The operational switches the public header and INTEGRATION.md document (TFP_COALESCE=0,
+// TFP_INDEX_DELTA=0, TFP_GROUP_STREAM=replicate): plain environment reads, TFP_TEST_KNOBS or not.
+// Each picks a form whose results are identical, so none can change what a search returns.
+inline const char* op_env(const char* name) {
+  const char* v = getenv(name);
+  return v && *v ? v : nullptr;
+}
 
 constexpr int kFramesPerBlock = 16;   // frames per wave tile of the generic kernel (16 lanes per frame)
 // Frames per wave tile of fingerprint8k_kernel's throughput launches. 16: the tile tail (deferred
@@ -25,6 +32,10 @@ constexpr int kFramesPerBlock = 16;   // frames per wave tile of the generic ker
 // buffer that lets 3 workgroups (3 waves/SIMD at <= 168 VGPRs) share a CU: 0.565 ms per C2
 // launch vs 0.536 (the LDS array is ~50 % busy at 2 waves/SIMD; a third wave adds contention).
 constexpr int kTile8k = 16;
+// fingerprint8k_kernel's throughput launches read a clip through a buffer resource whose range and
+// offsets are 32-bit byte counts: clips of this many samples or more take the generic kernel
+// (64-bit sample offsets) instead. (2^30 samples = 37 hours at 8 kHz.)
+constexpr int64_t kDirectMaxSamples = (int64_t(1) << 30) - (int64_t(1) << 16);
 constexpr int32_t kKeyOffset = 512;   // trunc(dB) key k stored at k + 512 (|k| <= 459)
 constexpr int32_t kKeyRange = 1024;
 
@@ -179,18 +190,45 @@ hipError_t launch_key_bits(const int64_t* d_rng_all, const int32_t* cols, int32_
 hipError_t launch_search_small(const double* d_q, const SmallQueries& sq, SearchConsts sc, const uint32_t* d_bits,
                                int32_t C, const int32_t* d_tiekey, SmallResult* h_out, hipStream_t s);
 
+// A grow-only device buffer (the clip-set cache's arrays and scratch): rebuilds reuse the space, so
+// no hipFree (which synchronises the device) runs between builds.
+struct CacheBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t reserve(size_t n);  // grow-only, 1/8 headroom
+  void release();
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+// The index rows in clip order (round 6, tfp_scan.hip): every row of the m1-sorted index as
+// key = t << 53 | column << 32 | (m2 ^ INT32_MIN), t = the key index (k + kKeyOffset, clamped to
+// [0, kKeyRange)) of the integer k nearest its max1 (floor((m1 + 500000) / 10^6)), ascending, with
+// the row's m1 beside it. For a tolerance below 1/2 the "%f" max1 box of key k lies inside the rows
+// whose nearest integer is k, so the clip-set cache at such a tolerance is a filter of this order
+// (rows whose m1 lies in their key's box), no sort: the order is built once (a radix sort) and
+// carried across index merges (launch_order_merge, tfp_index.hip).
+constexpr double kOrderMaxTol = 0.49;  // tolerances the order serves (fmt6(k +- tol) stays inside k's rows)
+hipError_t launch_order_fill(const int32_t* m1s, const int32_t* m2s, const int32_t* cols, int64_t R,
+                             unsigned long long* okey, int32_t* om1, hipStream_t s);
+hipError_t order_sort(const unsigned long long* kin, unsigned long long* kout, const int32_t* vin, int32_t* vout, int64_t n,
+                      CacheBuf* tmp, hipStream_t s);
+
 // General path (coefs = 2 and the vote's fallbacks; tfp_scan.hip). Clip-set cache of one index
-// version and tolerance, built from the key boxes' row ranges (d_rng_all, h_off = host prefix of
-// the box sizes, h_off[kKeyRange] = S rows in all boxes): per (key, clip) group the clip's max2
-// values in the key's box ("points", ascending), and the cell entries (key, cell, clip) of the
-// max2 axis cut into cells of width w. Not built (valid = false) past its limits: then every
-// frame takes the row scan.
+// version and tolerance: per (key, clip) group the clip's max2 values in the key's "%f" max1 box
+// ("points", ascending), the groups' clusters and the sweep's per-key window directory; and, for
+// the one-wave-per-frame cells form only (ensure_entries, built when that form first runs), the
+// cell entries (key, cell, clip) of the max2 axis cut into cells of width w. Built from the clip
+// order at tolerances up to kOrderMaxTol (build_from_order: hand-written filter / scan kernels), else
+// by sorting the boxes' rows (build). Not built (valid = false) past its limits: then every frame
+// takes the row scan.
 struct CellCache {
   static constexpr int32_t kMaxCols = 1 << 21;  // clip columns packed in 21 bits
   int32_t* p_m2 = nullptr;                 // [S] points of each group, ascending
+  uint32_t* k32 = nullptr;                 // [S] key << 21 | column of each point
   uint32_t* g_key = nullptr;               // [n1] key << 21 | column of each group, ascending
   int32_t* g_beg = nullptr;                // [n1 + 1] first point of each group
-  unsigned long long* e_key = nullptr;     // [n2] key << 52 | cell << 21 | column, ascending
+  unsigned long long* e_key = nullptr;     // [n2] key << 52 | cell << 21 | column, ascending (ensure_entries)
   int32_t* e_grp = nullptr;                // [n2] group of each entry
   int32_t* k_gbeg = nullptr;               // [kKeyRange + 1] first group of each key
   // Clusters (the sweep's form of the points): a group's points cut where consecutive points are
@@ -207,13 +245,26 @@ struct CellCache {
   int32_t nwin = 0;                        // ceil(columns / kWin)
   int64_t S = 0, n1 = 0, n2 = 0, w = 0, nc = 0, dgap = 0;
   bool valid = false;
+  bool entries = false;     // e_key / e_grp built
+  bool from_order = false;  // built by build_from_order (tests: tfp_index_cache_stats)
   hipError_t build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
                    int32_t ncols, int64_t nrows, double tole, hipStream_t s);
+  // from the clip order (okey, om1: n rows) at tolerance tole <= kOrderMaxTol; d_kbox = the keys'
+  // "%f" boxes at tole (launch_key_boxes)
+  hipError_t build_from_order(const unsigned long long* okey, const int32_t* om1, int64_t n, const int64_t* d_kbox,
+                              int32_t ncols, double tole, hipStream_t s);
+  hipError_t ensure_entries(hipStream_t s);
+  void invalidate() { valid = entries = from_order = false; S = n1 = n2 = nc = 0; }
   void release();
+  void swap(CellCache& o);
   CellCache() = default;
   CellCache(const CellCache&) = delete;
   CellCache& operator=(const CellCache&) = delete;
   ~CellCache() { release(); }
+
+ private:
+  CacheBuf b_p_m2, b_k32, b_g_key, b_g_beg, b_e_key, b_e_grp, b_k_gbeg, b_c_lo, b_c_hi, b_c_beg, b_kdir, b_tile;
+  void bind();  // the array pointers from the buffers
 };
 // Queries [q_begin, q_begin + nq) of the batch (frame boxes from prep_boxes, offsets d_qoff on the
 // device and h_qoff on the host); d_best[q] = (count << 32 | tie key), 0 = NOTFOUND.
@@ -241,7 +292,7 @@ struct WideScratch {
   uint32_t* ptot = nullptr;                          // [nchunks][256][kChunk / 2] the prefix counts' per-share totals, then their prefix
   int32_t* seg = nullptr;                            // [nchunks][2 * kKeyRange][2] sorted range
   int32_t* cbeg = nullptr;                           // [nchunks + 1] first sorted frame of each chunk
-  int32_t* info = nullptr;                           // [3]: frames kept, ineligible frames, wide windows
+  int32_t* info = nullptr;                           // [4]: frames kept, ineligible frames, wide windows, crowd bins
   int32_t* doff = nullptr;                           // [nchunks * kKeyRange + 1] each window segment's directory offset
   int32_t* dtab = nullptr;                           // [<= 4 nf] segment directories: first frame per L2 / U2 bucket
   void* tmp = nullptr;
@@ -265,7 +316,8 @@ struct WideScratch {
   // per chunk and bin the frame count and first sorted frame, each window segment's first / last
   // L2 and U2
   uint32_t* segstat = nullptr;
-  int32_t *ghist = nullptr, *bstart = nullptr, *segc = nullptr;
+  int32_t *ghist = nullptr, *bstart = nullptr;
+  int4* segk = nullptr;  // per (chunk, window segment): {min L2, min U2, bucket shift, directory offset}
   int4* gi4 = nullptr;                               // sort groups per chunk (tfp_scan.hip wide_bin_scan)
   int32_t* gb = nullptr;
   int64_t cap_groups = 0;

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "tfp_kernels.hpp"
+#include "tfp_bsearch.hpp"
 #include "tfp_math.hpp"
 
 namespace tfp {
@@ -182,26 +183,406 @@ hipError_t dmalloc(T** p, int64_t n) {
 
 }  // namespace
 
+namespace {
+
+// ---- the clip order and the cache built from it (round 6) ----------------------------------
+// Tiles of 4096 items, 16 per thread of 256, item b0 + k * 256 + t (coalesced loads); a tile's
+// exclusive prefix of a per-item flag in item order: chunk k, then wave, then lane.
+constexpr int kOT = 256;
+constexpr int kOPer = 16;
+constexpr int kOTile = kOT * kOPer;
+
+// The key index of the integer nearest m1 (micro-units): floor((m1 + 500000) / 10^6) + kKeyOffset,
+// clamped to [0, kKeyRange). A clamped row lies in no box of its key (|k| > 511 dB away).
+__device__ __forceinline__ uint32_t order_key_index(int32_t m1) {
+  const int64_t v = (int64_t)m1 + 500000;
+  const int64_t k = (v >= 0 ? v : v - 999999) / 1000000 + kKeyOffset;
+  return (uint32_t)(k < 0 ? 0 : k >= kKeyRange ? kKeyRange - 1 : k);
+}
+
+__global__ void order_fill_kernel(const int32_t* __restrict__ m1s, const int32_t* __restrict__ m2s,
+                                  const int32_t* __restrict__ cols, int64_t R, unsigned long long* __restrict__ okey,
+                                  int32_t* __restrict__ om1) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t m1 = m1s[i];
+    okey[i] = ((unsigned long long)order_key_index(m1) << 53) | ((unsigned long long)(uint32_t)cols[i] << 32) |
+              (uint32_t)(m2s[i] ^ INT32_MIN);
+    om1[i] = m1;
+  }
+}
+
+// Is order row i a point at this tolerance (its m1 inside its key's "%f" box)?
+__device__ __forceinline__ bool order_point(unsigned long long key, int32_t m1, const int64_t* __restrict__ kbox) {
+  const uint32_t t = (uint32_t)(key >> 53);
+  return (int64_t)m1 >= kbox[2 * t] && (int64_t)m1 <= kbox[2 * t + 1];
+}
+
+// In-tile exclusive prefix of the flags bits (bit k: item k * 256 + t) into pre[], via ballots and
+// 64 partial sums in csum (LDS, [kOPer][4]). Every thread of the tile calls it.
+__device__ __forceinline__ void tile_prefix(uint32_t bits, int32_t (&pre)[kOPer], int32_t (*csum)[kOT / 64]) {
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  uint32_t lo[kOPer];
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) {
+    const uint64_t m = __ballot((bits >> k) & 1u);
+    lo[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) csum[k][wv] = __popcll(m);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int32_t run = 0;
+    for (int k = 0; k < kOPer; k++)
+      for (int w = 0; w < kOT / 64; w++) {
+        const int32_t v = csum[k][w];
+        csum[k][w] = run;
+        run += v;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) pre[k] = csum[k][wv] + (int32_t)lo[k];
+  __syncthreads();  // (csum is reused by the caller's next call)
+}
+
+// Points per tile of the order (the tile's count into cnt[tile]).
+__global__ __launch_bounds__(kOT) void order_count_kernel(const unsigned long long* __restrict__ okey,
+                                                          const int32_t* __restrict__ om1, int64_t n,
+                                                          const int64_t* __restrict__ kbox, int32_t* __restrict__ cnt) {
+  __shared__ int32_t wsum[kOT / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
+  int32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) {
+    const int64_t i = b0 + k * kOT + threadIdx.x;
+    if (i < n) c += order_point(okey[i], om1[i], kbox);
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = 0;
+    for (int w = 0; w < kOT / 64; w++) t += wsum[w];
+    cnt[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan, in place, of nvec vectors of ntiles counts each (vector v at cnt + v (ntiles + 1));
+// each vector's total lands in its element ntiles. One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void tile_scan_kernel(int32_t* __restrict__ cnt, int32_t ntiles, int32_t nvec) {
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  const int32_t per = (ntiles + 1023) / 1024;
+  for (int32_t v = 0; v < nvec; v++) {
+    int32_t* c = cnt + (int64_t)v * (ntiles + 1);
+    const int32_t a = t * per, e = min(ntiles, a + per);
+    int32_t sum = 0;
+    for (int32_t i = a; i < e; i++) sum += c[i];
+    part[t] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the partial sums
+      const int32_t x = t >= o ? part[t - o] : 0;
+      __syncthreads();
+      part[t] += x;
+      __syncthreads();
+    }
+    int32_t run = part[t] - sum;
+    for (int32_t i = a; i < e; i++) {
+      const int32_t x = c[i];
+      c[i] = run;
+      run += x;
+    }
+    if (t == 1023) c[ntiles] = part[1023];
+    __syncthreads();
+  }
+}
+
+// The points: every order row inside its key's box, in order (p_m2 = its m2, k32 = key << 21 | col).
+__global__ __launch_bounds__(kOT) void order_points_kernel(const unsigned long long* __restrict__ okey,
+                                                           const int32_t* __restrict__ om1, int64_t n,
+                                                           const int64_t* __restrict__ kbox, const int32_t* __restrict__ off,
+                                                           int32_t* __restrict__ p_m2, uint32_t* __restrict__ k32) {
+  __shared__ int32_t csum[kOPer][kOT / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
+  unsigned long long key[kOPer];
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) {
+    const int64_t i = b0 + k * kOT + threadIdx.x;
+    key[k] = i < n ? okey[i] : 0ull;
+    if (i < n && order_point(key[k], om1[i], kbox)) bits |= 1u << k;
+  }
+  int32_t pre[kOPer];
+  tile_prefix(bits, pre, csum);
+  const int32_t base = off[blockIdx.x];
+#pragma unroll
+  for (int k = 0; k < kOPer; k++)
+    if ((bits >> k) & 1u) {
+      const int32_t j = base + pre[k];
+      p_m2[j] = (int32_t)((uint32_t)key[k] ^ 0x80000000u);
+      k32[j] = (uint32_t)(key[k] >> 32);  // key << 21 | column
+    }
+}
+
+// Point j starts a group when its (key, column) differs from point j - 1's, a cluster when it starts a
+// group or lies more than dgap above its predecessor.
+__device__ __forceinline__ void point_starts(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32, int64_t j,
+                                             int64_t dgap, bool& gs, bool& cs) {
+  gs = j == 0 || k32[j] != k32[j - 1];
+  cs = gs || (int64_t)p_m2[j] - (int64_t)p_m2[j - 1] > dgap;
+}
+
+__global__ __launch_bounds__(kOT) void point_count_kernel(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32,
+                                                          int64_t S, int64_t dgap, int32_t ntiles,
+                                                          int32_t* __restrict__ cnt) {
+  __shared__ int32_t wsum[2][kOT / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
+  int32_t g = 0, c = 0;
+#pragma unroll 4
+  for (int k = 0; k < kOPer; k++) {
+    const int64_t j = b0 + k * kOT + threadIdx.x;
+    if (j < S) {
+      bool gs, cs;
+      point_starts(p_m2, k32, j, dgap, gs, cs);
+      g += gs;
+      c += cs;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    g += __shfl_xor(g, o, 64);
+    c += __shfl_xor(c, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wsum[0][threadIdx.x >> 6] = g;
+    wsum[1][threadIdx.x >> 6] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t tg = 0, tc = 0;
+    for (int w = 0; w < kOT / 64; w++) {
+      tg += wsum[0][w];
+      tc += wsum[1][w];
+    }
+    cnt[blockIdx.x] = tg;
+    cnt[ntiles + 1 + blockIdx.x] = tc;
+  }
+}
+
+// Groups and clusters of the points: g_key / g_beg / c_beg per group, c_lo / c_hi per cluster;
+// the point S - 1 closes the arrays (g_beg[n1] = S, c_beg[n1] = nc).
+__global__ __launch_bounds__(kOT) void point_groups_kernel(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32,
+                                                           int64_t S, int64_t dgap, int32_t ntiles,
+                                                           const int32_t* __restrict__ off, uint32_t* __restrict__ g_key,
+                                                           int32_t* __restrict__ g_beg, int32_t* __restrict__ c_beg,
+                                                           int32_t* __restrict__ c_lo, int32_t* __restrict__ c_hi) {
+  __shared__ int32_t csum[kOPer][kOT / 64];
+  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
+  uint32_t gbits = 0, cbits = 0;
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) {
+    const int64_t j = b0 + k * kOT + threadIdx.x;
+    if (j < S) {
+      bool gs, cs;
+      point_starts(p_m2, k32, j, dgap, gs, cs);
+      gbits |= (uint32_t)gs << k;
+      cbits |= (uint32_t)cs << k;
+    }
+  }
+  int32_t gpre[kOPer], cpre[kOPer];
+  tile_prefix(gbits, gpre, csum);
+  tile_prefix(cbits, cpre, csum);
+  const int32_t gb = off[blockIdx.x], cb = off[ntiles + 1 + blockIdx.x];
+  const int32_t n1 = off[ntiles], nc = off[2 * (ntiles + 1) - 1];
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) {
+    const int64_t j = b0 + k * kOT + threadIdx.x;
+    if (j >= S) continue;
+    const bool gs = (gbits >> k) & 1u, cs = (cbits >> k) & 1u;
+    const int32_t c = cb + cpre[k] + (int32_t)cs - 1;  // this point's cluster
+    const int32_t v = p_m2[j];
+    if (gs) {
+      const int32_t g = gb + gpre[k];
+      g_key[g] = k32[j];
+      g_beg[g] = (int32_t)j;
+      c_beg[g] = c;
+    }
+    if (cs) c_lo[c] = v;
+    bool end = j == S - 1;
+    if (!end) {
+      bool gs1, cs1;
+      point_starts(p_m2, k32, j + 1, dgap, gs1, cs1);
+      end = cs1;
+    }
+    if (end) c_hi[c] = v;
+    if (j == S - 1) {
+      g_beg[n1] = (int32_t)S;
+      c_beg[n1] = nc;
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t CacheBuf::reserve(size_t n) {
+  if (n <= bytes) return hipSuccess;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+  const size_t want = std::max<size_t>(256, n + n / 8);
+  const hipError_t e = hipMalloc(&p, want);
+  if (e == hipSuccess) bytes = want;
+  return e;
+}
+
+void CacheBuf::release() {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  bytes = 0;
+}
+
+hipError_t launch_order_fill(const int32_t* m1s, const int32_t* m2s, const int32_t* cols, int64_t R,
+                             unsigned long long* okey, int32_t* om1, hipStream_t s) {
+  if (R <= 0) return hipSuccess;
+  hipLaunchKernelGGL(order_fill_kernel, dim3(grid_for(R)), dim3(256), 0, s, m1s, m2s, cols, R, okey, om1);
+  return hipGetLastError();
+}
+
+// The order's one sort (per full build; merges carry it): hipCUB's radix sort of the 63-bit keys
+// with m1 beside them.
+hipError_t order_sort(const unsigned long long* kin, unsigned long long* kout, const int32_t* vin, int32_t* vout, int64_t n,
+                      CacheBuf* tmp, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (n >= INT32_MAX) return hipErrorInvalidValue;
+  size_t tb = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb, kin, kout, vin, vout, (int)n, 0, 63, s);
+  if (e != hipSuccess) return e;
+  if ((e = tmp->reserve(tb)) != hipSuccess) return e;
+  tb = tmp->bytes;
+  return hipcub::DeviceRadixSort::SortPairs(tmp->p, tb, kin, kout, vin, vout, (int)n, 0, 63, s);
+}
+
+void CellCache::bind() {
+  p_m2 = b_p_m2.as<int32_t>();
+  k32 = b_k32.as<uint32_t>();
+  g_key = b_g_key.as<uint32_t>();
+  g_beg = b_g_beg.as<int32_t>();
+  e_key = b_e_key.as<unsigned long long>();
+  e_grp = b_e_grp.as<int32_t>();
+  k_gbeg = b_k_gbeg.as<int32_t>();
+  c_lo = b_c_lo.as<int32_t>();
+  c_hi = b_c_hi.as<int32_t>();
+  c_beg = b_c_beg.as<int32_t>();
+  kdir = b_kdir.as<int32_t>();
+}
+
 void CellCache::release() {
-  for (void* p : {(void*)p_m2, (void*)g_key, (void*)g_beg, (void*)e_key, (void*)e_grp, (void*)k_gbeg, (void*)c_lo,
-                  (void*)c_hi, (void*)c_beg, (void*)kdir})
-    if (p) (void)hipFree(p);
-  c_lo = c_hi = c_beg = kdir = nullptr;
+  for (CacheBuf* b : {&b_p_m2, &b_k32, &b_g_key, &b_g_beg, &b_e_key, &b_e_grp, &b_k_gbeg, &b_c_lo, &b_c_hi, &b_c_beg, &b_kdir,
+                      &b_tile})
+    b->release();
+  bind();
+  invalidate();
   nwin = 0;
-  nc = dgap = 0;
-  p_m2 = nullptr;
-  g_key = nullptr;
-  g_beg = nullptr;
-  e_key = nullptr;
-  e_grp = nullptr;
-  k_gbeg = nullptr;
-  S = n1 = n2 = 0;
-  valid = false;
+  w = dgap = 0;
+}
+
+void CellCache::swap(CellCache& o) {
+  std::swap(b_p_m2, o.b_p_m2);
+  std::swap(b_k32, o.b_k32);
+  std::swap(b_g_key, o.b_g_key);
+  std::swap(b_g_beg, o.b_g_beg);
+  std::swap(b_e_key, o.b_e_key);
+  std::swap(b_e_grp, o.b_e_grp);
+  std::swap(b_k_gbeg, o.b_k_gbeg);
+  std::swap(b_c_lo, o.b_c_lo);
+  std::swap(b_c_hi, o.b_c_hi);
+  std::swap(b_c_beg, o.b_c_beg);
+  std::swap(b_kdir, o.b_kdir);
+  std::swap(b_tile, o.b_tile);
+  std::swap(nwin, o.nwin);
+  std::swap(S, o.S);
+  std::swap(n1, o.n1);
+  std::swap(n2, o.n2);
+  std::swap(w, o.w);
+  std::swap(nc, o.nc);
+  std::swap(dgap, o.dgap);
+  std::swap(valid, o.valid);
+  std::swap(entries, o.entries);
+  std::swap(from_order, o.from_order);
+  bind();
+  o.bind();
+}
+
+// The per-key window directory and each key's first group (both build forms).
+static hipError_t cache_directory(CellCache* c, int32_t ncols, hipStream_t s, CacheBuf* b_k_gbeg, CacheBuf* b_kdir) {
+  hipError_t e;
+  if ((e = b_k_gbeg->reserve(sizeof(int32_t) * (kKeyRange + 1))) != hipSuccess) return e;
+  c->nwin = (ncols + CellCache::kWin - 1) / CellCache::kWin;
+  if ((e = b_kdir->reserve(sizeof(int32_t) * (size_t)kKeyRange * (c->nwin + 1))) != hipSuccess) return e;
+  hipLaunchKernelGGL(key_gbeg_kernel, dim3((kKeyRange + 256) / 256), dim3(256), 0, s, c->g_key, c->n1,
+                     b_k_gbeg->as<int32_t>());
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(cluster_kdir_kernel, dim3(grid_for((int64_t)kKeyRange * (c->nwin + 1))), dim3(256), 0, s, c->g_key,
+                     b_k_gbeg->as<int32_t>(), c->nwin, b_kdir->as<int32_t>());
+  return hipGetLastError();
+}
+
+hipError_t CellCache::build_from_order(const unsigned long long* okey, const int32_t* om1, int64_t n, const int64_t* d_kbox,
+                                       int32_t ncols, double tole, hipStream_t s) {
+  invalidate();
+  if (!(tole >= 0.0 && tole <= kOrderMaxTol) || ncols > kMaxCols || n <= 0 || n >= INT32_MAX) return hipSuccess;
+  w = (int64_t)ceil(2.0 * tole * 1e6) + 4;  // >= U2 - L2 of every fmt6 max2 window at this tolerance
+  dgap = std::max<int64_t>(0, (int64_t)floor(2.0 * tole * 1e6) - 3);
+  const int32_t nt = (int32_t)((n + kOTile - 1) / kOTile);
+  hipError_t e;
+  if ((e = b_tile.reserve(sizeof(int32_t) * 2 * ((size_t)nt + 1))) != hipSuccess) return e;
+  int32_t* cnt = b_tile.as<int32_t>();
+  // 1. the points: a count per tile, their offsets, the filter
+  hipLaunchKernelGGL(order_count_kernel, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, nt, 1);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  int32_t tot[2] = {0, 0};
+  if ((e = hipMemcpyAsync(&tot[0], cnt + nt, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess)
+    return e;
+  S = tot[0];
+  if (S <= 0) {
+    S = 0;
+    return hipSuccess;  // no row in any box: the row scan (which finds none either)
+  }
+  if ((e = b_p_m2.reserve(sizeof(int32_t) * (size_t)S)) != hipSuccess || (e = b_k32.reserve(sizeof(uint32_t) * (size_t)S)) != hipSuccess)
+    return e;
+  bind();
+  hipLaunchKernelGGL(order_points_kernel, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt, p_m2, k32);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // 2. groups and clusters: two counts per tile, their offsets, then the arrays
+  const int32_t nt2 = (int32_t)((S + kOTile - 1) / kOTile);
+  hipLaunchKernelGGL(point_count_kernel, dim3((unsigned)nt2), dim3(kOT), 0, s, p_m2, k32, S, dgap, nt2, cnt);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, nt2, 2);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(&tot[0], cnt + nt2, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipMemcpyAsync(&tot[1], cnt + 2 * (nt2 + 1) - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+      (e = hipStreamSynchronize(s)) != hipSuccess)
+    return e;
+  n1 = tot[0];
+  nc = tot[1];
+  if ((e = b_g_key.reserve(sizeof(uint32_t) * (size_t)n1)) != hipSuccess ||
+      (e = b_g_beg.reserve(sizeof(int32_t) * (size_t)(n1 + 1))) != hipSuccess ||
+      (e = b_c_beg.reserve(sizeof(int32_t) * (size_t)(n1 + 1))) != hipSuccess ||
+      (e = b_c_lo.reserve(sizeof(int32_t) * (size_t)nc)) != hipSuccess || (e = b_c_hi.reserve(sizeof(int32_t) * (size_t)nc)) != hipSuccess)
+    return e;
+  bind();
+  hipLaunchKernelGGL(point_groups_kernel, dim3((unsigned)nt2), dim3(kOT), 0, s, p_m2, k32, S, dgap, nt2, cnt, g_key, g_beg,
+                     c_beg, c_lo, c_hi);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = cache_directory(this, ncols, s, &b_k_gbeg, &b_kdir)) != hipSuccess) return e;
+  bind();
+  valid = true;
+  from_order = true;
+  return hipSuccess;
 }
 
 hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, const int32_t* m2s, const int32_t* cols,
                             int32_t ncols, int64_t nrows, double tole, hipStream_t s) {
-  release();
+  invalidate();
   S = h_off[kKeyRange];
   // limits of the packed keys and of hipcub's 32-bit counts; beyond them every frame takes the
   // row scan (correct, slower)
@@ -210,10 +591,12 @@ hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, cons
     return hipSuccess;
   }
   w = (int64_t)ceil(2.0 * tole * 1e6) + 4;  // >= U2 - L2 of every fmt6 max2 window at this tolerance
+  dgap = std::max<int64_t>(0, (int64_t)floor(2.0 * tole * 1e6) - 3);
+  // (tolerances above kOrderMaxTol only: a max1 box then spans several keys' rows of the clip
+  // order, so the boxes' rows are sorted here; the scratch is allocated for the build alone)
   hipError_t e;
   int64_t* d_off = nullptr;
-  unsigned long long *ka = nullptr, *kb = nullptr, *ea = nullptr, *eb = nullptr;
-  uint32_t* k32 = nullptr;
+  unsigned long long *ka = nullptr, *kb = nullptr;
   int32_t *glen = nullptr, *ga = nullptr, *gb = nullptr;
   int64_t* d_n = nullptr;
   void* tmp = nullptr;
@@ -229,94 +612,106 @@ hipError_t CellCache::build(const int64_t* d_rng_all, const int64_t* h_off, cons
   TFP_TRY(dmalloc(&ka, S));
   TFP_TRY(dmalloc(&kb, S));
   TFP_TRY(dmalloc(&d_n, 2));
+  TFP_TRY(dmalloc(&glen, S + 1));
   hipLaunchKernelGGL(cells_fill_kernel, dim3(grid_for(S)), dim3(256), 0, s, d_rng_all, d_off, m2s, cols, S, ka);
   TFP_TRY(hipGetLastError());
   // (key, col, m2) order: the groups, each group's points ascending
   TFP_TRY(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, ka, kb, (int)S, 0, 63, s));
   tb = t1;
-  TFP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, t1, k32, k32, glen, d_n, (int)S, s));
-  tb = t1 > tb ? t1 : tb;
-  TFP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, ea, eb, ga, gb, (int)(2 * S), 0, 62, s));
-  tb = t1 > tb ? t1 : tb;
-  TFP_TRY(hipcub::DeviceSelect::UniqueByKey(nullptr, t1, eb, gb, ea, ga, d_n + 1, (int)(2 * S), s));
+  TFP_TRY(hipcub::DeviceRunLengthEncode::Encode(nullptr, t1, k32, g_key, glen, d_n, (int)S, s));
   tb = t1 > tb ? t1 : tb;
   TFP_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, t1, glen, glen, (int)S, s));
   tb = t1 > tb ? t1 : tb;
   TFP_TRY(hipMalloc(&tmp, tb > 0 ? tb : 1));
   TFP_TRY(hipcub::DeviceRadixSort::SortKeys(tmp, tb, ka, kb, (int)S, 0, 63, s));
-  TFP_TRY(dmalloc(&p_m2, S));
-  TFP_TRY(dmalloc(&k32, S));
+  TFP_TRY(b_p_m2.reserve(sizeof(int32_t) * (size_t)S));
+  TFP_TRY(b_k32.reserve(sizeof(uint32_t) * (size_t)S));
+  TFP_TRY(b_g_key.reserve(sizeof(uint32_t) * (size_t)S));
+  bind();
   hipLaunchKernelGGL(cells_split_kernel, dim3(grid_for(S)), dim3(256), 0, s, kb, S, p_m2, k32);
   TFP_TRY(hipGetLastError());
-  (void)hipFree(ka);
-  (void)hipFree(kb);
-  ka = kb = nullptr;
-  TFP_TRY(dmalloc(&g_key, S));
-  TFP_TRY(dmalloc(&glen, S + 1));
   TFP_TRY(hipcub::DeviceRunLengthEncode::Encode(tmp, tb, k32, g_key, glen, d_n, (int)S, s));
   TFP_TRY(hipMemcpyAsync(nn, d_n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   TFP_TRY(hipStreamSynchronize(s));
   n1 = nn[0];
   // group offsets: exclusive sum of the run lengths, g_beg[n1] = S
-  TFP_TRY(dmalloc(&g_beg, n1 + 1));
+  TFP_TRY(b_g_beg.reserve(sizeof(int32_t) * (size_t)(n1 + 1)));
+  bind();
   TFP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, glen, g_beg, (int)n1, s));
-  TFP_TRY(hipMemcpyAsync(g_beg + n1, &S, sizeof(int32_t), hipMemcpyHostToDevice, s));  // S < 2^31
-  TFP_TRY(dmalloc(&k_gbeg, kKeyRange + 1));
-  hipLaunchKernelGGL(key_gbeg_kernel, dim3((kKeyRange + 256) / 256), dim3(256), 0, s, g_key, n1, k_gbeg);
-  TFP_TRY(hipGetLastError());
-  (void)hipFree(glen);
-  glen = nullptr;
-  // the sweep's clusters: flags into ga, their prefix into gb (both reallocated below)
-  dgap = std::max<int64_t>(0, (int64_t)floor(2.0 * tole * 1e6) - 3);
-  TFP_TRY(dmalloc(&ga, S));
-  TFP_TRY(dmalloc(&gb, S));
-  hipLaunchKernelGGL(cluster_flag_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, k32, S, dgap, ga);
-  TFP_TRY(hipGetLastError());
-  TFP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ga, gb, (int)S, s));
   {
+    const int32_t S32 = (int32_t)S;  // S < 2^31
+    TFP_TRY(hipMemcpyAsync(g_beg + n1, &S32, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    // the sweep's clusters: flags into ga, their prefix into gb
+    TFP_TRY(dmalloc(&ga, S));
+    TFP_TRY(dmalloc(&gb, S));
+    hipLaunchKernelGGL(cluster_flag_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, k32, S, dgap, ga);
+    TFP_TRY(hipGetLastError());
+    TFP_TRY(hipcub::DeviceScan::ExclusiveSum(tmp, tb, ga, gb, (int)S, s));
     int32_t last[2] = {0, 0};
     TFP_TRY(hipMemcpyAsync(&last[0], gb + S - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     TFP_TRY(hipMemcpyAsync(&last[1], ga + S - 1, sizeof(int32_t), hipMemcpyDeviceToHost, s));
-    TFP_TRY(hipStreamSynchronize(s));
+    TFP_TRY(hipStreamSynchronize(s));  // (also: S32 was read)
     nc = (int64_t)last[0] + last[1];
   }
-  TFP_TRY(dmalloc(&c_lo, nc));
-  TFP_TRY(dmalloc(&c_hi, nc));
-  TFP_TRY(dmalloc(&c_beg, n1 + 1));
+  TFP_TRY(b_c_lo.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(nc, 1)));
+  TFP_TRY(b_c_hi.reserve(sizeof(int32_t) * (size_t)std::max<int64_t>(nc, 1)));
+  TFP_TRY(b_c_beg.reserve(sizeof(int32_t) * (size_t)(n1 + 1)));
+  bind();
   hipLaunchKernelGGL(cluster_write_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, ga, gb, S, c_lo, c_hi);
   hipLaunchKernelGGL(cluster_gbeg_kernel, dim3(grid_for(n1 + 1)), dim3(256), 0, s, g_beg, gb, n1, S, nc, c_beg);
   TFP_TRY(hipGetLastError());
-  nwin = (ncols + kWin - 1) / kWin;
-  TFP_TRY(dmalloc(&kdir, (int64_t)kKeyRange * (nwin + 1)));
-  hipLaunchKernelGGL(cluster_kdir_kernel, dim3(grid_for((int64_t)kKeyRange * (nwin + 1))), dim3(256), 0, s, g_key, k_gbeg, nwin,
-                     kdir);
-  TFP_TRY(hipGetLastError());
-  TFP_TRY(hipStreamSynchronize(s));
-  (void)hipFree(ga);
-  (void)hipFree(gb);
-  ga = gb = nullptr;
-  TFP_TRY(dmalloc(&ea, 2 * S));
-  TFP_TRY(dmalloc(&eb, 2 * S));
-  TFP_TRY(dmalloc(&ga, 2 * S));
-  TFP_TRY(dmalloc(&gb, 2 * S));
-  hipLaunchKernelGGL(cells_entries_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, k32, S, g_key, n1, w, ea, ga);
-  TFP_TRY(hipGetLastError());
-  TFP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, ea, eb, ga, gb, (int)(2 * S), 0, 62, s));
-  TFP_TRY(hipcub::DeviceSelect::UniqueByKey(tmp, tb, eb, gb, ea, ga, d_n + 1, (int)(2 * S), s));
-  TFP_TRY(hipMemcpyAsync(nn + 1, d_n + 1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
-  TFP_TRY(hipStreamSynchronize(s));
-  n2 = nn[1];
-  e_key = ea;
-  e_grp = ga;
-  ea = nullptr;
-  ga = nullptr;
+  TFP_TRY(cache_directory(this, ncols, s, &b_k_gbeg, &b_kdir));
+  bind();
+  TFP_TRY(hipStreamSynchronize(s));  // (the scratch is freed below)
   valid = true;
 out:
 #undef TFP_TRY
-  for (void* p : {(void*)d_off, (void*)ka, (void*)kb, (void*)ea, (void*)eb, (void*)k32, (void*)glen, (void*)ga,
-                  (void*)gb, (void*)d_n, tmp})
+  for (void* p : {(void*)d_off, (void*)ka, (void*)kb, (void*)glen, (void*)ga, (void*)gb, (void*)d_n, tmp})
     if (p) (void)hipFree(p);
-  if (e != hipSuccess) release();
+  if (e != hipSuccess) invalidate();
+  return e;
+}
+
+// The cell entries (the one-wave-per-frame cells form's candidates: two per point, its own cell j
+// and j - 1, deduplicated per (key, cell, column)), built when that form first runs on this cache.
+hipError_t CellCache::ensure_entries(hipStream_t s) {
+  if (!valid || entries) return hipSuccess;
+  if (2 * S >= INT32_MAX) return hipErrorInvalidValue;
+  hipError_t e;
+  unsigned long long* eb = nullptr;
+  int32_t* gb = nullptr;
+  int64_t* d_n = nullptr;
+  void* tmp = nullptr;
+  size_t tb = 0, t1 = 0;
+  int64_t nn = 0;
+#define TFP_TRY(x)               \
+  do {                           \
+    e = (x);                     \
+    if (e != hipSuccess) goto out; \
+  } while (0)
+  TFP_TRY(b_e_key.reserve(sizeof(unsigned long long) * (size_t)(2 * S)));
+  TFP_TRY(b_e_grp.reserve(sizeof(int32_t) * (size_t)(2 * S)));
+  bind();
+  TFP_TRY(dmalloc(&eb, 2 * S));
+  TFP_TRY(dmalloc(&gb, 2 * S));
+  TFP_TRY(dmalloc(&d_n, 1));
+  TFP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, e_key, eb, e_grp, gb, (int)(2 * S), 0, 62, s));
+  tb = t1;
+  TFP_TRY(hipcub::DeviceSelect::UniqueByKey(nullptr, t1, eb, gb, e_key, e_grp, d_n, (int)(2 * S), s));
+  tb = t1 > tb ? t1 : tb;
+  TFP_TRY(hipMalloc(&tmp, tb > 0 ? tb : 1));
+  hipLaunchKernelGGL(cells_entries_kernel, dim3(grid_for(S)), dim3(256), 0, s, p_m2, k32, S, g_key, n1, w, e_key, e_grp);
+  TFP_TRY(hipGetLastError());
+  TFP_TRY(hipcub::DeviceRadixSort::SortPairs(tmp, tb, e_key, eb, e_grp, gb, (int)(2 * S), 0, 62, s));
+  TFP_TRY(hipcub::DeviceSelect::UniqueByKey(tmp, tb, eb, gb, e_key, e_grp, d_n, (int)(2 * S), s));
+  TFP_TRY(hipMemcpyAsync(&nn, d_n, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  TFP_TRY(hipStreamSynchronize(s));
+  n2 = nn;
+  entries = true;
+out:
+#undef TFP_TRY
+  for (void* p : {(void*)eb, (void*)gb, (void*)d_n, tmp})
+    if (p) (void)hipFree(p);
   return e;
 }
 
@@ -550,7 +945,7 @@ __global__ void wide_frame_query_kernel(const int64_t* __restrict__ qoff, int32_
                                         unsigned long long* __restrict__ best, uint32_t* __restrict__ segstat,
                                         int32_t* __restrict__ ghist, int64_t nghist) {
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, nt = (int64_t)gridDim.x * blockDim.x;
-  if (tid < 3) info[tid] = 0;
+  if (tid < 4) info[tid] = 0;
   for (int64_t i = tid; i < nseg; i += nt) seg[i] = 0;
   if (segstat) {  // (nseg / 2 segments of 3 words)
     for (int64_t i = tid; i < 3 * (nseg / 2); i += nt) segstat[i] = i % 3 == 1 ? 0xffffffffu : 0u;
@@ -821,13 +1216,13 @@ __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* _
 
 // The directories, from the sorted frames: frame i of a window segment is the first frame of the
 // buckets after its predecessor's bucket up to its own (each bucket written once), the last frame
-// also fills the buckets after its own with se. Lanes write short runs themselves; a long run (a
+// also fills the buckets after its own with se; the first writes the segment's constants (segk). Lanes write short runs themselves; a long run (a
 // sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
 // buckets per step, so no lane loops over thousands of buckets alone.
 __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
                                      int segshift, const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
                                      const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
-                                     int32_t* __restrict__ dtab) {
+                                     int32_t* __restrict__ dtab, int4* __restrict__ segk) {
   constexpr int32_t kShort = 8;
   const int64_t n = *pn;
   const int lane = threadIdx.x & 63;
@@ -849,6 +1244,7 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
         const int32_t l2min = L2s[sb], u2min = U2s[sb];
         const int shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
         const int32_t t0 = doff[ch * kKeyRange + skey];
+        if (i == sb) segk[ch * kKeyRange + skey] = make_int4(l2min, u2min, shf, t0);  // (wide_clips' constants)
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           const int64_t mn = h ? u2min : l2min;
@@ -888,10 +1284,10 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
 // place in it; wide_bin_scan (a workgroup per chunk) scans the counts into each bin's first frame
 // and writes the segment table, the directory offsets, the used keys and the non-empty bins;
 // wide_bin_scatter moves the keys to their places; one wave sorts each bin in registers or LDS
-// and writes the sorted windows, queries and segment of each frame (wide_bin_sort); the
-// directories are filled from those with a per-segment constants table (wide_dir_fill_bins).
+// and writes the sorted windows, queries and segment of each frame and the directory runs of its
+// window segment (wide_bin_sort, with wide_bin_scan's per-segment constants, segk).
 // Chunk ch's kept frames occupy [cbeg[ch], cbeg[ch] + kept) of the sorted arrays; the rest of its
-// input range holds no frame of a segment (query 0, segment -1), so the prefix counts run over the
+// input range holds no frame of a segment (query 0), so the prefix counts run over the
 // whole range. A bin whose frames all share (segment, L2, d), or whose segment has no max2 window,
 // is not sorted (any order counts the same). Any other bin above kBinCap frames sets info[2],
 // which sends the speculative batch to the library sort (as a window width outside the key's delta
@@ -1021,17 +1417,18 @@ __global__ __launch_bounds__(1024) void wide_bin_hist_kernel(const int64_t* __re
 
 // One workgroup per chunk: the bin counts scanned into each bin's first frame (bstart, relative to
 // cbeg[ch]), the sort groups (gi4, gb: wide_bin_sort), the segment table, the directory offsets
-// (chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
-// the table's size per frame), the used keys, the chunk's
-// tail of non-frames, and cbeg.
+// (in segk; chunk ch's directories at (4 << kDirScale) cbeg[ch]: 2 NB <= (4 << kDirScale) S per segment,
+// the table's size per frame), each window segment's directory constants (segk: {min L2, min U2 =
+// min L2 + dbase, bucket shift over the L2 range + 7, directory offset}), the used keys, the
+// chunk's tail of non-frames, and cbeg.
 __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __restrict__ qoff, int32_t nq, int32_t qch,
                                                              int32_t nch, const uint32_t* __restrict__ segstat,
                                                              const int32_t* __restrict__ ghist, int32_t* __restrict__ bstart,
-                                                             int32_t* __restrict__ seg, int32_t* __restrict__ doff,
-                                                             int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
+                                                             int32_t* __restrict__ seg, int32_t* __restrict__ ukeys, int32_t* __restrict__ nuk,
                                                              int32_t* __restrict__ cbeg, uint8_t* __restrict__ qis,
-                                                             int32_t* __restrict__ fseg, int4* __restrict__ gi4,
-                                                             int32_t* __restrict__ gb, int32_t gcap) {
+                                                             int4* __restrict__ gi4,
+                                                             int32_t* __restrict__ gb, int32_t gcap, int64_t dbase,
+                                                             int4* __restrict__ segk) {
   constexpr int NT = 1024, FPER = kNFine / NT;
   __shared__ int32_t base[kWideSegs], nbs[kWideSegs], shf[kWideSegs], ws[NT / 64];
   __shared__ uint32_t lmn[kWideSegs];
@@ -1066,7 +1463,7 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
   }
   __syncthreads();
   // segments: segment sk's bins [base, base + nb)
-  int32_t dv[2] = {0, 0};
+  int32_t dv[2] = {0, 0}, ns[2] = {0, 0};
 #pragma unroll
   for (int j = 0; j < 2; j++) {
     const int sk = 2 * t + j;
@@ -1077,7 +1474,7 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
         sg[0] = (int32_t)cb + b;
         sg[1] = (int32_t)cb + e;
         used[sk & (kKeyRange - 1)] = 1;
-        if (sk < kKeyRange) dv[j] = 2 << dir_log2(e - b);  // (the directory's entries)
+        if (sk < kKeyRange) dv[j] = 2 << dir_log2(e - b), ns[j] = e - b;  // (the directory's entries)
       }
     }
   }
@@ -1086,7 +1483,16 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
   (void)DT;
 #pragma unroll
   for (int j = 0; j < 2; j++) {
-    if (dv[j]) doff[(int64_t)ch * kKeyRange + 2 * t + j] = (4 << kDirScale) * (int32_t)cb + dof;
+    if (dv[j]) {
+      const int sk = 2 * t + j;
+      const int32_t o = (4 << kDirScale) * (int32_t)cb + dof;
+      const uint32_t* sst = segstat + ((int64_t)ch * kWideSegs + sk) * 3;
+      const uint32_t lo = sst[1], hi = sst[2];
+      const int32_t l2min = (int32_t)(lo ^ 0x80000000u);
+      // (U2 min beyond int32: such frames are out of range, info[1], and the batch is redone)
+      const int64_t u2min = min((int64_t)l2min + dbase, (int64_t)INT32_MAX);
+      segk[(int64_t)ch * kKeyRange + sk] = make_int4(l2min, (int32_t)u2min, dir_shift((int64_t)(hi - lo) + 7, dir_log2(ns[j])), o);
+    }
     dof += dv[j];
   }
   // the used keys, ascending
@@ -1123,11 +1529,8 @@ __global__ __launch_bounds__(1024) void wide_bin_scan_kernel(const int64_t* __re
     gi4[(int64_t)ch * gcap + gi] = make_int4(a, z, hs, hn);
     gb[(int64_t)ch * gcap + gi] = f;
   }
-  // the range's tail (no kept frame): query 0, no segment
-  for (int64_t i = cb + T + t; i < ce; i += NT) {
-    qis[i] = 0;
-    fseg[i] = -1;
-  }
+  // the range's tail (no kept frame): query 0
+  for (int64_t i = cb + T + t; i < ce; i += NT) qis[i] = 0;
 }
 
 // Each kept frame's key to its bin's place: kb[cbeg[ch] + bstart[ch][bin] + place].
@@ -1143,6 +1546,14 @@ __global__ void wide_bin_scatter_kernel(int64_t nf, int32_t qch, const int32_t* 
   }
 }
 
+__device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, int d) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int l) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
+  return ((unsigned long long)hi << 32) | lo;
+}
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
   return ((unsigned long long)hi << 32) | lo;
@@ -1192,20 +1603,66 @@ __device__ void bitonic_lds(unsigned long long* S, int N, int lane) {
       }
 }
 
+// A window segment's directory runs for one sorted frame (wide_dir_fill's rule): frame i at
+// absolute position pos writes the L2 and U2 buckets after its predecessor's (key kp; none at the
+// segment's first frame) up to its own, and the segment's last frame also the buckets after its
+// own (value se). sk4 = {l2min, u2min, shift, directory offset} of the segment (segk), sb / se its
+// bounds. A U2 bucket is (U2 - u2min) >> shift with u2min = l2min + dbase, i.e. (L2 - l2min + d)
+// >> shift: formed without dbase, it stays inside the directory even for a batch whose U2 leaves
+// int32 (info[1]: redone). Returns the runs in lo / hi / val / base (empty: lo > hi).
+__device__ __forceinline__ void dir_runs(int64_t pos, unsigned long long k, unsigned long long kp, int4 sk4, int32_t sb,
+                                         int32_t se, int32_t (&lo)[4], int32_t (&hi)[4], int32_t (&val)[4],
+                                         int32_t (&base)[4]) {
+  const int64_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), lp = (int32_t)((uint32_t)(kp >> 11) ^ 0x80000000u);
+  const int64_t dl = l2 - sk4.x, dp = lp - sk4.x;
+  const int lg = dir_log2(se - sb);
+  const int32_t nbk = 1 << lg;
+  const int32_t bi = (int32_t)(dl >> sk4.z), bu = (int32_t)((dl + (int64_t)((k >> 8) & 7)) >> sk4.z);
+  const bool first = pos == sb;
+  const int32_t bp = first ? -1 : (int32_t)(dp >> sk4.z), bq = first ? -1 : (int32_t)((dp + (int64_t)((kp >> 8) & 7)) >> sk4.z);
+  base[0] = base[2] = sk4.w;
+  base[1] = base[3] = sk4.w + nbk;
+  lo[0] = bp + 1, hi[0] = bi, val[0] = (int32_t)pos;
+  lo[1] = bq + 1, hi[1] = bu, val[1] = (int32_t)pos;
+  if (pos == se - 1) {
+    lo[2] = bi + 1, hi[2] = nbk - 1, val[2] = se;
+    lo[3] = bu + 1, hi[3] = nbk - 1, val[3] = se;
+  }
+}
+// Every lane's runs written: short ones by their lane, long ones (a sparse stretch of the value
+// range) by the whole wave, 64 buckets a step. (Call with every lane of the wave.)
+__device__ __forceinline__ void dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
+                                          const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
+  constexpr int32_t kShort = 8;
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int32_t len = hi[r] - lo[r] + 1;
+    if (len > 0 && len <= kShort)
+      for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
+    unsigned long long m = __ballot(len > kShort);
+    while (m) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64), o = __shfl(base[r], l, 64);
+      for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
+    }
+  }
+}
+
 // Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
 // (bins are monotone in the key, so sorting a run of whole bins sorts each of them): frames
 // [gi4[g].x, gi4[g].y) of the chunk, bins [gb[g], gb[g + 1]). One wave per group sorts it in
 // registers (up to 256 frames, 4 a lane) or LDS, and writes each sorted frame's L2, U2 (= L2 +
-// dbase + d), query and segment (ch << 11 | segment key); a frame that starts or ends a window
-// segment writes the segment's first or last L2 / U2 (segc) for the directory fill. A group above
-// kBinCap frames (a crowded bin) goes bin by bin: a bin whose frames all share (segment, L2, d), or
-// whose segment has no max2 window, needs no order; any other bin above kBinCap frames sets
-// info[2].
+// dbase + d) and query, and its window segment's directory runs (the frame before the
+// group: the greatest key of the group before it). A group above kBinCap frames (a crowded bin)
+// goes bin by bin: a bin whose frames all share (segment, L2, d), or whose segment has no max2
+// window, needs no order, and the waves of its 64-frame windows copy it; any other bin above
+// kBinCap frames sets info[2] (the batch is redone with the library sort).
 __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     const int32_t* __restrict__ bstart, const int4* __restrict__ gi4, const int32_t* __restrict__ gb, int32_t gcap,
     const int32_t* __restrict__ cbeg, const unsigned long long* __restrict__ kb, int64_t dbase,
-    const int32_t* __restrict__ seg, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s, uint8_t* __restrict__ qis,
-    int32_t* __restrict__ fseg, int32_t* __restrict__ segc, int32_t* __restrict__ info) {
+    const int32_t* __restrict__ seg, const int4* __restrict__ segk, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
+    uint8_t* __restrict__ qis, int32_t* __restrict__ dtab, int32_t* __restrict__ info) {
   __shared__ unsigned long long sk[kBinSortWaves][kBinCap];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ch = blockIdx.x;
@@ -1217,73 +1674,90 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   const int64_t cb = cbeg[ch];
   unsigned long long* S = sk[wv];
   auto sk_of = [](unsigned long long k) { return (int32_t)((k >> kPackSegShift) & (kWideSegs - 1)); };
-  // sorted frame p (chunk-relative) of key k; first / last: 1 when p starts / ends its segment, 2
-  // when it may (a neighbour outside the group: the segment table decides)
-  auto put = [&](int32_t p, unsigned long long k, int first, int last) {
-    const int64_t pos = cb + p;
-    const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
-    const int32_t u2 = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
-    L2s[pos] = l2;
-    U2s[pos] = u2;
-    qis[pos] = (uint8_t)(k & 255);
-    fseg[pos] = (ch << 11) | sgk;
-    if ((first || last) && sgk < kKeyRange) {
-      const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
-      int32_t* c4 = segc + ((int64_t)ch * kKeyRange + sgk) * 4;
-      if (first == 1 || (first == 2 && sg[0] == pos)) c4[0] = l2, c4[1] = u2;
-      if (last == 1 || (last == 2 && sg[1] == pos + 1)) c4[2] = l2, c4[3] = u2;
+  // the key before the group in sorted order: the greatest of the bin before S0 (kb is unsorted:
+  // its greatest over a range holding that whole bin, whose keys exceed those of the bins before
+  // it). That bin is the previous group's last (at most kBinCap frames from S0 on) or, when that
+  // group is empty, the one holding frame 64 (g - 1); a bin above kBinCap frames is a crowd of one
+  // value or has no max2 window (no directory), so any of its keys will do. None at the chunk start
+  // (S0 > 0 has g > 0: group 0 starts at frame 0).
+  unsigned long long kprev = 0;
+  if (S0 > 0 && S0 < S1) {
+    const int4 gr = gi4[(int64_t)ch * gcap + g - 1];
+    const int32_t lo = gr.x < S0 ? max(gr.x, S0 - kBinCap) : gr.w > kBinCap ? S0 - 1 : gr.z;
+    for (int32_t p = lo + lane; p < S0; p += 64) {
+      const unsigned long long k = kb[cb + p];
+      kprev = k > kprev ? k : kprev;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long y = shfl_xor_u64(kprev, o);
+      kprev = y > kprev ? y : kprev;
+    }
+  }
+  // sorted frame p (chunk-relative) of key k after key kp: its outputs and directory runs (valid:
+  // this lane has a frame; every lane calls)
+  auto put = [&](int32_t p, unsigned long long k, unsigned long long kp, bool valid) {
+    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
+    if (valid) {
+      const int64_t pos = cb + p;
+      const int32_t l2 = (int32_t)((uint32_t)(k >> 11) ^ 0x80000000u), sgk = sk_of(k);
+      L2s[pos] = l2;
+      U2s[pos] = (int32_t)(l2 + dbase + (int64_t)((k >> 8) & 7));
+      qis[pos] = (uint8_t)(k & 255);
+      if (sgk < kKeyRange) {
+        const int32_t* sg = seg + ((int64_t)ch * kWideSegs + sgk) * 2;
+        dir_runs(pos, k, kp, segk[(int64_t)ch * kKeyRange + sgk], sg[0], sg[1], lo, hi, val, base);
+      }
+    }
+    dir_write(dtab, lo, hi, val, base, lane);
   };
-  // frames [b, b + n) sorted in LDS, written
-  auto sort_lds = [&](int32_t b, int32_t n) {
+  // frames [b, b + n) sorted in LDS, written (kp: the key before them); returns their last key
+  auto sort_lds = [&](int32_t b, int32_t n, unsigned long long kp) {
     const int N = n <= 1 ? 1 : 1 << (32 - __clz(n - 1));
     for (int p = lane; p < N; p += 64) S[p] = p < n ? kb[cb + b + p] : ~0ull;
     bitonic_lds(S, N, lane);
-    for (int p = lane; p < n; p += 64) {
-      const unsigned long long k = S[p];
-      put(b + p, k, p == 0 ? 2 : sk_of(S[p - 1]) != sk_of(k), p == n - 1 ? 2 : sk_of(S[p + 1]) != sk_of(k));
+    for (int p0 = 0; p0 < n; p0 += 64) {
+      const int p = p0 + lane;
+      put(b + p, p < n ? S[p] : 0ull, p == 0 ? kp : S[p > 0 ? p - 1 : 0], p < n);
     }
+    return S[n - 1];
   };
-  // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
-  // batch is redone): each wave copies and checks its own, the wave of the bin's group those before
-  // the bin's first multiple of 64
-  auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1) {
-    // frames [p0, p1) of big bin [b, b + nb), unsorted: a frame whose (segment, L2, d) differs from
-    // the bin's first in a window segment sends the batch to the library sort
+  // frames [p0, p1) of big bin [b, b + nb), unsorted (kp: the key before the bin): a frame whose
+  // (segment, L2, d) differs from the bin's first in a window segment sends the batch to the
+  // library sort
+  auto copy_big = [&](int32_t b, int32_t nb, int32_t p0, int32_t p1, unsigned long long kp) {
     const unsigned long long k0 = kb[cb + b];
     bool odd = false;
-    for (int32_t p = p0 + lane; p < p1; p += 64) {
-      const unsigned long long k = kb[cb + p];
-      put(p, k, p == b ? 2 : 0, p == b + nb - 1 ? 2 : 0);
+    for (int32_t q0 = p0; q0 < p1; q0 += 64) {
+      const int32_t p = q0 + lane;
+      const unsigned long long k = p < p1 ? kb[cb + p] : k0;
+      put(p, k, p == b ? kp : k0, p < p1);
       odd = odd || ((k >> 8) != (k0 >> 8) && sk_of(k0) < kKeyRange);
     }
     if (__ballot(odd) && lane == 0) atomicAdd(&info[2], 1);
   };
-  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w));
+  // frames 64 g .. 64 g + 63 of a bin above kBinCap that holds frame 64 g (no order needed, or the
+  // batch is redone): each wave copies and checks its own (a bin starting at 64 g is this group's
+  // first: its predecessor is kprev), the wave of the bin's group those before the bin's first
+  // multiple of 64
+  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w), kprev);
   const int32_t n = S1 - S0;
   if (n <= 0) return;
-  // n <= 64 R: R keys a lane, sorted in registers; each frame's neighbours through the lanes
+  // n <= 64 R: R keys a lane, sorted in registers; each frame's predecessor through the lanes
   auto sort_regs = [&](auto rr) {
     constexpr int R = decltype(rr)::value;
     unsigned long long v[R];
 #pragma unroll
     for (int r = 0; r < R; r++) v[r] = 64 * r + lane < n ? kb[cb + S0 + 64 * r + lane] : ~0ull;
     bitonic_regs<R>(v, lane);
-    int32_t sg[R], prev[R], next[R];
-#pragma unroll
-    for (int r = 0; r < R; r++) sg[r] = sk_of(v[r]);
+    unsigned long long pv[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {  // (every lane: the shuffles read whole rows)
-      const int32_t up = __shfl_up(sg[r], 1, 64), dn = __shfl_down(sg[r], 1, 64);
-      const int32_t pl = __shfl(sg[r > 0 ? r - 1 : 0], 63, 64), nf = __shfl(sg[r + 1 < R ? r + 1 : r], 0, 64);
-      prev[r] = lane ? up : r ? pl : -1;
-      next[r] = lane < 63 ? dn : r + 1 < R ? nf : -1;
+      const unsigned long long up = shfl_up_u64(v[r], 1), last = shfl_u64(v[r > 0 ? r - 1 : 0], 63);
+      pv[r] = lane ? up : r ? last : kprev;
     }
 #pragma unroll
-    for (int r = 0; r < R; r++) {
-      const int32_t i = 64 * r + lane;
-      if (i < n) put(S0 + i, v[r], i == 0 ? 2 : prev[r] != sg[r], i == n - 1 ? 2 : next[r] != sg[r]);
-    }
+    for (int r = 0; r < R; r++) put(S0 + 64 * r + lane, v[r], pv[r], 64 * r + lane < n);
   };
   if (n <= 64) {
     sort_regs(std::integral_constant<int, 1>{});
@@ -1298,10 +1772,11 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     return;
   }
   if (n <= kBinCap) {
-    sort_lds(S0, n);
+    (void)sort_lds(S0, n, kprev);
     return;
   }
   // a crowded group: bin by bin (the bins' bounds 64 at a time)
+  unsigned long long klast = kprev;
   const int32_t fa = gb[(int64_t)ch * gcap + g], fz = gb[(int64_t)ch * gcap + g + 1];
   for (int32_t f0 = fa; f0 < fz; f0 += 64) {
     const int32_t bl = f0 + lane < fz ? bs[f0 + lane] : 0, nl = f0 + lane < fz ? bs[f0 + lane + 1] - bl : 0;
@@ -1309,67 +1784,15 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
       const int sl = __ffsll((long long)mb) - 1;
       const int32_t b = __builtin_amdgcn_readlane(bl, sl), nb = __builtin_amdgcn_readlane(nl, sl);
       if (nb <= kBinCap) {
-        sort_lds(b, nb);
+        klast = sort_lds(b, nb, klast);
         continue;
       }
       // frames that all share (segment, L2, d) need no order (a crowd of equal values: the silence
       // floor), nor do those of a segment without a max2 window: the waves of the bin's 64-frame
       // windows copy and check them, this one the frames before the bin's first multiple of 64
-      copy_big(b, nb, b, min(b + nb, (b + kGroup - 1) / kGroup * kGroup));
-    }
-  }
-}
-
-// wide_dir_fill over the bin-sorted frames: the segment of frame i from fseg, its constants from
-// the segment table, segc and doff (loads that depend on fseg only). Nothing after an overflow
-// (info[2] > 0: a bin was left unsorted, its frames without fseg; the batch is redone).
-__global__ void wide_dir_fill_bins_kernel(int64_t n, const int32_t* __restrict__ fseg, const int32_t* __restrict__ seg,
-                                          const int32_t* __restrict__ segc, const int32_t* __restrict__ L2s,
-                                          const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
-                                          int32_t* __restrict__ dtab, const int32_t* __restrict__ info) {
-  constexpr int32_t kShort = 8;
-  if (info[2] > 0) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t i0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; i0 < n; i0 += nw * 64) {
-    const int64_t i = i0 + lane;
-    int32_t lo[4] = {1, 1, 1, 1}, hi[4] = {0, 0, 0, 0}, val[4] = {0, 0, 0, 0}, base[4] = {0, 0, 0, 0};
-    if (i < n) {
-      const int32_t fs = fseg[i];
-      const int32_t xl = L2s[i], xu = U2s[i], xlp = i > 0 ? L2s[i - 1] : 0, xup = i > 0 ? U2s[i - 1] : 0;
-      if (fs >= 0 && (fs & kKeyRange) == 0) {
-        const int64_t ch = fs >> 11, key = fs & (kKeyRange - 1);
-        const int32_t* sg = seg + (ch * kWideSegs + key) * 2;
-        const int32_t* c4 = segc + (ch * kKeyRange + key) * 4;
-        const int32_t sb = sg[0], se = sg[1], t0 = doff[ch * kKeyRange + key];
-        const int32_t l2min = c4[0], u2min = c4[1];
-        const int lg = dir_log2(se - sb);
-        const int32_t nbk = 1 << lg;
-        const int shf = dir_shift(max((int64_t)c4[2] - l2min, (int64_t)c4[3] - u2min), lg);
-#pragma unroll
-        for (int hh = 0; hh < 2; hh++) {
-          const int64_t mn = hh ? u2min : l2min;
-          const int32_t bi = (int32_t)(((int64_t)(hh ? xu : xl) - mn) >> shf);
-          const int32_t bp = i == sb ? -1 : (int32_t)(((int64_t)(hh ? xup : xlp) - mn) >> shf);
-          base[hh] = base[2 + hh] = t0 + hh * nbk;
-          lo[hh] = bp + 1, hi[hh] = bi, val[hh] = (int32_t)i;
-          if (i == se - 1) lo[2 + hh] = bi + 1, hi[2 + hh] = nbk - 1, val[2 + hh] = se;
-        }
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int32_t len = hi[r] - lo[r] + 1;
-      if (len > 0 && len <= kShort)
-        for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
-      unsigned long long m = __ballot(len > kShort);
-      while (m) {
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64),
-                      o = __shfl(base[r], l, 64);
-        for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
-      }
+      copy_big(b, nb, b, min(b + nb, (b + kGroup - 1) / kGroup * kGroup), klast);
+      if (lane == 0) atomicAdd(&info[3], 1);  // (crowd bins copied: tfp_sweep_stats)
+      klast = kb[cb + b + nb - 1];  // (a crowd of one value: any of its keys)
     }
   }
 }
@@ -1381,6 +1804,11 @@ __global__ void wide_dir_fill_bins_kernel(int64_t n, const int32_t* __restrict__
 // of two 16-bit counts) among 64 frames by reading their queries out of the lanes (no per-frame
 // memory dependency).
 constexpr int kPortions = 256;
+#ifndef TFP_PSTEP
+#define TFP_PSTEP 4
+#endif
+constexpr int kPStep = TFP_PSTEP;  // frames per prefix-count row (1 or 4)
+static_assert(kPStep == 1 || kPStep == 4, "one row a frame, or a 4-byte word of queries a row");
 __device__ __forceinline__ void portion_range(const int32_t* cbeg, int ch, int p, int32_t& b, int32_t& r0, int32_t& r1) {
   b = cbeg[ch];
   const int32_t n = cbeg[ch + 1] - b;
@@ -1432,6 +1860,9 @@ __global__ __launch_bounds__(1024) void wide_pscan_kernel(uint32_t* __restrict__
 #pragma unroll
   for (int j = 0; j < 16; j++) t[64 * j] = base + v[j];
 }
+// The rows are checkpoints: frame i's row only when i % kPStep == kPStep - 1, at P[i / kPStep] (a
+// fourth of the bytes written; wide_clips adds the up to kPStep - 1 frames after the checkpoint
+// before a position from their queries, prefix_at).
 template <int QPL>
 __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __restrict__ cbeg, const uint8_t* __restrict__ qis,
                                                            const uint32_t* __restrict__ ptot, uint32_t* __restrict__ P) {
@@ -1441,32 +1872,39 @@ __global__ __launch_bounds__(1024) void wide_prefix_kernel(const int32_t* __rest
   uint32_t run = ptot[((int64_t)blockIdx.x * kPortions + p) * 64 + lane];
   for (int32_t i = r0; i < r1; i += 64) {
     const int32_t x = i + lane < r1 ? (int32_t)qis[b + i + lane] : kPadQ;
-    uint32_t* row = P + ((int64_t)b + i) * kWideW + lane;
+    const int32_t bi = b + i;  // (global frame of j = 0)
     const int m = min(64, r1 - i);
 #pragma unroll
     for (int j = 0; j < 64; j++) {
       run += prefix_inc<QPL>(__builtin_amdgcn_readlane(x, j), lane);
-      if (j < m) row[(int64_t)j * kWideW] = run;
+      if (j < m && ((bi + j) & (kPStep - 1)) == kPStep - 1) P[(int64_t)((bi + j) / kPStep) * kWideW + lane] = run;
     }
   }
 }
+// In-chunk prefix count at frame e (>= cb, the chunk's first frame) from the checkpoint rows: the
+// row at e itself, or the last checkpoint before e in the chunk (none: 0) plus the increments of
+// the frames after it up to e, read from their queries (one aligned 4-byte load; qis is padded).
+// e is wave-uniform (every caller's is a shuffled or read-lane value): as a scalar, the queries'
+// word is a scalar load and only the per-lane compare and add take vector registers.
+template <int QPL>
+__device__ __forceinline__ uint32_t prefix_at(const uint32_t* __restrict__ P, const uint8_t* __restrict__ qis, int32_t cb,
+                                              int32_t e, int lane) {
+  if constexpr (kPStep == 1) {
+    return P[(int64_t)e * kWideW + lane];
+  } else {
+    e = __builtin_amdgcn_readfirstlane(e);
+    const int32_t g = e / kPStep, f0 = g * kPStep;
+    if (e == f0 + kPStep - 1) return P[(int64_t)g * kWideW + lane];
+    uint32_t v = f0 - 1 >= cb ? P[(int64_t)(g - 1) * kWideW + lane] : 0u;
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(qis + f0);
+#pragma unroll
+    for (int j = 0; j < kPStep - 1; j++)
+      if (f0 + j <= e && f0 + j >= cb) v += prefix_inc<QPL>((int32_t)((w >> (8 * j)) & 255u), lane);
+    return v;
+  }
+}
 
-__device__ __forceinline__ int32_t lb32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] >= v
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-__device__ __forceinline__ int32_t ub32(const int32_t* a, int32_t n, int32_t v) {  // first a[i] > v
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] <= v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
+// lb32 / ub32: tfp_bsearch.hpp (both ends read with the first probe)
 
 // ---- clip-major sweep ------------------------------------------------------------------------
 // Work items are (chunk, key, clip group). A wave takes windows of kWin consecutive clip columns of
@@ -1507,7 +1945,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
-    const int32_t* __restrict__ tiekey, int32_t C, const int32_t* __restrict__ doff, const int32_t* __restrict__ dtab,
+    const uint8_t* __restrict__ qis, const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
     unsigned long long* __restrict__ part, const int32_t* __restrict__ stop) {
   // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
   // so the sweep reads nothing (the batch is redone; its maxima are not used)
@@ -1551,7 +1989,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
   };
   auto close_run = [&](uint32_t& cnt, int32_t a, int32_t b) {
-    cnt += P[(int64_t)b * kWideW + lane] - (a > sb ? P[(int64_t)(a - 1) * kWideW + lane] : base);
+    cnt += prefix_at<QPL>(P, qis, cb, b, lane) - (a > sb ? prefix_at<QPL>(P, qis, cb, a - 1, lane) : base);
   };
   // The chunk's used keys' segment constants, one key per lane, loaded once per wave instead of
   // once per window and key (three dependent loads ahead of every key's groups): the window loop
@@ -1565,11 +2003,11 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     kfb = sg[2 * (kq | kKeyRange)];
     kfe = sg[2 * (kq | kKeyRange) + 1];
     if (kse > ksb) {
-      const int lg = dir_log2(kse - ksb);
-      kl2 = L2s[ksb];
-      ku2 = U2s[ksb];
-      kshf = dir_shift(max((int64_t)L2s[kse - 1] - kl2, (int64_t)U2s[kse - 1] - ku2), lg);
-      ktoff = doff[(int64_t)ch * kKeyRange + kq];
+      const int4 c4 = segk[(int64_t)ch * kKeyRange + kq];
+      kl2 = c4.x;
+      ku2 = c4.y;
+      kshf = c4.z;
+      ktoff = c4.w;
     }
   }
   for (int32_t w = w0; w < w1; w++) {
@@ -1605,8 +2043,8 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           fb = sg[2 * (k | kKeyRange)];
           fe = sg[2 * (k | kKeyRange) + 1];
         }
-        base = se > sb && sb > cb ? P[(int64_t)(sb - 1) * kWideW + lane] : 0u;
-        fcnt = fe > fb ? P[(int64_t)(fe - 1) * kWideW + lane] - (fb > cb ? P[(int64_t)(fb - 1) * kWideW + lane] : 0u) : 0u;
+        base = se > sb && sb > cb ? prefix_at<QPL>(P, qis, cb, sb - 1, lane) : 0u;
+        fcnt = fe > fb ? prefix_at<QPL>(P, qis, cb, fe - 1, lane) - (fb > cb ? prefix_at<QPL>(P, qis, cb, fb - 1, lane) : 0u) : 0u;
         if (se <= sb) {  // no frame of the key has a max2 window: every group scores the rest
           for (; g < g1; g++) add((int32_t)(cv.g_key[g] & kColMask), fcnt);
           continue;
@@ -1618,12 +2056,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           shf = __builtin_amdgcn_readlane(kshf, sl);
           TL = dtab + __builtin_amdgcn_readlane(ktoff, sl);
         } else {
-          const int lg = dir_log2(se - sb);
-          nbk = 1 << lg;
-          l2min = L2s[sb];
-          u2min = U2s[sb];
-          shf = dir_shift(max((int64_t)L2s[se - 1] - l2min, (int64_t)U2s[se - 1] - u2min), lg);
-          TL = dtab + doff[(int64_t)ch * kKeyRange + k];
+          nbk = 1 << dir_log2(se - sb);
+          const int4 c4 = segk[(int64_t)ch * kKeyRange + k];
+          l2min = c4.x;
+          u2min = c4.y;
+          shf = c4.z;
+          TL = dtab + c4.w;
         }
         // A batch of consecutive groups whose items fit the 64 lanes: lane j holds group j's item
         // range [pj0, pj1) relative to the first item pb0.
@@ -1756,7 +2194,7 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
                                                              int32_t nq, unsigned long long* __restrict__ best,
                                                              const int32_t* __restrict__ info, int32_t* __restrict__ info_out) {
   // (the sweep's counts into the caller's host-mapped memory, read with the results: no copy launch)
-  if (info_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 3) info_out[threadIdx.x] = info[threadIdx.x];
+  if (info_out && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) info_out[threadIdx.x] = info[threadIdx.x];
   constexpr int Q = 64 * QPL, S = 1024 / Q;  // queries per chunk, slices
   __shared__ unsigned long long red[S][Q];
   // (gridDim.y workgroups per chunk, each over every gridDim.y-th slice of the maxima: a chunk's
@@ -1780,10 +2218,11 @@ __global__ __launch_bounds__(1024) void wide_part_max_kernel(const unsigned long
 void WideScratch::release() {
   for (void* p : {(void*)ka, (void*)kb, (void*)ua, (void*)ub, (void*)va, (void*)vb, (void*)L2s, (void*)U2s, (void*)qis,
                   (void*)P, (void*)seg, (void*)cbeg, (void*)info, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part,
-                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)bstart, (void*)segc, (void*)segstat,
+                  (void*)fq, (void*)doff, (void*)dtab, dtmp, tmp, (void*)bstart, (void*)segk, (void*)segstat,
                   (void*)ghist})
     if (p) (void)hipFree(p);
-  bstart = segc = ghist = nullptr;
+  bstart = ghist = nullptr;
+  segk = nullptr;
   segstat = nullptr;
   for (void* q : {(void*)gi4, (void*)gb})
     if (q) (void)hipFree(q);
@@ -1824,7 +2263,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
     cap_nf = 0;
     if ((e = dmalloc(&ka, nf)) || (e = dmalloc(&kb, nf)) || (e = dmalloc(&ua, nf)) || (e = dmalloc(&ub, nf)) ||
         (e = dmalloc(&va, nf)) || (e = dmalloc(&vb, nf)) || (e = dmalloc(&L2s, nf)) || (e = dmalloc(&U2s, nf)) ||
-        (e = dmalloc(&qis, nf)) || (e = dmalloc(&P, nf * kWideW)) || (e = dmalloc(&fq, nf)))
+        (e = dmalloc(&qis, nf + 16)) || (e = dmalloc(&P, (nf / kPStep + 2) * kWideW)) || (e = dmalloc(&fq, nf)))
       return e;
     size_t t1 = 0, t2 = 0;
     size_t t3 = 0;
@@ -1838,10 +2277,11 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
   }
   if (nch > cap_nch) {
     for (void* p : {(void*)seg, (void*)cbeg, (void*)doff, (void*)ptot, (void*)ukeys, (void*)nuk, (void*)part, dtmp,
-                    (void*)bstart, (void*)segc, (void*)segstat, (void*)ghist})
+                    (void*)bstart, (void*)segk, (void*)segstat, (void*)ghist})
       if (p) (void)hipFree(p);
     seg = cbeg = doff = ukeys = nuk = nullptr;
-    bstart = segc = ghist = nullptr;
+    bstart = ghist = nullptr;
+    segk = nullptr;
     segstat = nullptr;
     ptot = nullptr;
     part = nullptr;
@@ -1853,7 +2293,7 @@ hipError_t WideScratch::reserve(int64_t nf, int32_t nq, hipStream_t s) {
         (e = dmalloc(&part, (nq + 255) / 256 * (2 * kPartWaves) * 256)) ||  // up to 2 kPartWaves waves per chunk, either chunk size
         (e = dmalloc(&bstart, nch * (kNFine + 1))) ||
         (e = dmalloc(&segstat, nch * kWideSegs * 3)) || (e = dmalloc(&ghist, nch * kNFine)) ||
-        (e = dmalloc(&segc, nch * kKeyRange * 4)))
+        (e = dmalloc(&segk, nch * kKeyRange)))
       return e;
     size_t tb = 0;
     if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, doff, doff, (int)(nch * kKeyRange + 1), s))) return e;
@@ -1927,14 +2367,14 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       ws->cap_groups = nch * gcap;
     }
     hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
-                       ws->ghist, ws->bstart, ws->seg, ws->doff, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->va, ws->gi4, ws->gb,
-                       (int32_t)gcap);
+                       ws->ghist, ws->bstart, ws->seg, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->gi4, ws->gb,
+                       (int32_t)gcap, dbase, ws->segk);
     hipLaunchKernelGGL(wide_bin_scatter_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, qch, ws->fq, ws->ka,
                        reinterpret_cast<const uint32_t*>(ws->vb), ws->cbeg,
                        ws->bstart, ws->kb);
     hipLaunchKernelGGL(wide_bin_sort_kernel, dim3((unsigned)nch, (unsigned)((gcap + kBinSortWaves - 1) / kBinSortWaves)),
                        dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gi4, ws->gb, (int32_t)gcap, ws->cbeg, ws->kb, dbase, ws->seg,
-                       ws->L2s, ws->U2s, ws->qis, ws->va, ws->segc, ws->info);
+                       ws->segk, ws->L2s, ws->U2s, ws->qis, ws->dtab, ws->info);
     if (ws->debug_bins) {  // (TFP_DEBUG_BINS: the bin sort's counts of the first chunk, on stderr)
       std::vector<int32_t> bs(kNFine + 1);
       std::vector<int4> g(gcap);
@@ -1955,8 +2395,6 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
               bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
     }
-    hipLaunchKernelGGL(wide_dir_fill_bins_kernel, dim3(grid_for(nf)), dim3(256), 0, s, nf, ws->va, ws->seg, ws->segc, ws->L2s,
-                       ws->U2s, ws->doff, ws->dtab, ws->info);
   } else {
     size_t tb = ws->tmp_bytes;
     if (packed) {
@@ -1999,7 +2437,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
     (void)nd;
     hipLaunchKernelGGL(wide_dir_offsets_kernel, dim3(1), dim3(1024), 0, s, ws->seg, nch, ws->doff);
     hipLaunchKernelGGL(wide_dir_fill_kernel, dim3(grid_for(nf)), dim3(256), 0, s, ws->info, ws->kb,
-                       packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab);
+                       packed ? kPackSegShift : kWideSegShift, ws->seg, ws->L2s, ws->U2s, ws->doff, ws->dtab, ws->segk);
   }
   if (qch == 256) {
     hipLaunchKernelGGL(wide_pcount_kernel<4>, dim3((unsigned)nch, kPortions / 16), dim3(1024), 0, s, ws->cbeg, ws->qis, ws->ptot);
@@ -2048,14 +2486,14 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (!ws->ukeys_ready) hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
-                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, d_tiekey,
-                       C, ws->doff, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   }

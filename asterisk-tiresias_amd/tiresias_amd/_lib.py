@@ -77,6 +77,7 @@ _SIGS = {
     "tfp_index_commit": (C.c_int, [P]),
     "tfp_index_build_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
     "tfp_index_set_tiebreak": (C.c_int, [P, P, C.c_int32]),
+    "tfp_index_update_tiebreak": (C.c_int, [P, C.c_int32, P, C.c_int32]),
     "tfp_index_delta_stats": (C.c_int, [P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
     "tfp_search": (C.c_int, [P, P, C.c_int32, C.POINTER(SearchParams), P]),
     "tfp_search_batch": (C.c_int, [P, P, P, C.c_int32, C.POINTER(SearchParams), P]),
@@ -95,7 +96,11 @@ _SIGS = {
     "tfp_synchronize": (C.c_int, [P, P]),
     "tfp_group_create": (C.c_int, [P, C.c_int32, C.POINTER(P)]),
     "tfp_group_destroy": (None, [P]),
+    "tfp_index_cache_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 5),
+    "tfp_sweep_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 4),
     "tfp_group_size": (C.c_int32, [P]),
+    "tfp_group_tiebreak_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 3),
+    "tfp_group_peer_stats": (C.c_int, [P, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "tfp_group_last_error": (C.c_char_p, [P]),
     "tfp_group_engine": (P, [P, C.c_int32]),
     "tfp_group_fingerprint_batch": (C.c_int, [P, P, P, C.c_int32, C.c_int32, P, C.c_int64, C.POINTER(C.c_int64)]),

@@ -202,9 +202,28 @@ class Engine:
         self._chk(lib().tfp_index_delta_stats(self._h, C.byref(u), C.byref(c)))
         return u.value, c.value
 
+    def sweep_stats(self) -> dict:
+        """The coefs = 2 sweep's sort path per batch (tfp_sweep_stats): bin sort, library sort,
+        redone speculative passes, crowd bins copied."""
+        v = [C.c_int64() for _ in range(4)]
+        self._chk(lib().tfp_sweep_stats(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("bins", "library", "redone", "crowd"), [x.value for x in v]))
+
+    def index_cache_stats(self) -> dict:
+        """The coefs = 2 clip-set caches (tfp_index_cache_stats): builds, cached hits, builds from the
+        clip order, the clip order's full builds and merges."""
+        v = [C.c_int64() for _ in range(5)]
+        self._chk(lib().tfp_index_cache_stats(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("builds", "hits", "from_order", "order_builds", "order_merges"), [x.value for x in v]))
+
     def set_tiebreak(self, keys):
         keys = np.ascontiguousarray(keys, np.int32)
         self._chk(lib().tfp_index_set_tiebreak(self._h, keys.ctypes.data, len(keys)))
+
+    def update_tiebreak(self, first_clip_id: int, keys):
+        """tfp_index_update_tiebreak: the override's keys of clip ids first_clip_id.. only."""
+        keys = np.ascontiguousarray(keys, np.int32)
+        self._chk(lib().tfp_index_update_tiebreak(self._h, int(first_clip_id), keys.ctypes.data, len(keys)))
 
     def uuid_of_key(self, key: int) -> str:
         buf = C.create_string_buffer(64)
@@ -379,6 +398,20 @@ class Group:
 
     def size(self) -> int:
         return int(lib().tfp_group_size(self._h))
+
+    def tiebreak_stats(self) -> dict:
+        """tfp_group_tiebreak_stats: key respaces, new-clip-only pushes, shard delta updates that
+        re-sent every main column's key."""
+        v = [C.c_int64() for _ in range(3)]
+        check(lib().tfp_group_tiebreak_stats(self._h, *[C.byref(x) for x in v]))
+        return dict(zip(("respaces", "partial_pushes", "shard_full_key_updates"), [x.value for x in v]))
+
+    def peer_stats(self) -> dict:
+        """Peer access among the group's distinct devices (tfp_group_peer_stats): ordered pairs,
+        how many may access each other, for how many it is enabled."""
+        a, b, c = C.c_int32(), C.c_int32(), C.c_int32()
+        check(lib().tfp_group_peer_stats(self._h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"pairs": a.value, "can_access": b.value, "enabled": c.value}
 
     def engine_stats(self):
         """[(rows, clips)] of every shard's engine."""

@@ -90,12 +90,31 @@ def launch_plan(gpus: int, env, argv):
                      "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
 
 
+# Fields the device-group leg reports besides its timings (an N-GPU line shows which devices the
+# group spanned and whether xGMI peer access came up for every ordered pair of them).
+GROUP_FIELDS = ("n_devices", "devices", "peer_access", "shards_rows_clips", "equal_to_engine")
+
+
+def dist_report(dist, rank, world, backend, device):
+    """The world size every rank's process group reports, gathered on every rank (the bench line's
+    `dist`); a rank that disagrees stops the run."""
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "world_size": dist.get_world_size(), "device": device})
+    rep = {"backend": backend + (" (RCCL)" if backend == "nccl" else ""), "ranks": seen,
+           "all_ranks_saw_world": all(x["world_size"] == world for x in seen)}
+    if not rep["all_ranks_saw_world"]:
+        raise SystemExit(f"ranks disagree on the world size: {seen}")
+    return rep
+
+
 def launch_check(args):
     """--launch-check (tests/test_bench_launch.py): the ranks meet over gloo and rank 0 prints the
-    world size it sees, with no GPU call at all."""
+    world size it sees and every rank's report of it (the `dist` field of the bench line), with no
+    GPU call at all."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     n = world
+    rep = None
     if world > 1:
         import torch
         import torch.distributed as dist
@@ -103,9 +122,11 @@ def launch_check(args):
         t = torch.ones(1)
         dist.all_reduce(t)
         n = int(t.item())
+        rep = dist_report(dist, rank, world, "gloo", int(os.environ.get("LOCAL_RANK", "0")))
         dist.destroy_process_group()
     if rank == 0:
-        print(json.dumps({"launch_check": True, "gpus": args.gpus, "world_size": world, "ranks_met": n}), flush=True)
+        print(json.dumps({"launch_check": True, "gpus": args.gpus, "world_size": world, "ranks_met": n, "dist": rep,
+                          "group_fields": list(GROUP_FIELDS)}), flush=True)
 
 
 def main():
@@ -166,6 +187,8 @@ def main():
         else:
             dist.init_process_group(args.dist_backend)
     dev = torch.device("cuda", gpu)
+    # the world size every rank's process group reports (an 8-GPU line shows all eight met)
+    dist_info = dist_report(dist, rank, world, args.dist_backend, gpu) if dist else None
     eng = T.Engine(gpu)
     # a real (non-null) stream: every launch and every event goes on it
     stream = torch.cuda.Stream(dev)
@@ -275,6 +298,8 @@ def main():
         "derived": {"clips_per_s": value * nclips / (F or 1), "x_realtime": value * HOP / 8000.0,
                     "clip_seconds": n / 8000.0},
     }
+    if dist_info:
+        out["dist"] = dist_info
     del micro
 
     # ---------------------------------------------------------------- strong scaling (C2 fixed)
@@ -1023,12 +1048,21 @@ def run_group(args, eng, T, torch, dev, sh, rank, world, dist):
                   shard searching its clips, keys max-combined), median of 5 calls;
       latency     batch-1 host-PCM searches from C (bench/tfp_latency.c), p50 / p99;
       stream      configs[4]: 512 channels through tfp_group_stream_push ticks, from C.
+    Under N ranks the other ranks first release their engines (their clip shards leave the GPUs
+    the group spans), meet rank 0 at a barrier, then wait on the store for as long as the leg takes.
     Rank 0 runs it; the other ranks wait on the rendezvous store (no GPU work meanwhile)."""
     store = None
     if dist:
         store = dist.distributed_c10d._get_default_store()
         if rank != 0:
-            store.wait(["tfp_group_leg_done"], __import__("datetime").timedelta(seconds=900))
+            eng.close()
+            torch.cuda.empty_cache()
+        dist.barrier()
+        if rank != 0:
+            try:
+                store.wait(["tfp_group_leg_done"], __import__("datetime").timedelta(hours=4))
+            except Exception as ex:  # (the legs already measured stand; rank 0 prints the line)
+                log(f"[rank {rank}] group leg wait ended: {ex!r}")
             return None
     try:
         return _group_leg(args, eng, T, torch, dev, sh, world)
@@ -1064,7 +1098,8 @@ def _group_leg(args, eng, T, torch, dev, sh, world):
     g.index_commit()
     t_enrol = time.perf_counter() - t0
     shards = g.engine_stats()
-    log(f"group: {ndev} device(s), enrolled {args.db_clips} clips in {t_enrol:.1f} s, shards {shards}")
+    peers = g.peer_stats()
+    log(f"group: {ndev} device(s), enrolled {args.db_clips} clips in {t_enrol:.1f} s, shards {shards}, peer access {peers}")
 
     nq, qn = args.queries, 8000 * 5
     hq = np.ascontiguousarray(c3_queries(eng, torch, dev, sh, nq, args.db_clips).cpu().numpy())
@@ -1101,12 +1136,14 @@ def _group_leg(args, eng, T, torch, dev, sh, world):
     assert rc == 0, rc
     out = {"workload": f"configs[3] through the shim's handle: a tfp_group over {ndev} GPU(s) in one process, "
                        f"{args.db_clips} x 30 s clips sharded by clip, {nq} x 5 s queries from host PCM",
-           "n_devices": ndev, "shards_rows_clips": shards, "enrol_s": t_enrol,
+           "n_devices": ndev, "devices": list(range(ndev)), "peer_access": peers,
+           "shards_rows_clips": shards, "enrol_s": t_enrol,
            "batch_queries": nq, "batch_ms": batch_ms, "queries_per_s": nq / (batch_ms / 1e3), "found": found,
            "equal_to_engine": same,
            "latency_p50_ms": float(np.percentile(out_ms, 50)), "latency_p99_ms": float(np.percentile(out_ms, 99)),
            "latency_harness": "C loop over tfp_group_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries"
                               % (n_it, nl)}
+    assert set(GROUP_FIELDS) <= set(out), sorted(set(GROUP_FIELDS) - set(out))
     del hq
     if args.stream_channels > 0:
         nch, W, tick, nt = args.stream_channels, 24000, 160, args.stream_ticks

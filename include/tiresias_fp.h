@@ -89,7 +89,11 @@ int tfp_device_count(int32_t* count);
 int tfp_engine_create(int32_t device, tfp_engine** out);
 void tfp_engine_destroy(tfp_engine* eng); /* destroy the engine's streams first */
 const char* tfp_engine_last_error(const tfp_engine* eng); /* eng == NULL: this thread's last
-                                                          * engine-less error (tfp_wav_*) */
+                                                          * engine-less error (tfp_wav_*). The calling
+                                                          * thread's last failure on eng, else eng's
+                                                          * latest; the pointer stays valid until this
+                                                          * thread's next failing call or last_error
+                                                          * read on the same handle */
 int64_t tfp_frame_count(int64_t nsamples); /* ceil(n / 256) */
 
 /* ---- host buffers the engine reads in place ------------------------------------------- */
@@ -189,12 +193,30 @@ int tfp_index_build_stats(tfp_engine* eng, int64_t* full_builds, int64_t* merges
  * above 8, a row-scan fallback); results are unchanged either way. TFP_INDEX_DELTA=0 at engine
  * creation turns it off. Stats: delta updates so far and the clips in the delta now. */
 int tfp_index_delta_stats(tfp_engine* eng, int64_t* delta_updates, int32_t* delta_clips);
+/* The coefs = 2 clip-set caches (new in round 6): builds so far, searches served by a cached
+ * tolerance (the active one or one of three others kept, least recently used out), builds made from
+ * the clip order (tolerances up to 0.49: a filter, no sort), and the clip order's full builds (one
+ * radix sort per full index build, when first needed) and merges (carried through every index
+ * merge). Any pointer may be NULL. */
+/* The coefs = 2 sweep's frame sort per batch (new in round 6): batches whose hand-written bin sort
+ * stood, batches sorted by the library sort (a first pass that could not take the bin sort, or the
+ * redo), speculative passes redone (an overfull bin, a window width outside the packed key, a frame
+ * for the row scan), and the crowd bins (one value: the silence floor) the bin sort copied unsorted.
+ * Any pointer may be NULL. */
+int tfp_sweep_stats(tfp_engine* eng, int64_t* bins, int64_t* library, int64_t* redone, int64_t* crowd_bins);
+int tfp_index_cache_stats(tfp_engine* eng, int64_t* cache_builds, int64_t* cache_hits, int64_t* from_order,
+                          int64_t* order_builds, int64_t* order_merges);
 /* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
  * this engine's uuids). keys[clip_id] must order like the uuids across all shards and be
  * distinct over live clips. A clip added after this call has no key: the next search (or
  * tfp_index_commit) fails with TFP_E_ARG until the keys are set again; nclip_ids = 0 clears
  * the override. */
 int tfp_index_set_tiebreak(tfp_engine* eng, const int32_t* keys, int32_t nclip_ids);
+/* The override's keys of clip ids [first_clip_id, first_clip_id + n) only (new in round 6): a device
+ * group gives each clip enrolled since the last update its key without re-sending every clip's
+ * (first_clip_id <= the number of keys set so far). Keys of clips added since the last index update
+ * cost the next update O(new clips); keys of older clips refresh every column's. */
+int tfp_index_update_tiebreak(tfp_engine* eng, int32_t first_clip_id, const int32_t* keys, int32_t n);
 
 /* ---- search: fp_search_fingerprint_info (fp_handler.c:207-408) ---------------------- */
 int tfp_search(tfp_engine* eng, const tfp_frame* frames, int32_t nframes, const tfp_search_params* params,
@@ -274,6 +296,15 @@ typedef struct tfp_group tfp_group;
 int tfp_group_create(const int32_t* devices, int32_t ndevices, tfp_group** out);
 void tfp_group_destroy(tfp_group* g); /* destroy its streams first */
 int32_t tfp_group_size(const tfp_group* g);
+/* Peer access among the group's distinct devices (new in round 6): ordered pairs of distinct
+ * devices, how many of them hipDeviceCanAccessPeer allows, and for how many
+ * hipDeviceEnablePeerAccess succeeded (or was already on). Any pointer may be NULL. */
+int tfp_group_peer_stats(const tfp_group* g, int32_t* pairs, int32_t* can_access, int32_t* enabled);
+/* The group's tie-break keys (new in round 6): respaces (every key re-spread and sent to every shard:
+ * the first enrolment, a large batch, a gap exhausted), pushes of new clips' keys only, and the
+ * shards' index delta updates that still re-sent every main column's key. An enrolment of a few
+ * clips costs a push of their keys, not a pass over every clip. Any pointer may be NULL. */
+int tfp_group_tiebreak_stats(tfp_group* g, int64_t* respaces, int64_t* partial_pushes, int64_t* shard_full_key_updates);
 const char* tfp_group_last_error(const tfp_group* g);
 tfp_engine* tfp_group_engine(tfp_group* g, int32_t shard); /* for stats; do not change its index */
 int tfp_group_fingerprint_batch(tfp_group* g, const int16_t* pcm, const int64_t* offsets, int32_t nclips,

@@ -75,8 +75,8 @@ static void coalesce_test(int nthreads, int reps) {
     data[t].resize(64 + t);
     for (size_t i = 0; i < data[t].size(); i++) data[t][i] = (int16_t)(t * 31 + i);
   }
-  // the handle's uncoalesced search: fails (a message naming the query's length) when any query
-  // has a poisoned length, as a device allocation for it would
+  // the handle's uncoalesced search: fails for want of memory (a message naming the query's
+  // length) when any query has a poisoned length, as a device allocation for it would
   tfp::ErrorSlot slot;
   auto run = [&](const void* const* ptrs, const int64_t* lens, int32_t nq, bool, int32_t, const tfp_search_params*,
                  tfp_result* out) {
@@ -85,7 +85,7 @@ static void coalesce_test(int nthreads, int reps) {
         char m[64];
         snprintf(m, sizeof m, "poisoned query of %lld samples", (long long)lens[q]);
         slot.note(&slot, m);
-        return TFP_E_HIP;
+        return TFP_E_NOMEM;
       }
     for (int32_t q = 0; q < nq; q++) {
       const int16_t* x = static_cast<const int16_t*>(ptrs[q]);
@@ -120,7 +120,7 @@ static void coalesce_test(int nthreads, int reps) {
       bool poisoned = false;
       for (int q = 0; q < nq; q++) poisoned = poisoned || req.lens[q] % 7 == 3;
       if (poisoned) {  // this caller alone fails, with the message of its own request
-        CHECK(rc == TFP_E_HIP);
+        CHECK(rc == TFP_E_NOMEM);
         if (rc) slot.note(&slot, req.err.c_str());
         const char* m = slot.read(&slot);
         bool mine = false;
@@ -158,7 +158,40 @@ static void coalesce_test(int nthreads, int reps) {
   printf("coalescer: %lld calls in %lld batches\n", (long long)calls, (long long)batches);
 }
 
+// A combined batch that fails for another reason than memory (a kernel fault, a launch error) is not
+// re-run request by request: every request gets the leader's code and message, and the run is
+// called once.
+static void sticky_failure_test() {
+  tfp::ErrorSlot slot;
+  int runs = 0;
+  auto run = [&](const void* const*, const int64_t*, int32_t nq, bool, int32_t, const tfp_search_params*, tfp_result*) {
+    runs++;
+    if (nq > 1) {
+      slot.note(&slot, "device fault");
+      return TFP_E_HIP;
+    }
+    return TFP_OK;
+  };
+  std::vector<int16_t> x(300, 1);
+  std::vector<tfp::SearchReq> reqs(3);
+  std::vector<tfp_result> out(3);
+  std::vector<tfp::SearchReq*> batch;
+  for (int i = 0; i < 3; i++) {
+    reqs[i].ptrs.push_back(x.data());
+    reqs[i].lens.push_back(300);
+    reqs[i].sr = 8000;
+    reqs[i].P.coefs = 1;
+    reqs[i].out = &out[i];
+    batch.push_back(&reqs[i]);
+  }
+  tfp::exec_batch(batch, run, [&] { return std::string(slot.read(&slot)); });
+  CHECK(runs == 1);
+  for (auto& r : reqs) CHECK(r.rc == TFP_E_HIP && r.err == "device fault");
+  printf("sticky failure: one run, every request failed\n");
+}
+
 int main() {
+  sticky_failure_test();
   pool_test(3, 400);
   pool_test(8, 200);
   coalesce_test(32, 40);

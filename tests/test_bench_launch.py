@@ -42,7 +42,14 @@ def test_gpus_n_starts_n_ranks(n):
     line = [x for x in r.stdout.splitlines() if x.startswith("{")]
     assert len(line) == 1, r.stdout  # rank 0 alone prints
     got = json.loads(line[0])
+    rep = got.pop("dist")
+    fields = got.pop("group_fields")
     assert got == {"launch_check": True, "gpus": n, "world_size": n, "ranks_met": n}
+    # every rank's own report of the world size, as the bench line's `dist` field carries it
+    assert rep["all_ranks_saw_world"] and rep["backend"] == "gloo"
+    assert [r["rank"] for r in rep["ranks"]] == list(range(n)) and all(r["world_size"] == n for r in rep["ranks"])
+    # the device-group leg's line names the devices it spanned and their peer access
+    assert {"n_devices", "devices", "peer_access"} <= set(fields)
 
 
 def test_world_size_mismatch_is_refused():

@@ -223,3 +223,27 @@ def test_failing_caller_in_coalesced_batch_is_isolated(oracle, tfp_lib, kind, mo
         assert c1 - c0 == 32 * iters and b1 - b0 < c1 - c0  # calls were coalesced (some batches held the bad query)
     finally:
         h.close()
+
+
+def test_operational_switches_without_test_knobs(tfp_lib, monkeypatch):
+    """TFP_COALESCE=0 (include/tiresias_fp.h) is an operational switch: it takes effect without
+    TFP_TEST_KNOBS (which only gates the test-form knobs), so a deployment that follows the header
+    gets what it documents. A search through the engine then never enters the coalescer."""
+    from tiresias_amd._lib import lib
+    monkeypatch.setenv("TFP_TEST_KNOBS", "0")
+    n = 8000 * 4
+    pcm = tfp_lib.synth_pcm(11, range(3), n)
+    p = tfp_lib.params(1, 0.45)
+    for setting, expect_calls in (("0", 0), ("1", 1)):
+        monkeypatch.setenv("TFP_COALESCE", setting)
+        eng = tfp_lib.Engine(0)
+        try:
+            fr = eng.fingerprint_batch(pcm.reshape(-1), np.arange(4) * n)
+            nf = (n + 255) // 256
+            for c in range(3):
+                eng.index_add("%032x" % (c + 1), fr["m1"][c * nf:(c + 1) * nf], fr["m2"][c * nf:(c + 1) * nf])
+            eng.search_pcm_batch(pcm[1], [0, n], p)
+            calls, _ = _stats(lib().tfp_search_coalesce_stats, eng.handle)
+            assert calls == expect_calls, (setting, calls)
+        finally:
+            eng.close()

@@ -397,9 +397,90 @@ def test_configs2_timed_batch_all_4096_vs_sorted_oracle(c3db, oracle, tfp_lib, t
     qdb, qoff = _oracle_q(oracle, qpcm)
     w, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(1, 0.001))
     assert (w >= 0).sum() >= 1000  # (the bench reports ~1,500 found)
+    eng = c3db["eng"]
     for tol in (0.001, 0.45):
+        st0 = eng.sweep_stats()
         w2, _ = _check_keys(c3db, tfp_lib, torch, qpcm, d_q, qdb, qoff, tfp_lib.params(2, tol))
         assert (w2 >= 0).sum() > 0
+        # every batch of the check took the hand-written bin sort, none the library sort or a redo
+        # (tfp_sweep_stats), and the silence-floor crowd was copied unsorted
+        st = {k: v - st0[k] for k, v in eng.sweep_stats().items()}
+        assert st["bins"] >= 1 and st["library"] == 0 and st["redone"] == 0 and st["crowd"] >= 1, (tol, st)
+
+
+@pytest.mark.timeout(900)
+def test_configs4_stream_ticks_against_the_100k_db(c3db, oracle, tfp_lib, torch_cuda):
+    """configs[4] at the DB size bench.py times it against (src/application_handler.c:152-185,
+    248-312: each channel's last 3 s searched every tick): 512 channels of 160-sample ticks over the
+    100,000-clip DB, through tfp_stream on the DB's engine and through tfp_group_stream on a
+    two-shard group (devices 0, 0: channels split over the shards, window frame values exchanged)
+    holding the same clips. Each tick's results of 32 sampled channels == the oracle's sorted-index
+    search (93.8 M rows) of that channel's last 24,000 samples."""
+    torch = torch_cuda
+    eng, idx, uuids, db_clips = c3db["eng"], c3db["idx"], c3db["uuids"], c3db["db_clips"]
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    n_db, W, tick, nch, ticks = 8000 * 30, 24000, 160, 512, 3
+    nf_db = (n_db + HOP - 1) // HOP
+    nfw = (W + HOP - 1) // HOP
+    rng = np.random.default_rng(4545)
+    span = W + ticks * tick
+    src = [int(rng.integers(db_clips)) for _ in range(nch)]
+    offs = [256 * int(rng.integers(0, (n_db - span) // HOP)) + int(rng.integers(0, 4)) * 40 for _ in range(nch)]
+    pcm = tfp_lib.synth_pcm(SEED_DB, src, span, offsets=offs)
+    for c in range(3, nch, 4):  # unrelated audio on every 4th channel
+        pcm[c] = tfp_lib.synth_pcm(SEED_Q + 9, [c], span)[0]
+    p = tfp_lib.params(1, 0.001)
+
+    def run(st, label):
+        for t in range(W // tick):
+            st.push(np.ascontiguousarray(pcm[:, t * tick:(t + 1) * tick]))
+        checked = found = 0
+        for t in range(ticks):
+            s0 = W + t * tick
+            res = st.push(np.ascontiguousarray(pcm[:, s0:s0 + tick]), p)
+            chans = rng.choice(nch, 32, replace=False)
+            qdb = np.concatenate([oracle.fingerprint(pcm[c, s0 + tick - W:s0 + tick])[1] for c in chans])
+            w, mc = idx.search_batch(qdb[:, 0], qdb[:, 1], np.arange(len(chans) + 1) * nfw, 1, 0.001,
+                                     nthreads=ORACLE_THREADS)
+            for i, c in enumerate(chans):
+                exp = {"audio_uuid": uuids[w[i]], "match_count": int(mc[i]), "frame_count": nfw} if w[i] >= 0 else None
+                assert res[c] == exp, (label, t, int(c))
+                checked += 1
+                found += w[i] >= 0
+        assert checked == 32 * ticks and found > 20, (label, found)
+
+    st = tfp_lib.Stream(eng, nch, W)
+    try:
+        run(st, "engine")
+    finally:
+        st.close()
+    # the same clips in a two-shard device group, enrolled from the DB engine's fingerprints
+    g = tfp_lib.Group([0, 0])
+    try:
+        chunk = 2048
+        buf = torch.empty((chunk, n_db), dtype=torch.int16, device=dev)
+        micro = torch.empty((chunk * nf_db, 2), dtype=torch.int32, device=dev)
+        for s0 in range(0, db_clips, chunk):
+            ids = list(range(s0, min(db_clips, s0 + chunk)))
+            k = len(ids)
+            eng.synth_device(SEED_DB, ids, n_db, buf.data_ptr(), stream=stream)
+            eng.fingerprint_device(eng.plan(np.arange(k + 1, dtype=np.int64) * n_db), buf.data_ptr(), micro.data_ptr(), 0,
+                                   stream)
+            torch.cuda.synchronize()
+            rows = micro[:k * nf_db].cpu().numpy()
+            g.index_add_batch([uuids[i] for i in ids], np.arange(k + 1, dtype=np.int64) * nf_db, rows[:, 0], rows[:, 1])
+        del buf, micro
+        torch.cuda.empty_cache()
+        g.index_commit()
+        assert sum(c for _, c in g.engine_stats()) == db_clips
+        gs = tfp_lib.GroupStream(g, nch, W)
+        try:
+            run(gs, "group")
+        finally:
+            gs.close()
+    finally:
+        g.close()
 
 
 def noise_clips(n, nsamples, seed=0x7153C3):

@@ -233,3 +233,31 @@ def test_host_alloc_buffers_read_in_place(engine, tfp_lib):
     assert L.tfp_host_alloc(0, ctypes.byref(bad)) != 0
     L.tfp_host_free(None)
     engine.index_clear()
+
+
+def test_device_fingerprint_of_a_clip_past_the_buffer_range(engine, oracle, torch_cuda):
+    """A clip of >= 2^30 - 2^16 samples (kDirectMaxSamples, 37 h at 8 kHz) would overflow the 8 kHz
+    kernel's 32-bit buffer range and offsets; the plan sends it to the generic kernel (64-bit sample
+    offsets). Its first frames, frames in the middle and its zero-padded end equal the oracle's
+    fingerprints of the same samples (frame f depends only on hops f - 1 and f, so a slice that starts
+    one hop before frame f reproduces it from its second frame on)."""
+    torch = torch_cuda
+    n = (1 << 30) - (1 << 16) + 12345
+    pcm = torch.empty(n, dtype=torch.int16, device="cuda")
+    engine.synth_device(0x7153C3, [5], n, pcm.data_ptr())
+    plan = engine.plan(np.array([0, n], dtype=np.int64))
+    micro = torch.empty((plan.nframes, 2), dtype=torch.int32, device="cuda")
+    engine.fingerprint_device(plan, pcm.data_ptr(), micro.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    nf = plan.nframes
+    assert nf == (n + 255) // 256
+    for f0 in (0, nf // 2 + 3, nf - 40):
+        s0 = max(0, 256 * (f0 - 1))
+        s1 = min(n, 256 * (f0 + 40))
+        x = pcm[s0:s1].cpu().numpy()
+        _, _, want = oracle.fingerprint(x)
+        skip = 0 if f0 == 0 else 1
+        got = micro[f0:f0 + len(want) - skip].cpu().numpy()
+        assert np.array_equal(got, want[skip:skip + len(got)]), f0
+    del pcm, micro
+    torch.cuda.empty_cache()

@@ -232,3 +232,78 @@ def test_group_add_batch_all_or_nothing(tfp_lib, oracle, monkeypatch):
         assert _pairs(g.search_pcm_batch(q.reshape(-1), np.arange(7) * 16000, p)[0]) == exp
     finally:
         g.close()
+
+
+def test_group_enrolment_is_o_new_clips(oracle, tfp_lib):
+    """Single-clip enrolments into a populated group (the shim's fp_craete_audio_list_info path,
+    src/fp_handler.c:538-575 / src/app_tiresias.c:365-424; the clip is searchable at once,
+    :559-571): each new clip takes the middle of its uuid neighbours' tie-key gap, so no other key
+    changes and the shards get the new clips' keys only (tfp_index_update_tiebreak); their index
+    delta updates do not re-send the main columns' keys. Every batch-1 search after an add, and after
+    removals of an old and of a new clip, == the oracle over the live rows (ties to the greatest
+    uuid across shards)."""
+    import test_gpu_index as tgi
+    rng = np.random.default_rng(9191)
+    n0, nadd = 3000, 40
+    data = tgi._dense_db(rng, n0 + nadd, 30)
+    uu = _uuids(rng, n0 + nadd)
+    uu[n0 + 5] = "00000000-0000-4000-8000-000000000001"  # a new first uuid
+    uu[n0 + 6] = "ffffffff-ffff-4fff-bfff-ffffffffffff"  # a new last uuid
+    uu[n0 + 7] = uu[10][:-1] + ("0" if uu[10][-1] != "0" else "1")  # a neighbour of an old uuid
+    data[n0 + 8] = data[20]  # a copy of an old clip's rows: a tie decided by the uuid across shards
+    old = os.environ.get("TFP_INDEX_DELTA")
+    os.environ["TFP_INDEX_DELTA"] = "1"  # (test knob: the index delta at this DB size too)
+    try:
+        g = tfp_lib.Group([0, 0])
+    finally:
+        if old is None:
+            del os.environ["TFP_INDEX_DELTA"]
+        else:
+            os.environ["TFP_INDEX_DELTA"] = old
+    live = {}
+    p = tfp_lib.params(1, 0.001)
+    try:
+        foff = np.concatenate([[0], np.cumsum([len(data[c][0]) for c in range(n0)])]).astype(np.int64)
+        g.index_add_batch(uu[:n0], foff, np.concatenate([data[c][0] for c in range(n0)]),
+                          np.concatenate([data[c][1] for c in range(n0)]))
+        for c in range(n0):
+            live[uu[c]] = data[c]
+        g.index_commit()
+        st0 = g.tiebreak_stats()
+        found = 0
+
+        def check(src):
+            q = []
+            for c in src:
+                m1, m2 = data[c]
+                sel = rng.integers(0, len(m1), 25)
+                q.append(np.stack([m1[sel] / 1e6 + 0.0004, m2[sel] / 1e6], axis=1))
+            qdb = np.concatenate(q)
+            qoff = np.arange(len(src) + 1, dtype=np.int64) * 25
+            exp = _oracle_search(oracle, live, qdb[:, 0], qdb[:, 1], qoff, p)
+            fr = np.zeros(len(qdb), tfp_lib.FRAME_DTYPE)
+            fr["q1"], fr["q2"] = qdb[:, 0], qdb[:, 1]
+            for i in range(len(src)):
+                res, _ = g.search_batch(fr[qoff[i]:qoff[i + 1]], [0, 25], p)  # batch-1
+                got = None if res[0] is None else (res[0]["audio_uuid"], res[0]["match_count"])
+                assert got == exp[i], (i, src[i])
+            return sum(e is not None for e in exp)
+
+        for j in range(nadd):
+            c = n0 + j
+            g.index_add(uu[c], *data[c])
+            live[uu[c]] = data[c]
+            found += check([c, int(rng.integers(n0)), 20])
+        st = g.tiebreak_stats()
+        # the first enrolment's respace only; one push of new keys per add; at most one full key
+        # upload per shard (the first delta update widens the rows: a larger key buffer)
+        assert st["respaces"] == st0["respaces"], (st0, st)
+        assert st["partial_pushes"] - st0["partial_pushes"] >= nadd, (st0, st)
+        assert st["shard_full_key_updates"] - st0["shard_full_key_updates"] <= 2, (st0, st)
+        for u in (uu[33], uu[n0 + 3]):  # an old clip and a new one removed
+            g.index_remove(u)
+            del live[u]
+        found += check([n0 + 4, 20, n0 + 8, int(rng.integers(n0))])
+        assert found > nadd
+    finally:
+        g.close()

@@ -281,8 +281,8 @@ def test_sweep_8bit_count_field_edge(oracle, tfp_lib, tol):
 
 @pytest.mark.parametrize("tol", [0.001, 0.1])
 def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
-    """The sweep's bin sort (tfp_scan.hip wide_bins .. wide_dir_fill_bins) on bins of every size
-    class: 600 queries (three 256-query chunks, the last partly filled) whose max2 values mix a wide
+    """The sweep's bin sort (tfp_scan.hip wide_bin_hist .. wide_bin_sort, which also fills the
+    directories) on bins of every size class: 600 queries (three 256-query chunks, the last partly filled) whose max2 values mix a wide
     spread (bins of a few frames: the in-register sort), a 4 dB cluster (bins of hundreds: the LDS
     sort), repeated values (equal keys), frames whose max2 condition an ignore filter drops (their
     segment is not sorted), NULL values and keys over the ignore filter (not kept: the chunk's tail); then the same queries with a
@@ -336,8 +336,17 @@ def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
                 for c in range(nclips):
                     sel = clip == c
                     eng.index_add(uuids[c], m1[sel], m2[sel])
+                st0 = eng.sweep_stats()
                 res, fcs = eng.search_batch(frames, qoff, tfp_lib.params(2, tol, low, high))
                 got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
                 assert got == expect, (form, cluster_db, tol, [i for i in range(nq) if got[i] != expect[i]][:5])
+                # the sort path that ran (tfp_sweep_stats): a silent fallback to the library sort fails here
+                st = {k: v - st0[k] for k, v in eng.sweep_stats().items()}
+                if form == "libsort":
+                    assert (st["bins"], st["library"], st["redone"]) == (0, 1, 0), st
+                elif cluster_db == 4.0:
+                    assert (st["bins"], st["library"], st["redone"]) == (1, 0, 0), st
+                else:  # a bin of distinct values above the per-wave cap: redone with the library sort
+                    assert (st["bins"], st["library"], st["redone"]) == (0, 1, 1), st
             finally:
                 eng.close()
