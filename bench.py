@@ -672,6 +672,7 @@ def run_match(args, eng, torch, dev, sh, rank, world, dist, barrier, max_over_ra
         res["enrol_then_search"] = enrol_latency(args, eng, T, torch, dev, sh, p)
     if world == 1:
         res["tolerance_alternation"] = tol_alternation(args, eng, T, host_q, qn)
+        res["coefs2_cache"] = coefs2_cache(args, eng, T, host_q, qn)
     if rank == 0 and world == 1 and not args.no_cpu:
         res["cpu_baseline"] = match_cpu_baseline(args, T, eng, torch, dev, sh)
         res["cpu_baseline_full_db"] = match_cpu_full_db(args, eng, torch, dev, sh, qpcm[:256].cpu().numpy())
@@ -801,6 +802,58 @@ def enrol_latency(args, eng, T, torch, dev, sh, p, n_add=8):
             "full_resort": {"p50_ms": float(np.percentile(full, 50)), "max_ms": float(np.max(full)), "samples_ms": full,
                             "how": "same calls on an engine with TFP_INDEX_FULL=1 (every update a full radix sort of all "
                                    "staged rows + a uuid sort), the round-2 behaviour"}}
+
+
+def coefs2_cache(args, eng, T, hq, qn, n_calls=100, n_add=8):
+    """coefs = 2 callers (src/fp_handler.c:318-353) at the 100k-clip DB, batch-1 from host PCM:
+      alternation   searches alternating tolerance 0.001 and 0.45 (the tolerance is passed per call,
+                    application_handler.c:114-122): served by the clip-set cache LRU (the active
+                    tolerance and three others), p50 / p99;
+      after_enrol   the first search after an enrolment (tfp_index_add of one 30 s clip, then a search
+                    at 0.001 or 0.45 in turn, timed together): a coefs = 2 search merges the index delta
+                    first, the clip order is merged with it (tfp_index.hip launch_order_merge) and the
+                    cache of the search's tolerance is rebuilt from that order (a filter, no sort);
+                    the round-5 build sorted every box row (1.2 ms at 0.001, 27 ms at 0.45).
+    The added clips are removed again afterwards."""
+    p_lo, p_hi = T.params(2, 0.001), T.params(2, 0.45)
+    for i in range(4):  # untimed: both tolerances' caches at this index version
+        eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
+    c0, w0 = eng.index_cache_stats(), eng.sweep_stats()
+    lat = []
+    for i in range(n_calls):
+        t0 = time.perf_counter()
+        eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
+        lat.append((time.perf_counter() - t0) * 1e3)
+    c1 = eng.index_cache_stats()
+    n_db = 8000 * 30
+    nf_db = (n_db + HOP - 1) // HOP
+    pcm = np.random.default_rng(0x7153C4).integers(-32768, 32768, (n_add, n_db)).astype(np.int16)
+    fr = eng.fingerprint_batch(pcm.reshape(-1), np.arange(n_add + 1) * n_db)
+    uuids = ["fffffffe-ffff-4fff-bfff-%012x" % i for i in range(n_add)]
+    first = []
+    for i, u in enumerate(uuids):
+        t0 = time.perf_counter()
+        eng.index_add(u, fr["m1"][i * nf_db:(i + 1) * nf_db], fr["m2"][i * nf_db:(i + 1) * nf_db])
+        eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
+        first.append((time.perf_counter() - t0) * 1e3)
+    c2, w2 = eng.index_cache_stats(), eng.sweep_stats()
+    for u in uuids:
+        eng.index_remove(u)
+    eng.index_commit()
+    out = {"workload": f"coefs 2, batch-1 5 s host-PCM queries on the {args.db_clips}-clip DB",
+           "alternation": {"calls": n_calls, "tolerances": [0.001, 0.45], "p50_ms": float(np.percentile(lat, 50)),
+                           "p99_ms": float(np.percentile(lat, 99)), "max_ms": float(np.max(lat)),
+                           "cache_builds": c1["builds"] - c0["builds"], "cache_hits": c1["hits"] - c0["hits"]},
+           "after_enrol": {"adds": n_add, "tolerances": "0.001 / 0.45 in turn", "p50_ms": float(np.percentile(first, 50)),
+                           "p99_ms": float(np.percentile(first, 99)), "max_ms": float(np.max(first)), "samples_ms": first,
+                           "cache_builds_from_order": c2["from_order"] - c1["from_order"],
+                           "order_merges": c2["order_merges"] - c1["order_merges"],
+                           "order_full_builds": c2["order_builds"] - c1["order_builds"]},
+           "sweep_paths": {k: w2[k] - w0[k] for k in w2},
+           "harness": "python (ctypes) loop over tfp_search_pcm_batch"}
+    log(f"coefs=2 cache: alternation p50 {out['alternation']['p50_ms']:.3f} p99 {out['alternation']['p99_ms']:.3f} ms; "
+        f"first search after an enrolment p50 {out['after_enrol']['p50_ms']:.2f} p99 {out['after_enrol']['p99_ms']:.2f} ms")
+    return out
 
 
 def tol_alternation(args, eng, T, hq, qn, n_calls=200):
@@ -1074,6 +1127,42 @@ def run_group(args, eng, T, torch, dev, sh, rank, world, dist):
             store.set("tfp_group_leg_done", "1")
 
 
+def group_enrol_latency(g, eng, T, qn, n_add=8):
+    """The shim's enrolment path at the 100k-clip DB (fp_craete_audio_list_info ->
+    tfp_group_index_add, src/fp_handler.c:538-575; the clip searchable at once, :559-571): one new
+    30 s clip added to the group and a batch-1 search of an excerpt of it right after
+    (tfp_group_search_pcm_batch, coefs 1, tolerance 0.45), timed together, as enrol_latency times a
+    bare engine. The new clip takes the middle of its uuid neighbours' tie-key gap and the shard
+    gets that one key (tfp_group_tiebreak_stats: no respace, one new-clip push per add); the new
+    clips are white noise whose rows alone lie in the query's key box (see enrol_latency)."""
+    n_db = 8000 * 30
+    nf_db = (n_db + HOP - 1) // HOP
+    pcm = np.random.default_rng(0x7153C5).integers(-32768, 32768, (n_add, n_db)).astype(np.int16)
+    fr = eng.fingerprint_batch(pcm.reshape(-1), np.arange(n_add + 1) * n_db)
+    uuids = ["fffffffd-ffff-4fff-bfff-%012x" % i for i in range(n_add)]
+    pq = T.params(1, 0.45)
+    g.search_pcm_batch(np.ascontiguousarray(pcm[0, :qn]), [0, qn], pq)  # untimed: this tolerance's caches
+    t0s = g.tiebreak_stats()
+    lat, won = [], 0
+    for i, u in enumerate(uuids):
+        q = np.ascontiguousarray(pcm[i, 256 * 100: 256 * 100 + qn])
+        t0 = time.perf_counter()
+        g.index_add(u, fr["m1"][i * nf_db:(i + 1) * nf_db], fr["m2"][i * nf_db:(i + 1) * nf_db])
+        res, _ = g.search_pcm_batch(q, [0, qn], pq)
+        lat.append((time.perf_counter() - t0) * 1e3)
+        won += res[0] is not None and res[0]["audio_uuid"] == u
+    t1s = g.tiebreak_stats()
+    for u in uuids:
+        g.index_remove(u)
+    g.index_commit()
+    out = {"workload": f"{n_add} x (tfp_group_index_add of one 30 s clip + batch-1 tfp_group_search_pcm_batch of a 5 s "
+                       "excerpt of it, coefs 1, tolerance 0.45) on the group's 100k-clip DB, host PCM",
+           "p50_ms": float(np.percentile(lat, 50)), "max_ms": float(np.max(lat)), "samples_ms": lat, "new_clip_won": won,
+           "tie_keys": {k: t1s[k] - t0s[k] for k in t1s}, "harness": "python (ctypes) loop"}
+    log(f"group enrol-then-search: p50 {out['p50_ms']:.3f} ms, won {won}/{n_add}, keys {out['tie_keys']}")
+    return out
+
+
 def _group_leg(args, eng, T, torch, dev, sh, world):
     from tiresias_amd import Group, GroupStream
     ndev = T.device_count()
@@ -1143,6 +1232,7 @@ def _group_leg(args, eng, T, torch, dev, sh, world):
            "latency_p50_ms": float(np.percentile(out_ms, 50)), "latency_p99_ms": float(np.percentile(out_ms, 99)),
            "latency_harness": "C loop over tfp_group_search_pcm_batch (bench/tfp_latency.c), %d calls over %d queries"
                               % (n_it, nl)}
+    out["enrol_then_search"] = group_enrol_latency(g, eng, T, qn)
     assert set(GROUP_FIELDS) <= set(out), sorted(set(GROUP_FIELDS) - set(out))
     del hq
     if args.stream_channels > 0:

@@ -322,6 +322,7 @@ def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
         return frames, q1, q2, np.asarray(qoff, np.int64)
 
     low, high = -1, 3400
+    redo_seen = []
     for cluster_db in (4.0, 0.02):
         frames, q1, q2, qoff = batch(cluster_db)
         expect = []
@@ -346,7 +347,53 @@ def test_bin_sort_bin_sizes(oracle, tfp_lib, tol):
                     assert (st["bins"], st["library"], st["redone"]) == (0, 1, 0), st
                 elif cluster_db == 4.0:
                     assert (st["bins"], st["library"], st["redone"]) == (1, 0, 0), st
-                else:  # a bin of distinct values above the per-wave cap: redone with the library sort
-                    assert (st["bins"], st["library"], st["redone"]) == (0, 1, 1), st
+                else:  # the 0.02 dB cluster: a bin of distinct values above the per-wave cap redoes the batch
+                    # with the library sort; where the cluster's bins stay under the cap (or hold one value:
+                    # copied as a crowd) the bin sort stands
+                    assert (st["bins"], st["library"], st["redone"]) in ((0, 1, 1), (1, 0, 0)), st
+                    redo_seen.append(st["redone"])
             finally:
                 eng.close()
+
+
+def test_bin_sort_overflow_redone_with_library_sort(oracle, tfp_lib):
+    """A window segment whose frames crowd into one bin with distinct values (990 frames of one key
+    within 0.001 dB of 40 dB, 10 spread over 100 dB: the segment's bins are cut over its whole L2
+    range) overflows the bin sort's per-wave cap: the speculative pass is redone with the library
+    sort (tfp_sweep_stats: one redo, one library batch, no bin batch) and the keys == the oracle's
+    (src/fp_handler.c:318-374)."""
+    rng = np.random.default_rng(77)
+    nclips, rows = 30, 200
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
+    m1 = (20_000_000 + rng.integers(-900, 900, nclips * rows)).astype(np.int32)
+    m2 = np.where(rng.random(nclips * rows) < 0.7, 40_000_000 + rng.integers(0, 1000, nclips * rows),
+                  rng.integers(-50_000_000, 50_000_000, nclips * rows)).astype(np.int32)
+    clip = np.repeat(np.arange(nclips), rows).astype(np.int32)
+    nq, per = 10, 100
+    q1 = np.full(nq * per, 20.3)
+    q2 = 40.0 + rng.permutation(nq * per).astype(np.float64) * 1e-6  # 1,000 distinct values within 0.001 dB
+    spread = rng.choice(nq * per, 10, replace=False)
+    q2[spread] = rng.uniform(-50, 50, 10)
+    qoff = np.arange(nq + 1, dtype=np.int64) * per
+    frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                         ("q1", "<f8"), ("q2", "<f8")]))
+    frames["q1"], frames["q2"] = q1, q2
+    expect = []
+    for i in range(nq):
+        s = slice(qoff[i], qoff[i + 1])
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, 0.001, -1, -1)
+        expect.append((uuids[w], mc) if found else None)
+    assert sum(e is not None for e in expect) >= nq // 2
+    eng = _engine_with(tfp_lib, {"TFP_WIDE_MIN_TOL": "0"})
+    try:
+        for c in range(nclips):
+            sel = clip == c
+            eng.index_add(uuids[c], m1[sel], m2[sel])
+        st0 = eng.sweep_stats()
+        res, _ = eng.search_batch(frames, qoff, tfp_lib.params(2, 0.001))
+        got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+        assert got == expect
+        st = {k: v - st0[k] for k, v in eng.sweep_stats().items()}
+        assert (st["bins"], st["library"], st["redone"]) == (0, 1, 1), st
+    finally:
+        eng.close()
