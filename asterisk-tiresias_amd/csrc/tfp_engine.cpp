@@ -219,6 +219,9 @@ struct tfp_engine {
   static constexpr int kTolSlots = 3;
   TolSlot tol_lru[kTolSlots];
   uint64_t index_version = 1, tol_clock = 0;
+  // the main index's own version (builds and merges; a delta update leaves it): the clip-set caches
+  // hold main-index rows only, so they stay valid across delta updates
+  uint64_t main_version = 1;
   // general path: clip-set cache at tolerance cell_tol (tfp_scan.hip), built on first use per
   // index version and tolerance
   CellCache cells;
@@ -234,6 +237,18 @@ struct tfp_engine {
   // the coefs = 2 sweep's sort path per batch (tfp_sweep_stats): the bin sort's speculative pass
   // stood, the library sort ran, a speculative pass was redone; crowd bins the bin sort copied
   int64_t n_sweep_bins = 0, n_sweep_lib = 0, n_sweep_redo = 0, n_sweep_crowd = 0;
+  // coefs = 2 with an index delta (round 6): the delta's own clip-set cache (its staged rows in clip
+  // order, columns numbered from 0 in uuid order), swept after the main cache into the same maxima,
+  // so an enrolment followed by a coefs = 2 search does not merge the index (fp_handler.c:559-571:
+  // the reference's INSERT makes a clip searchable for the cost of its own rows)
+  CellCache dcells;
+  double dcell_tol = 0.0;
+  uint64_t dcell_version = 0, dl_version = 0;  // index versions of dcells and of the delta rows' order
+  bool dcell_fresh = false;
+  DevBuf dl_key, dl_m1, dl_key_b, dl_m1_b;
+  CacheBuf dl_sort_tmp;
+  bool delta_wide = true;  // TFP_DELTA_WIDE=0: coefs = 2 searches merge the delta first (A/B, tests)
+  int64_t n_delta_cell_builds = 0, n_delta_sweeps = 0;
   // the index rows in clip order (tfp_kernels.hpp), the source of the caches at tolerances up to
   // kOrderMaxTol: built on the first search that needs it, then carried through every merge
   DevBuf o_key, o_m1, o_key_b, o_m1_b, o_newcol;
@@ -1009,6 +1024,7 @@ int rebuild(tfp_engine* e) {
   e->removed_built = false;
   e->dirty = false;
   e->index_version++;  // (other tolerances' cached ranges and bitsets are for the previous index)
+  e->main_version++;
   e->rng_valid = carried;  // the key-range and clip-set caches follow the index (merge_index may carry the ranges and bitsets)
   e->key_bits_valid = carried && e->key_bits_valid;
   if (e->key_bits_valid) e->key_bits_cols = e->ncols;
@@ -1291,31 +1307,41 @@ int ensure_order(tfp_engine* e, hipStream_t s) {
   return TFP_OK;
 }
 
+// The keys' "%f" boxes at tolerance tole (launch_key_boxes), for the caches built from a clip order.
+int ensure_kbox(tfp_engine* e, double tole, hipStream_t s) {
+  if (e->kbox_valid && memcmp(&e->kbox_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  HIPCHK(e, e->kbox.reserve(sizeof(int64_t) * 2 * kKeyRange));
+  HIPCHK(e, launch_key_boxes(tole, e->kbox.as<int64_t>(), s));
+  e->kbox_tol = tole;
+  e->kbox_valid = true;
+  return TFP_OK;
+}
+
 // The general path's clip-set cache at tolerance tole (after ensure_ranges at tole): the active one,
 // or one of kCellSlots others (least recently used out), per index version. Built from the clip
 // order for tolerances up to kOrderMaxTol (no sort), else from the boxes' rows.
 int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
-  if (e->cell_fresh && e->cell_version == e->index_version && memcmp(&e->cell_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  if (e->cell_fresh && e->cell_version == e->main_version && memcmp(&e->cell_tol, &tole, sizeof tole) == 0) return TFP_OK;
   CellSlot* hit = nullptr;
   CellSlot* victim = &e->cell_lru[0];
   for (CellSlot& t : e->cell_lru) {
-    if (t.version != e->index_version) t.has = false;
+    if (t.version != e->main_version) t.has = false;
     if (t.has && memcmp(&t.tol, &tole, sizeof tole) == 0) hit = &t;
     if (t.has != victim->has ? !t.has : t.used < victim->used) victim = &t;
   }
-  const bool active = e->cell_fresh && e->cell_version == e->index_version;
+  const bool active = e->cell_fresh && e->cell_version == e->main_version;
   CellSlot* into = hit ? hit : victim;
   // the active cache (when current) goes into the slot the wanted one comes from (or the victim's,
   // whose buffers the build below then reuses)
   e->cells.swap(into->c);
   std::swap(e->cell_tol, into->tol);
   into->has = active;
-  into->version = e->index_version;
+  into->version = e->main_version;
   into->used = ++e->tol_clock;
   if (hit) {
     e->cell_tol = tole;
     e->cell_fresh = true;
-    e->cell_version = e->index_version;
+    e->cell_version = e->main_version;
     e->n_cell_hits++;
     return TFP_OK;
   }
@@ -1326,22 +1352,17 @@ int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
   if (tole >= 0.0 && tole <= kOrderMaxTol && e->nrows > 0 && e->nrows < INT32_MAX) {
     int rc = ensure_order(e, s);
     if (rc) return rc;
-    if (!e->kbox_valid || memcmp(&e->kbox_tol, &tole, sizeof tole) != 0) {
-      HIPCHK(e, e->kbox.reserve(sizeof(int64_t) * 2 * kKeyRange));
-      HIPCHK(e, launch_key_boxes(tole, e->kbox.as<int64_t>(), s));
-      e->kbox_tol = tole;
-      e->kbox_valid = true;
-    }
+    if ((rc = ensure_kbox(e, tole, s))) return rc;
     st = e->cells.build_from_order(e->o_key.as<unsigned long long>(), e->o_m1.as<int32_t>(), e->o_rows, e->kbox.as<int64_t>(),
-                                   e->ncols, tole, s);
+                                   (int32_t)e->col_clip.size(), tole, s);
     if (st == hipSuccess && e->cells.valid) e->n_cell_from_order++;
   } else {
     std::vector<int64_t> rng(2 * kKeyRange), off(kKeyRange + 1, 0);
     HIPCHK(e, hipMemcpyAsync(rng.data(), e->rng_all.p, sizeof(int64_t) * rng.size(), hipMemcpyDeviceToHost, s));
     HIPCHK(e, hipStreamSynchronize(s));
     for (int k = 0; k < kKeyRange; k++) off[k + 1] = off[k] + std::max<int64_t>(0, rng[2 * k + 1] - rng[2 * k]);
-    st = e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(), e->ncols, e->nrows,
-                        tole, s);
+    st = e->cells.build(e->rng_all.as<int64_t>(), off.data(), e->m2s.as<int32_t>(), e->cols.as<int32_t>(),
+                        (int32_t)e->col_clip.size(), e->nrows, tole, s);
   }
   if (st != hipSuccess) {
     (void)hipGetLastError();
@@ -1351,8 +1372,46 @@ int ensure_cells(tfp_engine* e, double tole, hipStream_t s) {
   }
   e->cell_tol = tole;
   e->cell_fresh = true;
-  e->cell_version = e->index_version;
+  e->cell_version = e->main_version;
   return TFP_OK;
+}
+
+// The index delta's clip-set cache at tolerance tole (<= kOrderMaxTol): the delta's staged rows in
+// clip order (sorted once per delta version, for any tolerance), then the main cache's filter.
+// Valid (or known empty: no delta row in a box) at the current index version.
+int ensure_delta_cells(tfp_engine* e, double tole, hipStream_t s) {
+  if (e->dcell_fresh && e->dcell_version == e->index_version && memcmp(&e->dcell_tol, &tole, sizeof tole) == 0) return TFP_OK;
+  e->dcell_fresh = false;
+  e->dcells.invalidate();
+  const int32_t D = (int32_t)e->delta_clip.size();
+  const int64_t n = e->delta_rows;
+  if (D > 0 && n > 0) {
+    if (e->dl_version != e->index_version) {
+      HIPCHK(e, e->dl_key.reserve_grow(sizeof(unsigned long long) * n));
+      HIPCHK(e, e->dl_m1.reserve_grow(sizeof(int32_t) * n));
+      HIPCHK(e, e->dl_key_b.reserve_grow(sizeof(unsigned long long) * n));
+      HIPCHK(e, e->dl_m1_b.reserve_grow(sizeof(int32_t) * n));
+      HIPCHK(e, launch_delta_order_fill(e->d_delta.as<DeltaClip>(), D, e->st_m1.as<int32_t>(), e->st_m2.as<int32_t>(),
+                                        e->dl_key_b.as<unsigned long long>(), e->dl_m1_b.as<int32_t>(), s));
+      HIPCHK(e, order_sort(e->dl_key_b.as<unsigned long long>(), e->dl_key.as<unsigned long long>(), e->dl_m1_b.as<int32_t>(),
+                           e->dl_m1.as<int32_t>(), n, &e->dl_sort_tmp, s));
+      e->dl_version = e->index_version;
+    }
+    int rc = ensure_kbox(e, tole, s);
+    if (rc) return rc;
+    HIPCHK(e, e->dcells.build_from_order(e->dl_key.as<unsigned long long>(), e->dl_m1.as<int32_t>(), n, e->kbox.as<int64_t>(),
+                                         D, tole, s));
+    e->n_delta_cell_builds++;
+  }
+  e->dcell_tol = tole;
+  e->dcell_version = e->index_version;
+  e->dcell_fresh = true;
+  return TFP_OK;
+}
+
+// Can the sweep serve a search at tolerance tole with the index delta beside the main index?
+bool delta_wide_ok(const tfp_engine* e, double tole) {
+  return e->delta_wide && tole >= 0.0 && tole <= kOrderMaxTol && tole >= e->wide_min_tol;
 }
 
 // ---- search core: frames' q values already on device (e->q, 2 doubles per frame) -----------
@@ -1371,9 +1430,12 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   sc.has_high = P->freq_ignore_high > 0;
   if (sc.has_low) sc.thr_low = 10 * log10((double)P->freq_ignore_low);
   if (sc.has_high) sc.thr_high = 10 * log10((double)P->freq_ignore_high);
-  // the index delta serves the coefs = 1 vote paths at the tolerances its bits cover; any other
-  // search reads the sorted rows, so the delta is merged into them first
-  if (!e->delta_clip.empty() && (sc.coefs != 1 || !delta_tol_ok(sc.tole)) && (rc = consolidate(e))) return rc;
+  // the index delta serves the coefs = 1 vote paths at the tolerances its bits cover, and the sweep
+  // (its own clip-set cache beside the main one) at tolerances up to kOrderMaxTol; any other search
+  // reads the sorted rows, so the delta is merged into them first
+  if (!e->delta_clip.empty() && ((sc.coefs == 1 && !delta_tol_ok(sc.tole)) || (sc.coefs != 1 && !delta_wide_ok(e, sc.tole))) &&
+      (rc = consolidate(e)))
+    return rc;
   const bool has_delta = !e->delta_clip.empty();
   const int64_t R_all = e->nrows + e->delta_rows;  // rows that may match (main index + delta)
 
@@ -1455,7 +1517,7 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
   int64_t max_frames = 0;
   for (int32_t i = 0; i < nq; i++) max_frames = std::max<int64_t>(max_frames, qo[i + 1] - qo[i]);
   const bool vote = sc.coefs == 1 && C > 0 && R_all > 0 && max_frames < 16384;  // packed scores exact below 16384 frames
-  if (!vote && has_delta) {  // (the general path reads the sorted rows)
+  if (!vote && has_delta && !delta_wide_ok(e, sc.tole)) {  // (the cells form and the row scan read the sorted rows)
     if ((rc = consolidate(e))) return rc;
     return search_core(e, h_qoff, nq, d_q, P, keys, d_keys_out, s);
   }
@@ -1510,7 +1572,9 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       // general path: the sweep by groups (tfp_scan.hip), unless a frame needs the row scan
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
       if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
-      if (e->cells.valid) {
+      // with a delta: its cache too (a failure to build it merges the delta, below)
+      const bool dsweep = has_delta && e->cells.valid && ensure_delta_cells(e, sc.tole, s) == TFP_OK;
+      if (e->cells.valid && (dsweep || !has_delta)) {
         HIPCHK(e, e->wide.reserve(nf, nq, s));
         bool ok = false;
         // (a device caller's output buffer takes the sweep's keys directly: zeroed by the prepare)
@@ -1530,6 +1594,11 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
             d_info = e->spec_pin_dev;
           }
           HIPCHK(e, launch_scan_wide(nq, nf, &e->cells, e->tiekey.as<int32_t>(), C, &e->wide, wbest, s, d_info, &spec_mapped));
+          if (dsweep && e->dcells.valid) {  // the delta's clips into the same maxima
+            HIPCHK(e, launch_scan_wide(nq, nf, &e->dcells, e->tiekey.as<int32_t>(), C, &e->wide, wbest, s, d_info, &spec_mapped,
+                                       e->delta_col0));
+            e->n_delta_sweeps++;
+          }
           done = true;
           swept = true;
           out_written = d_keys_out != nullptr;
@@ -1538,6 +1607,10 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
         if (e->dbg_vote) fprintf(stderr, "[tfp] general path: nq %d nf %lld C %d tol %g -> %s%s\n", nq, (long long)nf, C,
                                  sc.tole, ok ? "sweep by groups" : "cells / row scan", spec ? " (speculative)" : "");
       }
+    }
+    if (!done && has_delta) {  // the cells form and the row scan read the sorted rows: the delta merged first
+      if ((rc = consolidate(e))) return rc;
+      return search_core(e, h_qoff, nq, d_q, P, keys, d_keys_out, s);
     }
     if (!done && C > 0 && R > 0 && (sc.coefs == 1 || sc.coefs == 2)) {
       // general path (tfp_scan.hip): queries in chunks of <= 256 MB of scratch per array
@@ -1695,6 +1768,7 @@ int tfp_engine_create(int32_t device, tfp_engine** out) {
   e->wide.unpacked = tfp::knob("TFP_WIDE_UNPACKED") != nullptr;
   e->wide.libsort = tfp::knob("TFP_WIDE_LIBSORT") != nullptr;
   e->wide.debug_bins = tfp::knob("TFP_DEBUG_BINS") != nullptr;
+  if (const char* v = tfp::knob("TFP_DELTA_WIDE")) e->delta_wide = atoi(v) != 0;
   // operational switches (documented: tiresias_fp.h), read as plain environment variables
   if (const char* v = tfp::op_env("TFP_COALESCE")) e->coalesce = atoi(v) != 0;
   if (const char* v = tfp::op_env("TFP_INDEX_DELTA")) e->use_delta = atoi(v) != 0;
@@ -2221,7 +2295,8 @@ int tfp_sweep_stats(tfp_engine* e, int64_t* bins, int64_t* library, int64_t* red
 }
 
 int tfp_index_cache_stats(tfp_engine* e, int64_t* cache_builds, int64_t* cache_hits, int64_t* from_order,
-                          int64_t* order_builds, int64_t* order_merges) {
+                          int64_t* order_builds, int64_t* order_merges, int64_t* delta_cache_builds,
+                          int64_t* delta_sweeps) {
   if (!e) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   if (cache_builds) *cache_builds = e->n_cell_builds;
@@ -2229,6 +2304,8 @@ int tfp_index_cache_stats(tfp_engine* e, int64_t* cache_builds, int64_t* cache_h
   if (from_order) *from_order = e->n_cell_from_order;
   if (order_builds) *order_builds = e->n_order_builds;
   if (order_merges) *order_merges = e->n_order_merges;
+  if (delta_cache_builds) *delta_cache_builds = e->n_delta_cell_builds;
+  if (delta_sweeps) *delta_sweeps = e->n_delta_sweeps;
   return TFP_OK;
 }
 

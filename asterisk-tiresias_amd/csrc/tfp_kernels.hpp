@@ -213,6 +213,12 @@ hipError_t launch_order_fill(const int32_t* m1s, const int32_t* m2s, const int32
                              unsigned long long* okey, int32_t* om1, hipStream_t s);
 hipError_t order_sort(const unsigned long long* kin, unsigned long long* kout, const int32_t* vin, int32_t* vout, int64_t n,
                       CacheBuf* tmp, hipStream_t s);
+// The clip order of an index delta's staged rows (round 6): delta clip j (uuid order; tfp_index.hpp
+// DeltaClip) takes the local column j; rows are written clip after clip (unsorted: order_sort
+// follows).
+struct DeltaClip;
+hipError_t launch_delta_order_fill(const DeltaClip* d_dc, int32_t nd, const int32_t* st_m1, const int32_t* st_m2,
+                                   unsigned long long* okey, int32_t* om1, hipStream_t s);
 
 // General path (coefs = 2 and the vote's fallbacks; tfp_scan.hip). Clip-set cache of one index
 // version and tolerance: per (key, clip) group the clip's max2 values in the key's "%f" max1 box
@@ -343,8 +349,11 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
 // After prepare: d_best[q] = (count << 32 | tie key) for all nq queries (d_best zeroed on entry).
 // d_info_out (optional, device address of host-mapped memory): the clip-major sweep's last kernel
 // copies ws->info (3 ints) there; *info_written says whether it did.
+// col_base: the index column of the cache's column 0 (an index delta's cache numbers its clips
+// from 0; their tie keys are d_tiekey[col_base + column]). Maxima are combined into d_best with
+// an atomic max, so a second sweep over another cache adds its clips to the same results.
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s, int32_t* d_info_out = nullptr,
-                            bool* info_written = nullptr);
+                            bool* info_written = nullptr, int32_t col_base = 0);
 
 }  // namespace tfp

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "tfp_kernels.hpp"
+#include "tfp_index.hpp"
 #include "tfp_bsearch.hpp"
 #include "tfp_math.hpp"
 
@@ -208,6 +209,28 @@ __global__ void order_fill_kernel(const int32_t* __restrict__ m1s, const int32_t
     okey[i] = ((unsigned long long)order_key_index(m1) << 53) | ((unsigned long long)(uint32_t)cols[i] << 32) |
               (uint32_t)(m2s[i] ^ INT32_MIN);
     om1[i] = m1;
+  }
+}
+
+// An index delta's staged rows as order keys: block j takes clip j (local column j), its rows after
+// those of clips 0 .. j - 1.
+__global__ void delta_order_fill_kernel(const DeltaClip* __restrict__ dc, const int32_t* __restrict__ st_m1,
+                                        const int32_t* __restrict__ st_m2, unsigned long long* __restrict__ okey,
+                                        int32_t* __restrict__ om1) {
+  const int32_t j = blockIdx.x;
+  __shared__ int64_t out0;
+  if (threadIdx.x == 0) {
+    int64_t o = 0;
+    for (int32_t i = 0; i < j; i++) o += dc[i].n;
+    out0 = o;
+  }
+  __syncthreads();
+  const int64_t src = dc[j].off;
+  for (int32_t i = threadIdx.x; i < dc[j].n; i += blockDim.x) {
+    const int32_t m1 = st_m1[src + i];
+    okey[out0 + i] = ((unsigned long long)order_key_index(m1) << 53) | ((unsigned long long)(uint32_t)j << 32) |
+                     (uint32_t)(st_m2[src + i] ^ INT32_MIN);
+    om1[out0 + i] = m1;
   }
 }
 
@@ -443,6 +466,13 @@ hipError_t launch_order_fill(const int32_t* m1s, const int32_t* m2s, const int32
                              unsigned long long* okey, int32_t* om1, hipStream_t s) {
   if (R <= 0) return hipSuccess;
   hipLaunchKernelGGL(order_fill_kernel, dim3(grid_for(R)), dim3(256), 0, s, m1s, m2s, cols, R, okey, om1);
+  return hipGetLastError();
+}
+
+hipError_t launch_delta_order_fill(const DeltaClip* d_dc, int32_t nd, const int32_t* st_m1, const int32_t* st_m2,
+                                   unsigned long long* okey, int32_t* om1, hipStream_t s) {
+  if (nd <= 0) return hipSuccess;
+  hipLaunchKernelGGL(delta_order_fill_kernel, dim3((unsigned)nd), dim3(256), 0, s, d_dc, st_m1, st_m2, okey, om1);
   return hipGetLastError();
 }
 
@@ -1804,8 +1834,12 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
 // of two 16-bit counts) among 64 frames by reading their queries out of the lanes (no per-frame
 // memory dependency).
 constexpr int kPortions = 256;
+// (checkpoint rows every 4 frames, -DTFP_PSTEP=4, write a fourth of the bytes, but wide_clips then
+// adds up to 3 frames' increments per run end: C3 coefs = 2 0.86 / 0.73 / 0.81 / 0.89 ms at tol
+// 0.001 / 0.01 / 0.1 / 0.45 against 0.77 / 0.71 / 0.73 / 0.83 with a row per frame,
+// profiles/r06/c3_pstep_ab_r06h.txt)
 #ifndef TFP_PSTEP
-#define TFP_PSTEP 4
+#define TFP_PSTEP 1
 #endif
 constexpr int kPStep = TFP_PSTEP;  // frames per prefix-count row (1 or 4)
 static_assert(kPStep == 1 || kPStep == 4, "one row a frame, or a 4-byte word of queries a row");
@@ -1946,7 +1980,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
     const uint8_t* __restrict__ qis, const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
-    unsigned long long* __restrict__ part, const int32_t* __restrict__ stop) {
+    unsigned long long* __restrict__ part, const int32_t* __restrict__ stop, int32_t col_base) {
   // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
   // so the sweep reads nothing (the batch is redone; its maxima are not used)
   if (stop && stop[2] > 0) return;
@@ -2156,7 +2190,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
       }
     }
     // the window's clips: each query's best (count << 32 | tie key)
-    const int32_t tk = c0 + lane < C && lane < kWin ? tiekey[c0 + lane] : 0;
+    const int32_t tk = col_base + c0 + lane < C && lane < kWin ? tiekey[col_base + c0 + lane] : 0;
 #pragma unroll
     for (int j = 0; j < kWin; j++) {
       const uint32_t v = acc[j * 64 + lane];
@@ -2457,7 +2491,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
 
 hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, const int32_t* d_tiekey, int32_t C,
                             WideScratch* ws, unsigned long long* d_best, hipStream_t s, int32_t* d_info_out,
-                            bool* info_written) {
+                            bool* info_written, int32_t col_base) {
   if (info_written) *info_written = false;
   if (nq <= 0 || !cells || !cells->valid || !cells->k_gbeg) return hipErrorInvalidValue;
   (void)nf;
@@ -2487,13 +2521,13 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr);
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   }

@@ -96,7 +96,7 @@ _SIGS = {
     "tfp_synchronize": (C.c_int, [P, P]),
     "tfp_group_create": (C.c_int, [P, C.c_int32, C.POINTER(P)]),
     "tfp_group_destroy": (None, [P]),
-    "tfp_index_cache_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 5),
+    "tfp_index_cache_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 7),
     "tfp_sweep_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 4),
     "tfp_group_size": (C.c_int32, [P]),
     "tfp_group_tiebreak_stats": (C.c_int, [P] + [C.POINTER(C.c_int64)] * 3),
@@ -141,6 +141,8 @@ def lib() -> C.CDLL:
                               "(the HIP engine is the only implementation; there is no fallback)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
+            if os.environ.get("TFP_LIB_PATH") and not hasattr(L, name):
+                continue  # an older A/B build without this entry point (calling it raises AttributeError)
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -211,10 +211,11 @@ class Engine:
 
     def index_cache_stats(self) -> dict:
         """The coefs = 2 clip-set caches (tfp_index_cache_stats): builds, cached hits, builds from the
-        clip order, the clip order's full builds and merges."""
-        v = [C.c_int64() for _ in range(5)]
+        clip order, the clip order's full builds and merges, the index delta's caches and sweeps."""
+        v = [C.c_int64() for _ in range(7)]
         self._chk(lib().tfp_index_cache_stats(self._h, *[C.byref(x) for x in v]))
-        return dict(zip(("builds", "hits", "from_order", "order_builds", "order_merges"), [x.value for x in v]))
+        return dict(zip(("builds", "hits", "from_order", "order_builds", "order_merges", "delta_builds", "delta_sweeps"),
+                        [x.value for x in v]))
 
     def set_tiebreak(self, keys):
         keys = np.ascontiguousarray(keys, np.int32)

@@ -810,10 +810,12 @@ def coefs2_cache(args, eng, T, hq, qn, n_calls=100, n_add=8):
                     application_handler.c:114-122): served by the clip-set cache LRU (the active
                     tolerance and three others), p50 / p99;
       after_enrol   the first search after an enrolment (tfp_index_add of one 30 s clip, then a search
-                    at 0.001 or 0.45 in turn, timed together): a coefs = 2 search merges the index delta
-                    first, the clip order is merged with it (tfp_index.hip launch_order_merge) and the
-                    cache of the search's tolerance is rebuilt from that order (a filter, no sort);
-                    the round-5 build sorted every box row (1.2 ms at 0.001, 27 ms at 0.45).
+                    at 0.001 or 0.45 in turn, timed together): the new clips stay in the index delta
+                    and the sweep runs over the delta's own clip-set cache (its rows' clip order,
+                    filtered at the search's tolerance) beside the main caches, which stay; round 6
+                    first merged the delta and rebuilt the cache from the merged clip order (1.9-2.5
+                    ms at 0.001, 3.2-4.4 ms at 0.45), the round-5 build sorted every box row (1.2 ms
+                    at 0.001, 27 ms at 0.45, plus the merge).
     The added clips are removed again afterwards."""
     p_lo, p_hi = T.params(2, 0.001), T.params(2, 0.45)
     for i in range(4):  # untimed: both tolerances' caches at this index version
@@ -825,6 +827,7 @@ def coefs2_cache(args, eng, T, hq, qn, n_calls=100, n_add=8):
         eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
         lat.append((time.perf_counter() - t0) * 1e3)
     c1 = eng.index_cache_stats()
+    b1 = eng.index_build_stats()
     n_db = 8000 * 30
     nf_db = (n_db + HOP - 1) // HOP
     pcm = np.random.default_rng(0x7153C4).integers(-32768, 32768, (n_add, n_db)).astype(np.int16)
@@ -837,6 +840,7 @@ def coefs2_cache(args, eng, T, hq, qn, n_calls=100, n_add=8):
         eng.search_pcm_batch(hq[i % len(hq)], [0, qn], p_lo if i % 2 == 0 else p_hi)
         first.append((time.perf_counter() - t0) * 1e3)
     c2, w2 = eng.index_cache_stats(), eng.sweep_stats()
+    b2 = eng.index_build_stats()
     for u in uuids:
         eng.index_remove(u)
     eng.index_commit()
@@ -848,7 +852,10 @@ def coefs2_cache(args, eng, T, hq, qn, n_calls=100, n_add=8):
                            "p99_ms": float(np.percentile(first, 99)), "max_ms": float(np.max(first)), "samples_ms": first,
                            "cache_builds_from_order": c2["from_order"] - c1["from_order"],
                            "order_merges": c2["order_merges"] - c1["order_merges"],
-                           "order_full_builds": c2["order_builds"] - c1["order_builds"]},
+                           "order_full_builds": c2["order_builds"] - c1["order_builds"],
+                           "index_merges": b2[1] - b1[1], "index_full_builds": b2[0] - b1[0],
+                           "delta_cache_builds": c2["delta_builds"] - c1["delta_builds"],
+                           "delta_sweeps": c2["delta_sweeps"] - c1["delta_sweeps"]},
            "sweep_paths": {k: w2[k] - w0[k] for k in w2},
            "harness": "python (ctypes) loop over tfp_search_pcm_batch"}
     log(f"coefs=2 cache: alternation p50 {out['alternation']['p50_ms']:.3f} p99 {out['alternation']['p99_ms']:.3f} ms; "

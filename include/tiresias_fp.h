@@ -188,16 +188,18 @@ int tfp_index_build_stats(tfp_engine* eng, int64_t* full_builds, int64_t* merges
 /* Index delta (new in round 4): up to 512 clips enrolled since the last merge are searched beside
  * the sorted index by the coefs = 1 paths (the dialplan's, application_handler.c:180) without a
  * merge: an enrolment then costs its own rows, as the reference's INSERT into its B-tree does
- * (fp_handler.c:559-571, :745-753). The delta is merged when it outgrows that, when a clip of the
- * sorted index is removed, or before a search that reads the sorted rows (coefs = 2, a tolerance
- * above 8, a row-scan fallback); results are unchanged either way. TFP_INDEX_DELTA=0 at engine
+ * (fp_handler.c:559-571, :745-753). coefs = 2 searches (round 6) sweep the delta's own clip-set cache
+ * beside the main one. The delta is merged when it outgrows that, when a clip of the sorted index is
+ * removed, or before a search that reads the sorted rows (a coefs = 1 tolerance above 8, a coefs = 2
+ * tolerance above 0.49, a row-scan fallback); results are unchanged either way. TFP_INDEX_DELTA=0 at engine
  * creation turns it off. Stats: delta updates so far and the clips in the delta now. */
 int tfp_index_delta_stats(tfp_engine* eng, int64_t* delta_updates, int32_t* delta_clips);
 /* The coefs = 2 clip-set caches (new in round 6): builds so far, searches served by a cached
  * tolerance (the active one or one of three others kept, least recently used out), builds made from
- * the clip order (tolerances up to 0.49: a filter, no sort), and the clip order's full builds (one
+ * the clip order (tolerances up to 0.49: a filter, no sort), the clip order's full builds (one
  * radix sort per full index build, when first needed) and merges (carried through every index
- * merge). Any pointer may be NULL. */
+ * merge), and the index delta's caches built and sweeps run over them (an enrolment followed by a
+ * coefs = 2 search: the main caches stay, the delta's rows get their own). Any pointer may be NULL. */
 /* The coefs = 2 sweep's frame sort per batch (new in round 6): batches whose hand-written bin sort
  * stood, batches sorted by the library sort (a first pass that could not take the bin sort, or the
  * redo), speculative passes redone (an overfull bin, a window width outside the packed key, a frame
@@ -205,7 +207,8 @@ int tfp_index_delta_stats(tfp_engine* eng, int64_t* delta_updates, int32_t* delt
  * Any pointer may be NULL. */
 int tfp_sweep_stats(tfp_engine* eng, int64_t* bins, int64_t* library, int64_t* redone, int64_t* crowd_bins);
 int tfp_index_cache_stats(tfp_engine* eng, int64_t* cache_builds, int64_t* cache_hits, int64_t* from_order,
-                          int64_t* order_builds, int64_t* order_merges);
+                          int64_t* order_builds, int64_t* order_merges, int64_t* delta_cache_builds,
+                          int64_t* delta_sweeps);
 /* Multi-GPU sharding: override the tie-break key of each live clip (default: its rank among
  * this engine's uuids). keys[clip_id] must order like the uuids across all shards and be
  * distinct over live clips. A clip added after this call has no key: the next search (or
