@@ -2046,18 +2046,40 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
   }
   for (int32_t w = w0; w < w1; w++) {
     const int32_t c0 = kWin * w;
-#pragma unroll
-    for (int j = 0; j < kWin; j++) acc[j * 64 + lane] = 0u;
-    auto add = [&](int32_t col, uint32_t cnt) { acc[(col - c0) * 64 + lane] += cnt; };
-    for (int32_t u0 = 0; u0 < nu; u0 += 64) {
-      // the used keys with groups in this window, 64 keys a step
-      int32_t kk = 0, ga = 0, gb = 0;
-      if (u0 + lane < nu) {
-        kk = uk[u0 + lane];
-        ga = kdir[(int64_t)kk * (nwin + 1) + w];
-        gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
+    // the used keys with groups in this window, 64 keys a step; a window in which none of them
+    // has a group (up to 64 used keys: the first step's ballot) scores nothing, so its counts are
+    // neither cleared nor read
+    int32_t kk = 0, ga = 0, gb = 0;
+    if (lane < nu) {
+      kk = uk[lane];
+      ga = kdir[(int64_t)kk * (nwin + 1) + w];
+      gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
+    }
+    unsigned long long km = __ballot(gb > ga);
+    if (kpre && !km) continue;
+    // the window's columns that got a count (wave-uniform): each column's row is written by its
+    // first add and read only if written, so nothing is cleared and untouched columns cost nothing
+    uint32_t touched = 0;
+    auto add = [&](int32_t col, uint32_t cnt) {
+      const int32_t j = __builtin_amdgcn_readfirstlane(col - c0);
+      uint32_t* a = acc + j * 64 + lane;
+      if ((touched >> j) & 1u) {
+        *a += cnt;
+      } else {
+        *a = cnt;
+        touched |= 1u << j;
       }
-      unsigned long long km = __ballot(gb > ga);
+    };
+    for (int32_t u0 = 0; u0 < nu; u0 += 64) {
+      if (u0 > 0) {
+        kk = ga = gb = 0;
+        if (u0 + lane < nu) {
+          kk = uk[u0 + lane];
+          ga = kdir[(int64_t)kk * (nwin + 1) + w];
+          gb = kdir[(int64_t)kk * (nwin + 1) + w + 1];
+        }
+        km = __ballot(gb > ga);
+      }
       while (km) {
         const int sl = __ffsll((long long)km) - 1;
         km &= km - 1;
@@ -2190,9 +2212,10 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
       }
     }
     // the window's clips: each query's best (count << 32 | tie key)
+    if (!touched) continue;
     const int32_t tk = col_base + c0 + lane < C && lane < kWin ? tiekey[col_base + c0 + lane] : 0;
-#pragma unroll
-    for (int j = 0; j < kWin; j++) {
+    for (uint32_t tm = touched; tm; tm &= tm - 1) {
+      const int j = __builtin_ctz(tm);
       const uint32_t v = acc[j * 64 + lane];
       const unsigned long long t = (uint32_t)__builtin_amdgcn_readlane(tk, j);
 #pragma unroll
