@@ -1974,6 +1974,13 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001;
 // 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 constexpr int kClipOcc = 8;
+#ifndef TFP_CLIP_LAZY
+#define TFP_CLIP_LAZY 1  // count rows written on a column's first add (A/B: 0 clears all 16 per window)
+#endif
+#ifndef TFP_LAZY_GROUPS
+#define TFP_LAZY_GROUPS 8
+#endif
+constexpr int32_t kLazyGroups = TFP_LAZY_GROUPS;  // a window with this many groups clears its 16 rows
 template <int QPL>
 __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
@@ -2057,9 +2064,20 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
     unsigned long long km = __ballot(gb > ga);
     if (kpre && !km) continue;
-    // the window's columns that got a count (wave-uniform): each column's row is written by its
-    // first add and read only if written, so nothing is cleared and untouched columns cost nothing
+#if TFP_CLIP_LAZY
+    // the window's columns that got a count (wave-uniform): in a window with few groups (up to 64
+    // used keys: the first step's), each column's row is written by its first add and read only if
+    // written, so nothing is cleared and untouched columns cost nothing; a window with more groups
+    // clears all 16 rows and takes every column
+    int32_t ngr = gb - ga;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ngr += __shfl_xor(ngr, o, 64);
     uint32_t touched = 0;
+    if (!kpre || ngr >= kLazyGroups) {
+#pragma unroll
+      for (int j = 0; j < kWin; j++) acc[j * 64 + lane] = 0u;
+      touched = (1u << kWin) - 1;
+    }
     auto add = [&](int32_t col, uint32_t cnt) {
       const int32_t j = __builtin_amdgcn_readfirstlane(col - c0);
       uint32_t* a = acc + j * 64 + lane;
@@ -2070,6 +2088,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
         touched |= 1u << j;
       }
     };
+#else
+    constexpr uint32_t touched = (1u << kWin) - 1;
+#pragma unroll
+    for (int j = 0; j < kWin; j++) acc[j * 64 + lane] = 0u;
+    auto add = [&](int32_t col, uint32_t cnt) { acc[(col - c0) * 64 + lane] += cnt; };
+#endif
     for (int32_t u0 = 0; u0 < nu; u0 += 64) {
       if (u0 > 0) {
         kk = ga = gb = 0;
@@ -2212,10 +2236,9 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
       }
     }
     // the window's clips: each query's best (count << 32 | tie key)
-    if (!touched) continue;
+    if (!touched) continue;  // (TFP_CLIP_LAZY)
     const int32_t tk = col_base + c0 + lane < C && lane < kWin ? tiekey[col_base + c0 + lane] : 0;
-    for (uint32_t tm = touched; tm; tm &= tm - 1) {
-      const int j = __builtin_ctz(tm);
+    auto take = [&](int j) {
       const uint32_t v = acc[j * 64 + lane];
       const unsigned long long t = (uint32_t)__builtin_amdgcn_readlane(tk, j);
 #pragma unroll
@@ -2224,6 +2247,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
         const unsigned long long k = ((unsigned long long)c << 32) | t;
         if (c) r[b] = k > r[b] ? k : r[b];
       }
+    };
+    if (touched == (1u << kWin) - 1) {  // (all 16 rows read at once)
+#pragma unroll
+      for (int j = 0; j < kWin; j++) take(j);
+    } else {
+      for (uint32_t tm = touched; tm; tm &= tm - 1) take(__builtin_ctz(tm));
     }
   }
   // the workgroup's maxima (its waves share the chunk: xw is a multiple of kClipWaves), through
