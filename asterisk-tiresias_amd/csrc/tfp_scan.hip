@@ -234,37 +234,69 @@ __global__ void delta_order_fill_kernel(const DeltaClip* __restrict__ dc, const 
   }
 }
 
-// Is order row i a point at this tolerance (its m1 inside its key's "%f" box)?
-__device__ __forceinline__ bool order_point(unsigned long long key, int32_t m1, const int64_t* __restrict__ kbox) {
-  const uint32_t t = (uint32_t)(key >> 53);
+// Is an order row with max1 m1 a point at this tolerance (m1 inside the "%f" box of its key index,
+// which is order_key_index(m1) by construction: the key itself is not needed)?
+__device__ __forceinline__ bool order_point(int32_t m1, const int64_t* __restrict__ kbox) {
+  const uint32_t t = order_key_index(m1);
   return (int64_t)m1 >= kbox[2 * t] && (int64_t)m1 <= kbox[2 * t + 1];
 }
 
-// In-tile exclusive prefix of the flags bits (bit k: item k * 256 + t) into pre[], via ballots and
-// 64 partial sums in csum (LDS, [kOPer][4]). Every thread of the tile calls it.
-__device__ __forceinline__ void tile_prefix(uint32_t bits, int32_t (&pre)[kOPer], int32_t (*csum)[kOT / 64]) {
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  uint32_t lo[kOPer];
+// Block-wide exclusive prefix of one count per thread (kOT threads, thread order); *tot = the
+// block's total. wsum: kOT / 64 words of LDS. Every thread of the block calls it.
+__device__ __forceinline__ int32_t block_prefix(int32_t x, int32_t* wsum, int32_t* tot) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int32_t inc = x;
 #pragma unroll
-  for (int k = 0; k < kOPer; k++) {
-    const uint64_t m = __ballot((bits >> k) & 1u);
-    lo[k] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    if (lane == 0) csum[k][wv] = __popcll(m);
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += y;
   }
+  if (lane == 63) wsum[wv] = inc;
   __syncthreads();
-  if (t == 0) {
-    int32_t run = 0;
-    for (int k = 0; k < kOPer; k++)
-      for (int w = 0; w < kOT / 64; w++) {
-        const int32_t v = csum[k][w];
-        csum[k][w] = run;
-        run += v;
-      }
-  }
-  __syncthreads();
+  int32_t base = 0, all = 0;
 #pragma unroll
-  for (int k = 0; k < kOPer; k++) pre[k] = csum[k][wv] + (int32_t)lo[k];
-  __syncthreads();  // (csum is reused by the caller's next call)
+  for (int w = 0; w < kOT / 64; w++) {
+    const int32_t v = wsum[w];
+    base += w < wv ? v : 0;
+    all += v;
+  }
+  *tot = all;
+  return base + inc - x;
+}
+
+// Which of a thread's kOPer consecutive order rows (rows r0 = b0 + kOPer t ..: 16-byte loads of
+// their max1 only; the last tile's rows past n are not points) are points at this tolerance.
+__device__ __forceinline__ uint32_t order_rows(const int32_t* __restrict__ om1, int64_t n, const int64_t* __restrict__ kbox,
+                                               int64_t r0) {
+  int32_t m1[kOPer];
+  if (r0 + kOPer <= n) {
+    const int4* m4 = reinterpret_cast<const int4*>(om1 + r0);
+#pragma unroll
+    for (int q = 0; q < kOPer / 4; q++) {
+      const int4 v = m4[q];
+      m1[4 * q] = v.x;
+      m1[4 * q + 1] = v.y;
+      m1[4 * q + 2] = v.z;
+      m1[4 * q + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOPer; k++) m1[k] = r0 + k < n ? om1[r0 + k] : 0;
+  }
+  uint32_t bits = 0;
+  // the rows are in key order: when the thread's first and last row share a key index (nearly
+  // always), one box for all of them
+  const uint32_t t0 = order_key_index(m1[0]);
+  if (r0 + kOPer <= n && order_key_index(m1[kOPer - 1]) == t0) {
+    const int64_t lo = kbox[2 * t0], hi = kbox[2 * t0 + 1];
+#pragma unroll
+    for (int k = 0; k < kOPer; k++) bits |= (uint32_t)((int64_t)m1[k] >= lo && (int64_t)m1[k] <= hi) << k;
+    return bits;
+  }
+#pragma unroll
+  for (int k = 0; k < kOPer; k++)
+    if (r0 + k < n && order_point(m1[k], kbox)) bits |= 1u << k;
+  return bits;
 }
 
 // Points per tile of the order (the tile's count into cnt[tile]).
@@ -272,34 +304,34 @@ __global__ __launch_bounds__(kOT) void order_count_kernel(const unsigned long lo
                                                           const int32_t* __restrict__ om1, int64_t n,
                                                           const int64_t* __restrict__ kbox, int32_t* __restrict__ cnt) {
   __shared__ int32_t wsum[kOT / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
-  int32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < kOPer; k++) {
-    const int64_t i = b0 + k * kOT + threadIdx.x;
-    if (i < n) c += order_point(okey[i], om1[i], kbox);
-  }
-  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t t = 0;
-    for (int w = 0; w < kOT / 64; w++) t += wsum[w];
-    cnt[blockIdx.x] = t;
-  }
+  const uint32_t bits = order_rows(om1, n, kbox, (int64_t)blockIdx.x * kOTile + kOPer * threadIdx.x);
+  int32_t tot;
+  (void)block_prefix(__popc(bits), wsum, &tot);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = tot;
 }
 
 // Exclusive scan, in place, of nvec vectors of ntiles counts each (vector v at cnt + v (ntiles + 1));
-// each vector's total lands in its element ntiles. One workgroup of 1024 threads.
+// each vector's total lands in its element ntiles. One workgroup of 1024 threads: a vector of up to
+// kScanLds counts goes through LDS (coalesced loads and stores; each thread then scans its
+// contiguous share there), a longer one is scanned in place.
+constexpr int32_t kScanLds = 30720;
 __global__ __launch_bounds__(1024) void tile_scan_kernel(int32_t* __restrict__ cnt, int32_t ntiles, int32_t nvec) {
   __shared__ int32_t part[1024];
+  __shared__ int32_t buf[kScanLds];
   const int t = threadIdx.x;
   const int32_t per = (ntiles + 1023) / 1024;
+  const bool inlds = ntiles <= kScanLds;
   for (int32_t v = 0; v < nvec; v++) {
     int32_t* c = cnt + (int64_t)v * (ntiles + 1);
     const int32_t a = t * per, e = min(ntiles, a + per);
     int32_t sum = 0;
-    for (int32_t i = a; i < e; i++) sum += c[i];
+    if (inlds) {
+      for (int32_t i = t; i < ntiles; i += 1024) buf[i] = c[i];
+      __syncthreads();
+      for (int32_t i = a; i < e; i++) sum += buf[i];
+    } else {
+      for (int32_t i = a; i < e; i++) sum += c[i];
+    }
     part[t] = sum;
     __syncthreads();
     for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the partial sums
@@ -309,10 +341,20 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(int32_t* __restrict__ c
       __syncthreads();
     }
     int32_t run = part[t] - sum;
-    for (int32_t i = a; i < e; i++) {
-      const int32_t x = c[i];
-      c[i] = run;
-      run += x;
+    if (inlds) {
+      for (int32_t i = a; i < e; i++) {
+        const int32_t x = buf[i];
+        buf[i] = run;
+        run += x;
+      }
+      __syncthreads();
+      for (int32_t i = t; i < ntiles; i += 1024) c[i] = buf[i];
+    } else {
+      for (int32_t i = a; i < e; i++) {
+        const int32_t x = c[i];
+        c[i] = run;
+        run += x;
+      }
     }
     if (t == 1023) c[ntiles] = part[1023];
     __syncthreads();
@@ -320,73 +362,122 @@ __global__ __launch_bounds__(1024) void tile_scan_kernel(int32_t* __restrict__ c
 }
 
 // The points: every order row inside its key's box, in order (p_m2 = its m2, k32 = key << 21 | col).
+// kStage (dense points: most rows of a tile): the tile's points staged in LDS and written as one
+// contiguous run; sparse points are written where they fall (the 32 KB of staging would cost the
+// launch occupancy for nothing).
+template <bool kStage>
 __global__ __launch_bounds__(kOT) void order_points_kernel(const unsigned long long* __restrict__ okey,
                                                            const int32_t* __restrict__ om1, int64_t n,
                                                            const int64_t* __restrict__ kbox, const int32_t* __restrict__ off,
                                                            int32_t* __restrict__ p_m2, uint32_t* __restrict__ k32) {
-  __shared__ int32_t csum[kOPer][kOT / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
+  __shared__ int32_t wsum[kOT / 64];
+  __shared__ int32_t sv[kStage ? kOTile : 1];
+  __shared__ uint32_t sk[kStage ? kOTile : 1];
+  const int64_t r0 = (int64_t)blockIdx.x * kOTile + kOPer * threadIdx.x;
+  const uint32_t bits = order_rows(om1, n, kbox, r0);
+  int32_t tot;
+  int32_t j = block_prefix(__popc(bits), wsum, &tot);
+  // the points' keys: all of the thread's rows in 16-byte loads when most are points, else one by one
   unsigned long long key[kOPer];
-  uint32_t bits = 0;
+  if (__popc(bits) > kOPer / 4 && r0 + kOPer <= n) {
+    const ulonglong2* k2 = reinterpret_cast<const ulonglong2*>(okey + r0);
 #pragma unroll
-  for (int k = 0; k < kOPer; k++) {
-    const int64_t i = b0 + k * kOT + threadIdx.x;
-    key[k] = i < n ? okey[i] : 0ull;
-    if (i < n && order_point(key[k], om1[i], kbox)) bits |= 1u << k;
+    for (int q = 0; q < kOPer / 2; q++) {
+      const ulonglong2 v = k2[q];
+      key[2 * q] = v.x;
+      key[2 * q + 1] = v.y;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOPer; k++) key[k] = (bits >> k) & 1u ? okey[r0 + k] : 0ull;
   }
-  int32_t pre[kOPer];
-  tile_prefix(bits, pre, csum);
-  const int32_t base = off[blockIdx.x];
+  const int64_t o = off[blockIdx.x];
+  if constexpr (!kStage) {
+#pragma unroll
+    for (int k = 0; k < kOPer; k++)
+      if ((bits >> k) & 1u) {
+        p_m2[o + j] = (int32_t)((uint32_t)key[k] ^ 0x80000000u);
+        k32[o + j] = (uint32_t)(key[k] >> 32);  // key << 21 | column
+        j++;
+      }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < kOPer; k++)
     if ((bits >> k) & 1u) {
-      const int32_t j = base + pre[k];
-      p_m2[j] = (int32_t)((uint32_t)key[k] ^ 0x80000000u);
-      k32[j] = (uint32_t)(key[k] >> 32);  // key << 21 | column
+      sv[j] = (int32_t)((uint32_t)key[k] ^ 0x80000000u);
+      sk[j] = (uint32_t)(key[k] >> 32);
+      j++;
     }
+  __syncthreads();
+  for (int32_t i = threadIdx.x; i < tot; i += kOT) {
+    p_m2[o + i] = sv[i];
+    k32[o + i] = sk[i];
+  }
 }
 
-// Point j starts a group when its (key, column) differs from point j - 1's, a cluster when it starts a
-// group or lies more than dgap above its predecessor.
-__device__ __forceinline__ void point_starts(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32, int64_t j,
-                                             int64_t dgap, bool& gs, bool& cs) {
-  gs = j == 0 || k32[j] != k32[j - 1];
-  cs = gs || (int64_t)p_m2[j] - (int64_t)p_m2[j - 1] > dgap;
+// A thread's kOPer consecutive points j0 .. (16-byte loads) with their neighbours j0 - 1 and
+// j0 + kOPer: point j starts a group when its (key, column) differs from point j - 1's, a cluster
+// when it starts a group or lies more than dgap above its predecessor; it ends a cluster when
+// point j + 1 starts one or j is the last point. Bits of the points below S.
+__device__ __forceinline__ void point_flags(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32, int64_t S,
+                                            int64_t dgap, int64_t j0, int32_t (&v)[kOPer], uint32_t& gbits,
+                                            uint32_t& cbits, uint32_t& ebits) {
+  uint32_t kk[kOPer + 2];  // points j0 - 1 .. j0 + kOPer
+  int32_t vv[kOPer + 2];
+  if (j0 + kOPer <= S) {
+    const int4* v4 = reinterpret_cast<const int4*>(p_m2 + j0);
+    const uint4* k4 = reinterpret_cast<const uint4*>(k32 + j0);
+#pragma unroll
+    for (int q = 0; q < kOPer / 4; q++) {
+      const int4 a = v4[q];
+      const uint4 b = k4[q];
+      vv[1 + 4 * q] = a.x, vv[2 + 4 * q] = a.y, vv[3 + 4 * q] = a.z, vv[4 + 4 * q] = a.w;
+      kk[1 + 4 * q] = b.x, kk[2 + 4 * q] = b.y, kk[3 + 4 * q] = b.z, kk[4 + 4 * q] = b.w;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kOPer; k++) {
+      vv[1 + k] = j0 + k < S ? p_m2[j0 + k] : 0;
+      kk[1 + k] = j0 + k < S ? k32[j0 + k] : 0u;
+    }
+  }
+  const bool prev = j0 > 0 && j0 - 1 < S;  // (threads past the last point read nothing)
+  vv[0] = prev ? p_m2[j0 - 1] : 0;
+  kk[0] = prev ? k32[j0 - 1] : ~0u;  // (point 0 starts a group: no key equals ~0)
+  vv[kOPer + 1] = j0 + kOPer < S ? p_m2[j0 + kOPer] : 0;
+  kk[kOPer + 1] = j0 + kOPer < S ? k32[j0 + kOPer] : 0u;
+  gbits = cbits = ebits = 0;
+  bool cs_next = false;
+#pragma unroll
+  for (int k = kOPer; k >= 0; k--) {  // k: point j0 + k - 1 (k = kOPer: the neighbour j0 + kOPer)
+    const int64_t j = j0 + k;        // (the point whose flags this step forms: j0 + k)
+    const bool in = j < S;
+    const bool gs = in && kk[k + 1] != kk[k];
+    const bool cs = in && (gs || (int64_t)vv[k + 1] - (int64_t)vv[k] > dgap);
+    if (k < kOPer && in) {
+      gbits |= (uint32_t)gs << k;
+      cbits |= (uint32_t)cs << k;
+      ebits |= (uint32_t)(cs_next || j == S - 1) << k;
+    }
+    cs_next = cs;
+  }
+#pragma unroll
+  for (int k = 0; k < kOPer; k++) v[k] = vv[1 + k];
 }
 
 __global__ __launch_bounds__(kOT) void point_count_kernel(const int32_t* __restrict__ p_m2, const uint32_t* __restrict__ k32,
                                                           int64_t S, int64_t dgap, int32_t ntiles,
                                                           int32_t* __restrict__ cnt) {
-  __shared__ int32_t wsum[2][kOT / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
-  int32_t g = 0, c = 0;
-#pragma unroll 4
-  for (int k = 0; k < kOPer; k++) {
-    const int64_t j = b0 + k * kOT + threadIdx.x;
-    if (j < S) {
-      bool gs, cs;
-      point_starts(p_m2, k32, j, dgap, gs, cs);
-      g += gs;
-      c += cs;
-    }
-  }
-  for (int o = 32; o > 0; o >>= 1) {
-    g += __shfl_xor(g, o, 64);
-    c += __shfl_xor(c, o, 64);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    wsum[0][threadIdx.x >> 6] = g;
-    wsum[1][threadIdx.x >> 6] = c;
-  }
-  __syncthreads();
+  __shared__ int32_t wsum[kOT / 64];
+  int32_t v[kOPer];
+  uint32_t gbits, cbits, ebits;
+  point_flags(p_m2, k32, S, dgap, (int64_t)blockIdx.x * kOTile + kOPer * threadIdx.x, v, gbits, cbits, ebits);
+  int32_t tot;  // groups << 16 | clusters (each at most kOTile per tile)
+  (void)block_prefix((__popc(gbits) << 16) | __popc(cbits), wsum, &tot);
   if (threadIdx.x == 0) {
-    int32_t tg = 0, tc = 0;
-    for (int w = 0; w < kOT / 64; w++) {
-      tg += wsum[0][w];
-      tc += wsum[1][w];
-    }
-    cnt[blockIdx.x] = tg;
-    cnt[ntiles + 1 + blockIdx.x] = tc;
+    cnt[blockIdx.x] = tot >> 16;
+    cnt[ntiles + 1 + blockIdx.x] = tot & 0xffff;
   }
 }
 
@@ -397,45 +488,30 @@ __global__ __launch_bounds__(kOT) void point_groups_kernel(const int32_t* __rest
                                                            const int32_t* __restrict__ off, uint32_t* __restrict__ g_key,
                                                            int32_t* __restrict__ g_beg, int32_t* __restrict__ c_beg,
                                                            int32_t* __restrict__ c_lo, int32_t* __restrict__ c_hi) {
-  __shared__ int32_t csum[kOPer][kOT / 64];
-  const int64_t b0 = (int64_t)blockIdx.x * kOTile;
-  uint32_t gbits = 0, cbits = 0;
-#pragma unroll
-  for (int k = 0; k < kOPer; k++) {
-    const int64_t j = b0 + k * kOT + threadIdx.x;
-    if (j < S) {
-      bool gs, cs;
-      point_starts(p_m2, k32, j, dgap, gs, cs);
-      gbits |= (uint32_t)gs << k;
-      cbits |= (uint32_t)cs << k;
-    }
-  }
-  int32_t gpre[kOPer], cpre[kOPer];
-  tile_prefix(gbits, gpre, csum);
-  tile_prefix(cbits, cpre, csum);
-  const int32_t gb = off[blockIdx.x], cb = off[ntiles + 1 + blockIdx.x];
+  __shared__ int32_t wsum[kOT / 64];
+  const int64_t j0 = (int64_t)blockIdx.x * kOTile + kOPer * threadIdx.x;
+  int32_t v[kOPer];
+  uint32_t gbits, cbits, ebits;
+  point_flags(p_m2, k32, S, dgap, j0, v, gbits, cbits, ebits);
+  int32_t tot;
+  const int32_t pre = block_prefix((__popc(gbits) << 16) | __popc(cbits), wsum, &tot);
+  int32_t g = off[blockIdx.x] + (pre >> 16);                 // this thread's first group start
+  int32_t c = off[ntiles + 1 + blockIdx.x] + (pre & 0xffff) - 1;  // the cluster of the point before j0
   const int32_t n1 = off[ntiles], nc = off[2 * (ntiles + 1) - 1];
 #pragma unroll
   for (int k = 0; k < kOPer; k++) {
-    const int64_t j = b0 + k * kOT + threadIdx.x;
-    if (j >= S) continue;
-    const bool gs = (gbits >> k) & 1u, cs = (cbits >> k) & 1u;
-    const int32_t c = cb + cpre[k] + (int32_t)cs - 1;  // this point's cluster
-    const int32_t v = p_m2[j];
-    if (gs) {
-      const int32_t g = gb + gpre[k];
+    const int64_t j = j0 + k;
+    if ((cbits >> k) & 1u) {
+      c++;
+      c_lo[c] = v[k];
+    }
+    if ((gbits >> k) & 1u) {
       g_key[g] = k32[j];
       g_beg[g] = (int32_t)j;
       c_beg[g] = c;
+      g++;
     }
-    if (cs) c_lo[c] = v;
-    bool end = j == S - 1;
-    if (!end) {
-      bool gs1, cs1;
-      point_starts(p_m2, k32, j + 1, dgap, gs1, cs1);
-      end = cs1;
-    }
-    if (end) c_hi[c] = v;
+    if ((ebits >> k) & 1u) c_hi[c] = v[k];
     if (j == S - 1) {
       g_beg[n1] = (int32_t)S;
       c_beg[n1] = nc;
@@ -581,7 +657,10 @@ hipError_t CellCache::build_from_order(const unsigned long long* okey, const int
   if ((e = b_p_m2.reserve(sizeof(int32_t) * (size_t)S)) != hipSuccess || (e = b_k32.reserve(sizeof(uint32_t) * (size_t)S)) != hipSuccess)
     return e;
   bind();
-  hipLaunchKernelGGL(order_points_kernel, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt, p_m2, k32);
+  if (4 * S > n)  // (dense: most rows are points)
+    hipLaunchKernelGGL(order_points_kernel<true>, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt, p_m2, k32);
+  else
+    hipLaunchKernelGGL(order_points_kernel<false>, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt, p_m2, k32);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // 2. groups and clusters: two counts per tile, their offsets, then the arrays
   const int32_t nt2 = (int32_t)((S + kOTile - 1) / kOTile);
@@ -1977,10 +2056,6 @@ constexpr int kClipOcc = 8;
 #ifndef TFP_CLIP_LAZY
 #define TFP_CLIP_LAZY 1  // count rows written on a column's first add (A/B: 0 clears all 16 per window)
 #endif
-#ifndef TFP_LAZY_GROUPS
-#define TFP_LAZY_GROUPS 8
-#endif
-constexpr int32_t kLazyGroups = TFP_LAZY_GROUPS;  // a window with this many groups clears its 16 rows
 template <int QPL>
 __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     int32_t xw, const int32_t* __restrict__ seg, const int32_t* __restrict__ cbeg, CellView cv,
@@ -2065,19 +2140,11 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     unsigned long long km = __ballot(gb > ga);
     if (kpre && !km) continue;
 #if TFP_CLIP_LAZY
-    // the window's columns that got a count (wave-uniform): in a window with few groups (up to 64
-    // used keys: the first step's), each column's row is written by its first add and read only if
-    // written, so nothing is cleared and untouched columns cost nothing; a window with more groups
-    // clears all 16 rows and takes every column
-    int32_t ngr = gb - ga;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ngr += __shfl_xor(ngr, o, 64);
+    // the window's columns that got a count (wave-uniform): each column's row is written by its
+    // first add and read only if written, so nothing is cleared and untouched columns cost nothing
+    // (at C3 -3 % per coefs = 2 batch at tol 0.001 / 0.01, even at 0.1 / 0.45; clearing the rows
+    // of windows with many groups did not pay: profiles/r06/c3_window_ab_r06.txt)
     uint32_t touched = 0;
-    if (!kpre || ngr >= kLazyGroups) {
-#pragma unroll
-      for (int j = 0; j < kWin; j++) acc[j * 64 + lane] = 0u;
-      touched = (1u << kWin) - 1;
-    }
     auto add = [&](int32_t col, uint32_t cnt) {
       const int32_t j = __builtin_amdgcn_readfirstlane(col - c0);
       uint32_t* a = acc + j * 64 + lane;

@@ -61,9 +61,11 @@ out = {
     "algorithmic_bytes_per_launch": alg,
     "traffic_over_algorithmic": hbm / alg,
     "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes (scripts/profile_round.sh); "
-              "FETCH_SIZE x2 per MI355X_MICROARCH.md HBM section (gfx950 reports half the bytes of 16-B/lane "
-              "streaming reads; the PCM is read with global_load_dwordx4); WRITE_SIZE as reported "
-              "(uncalibrated for 4-B scattered stores)",
+              "FETCH_SIZE x2: MI355X_MICROARCH.md's HBM section gives the factor for 16-B/lane streaming reads, "
+              "and the kernel's 4-B buffer-load pattern was calibrated on the box in round 5 against a 512 MiB "
+              "buffer read once (scripts/microbench/fetch_calib.hip: 262.3 MB reported for the dword pattern, "
+              "256.0 MB for a 16-B stream: the same factor 2); WRITE_SIZE as reported (uncalibrated for 4-B "
+              "scattered stores)",
     "round": ROUND,
     "kernel_build": note,
 }
