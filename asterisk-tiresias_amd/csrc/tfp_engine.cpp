@@ -294,8 +294,11 @@ struct tfp_engine {
   int32_t key_bits_cols = -1;       // the column count key_bits was laid out for (its row width)
   Coalescer coal;          // concurrent small host-sample searches share one batch (tfp_coalesce.hpp)
   bool coalesce = true;    // TFP_COALESCE=0: every call runs alone (A/B)
+  hipEvent_t null_in = nullptr, null_out = nullptr;  // (NullStreamOrder)
   ~tfp_engine() {
     if (qoff_ev) (void)hipEventDestroy(qoff_ev);
+    if (null_in) (void)hipEventDestroy(null_in);
+    if (null_out) (void)hipEventDestroy(null_out);
   }
 };
 
@@ -319,6 +322,31 @@ int fail(tfp_engine* e, int code, const char* fmt, ...) {
       return fail((e), _st == hipErrorOutOfMemory ? TFP_E_NOMEM : TFP_E_HIP, "%s: %s", #expr,   \
                   hipGetErrorString(_st));                                                       \
   } while (0)
+
+// A device-form call given no stream (NULL) runs on the engine's own stream, ordered after the work
+// queued on the HIP null stream before the call and before the null stream's later work: the
+// null stream is the default stream of torch and of CUDA-style callers, and the engine's stream
+// is non-blocking, so without this a caller's default-stream producers and consumers (a torch
+// copy, a gloo all_gather of the frame values) could race the engine's kernels. Two event
+// records and two stream waits, no host wait.
+class NullStreamOrder {
+ public:
+  NullStreamOrder(tfp_engine* e, void* stream) : e_(e), on_(stream == nullptr) {
+    if (!on_) return;
+    if (!e_->null_in && hipEventCreateWithFlags(&e_->null_in, hipEventDisableTiming) != hipSuccess) e_->null_in = nullptr;
+    if (!e_->null_out && hipEventCreateWithFlags(&e_->null_out, hipEventDisableTiming) != hipSuccess) e_->null_out = nullptr;
+    ok_ = e_->null_in && e_->null_out && hipEventRecord(e_->null_in, nullptr) == hipSuccess &&
+          hipStreamWaitEvent(e_->stream, e_->null_in, 0) == hipSuccess;
+  }
+  bool ok() const { return !on_ || ok_; }
+  ~NullStreamOrder() {
+    if (on_ && ok_ && hipEventRecord(e_->null_out, e_->stream) == hipSuccess) (void)hipStreamWaitEvent(nullptr, e_->null_out, 0);
+  }
+
+ private:
+  tfp_engine* e_;
+  bool on_, ok_ = false;
+};
 
 // The device copy of the glibc log correction table (frame values == glibc's 10*log10|c|).
 int ensure_logfix(tfp_engine* e) {
@@ -1903,6 +1931,9 @@ int tfp_fingerprint_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pc
                            void* stream) {
   if (!e || !p || !d_micro || (!d_pcm && p->nsamples)) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
+  HIPCHK(e, hipSetDevice(e->device));
+  NullStreamOrder order(e, stream);
+  if (!order.ok()) return fail(e, TFP_E_HIP, "ordering after the null stream failed");
   const DspTables* T;
   bool fx = false;
   int rc = ensure_tables(e, p->sample_rate, &T, &fx);
@@ -1962,6 +1993,8 @@ int tfp_index_add_device(tfp_engine* e, int32_t nclips, const char* const* uuids
     return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
+  NullStreamOrder order(e, stream);
+  if (!order.ok()) return fail(e, TFP_E_HIP, "ordering after the null stream failed");
   std::unordered_map<std::string, int> seen;
   for (int32_t c = 0; c < nclips; c++) {
     if (!uuids[c] || !*uuids[c] || strlen(uuids[c]) >= 64) return fail(e, TFP_E_ARG, "bad uuid %d", c);
@@ -2333,6 +2366,8 @@ int tfp_search_device(tfp_engine* e, const tfp_plan* p, const int16_t* d_pcm, co
   if (!e || !p || !d_keys || !valid_params(P)) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
+  NullStreamOrder order(e, stream);
+  if (!order.ok()) return fail(e, TFP_E_HIP, "ordering after the null stream failed");
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   const DspTables* T;
   bool fx = false;
@@ -2356,6 +2391,8 @@ int tfp_search_q_device(tfp_engine* e, const double* d_q, const int64_t* qoff, i
     if (qoff[i + 1] < qoff[i]) return fail(e, TFP_E_ARG, "query offsets not monotone");
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
+  NullStreamOrder order(e, stream);
+  if (!order.ok()) return fail(e, TFP_E_HIP, "ordering after the null stream failed");
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   std::vector<unsigned long long> keys;
   return search_core(e, qoff, nq, d_q ? d_q + 2 * qoff[0] : d_q, P, keys, reinterpret_cast<unsigned long long*>(d_keys),
@@ -2566,6 +2603,8 @@ int tfp_synth_pcm_device(tfp_engine* e, const tfp_synth_spec* specs, int32_t ncl
   if (!e || nclips < 0 || spc < 0 || (nclips && (!specs || !d_out))) return TFP_E_ARG;
   std::lock_guard<std::recursive_mutex> lk(e->mu);
   HIPCHK(e, hipSetDevice(e->device));
+  NullStreamOrder order(e, stream);
+  if (!order.ok()) return fail(e, TFP_E_HIP, "ordering after the null stream failed");
   hipStream_t s = stream ? (hipStream_t)stream : e->stream;
   static_assert(sizeof(tfp_synth_spec) == sizeof(SynthSpecDev), "spec layout");
   int rc = upload(e, e->specs, specs, sizeof(tfp_synth_spec) * nclips);

@@ -147,7 +147,10 @@ int tfp_fingerprint_f32_batch(tfp_engine* eng, const float* x, const int64_t* of
 /* Device-resident batches (inputs already in HBM; used by the benchmark and by callers that
  * keep PCM on the GPU). A plan uploads the clip layout once. d_micro receives 2 int32 per
  * frame (m1, m2), d_db 2 doubles per frame (q1, q2) or may be NULL. stream: hipStream_t or
- * NULL for the engine's stream. Asynchronous: returns after the launch. */
+ * NULL for the engine's stream; a NULL-stream call (here and in every device form below) is
+ * ordered after the work queued on the HIP null stream before it and before the null stream's
+ * later work (the null stream is torch's default stream; the engine's stream is non-blocking).
+ * Asynchronous: returns after the launch. */
 int tfp_plan_create(tfp_engine* eng, const int64_t* offsets, int32_t nclips, int32_t sample_rate,
                     tfp_plan** out);
 void tfp_plan_destroy(tfp_plan* plan);
