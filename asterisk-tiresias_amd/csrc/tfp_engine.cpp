@@ -1601,7 +1601,12 @@ int search_core(tfp_engine* e, const int64_t* h_qoff, int32_t nq, const double* 
       if ((rc = ensure_ranges(e, sc.tole, s)) || (rc = ensure_cells(e, sc.tole, s))) return rc;
       if (e->dbg_vote && !e->cells.valid) fprintf(stderr, "[tfp] general path: no clip-set cache (row scan)\n");
       // with a delta: its cache too (a failure to build it merges the delta, below)
-      const bool dsweep = has_delta && e->cells.valid && ensure_delta_cells(e, sc.tole, s) == TFP_OK;
+      bool dsweep = has_delta && e->cells.valid;
+      if (dsweep && ensure_delta_cells(e, sc.tole, s) != TFP_OK) {
+        (void)hipGetLastError();
+        e->err.clear_own();  // (recovered: the merge below serves the batch)
+        dsweep = false;
+      }
       if (e->cells.valid && (dsweep || !has_delta)) {
         HIPCHK(e, e->wide.reserve(nf, nq, s));
         bool ok = false;

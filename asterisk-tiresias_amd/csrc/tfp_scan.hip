@@ -2139,6 +2139,8 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
     unsigned long long km = __ballot(gb > ga);
     if (kpre && !km) continue;
+    // the window's tie keys, requested before its groups (read at its end)
+    const int32_t tk = col_base + c0 + lane < C && lane < kWin ? tiekey[col_base + c0 + lane] : 0;
 #if TFP_CLIP_LAZY
     // the window's columns that got a count (wave-uniform): each column's row is written by its
     // first add and read only if written, so nothing is cleared and untouched columns cost nothing
@@ -2304,7 +2306,6 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     }
     // the window's clips: each query's best (count << 32 | tie key)
     if (!touched) continue;  // (TFP_CLIP_LAZY)
-    const int32_t tk = col_base + c0 + lane < C && lane < kWin ? tiekey[col_base + c0 + lane] : 0;
     auto take = [&](int j) {
       const uint32_t v = acc[j * 64 + lane];
       const unsigned long long t = (uint32_t)__builtin_amdgcn_readlane(tk, j);
