@@ -300,8 +300,7 @@ __device__ __forceinline__ uint32_t order_rows(const int32_t* __restrict__ om1, 
 }
 
 // Points per tile of the order (the tile's count into cnt[tile]).
-__global__ __launch_bounds__(kOT) void order_count_kernel(const unsigned long long* __restrict__ okey,
-                                                          const int32_t* __restrict__ om1, int64_t n,
+__global__ __launch_bounds__(kOT) void order_count_kernel(const int32_t* __restrict__ om1, int64_t n,
                                                           const int64_t* __restrict__ kbox, int32_t* __restrict__ cnt) {
   __shared__ int32_t wsum[kOT / 64];
   const uint32_t bits = order_rows(om1, n, kbox, (int64_t)blockIdx.x * kOTile + kOPer * threadIdx.x);
@@ -642,7 +641,7 @@ hipError_t CellCache::build_from_order(const unsigned long long* okey, const int
   if ((e = b_tile.reserve(sizeof(int32_t) * 2 * ((size_t)nt + 1))) != hipSuccess) return e;
   int32_t* cnt = b_tile.as<int32_t>();
   // 1. the points: a count per tile, their offsets, the filter
-  hipLaunchKernelGGL(order_count_kernel, dim3((unsigned)nt), dim3(kOT), 0, s, okey, om1, n, d_kbox, cnt);
+  hipLaunchKernelGGL(order_count_kernel, dim3((unsigned)nt), dim3(kOT), 0, s, om1, n, d_kbox, cnt);
   hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(1024), 0, s, cnt, nt, 1);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   int32_t tot[2] = {0, 0};
