@@ -317,6 +317,7 @@ struct WideScratch {
   int32_t* nuk = nullptr;                            // [nchunks] their number
   bool ukeys_ready = false;                          // prepare wrote ukeys / nuk (the bin sort)
   bool libsort = false;                              // TFP_WIDE_LIBSORT: the library sort on the speculative pass too
+  long long* wclk = nullptr;                         // (TFP_DEBUG_BINS: the bin sort's wave clocks)
   bool debug_bins = false;                           // TFP_DEBUG_BINS: the bin sort's counts on stderr
   // the bin sort (tfp_scan.hip wide_bin_hist ...): per (chunk, segment) frame count and L2 range,
   // per chunk and bin the frame count and first sorted frame, each window segment's first / last

@@ -1770,13 +1770,22 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     const int32_t* __restrict__ bstart, const int4* __restrict__ gi4, const int32_t* __restrict__ gb, int32_t gcap,
     const int32_t* __restrict__ cbeg, const unsigned long long* __restrict__ kb, int64_t dbase,
     const int32_t* __restrict__ seg, const int4* __restrict__ segk, int32_t* __restrict__ L2s, int32_t* __restrict__ U2s,
-    uint8_t* __restrict__ qis, int32_t* __restrict__ dtab, int32_t* __restrict__ info) {
+    uint8_t* __restrict__ qis, int32_t* __restrict__ dtab, int32_t* __restrict__ info, long long* __restrict__ wclk) {
   __shared__ unsigned long long sk[kBinSortWaves][kBinCap];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ch = blockIdx.x;
   const int32_t g = blockIdx.y * kBinSortWaves + wv;
   const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
   if (g + 1 >= gcap) return;  // (wave-uniform)
+  // (TFP_DEBUG_BINS: each wave's clock cycles, in wclk[ch][g])
+  struct WaveClock {
+    long long* w;
+    long long t0;
+    int lane;
+    __device__ ~WaveClock() {
+      if (w && lane == 0) *w = clock64() - t0;
+    }
+  } wave_clock{wclk ? wclk + (int64_t)ch * gcap + g : nullptr, clock64(), lane};
   const int4 gq = gi4[(int64_t)ch * gcap + g];
   const int32_t S0 = gq.x, S1 = gq.y;
   const int64_t cb = cbeg[ch];
@@ -2377,10 +2386,11 @@ void WideScratch::release() {
   bstart = ghist = nullptr;
   segk = nullptr;
   segstat = nullptr;
-  for (void* q : {(void*)gi4, (void*)gb})
+  for (void* q : {(void*)gi4, (void*)gb, (void*)wclk})
     if (q) (void)hipFree(q);
   gi4 = nullptr;
   gb = nullptr;
+  wclk = nullptr;
   cap_groups = 0;
   ptot = nullptr;
   ukeys = nuk = nullptr;
@@ -2518,6 +2528,11 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       ws->cap_groups = 0;
       if ((e = dmalloc(&ws->gi4, nch * gcap)) || (e = dmalloc(&ws->gb, nch * gcap))) return e;
       ws->cap_groups = nch * gcap;
+      if (ws->debug_bins) {
+        if (ws->wclk) (void)hipFree(ws->wclk);
+        ws->wclk = nullptr;
+        if ((e = dmalloc(&ws->wclk, nch * gcap))) return e;
+      }
     }
     hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
                        ws->ghist, ws->bstart, ws->seg, ws->ukeys, ws->nuk, ws->cbeg, ws->qis, ws->gi4, ws->gb,
@@ -2527,7 +2542,7 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
                        ws->bstart, ws->kb);
     hipLaunchKernelGGL(wide_bin_sort_kernel, dim3((unsigned)nch, (unsigned)((gcap + kBinSortWaves - 1) / kBinSortWaves)),
                        dim3(64 * kBinSortWaves), 0, s, ws->bstart, ws->gi4, ws->gb, (int32_t)gcap, ws->cbeg, ws->kb, dbase, ws->seg,
-                       ws->segk, ws->L2s, ws->U2s, ws->qis, ws->dtab, ws->info);
+                       ws->segk, ws->L2s, ws->U2s, ws->qis, ws->dtab, ws->info, ws->debug_bins ? ws->wclk : nullptr);
     if (ws->debug_bins) {  // (TFP_DEBUG_BINS: the bin sort's counts of the first chunk, on stderr)
       std::vector<int32_t> bs(kNFine + 1);
       std::vector<int4> g(gcap);
@@ -2547,6 +2562,24 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       }
       fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
               bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
+      // the slowest waves of every chunk, with their groups
+      std::vector<long long> wc(nch * gcap);
+      std::vector<int4> ga(nch * gcap);
+      if ((e = hipMemcpyAsync(wc.data(), ws->wclk, sizeof(long long) * nch * gcap, hipMemcpyDeviceToHost, s)) ||
+          (e = hipMemcpyAsync(ga.data(), ws->gi4, sizeof(int4) * nch * gcap, hipMemcpyDeviceToHost, s)) ||
+          (e = hipStreamSynchronize(s)))
+        return e;
+      std::vector<int64_t> ord(nch * gcap);
+      for (int64_t i = 0; i < nch * gcap; i++) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return wc[a] > wc[b]; });
+      double sum = 0;
+      for (long long v : wc) sum += (double)v;
+      fprintf(stderr, "[tfp] bin sort waves: %lld, mean %.0f cycles\n", (long long)(nch * gcap), sum / (double)(nch * gcap));
+      for (int i = 0; i < 12 && i < (int)ord.size(); i++) {
+        const int4 q = ga[ord[i]];
+        fprintf(stderr, "[tfp]   ch %lld g %lld: %lld cycles, frames [%d, %d) (%d), first bin %d of %d\n", (long long)(ord[i] / gcap),
+                (long long)(ord[i] % gcap), wc[ord[i]], q.x, q.y, q.y - q.x, q.z, q.w);
+      }
     }
   } else {
     size_t tb = ws->tmp_bytes;
