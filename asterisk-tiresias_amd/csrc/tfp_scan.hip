@@ -1401,6 +1401,9 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
 // which sends the speculative batch to the library sort (as a window width outside the key's delta
 // field does).
 constexpr int kNFine = 16384;        // bins per chunk at most (the per-segment counts halve until they fit)
+#ifndef TFP_BIN_CLOCKS
+#define TFP_BIN_CLOCKS 0
+#endif
 constexpr int kBinCap = 512;         // frames one wave sorts in LDS (16 KB a workgroup: 8 workgroups a CU)
 constexpr int kBinSortWaves = 4;     // waves per wide_bin_sort workgroup
 constexpr int kGroup = 64;           // a sort group: the bins whose first frame lies in [64 g, 64 g + 64)
@@ -1737,24 +1740,45 @@ __device__ __forceinline__ void dir_runs(int64_t pos, unsigned long long k, unsi
     lo[3] = bu + 1, hi[3] = nbk - 1, val[3] = se;
   }
 }
-// Every lane's runs written: short ones by their lane, long ones (a sparse stretch of the value
-// range) by the whole wave, 64 buckets a step. (Call with every lane of the wave.)
-__device__ __forceinline__ void dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
-                                          const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
-  constexpr int32_t kShort = 8;
+// Every lane's runs written: runs up to kLane buckets by their own lane (above 8: dwords to a
+// 16-byte boundary, then 16-byte stores: a sparse stretch of the value range gives a wave of 64 runs of
+// tens to hundreds of buckets), longer ones (e.g. the gap below a silence-floor crowd: up to a whole
+// directory) by the whole wave, 256 buckets a step. dtab 16-byte aligned. (Call with every lane.)
+__device__ __forceinline__ int64_t dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
+                                             const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
+  constexpr int32_t kLane = 256;
+  int64_t nlong = 0;  // (the buckets of runs above 8: TFP_BIN_CLOCKS)
+  int4* d4 = reinterpret_cast<int4*>(dtab);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     const int32_t len = hi[r] - lo[r] + 1;
-    if (len > 0 && len <= kShort)
+    if (len > 0 && len <= 8)
       for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
-    unsigned long long m = __ballot(len > kShort);
+    if (__ballot(len > 8 && len <= kLane) && len > 8 && len <= kLane) {
+      const int32_t v = val[r];
+      const int64_t e = (int64_t)base[r] + hi[r] + 1;
+      int64_t q = (int64_t)base[r] + lo[r];
+      for (; q < e && (q & 3); q++) dtab[q] = v;
+      for (const int4 v4 = make_int4(v, v, v, v); q + 4 <= e; q += 4) d4[q >> 2] = v4;
+      for (; q < e; q++) dtab[q] = v;
+      nlong += len;
+    }
+    unsigned long long m = __ballot(len > kLane);
     while (m) {
       const int l = __ffsll((long long)m) - 1;
       m &= m - 1;
-      const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64), o = __shfl(base[r], l, 64);
-      for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
+      const int32_t a = __builtin_amdgcn_readlane(lo[r], l), z = __builtin_amdgcn_readlane(hi[r], l),
+                    v = __builtin_amdgcn_readlane(val[r], l), o = __builtin_amdgcn_readlane(base[r], l);
+      // [s, e) absolute: its unaligned head and tail (< 4 each) by lanes, the rest as int4
+      const int64_t s = (int64_t)o + a, e = (int64_t)o + z + 1, s4 = (s + 3) & ~3ll, e4 = e & ~3ll;
+      if (lane < s4 - s) dtab[s + lane] = v;
+      if (lane < e - e4) dtab[e4 + lane] = v;
+      const int4 v4 = make_int4(v, v, v, v);
+      for (int64_t b = s4 / 4 + lane; b < e4 / 4; b += 64) d4[b] = v4;
+      nlong += e - s;
     }
   }
+  return nlong;
 }
 
 // Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
@@ -1777,15 +1801,38 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   const int32_t g = blockIdx.y * kBinSortWaves + wv;
   const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
   if (g + 1 >= gcap) return;  // (wave-uniform)
-  // (TFP_DEBUG_BINS: each wave's clock cycles, in wclk[ch][g])
+#if TFP_BIN_CLOCKS
+  // (a diagnostic build, -DTFP_BIN_CLOCKS=1 with TFP_DEBUG_BINS: each wave's clock cycles in
+  // wclk[ch][g][8]: the whole wave, the key before the group, the first crowd copy, the directory
+  // stores, the LDS sorts, the register sorts, the crowded-group loop; and the long runs' buckets)
   struct WaveClock {
     long long* w;
     long long t0;
     int lane;
+    long long c[8];
     __device__ ~WaveClock() {
-      if (w && lane == 0) *w = clock64() - t0;
+      if (w && lane == 0) {
+        w[0] = clock64() - t0;
+        for (int i = 1; i < 8; i++) w[i] = c[i];
+      }
     }
-  } wave_clock{wclk ? wclk + (int64_t)ch * gcap + g : nullptr, clock64(), lane};
+  } wave_clock{wclk ? wclk + ((int64_t)ch * gcap + g) * 8 : nullptr, clock64(), lane, {}};
+#define BCLK(i, ...)                                 \
+  do {                                               \
+    const long long t_ = clock64();                  \
+    __VA_ARGS__;                                     \
+    wave_clock.c[i] += clock64() - t_;               \
+  } while (0)
+#define BCLK_BEGIN(i) const long long t_##i = clock64()
+#define BCLK_END(i) wave_clock.c[i] += clock64() - t_##i
+#else
+#define BCLK_BEGIN(i) (void)0
+#define BCLK_END(i) (void)0
+#define BCLK(i, ...) \
+  do {               \
+    __VA_ARGS__;     \
+  } while (0)
+#endif
   const int4 gq = gi4[(int64_t)ch * gcap + g];
   const int32_t S0 = gq.x, S1 = gq.y;
   const int64_t cb = cbeg[ch];
@@ -1798,6 +1845,7 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   // value or has no max2 window (no directory), so any of its keys will do. None at the chunk start
   // (S0 > 0 has g > 0: group 0 starts at frame 0).
   unsigned long long kprev = 0;
+  BCLK_BEGIN(1);
   if (S0 > 0 && S0 < S1) {
     const int4 gr = gi4[(int64_t)ch * gcap + g - 1];
     const int32_t lo = gr.x < S0 ? max(gr.x, S0 - kBinCap) : gr.w > kBinCap ? S0 - 1 : gr.z;
@@ -1811,6 +1859,7 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
       kprev = y > kprev ? y : kprev;
     }
   }
+  BCLK_END(1);
   // sorted frame p (chunk-relative) of key k after key kp: its outputs and directory runs (valid:
   // this lane has a frame; every lane calls)
   auto put = [&](int32_t p, unsigned long long k, unsigned long long kp, bool valid) {
@@ -1826,7 +1875,11 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
         dir_runs(pos, k, kp, segk[(int64_t)ch * kKeyRange + sgk], sg[0], sg[1], lo, hi, val, base);
       }
     }
-    dir_write(dtab, lo, hi, val, base, lane);
+#if TFP_BIN_CLOCKS
+    BCLK(3, wave_clock.c[7] += dir_write(dtab, lo, hi, val, base, lane));
+#else
+    (void)dir_write(dtab, lo, hi, val, base, lane);
+#endif
   };
   // frames [b, b + n) sorted in LDS, written (kp: the key before them); returns their last key
   auto sort_lds = [&](int32_t b, int32_t n, unsigned long long kp) {
@@ -1857,7 +1910,7 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   // batch is redone): each wave copies and checks its own (a bin starting at 64 g is this group's
   // first: its predecessor is kprev), the wave of the bin's group those before the bin's first
   // multiple of 64
-  if (gq.w > kBinCap) copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w), kprev);
+  if (gq.w > kBinCap) BCLK(2, copy_big(gq.z, gq.w, max(g * kGroup, gq.z), min(g * kGroup + kGroup, gq.z + gq.w), kprev));
   const int32_t n = S1 - S0;
   if (n <= 0) return;
   // n <= 64 R: R keys a lane, sorted in registers; each frame's predecessor through the lanes
@@ -1877,33 +1930,55 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     for (int r = 0; r < R; r++) put(S0 + 64 * r + lane, v[r], pv[r], 64 * r + lane < n);
   };
   if (n <= 64) {
-    sort_regs(std::integral_constant<int, 1>{});
+    BCLK(5, sort_regs(std::integral_constant<int, 1>{}));
     return;
   }
   if (n <= 128) {
-    sort_regs(std::integral_constant<int, 2>{});
+    BCLK(5, sort_regs(std::integral_constant<int, 2>{}));
     return;
   }
   if (n <= 256) {
-    sort_regs(std::integral_constant<int, 4>{});
+    BCLK(5, sort_regs(std::integral_constant<int, 4>{}));
     return;
   }
   if (n <= kBinCap) {
-    (void)sort_lds(S0, n, kprev);
+    BCLK(4, (void)sort_lds(S0, n, kprev));
     return;
   }
-  // a crowded group: bin by bin (the bins' bounds 64 at a time)
+  // a crowded group: its bins 64 at a time, runs of small bins (contiguous frames, ascending keys)
+  // sorted together up to kBinCap frames, a crowd bin copied
   unsigned long long klast = kprev;
-  const int32_t fa = gb[(int64_t)ch * gcap + g], fz = gb[(int64_t)ch * gcap + g + 1];
+  const int32_t fa = gb[(int64_t)ch * gcap + g];
+  // the group's bins end at the first bin starting at or after S1 (the rest are empty: the last
+  // group's range runs to kNFine, thousands of empty bins past a silence-floor crowd), found 64
+  // probes a step
+  int32_t fz = gb[(int64_t)ch * gcap + g + 1];
+  for (int32_t lo = fa; fz - lo > 64;) {
+    const int32_t st = (fz - lo + 63) / 64, x = lo + (lane + 1) * st;
+    const int l = __ffsll((long long)__ballot(x >= fz || bs[x] >= S1)) - 1;  // (lane 63's x >= fz)
+    fz = min(fz, lo + (l + 1) * st);
+    lo += l * st;
+  }
+  int32_t pa = S0, pz = S0;  // the pending run of small bins: frames [pa, pz)
+  auto flush = [&]() {
+    if (pz > pa) BCLK(4, klast = sort_lds(pa, pz - pa, klast));
+  };
+  BCLK(6, {
   for (int32_t f0 = fa; f0 < fz; f0 += 64) {
     const int32_t bl = f0 + lane < fz ? bs[f0 + lane] : 0, nl = f0 + lane < fz ? bs[f0 + lane + 1] - bl : 0;
     for (unsigned long long mb = __ballot(nl > 0); mb; mb &= mb - 1) {
       const int sl = __ffsll((long long)mb) - 1;
       const int32_t b = __builtin_amdgcn_readlane(bl, sl), nb = __builtin_amdgcn_readlane(nl, sl);
       if (nb <= kBinCap) {
-        klast = sort_lds(b, nb, klast);
+        if (b != pz || b + nb - pa > kBinCap) {
+          flush();
+          pa = b;
+        }
+        pz = b + nb;
         continue;
       }
+      flush();
+      pa = pz = b + nb;
       // frames that all share (segment, L2, d) need no order (a crowd of equal values: the silence
       // floor), nor do those of a segment without a max2 window: the waves of the bin's 64-frame
       // windows copy and check them, this one the frames before the bin's first multiple of 64
@@ -1912,6 +1987,11 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
       klast = kb[cb + b + nb - 1];  // (a crowd of one value: any of its keys)
     }
   }
+  flush();
+  });
+#undef BCLK
+#undef BCLK_BEGIN
+#undef BCLK_END
 }
 
 // In-chunk prefix counts P[i][q] = frames of query q in [cbeg[ch], i], in three launches over
@@ -2531,7 +2611,8 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       if (ws->debug_bins) {
         if (ws->wclk) (void)hipFree(ws->wclk);
         ws->wclk = nullptr;
-        if ((e = dmalloc(&ws->wclk, nch * gcap))) return e;
+        if ((e = dmalloc(&ws->wclk, nch * gcap * 8))) return e;
+        if ((e = hipMemsetAsync(ws->wclk, 0, sizeof(long long) * nch * gcap * 8, s))) return e;
       }
     }
     hipLaunchKernelGGL(wide_bin_scan_kernel, dim3((unsigned)nch), dim3(1024), 0, s, d_qoff, nq, qch, (int32_t)nch, ws->segstat,
@@ -2563,22 +2644,28 @@ hipError_t launch_scan_wide_prepare(const FrameBox* boxes, const int64_t* d_qoff
       fprintf(stderr, "[tfp] bins chunk 0: kept %d, %d bins (largest %d, %d above %d), %d groups (largest %d, %d above); info %d %d %d\n",
               bs[kNFine], nb, mx, big, kBinCap, ng, gmx, gbig, inf[0], inf[1], inf[2]);
       // the slowest waves of every chunk, with their groups
-      std::vector<long long> wc(nch * gcap);
+      std::vector<long long> wc8(nch * gcap * 8), wc(nch * gcap);
       std::vector<int4> ga(nch * gcap);
-      if ((e = hipMemcpyAsync(wc.data(), ws->wclk, sizeof(long long) * nch * gcap, hipMemcpyDeviceToHost, s)) ||
+      if ((e = hipMemcpyAsync(wc8.data(), ws->wclk, sizeof(long long) * nch * gcap * 8, hipMemcpyDeviceToHost, s)) ||
           (e = hipMemcpyAsync(ga.data(), ws->gi4, sizeof(int4) * nch * gcap, hipMemcpyDeviceToHost, s)) ||
           (e = hipStreamSynchronize(s)))
         return e;
       std::vector<int64_t> ord(nch * gcap);
-      for (int64_t i = 0; i < nch * gcap; i++) ord[i] = i;
+      for (int64_t i = 0; i < nch * gcap; i++) ord[i] = i, wc[i] = wc8[i * 8];
       std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return wc[a] > wc[b]; });
-      double sum = 0;
+      double sum = 0, nlong = 0;
       for (long long v : wc) sum += (double)v;
-      fprintf(stderr, "[tfp] bin sort waves: %lld, mean %.0f cycles\n", (long long)(nch * gcap), sum / (double)(nch * gcap));
+      for (int64_t i = 0; i < nch * gcap; i++) nlong += (double)wc8[i * 8 + 7];
+      fprintf(stderr, "[tfp] bin sort waves: %lld, mean %.0f cycles, long-run buckets %.0f\n", (long long)(nch * gcap),
+              sum / (double)(nch * gcap), nlong);
       for (int i = 0; i < 12 && i < (int)ord.size(); i++) {
         const int4 q = ga[ord[i]];
-        fprintf(stderr, "[tfp]   ch %lld g %lld: %lld cycles, frames [%d, %d) (%d), first bin %d of %d\n", (long long)(ord[i] / gcap),
-                (long long)(ord[i] % gcap), wc[ord[i]], q.x, q.y, q.y - q.x, q.z, q.w);
+        const long long* c = &wc8[ord[i] * 8];
+        fprintf(stderr,
+                "[tfp]   ch %lld g %lld: %lld cycles (kprev %lld, crowd copy %lld, dir %lld, lds %lld, regs %lld, crowd loop %lld; long-run buckets %lld), "
+                "frames [%d, %d) (%d), first bin %d of %d\n",
+                (long long)(ord[i] / gcap), (long long)(ord[i] % gcap), c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], q.x, q.y,
+                q.y - q.x, q.z, q.w);
       }
     }
   } else {
