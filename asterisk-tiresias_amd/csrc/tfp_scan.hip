@@ -2107,6 +2107,46 @@ __device__ __forceinline__ uint32_t prefix_at(const uint32_t* __restrict__ P, co
 
 // lb32 / ub32: tfp_bsearch.hpp (both ends read with the first probe)
 
+#ifndef TFP_CLIP_DPP
+#define TFP_CLIP_DPP 1  // the sweep's lane scans through DPP (A/B: 0 takes ds_bpermute shuffles; even at C3)
+#endif
+// Inclusive max over lanes [gst, lane] of bm (gst <= lane, per lane): four row shifts, then rows 1
+// and 3 take lane 15 of the row before and rows 2 and 3 lane 31 (DPP: no LDS round trip per step).
+__device__ __forceinline__ int32_t seg_max_scan(int32_t bm, int32_t gst, int lane) {
+#if TFP_CLIP_DPP
+  const int rl = lane & 15;
+  int32_t y;
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x111, 0xf, 0xf, false);  // row_shr:1
+  if (rl >= 1 && lane - 1 >= gst) bm = max(bm, y);
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x112, 0xf, 0xf, false);  // row_shr:2
+  if (rl >= 2 && lane - 2 >= gst) bm = max(bm, y);
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x114, 0xf, 0xf, false);  // row_shr:4
+  if (rl >= 4 && lane - 4 >= gst) bm = max(bm, y);
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x118, 0xf, 0xf, false);  // row_shr:8
+  if (rl >= 8 && lane - 8 >= gst) bm = max(bm, y);
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x142, 0xa, 0xf, false);  // row_bcast:15 (rows 1, 3)
+  if ((lane & 16) && (lane & ~15) - 1 >= gst) bm = max(bm, y);
+  y = __builtin_amdgcn_update_dpp(bm, bm, 0x143, 0xc, 0xf, false);  // row_bcast:31 (rows 2, 3)
+  if (lane >= 32 && 31 >= gst) bm = max(bm, y);
+  return bm;
+#else
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(bm, o, 64);
+    if (lane - o >= gst) bm = max(bm, y);
+  }
+  return bm;
+#endif
+}
+// lane l's v from lane l - 1 (lane 0: its own)
+__device__ __forceinline__ int32_t lane_before(int32_t v) {
+#if TFP_CLIP_DPP
+  return __builtin_amdgcn_update_dpp(v, v, 0x138, 0xf, 0xf, false);  // wave_shr:1
+#else
+  return __shfl_up(v, 1, 64);
+#endif
+}
+
 // ---- clip-major sweep ------------------------------------------------------------------------
 // Work items are (chunk, key, clip group). A wave takes windows of kWin consecutive clip columns of
 // one chunk and, for each key the chunk uses, the groups of those clips (two kdir loads per key, no
@@ -2313,7 +2353,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           }
           const int nG = __popcll(__ballot(lane < left && pj1 <= 64));  // (pj1 grows with j: a prefix)
           if (nG == 0) {  // one group with more than 64 items: 64 at a time, runs merged across the steps
-            const int32_t pn = __shfl(pj1, 0, 64);
+            const int32_t pn = __builtin_amdgcn_readlane(pj1, 0);
             uint32_t cnt = fcnt;
             int32_t carry = -2, aopen = 0;
             bool open = false;
@@ -2322,34 +2362,29 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
               int32_t A = INT32_MAX, B = -2;
               if (i < pn) find_ab(cv.p_m2[pb0 + i], cv.p_hi[pb0 + i], A, B);
               const bool ok = A <= B;
-              int32_t bm = ok ? B : -2;
-#pragma unroll
-              for (int o = 1; o < 64; o <<= 1) {
-                const int32_t y = __shfl_up(bm, o, 64);
-                if (lane >= o) bm = max(bm, y);
-              }
-              int32_t pe = __shfl_up(bm, 1, 64);
+              const int32_t bm = seg_max_scan(ok ? B : -2, 0, lane);
+              int32_t pe = lane_before(bm);
               if (lane == 0) pe = -2;
               pe = max(pe, carry);
               unsigned long long starts = __ballot(ok && A > pe + 1);
               while (starts) {
                 const int s2 = __ffsll((long long)starts) - 1;
                 starts &= starts - 1;
-                const int32_t as = __shfl(A, s2, 64), ps = __shfl(pe, s2, 64);
+                const int32_t as = __builtin_amdgcn_readlane(A, s2), ps = __builtin_amdgcn_readlane(pe, s2);
                 if (open) close_run(cnt, aopen, ps);
                 open = true;
                 aopen = as;
               }
-              carry = max(carry, __shfl(bm, 63, 64));
+              carry = max(carry, __builtin_amdgcn_readlane(bm, 63));
             }
             if (open) close_run(cnt, aopen, carry);
-            add(__shfl(colj, 0, 64), cnt);
+            add(__builtin_amdgcn_readlane(colj, 0), cnt);
             g++;
             continue;
           }
           // every item of the batch on its own lane: its group (the last j < nG with pj0 <= lane, by
           // binary lifting over the lanes' starts) and its run [A, B] of the segment's frames
-          const int32_t npts = __shfl(pj1, nG - 1, 64);
+          const int32_t npts = __builtin_amdgcn_readlane(pj1, nG - 1);
           int gi = 0;
 #pragma unroll
           for (int bit = 32; bit >= 1; bit >>= 1) {
@@ -2361,17 +2396,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           int32_t A = INT32_MAX, B = -2;
           if (lane < npts) find_ab(cv.p_m2[pb0 + lane], cv.p_hi[pb0 + lane], A, B);
           const bool ok = lane < npts && A <= B;
-          int32_t bm = ok ? B : -2;
-#pragma unroll
-          for (int o = 1; o < 64; o <<= 1) {
-            const int32_t y = __shfl_up(bm, o, 64);
-            if (lane - o >= gst) bm = max(bm, y);
-          }
-          int32_t pe = __shfl_up(bm, 1, 64);
+          const int32_t bm = seg_max_scan(ok ? B : -2, gst, lane);
+          int32_t pe = lane_before(bm);
           if (lane == gst) pe = -2;
           const unsigned long long starts = __ballot(ok && A > pe + 1);
           for (int j = 0; j < nG; j++) {
-            const int32_t a0 = __shfl(pj0, j, 64), a1 = __shfl(pj1, j, 64);
+            const int32_t a0 = __builtin_amdgcn_readlane(pj0, j), a1 = __builtin_amdgcn_readlane(pj1, j);
             const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
             unsigned long long mm = starts & rng;
             uint32_t cnt = fcnt;
@@ -2380,13 +2410,13 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
             while (mm) {
               const int s2 = __ffsll((long long)mm) - 1;
               mm &= mm - 1;
-              const int32_t as = __shfl(A, s2, 64), ps = __shfl(pe, s2, 64);
+              const int32_t as = __builtin_amdgcn_readlane(A, s2), ps = __builtin_amdgcn_readlane(pe, s2);
               if (open) close_run(cnt, aopen, ps);
               open = true;
               aopen = as;
             }
-            if (open) close_run(cnt, aopen, __shfl(bm, a1 - 1, 64));
-            add(__shfl(colj, j, 64), cnt);
+            if (open) close_run(cnt, aopen, __builtin_amdgcn_readlane(bm, a1 - 1));
+            add(__builtin_amdgcn_readlane(colj, j), cnt);
           }
           g += nG;
         }
