@@ -1322,16 +1322,55 @@ __global__ __launch_bounds__(1024) void wide_dir_offsets_kernel(const int32_t* _
   if (t == 0) doff[nseg] = carry;
 }
 
+// Every lane's runs written: runs up to kLane buckets by their own lane (above 8: dwords to a
+// 16-byte boundary, then 16-byte stores: a sparse stretch of the value range gives a wave of 64 runs of
+// tens to hundreds of buckets), longer ones (e.g. the gap below a silence-floor crowd: up to a whole
+// directory) by the whole wave, 256 buckets a step. dtab 16-byte aligned. (Call with every lane.)
+__device__ __forceinline__ int64_t dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
+                                             const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
+  constexpr int32_t kLane = 256;
+  int64_t nlong = 0;  // (the buckets of runs above 8: TFP_BIN_CLOCKS)
+  int4* d4 = reinterpret_cast<int4*>(dtab);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int32_t len = hi[r] - lo[r] + 1;
+    if (len > 0 && len <= 8)
+      for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
+    if (__ballot(len > 8 && len <= kLane) && len > 8 && len <= kLane) {
+      const int32_t v = val[r];
+      const int64_t e = (int64_t)base[r] + hi[r] + 1;
+      int64_t q = (int64_t)base[r] + lo[r];
+      for (; q < e && (q & 3); q++) dtab[q] = v;
+      for (const int4 v4 = make_int4(v, v, v, v); q + 4 <= e; q += 4) d4[q >> 2] = v4;
+      for (; q < e; q++) dtab[q] = v;
+      nlong += len;
+    }
+    unsigned long long m = __ballot(len > kLane);
+    while (m) {
+      const int l = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const int32_t a = __builtin_amdgcn_readlane(lo[r], l), z = __builtin_amdgcn_readlane(hi[r], l),
+                    v = __builtin_amdgcn_readlane(val[r], l), o = __builtin_amdgcn_readlane(base[r], l);
+      // [s, e) absolute: its unaligned head and tail (< 4 each) by lanes, the rest as int4
+      const int64_t s = (int64_t)o + a, e = (int64_t)o + z + 1, s4 = (s + 3) & ~3ll, e4 = e & ~3ll;
+      if (lane < s4 - s) dtab[s + lane] = v;
+      if (lane < e - e4) dtab[e4 + lane] = v;
+      const int4 v4 = make_int4(v, v, v, v);
+      for (int64_t b = s4 / 4 + lane; b < e4 / 4; b += 64) d4[b] = v4;
+      nlong += e - s;
+    }
+  }
+  return nlong;
+}
 // The directories, from the sorted frames: frame i of a window segment is the first frame of the
 // buckets after its predecessor's bucket up to its own (each bucket written once), the last frame
-// also fills the buckets after its own with se; the first writes the segment's constants (segk). Lanes write short runs themselves; a long run (a
-// sparse stretch of the value range: outlying max2 values) is written by the whole wave, 64
-// buckets per step, so no lane loops over thousands of buckets alone.
+// also fills the buckets after its own with se; the first writes the segment's constants (segk).
+// The runs through dir_write (a long one, a sparse stretch of the value range, by the whole wave:
+// no lane loops over thousands of buckets alone).
 __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsigned long long* __restrict__ ck,
                                      int segshift, const int32_t* __restrict__ seg, const int32_t* __restrict__ L2s,
                                      const int32_t* __restrict__ U2s, const int32_t* __restrict__ doff,
                                      int32_t* __restrict__ dtab, int4* __restrict__ segk) {
-  constexpr int32_t kShort = 8;
   const int64_t n = *pn;
   const int lane = threadIdx.x & 63;
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
@@ -1364,20 +1403,7 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
         }
       }
     }
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      const int32_t len = hi[r] - lo[r] + 1;
-      if (len > 0 && len <= kShort)
-        for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
-      unsigned long long m = __ballot(len > kShort);
-      while (m) {
-        const int l = __ffsll((long long)m) - 1;
-        m &= m - 1;
-        const int32_t a = __shfl(lo[r], l, 64), z = __shfl(hi[r], l, 64), v = __shfl(val[r], l, 64),
-                      o = __shfl(base[r], l, 64);
-        for (int32_t b = a + lane; b <= z; b += 64) dtab[o + b] = v;
-      }
-    }
+    (void)dir_write(dtab, lo, hi, val, base, lane);
   }
 }
 
@@ -1661,8 +1687,9 @@ __device__ __forceinline__ unsigned long long shfl_up_u64(unsigned long long v, 
   const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, d, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), d, 64);
   return ((unsigned long long)hi << 32) | lo;
 }
-__device__ __forceinline__ unsigned long long shfl_u64(unsigned long long v, int l) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, l, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), l, 64);
+__device__ __forceinline__ unsigned long long readlane_u64(unsigned long long v, int l) {  // (l wave-uniform)
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l),
+                 hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l);
   return ((unsigned long long)hi << 32) | lo;
 }
 __device__ __forceinline__ unsigned long long shfl_xor_u64(unsigned long long v, int m) {
@@ -1739,46 +1766,6 @@ __device__ __forceinline__ void dir_runs(int64_t pos, unsigned long long k, unsi
     lo[2] = bi + 1, hi[2] = nbk - 1, val[2] = se;
     lo[3] = bu + 1, hi[3] = nbk - 1, val[3] = se;
   }
-}
-// Every lane's runs written: runs up to kLane buckets by their own lane (above 8: dwords to a
-// 16-byte boundary, then 16-byte stores: a sparse stretch of the value range gives a wave of 64 runs of
-// tens to hundreds of buckets), longer ones (e.g. the gap below a silence-floor crowd: up to a whole
-// directory) by the whole wave, 256 buckets a step. dtab 16-byte aligned. (Call with every lane.)
-__device__ __forceinline__ int64_t dir_write(int32_t* __restrict__ dtab, const int32_t (&lo)[4], const int32_t (&hi)[4],
-                                             const int32_t (&val)[4], const int32_t (&base)[4], int lane) {
-  constexpr int32_t kLane = 256;
-  int64_t nlong = 0;  // (the buckets of runs above 8: TFP_BIN_CLOCKS)
-  int4* d4 = reinterpret_cast<int4*>(dtab);
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    const int32_t len = hi[r] - lo[r] + 1;
-    if (len > 0 && len <= 8)
-      for (int32_t b = lo[r]; b <= hi[r]; b++) dtab[base[r] + b] = val[r];
-    if (__ballot(len > 8 && len <= kLane) && len > 8 && len <= kLane) {
-      const int32_t v = val[r];
-      const int64_t e = (int64_t)base[r] + hi[r] + 1;
-      int64_t q = (int64_t)base[r] + lo[r];
-      for (; q < e && (q & 3); q++) dtab[q] = v;
-      for (const int4 v4 = make_int4(v, v, v, v); q + 4 <= e; q += 4) d4[q >> 2] = v4;
-      for (; q < e; q++) dtab[q] = v;
-      nlong += len;
-    }
-    unsigned long long m = __ballot(len > kLane);
-    while (m) {
-      const int l = __ffsll((long long)m) - 1;
-      m &= m - 1;
-      const int32_t a = __builtin_amdgcn_readlane(lo[r], l), z = __builtin_amdgcn_readlane(hi[r], l),
-                    v = __builtin_amdgcn_readlane(val[r], l), o = __builtin_amdgcn_readlane(base[r], l);
-      // [s, e) absolute: its unaligned head and tail (< 4 each) by lanes, the rest as int4
-      const int64_t s = (int64_t)o + a, e = (int64_t)o + z + 1, s4 = (s + 3) & ~3ll, e4 = e & ~3ll;
-      if (lane < s4 - s) dtab[s + lane] = v;
-      if (lane < e - e4) dtab[e4 + lane] = v;
-      const int4 v4 = make_int4(v, v, v, v);
-      for (int64_t b = s4 / 4 + lane; b < e4 / 4; b += 64) d4[b] = v4;
-      nlong += e - s;
-    }
-  }
-  return nlong;
 }
 
 // Sort groups: group g of a chunk is the run of bins whose first frame lies in [64 g, 64 g + 64)
@@ -1923,7 +1910,7 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
     unsigned long long pv[R];
 #pragma unroll
     for (int r = 0; r < R; r++) {  // (every lane: the shuffles read whole rows)
-      const unsigned long long up = shfl_up_u64(v[r], 1), last = shfl_u64(v[r > 0 ? r - 1 : 0], 63);
+      const unsigned long long up = shfl_up_u64(v[r], 1), last = readlane_u64(v[r > 0 ? r - 1 : 0], 63);
       pv[r] = lane ? up : r ? last : kprev;
     }
 #pragma unroll
