@@ -397,3 +397,82 @@ def test_bin_sort_overflow_redone_with_library_sort(oracle, tfp_lib):
         assert (st["bins"], st["library"], st["redone"]) == (0, 1, 1), st
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("tol", [0.001, 0.3])
+def test_bin_sort_crowd_groups_and_sparse_directory_runs(oracle, tfp_lib, tol):
+    """The bin sort's crowded groups and its directory runs of every length (tfp_scan.hip
+    wide_bin_sort, dir_write). In every chunk one window segment (key 25) holds a crowd of one value
+    (a quarter of the frames at exactly 40 dB: copied unsorted) after small bins of distinct values
+    just below it in the same sort group (sorted together, then the crowd); another segment (key 24)
+    mixes a dense cluster, tight clumps 20-30 dB apart and a thin spread, so its directories have
+    runs of 1-8 buckets, of 9-256 (written by their own lanes) and of hundreds to thousands (by the
+    whole wave), from every alignment. Keys == the oracle (src/fp_handler.c:318-374); the batch took
+    the bin sort (no redo) and copied crowd bins (tfp_sweep_stats)."""
+    rng = np.random.default_rng(int(tol * 1e3) + 5)
+    nclips, rows, extra = 48, 250, 40
+    uuids = [str(uuidlib.UUID(bytes=rng.bytes(16), version=4)) for _ in range(nclips)]
+
+    def sparse_db(n):  # key 24's max2 mixture (dB)
+        u = rng.random(n)
+        return np.where(u < 0.4, 10.0 + rng.normal(0, 0.5, n),  # (wide enough that no bin passes 512 distinct values)
+               np.where(u < 0.6, -40.0 + rng.uniform(-1.0, 1.0, n),
+               np.where(u < 0.62, rng.uniform(-20.0, 0.0, n), 35.0 + rng.uniform(-1.5, 1.5, n))))
+
+    m1s, m2s, clips = [], [], []
+    for c in range(nclips):
+        k = rng.integers(20, 24, rows)
+        m1s.append(k * 1_000_000 + rng.integers(-800, 800, rows))  # (a frame's max1 box is its truncated max1 +- tol)
+        m2s.append(np.where(rng.random(rows) < 0.3, rng.normal(40e6, 2e6, rows), rng.uniform(-60e6, 40e6, rows)))
+        # rows of the crowd's key (max2 spread over 39-41 dB) and of the sparse key
+        m1s.append(np.full(extra, 25_000_000) + rng.integers(-400, 400, extra))
+        m2s.append(rng.uniform(39e6, 41e6, extra))
+        m1s.append(np.full(extra, 24_000_000) + rng.integers(-400, 400, extra))
+        m2s.append(sparse_db(extra) * 1e6)
+        clips.append(np.full(rows + 2 * extra, c))
+    m1 = np.concatenate(m1s).astype(np.int32)
+    m2 = np.concatenate(m2s).astype(np.int32)
+    clip = np.concatenate(clips).astype(np.int32)
+    nq = 520  # three 256-query chunks, the last partly filled
+    q1s, q2s, qoff = [], [], [0]
+    for i in range(nq):
+        c = int(rng.integers(nclips))
+        n = int(rng.integers(120, 200))
+        src = rng.choice(np.flatnonzero(clip == c)[:rows], n)
+        q1 = m1[src] / 1e6 + rng.normal(0, 0.0003, n)
+        q2 = m2[src] / 1e6 + rng.normal(0, 0.0003, n)
+        u = rng.random(n)
+        crowd, near, sparse = u < 0.25, (u >= 0.25) & (u < 0.28), (u >= 0.28) & (u < 0.40)
+        q1 = np.where(crowd | near, 25.3, np.where(sparse, 24.4, q1))
+        # the crowd at exactly 40 dB; its neighbours at least 2 mdB away (outside the crowd's bin)
+        side = np.where(rng.random(n) < 0.5, -1.0, 1.0)
+        q2 = np.where(crowd, 40.0, np.where(near, 40.0 + side * rng.uniform(0.002, 0.15, n), q2))
+        q2 = np.where(sparse, sparse_db(n), q2)
+        q1s.append(q1)
+        q2s.append(q2)
+        qoff.append(qoff[-1] + n)
+    q1 = np.concatenate(q1s)
+    q2 = np.concatenate(q2s)
+    qoff = np.asarray(qoff, np.int64)
+    frames = np.zeros(len(q1), np.dtype([("frame_idx", "<i4"), ("m1", "<i4"), ("m2", "<i4"), ("reserved", "<i4"),
+                                         ("q1", "<f8"), ("q2", "<f8")]))
+    frames["q1"], frames["q2"] = q1, q2
+    expect = []
+    for i in range(nq):
+        s = slice(qoff[i], qoff[i + 1])
+        found, w, mc, fc = oracle.search(m1, m2, clip, uuids, q1[s], q2[s], 2, tol, -1, -1)
+        expect.append((uuids[w], mc) if found else None)
+    assert sum(e is not None for e in expect) > nq // 2
+    eng = _engine_with(tfp_lib, {"TFP_WIDE_MIN_TOL": "0"})
+    try:
+        for c in range(nclips):
+            sel = clip == c
+            eng.index_add(uuids[c], m1[sel], m2[sel])
+        st0 = eng.sweep_stats()
+        res, _ = eng.search_batch(frames, qoff, tfp_lib.params(2, tol))
+        got = [None if r is None else (r["audio_uuid"], r["match_count"]) for r in res]
+        assert got == expect, (tol, [i for i in range(nq) if got[i] != expect[i]][:5])
+        st = {k: v - st0[k] for k, v in eng.sweep_stats().items()}
+        assert (st["bins"], st["library"], st["redone"]) == (1, 0, 0) and st["crowd"] >= 2, st
+    finally:
+        eng.close()
