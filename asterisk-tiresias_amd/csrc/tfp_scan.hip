@@ -1427,6 +1427,9 @@ __global__ void wide_dir_fill_kernel(const int32_t* __restrict__ pn, const unsig
 // which sends the speculative batch to the library sort (as a window width outside the key's delta
 // field does).
 constexpr int kNFine = 16384;        // bins per chunk at most (the per-segment counts halve until they fit)
+#ifndef TFP_BINSORT_REVERSE
+#define TFP_BINSORT_REVERSE 1
+#endif
 #ifndef TFP_BIN_CLOCKS
 #define TFP_BIN_CLOCKS 0
 #endif
@@ -1785,7 +1788,13 @@ __global__ __launch_bounds__(64 * kBinSortWaves) void wide_bin_sort_kernel(
   __shared__ unsigned long long sk[kBinSortWaves][kBinCap];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int ch = blockIdx.x;
+#if TFP_BINSORT_REVERSE
+  // groups in descending order of dispatch: a chunk's last groups, where the silence-floor crowd
+  // sorts (the longest waves), start first instead of last
+  const int32_t g = (gridDim.y - 1 - blockIdx.y) * kBinSortWaves + wv;
+#else
   const int32_t g = blockIdx.y * kBinSortWaves + wv;
+#endif
   const int32_t* bs = bstart + (int64_t)ch * (kNFine + 1);
   if (g + 1 >= gcap) return;  // (wave-uniform)
 #if TFP_BIN_CLOCKS
