@@ -2186,11 +2186,26 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
     const int32_t* __restrict__ kdir, int32_t nwin, const int32_t* __restrict__ ukeys, const int32_t* __restrict__ nuk,
     const int32_t* __restrict__ L2s, const int32_t* __restrict__ U2s, const uint32_t* __restrict__ P,
     const uint8_t* __restrict__ qis, const int32_t* __restrict__ tiekey, int32_t C, const int4* __restrict__ segk, const int32_t* __restrict__ dtab,
-    unsigned long long* __restrict__ part, const int32_t* __restrict__ stop, int32_t col_base) {
+    unsigned long long* __restrict__ part, const int32_t* __restrict__ stop, int32_t col_base, long long* __restrict__ wclk) {
   // stop (the bin sort's batches): info; info[2] > 0 left a bin unsorted and its directory unbuilt,
   // so the sweep reads nothing (the batch is redone; its maxima are not used)
   if (stop && stop[2] > 0) return;
   __shared__ __attribute__((aligned(16))) uint32_t accs[kClipWaves][kWin * 64];
+#if TFP_BIN_CLOCKS
+  // (the diagnostic build with TFP_DEBUG_BINS: each wave's clock cycles and dispatch order in wclk)
+  struct ClipClock {
+    long long* w;
+    long long t0;
+    __device__ ~ClipClock() {
+      if (w && (threadIdx.x & 63) == 0) {
+        w[0] = clock64() - t0;
+        w[1] = t0;
+      }
+    }
+  } clip_clock{wclk ? wclk + 2 * ((int64_t)blockIdx.x * kClipWaves + (threadIdx.x >> 6)) : nullptr, clock64()};
+#else
+  (void)wclk;
+#endif
   // wv through readfirstlane: the wave's chunk, window range and per-chunk pointers are then scalar
   // (as per-lane values they took 64-bit VGPR pairs, and 12 VGPRs spilled at 8 waves per SIMD)
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2782,19 +2797,43 @@ hipError_t launch_scan_wide(int32_t nq, int64_t nf, const CellCache* cells, cons
   const int64_t xcap = std::min<int64_t>(2 * kPartWaves, (int64_t)kPartWaves * (ws->qch / kWideCh));
   xw = std::min<int64_t>(xw, std::min<int64_t>(xcap, cells->nwin));
   xw = std::max<int64_t>(kClipWaves, (xw + kClipWaves - 1) / kClipWaves * kClipWaves);
+  // (TFP_DEBUG_BINS with a -DTFP_BIN_CLOCKS=1 build: the sweep's wave clocks in the bin sort's clock buffer)
+  long long* clk = TFP_BIN_CLOCKS && ws->debug_bins && ws->wclk && 2 * nch * xw <= 8 * ws->cap_groups ? ws->wclk : nullptr;
   if (!ws->ukeys_ready) hipLaunchKernelGGL(wide_ukeys_kernel, dim3((unsigned)nch), dim3(1024), 0, s, ws->seg, ws->ukeys, ws->nuk);
   if (ws->qch == 256) {
     hipLaunchKernelGGL(wide_clips_kernel<4>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base);
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base, clk);
     hipLaunchKernelGGL(wide_part_max_kernel<4>, dim3((unsigned)nch, 8), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
   } else {
     hipLaunchKernelGGL(wide_clips_kernel<2>, dim3((unsigned)(nch * xw / kClipWaves)), dim3(64 * kClipWaves), 0, s, (int32_t)xw,
                        ws->seg, ws->cbeg, cv, cells->kdir, cells->nwin, ws->ukeys, ws->nuk, ws->L2s, ws->U2s, ws->P, ws->qis, d_tiekey,
-                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base);
+                       C, ws->segk, ws->dtab, ws->part, ws->ukeys_ready ? ws->info : nullptr, col_base, clk);
     hipLaunchKernelGGL(wide_part_max_kernel<2>, dim3((unsigned)nch, 4), dim3(1024), 0, s, ws->part, (int32_t)(xw / kClipWaves),
                        nq, d_best, ws->info, d_info_out);
+  }
+  if (clk) {  // (TFP_DEBUG_BINS) the sweep's wave clocks: their spread
+    const int64_t nw = nch * xw;
+    std::vector<long long> wc(2 * nw);
+    hipError_t e;
+    if ((e = hipMemcpyAsync(wc.data(), clk, sizeof(long long) * 2 * nw, hipMemcpyDeviceToHost, s)) || (e = hipStreamSynchronize(s)))
+      return e;
+    std::vector<long long> c(nw);
+    for (int64_t i = 0; i < nw; i++) c[i] = wc[2 * i];
+    std::vector<long long> o = c;
+    std::sort(o.begin(), o.end());
+    double sum = 0;
+    for (long long v : c) sum += (double)v;
+    fprintf(stderr, "[tfp] clip sweep waves: %lld, mean %.0f, p50 %lld, p90 %lld, p99 %lld, max %lld cycles\n", (long long)nw,
+            sum / (double)nw, o[nw / 2], o[nw * 9 / 10], o[nw * 99 / 100], o[nw - 1]);
+    // the slowest waves' chunk and window share
+    std::vector<int64_t> ix(nw);
+    for (int64_t i = 0; i < nw; i++) ix[i] = i;
+    std::partial_sort(ix.begin(), ix.begin() + std::min<int64_t>(8, nw), ix.end(), [&](int64_t a, int64_t b) { return c[a] > c[b]; });
+    for (int i = 0; i < 8 && i < nw; i++)
+      fprintf(stderr, "[tfp]   wave %lld (chunk %lld, share %lld): %lld cycles\n", (long long)ix[i], (long long)(ix[i] / xw),
+              (long long)(ix[i] % xw), c[ix[i]]);
   }
   if (info_written) *info_written = d_info_out != nullptr;
   return hipGetLastError();
