@@ -2177,6 +2177,9 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001;
 // 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 constexpr int kClipOcc = 8;
+#ifndef TFP_CLIP_RUNQ
+#define TFP_CLIP_RUNQ 1  // a batch's run ends lane-parallel, their prefix rows four runs at a time (A/B: 0)
+#endif
 #ifndef TFP_CLIP_LAZY
 #define TFP_CLIP_LAZY 1  // count rows written on a column's first add (A/B: 0 clears all 16 per window)
 #endif
@@ -2411,6 +2414,51 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           int32_t pe = lane_before(bm);
           if (lane == gst) pe = -2;
           const unsigned long long starts = __ballot(ok && A > pe + 1);
+#if TFP_CLIP_RUNQ
+          // Every run's end at once, lane-parallel: a run starting at lane l ends where the next run
+          // of its group starts (pe there) or at its group's last item (bm). Then the runs' prefix
+          // rows four at a time: their eight loads in flight together, where one run's two loads
+          // each waited out a round trip before the next run's were issued (the batch's runs were
+          // a chain of dependent-latency steps). Each group's count (fcnt + its runs' deltas) goes
+          // to its column in group order, as before.
+          const unsigned long long later = lane < 63 ? starts & (~0ull << (lane + 1)) : 0ull;
+          const int nx = later ? (int)__builtin_ctzll(later) : 64;
+          const int32_t gend = __shfl(pj1, gi, 64);
+          const int32_t pen = __shfl(pe, nx < 64 ? nx : 63, 64), bme = __shfl(bm, gend > 0 ? gend - 1 : 0, 64);
+          const int32_t rend = nx < gend ? pen : bme;
+          int cg = 0;
+          uint32_t cnt = fcnt;
+          auto flush_to = [&](int gg) {
+            for (; cg < gg; cg++) {
+              add(__builtin_amdgcn_readlane(colj, cg), cnt);
+              cnt = fcnt;
+            }
+          };
+          for (unsigned long long rm = starts; rm;) {
+            int rl[4] = {0, 0, 0, 0}, nr = 0;
+            uint32_t hv[4] = {0u, 0u, 0u, 0u}, lv[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              if (rm) {
+                const int l = __ffsll((long long)rm) - 1;
+                rm &= rm - 1;
+                rl[k] = l;
+                nr = k + 1;
+                const int32_t a = __builtin_amdgcn_readlane(A, l), b = __builtin_amdgcn_readlane(rend, l);
+                hv[k] = prefix_at<QPL>(P, qis, cb, b, lane);
+                lv[k] = a > sb ? prefix_at<QPL>(P, qis, cb, a - 1, lane) : base;
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+              if (k < nr) {
+                flush_to(__builtin_amdgcn_readlane(gi, rl[k]));
+                cnt += hv[k] - lv[k];
+              }
+            }
+          }
+          flush_to(nG);
+#else
           for (int j = 0; j < nG; j++) {
             const int32_t a0 = __builtin_amdgcn_readlane(pj0, j), a1 = __builtin_amdgcn_readlane(pj1, j);
             const unsigned long long rng = (a1 >= 64 ? ~0ull : ((1ull << a1) - 1)) & ~((1ull << a0) - 1);
@@ -2429,6 +2477,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
             if (open) close_run(cnt, aopen, __builtin_amdgcn_readlane(bm, a1 - 1));
             add(__builtin_amdgcn_readlane(colj, j), cnt);
           }
+#endif
           g += nG;
         }
       }
