@@ -2178,7 +2178,9 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 // 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 constexpr int kClipOcc = 8;
 #ifndef TFP_CLIP_RUNQ
-#define TFP_CLIP_RUNQ 1  // a batch's run ends lane-parallel, their prefix rows four runs at a time (A/B: 0)
+// a batch's run ends lane-parallel, their prefix rows this many runs at a time (A/B: 0 one by one;
+// C3 tol 0.001 wide_clips 192 / 157 / 154 us at 0 / 4 / 6, 63 VGPRs at 6 and spills at 8)
+#define TFP_CLIP_RUNQ 4
 #endif
 #ifndef TFP_CLIP_LAZY
 #define TFP_CLIP_LAZY 1  // count rows written on a column's first add (A/B: 0 clears all 16 per window)
@@ -2417,7 +2419,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
 #if TFP_CLIP_RUNQ
           // Every run's end at once, lane-parallel: a run starting at lane l ends where the next run
           // of its group starts (pe there) or at its group's last item (bm). Then the runs' prefix
-          // rows four at a time: their eight loads in flight together, where one run's two loads
+          // rows kQ runs at a time: their 2 kQ loads in flight together, where one run's two loads
           // each waited out a round trip before the next run's were issued (the batch's runs were
           // a chain of dependent-latency steps). Each group's count (fcnt + its runs' deltas) goes
           // to its column in group order, as before.
@@ -2434,11 +2436,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
               cnt = fcnt;
             }
           };
+          constexpr int kQ = TFP_CLIP_RUNQ;
           for (unsigned long long rm = starts; rm;) {
-            int rl[4] = {0, 0, 0, 0}, nr = 0;
-            uint32_t hv[4] = {0u, 0u, 0u, 0u}, lv[4] = {0u, 0u, 0u, 0u};
+            int rl[kQ] = {}, nr = 0;
+            uint32_t hv[kQ] = {}, lv[kQ] = {};
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < kQ; k++) {
               if (rm) {
                 const int l = __ffsll((long long)rm) - 1;
                 rm &= rm - 1;
@@ -2450,7 +2453,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
               }
             }
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
+            for (int k = 0; k < kQ; k++) {
               if (k < nr) {
                 flush_to(__builtin_amdgcn_readlane(gi, rl[k]));
                 cnt += hv[k] - lv[k];
