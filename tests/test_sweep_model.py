@@ -135,3 +135,73 @@ def test_checkpoint_prefix_counts():
         for ch in range(nch):
             for e in range(int(cbeg[ch]), int(cbeg[ch + 1])):
                 assert (prefix_at(int(cbeg[ch]), e) == full[e]).all()
+
+
+def seg_max_scan_model(bm, gst):
+    """tfp_scan.hip seg_max_scan's DPP steps on 64 lanes: row_shr 1/2/4/8 inside 16-lane rows
+    (a lane whose source falls off its row keeps its value), then rows 1 and 3 take lane 15 of the
+    row before (row_bcast:15) and rows 2 and 3 lane 31 (row_bcast:31), each step taken only where
+    its source lies at or after the lane's group start gst."""
+    v = list(bm)
+    for n in (1, 2, 4, 8):
+        y = [v[l - n] if l % 16 >= n else v[l] for l in range(64)]
+        v = [max(v[l], y[l]) if (l % 16 >= n and l - n >= gst[l]) else v[l] for l in range(64)]
+    y = [v[(l & ~15) - 1] if (l >> 4) in (1, 3) else v[l] for l in range(64)]
+    v = [max(v[l], y[l]) if ((l & 16) and (l & ~15) - 1 >= gst[l]) else v[l] for l in range(64)]
+    y = [v[31] if l >= 32 else v[l] for l in range(64)]
+    v = [max(v[l], y[l]) if (l >= 32 and 31 >= gst[l]) else v[l] for l in range(64)]
+    return v
+
+
+def test_seg_max_scan_dpp_rule():
+    """The run-end scan's DPP form (seg_max_scan) equals its definition, the max of bm over lanes
+    [gst, lane] of the lane's group, for random group layouts (wide_clips' batches)."""
+    rng = np.random.default_rng(5)
+    for _ in range(300):
+        cuts = sorted(set([0] + list(rng.integers(1, 64, rng.integers(0, 20)))))
+        gst = [max(c for c in cuts if c <= l) for l in range(64)]
+        bm = [int(x) for x in rng.integers(-2, 1000, 64)]
+        want = [max(bm[gst[l]:l + 1]) for l in range(64)]
+        assert seg_max_scan_model(bm, gst) == want
+
+
+def test_run_queue_ends_equal_serial_closes():
+    """wide_clips' run queue (TFP_CLIP_RUNQ): each run's end found lane-parallel (the next start of
+    its group, where pe is the running max before it, else its group's last bm) gives the same runs
+    [A, end] per group as the serial form that closed the open run at every start and at the group's
+    end."""
+    rng = np.random.default_rng(9)
+    for _ in range(300):
+        npts = int(rng.integers(1, 65))
+        cuts = sorted(set([0] + list(rng.integers(1, npts, rng.integers(0, 12))) if npts > 1 else [0]))
+        ng = len(cuts)
+        pj0 = cuts + [npts] * (64 - ng)
+        pj1 = cuts[1:] + [npts] + [npts] * (64 - ng)
+        gi = [max(j for j in range(ng) if cuts[j] <= l) if l < npts else ng - 1 for l in range(64)]
+        gst = [cuts[gi[l]] for l in range(64)]
+        A = [int(x) for x in rng.integers(0, 200, 64)]
+        B = [a + int(w) - 3 for a, w in zip(A, rng.integers(0, 20, 64))]
+        ok = [l < npts and A[l] <= B[l] for l in range(64)]
+        bm = [max([B[k] if ok[k] else -2 for k in range(gst[l], l + 1)]) for l in range(64)]
+        pe = [-2 if l == gst[l] else bm[l - 1] for l in range(64)]
+        starts = [ok[l] and A[l] > pe[l] + 1 for l in range(64)]
+        serial = []
+        for j in range(ng):
+            runs, aopen = [], None
+            for l in range(pj0[j], pj1[j]):
+                if starts[l]:
+                    if aopen is not None:
+                        runs.append((aopen, pe[l]))
+                    aopen = A[l]
+            if aopen is not None:
+                runs.append((aopen, bm[pj1[j] - 1]))
+            serial.append(runs)
+        queued = [[] for _ in range(ng)]
+        for l in range(64):
+            if not starts[l]:
+                continue
+            nxt = next((k for k in range(l + 1, 64) if starts[k]), 64)
+            gend = pj1[gi[l]]
+            end = pe[nxt] if nxt < gend else bm[max(gend - 1, 0)]
+            queued[gi[l]].append((A[l], end))
+        assert queued == serial
