@@ -2134,6 +2134,16 @@ __device__ __forceinline__ int32_t seg_max_scan(int32_t bm, int32_t gst, int lan
   return bm;
 #endif
 }
+// OR of x over the wave (DPP: row shifts, then the rows' last lanes; no LDS round trip)
+__device__ __forceinline__ uint32_t wave_or_dpp(uint32_t x) {
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+  x |= (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
+}
 // lane l's v from lane l - 1 (lane 0: its own)
 __device__ __forceinline__ int32_t lane_before(int32_t v) {
 #if TFP_CLIP_DPP
@@ -2177,6 +2187,9 @@ __global__ __launch_bounds__(1024) void wide_ukeys_kernel(const int32_t* __restr
 // waves per SIMD the register budget is cut for (5, 6, 8: 1.185, 1.179, 1.151 ms at C3 tol 0.001;
 // 8 spilled 12 VGPRs before r04: the wave index is now scalar, 49 VGPRs)
 constexpr int kClipOcc = 8;
+#ifndef TFP_CLIP_GROUP_MASK
+#define TFP_CLIP_GROUP_MASK 1  // a batch's groups from a DPP-reduced mask of their starts (A/B: 0 binary lifting)
+#endif
 #ifndef TFP_CLIP_RUNQ
 // a batch's run ends lane-parallel, their prefix rows this many runs at a time (A/B: 0 one by one;
 // C3 tol 0.001 wide_clips 192 / 157 / 154 us at 0 / 4 / 6, 63 VGPRs at 6 and spills at 8)
@@ -2401,6 +2414,18 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           // every item of the batch on its own lane: its group (the last j < nG with pj0 <= lane, by
           // binary lifting over the lanes' starts) and its run [A, B] of the segment's frames
           const int32_t npts = __builtin_amdgcn_readlane(pj1, nG - 1);
+#if TFP_CLIP_GROUP_MASK
+          // the batch's group starts as one wave-uniform mask (groups are contiguous and non-empty:
+          // each starts one bit past its predecessor's items), OR-reduced through DPP: a lane's
+          // group, its start and the next group's start by bit counts, where a binary lifting took
+          // six dependent ds_bpermute
+          const unsigned long long bitj = lane < nG ? 1ull << pj0 : 0ull;
+          const unsigned long long gm = ((unsigned long long)wave_or_dpp((uint32_t)(bitj >> 32)) << 32) |
+                                        wave_or_dpp((uint32_t)bitj);
+          const unsigned long long le = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+          const int gi = __popcll(gm & le) - 1;
+          const int32_t gst = 63 - __clzll(gm & le);
+#else
           int gi = 0;
 #pragma unroll
           for (int bit = 32; bit >= 1; bit >>= 1) {
@@ -2409,6 +2434,7 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
             if (cand < nG && xx <= lane) gi = cand;
           }
           const int32_t gst = __shfl(pj0, gi, 64);
+#endif
           int32_t A = INT32_MAX, B = -2;
           if (lane < npts) find_ab(cv.p_m2[pb0 + lane], cv.p_hi[pb0 + lane], A, B);
           const bool ok = lane < npts && A <= B;
@@ -2425,7 +2451,12 @@ __global__ __launch_bounds__(64 * kClipWaves, kClipOcc) void wide_clips_kernel(
           // to its column in group order, as before.
           const unsigned long long later = lane < 63 ? starts & (~0ull << (lane + 1)) : 0ull;
           const int nx = later ? (int)__builtin_ctzll(later) : 64;
+#if TFP_CLIP_GROUP_MASK
+          const unsigned long long gab = gm & ~le;
+          const int32_t gend = gab ? (int32_t)__builtin_ctzll(gab) : npts;
+#else
           const int32_t gend = __shfl(pj1, gi, 64);
+#endif
           const int32_t pen = __shfl(pe, nx < 64 ? nx : 63, 64), bme = __shfl(bm, gend > 0 ? gend - 1 : 0, 64);
           const int32_t rend = nx < gend ? pen : bme;
           int cg = 0;
