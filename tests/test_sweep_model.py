@@ -205,3 +205,32 @@ def test_run_queue_ends_equal_serial_closes():
             end = pe[nxt] if nxt < gend else bm[max(gend - 1, 0)]
             queued[gi[l]].append((A[l], end))
         assert queued == serial
+
+
+def test_group_mask_equals_binary_lifting():
+    """wide_clips' batch groups from the mask of their starts (TFP_CLIP_GROUP_MASK: a lane's group
+    = set bits at or below it - 1, its start = the highest such bit, the next group's start = the
+    lowest bit above it or the batch's item count) equal the binary lifting over the groups' starts
+    pj0 (the last group j < nG with pj0[j] <= lane) for contiguous, non-empty groups."""
+    rng = np.random.default_rng(13)
+    for _ in range(500):
+        npts = int(rng.integers(1, 65))
+        cuts = sorted(set([0] + (list(rng.integers(1, npts, rng.integers(0, 20))) if npts > 1 else [])))
+        ng = len(cuts)
+        pj0 = cuts + [npts] * (64 - ng)
+        pj1 = cuts[1:] + [npts] * (65 - ng)
+        gm = 0
+        for j in range(ng):
+            gm |= 1 << pj0[j]
+        for lane in range(64):
+            gi = 0
+            for bit in (32, 16, 8, 4, 2, 1):
+                cand = gi + bit
+                if cand < ng and pj0[min(cand, 63)] <= lane:
+                    gi = cand
+            le = (1 << (lane + 1)) - 1
+            mgi = bin(gm & le).count("1") - 1
+            mgst = (gm & le).bit_length() - 1
+            above = gm & ~le & ((1 << 64) - 1)
+            mgend = (above & -above).bit_length() - 1 if above else npts
+            assert (mgi, mgst, mgend) == (gi, pj0[gi], pj1[gi]), (lane, cuts)
