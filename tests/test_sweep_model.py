@@ -215,7 +215,7 @@ def test_group_mask_equals_binary_lifting():
     rng = np.random.default_rng(13)
     for _ in range(500):
         npts = int(rng.integers(1, 65))
-        cuts = sorted(set([0] + (list(rng.integers(1, npts, rng.integers(0, 20))) if npts > 1 else [])))
+        cuts = sorted(set([0] + ([int(x) for x in rng.integers(1, npts, rng.integers(0, 20))] if npts > 1 else [])))
         ng = len(cuts)
         pj0 = cuts + [npts] * (64 - ng)
         pj1 = cuts[1:] + [npts] * (65 - ng)
